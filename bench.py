@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Ray Train tokens/sec, Llama-3-8B DDP (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+
+N=1: runs in-process. N>1: launched by the driver as
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N ... bench.py --gpus N ...
+one rank per GPU, process group over RCCL (xGMI). The worker function is the framework's Train
+loop (``ray_community_amd.train.llm.llama_train_loop_per_worker``): full forward + backward +
+bucketed DDP all-reduce + fused AdamW step inside the timed region, bf16 compute, fp32 master
+weights, random-init Llama-3-8B weights, synthetic tokens. Weak scaling (fixed per-GPU batch).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from ray_community_amd.train.llm import llama_train_loop_per_worker
+
+    m = llama_train_loop_per_worker({
+        "model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
+        "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb,
+    })
+    if rank == 0:
+        out = {
+            "metric": "ray_train_tokens_per_sec_llama3_8b_ddp",
+            "value": round(m["tokens_per_s"], 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(m["ms_per_step"], 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": args.micro_batch * world,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}",
+                "tokens_per_step": args.micro_batch * world * args.seq_len,
+                "optimizer": "AdamW fp32 master (fused HIP)",
+            },
+            "extra": {
+                "loss": round(m["loss"], 4),
+                "peak_mem_gb": round(m["mem_gb"], 2),
+                "model_tflops_per_gpu": round(m["tokens_per_s"] / world * m["flops_per_token"] / 1e12, 1),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,376 @@
+"""MI355X (gfx950) fused ops with autograd.
+
+Every op has two paths:
+  * CUDA/HIP tensors -> the hand-written gfx950 kernels in ``ops/csrc`` (mandatory on GPU:
+    a missing kernel library raises, there is no silent eager fallback);
+  * CPU tensors -> the plain PyTorch fp32 reference in ``ops/reference.py``.
+
+Reference parity notes: RMSNorm/SwiGLU/RoPE follow the HF Llama numerics (normalise in fp32,
+round to bf16 before the weight multiply). GAE follows
+``rllib/evaluation/postprocessing.py:compute_advantages`` (/root/reference) generalised to
+per-step terminated/done flags.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._lib import check, lib, stream_ptr
+
+__all__ = [
+    "rms_norm",
+    "swiglu",
+    "apply_rope_",
+    "rope_cos_sin",
+    "cross_entropy",
+    "grad_sumsq",
+    "compute_gae",
+    "standardize_",
+    "batched_concat",
+    "image_normalize",
+    "kernels_available",
+]
+
+rope_cos_sin = ref.rope_cos_sin
+
+
+def kernels_available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+# ----------------------------------------------------------------------------------- RMSNorm
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps, residual):
+        H = x.shape[-1]
+        x2 = x.contiguous().view(-1, H)
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        s = None
+        r2 = None
+        if residual is not None:
+            r2 = residual.contiguous().view(-1, H)
+            s = torch.empty_like(x2)
+        L = lib()
+        check(L.rca_rmsnorm_fwd(x2.data_ptr(), _p(r2), w.data_ptr(), y.data_ptr(), _p(s), rstd.data_ptr(), rows, H,
+                                float(eps), stream_ptr(x.device)), "rmsnorm_fwd")
+        saved = s if s is not None else x2
+        ctx.save_for_backward(saved, w, rstd)
+        ctx.has_res = residual is not None
+        ctx.shape = x.shape
+        if s is None:
+            return y.view(x.shape)
+        return y.view(x.shape), s.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, ds=None):
+        s, w, rstd = ctx.saved_tensors
+        H = s.shape[-1]
+        rows = s.shape[0]
+        dy2 = dy.contiguous().view(-1, H)
+        ds2 = ds.contiguous().view(-1, H) if ds is not None else None
+        dx = torch.empty_like(s)
+        L = lib()
+        nb = L.rca_rmsnorm_bwd_blocks(rows)
+        part = torch.empty(nb, H, device=s.device, dtype=torch.float32)
+        dw = torch.empty_like(w)
+        check(L.rca_rmsnorm_bwd(s.data_ptr(), dy2.data_ptr(), w.data_ptr(), rstd.data_ptr(), _p(ds2), dx.data_ptr(),
+                                part.data_ptr(), dw.data_ptr(), 0, 0, rows, H, stream_ptr(s.device)), "rmsnorm_bwd")
+        dx = dx.view(ctx.shape)
+        return dx, dw, None, (dx if ctx.has_res else None)
+
+
+def rms_norm(x, weight, eps: float = 1e-5, residual=None):
+    """RMSNorm(x [+ residual]) * weight. With ``residual`` returns ``(y, x + residual)``."""
+    if x.is_cuda:
+        assert x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16, "HIP RMSNorm expects bf16"
+        return _RMSNorm.apply(x, weight, eps, residual)
+    y, s = ref.rms_norm_ref(x, weight, eps, residual)
+    return y if residual is None else (y, s)
+
+
+# ----------------------------------------------------------------------------------- SwiGLU
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        F2 = gu.shape[-1]
+        F = F2 // 2
+        T = gu.numel() // F2
+        out = torch.empty(*gu.shape[:-1], F, device=gu.device, dtype=gu.dtype)
+        check(lib().rca_swiglu_fwd(gu.data_ptr(), out.data_ptr(), T, F, stream_ptr(gu.device)), "swiglu_fwd")
+        ctx.save_for_backward(gu)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        F2 = gu.shape[-1]
+        T = gu.numel() // F2
+        dgu = torch.empty_like(gu)
+        dout = dout.contiguous()
+        check(lib().rca_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), T, F2 // 2, stream_ptr(gu.device)),
+              "swiglu_bwd")
+        return dgu
+
+
+def swiglu(gu):
+    """silu(gu[..., :F]) * gu[..., F:] for the fused gate|up projection output."""
+    if gu.is_cuda:
+        return _SwiGLU.apply(gu)
+    return ref.swiglu_ref(gu)
+
+
+# ----------------------------------------------------------------------------------- RoPE
+class _RoPE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cs, seq_len, n_rot_heads, head_dim, positions):
+        T = qkv.shape[0]
+        row_stride = qkv.stride(0)
+        check(lib().rca_rope(qkv.data_ptr(), cs.data_ptr(), _p(positions), T, seq_len, n_rot_heads, row_stride, head_dim,
+                             0, stream_ptr(qkv.device)), "rope_fwd")
+        ctx.mark_dirty(qkv)
+        ctx.save_for_backward(cs, positions) if positions is not None else ctx.save_for_backward(cs)
+        ctx.meta = (seq_len, n_rot_heads, head_dim, positions is not None)
+        return qkv
+
+    @staticmethod
+    def backward(ctx, g):
+        seq_len, n_rot, D, has_pos = ctx.meta
+        saved = ctx.saved_tensors
+        cs = saved[0]
+        pos = saved[1] if has_pos else None
+        g = g.contiguous().clone()
+        check(lib().rca_rope(g.data_ptr(), cs.data_ptr(), _p(pos), g.shape[0], seq_len, n_rot, g.stride(0), D, 1,
+                             stream_ptr(g.device)), "rope_bwd")
+        return g, None, None, None, None, None
+
+
+def apply_rope_(qkv, cs, seq_len: int, n_q_heads: int, n_kv_heads: int, head_dim: int, positions=None):
+    """Rotate the q and k heads of a fused ``qkv`` [T, (Hq + 2*Hkv) * D] tensor in place.
+
+    Position of token t is ``positions[t]`` if given else ``t % seq_len``. ``cs`` comes from
+    :func:`rope_cos_sin`.
+    """
+    n_rot = n_q_heads + n_kv_heads
+    if qkv.is_cuda:
+        assert qkv.dim() == 2 and qkv.stride(1) == 1
+        pos = positions.to(torch.int32).contiguous() if positions is not None else None
+        return _RoPE.apply(qkv, cs, seq_len, n_rot, head_dim, pos)
+    T = qkv.shape[0]
+    pos = positions if positions is not None else torch.arange(T, device=qkv.device) % seq_len
+    x = qkv[:, : n_rot * head_dim].reshape(T, n_rot, head_dim)
+    rot = ref.rope_ref(x, cs, pos).reshape(T, n_rot * head_dim)
+    return torch.cat([rot, qkv[:, n_rot * head_dim:]], dim=1)
+
+
+# ----------------------------------------------------------------------------------- cross-entropy
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, inplace_backward):
+        logits = logits.contiguous()
+        T, V = logits.shape
+        labels = labels.contiguous().to(torch.int64)
+        loss = torch.empty(T, device=logits.device, dtype=torch.float32)
+        lse = torch.empty(T, device=logits.device, dtype=torch.float32)
+        check(lib().rca_ce_fwd(logits.data_ptr(), labels.data_ptr(), loss.data_ptr(), lse.data_ptr(), T, V, ignore_index,
+                               stream_ptr(logits.device)), "ce_fwd")
+        ctx.save_for_backward(logits, labels, lse)
+        ctx.ignore_index = ignore_index
+        ctx.inplace = inplace_backward
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        logits, labels, lse = ctx.saved_tensors
+        T, V = logits.shape
+        gl = gloss.contiguous().float()
+        d = logits if ctx.inplace else torch.empty_like(logits)
+        check(lib().rca_ce_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), gl.data_ptr(), 0.0, d.data_ptr(), T, V,
+                               ctx.ignore_index, stream_ptr(logits.device)), "ce_bwd")
+        return d, None, None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100, reduction: str = "mean", inplace_backward: bool = False):
+    """Softmax cross-entropy over the last dim of 2-D ``logits`` (bf16 on GPU).
+
+    ``inplace_backward=True`` writes dlogits over the logits buffer (only safe when nothing else
+    reads the logits after the loss).
+    """
+    if not logits.is_cuda:
+        return ref.cross_entropy_ref(logits, labels, ignore_index, reduction)
+    rows = _CrossEntropy.apply(logits, labels, ignore_index, inplace_backward)
+    if reduction == "none":
+        return rows
+    if reduction == "sum":
+        return rows.sum()
+    n = (labels != ignore_index).sum().clamp_min(1)
+    return rows.sum() / n
+
+
+# ----------------------------------------------------------------------------------- grad norm
+_WS = {}
+
+
+def _workspace(device, key, numel, dtype=torch.float32):
+    k = (str(device), key)
+    t = _WS.get(k)
+    if t is None or t.numel() < numel:
+        t = torch.empty(numel, device=device, dtype=dtype)
+        _WS[k] = t
+    return t
+
+
+def grad_sumsq(tensors, out=None):
+    """Device scalar sum of squares over a list of bf16/f32 tensors (no host sync)."""
+    tensors = [t for t in tensors if t is not None]
+    if not tensors:
+        return torch.zeros((), dtype=torch.float32)
+    dev = tensors[0].device
+    if not tensors[0].is_cuda:
+        return sum(t.float().pow(2).sum() for t in tensors)
+    out = torch.zeros(1, device=dev, dtype=torch.float32) if out is None else out
+    part = _workspace(dev, "sumsq", 1024)
+    L = lib()
+    st = stream_ptr(dev)
+    for i, t in enumerate(tensors):
+        t = t.contiguous()
+        dt = 0 if t.dtype == torch.bfloat16 else 1
+        if t.dtype not in (torch.bfloat16, torch.float32):
+            t = t.float()
+            dt = 1
+        check(L.rca_sumsq(t.data_ptr(), t.numel(), dt, part.data_ptr(), out.data_ptr(), 1 if i else 0, st), "sumsq")
+    return out
+
+
+# ----------------------------------------------------------------------------------- RL ops
+def compute_gae(rewards, values, terminateds, dones=None, gamma=0.99, lam=0.95, last_values=None, next_values=None,
+                standardize=False, eps=1e-4):
+    """GAE over [B, T] trajectories. Returns ``(advantages, value_targets)`` (float32).
+
+    ``dones`` (terminated or truncated) cuts the recurrence, ``terminateds`` zeroes the bootstrap.
+    ``next_values[b, t]`` = V(s_{t+1}) if available (exact under auto-reset/truncation); else
+    V(s_{t+1}) = values[b, t+1] and ``last_values[b]`` at the fragment end.
+    """
+    if dones is None:
+        dones = terminateds
+    squeeze = rewards.dim() == 1
+    if squeeze:
+        rewards, values, terminateds, dones = (x.unsqueeze(0) for x in (rewards, values, terminateds, dones))
+        if next_values is not None:
+            next_values = next_values.unsqueeze(0)
+        if last_values is not None:
+            last_values = torch.as_tensor(last_values).reshape(1)
+    B, T = rewards.shape
+    if rewards.is_cuda:
+        dev = rewards.device
+        f = lambda x: x.to(device=dev, dtype=torch.float32).contiguous() if x is not None else None  # noqa: E731
+        u8 = lambda x: x.to(device=dev, dtype=torch.uint8).contiguous()  # noqa: E731
+        r, v, nv, lv = f(rewards), f(values), f(next_values), f(last_values)
+        te, do = u8(terminateds), u8(dones)
+        adv = torch.empty(B, T, device=dev, dtype=torch.float32)
+        tgt = torch.empty_like(adv)
+        part = _workspace(dev, "gae_part", 2 * ((B + 3) // 4))
+        stats = _workspace(dev, "gae_stats", 2)
+        check(lib().rca_gae(r.data_ptr(), v.data_ptr(), _p(nv), _p(lv), te.data_ptr(), do.data_ptr(), adv.data_ptr(),
+                            tgt.data_ptr(), B, T, float(gamma), float(lam), 1 if standardize else 0, part.data_ptr(),
+                            stats.data_ptr(), float(eps), stream_ptr(dev)), "gae")
+    else:
+        adv, tgt = _gae_cpu(rewards, values, terminateds, dones, gamma, lam, last_values, next_values)
+        if standardize:
+            adv = (adv - adv.mean()) / (adv.std(unbiased=False) + eps)
+    if squeeze:
+        adv, tgt = adv[0], tgt[0]
+    return adv, tgt
+
+
+def _gae_cpu(rewards, values, terminateds, dones, gamma, lam, last_values, next_values):
+    r = torch.as_tensor(rewards, dtype=torch.float32)
+    v = torch.as_tensor(values, dtype=torch.float32)
+    te = torch.as_tensor(terminateds).bool()
+    do = torch.as_tensor(dones).bool()
+    B, T = r.shape
+    if next_values is not None:
+        nv = torch.as_tensor(next_values, dtype=torch.float32)
+    else:
+        lv = torch.zeros(B) if last_values is None else torch.as_tensor(last_values, dtype=torch.float32).reshape(B)
+        nv = torch.cat([v[:, 1:], lv[:, None]], dim=1)
+    delta = r + gamma * torch.where(te, torch.zeros_like(nv), nv) - v
+    c = gamma * lam * (~do).float()
+    adv = torch.empty_like(r)
+    A = torch.zeros(B)
+    for t in range(T - 1, -1, -1):  # vectorised over B
+        A = delta[:, t] + c[:, t] * A
+        adv[:, t] = A
+    return adv, adv + v
+
+
+def standardize_(x, eps=1e-4):
+    """In-place (x - mean) / (std + eps) over all elements (float32)."""
+    if x.is_cuda:
+        assert x.dtype == torch.float32 and x.is_contiguous()
+        part = _workspace(x.device, "std_part", 2048)
+        stats = _workspace(x.device, "std_stats", 2)
+        check(lib().rca_standardize(x.data_ptr(), x.numel(), part.data_ptr(), stats.data_ptr(), float(eps),
+                                    stream_ptr(x.device)), "standardize")
+        return x
+    m, s = x.mean(), x.std(unbiased=False)
+    return x.sub_(m).div_(s + eps)
+
+
+# ----------------------------------------------------------------------------------- data ops
+def batched_concat(tensors, dim=0):
+    """torch.cat along dim 0 of same-trailing-shape tensors in ONE kernel launch on GPU."""
+    if not tensors:
+        raise ValueError("empty list")
+    if not tensors[0].is_cuda or dim != 0 or len(tensors) == 1:
+        return torch.cat(tensors, dim=dim)
+    dev, dt = tensors[0].device, tensors[0].dtype
+    tail = tensors[0].shape[1:]
+    ts = [t.contiguous() for t in tensors]
+    for t in ts:
+        if t.shape[1:] != tail or t.dtype != dt or t.device != dev:
+            return torch.cat(tensors, dim=0)
+    out = torch.empty(sum(t.shape[0] for t in ts), *tail, device=dev, dtype=dt)
+    esz = out.element_size()
+    descs = []
+    off = 0
+    maxb = 0
+    for t in ts:
+        nb = t.numel() * esz
+        descs += [t.data_ptr(), off, nb]
+        off += nb
+        maxb = max(maxb, nb)
+    d = torch.tensor(descs, dtype=torch.int64).to(dev, non_blocking=True)
+    check(lib().rca_batched_copy(d.data_ptr(), len(ts), out.data_ptr(), maxb, stream_ptr(dev)), "batched_copy")
+    # keep sources + descriptor alive until the copy retires on this stream
+    for t in ts:
+        t.record_stream(torch.cuda.current_stream(dev))
+    d.record_stream(torch.cuda.current_stream(dev))
+    return out
+
+
+def image_normalize(u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), dtype=torch.bfloat16):
+    """uint8 [N, H, W, C] -> normalised [N, C, H, W] (bf16 or f32) on the device of ``u8``."""
+    if not u8.is_cuda:
+        return ref.image_normalize_ref(u8, mean, std, dtype)
+    import ctypes
+
+    u8 = u8.contiguous()
+    N, H, W, C = u8.shape
+    out = torch.empty(N, C, H, W, device=u8.device, dtype=dtype)
+    ma = (ctypes.c_float * 4)(*[float(m) for m in mean])
+    sa = (ctypes.c_float * 4)(*[float(s) for s in std])
+    check(lib().rca_image_normalize(u8.data_ptr(), out.data_ptr(), N, H, W, C, ctypes.cast(ma, ctypes.c_void_p),
+                                    ctypes.cast(sa, ctypes.c_void_p), 0 if dtype == torch.bfloat16 else 1,
+                                    stream_ptr(u8.device)), "image_normalize")
+    return out

@@ -1,0 +1,75 @@
+"""ctypes binding of the gfx950 kernel library.
+
+On a machine with a visible AMD GPU the HIP path is mandatory: if the library is missing
+and cannot be built, ``lib()`` raises instead of silently falling back to eager PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import build as _build
+
+_LOCK = threading.Lock()
+_LIB = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_float = ctypes.c_float
+
+_SIGS = {
+    "rca_rmsnorm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "rca_rmsnorm_bwd_blocks": (c_int, [c_int]),
+    "rca_rmsnorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_int, c_int, c_int, c_void_p]),
+    "rca_swiglu_fwd": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_void_p]),
+    "rca_swiglu_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
+    "rca_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "rca_ce_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_ll, c_void_p]),
+    "rca_ce_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_ll, c_int, c_ll, c_void_p]),
+    "rca_sumsq": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "rca_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float, c_float,
+                          c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
+    "rca_gae": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                        c_float, c_float, c_int, c_void_p, c_void_p, c_float, c_void_p]),
+    "rca_standardize": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_float, c_void_p]),
+    "rca_batched_copy": (c_int, [c_void_p, c_int, c_void_p, c_ll, c_void_p]),
+    "rca_image_normalize": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+}
+
+
+def lib():
+    """Load (building if needed) the kernel library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = _build.LIB_PATH
+        if not os.path.exists(path) or (_build.is_stale() and os.environ.get("RCA_NO_REBUILD") != "1"):
+            try:
+                _build.build()
+            except Exception as e:  # pragma: no cover - only on broken toolchains
+                if not os.path.exists(path):
+                    raise RuntimeError(f"ray_community_amd HIP kernels unavailable: {e}") from e
+        L = ctypes.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+        return L
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

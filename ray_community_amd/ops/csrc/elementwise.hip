@@ -1,0 +1,125 @@
+// Memory-bound fused elementwise kernels for the Llama training step on gfx950:
+//   * SwiGLU fwd/bwd on the fused gate|up projection output
+//   * RoPE fwd/bwd (rotate-half convention) applied in place on the fused qkv projection output
+// All accesses are 16 B per lane (8 x bf16). Grids are capped at 256 CUs x 8 blocks and
+// grid-stride the remainder (cdna_hip_programming.md Guideline 11).
+#include "common.h"
+
+static inline int grid_for(long long nvec, int block) {
+  long long g = (nvec + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+
+// gu: [T, 2F] (gate = gu[:, :F], up = gu[:, F:]), out: [T, F]
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out,
+                                                         long long T, int F) {
+  const int fv = F >> 3;
+  const long long n = T * fv;
+  // 32-bit index math (host guarantees n < 2^31): 64-bit division is emulated on CDNA
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n; i += gridDim.x * blockDim.x) {
+    const long long t = i / (unsigned)fv;
+    const int c = (int)(i - (unsigned)t * fv);
+    const u32x4* row = reinterpret_cast<const u32x4*>(gu + t * 2 * (long long)F);
+    float g[8], u[8], o[8];
+    unpack8(__builtin_nontemporal_load(row + c), g);
+    unpack8(__builtin_nontemporal_load(row + fv + c), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(silu_f(g[j]))) * u[j];
+    reinterpret_cast<u32x4*>(out + t * (long long)F)[c] = pack8(o);
+  }
+}
+
+// dgu[:, :F] = dout * up * dsilu(gate); dgu[:, F:] = dout * silu(gate)
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dout,
+                                                         bf16_t* __restrict__ dgu, long long T, int F) {
+  const int fv = F >> 3;
+  const long long n = T * fv;
+  // 32-bit index math (host guarantees n < 2^31): 64-bit division is emulated on CDNA
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n; i += gridDim.x * blockDim.x) {
+    const long long t = i / (unsigned)fv;
+    const int c = (int)(i - (unsigned)t * fv);
+    const u32x4* row = reinterpret_cast<const u32x4*>(gu + t * 2 * (long long)F);
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(row[c], g);
+    unpack8(row[fv + c], u);
+    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dout + t * (long long)F) + c), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.f / (1.f + __expf(-g[j]));
+      const float si = g[j] * sg;
+      du[j] = d[j] * bf2f(f2bf(si));
+      dg[j] = d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg));
+    }
+    u32x4* orow = reinterpret_cast<u32x4*>(dgu + t * 2 * (long long)F);
+    orow[c] = pack8(dg);
+    orow[fv + c] = pack8(du);
+  }
+}
+
+// RoPE in place on the first (Hq + Hk) heads of each row of qkv: [T, (Hq + 2*Hk) * D].
+// Token t has position pos[t] if pos != nullptr else (t % S). cs: [max_pos, D/2] float2 (cos, sin).
+// sign = +1 forward, -1 backward (rotation by -theta is the adjoint).
+// One thread handles 8 rotation pairs: x[i..i+7] and x[i+D/2..i+D/2+7].
+__global__ __launch_bounds__(256) void rope_kernel(bf16_t* __restrict__ qkv, const float2* __restrict__ cs,
+                                                   const int* __restrict__ pos, long long T, int S, int nheads_rot,
+                                                   int row_stride, int D, float sign) {
+  const int half = D >> 1;
+  const int per_head = half >> 3;  // threads per head
+  const long long per_row = (long long)nheads_rot * per_head;
+  const long long n = T * per_row;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n; i += gridDim.x * blockDim.x) {
+    const long long t = i / (unsigned)per_row;
+    const int r = (int)(i - (unsigned)t * (unsigned)per_row);
+    const int h = r / per_head;
+    const int c = (r - h * per_head) << 3;  // first pair index
+    const int p = pos ? pos[t] : (int)((unsigned)t % (unsigned)S);
+    bf16_t* base = qkv + t * (long long)row_stride + (long long)h * D;
+    u32x4* lo = reinterpret_cast<u32x4*>(base + c);
+    u32x4* hi = reinterpret_cast<u32x4*>(base + half + c);
+    float a[8], b[8], oa[8], ob[8];
+    unpack8(*lo, a);
+    unpack8(*hi, b);
+    const float4* csr = reinterpret_cast<const float4*>(cs + (long long)p * half + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 q = csr[j];  // (cos_j0, sin_j0, cos_j1, sin_j1)
+      const float c0 = q.x, s0 = sign * q.y, c1 = q.z, s1 = sign * q.w;
+      oa[2 * j] = a[2 * j] * c0 - b[2 * j] * s0;
+      ob[2 * j] = b[2 * j] * c0 + a[2 * j] * s0;
+      oa[2 * j + 1] = a[2 * j + 1] * c1 - b[2 * j + 1] * s1;
+      ob[2 * j + 1] = b[2 * j + 1] * c1 + a[2 * j + 1] * s1;
+    }
+    *lo = pack8(oa);
+    *hi = pack8(ob);
+  }
+}
+
+RCA_API int rca_swiglu_fwd(const void* gu, void* out, long long T, int F, hipStream_t stream) {
+  if (F % 8) return -1;
+  if (T * (F / 8) >= (1LL << 31)) return -2;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(T * (F / 8), 256)), dim3(256), 0, stream, (const bf16_t*)gu,
+                     (bf16_t*)out, T, F);
+  return (int)hipGetLastError();
+}
+
+RCA_API int rca_swiglu_bwd(const void* gu, const void* dout, void* dgu, long long T, int F, hipStream_t stream) {
+  if (F % 8) return -1;
+  if (T * (F / 8) >= (1LL << 31)) return -2;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8), 256)), dim3(256), 0, stream, (const bf16_t*)gu,
+                     (const bf16_t*)dout, (bf16_t*)dgu, T, F);
+  return (int)hipGetLastError();
+}
+
+RCA_API int rca_rope(void* qkv, const void* cs, const int* pos, long long T, int S, int nheads_rot, int row_stride,
+                     int D, int backward, hipStream_t stream) {
+  if (D % 16) return -1;
+  const long long n = T * nheads_rot * (D / 16);
+  if (n >= (1LL << 31)) return -2;
+  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (bf16_t*)qkv, (const float2*)cs, pos,
+                     T, S, nheads_rot, row_stride, D, backward ? -1.f : 1.f);
+  return (int)hipGetLastError();
+}

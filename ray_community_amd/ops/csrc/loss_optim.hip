@@ -1,0 +1,253 @@
+// Cross-entropy (fwd/bwd, bf16 logits, large vocab) and the flat-buffer AdamW / grad-norm
+// kernels for gfx950.
+//
+// Cross-entropy: one 512-thread block per token row; a single streaming pass computes the
+// online (max, sum-exp) per lane over 16-B vectors, merged across the block through LDS.
+// The backward writes dlogits (optionally in place over the logits, saving T*V*2 bytes).
+//
+// AdamW runs over ONE flat fp32 master buffer (the framework keeps all parameters of a
+// group contiguous), so a single launch streams ~28 B/param at HBM rate instead of a
+// multi-tensor-apply over thousands of small tensors. Global-norm clipping reads the
+// squared norm from device memory: no host synchronisation inside the step (graph-safe).
+#include "common.h"
+
+// ----------------------------------------------------------------------------- cross-entropy
+__global__ __launch_bounds__(512) void ce_fwd_kernel(const bf16_t* __restrict__ logits, const long long* __restrict__ labels,
+                                                     float* __restrict__ loss, float* __restrict__ lse_out, int V,
+                                                     long long ignore_index) {
+  __shared__ float sm[16], ss[16];
+  const long long row = blockIdx.x;
+  const bf16_t* x = logits + row * (long long)V;
+  const int nv = (V & 7) ? 0 : (V >> 3);  // rows are 16-B aligned only when V % 8 == 0
+  float m = -INFINITY, s = 0.f;
+  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    float f[8];
+    unpack8(__builtin_nontemporal_load(xv + c), f);
+    float vm = f[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) vm = fmaxf(vm, f[j]);
+    const float mn = fmaxf(m, vm);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += __expf(f[j] - mn);
+    s = s * __expf(m - mn) + acc;
+    m = mn;
+  }
+  for (int c = (nv << 3) + threadIdx.x; c < V; c += blockDim.x) {  // tail (V % 8)
+    const float f = bf2f(x[c]);
+    const float mn = fmaxf(m, f);
+    s = s * __expf(m - mn) + __expf(f - mn);
+    m = mn;
+  }
+  // merge (m, s) across the wave then the block
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const float mn = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+    m = mn;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[wid] = m;
+    ss[wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = -INFINITY;
+    const int nw = blockDim.x >> 6;
+    for (int i = 0; i < nw; ++i) M = fmaxf(M, sm[i]);
+    float S = 0.f;
+    for (int i = 0; i < nw; ++i) S += (sm[i] == -INFINITY) ? 0.f : ss[i] * __expf(sm[i] - M);
+    const float lse = M + __logf(S);
+    lse_out[row] = lse;
+    const long long lab = labels[row];
+    loss[row] = (lab == ignore_index || lab < 0 || lab >= V) ? 0.f : lse - bf2f(x[lab]);
+  }
+}
+
+// dlogits[r, j] = g[r] * (softmax_j - [j == label]); g = grad_loss[r] (or grad_scalar if grad_loss is null)
+__global__ __launch_bounds__(512) void ce_bwd_kernel(const bf16_t* __restrict__ logits, const long long* __restrict__ labels,
+                                                     const float* __restrict__ lse, const float* __restrict__ grad_loss,
+                                                     float grad_scalar, bf16_t* __restrict__ dlogits, int V,
+                                                     long long ignore_index) {
+  const long long row = blockIdx.x;
+  const long long lab = labels[row];
+  const bool ign = (lab == ignore_index || lab < 0 || lab >= V);
+  const float g = ign ? 0.f : (grad_loss ? grad_loss[row] : grad_scalar);
+  const float L = lse[row];
+  const bf16_t* x = logits + row * (long long)V;
+  bf16_t* dx = dlogits + row * (long long)V;
+  const int nv = (V & 7) ? 0 : (V >> 3);  // rows are 16-B aligned only when V % 8 == 0
+  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+  u32x4* dv = reinterpret_cast<u32x4*>(dx);
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    float f[8];
+    unpack8(xv[c], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float p = __expf(f[j] - L);
+      if ((long long)(c * 8 + j) == lab) p -= 1.f;
+      f[j] = g * p;
+    }
+    dv[c] = pack8(f);
+  }
+  for (int c = (nv << 3) + threadIdx.x; c < V; c += blockDim.x) {
+    float p = __expf(bf2f(x[c]) - L);
+    if ((long long)c == lab) p -= 1.f;
+    dx[c] = f2bf(g * p);
+  }
+}
+
+RCA_API int rca_ce_fwd(const void* logits, const long long* labels, float* loss, float* lse, long long T, int V,
+                       long long ignore_index, hipStream_t stream) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3((unsigned)T), dim3(512), 0, stream, (const bf16_t*)logits, labels, loss, lse, V,
+                     ignore_index);
+  return (int)hipGetLastError();
+}
+
+RCA_API int rca_ce_bwd(const void* logits, const long long* labels, const float* lse, const float* grad_loss,
+                       float grad_scalar, void* dlogits, long long T, int V, long long ignore_index, hipStream_t stream) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)T), dim3(512), 0, stream, (const bf16_t*)logits, labels, lse,
+                     grad_loss, grad_scalar, (bf16_t*)dlogits, V, ignore_index);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- grad norm
+// partial[b] = sum of squares of this block's grid-stride share; dtype 0 = bf16, 1 = f32
+template <int DT>
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const void* __restrict__ g, long long n, float* __restrict__ partial) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  if (DT == 0) {
+    const bf16_t* x = (const bf16_t*)g;
+    const long long nv = n >> 3;
+    const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
+      float f[8];
+      unpack8(__builtin_nontemporal_load(xv + i), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += f[j] * f[j];
+    }
+    for (long long i = (nv << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+      const float f = bf2f(x[i]);
+      acc += f * f;
+    }
+  } else {
+    const float* x = (const float*)g;
+    const long long nv = n >> 2;
+    const f32x4* xv = reinterpret_cast<const f32x4*>(x);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
+      const f32x4 f = __builtin_nontemporal_load(xv + i);
+      acc += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+    }
+    for (long long i = (nv << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+      acc += x[i] * x[i];
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partial, int nb, float* __restrict__ out,
+                                                           int accumulate) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += partial[i];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + acc : acc;
+}
+
+// out[0] (+)= sum(g^2). partial must hold >= 1024 floats. Deterministic (no atomics).
+RCA_API int rca_sumsq(const void* g, long long n, int dtype, float* partial, float* out, int accumulate, hipStream_t stream) {
+  long long nb = (n / (dtype == 0 ? 8 : 4) + 255) / 256;
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  if (dtype == 0)
+    hipLaunchKernelGGL(sumsq_partial_kernel<0>, dim3((int)nb), dim3(256), 0, stream, g, n, partial);
+  else
+    hipLaunchKernelGGL(sumsq_partial_kernel<1>, dim3((int)nb), dim3(256), 0, stream, g, n, partial);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, partial, (int)nb, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- AdamW
+struct AdamHP {
+  float lr, b1, b2, eps, wd, bc1, bc2, grad_mul, max_norm;
+};
+
+// global-norm clip of the (grad_mul-scaled) gradient: coef = min(1, max_norm / ||g * grad_mul||)
+__device__ __forceinline__ float clip_coef(const float* sumsq, float max_norm, float grad_mul) {
+  if (!sumsq || max_norm <= 0.f) return 1.f;
+  const float nrm = sqrtf(sumsq[0]) * fabsf(grad_mul);
+  return fminf(1.f, max_norm / (nrm + 1e-6f));
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamHP& hp) {
+  m = hp.b1 * m + (1.f - hp.b1) * g;
+  v = hp.b2 * v + (1.f - hp.b2) * g * g;
+  const float mh = m / hp.bc1;
+  const float vh = v / hp.bc2;
+  p = p - hp.lr * (mh / (sqrtf(vh) + hp.eps) + hp.wd * p);
+}
+
+// GDT: 0 = bf16 grads, 1 = f32 grads. p16 (optional) receives the bf16 copy of the master weights.
+template <int GDT>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, bf16_t* __restrict__ p16, const void* __restrict__ grad,
+                                                    float* __restrict__ m, float* __restrict__ v, long long n, AdamHP hp,
+                                                    const float* __restrict__ sumsq) {
+  const float gm = hp.grad_mul * clip_coef(sumsq, hp.max_norm, hp.grad_mul);
+  const long long nv = n >> 3;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
+    float g[8];
+    if (GDT == 0) {
+      unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(grad) + i), g);
+    } else {
+      const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(grad) + 2 * i);
+      const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(grad) + 2 * i + 1);
+      g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y; g[6] = b.z; g[7] = b.w;
+    }
+    f32x4* pp = reinterpret_cast<f32x4*>(p) + 2 * i;
+    f32x4* mp = reinterpret_cast<f32x4*>(m) + 2 * i;
+    f32x4* vp = reinterpret_cast<f32x4*>(v) + 2 * i;
+    f32x4 P0 = pp[0], P1 = pp[1], M0 = mp[0], M1 = mp[1], V0 = vp[0], V1 = vp[1];
+    float P[8] = {P0.x, P0.y, P0.z, P0.w, P1.x, P1.y, P1.z, P1.w};
+    float M[8] = {M0.x, M0.y, M0.z, M0.w, M1.x, M1.y, M1.z, M1.w};
+    float Vv[8] = {V0.x, V0.y, V0.z, V0.w, V1.x, V1.y, V1.z, V1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adam_elem(P[j], M[j], Vv[j], g[j] * gm, hp);
+    pp[0] = f32x4{P[0], P[1], P[2], P[3]};
+    pp[1] = f32x4{P[4], P[5], P[6], P[7]};
+    mp[0] = f32x4{M[0], M[1], M[2], M[3]};
+    mp[1] = f32x4{M[4], M[5], M[6], M[7]};
+    vp[0] = f32x4{Vv[0], Vv[1], Vv[2], Vv[3]};
+    vp[1] = f32x4{Vv[4], Vv[5], Vv[6], Vv[7]};
+    if (p16) reinterpret_cast<u32x4*>(p16)[i] = pack8(P);
+  }
+  // tail
+  for (long long i = (nv << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float g = (GDT == 0 ? bf2f(((const bf16_t*)grad)[i]) : ((const float*)grad)[i]) * gm;
+    float P = p[i], M = m[i], Vv = v[i];
+    adam_elem(P, M, Vv, g, hp);
+    p[i] = P;
+    m[i] = M;
+    v[i] = Vv;
+    if (p16) p16[i] = f2bf(P);
+  }
+}
+
+RCA_API int rca_adamw(float* p, void* p16, const void* grad, int grad_dtype, float* m, float* v, long long n, float lr,
+                      float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_mul, const float* sumsq,
+                      float max_norm, hipStream_t stream) {
+  AdamHP hp{lr, b1, b2, eps, wd, bc1, bc2, grad_mul, max_norm};
+  long long nb = ((n >> 3) + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  if (grad_dtype == 0)
+    hipLaunchKernelGGL(adamw_kernel<0>, dim3((int)nb), dim3(256), 0, stream, p, (bf16_t*)p16, grad, m, v, n, hp, sumsq);
+  else
+    hipLaunchKernelGGL(adamw_kernel<1>, dim3((int)nb), dim3(256), 0, stream, p, (bf16_t*)p16, grad, m, v, n, hp, sumsq);
+  return (int)hipGetLastError();
+}

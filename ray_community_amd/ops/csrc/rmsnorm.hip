@@ -1,0 +1,316 @@
+// RMSNorm forward/backward (optionally fused with the residual add) for gfx950.
+//
+// Layout: rows x H, bf16, row-major. One wave (64 lanes) owns one row; each lane moves
+// 16 B (8 x bf16) per access, so one wave-instruction covers 512 columns. For H a multiple
+// of 512 and <= 8192 the row stays in VGPRs between the reduction and the scale pass
+// (template VPL = H / 512); otherwise a generic two-pass loop re-reads the row (L1/L2 hit).
+//
+// Forward (fused): s = x + r (stored if sum_out), y = s * rsqrt(mean(s^2) + eps) * w
+// Backward: dx = rstd * (w*dy) - s * rstd^3 / H * sum(s*w*dy) (+ dres), dw = sum_rows dy*s*rstd
+// dw is reduced per block in LDS, then across blocks by a column-sum kernel (no atomics,
+// bitwise reproducible).
+#include "common.h"
+
+template <int VPL>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_reg(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                       const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                                                       bf16_t* __restrict__ sum_out, float* __restrict__ rstd,
+                                                       int rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * H);
+  u32x4 pv[VPL];  // the row stays packed in VGPRs: 4 registers per 8 elements
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) pv[i] = __builtin_nontemporal_load(xr + i * 64 + lane);
+  if (res) {
+    const u32x4* rr = reinterpret_cast<const u32x4*>(res + (size_t)row * H);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float a[8], t[8];
+      unpack8(pv[i], a);
+      unpack8(__builtin_nontemporal_load(rr + i * 64 + lane), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += t[j];
+      pv[i] = pack8(a);  // rounds like an unfused bf16 add
+    }
+    if (sum_out) {
+      u32x4* so = reinterpret_cast<u32x4*>(sum_out + (size_t)row * H);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) so[i * 64 + lane] = pv[i];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    float a[8];
+    unpack8(pv[i], a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)H + eps);
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  u32x4* yr = reinterpret_cast<u32x4*>(y + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    float a[8], wf[8], o[8];
+    unpack8(pv[i], a);
+    unpack8(wr[i * 64 + lane], wf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(a[j] * r)) * wf[j];
+    yr[i * 64 + lane] = pack8(o);
+  }
+  if (lane == 0) rstd[row] = r;
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_fwd_generic(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                           const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                                                           bf16_t* __restrict__ sum_out, float* __restrict__ rstd,
+                                                           int rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = H >> 3;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * H);
+  const u32x4* rr = res ? reinterpret_cast<const u32x4*>(res + (size_t)row * H) : nullptr;
+  u32x4* so = (res && sum_out) ? reinterpret_cast<u32x4*>(sum_out + (size_t)row * H) : nullptr;
+  float ss = 0.f;
+  for (int c = lane; c < nv; c += 64) {
+    float v[8];
+    unpack8(xr[c], v);
+    if (rr) {
+      float t[8];
+      unpack8(rr[c], t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + t[j]));
+      if (so) so[c] = pack8(v);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)H + eps);
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  u32x4* yr = reinterpret_cast<u32x4*>(y + (size_t)row * H);
+  for (int c = lane; c < nv; c += 64) {
+    float v[8], wf[8], o[8];
+    unpack8(xr[c], v);
+    if (rr) {
+      float t[8];
+      unpack8(rr[c], t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j] + t[j]));
+    }
+    unpack8(wr[c], wf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(v[j] * r)) * wf[j];
+    yr[c] = pack8(o);
+  }
+  if (lane == 0) rstd[row] = r;
+}
+
+// Backward. Each block (4 waves) walks rows with a grid stride; per-lane dw partials for
+// the lane's columns live in registers, then the 4 waves are summed through LDS and written
+// to dw_part[blockIdx.x][H] (fp32).
+template <int VPL>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_reg(const bf16_t* __restrict__ s, const bf16_t* __restrict__ dy,
+                                                       const bf16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                       const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                       float* __restrict__ dw_part, int rows, int H) {
+  // Rows stay packed in VGPRs (s, dy: 8 registers per 8 columns); the per-wave dw partial lives
+  // in this wave's own LDS slice (lane-private columns: no conflicts, no barrier in the loop), so
+  // the kernel holds ~5 waves/SIMD instead of 1 with register accumulators.
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nwave_total = gridDim.x * 4;
+  float* accw = lds + (size_t)wid * H;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    f32x4* a4 = reinterpret_cast<f32x4*>(accw + (i * 64 + lane) * 8);
+    a4[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    a4[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  const float invH = 1.f / (float)H;
+  for (int row = blockIdx.x * 4 + wid; row < rows; row += nwave_total) {
+    const u32x4* sr = reinterpret_cast<const u32x4*>(s + (size_t)row * H);
+    const u32x4* gr = reinterpret_cast<const u32x4*>(dy + (size_t)row * H);
+    u32x4 ps[VPL], pg[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      ps[i] = __builtin_nontemporal_load(sr + i * 64 + lane);
+      pg[i] = __builtin_nontemporal_load(gr + i * 64 + lane);
+    }
+    const float r = rstd[row];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float sv[8], gv[8], wf[8];
+      unpack8(ps[i], sv);
+      unpack8(pg[i], gv);
+      unpack8(wr[i * 64 + lane], wf);
+      f32x4* a4 = reinterpret_cast<f32x4*>(accw + (i * 64 + lane) * 8);
+      f32x4 a0 = a4[0], a1 = a4[1];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dot += sv[j] * wf[j] * gv[j];
+        const float contrib = gv[j] * bf2f(f2bf(sv[j] * r));
+        if (j < 4) a0[j] += contrib; else a1[j - 4] += contrib;
+      }
+      a4[0] = a0;
+      a4[1] = a1;
+    }
+    dot = wave_sum(dot);
+    const float c = dot * r * r * r * invH;
+    u32x4* xr = reinterpret_cast<u32x4*>(dx + (size_t)row * H);
+    const u32x4* drr = dres ? reinterpret_cast<const u32x4*>(dres + (size_t)row * H) : nullptr;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float sv[8], gv[8], wf[8], o[8];
+      unpack8(ps[i], sv);
+      unpack8(pg[i], gv);
+      unpack8(wr[i * 64 + lane], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = r * wf[j] * gv[j] - c * sv[j];
+      if (drr) {
+        float t[8];
+        unpack8(__builtin_nontemporal_load(drr + i * 64 + lane), t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += t[j];
+      }
+      xr[i * 64 + lane] = pack8(o);
+    }
+  }
+  __syncthreads();
+  float* out = dw_part + (size_t)blockIdx.x * H;
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    f32x4 t = *reinterpret_cast<f32x4*>(lds + c);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) t += *reinterpret_cast<f32x4*>(lds + (size_t)k * H + c);
+    *reinterpret_cast<f32x4*>(out + c) = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_bwd_generic(const bf16_t* __restrict__ s, const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                           const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                           float* __restrict__ dw_part, int rows, int H) {
+  // generic path: one block per grid-stride set of rows, dw partial accumulated in LDS (H <= 40960)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nv = H >> 3;
+  for (int c = threadIdx.x; c < 4 * H; c += blockDim.x) lds[c] = 0.f;
+  __syncthreads();
+  const float invH = 1.f / (float)H;
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  for (int row = blockIdx.x * 4 + wid; row < rows; row += gridDim.x * 4) {
+    const u32x4* sr = reinterpret_cast<const u32x4*>(s + (size_t)row * H);
+    const u32x4* gr = reinterpret_cast<const u32x4*>(dy + (size_t)row * H);
+    const float r = rstd[row];
+    float dot = 0.f;
+    for (int c = lane; c < nv; c += 64) {
+      float sv[8], gv[8], wf[8];
+      unpack8(sr[c], sv);
+      unpack8(gr[c], gv);
+      unpack8(wr[c], wf);
+      f32x4* a4 = reinterpret_cast<f32x4*>(lds + (size_t)wid * H + c * 8);
+      f32x4 a0 = a4[0], a1 = a4[1];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dot += sv[j] * wf[j] * gv[j];
+        const float contrib = gv[j] * bf2f(f2bf(sv[j] * r));
+        if (j < 4) a0[j] += contrib; else a1[j - 4] += contrib;
+      }
+      a4[0] = a0;
+      a4[1] = a1;
+    }
+    dot = wave_sum(dot);
+    const float cc = dot * r * r * r * invH;
+    u32x4* xr = reinterpret_cast<u32x4*>(dx + (size_t)row * H);
+    const u32x4* drr = dres ? reinterpret_cast<const u32x4*>(dres + (size_t)row * H) : nullptr;
+    for (int c = lane; c < nv; c += 64) {
+      float sv[8], gv[8], wf[8], o[8];
+      unpack8(sr[c], sv);
+      unpack8(gr[c], gv);
+      unpack8(wr[c], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = r * wf[j] * gv[j] - cc * sv[j];
+      if (drr) {
+        float t[8];
+        unpack8(drr[c], t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += t[j];
+      }
+      xr[c] = pack8(o);
+    }
+  }
+  __syncthreads();
+  float* out = dw_part + (size_t)blockIdx.x * H;
+  for (int c = threadIdx.x; c < H; c += blockDim.x) out[c] = lds[c] + lds[H + c] + lds[2 * H + c] + lds[3 * H + c];
+}
+
+// dw[c] = sum_b part[b][c]; written as bf16 (dw_bf16) and/or accumulated into fp32 (dw_f32 += ...)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int nb, int H,
+                                                     bf16_t* __restrict__ dw_bf16, float* __restrict__ dw_f32,
+                                                     int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= H) return;
+  float t = 0.f;
+  for (int b = 0; b < nb; ++b) t += part[(size_t)b * H + c];
+  if (dw_f32) dw_f32[c] = accumulate ? dw_f32[c] + t : t;
+  if (dw_bf16) dw_bf16[c] = f2bf(accumulate ? bf2f(dw_bf16[c]) + t : t);
+}
+
+RCA_API int rca_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd,
+                            int rows, int H, float eps, hipStream_t stream) {
+  if (H % 8 != 0) return -1;
+  dim3 block(256), grid((rows + 3) / 4);
+  auto X = (const bf16_t*)x;
+  auto R = (const bf16_t*)res;
+  auto W = (const bf16_t*)w;
+  auto Y = (bf16_t*)y;
+  auto S = (bf16_t*)sum_out;
+  switch (H) {
+    case 512: hipLaunchKernelGGL(rmsnorm_fwd_reg<1>, grid, block, 0, stream, X, R, W, Y, S, rstd, rows, H, eps); break;
+    case 1024: hipLaunchKernelGGL(rmsnorm_fwd_reg<2>, grid, block, 0, stream, X, R, W, Y, S, rstd, rows, H, eps); break;
+    case 2048: hipLaunchKernelGGL(rmsnorm_fwd_reg<4>, grid, block, 0, stream, X, R, W, Y, S, rstd, rows, H, eps); break;
+    case 4096: hipLaunchKernelGGL(rmsnorm_fwd_reg<8>, grid, block, 0, stream, X, R, W, Y, S, rstd, rows, H, eps); break;
+    case 8192: hipLaunchKernelGGL(rmsnorm_fwd_reg<16>, grid, block, 0, stream, X, R, W, Y, S, rstd, rows, H, eps); break;
+    default: hipLaunchKernelGGL(rmsnorm_fwd_generic, grid, block, 0, stream, X, R, W, Y, S, rstd, rows, H, eps);
+  }
+  return (int)hipGetLastError();
+}
+
+// returns the number of blocks used for dw partials; dw_part must hold nb*H floats (nb <= 512)
+RCA_API int rca_rmsnorm_bwd_blocks(int rows) {
+  int nb = (rows + 15) / 16;  // >= 4 rows per wave
+  if (nb > 512) nb = 512;
+  if (nb < 1) nb = 1;
+  return nb;
+}
+
+RCA_API int rca_rmsnorm_bwd(const void* s, const void* dy, const void* w, const float* rstd, const void* dres, void* dx,
+                            float* dw_part, void* dw_bf16, float* dw_f32, int accumulate, int rows, int H,
+                            hipStream_t stream) {
+  if (H % 8 != 0) return -1;
+  const int nb = rca_rmsnorm_bwd_blocks(rows);
+  dim3 block(256), grid(nb);
+  const size_t lds = (size_t)4 * H * sizeof(float);
+  if (lds > 160 * 1024) return -2;
+  auto S = (const bf16_t*)s;
+  auto G = (const bf16_t*)dy;
+  auto W = (const bf16_t*)w;
+  auto DR = (const bf16_t*)dres;
+  auto DX = (bf16_t*)dx;
+  switch (H) {
+    case 512: hipLaunchKernelGGL(rmsnorm_bwd_reg<1>, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H); break;
+    case 1024: hipLaunchKernelGGL(rmsnorm_bwd_reg<2>, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H); break;
+    // wider rows: the register-cached variant drops to 1-2 waves/SIMD; the two-pass generic
+    // kernel (second pass served from L2) keeps 7 waves/SIMD
+    default: hipLaunchKernelGGL(rmsnorm_bwd_generic, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H);
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, stream, dw_part, nb, H, (bf16_t*)dw_bf16, dw_f32,
+                     accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,81 @@
+"""Plain PyTorch fp32 references of every HIP op (numerics oracle for tests, CPU execution path)."""
+from __future__ import annotations
+
+import torch
+
+
+def rms_norm_ref(x, w, eps=1e-5, residual=None):
+    s = x if residual is None else (x.float() + residual.float()).to(x.dtype)
+    sf = s.float()
+    r = torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps)
+    y = (sf * r).to(x.dtype).float() * w.float()
+    return y.to(x.dtype), s
+
+
+def swiglu_ref(gu):
+    F = gu.shape[-1] // 2
+    g, u = gu[..., :F].float(), gu[..., F:].float()
+    return (torch.nn.functional.silu(g).to(gu.dtype).float() * u).to(gu.dtype)
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float = 500000.0, device=None):
+    """[max_pos, head_dim/2, 2] float32 table of (cos, sin) for the rotate-half convention."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    cs = torch.stack([f.cos(), f.sin()], dim=-1).float()
+    return cs.to(device) if device is not None else cs
+
+
+def rope_ref(x, cs, positions):
+    """x: [T, H, D] ; cs [max_pos, D/2, 2]; positions [T] -> rotated x (rotate-half convention)."""
+    D = x.shape[-1]
+    half = D // 2
+    c = cs[positions, :, 0][:, None, :]
+    s = cs[positions, :, 1][:, None, :]
+    xf = x.float()
+    a, b = xf[..., :half], xf[..., half:]
+    return torch.cat([a * c - b * s, b * c + a * s], dim=-1).to(x.dtype)
+
+
+def cross_entropy_ref(logits, labels, ignore_index=-100, reduction="mean"):
+    return torch.nn.functional.cross_entropy(logits.float(), labels, ignore_index=ignore_index, reduction=reduction)
+
+
+def adamw_ref(p, g, m, v, lr, b1, b2, eps, wd, step, grad_mul=1.0, clip=1.0):
+    g = g.float() * grad_mul * clip
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    p.sub_(lr * ((m / bc1) / ((v / bc2).sqrt() + eps) + wd * p))
+    return p
+
+
+def gae_ref(rewards, values, terminateds, dones, gamma, lam, last_values=None, next_values=None):
+    """rewards/values/...: [B, T] -> (advantages, value_targets) in fp64-accurate float32."""
+    B, T = rewards.shape
+    r = rewards.double()
+    v = values.double()
+    adv = torch.zeros_like(r)
+    for b in range(B):
+        A = 0.0
+        for t in range(T - 1, -1, -1):
+            if next_values is not None:
+                nv = float(next_values[b, t])
+            elif t + 1 < T:
+                nv = float(v[b, t + 1])
+            else:
+                nv = float(last_values[b]) if last_values is not None else 0.0
+            d = float(r[b, t]) + gamma * (0.0 if terminateds[b, t] else nv) - float(v[b, t])
+            c = gamma * lam * (0.0 if dones[b, t] else 1.0)
+            A = d + c * A
+            adv[b, t] = A
+    return adv.float(), (adv + v).float()
+
+
+def image_normalize_ref(u8, mean, std, dtype=torch.bfloat16):
+    x = u8.float() / 255.0
+    m = torch.tensor(mean, dtype=torch.float32).view(1, 1, 1, -1)
+    s = torch.tensor(std, dtype=torch.float32).view(1, 1, 1, -1)
+    return ((x - m) / s).permute(0, 3, 1, 2).contiguous().to(dtype)

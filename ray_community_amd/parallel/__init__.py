@@ -1,0 +1,7 @@
+"""Data/model parallel building blocks over RCCL (xGMI) — MI355X-first replacements for the
+reference's reliance on torch DDP/FSDP (``python/ray/train/torch/train_loop_utils.py``)."""
+from .flat import FlatParameters
+from .ddp import DistributedDataParallel
+from .optim import FlatAdamW
+
+__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW"]

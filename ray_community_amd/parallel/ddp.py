@@ -1,0 +1,105 @@
+"""Bucketed data-parallel gradient all-reduce over RCCL (xGMI), overlapped with backward.
+
+Reference behaviour: ``python/ray/train/torch/train_loop_utils.py:prepare_model`` wraps the
+model in ``torch.nn.parallel.DistributedDataParallel``. Here DDP is the framework's own:
+
+  * gradients live in ONE flat buffer (``FlatParameters``); each bucket is a contiguous slice,
+    so an all-reduce is issued on a view — no gradient packing/unpacking copies;
+  * a post-accumulate-grad hook per parameter counts arrivals per bucket; the moment a
+    bucket's last gradient lands its async all-reduce is launched (RCCL stream waits on the
+    compute stream via an event), so communication overlaps the rest of backward;
+  * buckets default to 256 MB: xGMI is point-to-point (7 links/GPU), ring all-reduce is
+    per-link bound, so a handful of large messages beats NVSwitch-style 25 MB buckets;
+  * averaging is NOT a separate pass: the all-reduce is a SUM and ``grad_scale`` (1/world)
+    is folded into the fused AdamW kernel.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .flat import FlatParameters
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0, broadcast_buffers=True,
+                 flat: Optional[FlatParameters] = None, average_in_optimizer: bool = True):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        self.flat = flat if flat is not None else FlatParameters(module, bucket_cap_mb=bucket_cap_mb)
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.average_in_optimizer = average_in_optimizer
+        self._sync = True
+        self._works: List[Optional[object]] = [None] * len(self.flat.buckets)
+        self._pending = [len(b.params) for b in self.flat.buckets]
+        self._hooks = []
+        if self.world > 1:
+            src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+            dist.broadcast(self.flat.data, src=src, group=process_group)
+            if broadcast_buffers:
+                for b in module.buffers():
+                    dist.broadcast(b, src=src, group=process_group)
+            for p in self.flat.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    # ------------------------------------------------------------------ hooks
+    def _on_grad(self, p):
+        if not self._sync:
+            return
+        bi = self.flat.param_bucket[id(p)]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        b = self.flat.buckets[bi]
+        view = self.flat.grad[b.start: b.end]
+        if not self.average_in_optimizer:
+            view.div_(self.world)
+        self._works[bi] = dist.all_reduce(view, group=self.pg, async_op=True)
+
+    def forward(self, *args, **kwargs):
+        if self._sync:
+            self._pending = [len(b.params) for b in self.flat.buckets]
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation: skip communication for micro-batches inside the context."""
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def finish_gradient_sync(self):
+        """Launch any bucket whose grads never arrived (unused params) and wait for all."""
+        if self.world <= 1:
+            return
+        for bi, w in enumerate(self._works):
+            if w is None:
+                self._launch(bi)
+        for bi, w in enumerate(self._works):
+            if w is not None:
+                w.wait()
+            self._works[bi] = None
+        self._pending = [len(b.params) for b in self.flat.buckets]
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world if (self.world > 1 and self.average_in_optimizer) else 1.0
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    def state_dict(self, *a, **k):
+        return self.module.state_dict(*a, **k)
+
+    def load_state_dict(self, sd, strict=True):
+        return self.module.load_state_dict(sd, strict=strict)

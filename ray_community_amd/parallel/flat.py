@@ -1,0 +1,112 @@
+"""Flat parameter / gradient storage.
+
+All trainable parameters of a module become views into ONE contiguous buffer, and their
+``.grad`` views into ONE contiguous gradient buffer. This is what lets the framework
+  * all-reduce gradients in a few large, contiguous buckets with zero packing copies
+    (xGMI ring collectives are per-link bandwidth bound: fewer, larger messages win), and
+  * run AdamW as one streaming HIP kernel over the whole model instead of a multi-tensor loop.
+
+Parameters are laid out in REVERSE registration order (≈ the order in which backward produces
+their gradients), decayed matrices first and the tiny no-decay vectors (norm weights, biases)
+last, so gradient buckets fill front to back during backward.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64  # elements; keeps every view 128-B aligned for 16-B vector access
+
+
+def _round_up(n, a=ALIGN):
+    return (n + a - 1) // a * a
+
+
+def default_no_decay(name: str, p: torch.Tensor) -> bool:
+    return p.dim() < 2 or name.endswith(".bias")
+
+
+@dataclass
+class Bucket:
+    index: int
+    start: int
+    end: int
+    params: List[nn.Parameter]
+
+
+class FlatParameters:
+    def __init__(self, module: nn.Module, bucket_cap_mb: float = 256.0,
+                 no_decay: Callable[[str, torch.Tensor], bool] = default_no_decay, grad_dtype=None):
+        seen = set()
+        named = []
+        for name, p in module.named_parameters():
+            if not p.requires_grad or id(p) in seen:
+                continue
+            seen.add(id(p))
+            named.append((name, p))
+        decay = [(n, p) for n, p in reversed(named) if not no_decay(n, p)]
+        nodecay = [(n, p) for n, p in reversed(named) if no_decay(n, p)]
+        self.names = [n for n, _ in decay + nodecay]
+        self.params = [p for _, p in decay + nodecay]
+        if not self.params:
+            raise ValueError("module has no trainable parameters")
+        dev = self.params[0].device
+        dtype = self.params[0].dtype
+        self.dtype = dtype
+        self.device = dev
+        offs = []
+        o = 0
+        for p in self.params:
+            offs.append(o)
+            o += _round_up(p.numel())
+        self.decay_end = sum(_round_up(p.numel()) for _, p in decay)
+        self.numel = o
+        self.offsets = offs
+        self.data = torch.zeros(o, dtype=dtype, device=dev)
+        gdt = grad_dtype or dtype
+        self.grad = torch.zeros(o, dtype=gdt, device=dev)
+        with torch.no_grad():
+            for p, off in zip(self.params, offs):
+                n = p.numel()
+                self.data[off: off + n].copy_(p.data.reshape(-1))
+                p.data = self.data[off: off + n].view_as(p)
+                if gdt == dtype:
+                    p.grad = self.grad[off: off + n].view_as(p)
+        self.grad_is_view = gdt == dtype
+        # buckets: contiguous ranges of the flat gradient buffer
+        cap = max(1, int(bucket_cap_mb * 1024 * 1024 / self.grad.element_size()))
+        self.buckets: List[Bucket] = []
+        cur: List[nn.Parameter] = []
+        start = 0
+        for p, off in zip(self.params, offs):
+            end_p = off + _round_up(p.numel())
+            # the no-decay tail always gets its own bucket (tiny, all-reduced last)
+            if cur and (end_p - start > cap or off == self.decay_end):
+                self.buckets.append(Bucket(len(self.buckets), start, off, cur))
+                cur, start = [], off
+            cur.append(p)
+        if cur:
+            self.buckets.append(Bucket(len(self.buckets), start, o, cur))
+        self.param_bucket = {}
+        for b in self.buckets:
+            for p in b.params:
+                self.param_bucket[id(p)] = b.index
+        self.param_offset = {id(p): off for p, off in zip(self.params, offs)}
+
+    def zero_grad(self):
+        self.grad.zero_()
+        if self.grad_is_view:
+            for p, off in zip(self.params, self.offsets):
+                if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
+                    p.grad = self.grad[off: off + p.numel()].view_as(p)
+
+    def param_slices(self, name_filter: Optional[Callable[[str], bool]] = None):
+        for n, p, off in zip(self.names, self.params, self.offsets):
+            if name_filter is None or name_filter(n):
+                yield n, p, off
+
+    def __len__(self):
+        return self.numel

@@ -1,0 +1,118 @@
+"""Fused flat AdamW with fp32 master weights.
+
+One HIP kernel launch per weight-decay group streams (fp32 master, bf16/f32 grad, m, v) ->
+(master, m, v, bf16 model weights) at HBM rate. Gradient averaging (1/world from DDP) and
+global-norm clipping (norm read from device memory) are folded into the same pass, so the
+step needs no host synchronisation and no extra elementwise passes.
+Works on any ``FlatParameters`` (CPU tensors use the PyTorch reference math).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import ops
+from ..ops._lib import check, lib, stream_ptr
+from .flat import FlatParameters
+
+
+class FlatAdamW:
+    def __init__(self, flat: FlatParameters, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
+                 weight_decay: float = 0.1, max_grad_norm: Optional[float] = 1.0, master_weights: bool = True,
+                 lr_schedule=None):
+        self.flat = flat
+        self.lr = lr
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.wd = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.lr_schedule = lr_schedule
+        self.step_count = 0
+        dev = flat.device
+        self.master_weights = master_weights and flat.dtype != torch.float32
+        self.master = flat.data.float() if self.master_weights else flat.data
+        self.m = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
+        self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.last_grad_norm = None  # device tensor (sum of squares, pre-scale)
+        self.track_grad_norm = False
+
+    @property
+    def param_groups(self):  # minimal torch.optim compatibility for LR schedulers / logging
+        return [{"lr": self.lr, "weight_decay": self.wd}]
+
+    def current_lr(self) -> float:
+        return self.lr_schedule(self.step_count) if self.lr_schedule else self.lr
+
+    def sync_master(self):
+        """Re-read model weights into the fp32 master copy (after load_state_dict)."""
+        if self.master_weights:
+            self.master.copy_(self.flat.data.float())
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0):
+        self.step_count += 1
+        t = self.step_count
+        lr = self.current_lr()
+        bc1 = 1.0 - self.b1 ** t
+        bc2 = 1.0 - self.b2 ** t
+        flat = self.flat
+        g = flat.grad
+        clip = self.max_grad_norm if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
+        if clip or self.track_grad_norm:
+            ops.grad_sumsq([g], out=self._sumsq)
+            self.last_grad_norm = self._sumsq  # sqrt taken lazily by grad_norm()
+        self._grad_scale = grad_scale
+        segs = [(0, flat.decay_end, self.wd), (flat.decay_end, flat.numel, 0.0)]
+        if g.is_cuda:
+            L = lib()
+            st = stream_ptr(g.device)
+            gdt = 0 if g.dtype == torch.bfloat16 else 1
+            if g.dtype not in (torch.bfloat16, torch.float32):
+                raise TypeError(f"unsupported grad dtype {g.dtype}")
+            esz_p = self.master.element_size()
+            esz_g = g.element_size()
+            for s, e, wd in segs:
+                n = e - s
+                if n <= 0:
+                    continue
+                p16 = flat.data.data_ptr() + s * flat.data.element_size() if self.master_weights else 0
+                check(L.rca_adamw(self.master.data_ptr() + s * esz_p, p16, g.data_ptr() + s * esz_g, gdt,
+                                  self.m.data_ptr() + s * 4, self.v.data_ptr() + s * 4, n, lr, self.b1, self.b2, self.eps,
+                                  wd, bc1, bc2, grad_scale, self._sumsq.data_ptr() if clip else 0, float(clip), st),
+                      "adamw")
+        else:
+            coef = 1.0
+            if clip:
+                nrm = math.sqrt(float(self._sumsq)) * abs(grad_scale)
+                coef = min(1.0, clip / (nrm + 1e-6))
+            for s, e, wd in segs:
+                if e <= s:
+                    continue
+                ops.reference.adamw_ref(self.master[s:e], g[s:e], self.m[s:e], self.v[s:e], lr, self.b1, self.b2,
+                                        self.eps, wd, t, grad_mul=grad_scale, clip=coef)
+            if self.master_weights:
+                flat.data.copy_(self.master.to(flat.dtype))
+
+    def grad_norm(self) -> float:
+        """Global grad norm of the last step (host sync — call only for logging)."""
+        if self.last_grad_norm is None:
+            return 0.0
+        return math.sqrt(float(self.last_grad_norm.item())) * abs(getattr(self, "_grad_scale", 1.0))
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    def state_dict(self):
+        return {"step": self.step_count, "m": self.m, "v": self.v, "master": self.master if self.master_weights else None,
+                "lr": self.lr, "betas": (self.b1, self.b2), "eps": self.eps, "wd": self.wd}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        if self.master_weights and sd.get("master") is not None:
+            self.master.copy_(sd["master"])
+            self.flat.data.copy_(self.master.to(self.flat.dtype))

@@ -1,0 +1,98 @@
+"""Llama pre-training loop (the Ray Train Llama-3-8B DDP headline workload).
+
+``llama_train_loop_per_worker(config)`` is a regular Train worker function: it runs under
+``TorchTrainer`` (one actor per GPU, process group over RCCL) and equally under an external
+``torchrun`` launch (one process per GPU). It builds the model directly on the GPU, wraps it
+in the framework's bucketed RCCL DDP, steps the fused flat AdamW, and reports timing.
+Synthetic token data of the configured shape (no dataset download is possible here).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+
+def _dist_info():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4, bucket_cap_mb=256.0,
+                         device=None, seed=1234, max_grad_norm=1.0, **model_overrides):
+    from ..models import build_llama
+    from ..parallel import DistributedDataParallel, FlatAdamW
+
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    rank, world = _dist_info()
+    torch.manual_seed(seed)
+    net = build_llama(model, device=device, max_seq_len=max(seq_len, 256), **model_overrides)
+    ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb)
+    opt = FlatAdamW(ddp.flat, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + rank)
+    V = net.cfg.vocab_size
+
+    def batch():
+        t = torch.randint(0, V, (micro_batch, seq_len + 1), device=device, generator=g)
+        return t[:, :-1].contiguous(), t[:, 1:].contiguous()
+
+    def step(tokens, labels):
+        loss = ddp(tokens, labels)
+        loss.backward()
+        ddp.finish_gradient_sync()
+        opt.step(grad_scale=ddp.grad_scale)
+        opt.zero_grad()
+        return loss
+
+    return net, ddp, opt, batch, step
+
+
+def llama_train_loop_per_worker(config: dict):
+    """Train-loop entry point. Config keys: model, seq_len, micro_batch, steps, warmup, lr,
+    bucket_cap_mb. Reports ``tokens_per_s`` (this worker) and ``ms_per_step``."""
+    from . import report
+
+    steps = int(config.get("steps", 10))
+    warmup = int(config.get("warmup", 3))
+    seq_len = int(config.get("seq_len", 4096))
+    mb = int(config.get("micro_batch", 2))
+    net, ddp, opt, batch, step = build_llama_training(
+        model=config.get("model", "llama3-8b"), seq_len=seq_len, micro_batch=mb, lr=config.get("lr", 3e-4),
+        bucket_cap_mb=config.get("bucket_cap_mb", 256.0), **config.get("model_overrides", {}))
+    rank, world = _dist_info()
+    data = [batch() for _ in range(2)]
+    loss = None
+    for i in range(warmup):
+        loss = step(*data[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = step(*data[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], device="cuda", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    tokens = steps * mb * seq_len * world
+    metrics = {
+        "loss": float(loss.item()) if loss is not None else float("nan"),
+        "elapsed_s": el,
+        "ms_per_step": 1000.0 * el / max(steps, 1),
+        "tokens_per_s": tokens / el if el > 0 else 0.0,
+        "world_size": world,
+        "mem_gb": torch.cuda.max_memory_allocated() / 1e9,
+        "flops_per_token": net.cfg.flops_per_token(seq_len),
+    }
+    report(metrics)
+    return metrics
