@@ -1,0 +1,64 @@
+"""ray_community_amd — an MI355X-native distributed compute framework with the capabilities of
+Ray (tasks, actors, objects, placement groups, collectives, Train, Tune, Data, Serve, RLlib).
+
+Core runtime: C++ shared-memory object store + C++ resource scheduler (``_native``), Python
+control plane. Compute path: PyTorch-ROCm + hand-written gfx950 HIP kernels (``ops``) + RCCL
+over xGMI (``parallel``, ``util.collective``).
+"""
+from __future__ import annotations
+
+__version__ = "0.1.0"
+
+import functools
+import inspect
+
+from . import exceptions
+from ._private.core_worker import DynamicObjectRefGenerator, ObjectRef, ObjectRefGenerator
+from ._private.ids import (ActorClassID, ActorID, FunctionID, JobID, NodeID, ObjectID, PlacementGroupID, TaskID,
+                           UniqueID, WorkerID)
+from ._private.worker import (LOCAL_MODE, SCRIPT_MODE, WORKER_MODE, available_resources, cancel, cluster_resources,
+                              free, get, get_actor, get_gpu_ids, get_runtime_context, init, is_initialized, kill,
+                              nodes, put, shutdown, timeline, wait)
+from .actor import ActorClass, ActorHandle, exit_actor, method
+from .remote_function import RemoteFunction
+
+
+def remote(*args, **kwargs):
+    """``@remote`` / ``@remote(num_cpus=..., num_gpus=..., ...)`` for functions and classes."""
+
+    def make(obj, opts):
+        if inspect.isclass(obj):
+            return ActorClass(obj, opts)
+        if callable(obj):
+            return RemoteFunction(obj, opts)
+        raise TypeError("The @remote decorator must be applied to either a function or a class.")
+
+    if len(args) == 1 and not kwargs and callable(args[0]):
+        return make(args[0], {})
+    if args:
+        raise TypeError("The @remote decorator must be applied either with no arguments and no parentheses, for "
+                        "example '@remote', or it must be applied using some of the arguments in the list "
+                        "['num_cpus', 'num_gpus', ...], for example '@remote(num_returns=2, resources={\"CustomResource\": 1})'.")
+    return lambda obj: make(obj, kwargs)
+
+
+_LAZY = {"util", "train", "tune", "data", "serve", "rllib", "dag", "air", "experimental", "models", "ops", "parallel",
+         "cluster_utils", "job_submission", "workflow", "runtime_env", "autoscaler", "utils"}
+
+
+def __getattr__(name):
+    if name in _LAZY:
+        import importlib
+
+        return importlib.import_module("." + name, __name__)
+    raise AttributeError(name)
+
+
+__all__ = [
+    "__version__", "remote", "init", "shutdown", "is_initialized", "get", "put", "wait", "cancel", "kill", "free",
+    "get_actor", "get_gpu_ids", "nodes", "cluster_resources", "available_resources", "timeline", "method",
+    "get_runtime_context", "ObjectRef", "ObjectRefGenerator", "DynamicObjectRefGenerator", "ActorHandle",
+    "ActorClass", "RemoteFunction", "exceptions", "exit_actor", "LOCAL_MODE", "SCRIPT_MODE", "WORKER_MODE",
+    "ActorID", "TaskID", "NodeID", "JobID", "ObjectID", "WorkerID", "FunctionID", "PlacementGroupID", "UniqueID",
+    "ActorClassID",
+]

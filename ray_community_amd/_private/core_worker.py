@@ -1,0 +1,562 @@
+"""Per-process core worker: ObjectRef, local reference counting, object get/put, task submission.
+
+Reference: ``python/ray/_raylet.pyx`` (CoreWorker, ObjectRef, ObjectRefGenerator) and
+``src/ray/core_worker/core_worker.cc``. The same ``CoreWorker`` class serves
+  * the driver in the head's process (``DirectClient``: in-process calls into the head), and
+  * worker processes / external drivers (``SocketClient``: framed RPC over a Unix socket).
+Objects are read zero-copy from the node's shm store; small objects travel inline.
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures
+import hashlib
+import itertools
+import os
+import socket
+import threading
+import time
+import weakref
+from typing import Any, Dict, List, Optional
+
+from .. import exceptions as exc
+from . import protocol as P
+from . import serialization as ser
+from .ids import new_id
+from .object_store import ObjectStore
+
+INLINE_THRESHOLD = 100 * 1024
+
+_core: Optional["CoreWorker"] = None
+
+
+def global_core() -> "CoreWorker":
+    if _core is None:
+        raise RuntimeError("ray_community_amd is not initialized; call init() first")
+    return _core
+
+
+def set_global_core(c):
+    global _core
+    _core = c
+
+
+# ====================================================================== ObjectRef
+class ObjectRef:
+    __slots__ = ("_id", "_core", "__weakref__")
+
+    def __init__(self, oid: bytes, _register=True):
+        self._id = oid
+        c = _core
+        self._core = c
+        if _register and c is not None:
+            c.ref_add(oid)
+
+    def __del__(self):
+        c = self._core
+        if c is not None:
+            try:
+                c.ref_remove(self._id)
+            except Exception:
+                pass
+
+    def binary(self):
+        return self._id
+
+    def hex(self):
+        return self._id.hex()
+
+    def task_id(self):
+        return None
+
+    def __hash__(self):
+        return hash(self._id)
+
+    def __eq__(self, other):
+        return isinstance(other, ObjectRef) and other._id == self._id
+
+    def __repr__(self):
+        return f"ObjectRef({self._id.hex()})"
+
+    def __reduce__(self):
+        ctx = ser.current_context()
+        if ctx is not None:
+            ctx.contained.append(self._id)
+        return (_rebuild_ref, (self._id,))
+
+    # futures / asyncio integration
+    def future(self) -> concurrent.futures.Future:
+        return global_core().as_future(self)
+
+    def __await__(self):
+        return asyncio.wrap_future(self.future()).__await__()
+
+    def _on_completed(self, cb):
+        f = self.future()
+        f.add_done_callback(lambda fut: cb(fut.result()))
+
+
+def _rebuild_ref(oid):
+    return ObjectRef(oid)
+
+
+class ObjectRefGenerator:
+    """Iterator over the outputs of a ``num_returns="streaming"`` task (reference:
+    ``ObjectRefGenerator`` in ``_raylet.pyx``). Yields ObjectRefs as the task produces them."""
+
+    def __init__(self, tid: bytes, main_ref: ObjectRef):
+        self._tid = tid
+        self._main = main_ref
+        self._i = 0
+        self._done = False
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return self._next_sync(None)
+
+    def _next_sync(self, timeout_s=None):
+        if self._done:
+            raise StopIteration
+        core = global_core()
+        oid = core.client.call("gen_next", self._tid, self._i, timeout_s)
+        if oid is None:
+            self._done = True
+            # surface a generator failure (stored on the task's main return object)
+            core.get([self._main], timeout=None, _raise=True)
+            raise StopIteration
+        self._i += 1
+        ref = ObjectRef(oid)
+        core.ref_remove_server_pin(oid)
+        return ref
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        loop = asyncio.get_running_loop()
+        try:
+            return await loop.run_in_executor(None, self._next_sync, None)
+        except StopIteration:
+            raise StopAsyncIteration
+
+    def completed(self):
+        return self._main
+
+    def is_finished(self):
+        return self._done
+
+
+class DynamicObjectRefGenerator:
+    """Return value of a ``num_returns="dynamic"`` task: an iterable of ObjectRefs."""
+
+    def __init__(self, refs):
+        self._refs = list(refs)
+
+    def __iter__(self):
+        return iter(self._refs)
+
+    def __len__(self):
+        return len(self._refs)
+
+
+# ====================================================================== clients
+class DirectClient:
+    """In-process calls into the head (driver co-located with the head)."""
+
+    def __init__(self, head):
+        self.head = head
+        self.key = "driver"
+
+    def call(self, method, *args, **kwargs):
+        head = self.head
+        with head.lock:
+            res = getattr(head, "rpc_" + method)(self.key, *args, **kwargs)
+        if res.__class__.__name__ == "Deferred":
+            ev = threading.Event()
+            res.add(lambda d: ev.set())
+            ev.wait()
+            if not res.ok:
+                raise res.value
+            return res.value
+        return res
+
+    def call_async(self, method, *args):
+        fut = concurrent.futures.Future()
+        head = self.head
+        try:
+            with head.lock:
+                res = getattr(head, "rpc_" + method)(self.key, *args)
+        except Exception as e:
+            fut.set_exception(e)
+            return fut
+        if res.__class__.__name__ == "Deferred":
+            def done(d):
+                if d.ok:
+                    fut.set_result(d.value)
+                else:
+                    fut.set_exception(d.value)
+            res.add(done)
+        else:
+            fut.set_result(res)
+        return fut
+
+    def ref_delta(self, adds, removes):
+        head = self.head
+        with head.lock:
+            for o in adds:
+                head._add_holder(o, self.key)
+            for o in removes:
+                head._remove_holder(o, self.key)
+
+    def submit(self, spec):
+        head = self.head
+        with head.lock:
+            head._submit(spec, self.key)
+
+    def close(self):
+        pass
+
+
+class SocketClient:
+    """Framed RPC client over the head's Unix socket (workers and external drivers)."""
+
+    def __init__(self, sock_path, kind, ident, on_message=None):
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(sock_path)
+        self.conn = P.Connection(s)
+        self._req = itertools.count(1)
+        self._pending: Dict[int, concurrent.futures.Future] = {}
+        self._lock = threading.Lock()
+        self.on_message = on_message
+        self.kind = kind
+        self._closed = False
+        self._adds: List[bytes] = []
+        self._removes: List[bytes] = []
+        self._rlock = threading.Lock()
+        self.hello = None
+        if kind == "client":
+            f = concurrent.futures.Future()
+            self._pending[0] = f
+        self._reader = threading.Thread(target=self._read_loop, name="rca-client-reader", daemon=True)
+        self._reader.start()
+        self.conn.send((P.REGISTER, kind, ident, os.getpid()))
+        if kind == "client":
+            self.hello = f.result(timeout=30)
+        self._flusher = threading.Thread(target=self._flush_loop, name="rca-ref-flush", daemon=True)
+        self._flusher.start()
+
+    def _read_loop(self):
+        while True:
+            try:
+                msg = self.conn.recv()
+            except Exception:
+                self._closed = True
+                with self._lock:
+                    for f in self._pending.values():
+                        if not f.done():
+                            f.set_exception(exc.RaySystemError("connection to the head was lost"))
+                if self.on_message is not None:
+                    try:
+                        self.on_message((P.EXIT,))
+                    except Exception:
+                        pass
+                return
+            if msg[0] == P.REPLY:
+                _, rid, ok, val = msg
+                with self._lock:
+                    f = self._pending.pop(rid, None)
+                if f is not None:
+                    if ok:
+                        f.set_result(val)
+                    else:
+                        f.set_exception(val if isinstance(val, BaseException) else exc.RaySystemError(str(val)))
+            elif self.on_message is not None:
+                self.on_message(msg)
+
+    def _flush_loop(self):
+        while not self._closed:
+            time.sleep(0.005)
+            self.flush_refs()
+
+    def flush_refs(self):
+        if not self._adds and not self._removes:
+            return
+        with self._rlock:
+            adds, self._adds = self._adds, []
+            removes, self._removes = self._removes, []
+        if adds or removes:
+            try:
+                self.conn.send((P.REF_DELTA, adds, removes))
+            except OSError:
+                pass
+
+    def call_async(self, method, *args, **kwargs):
+        rid = next(self._req)
+        f = concurrent.futures.Future()
+        with self._lock:
+            self._pending[rid] = f
+        self.flush_refs()
+        if self._closed:
+            raise exc.RaySystemError("connection to the head was lost")
+        self.conn.send((P.RPC, rid, method, args, kwargs))
+        return f
+
+    def call(self, method, *args, **kwargs):
+        return self.call_async(method, *args, **kwargs).result()
+
+    def ref_delta(self, adds, removes):
+        with self._rlock:
+            self._adds.extend(adds)
+            self._removes.extend(removes)
+
+    def submit(self, spec):
+        # fire-and-forget submission; errors surface through the return objects
+        self.call_async("submit", spec)
+
+    def send(self, msg):
+        self.flush_refs()
+        self.conn.send(msg)
+
+    def close(self):
+        self._closed = True
+        self.conn.close()
+
+
+# ====================================================================== CoreWorker
+class TaskContext(threading.local):
+    def __init__(self):
+        self.task_id = None
+        self.actor_id = None
+        self.task_name = None
+        self.put_index = 0
+
+
+class CoreWorker:
+    def __init__(self, mode: str, client, store: ObjectStore, node_id: str, job_id: bytes, namespace: str = "",
+                 worker_id: Optional[bytes] = None, session_dir: str = ""):
+        self.mode = mode  # "driver" | "worker" | "client"
+        self.client = client
+        self.store = store
+        self.node_id = node_id
+        self.job_id = job_id
+        self.namespace = namespace
+        self.worker_id = worker_id or new_id()
+        self.session_dir = session_dir
+        self._refs: Dict[bytes, int] = {}
+        self._ref_lock = threading.Lock()
+        self.ctx = TaskContext()
+        self.registered_functions = set()
+        self.gpu_pins: Dict[bytes, list] = {}
+        self.actor_id = None
+        self.gpu_ids = ()
+        self.assigned_resources = {}
+        self.current_actor = None
+        self._shutdown = False
+
+    # -------------------------------------------------------------- reference counting
+    def ref_add(self, oid):
+        with self._ref_lock:
+            n = self._refs.get(oid, 0)
+            self._refs[oid] = n + 1
+        if n == 0:
+            self.client.ref_delta((oid,), ())
+
+    def ref_remove(self, oid):
+        if self._shutdown:
+            return
+        with self._ref_lock:
+            n = self._refs.get(oid, 0) - 1
+            if n <= 0:
+                self._refs.pop(oid, None)
+            else:
+                self._refs[oid] = n
+        if n == 0:
+            self.client.ref_delta((), (oid,))
+
+    def ref_remove_server_pin(self, oid):
+        """The head pre-registered this process as a holder when it handed out ``oid``;
+        ObjectRef creation already counted it — nothing to undo (holder sets are idempotent)."""
+
+    def local_ref_count(self, oid):
+        return self._refs.get(oid, 0)
+
+    # -------------------------------------------------------------- objects
+    def _store_serialized(self, oid, s: ser.Serialized):
+        if s.total_size <= INLINE_THRESHOLD:
+            b = s.to_bytes()
+            return ("inline", b, len(b))
+        if self.store.put_serialized(oid, s):
+            return ("shm", None, s.total_size)
+        # store full: ask the head to spill, retry, else write a spill file directly
+        for _ in range(3):
+            self.client.call("make_room", s.total_size)
+            if self.store.put_serialized(oid, s):
+                return ("shm", None, s.total_size)
+        path = os.path.join(self.session_dir or "/tmp", "spill", oid.hex())
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "wb") as f:
+            f.write(s.to_bytes())
+        return ("spill", path, s.total_size)
+
+    def put(self, value, _owner_address=None) -> ObjectRef:
+        if isinstance(value, ObjectRef):
+            raise TypeError("Calling put() on an ObjectRef is not allowed.")
+        oid = new_id()
+        s = ser.serialize(value)
+        desc = self._store_serialized(oid, s)
+        if s.gpu_tensors:
+            self.gpu_pins[oid] = s.gpu_tensors
+        ref = ObjectRef(oid, _register=False)
+        with self._ref_lock:
+            self._refs[oid] = self._refs.get(oid, 0) + 1
+        self.client.call("put", oid, desc, s.contained, bool(s.gpu_tensors), s.flags) if self.mode != "driver" else \
+            self.client.call("put", oid, desc, s.contained, bool(s.gpu_tensors), s.flags)
+        return ref
+
+    def free_gpu_objects(self, oids):
+        for o in oids:
+            self.gpu_pins.pop(o, None)
+
+    def _materialize(self, oid, desc):
+        kind, data, size, flags = desc
+        if kind == "inline":
+            value, _ = ser.deserialize(data)
+        elif kind == "shm":
+            view = self.store.pin(oid)
+            if view is None:
+                # raced with spilling: ask again (the head restores it)
+                d2 = self.client.call("get", [oid], None)[0]
+                if d2[0] == "shm":
+                    view = self.store.pin(oid)
+                    if view is None:
+                        raise exc.ObjectLostError(oid.hex())
+                else:
+                    return self._materialize(oid, d2)
+            value, _ = ser.deserialize(memoryview(view))
+        elif kind == "spill":
+            with open(data, "rb") as f:
+                value, _ = ser.deserialize(f.read())
+        else:
+            raise exc.RaySystemError(f"bad object descriptor {kind}")
+        if flags & ser.FLAG_ERROR:
+            return _ErrorValue(value)
+        return value
+
+    def get(self, refs, timeout=None, _raise=True):
+        single = isinstance(refs, ObjectRef)
+        if single:
+            refs = [refs]
+        for r in refs:
+            if not isinstance(r, ObjectRef):
+                raise TypeError(f"get() expects ObjectRefs, got {type(r)}")
+        if not refs:
+            return []
+        oids = [r._id for r in refs]
+        descs = self.client.call("get", oids, timeout)
+        out = []
+        for oid, d in zip(oids, descs):
+            v = self._materialize(oid, d)
+            if isinstance(v, _ErrorValue):
+                if _raise:
+                    raise v.as_exception()
+                v = v.err
+            out.append(v)
+        return out[0] if single else out
+
+    def as_future(self, ref) -> concurrent.futures.Future:
+        out = concurrent.futures.Future()
+        f = self.client.call_async("get", [ref._id], None)
+
+        def done(fut):
+            try:
+                d = fut.result()[0]
+                v = self._materialize(ref._id, d)
+                if isinstance(v, _ErrorValue):
+                    out.set_exception(v.as_exception())
+                else:
+                    out.set_result(v)
+            except BaseException as e:  # noqa
+                out.set_exception(e)
+
+        f.add_done_callback(done)
+        return out
+
+    def wait(self, refs, num_returns=1, timeout=None, fetch_local=True):
+        if isinstance(refs, ObjectRef):
+            raise TypeError("wait() expected a list of ObjectRefs")
+        refs = list(refs)
+        if len(set(r._id for r in refs)) != len(refs):
+            raise ValueError("Wait requires a list of unique object refs.")
+        if num_returns <= 0:
+            raise ValueError("Invalid number of objects to return %d." % num_returns)
+        if num_returns > len(refs):
+            raise ValueError("num_returns cannot be greater than the number of objects provided.")
+        ready_ids = set(self.client.call("wait", [r._id for r in refs], num_returns, timeout, fetch_local))
+        ready = [r for r in refs if r._id in ready_ids][:num_returns]
+        rs = set(id(r) for r in ready)
+        not_ready = [r for r in refs if id(r) not in rs]
+        return ready, not_ready
+
+    # -------------------------------------------------------------- functions
+    def function_id(self, blob: bytes) -> bytes:
+        return hashlib.sha1(blob).digest()
+
+    # -------------------------------------------------------------- args
+    def encode_args(self, args, kwargs):
+        out = []
+        contained = []
+        deps = []
+        for a in list(args) + list(kwargs.values()):
+            if isinstance(a, ObjectRef):
+                out.append(("r", a._id))
+                deps.append(a)
+                continue
+            s = ser.serialize(a)
+            if s.gpu_tensors:
+                # GPU tensors passed by value become GPU objects owned by this process
+                ref = self._put_serialized(s)
+                out.append(("r", ref._id))
+                deps.append(ref)
+                continue
+            if s.total_size > INLINE_THRESHOLD:
+                ref = self._put_serialized(s)
+                out.append(("r", ref._id))
+                deps.append(ref)
+                continue
+            out.append(("v", s.to_bytes()))
+            contained.extend(s.contained)
+        return out, list(kwargs.keys()), contained, deps
+
+    def _put_serialized(self, s):
+        oid = new_id()
+        desc = self._store_serialized(oid, s)
+        if s.gpu_tensors:
+            self.gpu_pins[oid] = s.gpu_tensors
+        ref = ObjectRef(oid, _register=False)
+        with self._ref_lock:
+            self._refs[oid] = self._refs.get(oid, 0) + 1
+        self.client.call("put", oid, desc, s.contained, bool(s.gpu_tensors), s.flags)
+        return ref
+
+    def submit_spec(self, spec, deps=()):
+        spec["parent"] = self.ctx.task_id
+        spec["caller_node"] = self.node_id
+        self.client.submit(spec)
+
+    def shutdown(self):
+        self._shutdown = True
+
+
+class _ErrorValue:
+    __slots__ = ("err",)
+
+    def __init__(self, err):
+        self.err = err
+
+    def as_exception(self):
+        e = self.err
+        if isinstance(e, exc.RayTaskError):
+            return e.as_instanceof_cause()
+        return e

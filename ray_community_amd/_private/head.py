@@ -1,0 +1,1809 @@
+"""The head service: GCS tables + raylet (scheduler, worker pool, object directory) in one.
+
+Reference counterparts: ``src/ray/gcs/gcs_server/*`` (actor / placement-group / node / KV tables),
+``src/ray/raylet/{node_manager,worker_pool,local_task_manager}.cc``, and the ownership /
+reference-counting logic of ``src/ray/core_worker/{reference_count,task_manager}.cc``.
+
+Design: one head per session, living in the driver process (or in its own process via
+``ray_community_amd.scripts start --head``). A selector thread serves worker connections; driver
+API calls enter the same state machine directly under ``self.lock``. Resource accounting and
+queueing are delegated to the C++ ``Scheduler``; objects live in the C++ shm store. Node
+"virtualisation" (``cluster_utils.Cluster``) = extra scheduler nodes with their own worker pools.
+"""
+from __future__ import annotations
+
+import collections
+import json
+import logging
+import os
+import selectors
+import shutil
+import socket
+import subprocess
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Callable, Dict, List, Optional, Set
+
+from .. import exceptions as exc
+from . import protocol as P
+from .ids import new_id
+from .object_store import ObjectStore, default_store_capacity, native
+from .serialization import FLAG_ERROR, serialize
+
+log = logging.getLogger("ray_community_amd.head")
+
+DRIVER = "driver"
+INLINE_THRESHOLD = 100 * 1024
+
+# object states
+PENDING, READY, FREED = 0, 1, 2
+# task states
+T_WAIT_DEPS, T_QUEUED, T_WAIT_WORKER, T_RUNNING, T_FINISHED, T_FAILED, T_CANCELLED = range(7)
+TASK_STATE_NAMES = ["PENDING_ARGS_AVAIL", "PENDING_NODE_ASSIGNMENT", "PENDING_WORKER", "RUNNING", "FINISHED",
+                    "FAILED", "CANCELLED"]
+# actor states
+A_PENDING, A_ALIVE, A_RESTARTING, A_DEAD = "PENDING_CREATION", "ALIVE", "RESTARTING", "DEAD"
+
+
+class Deferred:
+    __slots__ = ("callbacks", "done", "value", "ok")
+
+    def __init__(self):
+        self.callbacks = []
+        self.done = False
+        self.value = None
+        self.ok = True
+
+    def resolve(self, value, ok=True):
+        if self.done:
+            return
+        self.done = True
+        self.value = value
+        self.ok = ok
+        cbs, self.callbacks = self.callbacks, []
+        for cb in cbs:
+            cb(self)
+
+    def add(self, cb):
+        if self.done:
+            cb(self)
+        else:
+            self.callbacks.append(cb)
+
+
+class ObjEntry:
+    __slots__ = ("oid", "state", "desc", "holders", "pins", "waiters", "contained", "task", "gpu_owner", "size",
+                 "flags", "created")
+
+    def __init__(self, oid, task=None):
+        self.oid = oid
+        self.state = PENDING
+        self.desc = None
+        self.holders: Set[str] = set()
+        self.pins = 0
+        self.waiters: List[Callable] = []
+        self.contained: List[bytes] = []
+        self.task = task
+        self.gpu_owner = None
+        self.size = 0
+        self.flags = 0
+        self.created = time.time()
+
+
+class TaskState:
+    __slots__ = ("tid", "spec", "state", "deps", "retries_left", "worker", "node", "demand", "owner", "key", "gpus",
+                 "times", "children", "parent", "cancelled", "blocked", "gen_items", "gen_done", "gen_waiters",
+                 "error_type", "attempt")
+
+    def __init__(self, tid, spec, owner):
+        self.tid = tid
+        self.spec = spec
+        self.state = T_WAIT_DEPS
+        self.deps: Set[bytes] = set()
+        self.retries_left = spec.get("max_retries", 0)
+        self.worker = None
+        self.node = None
+        self.demand = {}
+        self.owner = owner
+        self.key = None
+        self.gpus = ()
+        self.times = {"submit": time.time()}
+        self.children: List[bytes] = []
+        self.parent = spec.get("parent")
+        self.cancelled = False
+        self.blocked = False
+        self.gen_items: List[bytes] = []
+        self.gen_done = False
+        self.gen_waiters: Dict[int, List[Deferred]] = {}
+        self.error_type = None
+        self.attempt = 0
+
+
+class ActorState:
+    def __init__(self, aid, spec, owner):
+        self.aid = aid
+        self.spec = spec
+        self.state = A_PENDING
+        self.worker = None
+        self.node = None
+        self.queue: collections.deque = collections.deque()
+        self.inflight: Dict[bytes, TaskState] = {}
+        self.restarts_left = spec.get("max_restarts", 0)
+        self.num_restarts = 0
+        self.name = spec.get("actor_name")
+        self.namespace = spec.get("namespace", "")
+        self.detached = spec.get("lifetime") == "detached"
+        self.owner = owner
+        self.demand = {}
+        self.gpus = ()
+        self.death_cause = None
+        self.ready_waiters: List[Deferred] = []
+        self.creation_task: Optional[TaskState] = None
+        self.pid = None
+        self.killed = False
+
+
+class WorkerState:
+    def __init__(self, wid, node_id, env_key, proc, gpus):
+        self.wid = wid
+        self.node_id = node_id
+        self.env_key = env_key
+        self.proc = proc
+        self.conn: Optional[socket.socket] = None
+        self.reader = P.FrameReader()
+        self.send_lock = threading.Lock()
+        self.pid = proc.pid if proc else None
+        self.state = "starting"
+        self.task: Optional[TaskState] = None
+        self.actor: Optional[ActorState] = None
+        self.known_functions: Set[bytes] = set()
+        self.gpus = gpus
+        self.idle_since = time.time()
+        self.dead = False
+        self.gpu_objects: Set[bytes] = set()
+        self.out = collections.deque()
+
+
+class NodeState:
+    def __init__(self, node_id, resources, labels=None, is_head=False):
+        self.node_id = node_id
+        self.resources = dict(resources)
+        self.labels = labels or {}
+        self.is_head = is_head
+        self.idle: Dict[Any, List[WorkerState]] = collections.defaultdict(list)
+        self.starting: Dict[Any, int] = collections.defaultdict(int)
+        self.dispatch_q: Dict[Any, collections.deque] = collections.defaultdict(collections.deque)
+        self.gpu_free = [1.0] * int(resources.get("GPU", 0))
+        self.alive = True
+        self.start_time = time.time()
+
+
+class Head:
+    def __init__(self, session_dir: str, resources: dict, object_store_memory: Optional[int] = None,
+                 namespace: str = "", system_config: Optional[dict] = None, job_id: Optional[bytes] = None,
+                 labels: Optional[dict] = None):
+        self.lock = threading.RLock()
+        self.session_dir = session_dir
+        os.makedirs(session_dir, exist_ok=True)
+        self.spill_dir = os.path.join(session_dir, "spill")
+        os.makedirs(self.spill_dir, exist_ok=True)
+        self.logs_dir = os.path.join(session_dir, "logs")
+        os.makedirs(self.logs_dir, exist_ok=True)
+        self.config = dict(system_config or {})
+        self.namespace = namespace
+        self.job_id = job_id or new_id()
+        self.sched = native().Scheduler(float(self.config.get("scheduler_spread_threshold", 0.5)))
+        cap = object_store_memory or default_store_capacity()
+        self.store_name = "/rca_" + new_id().hex()[-16:]
+        self.store = ObjectStore(self.store_name, cap, create=True)
+        self.store_capacity = cap
+        self.objects: Dict[bytes, ObjEntry] = {}
+        self.tasks: Dict[bytes, TaskState] = {}
+        self.task_keys: Dict[int, TaskState] = {}
+        self._key = 0
+        self.actors: Dict[bytes, ActorState] = {}
+        self.named_actors: Dict[tuple, bytes] = {}
+        self.workers: Dict[bytes, WorkerState] = {}
+        self.nodes: Dict[str, NodeState] = {}
+        self.pgs: Dict[bytes, dict] = {}
+        self.pending_pgs: List[bytes] = []
+        self.kv: Dict[tuple, bytes] = {}
+        self.functions: Dict[bytes, bytes] = {}
+        self.events: collections.deque = collections.deque(maxlen=int(self.config.get("task_events_max", 100000)))
+        self.finished_tasks: collections.deque = collections.deque(maxlen=10000)
+        self.timers: List[tuple] = []
+        self.spilled_bytes = 0
+        self.num_spilled = 0
+        self.num_restored = 0
+        self.driver_gpu_objects: Set[bytes] = set()
+        self.driver_free_gpu_cb = None
+        self.driver_task_cancel_cb = None
+        self.shutting_down = False
+        # head node
+        self.head_node_id = new_id().hex()
+        self._add_node(self.head_node_id, resources, labels, is_head=True)
+        # network
+        self.sock_path = os.path.join(session_dir, "head.sock")
+        if os.path.exists(self.sock_path):
+            os.unlink(self.sock_path)
+        self.listener = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.listener.bind(self.sock_path)
+        self.listener.listen(1024)
+        self.listener.setblocking(False)
+        self.sel = selectors.DefaultSelector()
+        self.sel.register(self.listener, selectors.EVENT_READ, ("listen", None))
+        self._wake_r, self._wake_w = socket.socketpair()
+        self._wake_r.setblocking(False)
+        self.sel.register(self._wake_r, selectors.EVENT_READ, ("wake", None))
+        self.conn_worker: Dict[int, WorkerState] = {}
+        self.clients: Dict[int, "ClientConn"] = {}
+        self._thread = threading.Thread(target=self._loop, name="rca-head", daemon=True)
+        self._thread.start()
+        prestart = int(self.config.get("prestart_workers", min(2, int(resources.get("CPU", 1)))))
+        with self.lock:
+            for _ in range(prestart):
+                self._start_worker(self.nodes[self.head_node_id], self._env_key({}, ()), ())
+
+    # ================================================================== nodes
+    def _add_node(self, node_id, resources, labels=None, is_head=False):
+        res = {k: float(v) for k, v in resources.items() if v}
+        res.setdefault("memory", 8e9)
+        res[f"node:{node_id}"] = 1.0
+        if is_head:
+            res["node:__internal_head__"] = 1.0
+        self.sched.add_node(node_id, res)
+        self.nodes[node_id] = NodeState(node_id, res, labels, is_head)
+        return node_id
+
+    def add_node(self, resources: dict, labels=None) -> str:
+        with self.lock:
+            nid = new_id().hex()
+            self._add_node(nid, resources, labels)
+            self._schedule()
+            return nid
+
+    def remove_node(self, node_id: str):
+        with self.lock:
+            node = self.nodes.get(node_id)
+            if node is None or node.is_head:
+                return
+            node.alive = False
+            self.sched.remove_node(node_id)
+            for w in list(self.workers.values()):
+                if w.node_id == node_id and not w.dead:
+                    self._kill_worker(w)
+            self._schedule()
+
+    # ================================================================== main loop
+    def _loop(self):
+        while not self.shutting_down:
+            try:
+                events = self.sel.select(timeout=0.05)
+            except OSError:
+                if self.shutting_down:
+                    return
+                raise
+            for key, _ in events:
+                kind, obj = key.data
+                if kind == "listen":
+                    self._accept()
+                elif kind == "wake":
+                    try:
+                        self._wake_r.recv(65536)
+                    except BlockingIOError:
+                        pass
+                elif kind == "conn":
+                    self._read_conn(key.fileobj, obj)
+            if self.timers:
+                self._fire_timers()
+            self._reap_idle()
+
+    def wake(self):
+        try:
+            self._wake_w.send(b"x")
+        except OSError:
+            pass
+
+    def _accept(self):
+        while True:
+            try:
+                c, _ = self.listener.accept()
+            except (BlockingIOError, OSError):
+                return
+            c.setblocking(True)
+            cc = ClientConn(c)
+            self.sel.register(c, selectors.EVENT_READ, ("conn", cc))
+
+    def _read_conn(self, sock, cc):
+        try:
+            data = sock.recv(1 << 20)
+        except (ConnectionError, OSError):
+            data = b""
+        if not data:
+            self._on_disconnect(sock, cc)
+            return
+        for msg in cc.reader.feed(data):
+            try:
+                with self.lock:
+                    self._handle(cc, msg)
+            except Exception:
+                log.error("head: error handling %s\n%s", msg[0], traceback.format_exc())
+
+    def _on_disconnect(self, sock, cc):
+        try:
+            self.sel.unregister(sock)
+        except Exception:
+            pass
+        try:
+            sock.close()
+        except Exception:
+            pass
+        with self.lock:
+            if cc.worker is not None:
+                self._on_worker_death(cc.worker, "worker process exited")
+            elif cc.client_key is not None:
+                self._drop_holder_everywhere(cc.client_key)
+
+    def _send(self, cc_or_worker, msg):
+        conn = cc_or_worker.conn if isinstance(cc_or_worker, WorkerState) else cc_or_worker
+        if conn is None:
+            return
+        try:
+            conn.send(msg)
+        except OSError:
+            pass
+
+    # ================================================================== message dispatch
+    def _handle(self, cc, msg):
+        t = msg[0]
+        if t == P.TASK_DONE:
+            self._on_task_done(cc.worker, msg[1], msg[2], msg[3])
+        elif t == P.RPC:
+            _, req_id, method, args, kwargs = msg
+            caller = cc.key()
+            try:
+                fn = getattr(self, "rpc_" + method)
+                res = fn(caller, *args, **kwargs)
+            except Exception as e:
+                self._send(cc, (P.REPLY, req_id, False, e))
+                return
+            if isinstance(res, Deferred):
+                res.add(lambda d, cc=cc, req_id=req_id: self._send(cc, (P.REPLY, req_id, d.ok, d.value)))
+            else:
+                self._send(cc, (P.REPLY, req_id, True, res))
+        elif t == P.REF_DELTA:
+            key = cc.key()
+            for oid in msg[1]:
+                self._add_holder(oid, key)
+            for oid in msg[2]:
+                self._remove_holder(oid, key)
+        elif t == P.GEN_ITEM:
+            self._on_gen_item(msg[1], msg[2], msg[3])
+        elif t == P.BLOCKED:
+            self._on_blocked(cc.worker, msg[1])
+        elif t == P.REGISTER:
+            self._on_register(cc, msg)
+        elif t == P.LOG:
+            pass
+
+    def _on_register(self, cc, msg):
+        _, kind, ident, pid = msg[:4]
+        if kind == "worker":
+            w = self.workers.get(ident)
+            if w is None or w.dead:
+                cc.conn.send((P.EXIT,))
+                return
+            cc.worker = w
+            self.start_failures = 0
+            w.conn = cc.conn
+            w.pid = pid
+            w.state = "idle"
+            node = self.nodes[w.node_id]
+            node.starting[w.env_key] = max(0, node.starting[w.env_key] - 1)
+            self._worker_available(w)
+        else:  # client driver
+            cc.client_key = "client:" + ident.hex()
+            cc.conn.send((P.REPLY, 0, True, {"store": self.store_name, "node_id": self.head_node_id,
+                                              "job_id": self.job_id, "namespace": self.namespace,
+                                              "session_dir": self.session_dir}))
+
+    # ================================================================== objects
+    def _obj(self, oid, create=True, task=None) -> Optional[ObjEntry]:
+        e = self.objects.get(oid)
+        if e is None and create:
+            e = ObjEntry(oid, task)
+            self.objects[oid] = e
+        return e
+
+    def _add_holder(self, oid, key):
+        e = self.objects.get(oid)
+        if e is None:
+            if oid[:1] == b"A":
+                a = self.actors.get(oid[1:])
+                if a is not None:
+                    self._actor_handles(a).add(key)
+            return
+        if e.state != FREED:
+            e.holders.add(key)
+
+    def _remove_holder(self, oid, key):
+        if oid[:1] == b"A" and len(oid) == 21:
+            a = self.actors.get(oid[1:])
+            if a is not None:
+                self._actor_handles(a).discard(key)
+                self._maybe_kill_unreferenced(a)
+            return
+        e = self.objects.get(oid)
+        if e is None:
+            return
+        e.holders.discard(key)
+        self._maybe_free(e)
+
+    def _actor_handles(self, a):
+        hs = getattr(a, "handles", None)
+        if hs is None:
+            hs = set()
+            a.handles = hs
+        return hs
+
+    def _pin(self, oid, n=1):
+        e = self.objects.get(oid)
+        if e is not None:
+            e.pins += n
+        elif oid[:1] == b"A" and len(oid) == 21:
+            a = self.actors.get(oid[1:])
+            if a is not None:
+                a.pins = getattr(a, "pins", 0) + n
+
+    def _unpin(self, oid, n=1):
+        e = self.objects.get(oid)
+        if e is not None:
+            e.pins -= n
+            self._maybe_free(e)
+        elif oid[:1] == b"A" and len(oid) == 21:
+            a = self.actors.get(oid[1:])
+            if a is not None:
+                a.pins = getattr(a, "pins", 0) - n
+                self._maybe_kill_unreferenced(a)
+
+    def _maybe_kill_unreferenced(self, a):
+        if self._actor_handles(a) or getattr(a, "pins", 0) > 0 or a.detached or a.state == A_DEAD or a.name:
+            return
+        self._kill_actor(a, no_restart=True, reason="all handles to the actor went out of scope")
+
+    def _maybe_free(self, e: ObjEntry):
+        if e.holders or e.pins > 0 or e.state == FREED:
+            return
+        if e.state == PENDING:
+            return  # freed when the producing task completes (result discarded)
+        self._free(e)
+
+    def _free(self, e: ObjEntry):
+        e.state = FREED
+        d = e.desc
+        if d is not None:
+            if d[0] == "shm":
+                self.store.delete(e.oid)
+            elif d[0] == "spill":
+                try:
+                    os.unlink(d[1])
+                except OSError:
+                    pass
+        if e.gpu_owner is not None:
+            self._free_gpu_object(e.gpu_owner, e.oid)
+        e.desc = None
+        for c in e.contained:
+            self._unpin(c)
+        e.contained = []
+        self.objects.pop(e.oid, None)
+
+    def _free_gpu_object(self, owner, oid):
+        if owner == DRIVER:
+            if self.driver_free_gpu_cb:
+                self.driver_free_gpu_cb([oid])
+            return
+        w = self.workers.get(owner)
+        if w is not None and not w.dead:
+            self._send(w, (P.FREE_GPU, [oid]))
+
+    def _drop_holder_everywhere(self, key):
+        for e in list(self.objects.values()):
+            if key in e.holders:
+                e.holders.discard(key)
+                self._maybe_free(e)
+        for a in list(self.actors.values()):
+            hs = getattr(a, "handles", None)
+            if hs and key in hs:
+                hs.discard(key)
+                self._maybe_kill_unreferenced(a)
+
+    def _set_ready(self, e: ObjEntry, desc, contained=(), gpu_owner=None, flags=0):
+        if e.state == FREED:
+            return
+        e.desc = desc
+        e.flags = flags
+        e.size = desc[2] or 0
+        e.contained = list(contained)
+        for c in e.contained:
+            self._pin(c)
+        e.gpu_owner = gpu_owner
+        e.state = READY
+        ws, e.waiters = e.waiters, []
+        for cb in ws:
+            cb(e)
+        if not e.holders and e.pins <= 0:
+            self._free(e)
+
+    def _set_error(self, e: ObjEntry, err: BaseException):
+        b = serialize(err, error=True).to_bytes()
+        self._set_ready(e, ("inline", b, len(b)), flags=FLAG_ERROR)
+
+    def _when_ready(self, oids, cb_each):
+        for oid in oids:
+            e = self.objects.get(oid)
+            if e is None or e.state != PENDING:
+                cb_each(oid)
+            else:
+                e.waiters.append(lambda e, oid=oid: cb_each(oid))
+
+    def _desc_for(self, oid, caller):
+        """Descriptor handed to a reader (+ holder registration for refs nested inside)."""
+        e = self.objects.get(oid)
+        if e is None or e.state == FREED:
+            err = exc.ObjectLostError(oid.hex())
+            b = serialize(err, error=True).to_bytes()
+            return ("inline", b, len(b), FLAG_ERROR)
+        for c in e.contained:
+            ce = self.objects.get(c)
+            if ce is not None:
+                ce.holders.add(caller)
+        d = e.desc
+        if d[0] == "spill" and self.config.get("restore_spilled", True):
+            self._restore(e)
+            d = e.desc
+        return (d[0], d[1], d[2], e.flags)
+
+    # -------------------------------------------------------------- put
+    def rpc_put(self, caller, oid, desc, contained, is_gpu=False, flags=0):
+        e = self._obj(oid)
+        e.holders.add(caller)
+        owner = None
+        if is_gpu:
+            if caller == DRIVER:
+                owner = DRIVER
+            elif caller.startswith("w:"):
+                owner = bytes.fromhex(caller[2:])
+                w = self.workers.get(owner)
+                if w is not None:
+                    w.gpu_objects.add(oid)
+        self._set_ready(e, tuple(desc), contained, owner, flags)
+        return True
+
+    def rpc_make_room(self, caller, nbytes):
+        """Spill LRU objects until ``nbytes`` could fit (best effort). Returns freed bytes."""
+        return self._spill(nbytes)
+
+    def _spill(self, nbytes):
+        freed = 0
+        cands = self.store.lru_candidates(256)
+        for oid, size in cands:
+            e = self.objects.get(oid)
+            if e is None or e.state != READY or e.desc[0] != "shm":
+                continue
+            data = self.store.read_bytes(oid)
+            if data is None:
+                continue
+            path = os.path.join(self.spill_dir, oid.hex())
+            with open(path, "wb") as f:
+                f.write(data)
+            e.desc = ("spill", path, size)
+            self.store.delete(oid)
+            self.spilled_bytes += size
+            self.num_spilled += 1
+            freed += size
+            if freed >= nbytes * 1.2 + (1 << 20):
+                break
+        return freed
+
+    def _restore(self, e):
+        path, size = e.desc[1], e.desc[2]
+        try:
+            with open(path, "rb") as f:
+                data = f.read()
+        except OSError:
+            return
+        ok = self.store.put_bytes(e.oid, data)
+        if not ok:
+            self._spill(len(data))
+            ok = self.store.put_bytes(e.oid, data)
+        if ok:
+            e.desc = ("shm", None, size)
+            self.num_restored += 1
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+
+    # -------------------------------------------------------------- get / wait
+    def rpc_get(self, caller, oids, timeout=None):
+        d = Deferred()
+        remaining = {o for o in oids}
+        for oid in oids:
+            e = self.objects.get(oid)
+            if e is not None and e.state == PENDING:
+                continue
+            remaining.discard(oid)
+        if not remaining:
+            d.resolve([self._desc_for(o, caller) for o in oids])
+            return d
+        state = {"n": len(remaining)}
+
+        def one(oid):
+            if oid in remaining:
+                remaining.discard(oid)
+                state["n"] -= 1
+                if state["n"] == 0 and not d.done:
+                    d.resolve([self._desc_for(o, caller) for o in oids])
+
+        self._when_ready(list(remaining), one)
+        if timeout is not None and not d.done:
+            self._add_timer(timeout, lambda: d.resolve(exc.GetTimeoutError(
+                f"Get timed out: some object(s) not ready after {timeout}s."), ok=False))
+        self._maybe_block(caller, d)
+        return d
+
+    def _maybe_block(self, caller, d):
+        """A worker waiting in get/wait inside a normal task lends its CPU back (no deadlock when
+        tasks wait on tasks) and re-acquires it once the wait is over."""
+        if d.done or not caller.startswith("w:"):
+            return
+        w = self.workers.get(bytes.fromhex(caller[2:]))
+        if w is None or w.task is None:
+            return
+        self._on_blocked(w, True)
+        d.add(lambda _d, w=w: self._on_blocked(w, False))
+
+    def rpc_wait(self, caller, oids, num_returns, timeout=None, fetch_local=True):
+        d = Deferred()
+        ready = [o for o in oids if (self.objects.get(o) is None or self.objects[o].state != PENDING)]
+        if len(ready) >= num_returns or timeout == 0:
+            d.resolve(ready[:num_returns] if len(ready) > num_returns else ready)
+            return d
+        rs = set(ready)
+        order = list(ready)
+
+        def one(oid):
+            if d.done or oid in rs:
+                return
+            rs.add(oid)
+            order.append(oid)
+            if len(order) >= num_returns:
+                d.resolve(order[:num_returns])
+
+        self._when_ready([o for o in oids if o not in rs], one)
+        if timeout is not None and not d.done:
+            self._add_timer(timeout, lambda: d.resolve(list(order)))
+        self._maybe_block(caller, d)
+        return d
+
+    def rpc_object_ready(self, caller, oid):
+        e = self.objects.get(oid)
+        return e is None or e.state != PENDING
+
+    def rpc_free(self, caller, oids):
+        for oid in oids:
+            e = self.objects.get(oid)
+            if e is not None:
+                e.holders.clear()
+                e.pins = 0
+                if e.state == READY:
+                    self._free(e)
+
+    # ================================================================== functions
+    def rpc_register_function(self, caller, fid, blob):
+        self.functions.setdefault(fid, blob)
+        return True
+
+    # ================================================================== task submission
+    def rpc_submit(self, caller, spec):
+        self._submit(spec, caller)
+        return None
+
+    def _submit(self, spec, owner):
+        tid = spec["tid"]
+        if spec["kind"] == "actor_creation" and spec.get("actor_name"):
+            key = (spec.get("namespace", ""), spec["actor_name"])
+            old = self.named_actors.get(key)
+            if old is not None and self.actors.get(old) is not None and self.actors[old].state != A_DEAD:
+                raise ValueError(f"The name {spec['actor_name']} (namespace={key[0]}) is already taken.")
+        if spec.get("fblob") is not None:
+            self.functions.setdefault(spec["fid"], spec.pop("fblob"))
+        ts = TaskState(tid, spec, owner)
+        self.tasks[tid] = ts
+        parent = spec.get("parent")
+        if parent is not None and parent in self.tasks:
+            self.tasks[parent].children.append(tid)
+        for rid in spec["return_ids"]:
+            e = self._obj(rid, task=tid)
+            e.holders.add(owner)
+        if spec.get("generator") == "streaming":
+            pass
+        for c in spec.get("contained", ()):
+            self._pin(c)
+        deps = [a[1] for a in spec["args"] if a[0] == "r"]
+        for d in deps:
+            self._pin(d)
+        self._event(ts, "submit")
+        kind = spec["kind"]
+        if kind == "actor_creation":
+            self._create_actor(spec, owner, ts)
+        pending = {d for d in deps if (self.objects.get(d) is not None and self.objects[d].state == PENDING)}
+        ts.deps = pending
+        if kind == "actor_task":
+            a = self.actors.get(spec["actor_id"])
+            if a is None or a.state == A_DEAD:
+                self._fail_task(ts, exc.ActorDiedError(spec["actor_id"], self._actor_death_msg(a)))
+                return
+            a.queue.append(ts)
+            ts.state = T_QUEUED
+            if pending:
+                self._when_ready(list(pending), lambda oid, ts=ts, a=a: self._actor_dep_ready(a, ts, oid))
+            self._pump_actor(a)
+            return
+        if pending:
+            self._when_ready(list(pending), lambda oid, ts=ts: self._dep_ready(ts, oid))
+        else:
+            self._enqueue(ts)
+
+    def _dep_ready(self, ts, oid):
+        ts.deps.discard(oid)
+        if not ts.deps and ts.state == T_WAIT_DEPS and not ts.cancelled:
+            self._enqueue(ts)
+
+    def _actor_dep_ready(self, a, ts, oid):
+        ts.deps.discard(oid)
+        self._pump_actor(a)
+
+    def _demand_of(self, spec):
+        res = dict(spec.get("resources") or {})
+        strat = spec.get("strategy") or {}
+        if strat.get("kind") == "pg":
+            pgid = strat["pg_id"].hex()
+            idx = strat.get("bundle_index", -1)
+            out = {}
+            for k, v in res.items():
+                if v <= 0:
+                    continue
+                out[f"{k}_group_{idx}_{pgid}" if idx is not None and idx >= 0 else f"{k}_group_{pgid}"] = v
+            out[f"bundle_group_{idx}_{pgid}" if idx is not None and idx >= 0 else f"bundle_group_{pgid}"] = 0.001
+            return out
+        return {k: v for k, v in res.items() if v > 0}
+
+    def _enqueue(self, ts):
+        spec = ts.spec
+        ts.demand = self._demand_of(spec)
+        ts.state = T_QUEUED
+        self._key += 1
+        ts.key = self._key
+        self.task_keys[ts.key] = ts
+        strat = spec.get("strategy") or {}
+        kind = strat.get("kind")
+        code = 0
+        aff = ""
+        soft = False
+        if kind == "spread":
+            code = 1
+        elif kind == "node_affinity":
+            code = 2
+            aff = strat["node_id"]
+            soft = bool(strat.get("soft"))
+        preferred = spec.get("caller_node") or self.head_node_id
+        if not self.sched.is_feasible(ts.demand) and not (kind == "node_affinity" and soft):
+            if kind == "pg" and strat["pg_id"] in self.pgs and self.pgs[strat["pg_id"]]["state"] == "PENDING":
+                pass  # wait for the placement group to be placed
+            elif kind == "node_affinity" and not soft:
+                self._fail_task(ts, exc.TaskUnschedulableError(
+                    f"node {aff} is not alive or infeasible for {ts.demand}"))
+                return
+            else:
+                log.warning("task %s demands %s which no node can satisfy; it stays pending",
+                            spec.get("name"), ts.demand)
+        self.sched.enqueue(ts.key, ts.demand, code, preferred, aff, soft)
+        self._schedule()
+
+    def _schedule(self):
+        if self.shutting_down:
+            return
+        for key, node_id in self.sched.schedule(0):
+            ts = self.task_keys.pop(key, None)
+            if ts is None:
+                self.sched.release(node_id, {})
+                continue
+            if ts.cancelled:
+                self.sched.release(node_id, ts.demand)
+                continue
+            ts.node = node_id
+            node = self.nodes[node_id]
+            ts.gpus = self._assign_gpus(node, ts.demand, ts.spec)
+            ts.state = T_WAIT_WORKER
+            self._event(ts, "scheduled")
+            env_key = self._env_key(ts.spec.get("runtime_env") or {}, ts.gpus)
+            if ts.spec["kind"] == "actor_creation":
+                a = self.actors.get(ts.spec["actor_id"])
+                if a is None or a.state == A_DEAD:
+                    self.sched.release(node_id, ts.demand)
+                    self._release_gpus(node_id, ts.gpus, ts.demand)
+                    continue
+                a.node = node_id
+                a.demand = ts.demand
+                a.gpus = ts.gpus
+                # dedicated worker: reuse an idle CPU worker if the env matches, else spawn
+                w = self._pop_idle(node, env_key)
+                if w is None:
+                    node.dispatch_q[env_key].append(ts)
+                    self._start_worker(node, env_key, ts.gpus, ts.spec.get("runtime_env") or {})
+                else:
+                    self._dispatch(w, ts)
+                continue
+            w = self._pop_idle(node, env_key)
+            if w is not None:
+                self._dispatch(w, ts)
+            else:
+                node.dispatch_q[env_key].append(ts)
+                need = len(node.dispatch_q[env_key])
+                if node.starting[env_key] < need:
+                    self._start_worker(node, env_key, ts.gpus, ts.spec.get("runtime_env") or {})
+        self._try_place_pgs()
+
+    def _assign_gpus(self, node, demand, spec):
+        g = 0.0
+        for k, v in demand.items():
+            if k == "GPU" or (k.startswith("GPU_group_")):
+                g = max(g, v)
+        if g <= 0:
+            return ()
+        free = node.gpu_free
+        if g >= 1:
+            n = int(round(g))
+            ids = [i for i, c in enumerate(free) if c >= 0.9999][:n]
+            for i in ids:
+                free[i] = 0.0
+            return tuple(ids)
+        cands = sorted([i for i, c in enumerate(free) if c >= g - 1e-9], key=lambda i: free[i])
+        if not cands:
+            return ()
+        i = cands[0]
+        free[i] -= g
+        return (i,)
+
+    def _release_gpus(self, node_id, gpus, demand):
+        node = self.nodes.get(node_id)
+        if node is None or not gpus:
+            return
+        g = 0.0
+        for k, v in demand.items():
+            if k == "GPU" or k.startswith("GPU_group_"):
+                g = max(g, v)
+        per = 1.0 if g >= 1 else g
+        for i in gpus:
+            if i < len(node.gpu_free):
+                node.gpu_free[i] = min(1.0, node.gpu_free[i] + per)
+
+    def _env_key(self, runtime_env, gpus):
+        env = json.dumps(runtime_env, sort_keys=True, default=str) if runtime_env else ""
+        return (env, tuple(gpus))
+
+    def _pop_idle(self, node, env_key):
+        lst = node.idle.get(env_key)
+        while lst:
+            w = lst.pop()
+            if not w.dead:
+                return w
+        return None
+
+    # ================================================================== worker pool
+    def _start_worker(self, node, env_key, gpus, runtime_env=None):
+        wid = new_id()
+        env = dict(os.environ)
+        env["RCA_HEAD_SOCK"] = self.sock_path
+        env["RCA_WORKER_ID"] = wid.hex()
+        env["RCA_NODE_ID"] = node.node_id
+        env["RCA_STORE"] = self.store_name
+        env["RCA_SESSION_DIR"] = self.session_dir
+        env["RCA_JOB_ID"] = self.job_id.hex()
+        env["RCA_NAMESPACE"] = self.namespace
+        env["RCA_SYS_PATH"] = json.dumps([p for p in sys.path if p])
+        pkg_parent = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        pp = env.get("PYTHONPATH", "")
+        env["PYTHONPATH"] = pkg_parent + (os.pathsep + pp if pp else "")
+        env["RCA_GPU_IDS"] = ",".join(str(g) for g in gpus)
+        env.setdefault("PYTHONUNBUFFERED", "1")
+        if gpus:
+            vis = _parent_visible_devices()
+            phys = [vis[g] if vis and g < len(vis) else str(g) for g in gpus]
+            env["HIP_VISIBLE_DEVICES"] = ",".join(phys)
+            env.pop("CUDA_VISIBLE_DEVICES", None)
+        else:
+            if self.config.get("hide_gpus_from_cpu_workers", True):
+                env["HIP_VISIBLE_DEVICES"] = ""
+                env["ROCR_VISIBLE_DEVICES_RCA_HIDDEN"] = "1"
+        renv = runtime_env or {}
+        for k, v in (renv.get("env_vars") or {}).items():
+            env[str(k)] = str(v)
+        if renv.get("working_dir"):
+            env["RCA_WORKING_DIR"] = str(renv["working_dir"])
+        if renv.get("py_modules"):
+            env["RCA_PY_MODULES"] = json.dumps([str(p) for p in renv["py_modules"]])
+        out_path = os.path.join(self.logs_dir, f"worker-{wid.hex()}.out")
+        try:
+            logf = open(out_path, "ab")
+        except OSError:
+            logf = subprocess.DEVNULL
+        cmd = [sys.executable, "-u", "-m", "ray_community_amd._private.worker_main"]
+        proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                cwd=os.getcwd(), start_new_session=True)
+        if logf is not subprocess.DEVNULL:
+            logf.close()
+        w = WorkerState(wid, node.node_id, env_key, proc, gpus)
+        w.log_path = out_path
+        self.workers[wid] = w
+        node.starting[env_key] += 1
+        return w
+
+    def _worker_available(self, w: WorkerState):
+        if w.dead or w.actor is not None:
+            return
+        node = self.nodes.get(w.node_id)
+        if node is None or not node.alive:
+            self._kill_worker(w)
+            return
+        q = node.dispatch_q.get(w.env_key)
+        while q:
+            ts = q.popleft()
+            if ts.cancelled or ts.state != T_WAIT_WORKER:
+                continue
+            self._dispatch(w, ts)
+            return
+        w.state = "idle"
+        w.task = None
+        w.idle_since = time.time()
+        node.idle[w.env_key].append(w)
+
+    def _reap_idle(self):
+        now = time.time()
+        if getattr(self, "_last_reap", 0) > now - 0.5:
+            return
+        self._last_reap = now
+        with self.lock:
+            for w in list(self.workers.values()):
+                if w.state == "starting" and w.proc is not None and w.proc.poll() is not None:
+                    self.start_failures = getattr(self, "start_failures", 0) + 1
+                    reason = (f"worker failed to start (exit code {w.proc.returncode}); "
+                              f"see {getattr(w, 'log_path', '')}")
+                    if self.start_failures >= 5:
+                        self._fail_unstartable(w, reason)
+                    self._on_worker_death(w, reason)
+        keep = int(self.config.get("max_idle_workers", 16))
+        timeout = float(self.config.get("idle_worker_timeout_s", 60))
+        with self.lock:
+            for node in self.nodes.values():
+                n_idle = sum(len(v) for v in node.idle.values())
+                if n_idle <= keep:
+                    continue
+                for key, lst in node.idle.items():
+                    for w in list(lst):
+                        if n_idle <= keep:
+                            break
+                        if now - w.idle_since > timeout:
+                            lst.remove(w)
+                            self._kill_worker(w)
+                            n_idle -= 1
+
+    def _fail_unstartable(self, w, reason):
+        """Workers for this env keep crashing at startup: fail the work queued for them."""
+        node = self.nodes.get(w.node_id)
+        if node is None:
+            return
+        tail = ""
+        try:
+            with open(getattr(w, "log_path", ""), "rb") as f:
+                tail = f.read()[-2000:].decode(errors="replace")
+        except OSError:
+            pass
+        err = exc.RuntimeEnvSetupError(f"{reason}\n{tail}")
+        q = node.dispatch_q.get(w.env_key)
+        while q:
+            ts = q.popleft()
+            self._release_task_resources(ts)
+            if ts.spec["kind"] == "actor_creation":
+                a = self.actors.get(ts.spec["actor_id"])
+                if a is not None:
+                    a.death_cause = str(err)
+                    a.killed = True
+                    self._on_actor_worker_death(a, str(err), None)
+            self._fail_task(ts, err)
+        self.start_failures = 0
+
+    def _kill_worker(self, w: WorkerState):
+        if w.dead:
+            return
+        try:
+            if w.conn is not None:
+                w.conn.send((P.EXIT,))
+        except OSError:
+            pass
+        try:
+            if w.proc is not None:
+                w.proc.kill()
+        except Exception:
+            pass
+
+    # ================================================================== dispatch / completion
+    def _dispatch(self, w: WorkerState, ts: TaskState):
+        spec = ts.spec
+        ts.worker = w.wid
+        ts.state = T_RUNNING
+        ts.attempt += 1
+        ts.times["start"] = time.time()
+        w.state = "busy"
+        w.task = ts
+        args = []
+        for a in spec["args"]:
+            if a[0] == "r":
+                args.append(("d", a[1], self._desc_for(a[1], "w:" + w.wid.hex())))
+            else:
+                args.append(a)
+        msg = dict(spec)
+        msg["args"] = args
+        msg["gpu_ids"] = ts.gpus
+        msg["node_id"] = ts.node
+        fid = spec.get("fid")
+        if fid is not None and fid not in w.known_functions:
+            msg["fblob"] = self.functions.get(fid)
+            w.known_functions.add(fid)
+        if spec["kind"] == "actor_creation":
+            a = self.actors[spec["actor_id"]]
+            a.worker = w.wid
+            a.pid = w.pid
+            w.actor = a
+        self._event(ts, "running", worker=w)
+        self._send(w, (P.EXECUTE, msg))
+
+    def _on_task_done(self, w: WorkerState, tid, results, info):
+        ts = self.tasks.get(tid)
+        if w is not None and w.task is ts:
+            w.task = None
+        if ts is None:
+            return
+        if ts.blocked:
+            ts.blocked = False
+        spec = ts.spec
+        kind = spec["kind"]
+        failed = info.get("error", False)
+        retry_exc = info.get("retryable", False)
+        if failed and retry_exc and ts.retries_left != 0 and not ts.cancelled and kind == "task":
+            ts.retries_left -= 1
+            self._release_task_resources(ts)
+            self._event(ts, "retry")
+            if w is not None:
+                self._worker_available(w)
+            ts.state = T_WAIT_DEPS
+            self._enqueue(ts)
+            return
+        ts.state = T_FAILED if failed else T_FINISHED
+        ts.times["end"] = time.time()
+        ts.error_type = info.get("error_type")
+        self._event(ts, "failed" if failed else "finished", worker=w)
+        gpu_owner = ("w:" + w.wid.hex()) if w is not None else None
+        for rid, res in zip(spec["return_ids"], results):
+            e = self.objects.get(rid)
+            if e is None:
+                if res[0] == "shm":
+                    self.store.delete(rid)
+                continue
+            desc, contained, flags, is_gpu = res[0:3], res[3], res[4], res[5]
+            owner = w.wid if (is_gpu and w is not None) else None
+            if owner is not None:
+                w.gpu_objects.add(rid)
+            self._set_ready(e, tuple(desc), contained, owner, flags)
+        if kind == "task" and spec.get("generator") == "streaming":
+            ts.gen_done = True
+            self._flush_gen_waiters(ts)
+        self._finish_task_bookkeeping(ts)
+        if kind == "actor_creation":
+            a = self.actors.get(spec["actor_id"])
+            if a is None:
+                return
+            if failed:
+                a.death_cause = info.get("error_msg", "actor constructor failed")
+                self._kill_actor(a, no_restart=True, reason=a.death_cause, init_failed=True)
+            else:
+                a.state = A_ALIVE
+                for d in a.ready_waiters:
+                    d.resolve(True)
+                a.ready_waiters = []
+                self._pump_actor(a)
+            return
+        if kind == "actor_task":
+            a = self.actors.get(spec["actor_id"])
+            if a is not None:
+                a.inflight.pop(tid, None)
+                if info.get("actor_exit"):
+                    self._kill_actor(a, no_restart=True, reason="exit_actor() called", graceful=True)
+            return
+        self._release_task_resources(ts)
+        if w is not None:
+            self._worker_available(w)
+        self._schedule()
+
+    def _finish_task_bookkeeping(self, ts):
+        spec = ts.spec
+        for a in spec["args"]:
+            if a[0] == "r":
+                self._unpin(a[1])
+        for c in spec.get("contained", ()):
+            self._unpin(c)
+        self.finished_tasks.append(ts.tid)
+        while len(self.finished_tasks) > 9000:
+            old = self.finished_tasks.popleft()
+            self.tasks.pop(old, None)
+
+    def _release_task_resources(self, ts):
+        if ts.node is not None and ts.demand is not None:
+            if not ts.blocked:
+                self.sched.release(ts.node, ts.demand)
+            else:
+                rest = {k: v for k, v in ts.demand.items() if k != "CPU" and not k.startswith("CPU_group")}
+                self.sched.release(ts.node, rest)
+            self._release_gpus(ts.node, ts.gpus, ts.demand)
+            ts.demand = {}
+            ts.gpus = ()
+
+    def _fail_task(self, ts, err):
+        ts.state = T_FAILED
+        ts.times["end"] = time.time()
+        ts.error_type = type(err).__name__
+        for rid in ts.spec["return_ids"]:
+            e = self.objects.get(rid)
+            if e is not None and e.state == PENDING:
+                self._set_error(e, err)
+        if ts.spec.get("generator") == "streaming":
+            ts.gen_done = True
+            self._flush_gen_waiters(ts)
+        self._event(ts, "failed")
+        self._finish_task_bookkeeping(ts)
+
+    def _on_blocked(self, w, flag):
+        if w is None or w.task is None:
+            return
+        ts = w.task
+        if ts.spec["kind"] != "task" or ts.node is None:
+            return
+        cpu = {k: v for k, v in ts.demand.items() if k == "CPU" or k.startswith("CPU_group")}
+        if not cpu:
+            return
+        if flag and not ts.blocked:
+            ts.blocked = True
+            self.sched.release(ts.node, cpu)
+            self._schedule()
+        elif not flag and ts.blocked:
+            ts.blocked = False
+            self.sched.acquire(ts.node, cpu, True)
+
+    def _on_worker_death(self, w: WorkerState, reason):
+        if w.dead:
+            return
+        w.dead = True
+        node = self.nodes.get(w.node_id)
+        if w.state == "starting" and node is not None:
+            node.starting[w.env_key] = max(0, node.starting[w.env_key] - 1)
+        if node is not None:
+            lst = node.idle.get(w.env_key)
+            if lst and w in lst:
+                lst.remove(w)
+        self.workers.pop(w.wid, None)
+        # GPU objects owned by the worker are lost
+        for oid in list(w.gpu_objects):
+            e = self.objects.get(oid)
+            if e is not None and e.state == READY:
+                e.gpu_owner = None
+                e.desc = ("inline", serialize(exc.OwnerDiedError(oid.hex()), error=True).to_bytes(), 0)
+                e.flags = FLAG_ERROR
+        ts = w.task
+        w.task = None
+        if w.actor is not None:
+            a = w.actor
+            self._on_actor_worker_death(a, reason, ts)
+        elif ts is not None and ts.state == T_RUNNING:
+            self._release_task_resources(ts)
+            if ts.cancelled:
+                self._fail_task(ts, exc.TaskCancelledError(ts.tid.hex()))
+            elif ts.retries_left != 0:
+                ts.retries_left -= 1
+                self._event(ts, "retry")
+                ts.state = T_WAIT_DEPS
+                self._enqueue(ts)
+            else:
+                self._fail_task(ts, exc.WorkerCrashedError(
+                    f"The worker died unexpectedly while executing task {ts.spec.get('name')} ({reason})."))
+        self._schedule()
+        # keep the pool warm for queued work
+        if node is not None and node.alive:
+            for key, q in node.dispatch_q.items():
+                if q and node.starting[key] < len(q):
+                    self._start_worker(node, key, q[0].gpus, q[0].spec.get("runtime_env") or {})
+
+    # ================================================================== streaming generators
+    def _on_gen_item(self, tid, index, res):
+        ts = self.tasks.get(tid)
+        oid = res[6]
+        e = self._obj(oid, task=tid)
+        if ts is not None:
+            e.holders.add(ts.owner)
+            while len(ts.gen_items) <= index:
+                ts.gen_items.append(None)
+            ts.gen_items[index] = oid
+        desc, contained, flags = res[0:3], res[3], res[4]
+        self._set_ready(e, tuple(desc), contained, None, flags)
+        if ts is not None:
+            self._flush_gen_waiters(ts)
+
+    def _flush_gen_waiters(self, ts):
+        for idx in list(ts.gen_waiters):
+            if idx < len(ts.gen_items) and ts.gen_items[idx] is not None:
+                for d in ts.gen_waiters.pop(idx):
+                    d.resolve(ts.gen_items[idx])
+            elif ts.gen_done:
+                for d in ts.gen_waiters.pop(idx):
+                    d.resolve(None)
+
+    def rpc_gen_next(self, caller, tid, index, timeout=None):
+        ts = self.tasks.get(tid)
+        d = Deferred()
+        if ts is None:
+            d.resolve(None)
+            return d
+        if index < len(ts.gen_items) and ts.gen_items[index] is not None:
+            oid = ts.gen_items[index]
+            e = self.objects.get(oid)
+            if e is not None:
+                e.holders.add(caller)
+            d.resolve(oid)
+            return d
+        if ts.gen_done:
+            # error of the generator task is surfaced through its return object
+            d.resolve(None)
+            return d
+        ts.gen_waiters.setdefault(index, []).append(d)
+        if timeout is not None:
+            self._add_timer(timeout, lambda: d.resolve(exc.GetTimeoutError("generator next timed out"), ok=False))
+        return d
+
+    # ================================================================== actors
+    def _create_actor(self, spec, owner, ts):
+        aid = spec["actor_id"]
+        a = ActorState(aid, spec, owner)
+        a.creation_task = ts
+        self._actor_handles(a).add(owner)
+        self.actors[aid] = a
+        if a.name:
+            key = (a.namespace, a.name)
+            if key in self.named_actors and self.actors.get(self.named_actors[key]) is not None and \
+                    self.actors[self.named_actors[key]].state != A_DEAD:
+                raise ValueError(f"The name {a.name} (namespace={a.namespace}) is already taken.")
+            self.named_actors[key] = aid
+
+    def rpc_actor_name_available(self, caller, name, namespace):
+        aid = self.named_actors.get((namespace, name))
+        return aid is None or self.actors.get(aid) is None or self.actors[aid].state == A_DEAD
+
+    def _pump_actor(self, a: ActorState):
+        if a.state != A_ALIVE:
+            return
+        w = self.workers.get(a.worker)
+        if w is None or w.dead:
+            return
+        while a.queue:
+            ts = a.queue[0]
+            if ts.cancelled:
+                a.queue.popleft()
+                continue
+            if ts.deps:
+                # keep submission order: later calls wait behind an unresolved earlier call
+                return
+            a.queue.popleft()
+            a.inflight[ts.tid] = ts
+            ts.node = a.node
+            self._dispatch_actor_task(w, ts)
+
+    def _dispatch_actor_task(self, w, ts):
+        spec = ts.spec
+        ts.worker = w.wid
+        ts.state = T_RUNNING
+        ts.times["start"] = time.time()
+        args = []
+        for x in spec["args"]:
+            if x[0] == "r":
+                args.append(("d", x[1], self._desc_for(x[1], "w:" + w.wid.hex())))
+            else:
+                args.append(x)
+        msg = dict(spec)
+        msg["args"] = args
+        self._event(ts, "running", worker=w)
+        self._send(w, (P.EXECUTE, msg))
+
+    def _on_actor_worker_death(self, a: ActorState, reason, running_ts):
+        if a.state == A_DEAD:
+            return
+        inflight = list(a.inflight.values())
+        a.inflight.clear()
+        if a.node is not None and not getattr(a, "_res_released", False):
+            self.sched.release(a.node, a.demand)
+            self._release_gpus(a.node, a.gpus, a.demand)
+        a.worker = None
+        can_restart = (not a.killed) and (a.restarts_left != 0)
+        if running_ts is not None and running_ts.spec["kind"] == "actor_creation" and running_ts.state == T_RUNNING:
+            can_restart = can_restart and True
+        if can_restart:
+            if a.restarts_left > 0:
+                a.restarts_left -= 1
+            a.num_restarts += 1
+            a.state = A_RESTARTING
+            self._event_actor(a, "restarting")
+            # in-flight calls: retry if allowed, else fail
+            retry = []
+            for ts in inflight:
+                mtr = ts.spec.get("max_task_retries", 0)
+                if mtr != 0:
+                    ts.spec["max_task_retries"] = mtr - 1 if mtr > 0 else mtr
+                    ts.state = T_QUEUED
+                    retry.append(ts)
+                else:
+                    self._fail_task(ts, exc.ActorDiedError(a.aid, f"The actor died: {reason}"))
+            for ts in reversed(retry):
+                a.queue.appendleft(ts)
+            cts = a.creation_task
+            cts.state = T_WAIT_DEPS
+            cts.retries_left = 0
+            # the creation task's args are still pinned (never finished bookkeeping twice)
+            self._enqueue(cts)
+        else:
+            a.state = A_DEAD
+            a.death_cause = a.death_cause or reason
+            self._event_actor(a, "dead")
+            err = exc.ActorDiedError(a.aid, self._actor_death_msg(a))
+            for ts in inflight:
+                self._fail_task(ts, err)
+            while a.queue:
+                self._fail_task(a.queue.popleft(), err)
+            cts = a.creation_task
+            if cts is not None and cts.state in (T_RUNNING, T_WAIT_WORKER, T_QUEUED, T_WAIT_DEPS):
+                self._fail_task(cts, exc.ActorDiedError(a.aid, self._actor_death_msg(a), actor_init_failed=True))
+            for d in a.ready_waiters:
+                d.resolve(exc.ActorDiedError(a.aid, self._actor_death_msg(a)), ok=False)
+            a.ready_waiters = []
+
+    def _actor_death_msg(self, a):
+        if a is None:
+            return "The actor is dead (unknown actor)."
+        return f"The actor {a.spec.get('class_name', '')} ({a.aid.hex()}) died: {a.death_cause or 'unknown cause'}"
+
+    def _kill_actor(self, a: ActorState, no_restart=True, reason="ray.kill() called", init_failed=False,
+                    graceful=False):
+        if a.state == A_DEAD:
+            return
+        if no_restart:
+            a.killed = True
+            a.restarts_left = 0
+        a.death_cause = reason
+        w = self.workers.get(a.worker) if a.worker else None
+        if w is not None and not w.dead:
+            if graceful:
+                self._send(w, (P.EXIT,))
+            else:
+                self._kill_worker(w)
+            # death is finalised when the connection drops
+            if no_restart:
+                # pending (not yet dispatched) calls fail right away
+                err = exc.ActorDiedError(a.aid, self._actor_death_msg(a), actor_init_failed=init_failed)
+                while a.queue:
+                    self._fail_task(a.queue.popleft(), err)
+        else:
+            cts = a.creation_task
+            if cts is not None and cts.key is not None and cts.key in self.task_keys:
+                self.sched.cancel(cts.key)
+                self.task_keys.pop(cts.key, None)
+            if cts is not None:
+                for node in self.nodes.values():
+                    for q in node.dispatch_q.values():
+                        if cts in q:
+                            q.remove(cts)
+                            if cts.node:
+                                self.sched.release(cts.node, cts.demand)
+                                self._release_gpus(cts.node, cts.gpus, cts.demand)
+                            a._res_released = True
+            self._on_actor_worker_death(a, reason, None)
+
+    def rpc_kill_actor(self, caller, aid, no_restart=True):
+        a = self.actors.get(aid)
+        if a is None:
+            raise ValueError("unknown actor")
+        self._kill_actor(a, no_restart=no_restart)
+        return True
+
+    def rpc_get_actor(self, caller, name, namespace):
+        aid = self.named_actors.get((namespace, name))
+        a = self.actors.get(aid) if aid else None
+        if a is None or a.state == A_DEAD:
+            return None
+        self._actor_handles(a).add(caller)
+        return {"actor_id": a.aid, "meta": a.spec.get("class_meta")}
+
+    def rpc_actor_ready(self, caller, aid):
+        a = self.actors.get(aid)
+        d = Deferred()
+        if a is None:
+            d.resolve(exc.ActorDiedError(aid, "unknown actor"), ok=False)
+        elif a.state == A_ALIVE:
+            d.resolve(True)
+        elif a.state == A_DEAD:
+            d.resolve(exc.ActorDiedError(aid, self._actor_death_msg(a)), ok=False)
+        else:
+            a.ready_waiters.append(d)
+        return d
+
+    def rpc_actor_info(self, caller, aid):
+        a = self.actors.get(aid)
+        if a is None:
+            return None
+        return {"state": a.state, "num_restarts": a.num_restarts, "node_id": a.node, "pid": a.pid,
+                "name": a.name, "death_cause": a.death_cause}
+
+    # ================================================================== cancel
+    def rpc_cancel(self, caller, oid, force=False, recursive=True):
+        e = self.objects.get(oid)
+        tid = e.task if e is not None else None
+        ts = self.tasks.get(tid) if tid else None
+        if ts is None:
+            return False
+        self._cancel_task(ts, force, recursive)
+        return True
+
+    def _cancel_task(self, ts, force, recursive):
+        if ts.state in (T_FINISHED, T_FAILED, T_CANCELLED):
+            return
+        ts.cancelled = True
+        if recursive:
+            for c in ts.children:
+                cts = self.tasks.get(c)
+                if cts is not None:
+                    self._cancel_task(cts, force, recursive)
+        kind = ts.spec["kind"]
+        if ts.state in (T_WAIT_DEPS, T_QUEUED, T_WAIT_WORKER):
+            if ts.key is not None and self.sched.cancel(ts.key):
+                self.task_keys.pop(ts.key, None)
+            if ts.state == T_WAIT_WORKER and ts.node:
+                self.sched.release(ts.node, ts.demand)
+                self._release_gpus(ts.node, ts.gpus, ts.demand)
+            if kind == "actor_task":
+                a = self.actors.get(ts.spec["actor_id"])
+                if a is not None and ts in a.queue:
+                    a.queue.remove(ts)
+            self._fail_task(ts, exc.TaskCancelledError(ts.tid.hex()))
+            ts.state = T_CANCELLED
+            self._schedule()
+            return
+        if ts.state == T_RUNNING:
+            w = self.workers.get(ts.worker)
+            if kind == "actor_task":
+                if w is not None:
+                    self._send(w, (P.CANCEL, ts.tid, False))
+                return
+            if w is not None:
+                if force:
+                    self._kill_worker(w)
+                else:
+                    self._send(w, (P.CANCEL, ts.tid, False))
+
+    # ================================================================== placement groups
+    def rpc_create_pg(self, caller, pg_id, bundles, strategy, name="", lifetime=None):
+        pg = {"pg_id": pg_id, "bundles": bundles, "strategy": strategy, "name": name, "state": "PENDING",
+              "nodes": None, "waiters": [], "created": time.time(), "lifetime": lifetime}
+        self.pgs[pg_id] = pg
+        for b in bundles:
+            if not self.sched.is_feasible({k: v for k, v in b.items() if v > 0}):
+                pg["infeasible"] = True
+        self.pending_pgs.append(pg_id)
+        self._try_place_pgs()
+        return True
+
+    def _try_place_pgs(self):
+        if not self.pending_pgs:
+            return
+        still = []
+        placed_any = False
+        for pg_id in self.pending_pgs:
+            pg = self.pgs.get(pg_id)
+            if pg is None or pg["state"] != "PENDING":
+                continue
+            bundles = [{k: float(v) for k, v in b.items() if v > 0} for b in pg["bundles"]]
+            nodes = self.sched.create_pg(pg_id.hex(), bundles, pg["strategy"])
+            if nodes is None:
+                still.append(pg_id)
+                continue
+            pg["nodes"] = list(nodes)
+            pg["state"] = "CREATED"
+            # per-bundle GPU bookkeeping happens at task grant time (node.gpu_free)
+            for d in pg["waiters"]:
+                d.resolve(True)
+            pg["waiters"] = []
+            placed_any = True
+        self.pending_pgs = still
+        if placed_any:
+            self._schedule()
+
+    def rpc_pg_ready(self, caller, pg_id, timeout=None):
+        pg = self.pgs.get(pg_id)
+        d = Deferred()
+        if pg is None or pg["state"] == "REMOVED":
+            d.resolve(ValueError("placement group removed"), ok=False)
+        elif pg["state"] == "CREATED":
+            d.resolve(True)
+        else:
+            pg["waiters"].append(d)
+            if timeout is not None:
+                self._add_timer(timeout, lambda: d.resolve(False))
+        return d
+
+    def rpc_remove_pg(self, caller, pg_id):
+        pg = self.pgs.get(pg_id)
+        if pg is None:
+            return False
+        if pg_id in self.pending_pgs:
+            self.pending_pgs.remove(pg_id)
+        # kill actors placed in the group
+        for a in list(self.actors.values()):
+            st = a.spec.get("strategy") or {}
+            if st.get("kind") == "pg" and st.get("pg_id") == pg_id and a.state != A_DEAD:
+                self._kill_actor(a, no_restart=True, reason="placement group removed")
+        if pg["state"] == "CREATED":
+            self.sched.remove_pg(pg_id.hex())
+        pg["state"] = "REMOVED"
+        for d in pg["waiters"]:
+            d.resolve(False)
+        pg["waiters"] = []
+        self._schedule()
+        return True
+
+    def rpc_pg_table(self, caller, pg_id=None):
+        def info(pg):
+            return {"placement_group_id": pg["pg_id"].hex(), "name": pg["name"], "strategy": pg["strategy"],
+                    "state": pg["state"], "bundles": {i: dict(b) for i, b in enumerate(pg["bundles"])},
+                    "bundles_to_node_id": {i: n for i, n in enumerate(pg["nodes"] or [])}}
+
+        if pg_id is not None:
+            pg = self.pgs.get(pg_id)
+            return info(pg) if pg else {}
+        return {pg["pg_id"].hex(): info(pg) for pg in self.pgs.values()}
+
+    def rpc_get_named_pg(self, caller, name):
+        for pg in self.pgs.values():
+            if pg["name"] == name and pg["state"] != "REMOVED":
+                return {"pg_id": pg["pg_id"], "bundles": pg["bundles"], "strategy": pg["strategy"]}
+        return None
+
+    # ================================================================== cluster info
+    def rpc_cluster_resources(self, caller):
+        tot = collections.Counter()
+        for nid, res in self.sched.totals().items():
+            for k, v in res.items():
+                if "_group_" in k:
+                    continue
+                tot[k] += v
+        return dict(tot)
+
+    def rpc_available_resources(self, caller):
+        tot = collections.Counter()
+        for nid, res in self.sched.available().items():
+            for k, v in res.items():
+                if "_group_" in k:
+                    continue
+                if v > 0:
+                    tot[k] += v
+        return dict(tot)
+
+    def rpc_nodes(self, caller):
+        totals = self.sched.totals()
+        out = []
+        for nid, n in self.nodes.items():
+            out.append({"NodeID": nid, "Alive": n.alive, "NodeManagerAddress": "127.0.0.1",
+                        "NodeManagerHostname": socket.gethostname(),
+                        "Resources": {k: v for k, v in totals.get(nid, n.resources).items() if "_group_" not in k},
+                        "Labels": n.labels, "alive": n.alive, "IsHead": n.is_head,
+                        "ObjectStoreSocketName": self.store_name})
+        return out
+
+    # ================================================================== KV
+    def rpc_kv_put(self, caller, key, value, overwrite=True, namespace=None):
+        k = (namespace, key)
+        if not overwrite and k in self.kv:
+            return False
+        existed = k in self.kv
+        self.kv[k] = value
+        return not existed
+
+    def rpc_kv_get(self, caller, key, namespace=None):
+        return self.kv.get((namespace, key))
+
+    def rpc_kv_del(self, caller, key, namespace=None, del_by_prefix=False):
+        if del_by_prefix:
+            ks = [k for k in self.kv if k[0] == namespace and k[1].startswith(key)]
+            for k in ks:
+                del self.kv[k]
+            return len(ks)
+        return 1 if self.kv.pop((namespace, key), None) is not None else 0
+
+    def rpc_kv_keys(self, caller, prefix, namespace=None):
+        return [k[1] for k in self.kv if k[0] == namespace and k[1].startswith(prefix)]
+
+    def rpc_kv_exists(self, caller, key, namespace=None):
+        return (namespace, key) in self.kv
+
+    # ================================================================== state / observability
+    def _event(self, ts, what, worker=None):
+        self.events.append((time.time(), ts.tid, what, ts.spec.get("name"), worker.pid if worker else None,
+                            ts.node))
+
+    def _event_actor(self, a, what):
+        self.events.append((time.time(), a.aid, "actor_" + what, a.spec.get("class_name"), a.pid, a.node))
+
+    def rpc_list_tasks(self, caller, limit=10000):
+        out = []
+        for ts in list(self.tasks.values())[-limit:]:
+            out.append({"task_id": ts.tid.hex(), "name": ts.spec.get("name"), "state": TASK_STATE_NAMES[ts.state],
+                        "type": {"task": "NORMAL_TASK", "actor_task": "ACTOR_TASK",
+                                 "actor_creation": "ACTOR_CREATION_TASK"}[ts.spec["kind"]],
+                        "node_id": ts.node, "worker_id": ts.worker.hex() if ts.worker else None,
+                        "actor_id": ts.spec.get("actor_id").hex() if ts.spec.get("actor_id") else None,
+                        "required_resources": ts.spec.get("resources"), "error_type": ts.error_type,
+                        "attempt_number": max(0, ts.attempt - 1),
+                        "start_time_ms": int(ts.times.get("start", 0) * 1000),
+                        "end_time_ms": int(ts.times.get("end", 0) * 1000),
+                        "func_or_class_name": ts.spec.get("name")})
+        return out
+
+    def rpc_list_actors(self, caller):
+        out = []
+        for a in self.actors.values():
+            out.append({"actor_id": a.aid.hex(), "class_name": a.spec.get("class_name"), "state": a.state,
+                        "name": a.name or "", "namespace": a.namespace, "pid": a.pid, "node_id": a.node,
+                        "num_restarts": a.num_restarts, "death_cause": a.death_cause,
+                        "is_detached": a.detached, "required_resources": a.spec.get("resources")})
+        return out
+
+    def rpc_list_objects(self, caller):
+        out = []
+        for e in self.objects.values():
+            out.append({"object_id": e.oid.hex(), "object_size": e.size,
+                        "task_status": "FINISHED" if e.state == READY else "PENDING",
+                        "reference_type": "LOCAL_REFERENCE" if e.holders else "PINNED_IN_MEMORY",
+                        "num_holders": len(e.holders), "pins": e.pins,
+                        "storage": e.desc[0] if e.desc else None, "gpu": e.gpu_owner is not None})
+        return out
+
+    def rpc_list_workers(self, caller):
+        return [{"worker_id": w.wid.hex(), "pid": w.pid, "node_id": w.node_id, "state": w.state,
+                 "is_actor": w.actor is not None, "gpu_ids": list(w.gpus)} for w in self.workers.values()]
+
+    def rpc_store_stats(self, caller):
+        s = dict(self.store.stats())
+        s.update({"spilled_bytes": self.spilled_bytes, "num_spilled": self.num_spilled,
+                  "num_restored": self.num_restored, "num_tracked_objects": len(self.objects)})
+        return s
+
+    def rpc_timeline(self, caller):
+        evs = []
+        open_ = {}
+        for t, tid, what, name, pid, node in self.events:
+            if what == "running":
+                open_[tid] = (t, name, pid, node)
+            elif what in ("finished", "failed") and tid in open_:
+                st, nm, p, nd = open_.pop(tid)
+                evs.append({"name": nm or "task", "cat": "task", "ph": "X", "ts": st * 1e6, "dur": (t - st) * 1e6,
+                            "pid": nd or "node", "tid": p or 0, "args": {"task_id": tid.hex(), "state": what}})
+        return evs
+
+    def rpc_ping(self, caller):
+        return "pong"
+
+    # ================================================================== timers
+    def _add_timer(self, delay, fn):
+        self.timers.append((time.time() + delay, fn))
+        self.wake()
+
+    def _fire_timers(self):
+        now = time.time()
+        with self.lock:
+            due = [t for t in self.timers if t[0] <= now]
+            if not due:
+                return
+            self.timers = [t for t in self.timers if t[0] > now]
+            for _, fn in due:
+                try:
+                    fn()
+                except Exception:
+                    log.error("timer failed\n%s", traceback.format_exc())
+
+    # ================================================================== shutdown
+    def shutdown(self):
+        with self.lock:
+            if self.shutting_down:
+                return
+            self.shutting_down = True
+            for w in list(self.workers.values()):
+                try:
+                    if w.conn is not None:
+                        w.conn.send((P.EXIT,))
+                except OSError:
+                    pass
+        deadline = time.time() + 2.0
+        for w in list(self.workers.values()):
+            if w.proc is None:
+                continue
+            try:
+                w.proc.wait(timeout=max(0.05, deadline - time.time()))
+            except Exception:
+                try:
+                    os.killpg(w.proc.pid, 9)
+                except Exception:
+                    try:
+                        w.proc.kill()
+                    except Exception:
+                        pass
+        for w in list(self.workers.values()):
+            if w.proc is not None:
+                try:
+                    w.proc.wait(timeout=1)
+                except Exception:
+                    pass
+        self._thread.join(timeout=2)
+        try:
+            self.sel.close()
+        except Exception:
+            pass
+        try:
+            self.listener.close()
+            os.unlink(self.sock_path)
+        except OSError:
+            pass
+        self.store.unlink()
+        if self.config.get("cleanup_session_dir", True):
+            shutil.rmtree(self.spill_dir, ignore_errors=True)
+
+
+class ClientConn:
+    """Head-side view of one socket (a worker or an external driver)."""
+
+    def __init__(self, sock):
+        self.conn = P.Connection(sock)
+        self.reader = P.FrameReader()
+        self.worker: Optional[WorkerState] = None
+        self.client_key: Optional[str] = None
+
+    def key(self):
+        if self.worker is not None:
+            return "w:" + self.worker.wid.hex()
+        return self.client_key or "anon"
+
+    def send(self, msg):
+        self.conn.send(msg)
+
+
+def _parent_visible_devices():
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            return [x.strip() for x in v.split(",") if x.strip()]
+    return None

@@ -1,0 +1,311 @@
+"""Public core API implementation (reference: ``python/ray/_private/worker.py``)."""
+from __future__ import annotations
+
+import atexit
+import glob
+import json
+import logging
+import os
+import threading
+import time
+from typing import Any, List, Optional, Sequence
+
+from .. import exceptions as exc
+from . import core_worker as cw
+from .core_worker import CoreWorker, DirectClient, ObjectRef, SocketClient
+
+log = logging.getLogger("ray_community_amd")
+
+SCRIPT_MODE = 0
+WORKER_MODE = 1
+LOCAL_MODE = 2
+
+_state = {"head": None, "core": None, "mode": None, "namespace": "", "runtime_env": None, "init_lock": threading.RLock()}
+
+
+def _attach_worker_core(core):
+    _state["core"] = core
+    _state["mode"] = WORKER_MODE
+    _state["namespace"] = core.namespace
+
+
+def is_initialized() -> bool:
+    return _state["core"] is not None
+
+
+def _core() -> CoreWorker:
+    c = _state["core"]
+    if c is None:
+        init()
+        c = _state["core"]
+    return c
+
+
+def _detect_gpus() -> int:
+    v = os.environ.get("HIP_VISIBLE_DEVICES")
+    if v is None:
+        v = os.environ.get("CUDA_VISIBLE_DEVICES")
+    if v is not None:
+        return len([x for x in v.split(",") if x.strip() != ""])
+    n = 0
+    for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(p) as f:
+                txt = f.read()
+            for line in txt.splitlines():
+                if line.startswith("simd_count"):
+                    if int(line.split()[1]) > 0:
+                        n += 1
+                    break
+        except OSError:
+            pass
+    return n
+
+
+def _detect_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count() or 1
+
+
+def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_gpus: Optional[int] = None,
+         resources: Optional[dict] = None, labels: Optional[dict] = None, object_store_memory: Optional[int] = None,
+         local_mode: bool = False, ignore_reinit_error: bool = False, include_dashboard=None, dashboard_host=None,
+         dashboard_port=None, job_config=None, configure_logging=True, logging_level=logging.INFO,
+         logging_format=None, log_to_driver=True, namespace: Optional[str] = None, runtime_env=None,
+         _system_config: Optional[dict] = None, _temp_dir: Optional[str] = None, **kwargs):
+    """Start (or connect to) a session. Returns a context dict-like with ``address_info``."""
+    with _state["init_lock"]:
+        if _state["core"] is not None:
+            if ignore_reinit_error:
+                return RayContext(_state)
+            raise RuntimeError("Maybe you called init() twice by accident? Use ignore_reinit_error=True.")
+        if address is None:
+            address = os.environ.get("RAY_ADDRESS") or os.environ.get("RCA_ADDRESS")
+        if address in ("local", None):
+            address = None
+        ns = namespace if namespace is not None else ("" if address else "anon_" + os.urandom(4).hex())
+        if address is not None:
+            sock = _resolve_address(address)
+            ident = os.urandom(20)
+            client = SocketClient(sock, "client", ident)
+            hello = client.hello
+            from .object_store import ObjectStore
+
+            store = ObjectStore(hello["store"])
+            core = CoreWorker("client", client, store, hello["node_id"], hello["job_id"], ns,
+                              session_dir=hello["session_dir"])
+            _state.update(head=None, core=core, mode=SCRIPT_MODE, namespace=ns, address=sock)
+        else:
+            from .head import Head
+
+            res = dict(resources or {})
+            res["CPU"] = float(num_cpus if num_cpus is not None else _detect_cpus())
+            ng = num_gpus if num_gpus is not None else _detect_gpus()
+            if ng:
+                res["GPU"] = float(ng)
+                res.setdefault("accelerator_type:MI355X", 1.0)
+            res.setdefault("memory", float(_mem_bytes() * 0.7))
+            root = _temp_dir or os.environ.get("RCA_TEMP_DIR") or "/tmp/rca"
+            session = os.path.join(root, f"session_{time.strftime('%Y%m%d-%H%M%S')}_{os.getpid()}_{os.urandom(2).hex()}")
+            sysconf = dict(_system_config or {})
+            head = Head(session, res, object_store_memory=object_store_memory, namespace=ns, system_config=sysconf,
+                        labels=labels)
+            res["object_store_memory"] = float(head.store_capacity)
+            client = DirectClient(head)
+            core = CoreWorker("driver", client, head.store, head.head_node_id, head.job_id, ns,
+                              session_dir=session)
+            head.driver_free_gpu_cb = core.free_gpu_objects
+            _state.update(head=head, core=core, mode=SCRIPT_MODE, namespace=ns, address=head.sock_path)
+            try:
+                os.makedirs(root, exist_ok=True)
+                with open(os.path.join(root, "latest_session.json"), "w") as f:
+                    json.dump({"sock": head.sock_path, "pid": os.getpid(), "session": session}, f)
+            except OSError:
+                pass
+        _state["runtime_env"] = runtime_env
+        cw.set_global_core(core)
+        return RayContext(_state)
+
+
+def _mem_bytes():
+    try:
+        import psutil
+
+        return psutil.virtual_memory().total
+    except Exception:
+        return 16 << 30
+
+
+def _resolve_address(address: str) -> str:
+    if address == "auto":
+        root = os.environ.get("RCA_TEMP_DIR", "/tmp/rca")
+        path = os.path.join(root, "latest_session.json")
+        with open(path) as f:
+            return json.load(f)["sock"]
+    if address.startswith("unix://"):
+        return address[len("unix://"):]
+    if os.path.exists(address):
+        return address
+    raise ConnectionError(f"cannot resolve address {address!r}")
+
+
+class RayContext(dict):
+    def __init__(self, st):
+        super().__init__(address=st.get("address"), node_id=st["core"].node_id if st["core"] else None,
+                         namespace=st.get("namespace"))
+        self.address_info = dict(self)
+        self.dashboard_url = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        shutdown()
+
+    def disconnect(self):
+        shutdown()
+
+
+def shutdown(_exiting_interpreter: bool = False):
+    with _state["init_lock"]:
+        core = _state["core"]
+        head = _state["head"]
+        if core is None:
+            return
+        if _state["mode"] == WORKER_MODE:
+            return
+        core.shutdown()
+        cw.set_global_core(None)
+        _state.update(core=None, head=None, mode=None)
+        if head is not None:
+            head.shutdown()
+        else:
+            try:
+                core.client.close()
+            except Exception:
+                pass
+        _run_shutdown_hooks()
+
+
+_shutdown_hooks = []
+
+
+def _register_shutdown_hook(fn):
+    _shutdown_hooks.append(fn)
+
+
+def _run_shutdown_hooks():
+    for fn in list(_shutdown_hooks):
+        try:
+            fn()
+        except Exception:
+            pass
+
+
+atexit.register(lambda: shutdown(True))
+
+
+# ---------------------------------------------------------------------------------- objects
+def put(value, *, _owner=None) -> ObjectRef:
+    return _core().put(value)
+
+
+def get(object_refs, *, timeout: Optional[float] = None):
+    core = _core()
+    from .core_worker import ObjectRefGenerator
+
+    if isinstance(object_refs, ObjectRefGenerator):
+        object_refs = list(object_refs)
+    if isinstance(object_refs, (list, tuple)):
+        refs = list(object_refs)
+        if not refs:
+            return []
+        for r in refs:
+            if not isinstance(r, ObjectRef):
+                raise ValueError(f"'object_refs' must either be an ObjectRef or a list of ObjectRefs; got {type(r)}")
+        return core.get(refs, timeout=timeout)
+    if not isinstance(object_refs, ObjectRef):
+        raise ValueError(f"'object_refs' must either be an ObjectRef or a list of ObjectRefs; got {type(object_refs)}")
+    return core.get(object_refs, timeout=timeout)
+
+
+def wait(object_refs, *, num_returns: int = 1, timeout: Optional[float] = None, fetch_local: bool = True):
+    return _core().wait(object_refs, num_returns=num_returns, timeout=timeout, fetch_local=fetch_local)
+
+
+def cancel(object_ref, *, force: bool = False, recursive: bool = True):
+    from .core_worker import ObjectRefGenerator
+
+    if isinstance(object_ref, ObjectRefGenerator):
+        object_ref = object_ref._main
+    if not isinstance(object_ref, ObjectRef):
+        raise TypeError("cancel() only supports ObjectRefs")
+    return _core().client.call("cancel", object_ref._id, force, recursive)
+
+
+def free(object_refs, local_only=False):
+    if isinstance(object_refs, ObjectRef):
+        object_refs = [object_refs]
+    _core().client.call("free", [r._id for r in object_refs])
+
+
+# ---------------------------------------------------------------------------------- cluster
+def nodes():
+    return _core().client.call("nodes")
+
+
+def cluster_resources():
+    return _core().client.call("cluster_resources")
+
+
+def available_resources():
+    return _core().client.call("available_resources")
+
+
+def get_gpu_ids():
+    core = _core()
+    return list(core.gpu_ids)
+
+
+def timeline(filename=None):
+    evs = _core().client.call("timeline")
+    if filename:
+        with open(filename, "w") as f:
+            json.dump(evs, f)
+        return None
+    return evs
+
+
+def kill(actor, *, no_restart: bool = True):
+    from ..actor import ActorHandle
+
+    if not isinstance(actor, ActorHandle):
+        raise ValueError(f"kill() only supported for actors. Got: {type(actor)}.")
+    _core().client.call("kill_actor", actor._actor_id, no_restart)
+
+
+def get_actor(name: str, namespace: Optional[str] = None):
+    from ..actor import ActorHandle
+
+    if not name:
+        raise ValueError("Please supply a non-empty value to get_actor")
+    core = _core()
+    ns = namespace if namespace is not None else core.namespace
+    info = core.client.call("get_actor", name, ns)
+    if info is None:
+        raise ValueError(f"Failed to look up actor with name '{name}'. This could because 1. You are trying to look "
+                         f"up a named actor you didn't create. 2. The named actor died. 3. You did not use a "
+                         f"namespace matching the namespace of the actor.")
+    return ActorHandle._from_meta(info["actor_id"], info["meta"])
+
+
+def get_runtime_context():
+    from ..runtime_context import RuntimeContext
+
+    return RuntimeContext(_core())
+
+
+def _head():
+    return _state["head"]

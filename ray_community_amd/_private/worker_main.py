@@ -1,0 +1,377 @@
+"""Worker process main loop (reference: ``python/ray/_private/workers/default_worker.py`` and the
+task-execution path of ``_raylet.pyx:execute_task``).
+
+A worker connects to the head, then executes tasks pushed to it. Normal tasks and default
+actors run on the main thread in arrival order; threaded actors (``max_concurrency > 1``) use a
+thread pool; async actors run coroutines on a dedicated asyncio loop.
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures
+import ctypes
+import inspect
+import json
+import os
+import queue
+import sys
+import threading
+import traceback
+
+
+def _setup_paths():
+    try:
+        for p in reversed(json.loads(os.environ.get("RCA_SYS_PATH", "[]"))):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+    except Exception:
+        pass
+    wd = os.environ.get("RCA_WORKING_DIR")
+    if wd:
+        try:
+            os.chdir(wd)
+            sys.path.insert(0, wd)
+        except OSError:
+            pass
+    for p in json.loads(os.environ.get("RCA_PY_MODULES", "[]") or "[]"):
+        d = p if os.path.isdir(p) else os.path.dirname(p)
+        if d not in sys.path:
+            sys.path.insert(0, d)
+
+
+_setup_paths()
+
+from .. import exceptions as exc  # noqa: E402
+from . import protocol as P  # noqa: E402
+from . import serialization as ser  # noqa: E402
+from .core_worker import (CoreWorker, DynamicObjectRefGenerator, ObjectRef, SocketClient, _ErrorValue,  # noqa: E402
+                          set_global_core)
+from .ids import new_id  # noqa: E402
+from .object_store import ObjectStore  # noqa: E402
+
+
+class _ActorExit(BaseException):
+    pass
+
+
+class Worker:
+    def __init__(self):
+        env = os.environ
+        self.wid = bytes.fromhex(env["RCA_WORKER_ID"])
+        self.inbox: "queue.Queue" = queue.Queue()
+        self.functions = {}
+        self.actor = None
+        self.actor_spec = None
+        self.pool = None
+        self.aloop = None
+        self.asem = None
+        self.running = {}  # tid -> thread ident
+        self.exiting = False
+        self.client = SocketClient(env["RCA_HEAD_SOCK"], "worker", self.wid, on_message=self._on_message)
+        self.store = ObjectStore(env["RCA_STORE"])
+        self.core = CoreWorker("worker", self.client, self.store, env["RCA_NODE_ID"], bytes.fromhex(env["RCA_JOB_ID"]),
+                               env.get("RCA_NAMESPACE", ""), worker_id=self.wid, session_dir=env.get("RCA_SESSION_DIR", ""))
+        gids = env.get("RCA_GPU_IDS", "")
+        self.core.gpu_ids = tuple(int(x) for x in gids.split(",") if x != "")
+        set_global_core(self.core)
+        from .. import _private as _p  # noqa
+
+        from . import worker as api_worker
+
+        api_worker._attach_worker_core(self.core)
+
+    # ------------------------------------------------------------------ messaging
+    def _on_message(self, msg):
+        t = msg[0]
+        if t == P.EXECUTE:
+            spec = msg[1]
+            if self.aloop is not None and spec["kind"] == "actor_task":
+                asyncio.run_coroutine_threadsafe(self._run_async(spec), self.aloop)
+            elif self.pool is not None and spec["kind"] == "actor_task":
+                self.pool.submit(self._execute, spec)
+            else:
+                self.inbox.put(spec)
+        elif t == P.EXIT:
+            self.exiting = True
+            self.inbox.put(None)
+        elif t == P.CANCEL:
+            self._cancel(msg[1], msg[2])
+        elif t == P.FREE_GPU:
+            self.core.free_gpu_objects(msg[1])
+
+    def _cancel(self, tid, force):
+        if force:
+            os._exit(1)
+        ident = self.running.get(tid)
+        if ident is None:
+            return
+        fut = getattr(self, "_async_tasks", {}).get(tid)
+        if fut is not None:
+            self.aloop.call_soon_threadsafe(fut.cancel)
+            return
+        ctypes.pythonapi.PyThreadState_SetAsyncExc(ctypes.c_ulong(ident), ctypes.py_object(exc.TaskCancelledError))
+
+    def loop(self):
+        while True:
+            spec = self.inbox.get()
+            if spec is None:
+                break
+            self._execute(spec)
+        self._exit()
+
+    def _exit(self):
+        try:
+            self.client.flush_refs()
+        except Exception:
+            pass
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    # ------------------------------------------------------------------ execution
+    def _resolve_args(self, spec):
+        vals = []
+        for a in spec["args"]:
+            if a[0] == "v":
+                v, _ = ser.deserialize(a[1])
+            else:  # ("d", oid, desc)
+                v = self.core._materialize(a[1], a[2])
+                if isinstance(v, _ErrorValue):
+                    raise _DepError(v.err)
+            vals.append(v)
+        kw = spec.get("kw_names") or []
+        if kw:
+            pos, kv = vals[: len(vals) - len(kw)], vals[len(vals) - len(kw):]
+            return pos, dict(zip(kw, kv))
+        return vals, {}
+
+    def _get_function(self, spec):
+        fid = spec.get("fid")
+        if spec.get("fblob") is not None:
+            self.functions[fid] = ser.loads_function(spec["fblob"])
+        fn = self.functions.get(fid)
+        if fn is None:
+            raise exc.RaySystemError(f"function {spec.get('name')} not available on this worker")
+        return fn
+
+    def _set_ctx(self, spec):
+        c = self.core.ctx
+        c.task_id = spec["tid"]
+        c.task_name = spec.get("name")
+        c.put_index = 0
+        if spec.get("gpu_ids") is not None and spec["kind"] != "actor_task":
+            self.core.gpu_ids = tuple(spec.get("gpu_ids") or ())
+        self.core.assigned_resources = spec.get("resources") or {}
+
+    def _execute(self, spec):
+        tid = spec["tid"]
+        kind = spec["kind"]
+        self._set_ctx(spec)
+        self.running[tid] = threading.get_ident()
+        info = {}
+        results = None
+        try:
+            try:
+                args, kwargs = self._resolve_args(spec)
+                if kind == "actor_creation":
+                    cls = self._get_function(spec)
+                    self._setup_actor(spec, cls)
+                    self.actor = cls(*args, **kwargs) if not spec.get("is_cross_lang") else None
+                    value = None
+                elif kind == "actor_task":
+                    method = spec["method"]
+                    if method == "__ray_terminate__":
+                        raise _ActorExit()
+                    if method == "__ray_ready__":
+                        value = True
+                    elif method == "__ray_call__":
+                        fn, args = args[0], args[1:]
+                        value = fn(self.actor, *args, **kwargs)
+                    else:
+                        value = getattr(self.actor, method)(*args, **kwargs)
+                else:
+                    fn = self._get_function(spec)
+                    value = fn(*args, **kwargs)
+                results = self._pack_returns(spec, value)
+            except _ActorExit:
+                info["actor_exit"] = True
+                results = self._pack_returns(spec, None) if spec["return_ids"] else []
+        except _DepError as d:
+            results, info = self._error_results(spec, d.err, dep=True)
+        except exc.TaskCancelledError as e:
+            results, info = self._error_results(spec, exc.TaskCancelledError(tid.hex()))
+            info["retryable"] = False
+        except BaseException as e:  # noqa
+            if _is_exit_actor(e):
+                info["actor_exit"] = True
+                results = self._pack_returns(spec, None) if spec["return_ids"] else []
+            else:
+                results, info = self._error_results(spec, e)
+        finally:
+            self.running.pop(tid, None)
+        self.client.send((P.TASK_DONE, tid, results, info))
+        if kind == "actor_creation" and info.get("error"):
+            pass
+
+    def _error_results(self, spec, e, dep=False):
+        if dep or isinstance(e, exc.RayTaskError):
+            err = e
+        else:
+            actor_repr = None
+            if self.actor is not None:
+                try:
+                    actor_repr = repr(self.actor)
+                except Exception:
+                    actor_repr = None
+            err = exc.RayTaskError.from_exception(e, spec.get("name") or "task", actor_repr=actor_repr,
+                                                  actor_id=self.core.actor_id)
+        b = ser.serialize(err, error=True)
+        data = b.to_bytes()
+        res = [("inline", data, len(data), [], ser.FLAG_ERROR, False) for _ in spec["return_ids"]]
+        info = {"error": True, "error_type": type(e).__name__,
+                "error_msg": "".join(traceback.format_exception_only(type(e), e)).strip()}
+        re_ = spec.get("retry_exceptions")
+        if re_ and not dep:
+            if re_ is True:
+                info["retryable"] = True
+            elif isinstance(re_, (list, tuple)):
+                info["retryable"] = any(isinstance(e, t) for t in re_)
+        return res, info
+
+    def _pack_one(self, oid, value):
+        s = ser.serialize(value)
+        desc = self.core._store_serialized(oid, s)
+        if s.gpu_tensors:
+            self.core.gpu_pins[oid] = s.gpu_tensors
+        return (desc[0], desc[1], desc[2], s.contained, s.flags, bool(s.gpu_tensors))
+
+    def _pack_returns(self, spec, value):
+        rids = spec["return_ids"]
+        gen = spec.get("generator")
+        if gen == "streaming":
+            n = 0
+            it = value
+            if inspect.isgenerator(it) or hasattr(it, "__next__") or hasattr(it, "__iter__"):
+                for item in it:
+                    oid = new_id()
+                    r = self._pack_one(oid, item)
+                    self.client.send((P.GEN_ITEM, spec["tid"], n, r + (oid,)))
+                    n += 1
+            return [self._pack_one(rids[0], n)] if rids else []
+        if gen == "dynamic":
+            refs = []
+            for item in value:
+                oid = new_id()
+                r = self._pack_one(oid, item)
+                # register the item object with the head, owned by the caller through the container
+                self.client.call("put", oid, r[0:3], r[3], r[5], r[4])
+                refs.append(ObjectRef(oid))
+            out = [self._pack_one(rids[0], DynamicObjectRefGenerator(refs))]
+            return out
+        n = len(rids)
+        if n == 0:
+            return []
+        if n == 1:
+            return [self._pack_one(rids[0], value)]
+        if not isinstance(value, (tuple, list)) or len(value) != n:
+            raise ValueError(f"Task returned {type(value).__name__} but num_returns={n}; "
+                             f"return a tuple/list of length {n}.")
+        return [self._pack_one(r, v) for r, v in zip(rids, value)]
+
+    # ------------------------------------------------------------------ actors
+    def _setup_actor(self, spec, cls):
+        self.actor_spec = spec
+        self.core.actor_id = spec["actor_id"]
+        self.core.gpu_ids = tuple(spec.get("gpu_ids") or ())
+        mc = spec.get("max_concurrency")
+        is_async = any(inspect.iscoroutinefunction(getattr(cls, n, None)) or inspect.isasyncgenfunction(
+            getattr(cls, n, None)) for n in dir(cls) if not n.startswith("__"))
+        if is_async:
+            self.aloop = asyncio.new_event_loop()
+            self._async_tasks = {}
+            t = threading.Thread(target=self.aloop.run_forever, name="rca-actor-asyncio", daemon=True)
+            t.start()
+            self.asem = None
+            self._amc = mc or 1000
+        elif mc and mc > 1:
+            self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=mc, thread_name_prefix="rca-actor")
+        groups = spec.get("concurrency_groups") or {}
+        self.group_pools = {g: concurrent.futures.ThreadPoolExecutor(max_workers=n) for g, n in groups.items()}
+
+    async def _run_async(self, spec):
+        if self.asem is None:
+            self.asem = asyncio.Semaphore(self._amc)
+        async with self.asem:
+            tid = spec["tid"]
+            self._set_ctx(spec)
+            info = {}
+            try:
+                args, kwargs = self._resolve_args(spec)
+                method = spec["method"]
+                if method == "__ray_terminate__":
+                    raise _ActorExit()
+                if method == "__ray_ready__":
+                    fn = lambda: True  # noqa: E731
+                else:
+                    fn = getattr(self.actor, method) if method != "__ray_call__" else None
+                if fn is None:
+                    f0, args = args[0], args[1:]
+                    value = f0(self.actor, *args, **kwargs)
+                else:
+                    value = fn(*args, **kwargs)
+                if inspect.isawaitable(value):
+                    task = asyncio.ensure_future(value)
+                    self._async_tasks[tid] = task
+                    self.running[tid] = 0
+                    try:
+                        value = await task
+                    finally:
+                        self._async_tasks.pop(tid, None)
+                        self.running.pop(tid, None)
+                elif inspect.isasyncgen(value):
+                    items = []
+                    async for x in value:
+                        items.append(x)
+                    value = iter(items)
+                loop = asyncio.get_running_loop()
+                results = await loop.run_in_executor(None, self._pack_returns, spec, value)
+            except _ActorExit:
+                info["actor_exit"] = True
+                results = []
+                for rid in spec["return_ids"]:
+                    results.append(self._pack_one(rid, None))
+            except asyncio.CancelledError:
+                results, info = self._error_results(spec, exc.TaskCancelledError(tid.hex()))
+            except _DepError as d:
+                results, info = self._error_results(spec, d.err, dep=True)
+            except BaseException as e:  # noqa
+                if _is_exit_actor(e):
+                    info["actor_exit"] = True
+                    results = [self._pack_one(rid, None) for rid in spec["return_ids"]]
+                else:
+                    results, info = self._error_results(spec, e)
+            self.client.send((P.TASK_DONE, tid, results, info))
+
+
+class _DepError(Exception):
+    def __init__(self, err):
+        super().__init__(str(err))
+        self.err = err
+
+
+def _is_exit_actor(e):
+    return type(e).__name__ == "AsyncioActorExit" or type(e).__name__ == "_ActorExitSignal"
+
+
+def main():
+    w = Worker()
+    try:
+        w.loop()
+    except KeyboardInterrupt:
+        pass
+    finally:
+        w._exit()
+
+
+if __name__ == "__main__":
+    main()

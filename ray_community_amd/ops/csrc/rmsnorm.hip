@@ -251,15 +251,31 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_generic(const bf16_t* __restr
 }
 
 // dw[c] = sum_b part[b][c]; written as bf16 (dw_bf16) and/or accumulated into fp32 (dw_f32 += ...)
+// Block = 16 column-quads (64 columns, f32x4 per lane) x 16 row groups; the 16 partial sums per
+// column are combined through LDS. Grid = H / 64 blocks, each streaming nb rows of 256 B.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int nb, int H,
                                                      bf16_t* __restrict__ dw_bf16, float* __restrict__ dw_f32,
                                                      int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= H) return;
-  float t = 0.f;
-  for (int b = 0; b < nb; ++b) t += part[(size_t)b * H + c];
-  if (dw_f32) dw_f32[c] = accumulate ? dw_f32[c] + t : t;
-  if (dw_bf16) dw_bf16[c] = f2bf(accumulate ? bf2f(dw_bf16[c]) + t : t);
+  __shared__ f32x4 red[16][16];
+  const int cq = threadIdx.x & 15;  // column quad within the block
+  const int rg = threadIdx.x >> 4;  // row group
+  const int c = (blockIdx.x * 16 + cq) * 4;
+  f32x4 t = {0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+    for (int b = rg; b < nb; b += 16) t += *reinterpret_cast<const f32x4*>(part + (size_t)b * H + c);
+  }
+  red[rg][cq] = t;
+  __syncthreads();
+  if (rg == 0 && c < H) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][cq];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = t[j];
+      if (dw_f32) dw_f32[c + j] = accumulate ? dw_f32[c + j] + v : v;
+      if (dw_bf16) dw_bf16[c + j] = f2bf(accumulate ? bf2f(dw_bf16[c + j]) + v : v);
+    }
+  }
 }
 
 RCA_API int rca_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd,
@@ -310,7 +326,7 @@ RCA_API int rca_rmsnorm_bwd(const void* s, const void* dy, const void* w, const 
     // kernel (second pass served from L2) keeps 7 waves/SIMD
     default: hipLaunchKernelGGL(rmsnorm_bwd_generic, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H);
   }
-  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, stream, dw_part, nb, H, (bf16_t*)dw_bf16, dw_f32,
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, stream, dw_part, nb, H, (bf16_t*)dw_bf16, dw_f32,
                      accumulate);
   return (int)hipGetLastError();
 }
