@@ -1108,7 +1108,7 @@ class Head:
             if owner is not None:
                 w.gpu_objects.add(rid)
             self._set_ready(e, tuple(desc), contained, owner, flags)
-        if kind == "task" and spec.get("generator") == "streaming":
+        if spec.get("generator") == "streaming":
             ts.gen_done = True
             self._flush_gen_waiters(ts)
         self._finish_task_bookkeeping(ts)

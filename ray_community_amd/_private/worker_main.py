@@ -210,6 +210,7 @@ class Worker:
         finally:
             self.running.pop(tid, None)
         self.client.send((P.TASK_DONE, tid, results, info))
+        self._keepalive = None
         if kind == "actor_creation" and info.get("error"):
             pass
 
@@ -266,7 +267,10 @@ class Worker:
                 # register the item object with the head, owned by the caller through the container
                 self.client.call("put", oid, r[0:3], r[3], r[5], r[4])
                 refs.append(ObjectRef(oid))
-            out = [self._pack_one(rids[0], DynamicObjectRefGenerator(refs))]
+            container = DynamicObjectRefGenerator(refs)
+            out = [self._pack_one(rids[0], container)]
+            # keep the item refs alive until TASK_DONE (which pins them) has been sent
+            self._keepalive = container
             return out
         n = len(rids)
         if n == 0:

@@ -207,7 +207,8 @@ class ActorHandle:
                 pass
 
     def __getattr__(self, name):
-        if name.startswith("__") and name.endswith("__") and name not in ("__ray_terminate__", "__ray_call__"):
+        if name.startswith("__") and name.endswith("__") and name not in ("__ray_terminate__", "__ray_call__",
+                                                                          "__ray_ready__"):
             raise AttributeError(name)
         meta = self.__dict__.get("_meta") or {}
         methods = meta.get("methods", {})

@@ -135,6 +135,9 @@ class ObjectLostError(RayError):
         self.object_ref_hex = object_ref_hex
         super().__init__(f"Object {object_ref_hex} is lost.")
 
+    def __reduce__(self):
+        return (type(self), (self.object_ref_hex,))
+
 
 class ObjectFetchTimedOutError(ObjectLostError):
     pass

@@ -29,3 +29,30 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture
+def shutdown_only():
+    yield None
+    import ray_community_amd as ray
+
+    ray.shutdown()
+
+
+@pytest.fixture
+def ray_start_regular(request):
+    import ray_community_amd as ray
+
+    params = getattr(request, "param", {}) or {}
+    ctx = ray.init(num_cpus=params.get("num_cpus", 4), **{k: v for k, v in params.items() if k != "num_cpus"})
+    yield ctx
+    ray.shutdown()
+
+
+@pytest.fixture
+def ray_start_cluster():
+    from ray_community_amd.cluster_utils import Cluster
+
+    c = Cluster()
+    yield c
+    c.shutdown()

@@ -1,0 +1,222 @@
+"""Actor tests (modelled on reference python/ray/tests/test_actor*.py)."""
+import asyncio
+import os
+import threading
+import time
+
+import pytest
+
+import ray_community_amd as ray
+from ray_community_amd import exceptions as exc
+
+
+@ray.remote
+class Counter:
+    def __init__(self, start=0):
+        self.n = start
+
+    def inc(self, k=1):
+        self.n += k
+        return self.n
+
+    def get(self):
+        return self.n
+
+    def pid(self):
+        return os.getpid()
+
+    def fail(self):
+        raise KeyError("nope")
+
+    def die(self):
+        os._exit(1)
+
+
+def _alive(pid):
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("State:"):
+                    return "Z" not in line.split()[1]
+    except OSError:
+        return False
+    return True
+
+
+def test_actor_basic_and_ordering(ray_start_regular):
+    c = Counter.remote(10)
+    refs = [c.inc.remote() for _ in range(50)]
+    assert ray.get(refs) == list(range(11, 61))
+    assert ray.get(c.get.remote()) == 60
+
+
+def test_actor_error_keeps_actor_alive(ray_start_regular):
+    c = Counter.remote()
+    with pytest.raises(KeyError):
+        ray.get(c.fail.remote())
+    assert ray.get(c.inc.remote()) == 1
+
+
+def test_actor_handle_passing(ray_start_regular):
+    c = Counter.remote()
+
+    @ray.remote
+    def use(h):
+        return ray.get(h.inc.remote(5))
+
+    assert ray.get(use.remote(c)) == 5
+    assert ray.get(c.get.remote()) == 5
+
+
+def test_named_actor(ray_start_regular):
+    c = Counter.options(name="ctr").remote()
+    ray.get(c.inc.remote())
+    h = ray.get_actor("ctr")
+    assert ray.get(h.get.remote()) == 1
+    with pytest.raises(ValueError):
+        Counter.options(name="ctr").remote()
+    h2 = Counter.options(name="ctr", get_if_exists=True).remote()
+    assert ray.get(h2.get.remote()) == 1
+    with pytest.raises(ValueError):
+        ray.get_actor("nope")
+
+
+def test_kill_actor(ray_start_regular):
+    c = Counter.remote()
+    ray.get(c.inc.remote())
+    ray.kill(c)
+    with pytest.raises(exc.RayActorError):
+        ray.get(c.inc.remote(), timeout=10)
+
+
+def test_actor_restart(ray_start_regular):
+    c = Counter.options(max_restarts=1).remote()
+    p1 = ray.get(c.pid.remote())
+    with pytest.raises(exc.RayActorError):
+        ray.get(c.die.remote())
+    p2 = ray.get(c.pid.remote(), timeout=20)
+    assert p1 != p2
+    assert ray.get(c.get.remote()) == 0  # state re-initialised
+    with pytest.raises(exc.RayActorError):
+        ray.get(c.die.remote())
+    with pytest.raises(exc.RayActorError):
+        ray.get(c.get.remote(), timeout=10)
+
+
+def test_actor_init_failure(ray_start_regular):
+    @ray.remote
+    class Bad:
+        def __init__(self):
+            raise RuntimeError("ctor")
+
+        def f(self):
+            return 1
+
+    b = Bad.remote()
+    with pytest.raises(exc.RayActorError):
+        ray.get(b.f.remote(), timeout=10)
+
+
+def test_async_actor(ray_start_regular):
+    @ray.remote
+    class A:
+        def __init__(self):
+            self.ev = None
+
+        async def wait_and_get(self, t):
+            await asyncio.sleep(t)
+            return t
+
+    a = A.remote()
+    t0 = time.time()
+    out = ray.get([a.wait_and_get.remote(0.5) for _ in range(20)])
+    assert out == [0.5] * 20
+    assert time.time() - t0 < 5  # concurrent, not 10 s
+
+
+def test_threaded_actor(ray_start_regular):
+    @ray.remote(max_concurrency=4)
+    class T:
+        def work(self):
+            time.sleep(0.3)
+            return threading.get_ident()
+
+    t = T.remote()
+    t0 = time.time()
+    ids = ray.get([t.work.remote() for _ in range(4)])
+    assert time.time() - t0 < 1.1
+    assert len(set(ids)) > 1
+
+
+def test_actor_method_num_returns(ray_start_regular):
+    @ray.remote
+    class M:
+        @ray.method(num_returns=2)
+        def two(self):
+            return 1, 2
+
+    m = M.remote()
+    a, b = m.two.remote()
+    assert ray.get([a, b]) == [1, 2]
+
+
+def test_exit_actor(ray_start_regular):
+    @ray.remote
+    class E:
+        def bye(self):
+            ray.exit_actor()
+
+        def ping(self):
+            return 1
+
+    e = E.remote()
+    assert ray.get(e.ping.remote()) == 1
+    ray.get(e.bye.remote())
+    with pytest.raises(exc.RayActorError):
+        ray.get(e.ping.remote(), timeout=10)
+
+
+def test_actor_out_of_scope_is_killed(ray_start_regular):
+    c = Counter.remote()
+    pid = ray.get(c.pid.remote())
+    del c
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        if not _alive(pid):
+            break
+        time.sleep(0.1)
+    else:
+        pytest.fail("actor process still alive after its handle went out of scope")
+
+
+def test_detached_actor_survives_handle(ray_start_regular):
+    c = Counter.options(name="det", lifetime="detached").remote()
+    ray.get(c.inc.remote())
+    del c
+    time.sleep(0.5)
+    assert ray.get(ray.get_actor("det").get.remote()) == 1
+
+
+def test_actor_generator(ray_start_regular):
+    @ray.remote
+    class G:
+        def stream(self, n):
+            for i in range(n):
+                yield i
+
+    g = G.remote()
+    assert [ray.get(r) for r in g.stream.remote(4)] == [0, 1, 2, 3]
+
+
+def test_actor_gpu_assignment_without_gpus(ray_start_regular):
+    @ray.remote
+    class X:
+        def gpus(self):
+            return ray.get_gpu_ids()
+
+    assert ray.get(X.remote().gpus.remote()) == []
+
+
+def test_ready(ray_start_regular):
+    c = Counter.remote()
+    assert ray.get(c.__ray_ready__.remote()) is True

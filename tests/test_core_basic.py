@@ -1,0 +1,282 @@
+"""Core API tests (modelled on reference python/ray/tests/test_basic*.py, test_actor*.py)."""
+import asyncio
+import os
+import time
+
+import numpy as np
+import pytest
+
+import ray_community_amd as ray
+from ray_community_amd import exceptions as exc
+
+
+def test_simple_task(ray_start_regular):
+    @ray.remote
+    def f(x, y=1):
+        return x + y
+
+    assert ray.get(f.remote(1)) == 2
+    assert ray.get(f.remote(1, y=5)) == 6
+    assert ray.get([f.remote(i) for i in range(20)]) == [i + 1 for i in range(20)]
+
+
+def test_task_chain_and_refs_as_args(ray_start_regular):
+    @ray.remote
+    def add(a, b):
+        return a + b
+
+    r = ray.put(1)
+    for _ in range(10):
+        r = add.remote(r, 1)
+    assert ray.get(r) == 11
+
+
+def test_multiple_returns(ray_start_regular):
+    @ray.remote(num_returns=3)
+    def f():
+        return 1, 2, 3
+
+    a, b, c = f.remote()
+    assert ray.get([a, b, c]) == [1, 2, 3]
+
+    @ray.remote
+    def g():
+        return 1
+
+    assert g.options(num_returns=0).remote() is None
+
+
+def test_large_objects_zero_copy(ray_start_regular):
+    a = np.random.rand(1 << 20)
+    r = ray.put(a)
+    b = ray.get(r)
+    assert np.array_equal(a, b)
+    assert not b.flags.writeable  # shm-backed view
+
+    @ray.remote
+    def s(x):
+        return float(x.sum())
+
+    assert abs(ray.get(s.remote(r)) - a.sum()) < 1e-6
+    assert abs(ray.get(s.remote(a)) - a.sum()) < 1e-6
+
+    @ray.remote
+    def big():
+        return np.ones((1000, 1000), dtype=np.float32)
+
+    assert ray.get(big.remote()).sum() == 1e6
+
+
+def test_torch_tensor_roundtrip(ray_start_regular):
+    import torch
+
+    t = torch.randn(100, 100).to(torch.bfloat16)
+    out = ray.get(ray.put(t))
+    assert out.dtype == torch.bfloat16 and torch.equal(out, t)
+
+    @ray.remote
+    def double(x):
+        return x * 2
+
+    assert torch.equal(ray.get(double.remote(t)), t * 2)
+
+
+def test_task_error(ray_start_regular):
+    @ray.remote
+    def bad():
+        raise ValueError("boom")
+
+    with pytest.raises(ValueError) as ei:
+        ray.get(bad.remote())
+    assert isinstance(ei.value, exc.RayTaskError)
+    assert "boom" in str(ei.value)
+
+    @ray.remote
+    def dep(x):
+        return x
+
+    with pytest.raises(ValueError):
+        ray.get(dep.remote(bad.remote()))
+
+
+def test_retry_exceptions(ray_start_regular, tmp_path):
+    counter = tmp_path / "c"
+    counter.write_text("0")
+
+    @ray.remote(max_retries=3, retry_exceptions=True)
+    def flaky(p):
+        n = int(open(p).read()) + 1
+        open(p, "w").write(str(n))
+        if n < 3:
+            raise RuntimeError("flaky")
+        return n
+
+    assert ray.get(flaky.remote(str(counter))) == 3
+
+
+def test_worker_crash_retry(ray_start_regular, tmp_path):
+    marker = tmp_path / "m"
+
+    @ray.remote(max_retries=2)
+    def die_once(p):
+        if not os.path.exists(p):
+            open(p, "w").write("x")
+            os._exit(1)
+        return "ok"
+
+    assert ray.get(die_once.remote(str(marker))) == "ok"
+
+    @ray.remote(max_retries=0)
+    def die():
+        os._exit(1)
+
+    with pytest.raises(exc.WorkerCrashedError):
+        ray.get(die.remote())
+
+
+def test_wait(ray_start_regular):
+    @ray.remote
+    def sleep(t):
+        time.sleep(t)
+        return t
+
+    refs = [sleep.remote(0.01), sleep.remote(2.0), sleep.remote(0.02)]
+    ready, not_ready = ray.wait(refs, num_returns=2, timeout=5)
+    assert len(ready) == 2 and len(not_ready) == 1
+    assert set(ray.get(ready)) == {0.01, 0.02}
+    ready, not_ready = ray.wait([sleep.remote(5)], timeout=0.1)
+    assert ready == [] and len(not_ready) == 1
+    with pytest.raises(ValueError):
+        ray.wait(refs, num_returns=4)
+
+
+def test_get_timeout(ray_start_regular):
+    @ray.remote
+    def slow():
+        time.sleep(5)
+
+    with pytest.raises(exc.GetTimeoutError):
+        ray.get(slow.remote(), timeout=0.2)
+
+
+def test_nested_tasks(ray_start_regular):
+    @ray.remote
+    def leaf(i):
+        return i
+
+    @ray.remote
+    def parent(n):
+        return sum(ray.get([leaf.remote(i) for i in range(n)]))
+
+    # more parents than CPUs: blocked parents must lend their CPU to children
+    assert ray.get([parent.remote(5) for _ in range(8)]) == [10] * 8
+
+
+def test_nested_object_refs(ray_start_regular):
+    @ray.remote
+    def make():
+        return [ray.put(i) for i in range(3)]
+
+    refs = ray.get(make.remote())
+    assert ray.get(refs) == [0, 1, 2]
+    inner = ray.put(7)
+    outer = ray.put({"x": inner})
+    del inner
+    assert ray.get(ray.get(outer)["x"]) == 7
+
+
+def test_custom_resources(shutdown_only):
+    ray.init(num_cpus=2, resources={"special": 1})
+
+    @ray.remote(resources={"special": 1})
+    def f():
+        return ray.get_runtime_context().get_assigned_resources()
+
+    r = ray.get(f.remote())
+    assert r.get("special") == 1
+    assert ray.cluster_resources()["special"] == 1
+
+
+def test_runtime_context_and_env(ray_start_regular):
+    @ray.remote(runtime_env={"env_vars": {"FOO": "bar"}})
+    def env():
+        ctx = ray.get_runtime_context()
+        return os.environ.get("FOO"), ctx.get_task_id() is not None, ctx.get_job_id()
+
+    foo, has_tid, job = ray.get(env.remote())
+    assert foo == "bar" and has_tid and job == ray.get_runtime_context().get_job_id()
+
+
+def test_cancel(ray_start_regular):
+    @ray.remote
+    def forever():
+        while True:
+            time.sleep(0.01)
+
+    r = forever.remote()
+    time.sleep(0.5)
+    ray.cancel(r)
+    with pytest.raises(exc.TaskCancelledError):
+        ray.get(r, timeout=10)
+    r2 = forever.remote()
+    time.sleep(0.3)
+    ray.cancel(r2, force=True)
+    with pytest.raises((exc.TaskCancelledError, exc.WorkerCrashedError)):
+        ray.get(r2, timeout=10)
+
+
+def test_streaming_generator(ray_start_regular):
+    @ray.remote
+    def gen(n):
+        for i in range(n):
+            yield i * i
+
+    out = [ray.get(r) for r in gen.remote(5)]
+    assert out == [0, 1, 4, 9, 16]
+
+    @ray.remote(num_returns="dynamic")
+    def dyn(n):
+        for i in range(n):
+            yield i
+
+    g = ray.get(dyn.remote(4))
+    assert [ray.get(r) for r in g] == [0, 1, 2, 3]
+
+
+def test_put_get_many_small(ray_start_regular):
+    refs = [ray.put(i) for i in range(500)]
+    assert ray.get(refs) == list(range(500))
+
+
+def test_object_store_spill(shutdown_only):
+    ray.init(num_cpus=2, object_store_memory=40 << 20)
+    refs = [ray.put(np.full(2_000_000, i, dtype=np.float64)) for i in range(8)]  # 16 MB each
+    for i, r in enumerate(refs):
+        assert ray.get(r)[0] == i
+    from ray_community_amd._private.worker import _core
+
+    stats = _core().client.call("store_stats")
+    assert stats["num_spilled"] > 0
+
+
+def test_options_validation(ray_start_regular):
+    @ray.remote
+    def f():
+        return 1
+
+    with pytest.raises(ValueError):
+        f.options(bad_opt=1)
+    with pytest.raises(TypeError):
+        f()
+
+
+def test_asyncio_driver_await(ray_start_regular):
+    @ray.remote
+    def f():
+        return 5
+
+    async def main():
+        return await f.remote()
+
+    assert asyncio.run(main()) == 5
+    assert f.remote().future().result() == 5

@@ -1,0 +1,132 @@
+"""Scheduling / placement-group tests (reference: test_placement_group*.py, test_scheduling*.py)."""
+import time
+
+import pytest
+
+import ray_community_amd as ray
+from ray_community_amd import exceptions as exc
+from ray_community_amd.util import placement_group, placement_group_table, remove_placement_group
+from ray_community_amd.util.scheduling_strategies import (NodeAffinitySchedulingStrategy,
+                                                          PlacementGroupSchedulingStrategy)
+
+
+def _node_of():
+    return ray.get_runtime_context().get_node_id()
+
+
+def test_multi_node_spread(ray_start_cluster):
+    c = ray_start_cluster
+    c.add_node(num_cpus=2)
+    for _ in range(3):
+        c.add_node(num_cpus=2)
+    assert len(ray.nodes()) == 4
+
+    @ray.remote(num_cpus=1, scheduling_strategy="SPREAD")
+    def where():
+        time.sleep(0.2)
+        return _node_of()
+
+    nodes = set(ray.get([where.remote() for _ in range(8)]))
+    assert len(nodes) == 4
+
+
+def test_node_affinity(ray_start_cluster):
+    c = ray_start_cluster
+    c.add_node(num_cpus=1)
+    n2 = c.add_node(num_cpus=1, resources={"x": 1})
+
+    @ray.remote
+    def where():
+        return _node_of()
+
+    s = NodeAffinitySchedulingStrategy(n2.node_id, soft=False)
+    assert ray.get(where.options(scheduling_strategy=s).remote()) == n2.node_id
+
+    @ray.remote(resources={"x": 1})
+    def on_x():
+        return _node_of()
+
+    assert ray.get(on_x.remote()) == n2.node_id
+
+
+def test_placement_group_strict_spread(ray_start_cluster):
+    c = ray_start_cluster
+    c.add_node(num_cpus=2)
+    c.add_node(num_cpus=2)
+    c.add_node(num_cpus=2)
+    pg = placement_group([{"CPU": 1}] * 3, strategy="STRICT_SPREAD")
+    assert ray.get(pg.ready(), timeout=10)
+    t = placement_group_table(pg)
+    assert len(set(t["bundles_to_node_id"].values())) == 3
+
+    @ray.remote(num_cpus=1)
+    def where():
+        return _node_of()
+
+    nodes = ray.get([where.options(scheduling_strategy=PlacementGroupSchedulingStrategy(pg, i)).remote()
+                     for i in range(3)])
+    assert [t["bundles_to_node_id"][i] for i in range(3)] == nodes
+    remove_placement_group(pg)
+    assert placement_group_table(pg)["state"] == "REMOVED"
+
+
+def test_placement_group_pack_and_pending(ray_start_regular):
+    pg = placement_group([{"CPU": 2}, {"CPU": 2}], strategy="PACK")
+    assert pg.wait(10)
+    pg2 = placement_group([{"CPU": 2}], strategy="PACK")
+    assert not pg2.wait(0.5)  # all 4 CPUs reserved by pg
+    remove_placement_group(pg)
+    assert pg2.wait(10)
+
+    @ray.remote(num_cpus=1)
+    class A:
+        def ok(self):
+            return 1
+
+    a = A.options(scheduling_strategy=PlacementGroupSchedulingStrategy(pg2, 0)).remote()
+    assert ray.get(a.ok.remote()) == 1
+    remove_placement_group(pg2)
+    with pytest.raises(exc.RayActorError):
+        ray.get(a.ok.remote(), timeout=10)
+
+
+def test_placement_group_validation(ray_start_regular):
+    with pytest.raises(ValueError):
+        placement_group([], strategy="PACK")
+    with pytest.raises(ValueError):
+        placement_group([{"CPU": 1}], strategy="FOO")
+
+
+def test_resources_accounting(ray_start_regular):
+    total = ray.cluster_resources()["CPU"]
+
+    @ray.remote(num_cpus=2)
+    class Holder:
+        def ping(self):
+            return 1
+
+    h = Holder.remote()
+    ray.get(h.ping.remote())
+    avail = ray.available_resources().get("CPU", 0)
+    assert avail == total - 2
+    ray.kill(h)
+    deadline = time.time() + 10
+    while time.time() < deadline and ray.available_resources().get("CPU", 0) != total:
+        time.sleep(0.05)
+    assert ray.available_resources()["CPU"] == total
+
+
+def test_remove_node_fails_tasks(ray_start_cluster):
+    c = ray_start_cluster
+    c.add_node(num_cpus=1)
+    n = c.add_node(num_cpus=1, resources={"only_here": 1})
+
+    @ray.remote(resources={"only_here": 1}, max_retries=0)
+    def hang():
+        time.sleep(30)
+
+    r = hang.remote()
+    time.sleep(1.0)
+    c.remove_node(n)
+    with pytest.raises((exc.WorkerCrashedError, exc.RayError)):
+        ray.get(r, timeout=20)
