@@ -100,7 +100,7 @@ class RemoteFunction:
             raise ValueError(f"Invalid option keyword(s) {sorted(bad)} for remote functions.")
         self._blob = None
         self._fid = None
-        self._name = getattr(function, "__qualname__", getattr(function, "__name__", "task"))
+        self._name = getattr(function, "__name__", "task")
         functools.update_wrapper(self, function)
 
     def __call__(self, *args, **kwargs):

@@ -1,0 +1,154 @@
+"""ray.util tests: ActorPool, Queue, multiprocessing Pool, collective (gloo), metrics, state, KV."""
+import time
+
+import numpy as np
+import pytest
+
+import ray_community_amd as ray
+from ray_community_amd.util import collective as col
+
+
+@ray.remote
+class Doubler:
+    def double(self, x):
+        return 2 * x
+
+
+def test_actor_pool(ray_start_regular):
+    from ray_community_amd.util import ActorPool
+
+    pool = ActorPool([Doubler.remote() for _ in range(3)])
+    assert list(pool.map(lambda a, v: a.double.remote(v), range(10))) == [2 * i for i in range(10)]
+    assert sorted(pool.map_unordered(lambda a, v: a.double.remote(v), range(10))) == [2 * i for i in range(10)]
+    pool.submit(lambda a, v: a.double.remote(v), 4)
+    assert pool.get_next() == 8
+    assert not pool.has_next()
+
+
+def test_queue(ray_start_regular):
+    from ray_community_amd.util.queue import Empty, Queue
+
+    q = Queue(maxsize=10)
+    for i in range(5):
+        q.put(i)
+    assert q.qsize() == 5
+    assert [q.get() for _ in range(5)] == list(range(5))
+    assert q.empty()
+    with pytest.raises(Empty):
+        q.get(block=False)
+    with pytest.raises(Empty):
+        q.get(timeout=0.1)
+
+    @ray.remote
+    def producer(q):
+        for i in range(3):
+            q.put(i)
+
+    ray.get(producer.remote(q))
+    assert q.get_nowait_batch(3) == [0, 1, 2]
+
+
+def test_multiprocessing_pool(ray_start_regular):
+    from ray_community_amd.util.multiprocessing import Pool
+
+    with Pool(processes=2) as p:
+        assert p.map(abs, [-1, -2, 3]) == [1, 2, 3]
+        assert p.starmap(pow, [(2, 3), (3, 2)]) == [8, 9]
+        assert p.apply(max, (1, 5)) == 5
+        assert sorted(p.imap_unordered(abs, [-3, -4])) == [3, 4]
+
+
+def test_collective_gloo_actors(ray_start_regular):
+    @ray.remote
+    class W:
+        def __init__(self, rank):
+            self.rank = rank
+
+        def setup(self, world):
+            col.init_collective_group(world, self.rank, backend="gloo", group_name="g")
+            return True
+
+        def run(self):
+            import torch
+
+            t = torch.ones(4) * (self.rank + 1)
+            col.allreduce(t, group_name="g")
+            b = torch.full((2,), float(self.rank))
+            col.broadcast(b, src_rank=1, group_name="g")
+            outs = [torch.zeros(3) for _ in range(2)]
+            col.allgather(outs, torch.full((3,), float(self.rank)), group_name="g")
+            if self.rank == 0:
+                col.send(torch.arange(3.0), 1, group_name="g")
+                got = None
+            else:
+                got = torch.zeros(3)
+                col.recv(got, 0, group_name="g")
+                got = got.tolist()
+            rs = torch.zeros(2)
+            col.reducescatter(rs, [torch.ones(2) * (self.rank + 1), torch.ones(2) * 10], group_name="g")
+            col.barrier(group_name="g")
+            return t.tolist(), b.tolist(), [o.tolist() for o in outs], got, rs.tolist(), col.get_rank("g")
+
+    ws = [W.remote(i) for i in range(2)]
+    assert ray.get([w.setup.remote(2) for w in ws]) == [True, True]
+    r0, r1 = ray.get([w.run.remote() for w in ws])
+    assert r0[0] == [3.0] * 4 and r1[0] == [3.0] * 4
+    assert r0[1] == [1.0, 1.0]
+    assert r1[2] == [[0.0] * 3, [1.0] * 3]
+    assert r1[3] == [0.0, 1.0, 2.0]
+    assert r0[4] == [3.0, 3.0] and r1[4] == [20.0, 20.0]
+    assert (r0[5], r1[5]) == (0, 1)
+
+
+def test_collective_declarative(ray_start_regular):
+    @ray.remote
+    class W:
+        def go(self):
+            import torch
+
+            t = torch.ones(2)
+            col.allreduce(t, group_name="decl")
+            return t.tolist()
+
+    ws = [W.remote() for _ in range(3)]
+    col.create_collective_group(ws, 3, [0, 1, 2], backend="gloo", group_name="decl")
+    assert ray.get([w.go.remote() for w in ws]) == [[3.0, 3.0]] * 3
+
+
+def test_metrics():
+    from ray_community_amd.util.metrics import Counter, Gauge, Histogram, export_prometheus
+
+    c = Counter("reqs", "requests", tag_keys=("route",))
+    c.inc(2, {"route": "/a"})
+    g = Gauge("temp")
+    g.set(3.5)
+    h = Histogram("lat", boundaries=[1, 10], tag_keys=("x",)).set_default_tags({"x": "y"})
+    h.observe(5)
+    txt = export_prometheus()
+    assert 'reqs{route="/a"} 2.0' in txt and "temp 3.5" in txt and 'lat_bucket{x="y",le="10"} 1' in txt
+    with pytest.raises(ValueError):
+        c.inc(1, {"bad": 1})
+
+
+def test_state_api_and_kv(ray_start_regular):
+    from ray_community_amd.experimental import internal_kv as kv
+    from ray_community_amd.util import state
+
+    @ray.remote
+    def f():
+        return 1
+
+    ray.get([f.remote() for _ in range(3)])
+    a = Doubler.remote()
+    ray.get(a.double.remote(1))
+    tasks = state.list_tasks()
+    assert sum(1 for t in tasks if t["state"] == "FINISHED") >= 3
+    assert any(x["class_name"] == "Doubler" and x["state"] == "ALIVE" for x in state.list_actors())
+    assert state.summarize_tasks()["cluster"]["total_tasks"] >= 4
+    assert len(state.list_nodes()) == 1
+    assert not kv._internal_kv_put("k", b"v")
+    assert kv._internal_kv_get("k") == b"v"
+    assert kv._internal_kv_list("k") == [b"k"]
+    assert kv._internal_kv_del("k") == 1
+    tl = ray.timeline()
+    assert any(e["name"] == "f" for e in tl)
