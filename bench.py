@@ -34,22 +34,24 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    import ray_community_amd as ray
+    from ray_community_amd.train import RunConfig, ScalingConfig
     from ray_community_amd.train.llm import llama_train_loop_per_worker
+    from ray_community_amd.train.torch import TorchTrainer
 
-    m = llama_train_loop_per_worker({
-        "model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
-        "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb,
-    })
+    loop_config = {"model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
+                   "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb}
+    # N=1: TorchTrainer runs the loop in a GPU worker actor of a local session.
+    # N>1 under torchrun: TorchTrainer binds to the launcher's ranks (one process per GPU,
+    # RCCL process group over xGMI) and runs this rank's share of the job.
+    trainer = TorchTrainer(llama_train_loop_per_worker, train_loop_config=loop_config,
+                           scaling_config=ScalingConfig(num_workers=max(1, world), use_gpu=True),
+                           run_config=RunConfig(name="bench_llama", storage_path="/tmp/rca_bench"))
+    result = trainer.fit()
+    m = result.metrics
     if rank == 0:
         out = {
             "metric": "ray_train_tokens_per_sec_llama3_8b_ddp",
@@ -80,8 +82,13 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+    if ray.is_initialized():
+        ray.shutdown()
 
 
 if __name__ == "__main__":

@@ -27,13 +27,18 @@ from .flat import FlatParameters
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0, broadcast_buffers=True,
-                 flat: Optional[FlatParameters] = None, average_in_optimizer: bool = True):
+                 flat: Optional[FlatParameters] = None, average_in_optimizer: bool = True,
+                 auto_finalize: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.flat = flat if flat is not None else FlatParameters(module, bucket_cap_mb=bucket_cap_mb)
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.average_in_optimizer = average_in_optimizer
+        # drop-in mode for plain torch optimizers: wait for all buckets at the end of backward
+        # (an autograd-engine callback, as torch DDP does) so optimizer.step() sees synced grads
+        self.auto_finalize = auto_finalize
+        self._finalize_queued = False
         self._sync = True
         self._works: List[Optional[object]] = [None] * len(self.flat.buckets)
         self._pending = [len(b.params) for b in self.flat.buckets]
@@ -51,6 +56,9 @@ class DistributedDataParallel(nn.Module):
     def _on_grad(self, p):
         if not self._sync:
             return
+        if self.auto_finalize and not self._finalize_queued:
+            self._finalize_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_cb)
         bi = self.flat.param_bucket[id(p)]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
@@ -77,6 +85,10 @@ class DistributedDataParallel(nn.Module):
             yield
         finally:
             self._sync = prev
+
+    def _finalize_cb(self):
+        self._finalize_queued = False
+        self.finish_gradient_sync()
 
     def finish_gradient_sync(self):
         """Launch any bucket whose grads never arrived (unused params) and wait for all."""

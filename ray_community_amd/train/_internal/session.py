@@ -79,6 +79,17 @@ class _Session:
         rec = dict(metrics)
         rec.setdefault("training_iteration", self.iteration)
         self.history.append(rec)
+        if checkpoint is not None and self.context.trial_dir:
+            # persist synchronously (the caller may delete its temp dir right after report)
+            import shutil
+
+            from .._checkpoint import Checkpoint
+
+            start = int(self.context.metadata.get("_ckpt_start", 0))
+            dst = os.path.join(self.context.trial_dir, f"checkpoint_{start + self.iteration - 1:06d}")
+            if os.path.abspath(checkpoint.path) != os.path.abspath(dst):
+                shutil.copytree(checkpoint.path, dst, dirs_exist_ok=True)
+            checkpoint = Checkpoint.from_directory(dst)
         if checkpoint is not None:
             self.checkpoint = checkpoint
         self.results.put((rec, checkpoint))
