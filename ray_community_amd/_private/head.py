@@ -471,6 +471,8 @@ class Head:
     def _maybe_kill_unreferenced(self, a):
         if self._actor_handles(a) or getattr(a, "pins", 0) > 0 or a.detached or a.state == A_DEAD or a.name:
             return
+        if a.queue or a.inflight:
+            return  # submitted calls keep the actor alive until they finish (re-checked on completion)
         self._kill_actor(a, no_restart=True, reason="all handles to the actor went out of scope")
 
     def _maybe_free(self, e: ObjEntry):
@@ -1132,6 +1134,8 @@ class Head:
                 a.inflight.pop(tid, None)
                 if info.get("actor_exit"):
                     self._kill_actor(a, no_restart=True, reason="exit_actor() called", graceful=True)
+                else:
+                    self._maybe_kill_unreferenced(a)
             return
         self._release_task_resources(ts)
         if w is not None:

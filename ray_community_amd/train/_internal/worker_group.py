@@ -76,8 +76,12 @@ class _TrainWorker:
 
     def poll(self, timeout: float = 1.0):
         """Return ("result", metrics, checkpoint_path) | ("done", return_value) | ("error", exc) | ("wait",)."""
+        sess = getattr(self, "_sess", None)
+        if sess is None:  # threaded actor: a poll can overtake start()
+            time.sleep(min(timeout, 0.05))
+            return ("wait",)
         try:
-            item = self._sess.results.get(timeout=timeout)
+            item = sess.results.get(timeout=timeout)
         except queue.Empty:
             return ("wait",)
         if item is None:

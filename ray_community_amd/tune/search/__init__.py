@@ -1,0 +1,200 @@
+"""Search algorithms (reference: ``python/ray/tune/search``)."""
+from __future__ import annotations
+
+import copy
+import itertools
+import random
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from .sample import Domain, Function
+
+UNRESOLVED_SEARCH_SPACE = "unresolved"
+
+
+def _walk(d, prefix=()):
+    if isinstance(d, dict):
+        if set(d.keys()) == {"grid_search"}:
+            yield prefix, d
+            return
+        for k, v in d.items():
+            yield from _walk(v, prefix + (k,))
+    elif isinstance(d, (list, tuple)) and any(isinstance(x, (dict, Domain)) for x in d):
+        for i, v in enumerate(d):
+            yield from _walk(v, prefix + (i,))
+    else:
+        yield prefix, d
+
+
+def _set(d, path, value):
+    for k in path[:-1]:
+        d = d[k]
+    d[path[-1]] = value
+
+
+def _get(d, path):
+    for k in path:
+        d = d[k]
+    return d
+
+
+class Searcher:
+    FINISHED = "FINISHED"
+
+    def __init__(self, metric: Optional[str] = None, mode: Optional[str] = None):
+        self._metric = metric
+        self._mode = mode
+
+    @property
+    def metric(self):
+        return self._metric
+
+    @property
+    def mode(self):
+        return self._mode
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        if self._metric is None:
+            self._metric = metric
+        if self._mode is None:
+            self._mode = mode
+        return True
+
+    def suggest(self, trial_id: str) -> Optional[Dict]:
+        raise NotImplementedError
+
+    def on_trial_result(self, trial_id: str, result: Dict):
+        pass
+
+    def on_trial_complete(self, trial_id: str, result: Optional[Dict] = None, error: bool = False):
+        pass
+
+    def save(self, path):
+        pass
+
+    def restore(self, path):
+        pass
+
+
+def generate_variants(spec: Dict, num_samples: int = 1, rng=None) -> List[Dict]:
+    """Grid search cross product x num_samples, then resolve every Domain (sample_from last)."""
+    rng = rng or np.random
+    grid_axes = [(p, v["grid_search"]) for p, v in _walk(spec) if isinstance(v, dict) and "grid_search" in v]
+    combos = list(itertools.product(*[vals for _, vals in grid_axes])) if grid_axes else [()]
+    out = []
+    for _ in range(num_samples):
+        for combo in combos:
+            cfg = copy.deepcopy(spec)
+            for (p, _), val in zip(grid_axes, combo):
+                _set(cfg, p, val)
+            funcs = []
+            for p, v in _walk(cfg):
+                if isinstance(v, Function):
+                    funcs.append((p, v))
+                elif isinstance(v, Domain):
+                    _set(cfg, p, v.sample(random_state=rng))
+            for p, v in funcs:
+                _set(cfg, p, v.sample(spec=_Spec(cfg), random_state=rng))
+            out.append(cfg)
+    return out
+
+
+class _Spec(dict):
+    """Lets sample_from lambdas use ``spec.config.x`` like the reference."""
+
+    def __init__(self, cfg):
+        super().__init__(config=cfg)
+        self.config = _AttrDict(cfg)
+
+
+class _AttrDict(dict):
+    def __getattr__(self, k):
+        v = self[k]
+        return _AttrDict(v) if isinstance(v, dict) else v
+
+
+class BasicVariantGenerator(Searcher):
+    def __init__(self, points_to_evaluate: Optional[List[Dict]] = None, max_concurrent: int = 0,
+                 constant_grid_search: bool = False, random_state=None):
+        super().__init__()
+        self._points = list(points_to_evaluate or [])
+        self._queue: List[Dict] = []
+        self._rng = np.random.RandomState(random_state) if random_state is not None else np.random
+        self.max_concurrent = max_concurrent
+        self._finished = False
+
+    def set_space(self, param_space: Dict, num_samples: int):
+        self._queue = list(self._points) + generate_variants(param_space, num_samples, self._rng)
+
+    def total(self):
+        return len(self._queue)
+
+    def suggest(self, trial_id):
+        if not self._queue:
+            return Searcher.FINISHED
+        return self._queue.pop(0)
+
+
+class ConcurrencyLimiter(Searcher):
+    def __init__(self, searcher: Searcher, max_concurrent: int, batch: bool = False):
+        super().__init__(searcher.metric, searcher.mode)
+        self.searcher = searcher
+        self.max_concurrent = max_concurrent
+        self.live = set()
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        return self.searcher.set_search_properties(metric, mode, config, **spec)
+
+    def suggest(self, trial_id):
+        if len(self.live) >= self.max_concurrent:
+            return None
+        s = self.searcher.suggest(trial_id)
+        if s is not None and s != Searcher.FINISHED:
+            self.live.add(trial_id)
+        return s
+
+    def on_trial_result(self, trial_id, result):
+        self.searcher.on_trial_result(trial_id, result)
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        self.live.discard(trial_id)
+        self.searcher.on_trial_complete(trial_id, result, error)
+
+
+class RandomSearch(Searcher):
+    """Independent random sampling from a space of Domains (the unit for model-based searchers)."""
+
+    def __init__(self, space: Optional[Dict] = None, metric=None, mode=None, seed=None):
+        super().__init__(metric, mode)
+        self.space = space
+        self._rng = np.random.RandomState(seed)
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        super().set_search_properties(metric, mode, config)
+        if self.space is None:
+            self.space = config
+        return True
+
+    def suggest(self, trial_id):
+        return generate_variants(self.space, 1, self._rng)[0]
+
+
+class Repeater(Searcher):
+    def __init__(self, searcher: Searcher, repeat: int = 1, set_index: bool = True):
+        super().__init__(searcher.metric, searcher.mode)
+        self.searcher = searcher
+        self.repeat = repeat
+        self._current = None
+        self._left = 0
+
+    def suggest(self, trial_id):
+        if self._left == 0:
+            self._current = self.searcher.suggest(trial_id)
+            self._left = self.repeat
+        self._left -= 1
+        return copy.deepcopy(self._current)
+
+
+__all__ = ["Searcher", "BasicVariantGenerator", "ConcurrencyLimiter", "RandomSearch", "Repeater",
+           "generate_variants"]

@@ -1,0 +1,693 @@
+"""Tuner / trial controller / ResultGrid (reference: ``python/ray/tune/tuner.py``,
+``tune/execution/tune_controller.py``, ``tune/result_grid.py``, ``tune/trainable/trainable.py``).
+
+Trials run as actors (function and class trainables) or as driver-side threads that orchestrate
+their own worker group (Train ``Trainer`` objects); the controller streams their reports,
+applies stopping criteria, the scheduler's decisions and the searcher's suggestions, and keeps a
+JSON experiment state so an interrupted experiment can be restored.
+"""
+from __future__ import annotations
+
+import copy
+import inspect
+import json
+import logging
+import os
+import queue
+import shutil
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Union
+
+from ..air.config import CheckpointConfig, FailureConfig, RunConfig
+from ..air.result import Result
+from .schedulers import FIFOScheduler, TrialScheduler
+from .search import BasicVariantGenerator, ConcurrencyLimiter, Searcher
+
+log = logging.getLogger("ray_community_amd.tune")
+
+PENDING, RUNNING, PAUSED, TERMINATED, ERROR = "PENDING", "RUNNING", "PAUSED", "TERMINATED", "ERROR"
+
+
+@dataclass
+class TuneConfig:
+    metric: Optional[str] = None
+    mode: Optional[str] = None
+    search_alg: Optional[Searcher] = None
+    scheduler: Optional[TrialScheduler] = None
+    num_samples: int = 1
+    max_concurrent_trials: Optional[int] = None
+    time_budget_s: Optional[float] = None
+    reuse_actors: bool = False
+    trial_name_creator: Optional[Callable] = None
+    trial_dirname_creator: Optional[Callable] = None
+    chdir_to_trial_dir: bool = False
+
+    def __post_init__(self):
+        if self.mode not in (None, "min", "max"):
+            raise ValueError("`mode` must be 'min' or 'max'")
+
+
+class Trainable:
+    """Class API: override setup/step/save_checkpoint/load_checkpoint."""
+
+    def __init__(self, config: Optional[Dict] = None, **kw):
+        self.config = config or {}
+        self._iteration = 0
+        self.setup(copy.deepcopy(self.config))
+
+    def setup(self, config):
+        pass
+
+    def step(self) -> Dict:
+        raise NotImplementedError
+
+    def save_checkpoint(self, checkpoint_dir: str) -> Optional[Dict]:
+        return None
+
+    def load_checkpoint(self, checkpoint):
+        pass
+
+    def cleanup(self):
+        pass
+
+    def reset_config(self, new_config) -> bool:
+        return False
+
+    @property
+    def iteration(self):
+        return self._iteration
+
+    @property
+    def training_iteration(self):
+        return self._iteration
+
+
+class Stopper:
+    def __call__(self, trial_id: str, result: Dict) -> bool:
+        return False
+
+    def stop_all(self) -> bool:
+        return False
+
+
+class _ClassTrainableRunner:
+    def __init__(self, cls, config, checkpoint_path=None):
+        self.t = cls(config)
+        if checkpoint_path:
+            st = None
+            p = os.path.join(checkpoint_path, "_state.json")
+            if os.path.exists(p):
+                with open(p) as f:
+                    st = json.load(f)
+            if st:
+                self.t._iteration = st.get("iteration", 0)
+            data = self._load_dict(checkpoint_path)
+            self.t.load_checkpoint(data if data is not None else checkpoint_path)
+
+    @staticmethod
+    def _load_dict(path):
+        p = os.path.join(path, "_dict_checkpoint.pkl")
+        if os.path.exists(p):
+            import pickle
+
+            with open(p, "rb") as f:
+                return pickle.load(f)
+        return None
+
+    def step(self):
+        r = self.t.step() or {}
+        self.t._iteration += 1
+        r = dict(r)
+        r.setdefault("training_iteration", self.t._iteration)
+        return r
+
+    def save(self, path):
+        os.makedirs(path, exist_ok=True)
+        d = self.t.save_checkpoint(path)
+        if isinstance(d, dict):
+            import pickle
+
+            with open(os.path.join(path, "_dict_checkpoint.pkl"), "wb") as f:
+                pickle.dump(d, f)
+        with open(os.path.join(path, "_state.json"), "w") as f:
+            json.dump({"iteration": self.t._iteration}, f)
+        return path
+
+    def stop(self):
+        self.t.cleanup()
+        return True
+
+
+class Trial:
+    def __init__(self, trial_id: str, config: Dict, local_path: str, resources: Dict):
+        self.trial_id = trial_id
+        self.config = config
+        self.local_path = local_path
+        self.resources = resources
+        self.status = PENDING
+        self.last_result: Dict = {}
+        self.metrics_history: List[Dict] = []
+        self.checkpoint = None
+        self.error: Optional[BaseException] = None
+        self.num_failures = 0
+        self.start_time = None
+        self.runner = None
+        self.thread_q: Optional[queue.Queue] = None
+        self.stop_flag = False
+        self.restore_path = None
+        self.iteration_offset = 0
+
+    def __repr__(self):
+        return f"Trial({self.trial_id}, {self.status})"
+
+
+class ResultGrid:
+    def __init__(self, results: List[Result], metric=None, mode=None, experiment_path=None):
+        self._results = results
+        self._metric = metric
+        self._mode = mode
+        self.experiment_path = experiment_path
+
+    def __len__(self):
+        return len(self._results)
+
+    def __getitem__(self, i) -> Result:
+        return self._results[i]
+
+    def __iter__(self):
+        return iter(self._results)
+
+    @property
+    def errors(self):
+        return [r.error for r in self._results if r.error is not None]
+
+    @property
+    def num_errors(self):
+        return len(self.errors)
+
+    @property
+    def num_terminated(self):
+        return len([r for r in self._results if r.error is None])
+
+    def get_best_result(self, metric: Optional[str] = None, mode: Optional[str] = None, scope: str = "last",
+                        filter_nan_and_inf: bool = True) -> Result:
+        metric = metric or self._metric
+        mode = mode or self._mode
+        if not metric or not mode:
+            raise ValueError("No metric/mode provided to get_best_result and none set in TuneConfig.")
+        best, bv = None, None
+        for r in self._results:
+            if not r.metrics_history and not r.metrics:
+                continue
+            if scope == "last":
+                vals = [r.metrics.get(metric)] if r.metrics else []
+            else:
+                vals = [m.get(metric) for m in r.metrics_history]
+            vals = [v for v in vals if v is not None and (not filter_nan_and_inf or _finite(v))]
+            if not vals:
+                continue
+            v = max(vals) if mode == "max" else min(vals)
+            if bv is None or (v > bv if mode == "max" else v < bv):
+                best, bv = r, v
+        if best is None:
+            raise RuntimeError(f"No best trial found for metric {metric}.")
+        return best
+
+    def get_dataframe(self, filter_metric=None, filter_mode=None):
+        import pandas as pd
+
+        rows = []
+        for r in self._results:
+            row = dict(r.metrics or {})
+            for k, v in (row.pop("config", None) or {}).items():
+                row[f"config/{k}"] = v
+            row["logdir"] = r.path
+            rows.append(row)
+        return pd.DataFrame(rows)
+
+
+def _finite(v):
+    try:
+        import math
+
+        return math.isfinite(float(v))
+    except (TypeError, ValueError):
+        return True
+
+
+class TuneController:
+    def __init__(self, trainable, param_space: Dict, tune_config: TuneConfig, run_config: RunConfig,
+                 exp_dir: str, restored_trials: Optional[List[Trial]] = None):
+        self.trainable = trainable
+        self.param_space = param_space or {}
+        self.tc = tune_config
+        self.rc = run_config
+        self.exp_dir = exp_dir
+        os.makedirs(exp_dir, exist_ok=True)
+        self.scheduler = tune_config.scheduler or FIFOScheduler()
+        self.scheduler.set_search_properties(tune_config.metric, tune_config.mode)
+        self.searcher = tune_config.search_alg or BasicVariantGenerator()
+        inner = self.searcher.searcher if isinstance(self.searcher, ConcurrencyLimiter) else self.searcher
+        if isinstance(inner, BasicVariantGenerator):
+            inner.set_space(self.param_space, tune_config.num_samples)
+            self._budget = None  # until exhausted
+        else:
+            self.searcher.set_search_properties(tune_config.metric, tune_config.mode, self.param_space)
+            self._budget = tune_config.num_samples
+        self.trials: List[Trial] = list(restored_trials or [])
+        self._searcher_done = bool(restored_trials)
+        self.kind = self._kind(trainable)
+        self.resources = getattr(trainable, "_rca_resources", None) or {"CPU": 1}
+        self.max_conc = tune_config.max_concurrent_trials or self._default_concurrency()
+        self._t0 = time.time()
+        self._stop_all = False
+
+    # ----------------------------------------------------------------------- helpers
+    def _kind(self, t):
+        from ..train.data_parallel_trainer import BaseTrainer
+
+        if isinstance(t, BaseTrainer):
+            return "trainer"
+        if inspect.isclass(t) and issubclass(t, Trainable):
+            return "class"
+        if callable(t):
+            return "function"
+        raise TypeError(f"unsupported trainable {t!r}")
+
+    def _default_concurrency(self):
+        from .._private.worker import cluster_resources
+
+        if self.kind == "trainer":
+            return 1 << 30
+        cr = cluster_resources()
+        n = 1 << 30
+        for k, v in self.resources.items():
+            if v > 0:
+                n = min(n, int(cr.get(k, 0) // v))
+        return max(1, n)
+
+    def get_trial(self, trial_id):
+        for t in self.trials:
+            if t.trial_id == trial_id:
+                return t
+        return None
+
+    def _new_trial(self):
+        if self._searcher_done:
+            return None
+        if self._budget is not None and self._budget <= 0:
+            self._searcher_done = True
+            return None
+        tid = uuid.uuid4().hex[:8]
+        cfg = self.searcher.suggest(tid)
+        if cfg == Searcher.FINISHED:
+            self._searcher_done = True
+            return None
+        if cfg is None:
+            return None
+        if self._budget is not None:
+            self._budget -= 1
+        name = f"trial_{len(self.trials):05d}_{tid}"
+        if self.tc.trial_dirname_creator:
+            name = self.tc.trial_dirname_creator(_TrialView(tid, cfg))
+        t = Trial(tid, cfg, os.path.join(self.exp_dir, name), self.resources)
+        os.makedirs(t.local_path, exist_ok=True)
+        self.trials.append(t)
+        self.scheduler.on_trial_add(self, t)
+        return t
+
+    # ----------------------------------------------------------------------- lifecycle
+    def _start(self, trial: Trial):
+        from .._private.worker import get
+        from ..actor import ActorClass
+        from ..train._internal.session import TrainContext
+        from ..train._internal.worker_group import _TrainWorker
+
+        trial.status = RUNNING
+        trial.start_time = time.time()
+        trial.stop_flag = False
+        ckpt = trial.checkpoint if trial.restore_path is None else _ckpt(trial.restore_path)
+        trial.restore_path = None
+        res = dict(self.resources)
+        opts = {"num_cpus": res.pop("CPU", 0), "num_gpus": res.pop("GPU", 0), "resources": res or None,
+                "max_concurrency": 4}
+        opts = {k: v for k, v in opts.items() if v is not None}
+        if self.kind == "function":
+            cls = ActorClass(_TrainWorker, opts)
+            trial.runner = cls.remote()
+            ctx = TrainContext(trial_dir=trial.local_path, trial_id=trial.trial_id,
+                               trial_name=os.path.basename(trial.local_path),
+                               experiment_name=os.path.basename(self.exp_dir),
+                               metadata={"_ckpt_start": _next_ckpt_index(trial.local_path)})
+            fn = self.trainable
+            takes = len(inspect.signature(fn).parameters) >= 1
+            cfg = copy.deepcopy(trial.config)
+            # non-blocking: the actor may wait for resources; the first poll queues behind start()
+            trial.runner.start.remote(fn if takes else (lambda c, f=fn: f()), cfg, ctx, ckpt, {})
+            trial.pending = trial.runner.poll.remote(0.05)
+        elif self.kind == "class":
+            cls = ActorClass(_ClassTrainableRunner, {k: v for k, v in opts.items() if k != "max_concurrency"})
+            trial.runner = cls.remote(self.trainable, copy.deepcopy(trial.config), ckpt.path if ckpt else None)
+            trial.pending = trial.runner.step.remote()
+        else:
+            trial.thread_q = queue.Queue()
+            trainer = self.trainable._with_config(trial.config)
+            trainer._in_tune = True
+            if ckpt is not None:
+                trainer.resume_from_checkpoint = ckpt
+
+            def cb(m, c, trial=trial):
+                trial.thread_q.put(("result", m, c))
+                return trial.stop_flag
+
+            def run(trial=trial, trainer=trainer):
+                try:
+                    r = trainer._fit_in_trial(trial.local_path, cb)
+                    trial.thread_q.put(("done", r.error))
+                except BaseException as e:  # noqa
+                    trial.thread_q.put(("done", e))
+
+            th = threading.Thread(target=run, daemon=True)
+            th.start()
+            trial.runner = th
+
+    def _poll(self, trial: Trial):
+        """-> list of events: ("result", metrics, ckpt_path) / ("done", err)."""
+        from .._private.worker import get, wait
+
+        if self.kind == "function":
+            ready, _ = wait([trial.pending], timeout=0.01)
+            if not ready:
+                return []
+            try:
+                r = get(trial.pending)
+            except Exception as e:  # noqa - the trial actor died
+                return [("done", e)]
+            trial.pending = trial.runner.poll.remote(0.05)
+            if r[0] == "wait":
+                return []
+            if r[0] == "result":
+                return [("result", r[1], r[2])]
+            if r[0] == "done":
+                return [("done", None)]
+            return [("done", r[1])]
+        if self.kind == "class":
+            ready, _ = wait([trial.pending], timeout=0.02)
+            if not ready:
+                return []
+            try:
+                res = get(trial.pending)
+            except Exception as e:  # noqa
+                return [("done", e)]
+            ck = None
+            freq = self.rc.checkpoint_config.checkpoint_frequency
+            it = res.get("training_iteration", 0)
+            if freq and it % freq == 0:
+                ck = get(trial.runner.save.remote(
+                    os.path.join(trial.local_path, f"checkpoint_{_next_ckpt_index(trial.local_path):06d}")))
+            trial.pending = None
+            if res.get("done"):
+                return [("result", res, ck), ("done", None)]
+            return [("result", res, ck)]
+        out = []
+        while True:
+            try:
+                ev = trial.thread_q.get(timeout=0.02 if not out else 0)
+            except queue.Empty:
+                break
+            if ev[0] == "result":
+                out.append(("result", ev[1], ev[2].path if ev[2] is not None else None))
+            else:
+                out.append(("done", ev[1]))
+        return out
+
+    def _stop_runner(self, trial: Trial, save=False):
+        from .._private.worker import get, kill
+
+        if self.kind in ("function", "class") and trial.runner is not None:
+            if save and self.kind == "class":
+                try:
+                    p = get(trial.runner.save.remote(os.path.join(
+                        trial.local_path, f"checkpoint_{_next_ckpt_index(trial.local_path):06d}")))
+                    trial.checkpoint = _ckpt(p)
+                except Exception:
+                    pass
+            try:
+                kill(trial.runner)
+            except Exception:
+                pass
+        elif self.kind == "trainer" and trial.runner is not None:
+            trial.stop_flag = True
+            trial.runner.join(timeout=60)
+        trial.runner = None
+
+    def exploit(self, trial: Trial, donor: Trial, new_config: Dict):
+        """PBT: restart ``trial`` from ``donor``'s latest checkpoint with ``new_config``."""
+        self._stop_runner(trial)
+        dst = os.path.join(trial.local_path, f"checkpoint_{_next_ckpt_index(trial.local_path):06d}")
+        shutil.copytree(donor.checkpoint.path, dst, dirs_exist_ok=True)
+        trial.config = new_config
+        trial.restore_path = dst
+        trial.checkpoint = _ckpt(dst)
+        trial.iteration_offset = trial.last_result.get("training_iteration", 0)
+        trial.status = PENDING
+
+    def _should_stop(self, trial, result) -> bool:
+        stop = self.rc.stop
+        if stop is None:
+            return bool(result.get("done"))
+        if isinstance(stop, dict):
+            for k, v in stop.items():
+                if k in result and result[k] >= v:
+                    return True
+            return bool(result.get("done"))
+        if isinstance(stop, Stopper):
+            if stop.stop_all():
+                self._stop_all = True
+            return bool(stop(trial.trial_id, result))
+        if callable(stop):
+            return bool(stop(trial.trial_id, result))
+        return False
+
+    def _on_result(self, trial: Trial, metrics: Dict, ckpt_path: Optional[str]):
+        m = dict(metrics)
+        if trial.iteration_offset:
+            m["training_iteration"] = m.get("training_iteration", 0) + trial.iteration_offset
+        m.setdefault("training_iteration", len(trial.metrics_history) + 1)
+        m["trial_id"] = trial.trial_id
+        m["time_total_s"] = time.time() - trial.start_time
+        m["timestamp"] = time.time()
+        m["config"] = trial.config
+        trial.last_result = m
+        trial.metrics_history.append(m)
+        if ckpt_path:
+            trial.checkpoint = _ckpt(ckpt_path)
+        with open(os.path.join(trial.local_path, "result.json"), "a") as f:
+            f.write(json.dumps(_jsonable(m)) + "\n")
+        self.searcher.on_trial_result(trial.trial_id, m)
+        for cb in (self.rc.callbacks or []):
+            if hasattr(cb, "on_trial_result"):
+                cb.on_trial_result(iteration=0, trials=self.trials, trial=trial, result=m)
+        if self._should_stop(trial, m):
+            return TrialScheduler.STOP
+        return self.scheduler.on_trial_result(self, trial, m)
+
+    def _complete(self, trial: Trial, err=None):
+        if err is not None:
+            trial.num_failures += 1
+            mf = self.rc.failure_config.max_failures
+            if mf < 0 or trial.num_failures <= mf:
+                trial.status = PENDING
+                trial.restore_path = trial.checkpoint.path if trial.checkpoint else None
+                trial.iteration_offset = trial.last_result.get("training_iteration", 0) if trial.checkpoint else 0
+                return
+            trial.status = ERROR
+            trial.error = err
+            self.scheduler.on_trial_error(self, trial)
+            self.searcher.on_trial_complete(trial.trial_id, trial.last_result, error=True)
+            if self.rc.failure_config.fail_fast:
+                self._stop_all = True
+        else:
+            trial.status = TERMINATED
+            self.scheduler.on_trial_complete(self, trial, trial.last_result)
+            self.searcher.on_trial_complete(trial.trial_id, trial.last_result)
+        for cb in (self.rc.callbacks or []):
+            if hasattr(cb, "on_trial_complete"):
+                cb.on_trial_complete(iteration=0, trials=self.trials, trial=trial)
+
+    def run(self):
+        from .._private import worker as w
+
+        if not w.is_initialized():
+            w.init()
+        while True:
+            if self.tc.time_budget_s and time.time() - self._t0 > self.tc.time_budget_s:
+                self._stop_all = True
+            running = [t for t in self.trials if t.status == RUNNING]
+            if self._stop_all:
+                for t in running:
+                    self._stop_runner(t)
+                    t.status = TERMINATED
+                break
+            # launch
+            while len(running) < self.max_conc:
+                t = next((x for x in self.trials if x.status == PENDING), None)
+                if t is None:
+                    t = self._new_trial()
+                if t is None:
+                    break
+                self._start(t)
+                running.append(t)
+            if not running:
+                if self._searcher_done or all(t.status in (TERMINATED, ERROR) for t in self.trials) and \
+                        self._new_trial_blocked():
+                    break
+                time.sleep(0.01)
+                continue
+            for t in running:
+                if t.status != RUNNING:
+                    continue
+                for ev in self._poll(t):
+                    if ev[0] == "result":
+                        decision = self._on_result(t, ev[1], ev[2])
+                        if decision == TrialScheduler.STOP:
+                            self._stop_runner(t)
+                            self._complete(t)
+                            break
+                        if decision == TrialScheduler.PAUSE:
+                            self._stop_runner(t, save=True)
+                            t.status = PAUSED
+                            break
+                        if decision == TrialScheduler.NOOP:
+                            break  # exploit() already restarted the trial
+                        if self.kind == "class" and t.status == RUNNING and t.runner is not None:
+                            t.pending = t.runner.step.remote()
+                    else:
+                        self._stop_runner(t)
+                        self._complete(t, ev[1])
+                        break
+            self._save_state()
+            # resume paused trials when nothing else is pending
+            if not any(x.status in (PENDING,) for x in self.trials) and self._searcher_done:
+                for x in self.trials:
+                    if x.status == PAUSED and len([y for y in self.trials if y.status == RUNNING]) < self.max_conc:
+                        x.status = PENDING
+                        x.restore_path = x.checkpoint.path if x.checkpoint else None
+                        x.iteration_offset = x.last_result.get("training_iteration", 0)
+        self._save_state()
+        return self._results()
+
+    def _new_trial_blocked(self):
+        return self._searcher_done
+
+    def _results(self):
+        out = []
+        for t in self.trials:
+            out.append(Result(metrics=t.last_result or None, checkpoint=t.checkpoint, error=t.error,
+                              path=t.local_path, metrics_history=t.metrics_history))
+        return ResultGrid(out, self.tc.metric, self.tc.mode, self.exp_dir)
+
+    def _save_state(self):
+        st = {"trials": [{"trial_id": t.trial_id, "config": _jsonable(t.config), "status": t.status,
+                          "local_path": t.local_path, "last_result": _jsonable(t.last_result),
+                          "checkpoint": t.checkpoint.path if t.checkpoint else None,
+                          "error": repr(t.error) if t.error else None} for t in self.trials]}
+        tmp = os.path.join(self.exp_dir, ".experiment_state.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(st, f)
+        os.replace(tmp, os.path.join(self.exp_dir, "experiment_state.json"))
+
+
+class _TrialView:
+    def __init__(self, tid, cfg):
+        self.trial_id = tid
+        self.config = cfg
+
+
+def _ckpt(path):
+    from ..train._checkpoint import Checkpoint
+
+    return Checkpoint.from_directory(path) if path else None
+
+
+def _next_ckpt_index(path):
+    if not os.path.isdir(path):
+        return 0
+    idx = [int(d.split("_")[-1]) for d in os.listdir(path) if d.startswith("checkpoint_") and d.split("_")[-1].isdigit()]
+    return max(idx) + 1 if idx else 0
+
+
+def _jsonable(d):
+    out = {}
+    for k, v in (d or {}).items():
+        try:
+            json.dumps(v)
+            out[k] = v
+        except TypeError:
+            out[k] = _jsonable(v) if isinstance(v, dict) else repr(v)
+    return out
+
+
+class Tuner:
+    def __init__(self, trainable=None, *, param_space: Optional[Dict] = None, tune_config: Optional[TuneConfig] = None,
+                 run_config: Optional[RunConfig] = None, _restored_trials=None, _exp_dir=None):
+        self.trainable = trainable
+        self.param_space = param_space or {}
+        self.tune_config = tune_config or TuneConfig()
+        from ..train.data_parallel_trainer import BaseTrainer
+
+        if run_config is None and isinstance(trainable, BaseTrainer):
+            run_config = trainable.run_config
+        self.run_config = run_config or RunConfig()
+        self._restored = _restored_trials
+        self._exp_dir = _exp_dir
+
+    def fit(self) -> ResultGrid:
+        name = self.run_config.name or f"{_tname(self.trainable)}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
+        exp_dir = self._exp_dir or os.path.join(os.path.expanduser(self.run_config.storage_path), name)
+        ctrl = TuneController(self.trainable, self.param_space, self.tune_config, self.run_config, exp_dir,
+                              self._restored)
+        return ctrl.run()
+
+    def get_results(self) -> ResultGrid:
+        return self.fit()
+
+    @classmethod
+    def can_restore(cls, path: str) -> bool:
+        return os.path.exists(os.path.join(path, "experiment_state.json"))
+
+    @classmethod
+    def restore(cls, path: str, trainable, *, param_space=None, resume_unfinished=True, resume_errored=False,
+                restart_errored=False, tune_config=None, run_config=None) -> "Tuner":
+        with open(os.path.join(path, "experiment_state.json")) as f:
+            st = json.load(f)
+        trials = []
+        for d in st["trials"]:
+            t = Trial(d["trial_id"], d["config"], d["local_path"], {"CPU": 1})
+            t.last_result = d["last_result"] or {}
+            t.checkpoint = _ckpt(d["checkpoint"])
+            hp = os.path.join(t.local_path, "result.json")
+            if os.path.exists(hp):
+                with open(hp) as f:
+                    t.metrics_history = [json.loads(l) for l in f if l.strip()]
+            status = d["status"]
+            if status == TERMINATED:
+                t.status = TERMINATED
+            elif status == ERROR and not (resume_errored or restart_errored):
+                t.status = ERROR
+                t.error = RuntimeError(d.get("error") or "trial errored")
+            else:
+                t.status = PENDING
+                if not restart_errored and t.checkpoint is not None:
+                    t.restore_path = t.checkpoint.path
+                    t.iteration_offset = t.last_result.get("training_iteration", 0)
+            trials.append(t)
+        return cls(trainable, param_space=param_space, tune_config=tune_config, run_config=run_config,
+                   _restored_trials=trials, _exp_dir=path)
+
+
+def _tname(t):
+    return getattr(t, "__name__", type(t).__name__)
