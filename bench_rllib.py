@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Secondary benchmark: RLlib PPO env-steps/sec on the Atari-shaped task (BASELINE.json config
+"RLlib PPO Atari, GPU learners + vectorized env actors (SampleBatch HIP GAE)").
+
+    python bench_rllib.py --learners L --runners R --envs-per-runner E --iters K --warmup W
+
+Env runners are CPU actors stepping E vectorised SyntheticAtari envs (84x84x4 uint8, Discrete(6):
+ALE is not installed here); the learner(s) run on MI355X GPUs (GAE / advantage normalisation /
+frame preprocessing as HIP kernels; with L > 1 learners, gradients all-reduced over RCCL).
+Prints ONE JSON line with whole-job env-steps/s over K timed training iterations.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--learners", type=int, default=0, help="0 = one local GPU learner in the driver")
+    ap.add_argument("--runners", type=int, default=None)
+    ap.add_argument("--envs-per-runner", type=int, default=16)
+    ap.add_argument("--train-batch", type=int, default=8192)
+    ap.add_argument("--minibatch", type=int, default=1024)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--env", default="ALE/Pong-v5")
+    args = ap.parse_args()
+
+    import torch
+
+    import ray_community_amd as ray
+    from ray_community_amd.rllib import PPOConfig
+
+    ncpu = len(os.sched_getaffinity(0))
+    runners = args.runners if args.runners is not None else max(1, min(16, ncpu - 2))
+    ngpu = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    ray.init(num_cpus=max(ncpu, runners + 2), num_gpus=ngpu)
+    cfg = (PPOConfig().environment(args.env)
+           .env_runners(num_env_runners=runners, num_envs_per_env_runner=args.envs_per_runner)
+           .training(lr=2.5e-4, train_batch_size=args.train_batch, minibatch_size=args.minibatch,
+                     num_epochs=args.epochs, clip_param=0.1, vf_clip_param=10.0, entropy_coeff=0.01,
+                     kl_coeff=0.5, lambda_=0.95, gamma=0.99, model={"vf_share_layers": True}))
+    if args.learners > 0:
+        cfg.learners(num_learners=args.learners, num_gpus_per_learner=1 if ngpu else 0)
+    else:
+        cfg.resources(num_gpus=1 if ngpu else 0)
+    algo = cfg.build()
+    for _ in range(args.warmup):
+        algo.train()
+    t0 = time.perf_counter()
+    steps = 0
+    last = None
+    for _ in range(args.iters):
+        r = algo.train()
+        steps += r["num_env_steps_sampled_this_iter"]
+        last = r
+    dt = time.perf_counter() - t0
+    out = {"metric": "rllib_ppo_env_steps_per_sec", "value": round(steps / dt, 1), "unit": "env-steps/s",
+           "n_gpus": max(1, args.learners) if ngpu else 0, "iters": args.iters, "warmup": args.warmup,
+           "higher_is_better": True, "vs_baseline": None, "data": "SyntheticAtari (84x84x4 uint8, Discrete(6))",
+           "config": {"env_runners": runners, "envs_per_runner": args.envs_per_runner,
+                      "train_batch_size": args.train_batch, "minibatch": args.minibatch, "epochs": args.epochs,
+                      "learners": args.learners},
+           "extra": {"learner_time_s": last["info"]["learner"]["default_policy"].get("learner_time_s"),
+                     "iter_time_s": dt / max(1, args.iters)}}
+    print(json.dumps(out), flush=True)
+    algo.stop()
+    ray.shutdown()
+
+
+if __name__ == "__main__":
+    main()

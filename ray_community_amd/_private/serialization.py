@@ -98,8 +98,17 @@ def _reduce_cpu_tensor(t):
 
 
 def _rebuild_gpu_tensor(rebuild_fn, args):
+    import torch
+
     try:
-        return rebuild_fn(*args)
+        # the HIP context must exist (and be current on the storage's device) before the IPC open
+        torch.cuda.init()
+        dev = args[6] if len(args) > 6 and isinstance(args[6], int) else torch.cuda.current_device()
+        if dev >= torch.cuda.device_count():
+            dev = torch.cuda.current_device()
+        with torch.cuda.device(dev):
+            torch.cuda.current_stream().synchronize()
+            return rebuild_fn(*args)
     except Exception as e:  # pragma: no cover - depends on device visibility
         raise RuntimeError(f"could not map GPU object into this process (HIP IPC): {e}") from e
 

@@ -1,0 +1,7 @@
+from .algorithm import Algorithm
+from .algorithm_config import AlgorithmConfig
+from .dqn import DQN, DQNConfig
+from .ppo import PPO, PPOConfig
+from .registry import ALGORITHMS, get_algorithm_class
+
+__all__ = ["Algorithm", "AlgorithmConfig", "PPO", "PPOConfig", "DQN", "DQNConfig", "get_algorithm_class", "ALGORITHMS"]

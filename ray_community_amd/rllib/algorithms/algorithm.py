@@ -1,0 +1,256 @@
+"""Algorithm base (reference: ``rllib/algorithms/algorithm.py``). An Algorithm is also a Tune
+class trainable (``step() -> train()``)."""
+from __future__ import annotations
+
+import json
+import os
+import pickle
+import time
+from collections import deque
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ...tune.tuner import Trainable
+from ..env.env_runner import EnvRunner
+from ..policy.sample_batch import SampleBatch, concat_samples
+from .algorithm_config import AlgorithmConfig
+
+
+class Algorithm(Trainable):
+    _default_config_cls = AlgorithmConfig
+
+    def __init__(self, config: Optional[AlgorithmConfig] = None, env=None, **kw):
+        if isinstance(config, dict):
+            config = self._default_config_cls().update_from_dict(config)
+        self.config = config or self._default_config_cls()
+        if env is not None:
+            self.config.env = env
+        self._iteration = 0
+        self._timesteps_total = 0
+        self._episodes_total = 0
+        self._weights_version = 0
+        self._recent = deque(maxlen=self.config.metrics_num_episodes_for_smoothing)
+        self.setup(self.config)
+
+    # Tune class-trainable path: Trainable.__init__ is bypassed (config already built)
+    def setup(self, config):
+        from ..._private import worker as w
+
+        if not w.is_initialized():
+            w.init()
+        if isinstance(config, dict):
+            self.config = self._default_config_cls().update_from_dict(config)
+        cfg = self.config
+        rd = cfg.runner_dict()
+        rd.update(self._runner_extra())
+        self.local_runner = EnvRunner(rd, 0)
+        self.obs_space, self.act_space = self.local_runner.spaces()
+        self.remote_runners = []
+        if cfg.num_env_runners > 0:
+            from ...actor import ActorClass
+
+            cls = ActorClass(EnvRunner, {"num_cpus": cfg.num_cpus_per_env_runner})
+            self.remote_runners = [cls.remote(rd, i + 1) for i in range(cfg.num_env_runners)]
+        from ..core.learner import LearnerGroup
+
+        ld = cfg.to_dict()
+        ld.update(self._runner_extra())
+        self.learner_group = LearnerGroup(ld, self.obs_space, self.act_space)
+        self._sync_weights()
+
+    def _runner_extra(self):
+        return {}
+
+    # ------------------------------------------------------------------ rollouts
+    def _sync_weights(self):
+        from ..._private.worker import get, put
+
+        st = self.learner_group.get_weights()
+        self._weights_version += 1
+        self.local_runner.set_weights(st, self._weights_version)
+        if self.remote_runners:
+            ref = put(st)
+            get([r.set_weights.remote(ref, self._weights_version) for r in self.remote_runners])
+
+    def _sample(self, steps_total: int) -> SampleBatch:
+        from ..._private.worker import get
+
+        if self.remote_runners:
+            per = max(1, steps_total // len(self.remote_runners))
+            batches = get([r.sample.remote(per) for r in self.remote_runners])
+        else:
+            batches = [self.local_runner.sample(steps_total)]
+        return concat_samples(batches)
+
+    def _collect_metrics(self):
+        from ..._private.worker import get
+
+        ms = [self.local_runner.get_metrics()]
+        if self.remote_runners:
+            ms += get([r.get_metrics.remote() for r in self.remote_runners])
+        eps = [e for m in ms for e in m["episodes"]]
+        for e in eps:
+            self._recent.append(e)
+        self._episodes_total += len(eps)
+        return eps
+
+    # ------------------------------------------------------------------ API
+    def training_step(self) -> Dict:
+        raise NotImplementedError
+
+    def step(self):
+        return self.train()
+
+    def train(self) -> Dict:
+        t0 = time.perf_counter()
+        info = self.training_step()
+        eps = self._collect_metrics()
+        self._iteration += 1
+        rets = [e[0] for e in self._recent]
+        lens = [e[1] for e in self._recent]
+        dt = time.perf_counter() - t0
+        res = {
+            "training_iteration": self._iteration,
+            "episode_reward_mean": float(np.mean(rets)) if rets else float("nan"),
+            "episode_reward_max": float(np.max(rets)) if rets else float("nan"),
+            "episode_reward_min": float(np.min(rets)) if rets else float("nan"),
+            "episode_len_mean": float(np.mean(lens)) if lens else float("nan"),
+            "episodes_this_iter": len(eps),
+            "episodes_total": self._episodes_total,
+            "timesteps_total": self._timesteps_total,
+            "num_env_steps_sampled": self._timesteps_total,
+            "num_env_steps_sampled_this_iter": info.pop("_steps_this_iter", 0),
+            "time_this_iter_s": dt,
+            "info": {"learner": {"default_policy": info}},
+        }
+        res["env_steps_per_sec"] = res["num_env_steps_sampled_this_iter"] / dt if dt > 0 else 0.0
+        res["env_runners"] = {"episode_return_mean": res["episode_reward_mean"],
+                              "episode_return_max": res["episode_reward_max"],
+                              "episode_return_min": res["episode_reward_min"],
+                              "episode_len_mean": res["episode_len_mean"],
+                              "num_episodes": len(eps)}
+        iv = self.config.evaluation_interval
+        if iv and self._iteration % iv == 0:
+            res["evaluation"] = self.evaluate()
+        return res
+
+    def evaluate(self) -> Dict:
+        cfg = self.config
+        rd = cfg.runner_dict()
+        rd.update(self._runner_extra())
+        rd.update(cfg.evaluation_config or {})
+        rd["seed"] = (cfg.seed or 0) + 99991
+        if not hasattr(self, "_eval_runner"):
+            self._eval_runner = EnvRunner(rd, 10_000)
+        self._eval_runner.set_weights(self.learner_group.get_weights(), self._weights_version)
+        self._eval_runner.get_metrics()
+        eps = []
+        guard = 0
+        while len(eps) < cfg.evaluation_duration and guard < 10000:
+            self._eval_runner.sample(self._eval_runner.N * 64, explore=False)
+            eps += self._eval_runner.get_metrics()["episodes"]
+            guard += 1
+        rets = [e[0] for e in eps]
+        return {"episode_reward_mean": float(np.mean(rets)) if rets else float("nan"),
+                "env_runners": {"episode_return_mean": float(np.mean(rets)) if rets else float("nan")},
+                "num_episodes": len(eps)}
+
+    def compute_single_action(self, observation, explore: bool = False, **kw):
+        obs = torch.as_tensor(np.asarray(observation)[None])
+        m = self.local_runner.module
+        m.set_state(self.learner_group.get_weights())
+        if explore:
+            a, _, _, _ = m.forward_exploration(obs)
+        else:
+            a, _ = m.forward_inference(obs)
+        a = a[0].numpy()
+        return int(a) if a.ndim == 0 else a
+
+    def get_module(self):
+        m = self.local_runner.module
+        m.set_state(self.learner_group.get_weights())
+        return m
+
+    def get_weights(self):
+        return self.learner_group.get_weights()
+
+    def set_weights(self, w):
+        self.learner_group.call("set_weights", w)
+        self._sync_weights()
+
+    def save_checkpoint(self, checkpoint_dir: str):
+        os.makedirs(checkpoint_dir, exist_ok=True)
+        st = {"learner": self.learner_group.call("get_state"), "iteration": self._iteration,
+              "timesteps_total": self._timesteps_total, "config": self.config.to_dict(),
+              "extra": self._extra_state()}
+        with open(os.path.join(checkpoint_dir, "algorithm_state.pkl"), "wb") as f:
+            pickle.dump(st, f)
+        with open(os.path.join(checkpoint_dir, "rllib_checkpoint.json"), "w") as f:
+            json.dump({"type": "Algorithm", "algo": type(self).__name__, "format": "rca-1"}, f)
+        return checkpoint_dir
+
+    def load_checkpoint(self, checkpoint):
+        path = checkpoint if isinstance(checkpoint, str) else getattr(checkpoint, "path", checkpoint)
+        with open(os.path.join(path, "algorithm_state.pkl"), "rb") as f:
+            st = pickle.load(f)
+        self.learner_group.call("set_state", st["learner"])
+        self._iteration = st["iteration"]
+        self._timesteps_total = st["timesteps_total"]
+        self._load_extra_state(st.get("extra") or {})
+        self._sync_weights()
+
+    def _extra_state(self):
+        return {}
+
+    def _load_extra_state(self, st):
+        pass
+
+    def save(self, checkpoint_dir: Optional[str] = None):
+        from ...train._checkpoint import Checkpoint
+
+        d = checkpoint_dir or os.path.join(os.path.expanduser("~/rca_results"), "rllib", f"{type(self).__name__}_"
+                                           f"{int(time.time())}", f"checkpoint_{self._iteration:06d}")
+        self.save_checkpoint(d)
+        return _SaveResult(Checkpoint.from_directory(d))
+
+    def restore(self, checkpoint):
+        self.load_checkpoint(checkpoint)
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint):
+        path = checkpoint if isinstance(checkpoint, str) else checkpoint.path
+        with open(os.path.join(path, "algorithm_state.pkl"), "rb") as f:
+            st = pickle.load(f)
+        algo = cls(config=cls._default_config_cls().update_from_dict(st["config"]))
+        algo.load_checkpoint(path)
+        return algo
+
+    def stop(self):
+        from ..._private.worker import kill
+
+        for r in self.remote_runners:
+            try:
+                kill(r)
+            except Exception:
+                pass
+        self.remote_runners = []
+        self.learner_group.shutdown()
+
+    cleanup = stop
+
+    @property
+    def iteration(self):
+        return self._iteration
+
+
+class _SaveResult:
+    def __init__(self, checkpoint):
+        self.checkpoint = checkpoint
+
+    def __fspath__(self):
+        return self.checkpoint.path
+
+    def __str__(self):
+        return self.checkpoint.path

@@ -1,0 +1,190 @@
+"""AlgorithmConfig builder (reference: ``rllib/algorithms/algorithm_config.py``)."""
+from __future__ import annotations
+
+import copy
+from typing import Any, Dict, Optional
+
+
+class AlgorithmConfig:
+    algo_class = None
+
+    def __init__(self, algo_class=None):
+        if algo_class is not None:
+            self.algo_class = algo_class
+        # environment
+        self.env = None
+        self.env_config: Dict = {}
+        self.observation_space = None
+        self.action_space = None
+        # env runners
+        self.num_env_runners = 0
+        self.num_envs_per_env_runner = 1
+        self.rollout_fragment_length: Any = "auto"
+        self.batch_mode = "truncate_episodes"
+        self.num_cpus_per_env_runner = 1
+        self.explore = True
+        # training
+        self.gamma = 0.99
+        self.lr = 0.001
+        self.lr_schedule = None
+        self.grad_clip = None
+        self.train_batch_size = 4000
+        self.model: Dict = {"fcnet_hiddens": [256, 256], "fcnet_activation": "tanh", "vf_share_layers": False}
+        # resources / learners
+        self.num_gpus = 0
+        self.num_learners = 0
+        self.num_gpus_per_learner = 0
+        self.framework_str = "torch"
+        # evaluation
+        self.evaluation_interval = None
+        self.evaluation_duration = 10
+        self.evaluation_duration_unit = "episodes"
+        self.evaluation_num_env_runners = 0
+        self.evaluation_config: Dict = {}
+        # misc
+        self.seed = None
+        self.metrics_num_episodes_for_smoothing = 100
+        self.min_sample_timesteps_per_iteration = 0
+
+    # ------------------------------------------------------------------ builder methods
+    def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None, **kw):
+        if env is not None:
+            self.env = env
+        if env_config is not None:
+            self.env_config = dict(env_config)
+        self.observation_space = observation_space or self.observation_space
+        self.action_space = action_space or self.action_space
+        return self
+
+    def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None, rollout_fragment_length=None,
+                    batch_mode=None, num_cpus_per_env_runner=None, explore=None, **kw):
+        for k, v in dict(num_env_runners=num_env_runners, num_envs_per_env_runner=num_envs_per_env_runner,
+                         rollout_fragment_length=rollout_fragment_length, batch_mode=batch_mode,
+                         num_cpus_per_env_runner=num_cpus_per_env_runner, explore=explore).items():
+            if v is not None:
+                setattr(self, k, v)
+        return self
+
+    def rollouts(self, *, num_rollout_workers=None, num_envs_per_worker=None, rollout_fragment_length=None,
+                 batch_mode=None, **kw):
+        return self.env_runners(num_env_runners=num_rollout_workers, num_envs_per_env_runner=num_envs_per_worker,
+                                rollout_fragment_length=rollout_fragment_length, batch_mode=batch_mode)
+
+    def training(self, **kw):
+        aliases = {"sgd_minibatch_size": "minibatch_size", "num_sgd_iter": "num_epochs", "lambda": "lambda_"}
+        for k, v in kw.items():
+            k = aliases.get(k, k)
+            if k == "model" and v is not None:
+                m = dict(self.model)
+                m.update(v)
+                self.model = m
+                continue
+            setattr(self, k, v)
+        return self
+
+    def resources(self, *, num_gpus=None, num_cpus_for_main_process=None, **kw):
+        if num_gpus is not None:
+            self.num_gpus = num_gpus
+        return self
+
+    def learners(self, *, num_learners=None, num_gpus_per_learner=None, **kw):
+        if num_learners is not None:
+            self.num_learners = num_learners
+        if num_gpus_per_learner is not None:
+            self.num_gpus_per_learner = num_gpus_per_learner
+        return self
+
+    def framework(self, framework="torch", **kw):
+        if framework not in ("torch", None):
+            raise ValueError("only the torch framework is supported on MI355X")
+        self.framework_str = "torch"
+        return self
+
+    def evaluation(self, *, evaluation_interval=None, evaluation_duration=None, evaluation_duration_unit=None,
+                   evaluation_num_env_runners=None, evaluation_config=None, **kw):
+        for k, v in dict(evaluation_interval=evaluation_interval, evaluation_duration=evaluation_duration,
+                         evaluation_duration_unit=evaluation_duration_unit,
+                         evaluation_num_env_runners=evaluation_num_env_runners,
+                         evaluation_config=evaluation_config).items():
+            if v is not None:
+                setattr(self, k, v)
+        return self
+
+    def debugging(self, *, seed=None, **kw):
+        if seed is not None:
+            self.seed = seed
+        return self
+
+    def reporting(self, *, metrics_num_episodes_for_smoothing=None, min_sample_timesteps_per_iteration=None, **kw):
+        if metrics_num_episodes_for_smoothing is not None:
+            self.metrics_num_episodes_for_smoothing = metrics_num_episodes_for_smoothing
+        if min_sample_timesteps_per_iteration is not None:
+            self.min_sample_timesteps_per_iteration = min_sample_timesteps_per_iteration
+        return self
+
+    def rl_module(self, *, model_config=None, model_config_dict=None, **kw):
+        m = model_config or model_config_dict
+        if m:
+            self.model = {**self.model, **dict(m)}
+        return self
+
+    def api_stack(self, **kw):
+        return self
+
+    def multi_agent(self, **kw):
+        if kw.get("policies") and len(kw["policies"]) > 1:
+            raise NotImplementedError("multi-agent training is not supported yet")
+        return self
+
+    def offline_data(self, **kw):
+        return self
+
+    def callbacks(self, cb=None, **kw):
+        self._callbacks = cb
+        return self
+
+    # ------------------------------------------------------------------ misc
+    def copy(self, copy_frozen=None):
+        return copy.deepcopy(self)
+
+    def to_dict(self) -> Dict:
+        d = {k: v for k, v in self.__dict__.items() if not k.startswith("_")}
+        d["framework"] = self.framework_str
+        return d
+
+    def update_from_dict(self, d: Dict):
+        for k, v in d.items():
+            if k == "framework":
+                continue
+            if k == "lambda":
+                k = "lambda_"
+            setattr(self, k, v)
+        return self
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls().update_from_dict(d)
+
+    def get_rollout_fragment_length(self):
+        if self.rollout_fragment_length == "auto":
+            n = max(1, self.num_env_runners) * self.num_envs_per_env_runner
+            return max(1, self.train_batch_size // n)
+        return int(self.rollout_fragment_length)
+
+    def build(self, env=None, logger_creator=None, use_copy=True):
+        if env is not None:
+            self.env = env
+        return self.algo_class(config=self.copy() if use_copy else self)
+
+    build_algo = build
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+    def get(self, k, default=None):
+        return getattr(self, k, default)
+
+    def runner_dict(self) -> Dict:
+        d = self.to_dict()
+        d["rollout_fragment_length"] = self.get_rollout_fragment_length()
+        return d

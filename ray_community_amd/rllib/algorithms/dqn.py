@@ -1,0 +1,83 @@
+"""DQN (reference: ``rllib/algorithms/dqn``): double-Q, target network, epsilon-greedy,
+uniform replay."""
+from __future__ import annotations
+
+from typing import Dict
+
+import numpy as np
+
+from ..policy.sample_batch import SampleBatch, concat_samples
+from ..utils.replay_buffers import ReplayBuffer
+from .algorithm import Algorithm
+from .algorithm_config import AlgorithmConfig
+
+
+class DQNConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class=algo_class or DQN)
+        self.lr = 5e-4
+        self.train_batch_size = 32
+        self.replay_buffer_config = {"capacity": 50000}
+        self.target_network_update_freq = 500
+        self.num_steps_sampled_before_learning_starts = 1000
+        self.double_q = True
+        self.n_step = 1
+        self.epsilon = [(0, 1.0), (10000, 0.05)]
+        self.training_intensity = None
+        self.rollout_fragment_length = 4
+        self.td_error_loss_fn = "huber"
+        self.model = {"fcnet_hiddens": [256, 256], "fcnet_activation": "relu", "vf_share_layers": True}
+
+
+class DQN(Algorithm):
+    _default_config_cls = DQNConfig
+
+    @classmethod
+    def get_default_config(cls):
+        return DQNConfig()
+
+    def _runner_extra(self):
+        return {"q_head": True}
+
+    def setup(self, config):
+        super().setup(config)
+        self.buffer = ReplayBuffer(self.config.replay_buffer_config.get("capacity", 50000), seed=self.config.seed)
+        self._last_target = 0
+
+    def _epsilon(self):
+        sched = self.config.epsilon
+        t = self._timesteps_total
+        for (t0, v0), (t1, v1) in zip(sched, sched[1:]):
+            if t0 <= t < t1:
+                return v0 + (v1 - v0) * (t - t0) / (t1 - t0)
+        return sched[-1][1]
+
+    def training_step(self) -> Dict:
+        from ..._private.worker import get
+
+        cfg = self.config
+        eps = self._epsilon()
+        steps = max(1, cfg.get_rollout_fragment_length()) * self.local_runner.N
+        if self.remote_runners:
+            batches = get([r.sample_transitions.remote(steps, eps) for r in self.remote_runners])
+        else:
+            batches = [self.local_runner.sample_transitions(steps, eps)]
+        b = concat_samples(batches)
+        self.buffer.add(b)
+        n = b.count
+        self._timesteps_total += n
+        info = {"epsilon": eps}
+        if self._timesteps_total >= cfg.num_steps_sampled_before_learning_starts:
+            k = 1
+            if cfg.training_intensity:
+                k = max(1, int(round(cfg.training_intensity * n / cfg.train_batch_size)))
+            for _ in range(k):
+                mb = self.buffer.sample(cfg.train_batch_size)
+                mb.pop("batch_indexes", None)
+                info.update(self.learner_group.update("dqn", mb))
+            if self._timesteps_total - self._last_target >= cfg.target_network_update_freq:
+                self.learner_group.call("sync_target")
+                self._last_target = self._timesteps_total
+            self._sync_weights()
+        info["_steps_this_iter"] = n
+        return info

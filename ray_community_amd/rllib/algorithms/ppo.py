@@ -1,0 +1,53 @@
+"""PPO (reference: ``rllib/algorithms/ppo/ppo.py``, ``ppo_torch_learner.py``)."""
+from __future__ import annotations
+
+from typing import Dict
+
+from .algorithm import Algorithm
+from .algorithm_config import AlgorithmConfig
+
+
+class PPOConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class=algo_class or PPO)
+        self.lr = 5e-5
+        self.lambda_ = 1.0
+        self.use_gae = True
+        self.use_critic = True
+        self.kl_coeff = 0.2
+        self.kl_target = 0.01
+        self.use_kl_loss = True
+        self.clip_param = 0.3
+        self.vf_clip_param = 10.0
+        self.vf_loss_coeff = 1.0
+        self.entropy_coeff = 0.0
+        self.train_batch_size = 4000
+        self.minibatch_size = 128
+        self.num_epochs = 30
+        self.grad_clip = None
+
+    @property
+    def sgd_minibatch_size(self):
+        return self.minibatch_size
+
+    @property
+    def num_sgd_iter(self):
+        return self.num_epochs
+
+
+class PPO(Algorithm):
+    _default_config_cls = PPOConfig
+
+    @classmethod
+    def get_default_config(cls):
+        return PPOConfig()
+
+    def training_step(self) -> Dict:
+        cfg = self.config
+        batch = self._sample(cfg.train_batch_size)
+        n = batch.count
+        self._timesteps_total += n
+        info = self.learner_group.update("ppo", batch)
+        self._sync_weights()
+        info["_steps_this_iter"] = n
+        return info

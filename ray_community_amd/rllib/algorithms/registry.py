@@ -1,0 +1,33 @@
+"""Algorithm registry (reference: ``rllib/algorithms/registry.py``)."""
+
+
+def _ppo():
+    from .ppo import PPO, PPOConfig
+
+    return PPO, PPOConfig()
+
+
+def _dqn():
+    from .dqn import DQN, DQNConfig
+
+    return DQN, DQNConfig()
+
+
+def _impala():
+    from .impala import IMPALA, IMPALAConfig
+
+    return IMPALA, IMPALAConfig()
+
+
+def _appo():
+    from .impala import APPO, APPOConfig
+
+    return APPO, APPOConfig()
+
+
+ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo}
+
+
+def get_algorithm_class(name: str, return_config: bool = False):
+    cls, cfg = ALGORITHMS[name]()
+    return (cls, cfg) if return_config else cls

@@ -1,0 +1,280 @@
+"""Learners and LearnerGroup (reference: ``rllib/core/learner/{learner,learner_group}.py``).
+
+A learner owns the RLModule on its GPU. Its update keeps the whole train batch resident in HBM:
+one host->device copy, GAE + advantage standardisation as HIP kernels over the env-major
+``[N, T]`` fragments, then the minibatch SGD epochs by device-side index permutation.
+With ``num_learners > 1`` every learner is a GPU actor in one RCCL process group and gradients
+are all-reduced by the framework's bucketed DDP; the batch is split along the env axis.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ... import ops
+from ..policy.sample_batch import SampleBatch
+from .rl_module import RLModule
+
+
+def _device(use_gpu: bool):
+    if use_gpu and torch.cuda.is_available():
+        idx = os.environ.get("RCA_TRAIN_DEVICE_INDEX")
+        return torch.device("cuda", int(idx) if idx is not None else torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class Learner:
+    def __init__(self, config: Dict, obs_space, act_space, use_gpu: bool = False):
+        self.cfg = config
+        self.device = _device(use_gpu)
+        seed = config.get("seed")
+        if seed is not None:
+            torch.manual_seed(int(seed))
+        self.module = RLModule(obs_space, act_space, config.get("model"), q_head=config.get("q_head", False)).to(
+            self.device)
+        self.ddp = None
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            from ...parallel import DistributedDataParallel
+
+            self.ddp = DistributedDataParallel(self.module, bucket_cap_mb=64, average_in_optimizer=False,
+                                               auto_finalize=True)
+        self.opt = torch.optim.Adam(self.module.parameters(), lr=config.get("lr", 5e-5),
+                                    eps=config.get("adam_epsilon", 1e-8))
+        self.kl_coeff = config.get("kl_coeff", 0.2)
+        self.target = None
+        self.num_updates = 0
+
+    def forward(self, obs):
+        return (self.ddp or self.module)(obs)
+
+    def get_weights(self):
+        return self.module.get_state()
+
+    def set_weights(self, state):
+        self.module.set_state(state)
+
+    def get_state(self):
+        return {"module": self.module.get_state(), "opt": self.opt.state_dict(), "kl_coeff": self.kl_coeff}
+
+    def set_state(self, st):
+        self.module.set_state(st["module"])
+        self.opt.load_state_dict(st["opt"])
+        self.kl_coeff = st.get("kl_coeff", self.kl_coeff)
+
+    def _lr(self):
+        sched = self.cfg.get("lr_schedule")
+        if not sched:
+            return self.cfg.get("lr", 5e-5)
+        t = self.num_updates
+        pts = sorted(sched)
+        for (t0, v0), (t1, v1) in zip(pts, pts[1:]):
+            if t0 <= t < t1:
+                return v0 + (v1 - v0) * (t - t0) / (t1 - t0)
+        return pts[-1][1]
+
+    def _step(self, loss):
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        gc = self.cfg.get("grad_clip")
+        gn = None
+        if gc:
+            gn = torch.nn.utils.clip_grad_norm_(self.module.parameters(), gc)
+        for g in self.opt.param_groups:
+            g["lr"] = self._lr()
+        self.opt.step()
+        return gn
+
+    # ------------------------------------------------------------------ PPO
+    def update_ppo(self, batch: SampleBatch) -> Dict:
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        b = batch.to_device(self.device)
+        N, T = batch.fragment_shape
+        rew, vf, nvf = b["rewards"], b["vf_preds"], b["next_vf_preds"]
+        term, trunc = b["terminateds"], b["truncateds"]
+        done = term | trunc
+        gamma, lam = cfg.get("gamma", 0.99), cfg.get("lambda_", 1.0)
+        if cfg.get("use_gae", True):
+            adv, vt = ops.compute_gae(rew, vf, term, done, gamma, lam, next_values=nvf, standardize=False)
+        else:
+            adv, vt = ops.compute_gae(rew, torch.zeros_like(vf), term, done, gamma, 1.0,
+                                      next_values=torch.zeros_like(nvf))
+            adv = adv - vf
+        adv = adv.reshape(-1).contiguous()
+        vt = vt.reshape(-1)
+        ops.standardize_(adv)
+        obs = b["obs"].reshape((N * T,) + tuple(b["obs"].shape[2:]))
+        act = b["actions"].reshape((N * T,) + tuple(b["actions"].shape[2:]))
+        old_logp = b["action_logp"].reshape(-1)
+        old_vf = vf.reshape(-1)
+        old_logits = b["action_dist_inputs"].reshape(N * T, -1) if "action_dist_inputs" in b else None
+        n = N * T
+        mb = min(int(cfg.get("minibatch_size", 128)), n)
+        epochs = int(cfg.get("num_epochs", 30))
+        clip, vclip = cfg.get("clip_param", 0.3), cfg.get("vf_clip_param", 10.0)
+        vf_coeff, ent_coeff = cfg.get("vf_loss_coeff", 1.0), cfg.get("entropy_coeff", 0.0)
+        use_kl = cfg.get("use_kl_loss", True) and old_logits is not None
+        stats = {"policy_loss": 0.0, "vf_loss": 0.0, "entropy": 0.0, "mean_kl": 0.0, "total_loss": 0.0}
+        count = 0
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(1234 + self.num_updates)
+        for _ in range(epochs):
+            perm = torch.randperm(n, device=self.device, generator=gen)
+            for i in range(0, n - mb + 1, mb):
+                idx = perm[i: i + mb]
+                logits, v = self.forward(obs[idx])
+                d = self.module.dist(logits)
+                lp = d.logp(act[idx])
+                ratio = torch.exp(lp - old_logp[idx])
+                a_mb = adv[idx]
+                surr = torch.min(ratio * a_mb, ratio.clamp(1 - clip, 1 + clip) * a_mb)
+                vf_err = (v - vt[idx]) ** 2
+                vf_loss = vf_err.clamp(0, vclip) if vclip else vf_err
+                ent = d.entropy()
+                loss = -surr.mean() + vf_coeff * vf_loss.mean() - ent_coeff * ent.mean()
+                if use_kl:
+                    kl = self.module.dist(old_logits[idx]).kl(d).mean()
+                    if self.kl_coeff > 0:
+                        loss = loss + self.kl_coeff * kl
+                else:
+                    kl = torch.zeros((), device=self.device)
+                self._step(loss)
+                stats["policy_loss"] += -surr.mean().detach()
+                stats["vf_loss"] += vf_loss.mean().detach()
+                stats["entropy"] += ent.mean().detach()
+                stats["mean_kl"] += kl.detach()
+                stats["total_loss"] += loss.detach()
+                count += 1
+        out = {k: float(v) / max(count, 1) for k, v in stats.items()}
+        if use_kl:
+            kt = cfg.get("kl_target", 0.01)
+            if out["mean_kl"] > 2.0 * kt:
+                self.kl_coeff *= 1.5
+            elif out["mean_kl"] < 0.5 * kt:
+                self.kl_coeff *= 0.5
+        self.num_updates += 1
+        ev = 1 - torch.var(vt - old_vf) / (torch.var(vt) + 1e-8)
+        out.update({"kl_coeff": self.kl_coeff, "vf_explained_var": float(ev), "num_minibatches": count,
+                    "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr()})
+        return out
+
+    # ------------------------------------------------------------------ DQN
+    def update_dqn(self, batch: SampleBatch) -> Dict:
+        cfg = self.cfg
+        if self.target is None:
+            import copy
+
+            self.target = copy.deepcopy(self.module)
+        b = batch.to_device(self.device)
+        q = self.module.q_values(b["obs"])
+        qa = q.gather(1, b["actions"].long().unsqueeze(1)).squeeze(1)
+        with torch.no_grad():
+            qn_t = self.target.q_values(b["new_obs"])
+            if cfg.get("double_q", True):
+                an = self.module.q_values(b["new_obs"]).argmax(1, keepdim=True)
+                qn = qn_t.gather(1, an).squeeze(1)
+            else:
+                qn = qn_t.max(1).values
+            y = b["rewards"] + cfg.get("gamma", 0.99) ** cfg.get("n_step", 1) * (1 - b["terminateds"].float()) * qn
+        td = qa - y
+        loss = torch.nn.functional.huber_loss(qa, y, delta=1.0) if cfg.get("td_error_loss_fn", "huber") == "huber" \
+            else (td ** 2).mean()
+        self._step(loss)
+        self.num_updates += 1
+        return {"loss": loss.item(), "mean_q": qa.mean().item(), "mean_td_error": td.abs().mean().item()}
+
+    def sync_target(self):
+        if self.target is not None:
+            self.target.load_state_dict(self.module.state_dict())
+
+
+class _LearnerActor:
+    def __init__(self):
+        self.learner = None
+
+    def build(self, config, obs_space, act_space, use_gpu):
+        self.learner = Learner(config, obs_space, act_space, use_gpu)
+        return True
+
+    def update(self, kind, batch):
+        return self.learner.update_ppo(batch) if kind == "ppo" else self.learner.update_dqn(batch)
+
+    def call(self, name, *args):
+        return getattr(self.learner, name)(*args)
+
+
+class LearnerGroup:
+    """``num_learners == 0``: one local learner in the driver (on a GPU if the driver has one).
+    ``num_learners >= 1``: GPU learner actors in a placement group, one RCCL process group."""
+
+    def __init__(self, config: Dict, obs_space, act_space):
+        self.cfg = config
+        self.n = int(config.get("num_learners", 0))
+        gpus = float(config.get("num_gpus_per_learner", 0) or 0)
+        self.use_gpu = gpus > 0 or (self.n == 0 and config.get("num_gpus", 0) > 0)
+        if self.n == 0:
+            self.local = Learner(config, obs_space, act_space, self.use_gpu)
+            self.wg = None
+            return
+        from ...train._internal.worker_group import WorkerGroup
+        from ...train.torch.config import TorchConfig, _TorchBackend
+        from ...air.config import ScalingConfig
+        from ..._private.worker import get
+
+        res = {"CPU": 1, "GPU": gpus} if gpus else {"CPU": 1}
+        self.wg = WorkerGroup(self.n, res, "PACK", actor_cls=_LearnerActor)
+        sc = ScalingConfig(num_workers=self.n, use_gpu=gpus > 0, resources_per_worker=res)
+        _TorchBackend().on_start(self.wg, TorchConfig(), sc)
+        get([w.build.remote(config, obs_space, act_space, gpus > 0) for w in self.wg.workers])
+        self.local = None
+
+    def update(self, kind: str, batch: SampleBatch) -> Dict:
+        if self.local is not None:
+            return self.local.update_ppo(batch) if kind == "ppo" else self.local.update_dqn(batch)
+        from ..._private.worker import get
+
+        shards = _split(batch, self.n)
+        res = get([w.update.remote(kind, s) for w, s in zip(self.wg.workers, shards)])
+        out = {}
+        for k in res[0]:
+            vals = [r[k] for r in res if isinstance(r.get(k), (int, float))]
+            if vals:
+                out[k] = float(np.mean(vals))
+        return out
+
+    def call(self, name, *args):
+        if self.local is not None:
+            return getattr(self.local, name)(*args)
+        from ..._private.worker import get
+
+        return get([w.call.remote(name, *args) for w in self.wg.workers])[0]
+
+    def get_weights(self):
+        return self.call("get_weights")
+
+    def shutdown(self):
+        if self.wg is not None:
+            self.wg.shutdown()
+
+
+def _split(batch: SampleBatch, n: int) -> List[SampleBatch]:
+    if batch.fragment_shape is not None:
+        N, T = batch.fragment_shape
+        per = [N // n + (1 if i < N % n else 0) for i in range(n)]
+        outs, s = [], 0
+        for p in per:
+            sb = SampleBatch({k: v[s: s + p] for k, v in batch.items()})
+            sb.fragment_shape = (p, T)
+            outs.append(sb)
+            s += p
+        return outs
+    c = batch.count
+    per = math.ceil(c / n)
+    return [batch.slice(i * per, min(c, (i + 1) * per)) for i in range(n)]

@@ -1,0 +1,171 @@
+"""RLModule + catalog for torch (reference: ``rllib/core/rl_module/torch``, ``rllib/core/models``).
+
+Encoders: MLP for vector observations, Nature-CNN for 84x84 image stacks (uint8 HWC; the
+uint8 -> float NCHW conversion runs as the ``image_normalize`` HIP kernel on GPU). Heads:
+policy logits (Categorical) or mean/log-std (DiagGaussian), value head; optional Q head for DQN.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..utils.spaces import Box, Discrete
+
+
+class Categorical:
+    def __init__(self, logits):
+        self.logits = logits - logits.logsumexp(-1, keepdim=True)
+
+    def sample(self):
+        return torch.multinomial(self.logits.exp(), 1).squeeze(-1)
+
+    def deterministic_sample(self):
+        return self.logits.argmax(-1)
+
+    def logp(self, a):
+        return self.logits.gather(-1, a.long().unsqueeze(-1)).squeeze(-1)
+
+    def entropy(self):
+        p = self.logits.exp()
+        return -(p * self.logits).sum(-1)
+
+    def kl(self, other):
+        p = self.logits.exp()
+        return (p * (self.logits - other.logits)).sum(-1)
+
+
+class DiagGaussian:
+    def __init__(self, inputs):
+        self.mean, log_std = inputs.chunk(2, dim=-1)
+        self.log_std = log_std.clamp(-20, 2)
+        self.std = self.log_std.exp()
+
+    def sample(self):
+        return self.mean + self.std * torch.randn_like(self.mean)
+
+    def deterministic_sample(self):
+        return self.mean
+
+    def logp(self, a):
+        return (-0.5 * ((a - self.mean) / self.std) ** 2 - self.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+
+    def entropy(self):
+        return (self.log_std + 0.5 * math.log(2 * math.pi * math.e)).sum(-1)
+
+    def kl(self, other):
+        return (other.log_std - self.log_std + (self.std ** 2 + (self.mean - other.mean) ** 2) /
+                (2.0 * other.std ** 2) - 0.5).sum(-1)
+
+
+def _act(name):
+    return {"tanh": nn.Tanh, "relu": nn.ReLU, "swish": nn.SiLU, "silu": nn.SiLU, "linear": nn.Identity,
+            "elu": nn.ELU}[name]
+
+
+def _mlp(inp, hiddens, act):
+    layers = []
+    d = inp
+    for h in hiddens:
+        layers += [nn.Linear(d, h), _act(act)()]
+        d = h
+    return nn.Sequential(*layers), d
+
+
+class NatureCNN(nn.Module):
+    def __init__(self, in_ch, out_dim=512):
+        super().__init__()
+        self.net = nn.Sequential(nn.Conv2d(in_ch, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
+                                 nn.Conv2d(64, 64, 3, 1), nn.ReLU(), nn.Flatten(), nn.Linear(64 * 7 * 7, out_dim),
+                                 nn.ReLU())
+        self.out_dim = out_dim
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def preprocess_obs(obs: torch.Tensor) -> torch.Tensor:
+    """uint8 [B, H, W, C] frames -> float [B, C, H, W] / 255 (one HIP kernel on GPU)."""
+    if obs.dtype == torch.uint8 and obs.dim() == 4:
+        if obs.is_cuda:
+            from ...ops import image_normalize
+
+            C = obs.shape[-1]
+            return image_normalize(obs, mean=(0.0,) * C, std=(1.0,) * C, dtype=torch.float32)
+        return obs.permute(0, 3, 1, 2).float().div_(255.0)
+    return obs.float()
+
+
+class RLModule(nn.Module):
+    """Actor-critic module used by PPO/IMPALA/APPO (and DQN via ``q_head``)."""
+
+    def __init__(self, observation_space, action_space, model_config: Optional[Dict] = None, q_head=False):
+        super().__init__()
+        cfg = dict(model_config or {})
+        self.obs_space = observation_space
+        self.act_space = action_space
+        hiddens = cfg.get("fcnet_hiddens", [256, 256])
+        act = cfg.get("fcnet_activation", "tanh")
+        self.vf_share = cfg.get("vf_share_layers", False)
+        self.is_image = len(observation_space.shape) == 3
+        if isinstance(action_space, Discrete):
+            self.n_out = action_space.n
+            self.dist_cls = Categorical
+        else:
+            self.n_out = 2 * int(np.prod(action_space.shape))
+            self.dist_cls = DiagGaussian
+        if self.is_image:
+            self.encoder = NatureCNN(observation_space.shape[-1], cfg.get("conv_out", 512))
+            feat = self.encoder.out_dim
+            self.vf_encoder = None
+            self.vf_share = True
+        else:
+            inp = int(np.prod(observation_space.shape))
+            self.encoder, feat = _mlp(inp, hiddens, act)
+            self.vf_encoder = None if self.vf_share else _mlp(inp, hiddens, act)[0]
+        self.pi = nn.Linear(feat, self.n_out)
+        self.vf = nn.Linear(feat, 1)
+        self.q_head = nn.Linear(feat, self.n_out) if q_head else None
+        nn.init.orthogonal_(self.pi.weight, 0.01)
+        nn.init.zeros_(self.pi.bias)
+
+    def _x(self, obs):
+        x = preprocess_obs(obs)
+        return x if self.is_image else x.reshape(x.shape[0], -1)
+
+    def forward(self, obs):
+        x = self._x(obs)
+        h = self.encoder(x)
+        logits = self.pi(h)
+        hv = h if self.vf_encoder is None else self.vf_encoder(x)
+        v = self.vf(hv).squeeze(-1)
+        return logits, v
+
+    def q_values(self, obs):
+        h = self.encoder(self._x(obs))
+        return self.q_head(h)
+
+    def dist(self, logits):
+        return self.dist_cls(logits)
+
+    @torch.no_grad()
+    def forward_inference(self, obs):
+        logits, v = self.forward(obs)
+        return self.dist(logits).deterministic_sample(), v
+
+    @torch.no_grad()
+    def forward_exploration(self, obs):
+        logits, v = self.forward(obs)
+        d = self.dist(logits)
+        a = d.sample()
+        return a, d.logp(a), v, logits
+
+    def get_state(self):
+        return {k: v.detach().cpu() for k, v in self.state_dict().items()}
+
+    def set_state(self, state):
+        self.load_state_dict(state)

@@ -1,0 +1,162 @@
+"""Env runners (reference: ``rllib/env/single_agent_env_runner.py``, ``evaluation/rollout_worker.py``).
+
+Each runner owns a natively vectorised env (N sub-envs stepped as one numpy batch) and a CPU
+copy of the RLModule; it returns rollout fragments as env-major ``[N, T]`` column blocks with
+the value bootstraps needed for exact GAE under auto-reset and truncation (``next_vf_preds``).
+"""
+from __future__ import annotations
+
+import collections
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..core.rl_module import RLModule
+from ..policy.sample_batch import SampleBatch
+from .envs import make_vector_env
+
+
+class EnvRunner:
+    def __init__(self, config: Dict, worker_index: int = 0):
+        torch.set_num_threads(int(config.get("num_cpus_per_env_runner_threads", 1)))
+        self.cfg = config
+        self.worker_index = worker_index
+        seed = config.get("seed")
+        self.seed = None if seed is None else int(seed) + 1000 * worker_index
+        if self.seed is not None:
+            torch.manual_seed(self.seed)
+        self.env = make_vector_env(config["env"], config.get("num_envs_per_env_runner", 1), config.get("env_config"),
+                                   seed=self.seed)
+        self.N = self.env.num_envs
+        self.module = RLModule(self.env.observation_space, self.env.action_space, config.get("model"),
+                               q_head=config.get("q_head", False))
+        self.module.eval()
+        self.obs, _ = self.env.reset(seed=self.seed)
+        self.ep_ret = np.zeros(self.N)
+        self.ep_len = np.zeros(self.N, dtype=np.int64)
+        self.completed = collections.deque(maxlen=int(config.get("metrics_num_episodes_for_smoothing", 100)))
+        self.new_episodes = []
+        self.steps_sampled = 0
+        self.weights_version = -1
+        self._rng = np.random.default_rng(self.seed)
+
+    def spaces(self):
+        return self.env.observation_space, self.env.action_space
+
+    def set_weights(self, state, version: int = 0):
+        if version != self.weights_version:
+            self.module.set_state(state)
+            self.weights_version = version
+        return True
+
+    def get_weights(self):
+        return self.module.get_state()
+
+    def _track(self, rew, term, trunc):
+        self.ep_ret += rew
+        self.ep_len += 1
+        done = term | trunc
+        if done.any():
+            for i in np.nonzero(done)[0]:
+                ep = (float(self.ep_ret[i]), int(self.ep_len[i]))
+                self.completed.append(ep)
+                self.new_episodes.append(ep)
+            self.ep_ret[done] = 0
+            self.ep_len[done] = 0
+
+    @torch.no_grad()
+    def sample(self, num_steps: Optional[int] = None, explore: bool = True) -> SampleBatch:
+        """On-policy fragment of T = num_steps // N steps per sub-env (PPO / IMPALA)."""
+        T = max(1, int(num_steps or self.cfg.get("rollout_fragment_length", 64) * self.N) // self.N)
+        N = self.N
+        obs_buf = np.empty((N, T) + self.obs.shape[1:], dtype=self.obs.dtype)
+        act_shape = () if self.module.dist_cls.__name__ == "Categorical" else self.env.action_space.shape
+        acts = np.empty((N, T) + tuple(act_shape), dtype=np.int64 if act_shape == () else np.float32)
+        logp = np.empty((N, T), dtype=np.float32)
+        vf = np.empty((N, T), dtype=np.float32)
+        rew = np.empty((N, T), dtype=np.float32)
+        term = np.empty((N, T), dtype=bool)
+        trunc = np.empty((N, T), dtype=bool)
+        logits_buf = None
+        trunc_fix = []  # (t, env indices, final obs)
+        for t in range(T):
+            o = torch.from_numpy(self.obs)
+            if explore:
+                a, lp, v, logits = self.module.forward_exploration(o)
+            else:
+                a, v = self.module.forward_inference(o)
+                lp = torch.zeros(N)
+                logits = None
+            if logits is not None:
+                if logits_buf is None:
+                    logits_buf = np.empty((N, T, logits.shape[-1]), dtype=np.float32)
+                logits_buf[:, t] = logits.numpy()
+            obs_buf[:, t] = self.obs
+            an = a.numpy()
+            acts[:, t] = an
+            logp[:, t] = lp.numpy()
+            vf[:, t] = v.numpy()
+            nobs, r, te, tr, info = self.env.step(an)
+            rew[:, t] = r
+            term[:, t] = te
+            trunc[:, t] = tr
+            if tr.any():
+                idx = np.nonzero(tr)[0]
+                trunc_fix.append((t, idx, info["final_obs"][idx]))
+            self._track(r, te, tr)
+            self.obs = nobs
+        last_v = self.module.forward(torch.from_numpy(self.obs))[1].numpy()
+        next_vf = np.empty_like(vf)
+        next_vf[:, :-1] = vf[:, 1:]
+        next_vf[:, -1] = last_v
+        if trunc_fix:
+            fo = np.concatenate([x[2] for x in trunc_fix], axis=0)
+            fv = self.module.forward(torch.from_numpy(fo))[1].numpy()
+            k = 0
+            for t, idx, _ in trunc_fix:
+                next_vf[idx, t] = fv[k: k + len(idx)]
+                k += len(idx)
+        self.steps_sampled += N * T
+        b = SampleBatch({SampleBatch.OBS: obs_buf, SampleBatch.ACTIONS: acts, SampleBatch.ACTION_LOGP: logp,
+                         SampleBatch.VF_PREDS: vf, SampleBatch.REWARDS: rew, SampleBatch.TERMINATEDS: term,
+                         SampleBatch.TRUNCATEDS: trunc, SampleBatch.NEXT_VF_PREDS: next_vf})
+        if logits_buf is not None:
+            b[SampleBatch.ACTION_DIST_INPUTS] = logits_buf
+        b.fragment_shape = (N, T)
+        return b
+
+    @torch.no_grad()
+    def sample_transitions(self, num_steps: int, epsilon: float = 0.0) -> SampleBatch:
+        """Off-policy transitions (DQN): epsilon-greedy on the Q head."""
+        N = self.N
+        T = max(1, int(num_steps) // N)
+        out = {k: [] for k in ("obs", "actions", "rewards", "new_obs", "terminateds")}
+        for _ in range(T):
+            q = self.module.q_values(torch.from_numpy(self.obs))
+            a = q.argmax(-1).numpy()
+            rnd = self._rng.random(N) < epsilon
+            if rnd.any():
+                a[rnd] = self._rng.integers(0, self.env.action_space.n, int(rnd.sum()))
+            nobs, r, te, tr, info = self.env.step(a)
+            done = te | tr
+            nxt = np.where(done.reshape((-1,) + (1,) * (nobs.ndim - 1)), info["final_obs"], nobs)
+            out["obs"].append(self.obs)
+            out["actions"].append(a)
+            out["rewards"].append(r)
+            out["new_obs"].append(nxt)
+            out["terminateds"].append(te)
+            self._track(r, te, tr)
+            self.obs = nobs
+        self.steps_sampled += N * T
+        return SampleBatch({k: np.concatenate(v, axis=0) if k in ("obs", "new_obs") else np.concatenate(v) for k, v
+                            in out.items()})
+
+    def get_metrics(self) -> Dict:
+        eps = self.new_episodes
+        self.new_episodes = []
+        return {"episodes": eps, "num_env_steps_sampled": self.steps_sampled}
+
+    def ping(self):
+        return "ok"

@@ -1,0 +1,314 @@
+"""Environments: a gymnasium-style single-env API plus natively vectorised numpy envs.
+
+gymnasium / ALE are not installed in this environment, so the framework ships:
+  * ``CartPole-v1`` and ``Pendulum-v1`` (classic-control dynamics, vectorised over N envs);
+  * ``SyntheticAtari-v0`` — an Atari-shaped task (84x84x4 uint8 frame stacks, Discrete(6)
+    actions, +/-1 rewards): a falling-ball "catch" game rendered into 84x84 frames, used as the
+    shape-faithful stand-in for ALE games (``ALE/*`` ids resolve to it, flagged in ``info``).
+Custom envs: ``register_env(name, creator)`` with a gym-like object exposing
+``reset() -> (obs, info)`` and ``step(a) -> (obs, r, terminated, truncated, info)``.
+Reference: ``rllib/env/{vector_env,single_agent_env_runner}.py`` and gymnasium semantics.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Callable, Dict, Optional, Tuple
+
+import numpy as np
+
+from ..utils.spaces import Box, Discrete
+
+_REGISTRY: Dict[str, Callable] = {}
+
+
+def register_env(name: str, creator: Callable):
+    _REGISTRY[name] = creator
+
+
+class Env:
+    observation_space = None
+    action_space = None
+    metadata = {}
+
+    def reset(self, *, seed=None, options=None):
+        raise NotImplementedError
+
+    def step(self, action):
+        raise NotImplementedError
+
+    def close(self):
+        pass
+
+
+class VectorEnv:
+    """N environments stepped as one batch. ``step`` auto-resets finished sub-envs and returns the
+    pre-reset observation in ``info["final_obs"]`` (row-aligned, valid where done)."""
+
+    num_envs: int
+    observation_space = None
+    action_space = None
+
+    def reset(self, seed=None):
+        raise NotImplementedError
+
+    def step(self, actions):
+        raise NotImplementedError
+
+
+class CartPoleVec(VectorEnv):
+    def __init__(self, num_envs=1, max_episode_steps=500, seed=None):
+        self.num_envs = num_envs
+        self.gravity, self.masscart, self.masspole, self.length = 9.8, 1.0, 0.1, 0.5
+        self.total_mass = self.masscart + self.masspole
+        self.polemass_length = self.masspole * self.length
+        self.force_mag, self.tau = 10.0, 0.02
+        self.theta_th = 12 * 2 * math.pi / 360
+        self.x_th = 2.4
+        high = np.array([self.x_th * 2, np.finfo(np.float32).max, self.theta_th * 2, np.finfo(np.float32).max],
+                        dtype=np.float32)
+        self.observation_space = Box(-high, high, dtype=np.float32)
+        self.action_space = Discrete(2)
+        self.max_steps = max_episode_steps
+        self.rng = np.random.default_rng(seed)
+        self.state = np.zeros((num_envs, 4), dtype=np.float64)
+        self.t = np.zeros(num_envs, dtype=np.int64)
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.state = self.rng.uniform(-0.05, 0.05, size=(self.num_envs, 4))
+        self.t[:] = 0
+        return self.state.astype(np.float32), {}
+
+    def step(self, actions):
+        a = np.asarray(actions).reshape(-1)
+        x, x_dot, th, th_dot = self.state.T
+        force = np.where(a == 1, self.force_mag, -self.force_mag)
+        ct, st = np.cos(th), np.sin(th)
+        temp = (force + self.polemass_length * th_dot ** 2 * st) / self.total_mass
+        thacc = (self.gravity * st - ct * temp) / (
+            self.length * (4.0 / 3.0 - self.masspole * ct ** 2 / self.total_mass))
+        xacc = temp - self.polemass_length * thacc * ct / self.total_mass
+        x = x + self.tau * x_dot
+        x_dot = x_dot + self.tau * xacc
+        th = th + self.tau * th_dot
+        th_dot = th_dot + self.tau * thacc
+        self.state = np.stack([x, x_dot, th, th_dot], axis=1)
+        self.t += 1
+        term = (x < -self.x_th) | (x > self.x_th) | (th < -self.theta_th) | (th > self.theta_th)
+        trunc = (self.t >= self.max_steps) & ~term
+        rew = np.ones(self.num_envs, dtype=np.float32)
+        obs = self.state.astype(np.float32)
+        done = term | trunc
+        final = obs.copy()
+        if done.any():
+            n = int(done.sum())
+            self.state[done] = self.rng.uniform(-0.05, 0.05, size=(n, 4))
+            self.t[done] = 0
+            obs = self.state.astype(np.float32)
+        return obs, rew, term, trunc, {"final_obs": final}
+
+
+class PendulumVec(VectorEnv):
+    def __init__(self, num_envs=1, max_episode_steps=200, seed=None):
+        self.num_envs = num_envs
+        self.max_speed, self.max_torque, self.dt, self.g, self.m, self.l = 8.0, 2.0, 0.05, 10.0, 1.0, 1.0
+        self.observation_space = Box(np.array([-1, -1, -8.0]), np.array([1, 1, 8.0]), dtype=np.float32)
+        self.action_space = Box(-2.0, 2.0, shape=(1,), dtype=np.float32)
+        self.max_steps = max_episode_steps
+        self.rng = np.random.default_rng(seed)
+        self.th = np.zeros(num_envs)
+        self.thd = np.zeros(num_envs)
+        self.t = np.zeros(num_envs, dtype=np.int64)
+
+    def _obs(self):
+        return np.stack([np.cos(self.th), np.sin(self.th), self.thd], axis=1).astype(np.float32)
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.th = self.rng.uniform(-np.pi, np.pi, self.num_envs)
+        self.thd = self.rng.uniform(-1, 1, self.num_envs)
+        self.t[:] = 0
+        return self._obs(), {}
+
+    def step(self, actions):
+        u = np.clip(np.asarray(actions, dtype=np.float64).reshape(self.num_envs, -1)[:, 0], -self.max_torque,
+                    self.max_torque)
+        thn = ((self.th + np.pi) % (2 * np.pi)) - np.pi
+        cost = thn ** 2 + 0.1 * self.thd ** 2 + 0.001 * u ** 2
+        self.thd = np.clip(self.thd + (3 * self.g / (2 * self.l) * np.sin(self.th) + 3.0 / (self.m * self.l ** 2) * u)
+                           * self.dt, -self.max_speed, self.max_speed)
+        self.th = self.th + self.thd * self.dt
+        self.t += 1
+        trunc = self.t >= self.max_steps
+        term = np.zeros(self.num_envs, dtype=bool)
+        obs = self._obs()
+        final = obs.copy()
+        if trunc.any():
+            n = int(trunc.sum())
+            self.th[trunc] = self.rng.uniform(-np.pi, np.pi, n)
+            self.thd[trunc] = self.rng.uniform(-1, 1, n)
+            self.t[trunc] = 0
+            obs = self._obs()
+        return obs, (-cost).astype(np.float32), term, trunc, {"final_obs": final}
+
+
+class SyntheticAtariVec(VectorEnv):
+    """Atari-shaped catch game: 84x84 frames, 4-frame stack (HWC uint8), Discrete(6) (NOOP, FIRE,
+    RIGHT, LEFT, RIGHTFIRE, LEFTFIRE as in Pong's action set). A ball falls one row per step
+    (randomised start column and drift); the paddle on the bottom rows catches it (+1) or misses
+    (-1); an episode is ``balls_per_episode`` balls."""
+
+    H = W = 84
+    STACK = 4
+
+    def __init__(self, num_envs=1, balls_per_episode=5, max_episode_steps=10000, seed=None, frameskip=1):
+        self.num_envs = num_envs
+        self.observation_space = Box(0, 255, shape=(self.H, self.W, self.STACK), dtype=np.uint8)
+        self.action_space = Discrete(6)
+        self.balls = balls_per_episode
+        self.max_steps = max_episode_steps
+        self.rng = np.random.default_rng(seed)
+        n = num_envs
+        self.frames = np.zeros((n, self.H, self.W, self.STACK), dtype=np.uint8)
+        self.bx = np.zeros(n)
+        self.by = np.zeros(n)
+        self.vx = np.zeros(n)
+        self.px = np.full(n, self.W / 2)
+        self.left = np.zeros(n, dtype=np.int64)
+        self.t = np.zeros(n, dtype=np.int64)
+        self._ar = np.arange(n)
+
+    def _new_ball(self, idx):
+        k = len(idx) if hasattr(idx, "__len__") else int(np.sum(idx))
+        self.bx[idx] = self.rng.uniform(4, self.W - 4, k)
+        self.by[idx] = 0.0
+        self.vx[idx] = self.rng.uniform(-1.0, 1.0, k)
+
+    def _render(self, mask=None):
+        idx = self._ar if mask is None else np.nonzero(mask)[0]
+        if len(idx) == 0:
+            return
+        f = np.zeros((len(idx), self.H, self.W), dtype=np.uint8)
+        by = np.clip(self.by[idx].astype(np.int64), 0, self.H - 2)
+        bx = np.clip(self.bx[idx].astype(np.int64), 0, self.W - 2)
+        px = np.clip(self.px[idx].astype(np.int64), 6, self.W - 7)
+        rr = np.arange(len(idx))
+        for dy in (0, 1):
+            for dx in (0, 1):
+                f[rr, by + dy, bx + dx] = 255
+        for dx in range(-6, 7):
+            f[rr, self.H - 2, px + dx] = 200
+            f[rr, self.H - 1, px + dx] = 200
+        fr = self.frames[idx]
+        fr[..., :-1] = fr[..., 1:]
+        fr[..., -1] = f
+        self.frames[idx] = fr
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self._new_ball(self._ar)
+        self.px[:] = self.W / 2
+        self.left[:] = self.balls
+        self.t[:] = 0
+        self.frames[:] = 0
+        for _ in range(self.STACK):
+            self._render()
+        return self.frames.copy(), {"synthetic_atari": True}
+
+    def step(self, actions):
+        a = np.asarray(actions).reshape(-1)
+        move = np.where(np.isin(a, (2, 4)), 3.0, np.where(np.isin(a, (3, 5)), -3.0, 0.0))
+        self.px = np.clip(self.px + move, 6, self.W - 7)
+        self.bx = np.clip(self.bx + self.vx, 1, self.W - 3)
+        self.vx = np.where((self.bx <= 1) | (self.bx >= self.W - 3), -self.vx, self.vx)
+        self.by += 2.0
+        self.t += 1
+        rew = np.zeros(self.num_envs, dtype=np.float32)
+        landed = self.by >= self.H - 3
+        if landed.any():
+            hit = np.abs(self.bx - self.px) <= 7
+            rew[landed & hit] = 1.0
+            rew[landed & ~hit] = -1.0
+            self.left[landed] -= 1
+            self._new_ball(landed)
+        term = self.left <= 0
+        trunc = (self.t >= self.max_steps) & ~term
+        self._render()
+        obs = self.frames.copy()
+        done = term | trunc
+        final = obs
+        if done.any():
+            final = obs.copy()
+            self.left[done] = self.balls
+            self.t[done] = 0
+            self.px[done] = self.W / 2
+            self.frames[done] = 0
+            for _ in range(self.STACK):
+                self._render(done)
+            obs = self.frames.copy()
+        return obs, rew, term, trunc, {"final_obs": final, "synthetic_atari": True}
+
+
+class SingleToVector(VectorEnv):
+    """Wrap N independent gym-style envs into the VectorEnv interface."""
+
+    def __init__(self, make_env: Callable, num_envs: int, seed=None):
+        self.envs = [make_env() for _ in range(num_envs)]
+        self.num_envs = num_envs
+        self.observation_space = self.envs[0].observation_space
+        self.action_space = self.envs[0].action_space
+        self._seed = seed
+
+    def reset(self, seed=None):
+        obs = []
+        for i, e in enumerate(self.envs):
+            s = None if seed is None and self._seed is None else (seed or self._seed) + i
+            o, _ = e.reset(seed=s)
+            obs.append(o)
+        return np.stack(obs), {}
+
+    def step(self, actions):
+        obs, rew, term, trunc, finals = [], [], [], [], []
+        for e, a in zip(self.envs, actions):
+            o, r, te, tr, _ = e.step(a)
+            finals.append(o)
+            if te or tr:
+                o, _ = e.reset()
+            obs.append(o)
+            rew.append(r)
+            term.append(te)
+            trunc.append(tr)
+        return (np.stack(obs), np.asarray(rew, dtype=np.float32), np.asarray(term), np.asarray(trunc),
+                {"final_obs": np.stack(finals)})
+
+
+def make_vector_env(env, num_envs: int, env_config: Optional[dict] = None, seed=None) -> VectorEnv:
+    cfg = dict(env_config or {})
+    if isinstance(env, str):
+        if env in _REGISTRY:
+            return SingleToVector(lambda: _REGISTRY[env](cfg), num_envs, seed)
+        if env == "CartPole-v1" or env == "CartPole-v0":
+            return CartPoleVec(num_envs, max_episode_steps=500 if env.endswith("1") else 200, seed=seed)
+        if env == "Pendulum-v1":
+            return PendulumVec(num_envs, seed=seed)
+        if env.startswith("ALE/") or env == "SyntheticAtari-v0" or "NoFrameskip" in env:
+            return SyntheticAtariVec(num_envs, seed=seed, **{k: v for k, v in cfg.items()
+                                                             if k in ("balls_per_episode", "max_episode_steps")})
+        raise ValueError(f"unknown env {env!r}; register it with register_env()")
+    if isinstance(env, type) and issubclass(env, VectorEnv):
+        return env(num_envs=num_envs, **cfg)
+    if callable(env):
+        return SingleToVector(lambda: env(cfg) if _takes_arg(env) else env(), num_envs, seed)
+    raise ValueError(f"unsupported env spec {env!r}")
+
+
+def _takes_arg(f):
+    import inspect
+
+    try:
+        return len(inspect.signature(f).parameters) >= 1
+    except (TypeError, ValueError):
+        return True

@@ -118,8 +118,10 @@ class _ClassTrainableRunner:
         return None
 
     def step(self):
+        before = self.t._iteration
         r = self.t.step() or {}
-        self.t._iteration += 1
+        if self.t._iteration == before:  # trainables like Algorithm count their own iterations
+            self.t._iteration += 1
         r = dict(r)
         r.setdefault("training_iteration", self.t._iteration)
         return r

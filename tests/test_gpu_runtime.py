@@ -77,3 +77,15 @@ def test_rccl_collective_group_single_rank(ray_gpu):
             return t.sum().item()
 
     assert ray.get(W.remote().go.remote()) == 8.0
+
+
+def test_ppo_gpu_learner_synthetic_atari(ray_gpu):
+    from ray_community_amd.rllib import PPOConfig
+
+    cfg = (PPOConfig().environment("ALE/Pong-v5").env_runners(num_env_runners=1, num_envs_per_env_runner=4)
+           .training(train_batch_size=256, minibatch_size=128, num_epochs=1).resources(num_gpus=1))
+    algo = cfg.build()
+    assert algo.learner_group.local.device.type == "cuda"
+    r = algo.train()
+    assert r["num_env_steps_sampled_this_iter"] == 256
+    algo.stop()

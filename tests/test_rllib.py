@@ -1,0 +1,115 @@
+"""RLlib tests (modelled on reference rllib/algorithms/ppo/tests/test_ppo.py, dqn tests)."""
+import numpy as np
+import pytest
+import torch
+
+import ray_community_amd as ray
+from ray_community_amd import ops
+from ray_community_amd.rllib import PPOConfig, DQNConfig, SampleBatch
+from ray_community_amd.rllib.env import make_vector_env
+from ray_community_amd.rllib.evaluation.postprocessing import compute_advantages, discount_cumsum
+
+
+def test_vector_envs():
+    for name, shape in [("CartPole-v1", (4,)), ("Pendulum-v1", (3,)), ("ALE/Pong-v5", (84, 84, 4))]:
+        env = make_vector_env(name, 3, seed=0)
+        obs, _ = env.reset(seed=0)
+        assert obs.shape == (3,) + shape
+        for _ in range(5):
+            a = np.stack([env.action_space.sample() for _ in range(3)])
+            obs, r, te, tr, info = env.step(a)
+            assert obs.shape == (3,) + shape and r.shape == (3,) and "final_obs" in info
+
+
+def test_compute_advantages_reference_api():
+    b = SampleBatch({"rewards": np.array([1.0, 1.0, 1.0]), "vf_preds": np.array([0.5, 0.5, 0.5])})
+    b = compute_advantages(b, last_r=0.0, gamma=0.9, lambda_=1.0)
+    expect = discount_cumsum(np.array([1.0, 1.0, 1.0, 0.0]), 0.9)[:-1] - 0.5
+    assert np.allclose(b["advantages"], expect, atol=1e-5)
+
+
+def test_sample_batch_ops():
+    b = SampleBatch({"a": np.arange(10), "b": np.arange(10) * 2})
+    assert b.count == 10
+    mbs = list(b.minibatches(4, rng=np.random.default_rng(0)))
+    assert len(mbs) == 2 and all(m.count == 4 for m in mbs)
+    b.shuffle(np.random.default_rng(0))
+    assert sorted(b["a"].tolist()) == list(range(10))
+
+
+def test_ppo_cartpole_learns(shutdown_only):
+    ray.init(num_cpus=4)
+    config = (PPOConfig().environment("CartPole-v1")
+              .env_runners(num_env_runners=2, num_envs_per_env_runner=8)
+              .training(lr=3e-4, train_batch_size=2048, minibatch_size=256, num_epochs=8, vf_loss_coeff=0.01,
+                        model={"fcnet_hiddens": [64, 64]})
+              .debugging(seed=0))
+    algo = config.build()
+    best = 0
+    for i in range(25):
+        r = algo.train()
+        best = max(best, r["episode_reward_mean"])
+        if best > 150:
+            break
+    assert best > 150, best
+    assert r["timesteps_total"] >= 2048
+    a = algo.compute_single_action(np.zeros(4, dtype=np.float32))
+    assert a in (0, 1)
+    algo.stop()
+
+
+def test_ppo_checkpoint_roundtrip(shutdown_only, tmp_path):
+    ray.init(num_cpus=2)
+    config = PPOConfig().environment("CartPole-v1").training(train_batch_size=256, minibatch_size=64, num_epochs=1)
+    algo = config.build()
+    algo.train()
+    res = algo.save(str(tmp_path / "ck"))
+    w = algo.get_weights()
+    algo2 = PPOConfig().environment("CartPole-v1").build()
+    algo2.restore(res.checkpoint.path)
+    w2 = algo2.get_weights()
+    assert all(torch.equal(w[k], w2[k]) for k in w)
+    assert algo2.iteration == 1
+    algo.stop()
+    algo2.stop()
+
+
+def test_dqn_cartpole_improves(shutdown_only):
+    ray.init(num_cpus=2)
+    config = (DQNConfig().environment("CartPole-v1").env_runners(num_envs_per_env_runner=4)
+              .training(lr=1e-3, train_batch_size=64, training_intensity=8, num_steps_sampled_before_learning_starts=500,
+                        target_network_update_freq=400, model={"fcnet_hiddens": [64, 64]})
+              .debugging(seed=1))
+    config.epsilon = [(0, 1.0), (4000, 0.05)]
+    algo = config.build()
+    best = 0
+    for i in range(2000):
+        r = algo.train()
+        if r["episode_reward_mean"] == r["episode_reward_mean"]:
+            best = max(best, r["episode_reward_mean"])
+        if best > 100:
+            break
+    assert best > 100, best
+    algo.stop()
+
+
+def test_ppo_synthetic_atari_smoke(shutdown_only):
+    ray.init(num_cpus=2)
+    config = (PPOConfig().environment("ALE/Pong-v5").env_runners(num_envs_per_env_runner=4)
+              .training(train_batch_size=128, minibatch_size=64, num_epochs=1))
+    algo = config.build()
+    r = algo.train()
+    assert r["num_env_steps_sampled_this_iter"] == 128
+    algo.stop()
+
+
+def test_ppo_in_tune(shutdown_only, tmp_path):
+    from ray_community_amd import tune
+    from ray_community_amd.rllib import PPO
+    from ray_community_amd.train import RunConfig
+
+    ray.init(num_cpus=4)
+    cfg = PPOConfig().environment("CartPole-v1").training(train_batch_size=256, minibatch_size=64, num_epochs=1)
+    grid = tune.Tuner(PPO, param_space=cfg.to_dict(),
+                      run_config=RunConfig(stop={"training_iteration": 2}, storage_path=str(tmp_path))).fit()
+    assert grid.num_errors == 0 and grid[0].metrics["training_iteration"] == 2
