@@ -1,0 +1,17 @@
+"""Ray Data equivalent (reference: ``python/ray/data``)."""
+from .aggregate import AbsMax, AggregateFn, Count, Max, Mean, Min, Std, Sum, Unique
+from .block import BlockAccessor
+from .context import DataContext, DatasetContext
+from .dataset import ActorPoolStrategy, Dataset, MaterializedDataset, Schema, TaskPoolStrategy
+from .grouped_data import GroupedData
+from .iterator import DataIterator
+from .read_api import (Datasource, from_arrow, from_huggingface, from_items, from_numpy, from_numpy_refs, from_pandas,
+                       from_torch, range, range_tensor, read_binary_files, read_csv, read_datasource, read_images,
+                       read_json, read_numpy, read_parquet, read_text)
+
+__all__ = ["Dataset", "MaterializedDataset", "DataIterator", "GroupedData", "ActorPoolStrategy", "TaskPoolStrategy",
+           "DataContext", "DatasetContext", "Schema", "BlockAccessor", "range", "range_tensor", "from_items",
+           "from_numpy", "from_numpy_refs", "from_pandas", "from_arrow", "from_torch", "from_huggingface",
+           "read_parquet", "read_csv", "read_json", "read_text", "read_numpy", "read_binary_files", "read_images",
+           "read_datasource", "Datasource", "AggregateFn", "Count", "Sum", "Min", "Max", "Mean", "Std", "AbsMax",
+           "Unique"]

@@ -1,0 +1,216 @@
+"""Blocks (reference: ``python/ray/data/block.py``, ``_internal/{arrow,pandas}_block.py``).
+
+A block is either a ``pyarrow.Table`` (tabular sources) or a ``dict[str, np.ndarray]`` "numpy
+block" (tensor-friendly: image batches stay ndarrays, zero conversion for
+``batch_format="numpy"``). ``BlockAccessor`` hides the difference.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Iterator, List, Optional, Union
+
+import numpy as np
+
+try:
+    import pyarrow as pa
+except ImportError:  # pragma: no cover
+    pa = None
+
+Block = Union["pa.Table", Dict[str, np.ndarray]]
+
+
+def _is_arrow(b):
+    return pa is not None and isinstance(b, pa.Table)
+
+
+def _is_pandas(b):
+    try:
+        import pandas as pd
+
+        return isinstance(b, pd.DataFrame)
+    except ImportError:
+        return False
+
+
+def _np_col(v):
+    if isinstance(v, np.ndarray):
+        return v
+    if isinstance(v, list):
+        try:
+            arr = np.asarray(v)
+            if arr.dtype == object and len(v) and isinstance(v[0], np.ndarray):
+                return np.stack(v)
+            return arr
+        except (ValueError, TypeError):
+            a = np.empty(len(v), dtype=object)
+            a[:] = v
+            return a
+    try:
+        import torch
+
+        if isinstance(v, torch.Tensor):
+            return v.detach().cpu().numpy()
+    except ImportError:
+        pass
+    return np.asarray(v)
+
+
+class BlockAccessor:
+    def __init__(self, block):
+        self.b = block
+
+    @staticmethod
+    def for_block(block) -> "BlockAccessor":
+        return BlockAccessor(normalize_block(block))
+
+    def num_rows(self) -> int:
+        b = self.b
+        if _is_arrow(b):
+            return b.num_rows
+        if not b:
+            return 0
+        return len(next(iter(b.values())))
+
+    def size_bytes(self) -> int:
+        b = self.b
+        if _is_arrow(b):
+            return b.nbytes
+        return int(sum(getattr(v, "nbytes", 0) for v in b.values()))
+
+    def column_names(self) -> List[str]:
+        return list(self.b.column_names) if _is_arrow(self.b) else list(self.b.keys())
+
+    def schema(self):
+        b = self.b
+        if _is_arrow(b):
+            return b.schema
+        return {k: (v.dtype, v.shape[1:]) for k, v in b.items()}
+
+    def slice(self, start, end) -> Block:
+        b = self.b
+        if _is_arrow(b):
+            return b.slice(start, end - start)
+        return {k: v[start:end] for k, v in b.items()}
+
+    def take(self, idx) -> Block:
+        b = self.b
+        if _is_arrow(b):
+            return b.take(pa.array(np.asarray(idx, dtype=np.int64)))
+        return {k: v[idx] for k, v in b.items()}
+
+    def to_numpy(self) -> Dict[str, np.ndarray]:
+        b = self.b
+        if _is_arrow(b):
+            out = {}
+            for name in b.column_names:
+                col = b.column(name)
+                try:
+                    out[name] = col.to_numpy(zero_copy_only=False)
+                except Exception:
+                    out[name] = np.asarray(col.to_pylist(), dtype=object)
+                if out[name].dtype == object and len(out[name]) and isinstance(out[name][0], (list, np.ndarray)):
+                    try:
+                        out[name] = np.stack([np.asarray(x) for x in out[name]])
+                    except ValueError:
+                        pass
+            return out
+        return dict(b)
+
+    def to_pandas(self):
+        import pandas as pd
+
+        b = self.b
+        if _is_arrow(b):
+            return b.to_pandas()
+        cols = {}
+        for k, v in b.items():
+            cols[k] = list(v) if v.ndim > 1 else v
+        return pd.DataFrame(cols)
+
+    def to_arrow(self):
+        b = self.b
+        if _is_arrow(b):
+            return b
+        cols = {}
+        for k, v in b.items():
+            if v.ndim > 1:
+                cols[k] = pa.array(list(v.reshape(len(v), -1)))
+            else:
+                cols[k] = pa.array(v) if v.dtype != object else pa.array(list(v))
+        return pa.table(cols)
+
+    def to_batch(self, fmt: str):
+        if fmt in ("numpy", "default", None):
+            return self.to_numpy()
+        if fmt == "pandas":
+            return self.to_pandas()
+        if fmt in ("pyarrow", "arrow"):
+            return self.to_arrow()
+        raise ValueError(f"unknown batch_format {fmt}")
+
+    def iter_rows(self) -> Iterator[Dict[str, Any]]:
+        cols = self.to_numpy()
+        n = self.num_rows()
+        keys = list(cols)
+        for i in range(n):
+            yield {k: _py(cols[k][i]) for k in keys}
+
+
+def _py(x):
+    if isinstance(x, np.generic):
+        return x.item()
+    return x
+
+
+def normalize_block(x) -> Block:
+    """Convert a UDF output / batch into a block."""
+    if x is None:
+        return {}
+    if _is_arrow(x):
+        return x
+    if _is_pandas(x):
+        if pa is not None:
+            try:
+                return pa.Table.from_pandas(x, preserve_index=False)
+            except Exception:
+                pass
+        return {c: _np_col(list(x[c])) for c in x.columns}
+    if isinstance(x, dict):
+        return {str(k): _np_col(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return rows_to_block(x)
+    raise TypeError(f"cannot convert {type(x)} to a block; return a dict of arrays, pandas or pyarrow")
+
+
+def rows_to_block(rows: List[Any]) -> Block:
+    if not rows:
+        return {}
+    if not isinstance(rows[0], dict):
+        rows = [{"item": r} for r in rows]
+    keys = list(rows[0].keys())
+    return {k: _np_col([r[k] for r in rows]) for k in keys}
+
+
+def concat_blocks(blocks: List[Block]) -> Block:
+    blocks = [b for b in blocks if BlockAccessor(b).num_rows() > 0]
+    if not blocks:
+        return {}
+    if len(blocks) == 1:
+        return blocks[0]
+    if all(_is_arrow(b) for b in blocks):
+        return pa.concat_tables(blocks, promote_options="default")
+    nps = [BlockAccessor(b).to_numpy() for b in blocks]
+    keys = list(nps[0].keys())
+    out = {}
+    for k in keys:
+        parts = [n[k] for n in nps]
+        try:
+            out[k] = np.concatenate(parts, axis=0)
+        except ValueError:
+            a = np.empty(sum(len(p) for p in parts), dtype=object)
+            a[:] = [x for p in parts for x in p]
+            out[k] = a
+    return out
+
+
+class BlockMetadata(dict):
+    pass

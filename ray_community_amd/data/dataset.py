@@ -1,0 +1,611 @@
+"""Dataset (reference: ``python/ray/data/dataset.py``): lazy, block-based, streaming."""
+from __future__ import annotations
+
+import collections
+import inspect
+import itertools
+import math
+import os
+from typing import Any, Callable, Dict, Iterable, Iterator, List, Optional, Tuple, Union
+
+import numpy as np
+
+from .block import BlockAccessor, concat_blocks, normalize_block
+from ._internal import execution as X
+
+_MAP_KINDS = {"map_batches", "map", "flat_map", "filter", "add_column", "drop_columns", "select_columns",
+              "rename_columns"}
+
+
+def _cpus():
+    try:
+        from .._private.worker import cluster_resources, is_initialized
+
+        if is_initialized():
+            return max(1, int(cluster_resources().get("CPU", 1)))
+    except Exception:
+        pass
+    return os.cpu_count() or 1
+
+
+def _ensure_init():
+    from .._private import worker as w
+
+    if not w.is_initialized():
+        w.init()
+
+
+class ActorPoolStrategy:
+    def __init__(self, size: Optional[int] = None, min_size: Optional[int] = None, max_size: Optional[int] = None,
+                 max_tasks_in_flight_per_actor: int = 4):
+        self.size = size or max_size or min_size or 1
+        self.max_tasks_in_flight_per_actor = max_tasks_in_flight_per_actor
+
+
+class TaskPoolStrategy:
+    def __init__(self, size: Optional[int] = None):
+        self.size = size
+
+
+class Schema:
+    def __init__(self, names, types):
+        self.names = list(names)
+        self.types = list(types)
+
+    def __repr__(self):
+        return "Schema(" + ", ".join(f"{n}: {t}" for n, t in zip(self.names, self.types)) + ")"
+
+    def __eq__(self, o):
+        return isinstance(o, Schema) and o.names == self.names
+
+
+class Dataset:
+    def __init__(self, inputs: List, ops: Optional[List[Dict]] = None, name: Optional[str] = None):
+        self._inputs = inputs
+        self._ops = list(ops or [])
+        self._name = name
+        self._materialized: Optional[List[Tuple[Any, Any]]] = None
+
+    # ------------------------------------------------------------------ plan helpers
+    def _with(self, op) -> "Dataset":
+        return Dataset(self._inputs, self._ops + [op], self._name)
+
+    def _iter_refs(self) -> Iterator[Tuple[Any, Any]]:
+        _ensure_init()
+        if self._materialized is not None:
+            return iter(self._materialized)
+        window = max(2, 2 * _cpus())
+        it = X.source_stage(self._inputs, window)
+        pending_tasks: List[Dict] = []
+        for op in self._ops:
+            if op["kind"] in _MAP_KINDS and op.get("compute") != "actors":
+                pending_tasks.append(op)
+                continue
+            if pending_tasks:
+                it = X.task_map_stage(it, pending_tasks, window, _task_opts(pending_tasks))
+                pending_tasks = []
+            if op["kind"] in _MAP_KINDS:  # actor pool stage
+                it = X.actor_map_stage(it, op, [], [], op["pool_size"], op["actor_opts"],
+                                       op.get("max_tasks_in_flight_per_actor", 4))
+            elif op["kind"] == "limit":
+                it = X.limit_stage(it, op["n"])
+            elif op["kind"] == "alltoall":
+                mats = list(it)
+                it = iter(op["fn"](mats))
+            else:
+                raise ValueError(op["kind"])
+        if pending_tasks:
+            it = X.task_map_stage(it, pending_tasks, window, _task_opts(pending_tasks))
+        return it
+
+    def _refs(self) -> List[Tuple[Any, Any]]:
+        if self._materialized is None:
+            self._materialized = list(self._iter_refs())
+            self._inputs = [("ref", b, m) for b, m in self._materialized]
+            self._ops = []
+        return self._materialized
+
+    def _metas(self):
+        from .._private.worker import get
+
+        refs = self._refs()
+        return get([m for _, m in refs]) if refs else []
+
+    # ------------------------------------------------------------------ transforms
+    def map_batches(self, fn, *, batch_size: Union[int, None, str] = "default", compute=None,
+                    batch_format: Optional[str] = "default", zero_copy_batch: bool = False, fn_args=None,
+                    fn_kwargs=None, fn_constructor_args=None, fn_constructor_kwargs=None, num_cpus=None,
+                    num_gpus=None, concurrency=None, **ray_remote_args) -> "Dataset":
+        if batch_size == "default":
+            batch_size = 1024 if not inspect.isclass(fn) else 1024
+        op = {"kind": "map_batches", "fn": fn, "batch_size": batch_size, "batch_format": batch_format,
+              "fn_args": tuple(fn_args or ()), "fn_kwargs": dict(fn_kwargs or {}), "num_cpus": num_cpus,
+              "num_gpus": num_gpus, "ray_remote_args": ray_remote_args}
+        return self._with(_compute(op, fn, compute, concurrency, fn_constructor_args, fn_constructor_kwargs, num_cpus,
+                                   num_gpus, ray_remote_args))
+
+    def map(self, fn, *, compute=None, fn_args=None, fn_kwargs=None, fn_constructor_args=None,
+            fn_constructor_kwargs=None, num_cpus=None, num_gpus=None, concurrency=None, **ray_remote_args):
+        op = {"kind": "map", "fn": fn, "fn_args": tuple(fn_args or ()), "fn_kwargs": dict(fn_kwargs or {}),
+              "num_cpus": num_cpus, "num_gpus": num_gpus, "ray_remote_args": ray_remote_args}
+        return self._with(_compute(op, fn, compute, concurrency, fn_constructor_args, fn_constructor_kwargs, num_cpus,
+                                   num_gpus, ray_remote_args))
+
+    def flat_map(self, fn, *, compute=None, fn_args=None, fn_kwargs=None, fn_constructor_args=None,
+                 fn_constructor_kwargs=None, num_cpus=None, num_gpus=None, concurrency=None, **ray_remote_args):
+        op = {"kind": "flat_map", "fn": fn, "fn_args": tuple(fn_args or ()), "fn_kwargs": dict(fn_kwargs or {}),
+              "num_cpus": num_cpus, "num_gpus": num_gpus, "ray_remote_args": ray_remote_args}
+        return self._with(_compute(op, fn, compute, concurrency, fn_constructor_args, fn_constructor_kwargs, num_cpus,
+                                   num_gpus, ray_remote_args))
+
+    def filter(self, fn=None, *, expr: Optional[str] = None, compute=None, concurrency=None, **kw):
+        op = {"kind": "filter", "fn": fn, "expr": expr}
+        return self._with(_compute(op, fn, compute, concurrency, None, None, None, None, kw))
+
+    def add_column(self, col: str, fn: Callable, *, batch_format: str = "pandas", **kw):
+        return self._with({"kind": "add_column", "col": col, "fn": fn, "batch_format": batch_format})
+
+    def drop_columns(self, cols: List[str], **kw):
+        return self._with({"kind": "drop_columns", "cols": list(cols)})
+
+    def select_columns(self, cols: List[str], **kw):
+        return self._with({"kind": "select_columns", "cols": list(cols) if not isinstance(cols, str) else [cols]})
+
+    def rename_columns(self, names: Dict[str, str], **kw):
+        return self._with({"kind": "rename_columns", "mapping": dict(names)})
+
+    def limit(self, limit: int) -> "Dataset":
+        return self._with({"kind": "limit", "n": int(limit)})
+
+    def repartition(self, num_blocks: int, *, shuffle: bool = False, seed=None) -> "Dataset":
+        def fn(refs):
+            return _repartition(refs, num_blocks, shuffle, seed)
+
+        return self._with({"kind": "alltoall", "fn": fn})
+
+    def random_shuffle(self, *, seed: Optional[int] = None, num_blocks: Optional[int] = None, **kw) -> "Dataset":
+        def fn(refs):
+            k = num_blocks or max(1, len(refs))
+            return _repartition(refs, k, True, seed)
+
+        return self._with({"kind": "alltoall", "fn": fn})
+
+    def randomize_block_order(self, *, seed: Optional[int] = None) -> "Dataset":
+        def fn(refs):
+            rng = np.random.default_rng(seed)
+            idx = rng.permutation(len(refs))
+            return [refs[i] for i in idx]
+
+        return self._with({"kind": "alltoall", "fn": fn})
+
+    def sort(self, key: Union[str, List[str]], descending: bool = False) -> "Dataset":
+        k = key if isinstance(key, str) else key[0]
+
+        def fn(refs):
+            return _sort(refs, k, descending)
+
+        return self._with({"kind": "alltoall", "fn": fn})
+
+    def groupby(self, key: Union[str, List[str], None]) -> "GroupedData":
+        from .grouped_data import GroupedData
+
+        return GroupedData(self, key)
+
+    def union(self, *others: "Dataset") -> "Dataset":
+        parts = [self] + list(others)
+
+        def fn(refs, parts=parts):
+            out = list(refs)
+            for o in parts[1:]:
+                out.extend(o._refs())
+            return out
+
+        return self._with({"kind": "alltoall", "fn": fn})
+
+    def zip(self, other: "Dataset") -> "Dataset":
+        def fn(refs):
+            from .._private.worker import get
+
+            mine = get([m for _, m in refs])
+            counts = [m["num_rows"] for m in mine]
+            theirs = _repartition_to_sizes(other._refs(), counts)
+            z = X._remote_fn(_zip_blocks, {"num_cpus": 1})
+            return [tuple(z.remote(a[0], b[0])) for a, b in zip(refs, theirs)]
+
+        return self._with({"kind": "alltoall", "fn": fn})
+
+    def random_sample(self, fraction: float, *, seed: Optional[int] = None) -> "Dataset":
+        def sample(batch, fraction=fraction, seed=seed):
+            n = len(next(iter(batch.values()))) if batch else 0
+            rng = np.random.default_rng(seed)
+            mask = rng.random(n) < fraction
+            return {k: v[mask] for k, v in batch.items()}
+
+        return self.map_batches(sample, batch_format="numpy", batch_size=None)
+
+    # ------------------------------------------------------------------ splits
+    def split(self, n: int, *, equal: bool = False, locality_hints=None) -> List["MaterializedDataset"]:
+        refs = self._refs()
+        metas = self._metas()
+        total = sum(m["num_rows"] for m in metas)
+        if equal:
+            per = total // n
+            sizes = [per] * n
+        else:
+            sizes = [total // n + (1 if i < total % n else 0) for i in range(n)]
+        parts = _repartition_to_sizes(refs, sizes, metas)
+        return [MaterializedDataset([p]) for p in parts]
+
+    def split_at_indices(self, indices: List[int]) -> List["MaterializedDataset"]:
+        metas = self._metas()
+        total = sum(m["num_rows"] for m in metas)
+        bounds = [0] + list(indices) + [total]
+        sizes = [max(0, b - a) for a, b in zip(bounds[:-1], bounds[1:])]
+        parts = _repartition_to_sizes(self._refs(), sizes, metas)
+        return [MaterializedDataset([p]) for p in parts]
+
+    def split_proportionately(self, proportions: List[float]):
+        total = self.count()
+        idx = []
+        acc = 0
+        for p in proportions:
+            acc += int(total * p)
+            idx.append(acc)
+        return self.split_at_indices(idx)
+
+    def train_test_split(self, test_size: Union[int, float], *, shuffle: bool = False, seed=None):
+        ds = self.random_shuffle(seed=seed) if shuffle else self
+        total = ds.count()
+        n_test = int(test_size) if isinstance(test_size, int) else int(math.ceil(total * test_size))
+        a, b = ds.split_at_indices([total - n_test])
+        return a, b
+
+    def streaming_split(self, n: int, *, equal: bool = False, locality_hints=None) -> List["DataIterator"]:
+        return [p.iterator() for p in self.split(n, equal=equal)]
+
+    # ------------------------------------------------------------------ consumption
+    def iterator(self) -> "DataIterator":
+        from .iterator import DataIterator
+
+        return DataIterator(self)
+
+    def iter_batches(self, **kw):
+        return self.iterator().iter_batches(**kw)
+
+    def iter_torch_batches(self, **kw):
+        return self.iterator().iter_torch_batches(**kw)
+
+    def iter_rows(self, **kw) -> Iterator[Dict]:
+        from .._private.worker import get
+
+        for b, _ in self._iter_refs():
+            yield from BlockAccessor(get(b)).iter_rows()
+
+    def take(self, limit: int = 20) -> List[Dict]:
+        out = []
+        for r in self.limit(limit).iter_rows():
+            out.append(r)
+            if len(out) >= limit:
+                break
+        return out
+
+    def take_all(self, limit: Optional[int] = None) -> List[Dict]:
+        out = list(self.iter_rows())
+        if limit is not None and len(out) > limit:
+            raise ValueError(f"The dataset has more than the given limit of {limit} records.")
+        return out
+
+    def take_batch(self, batch_size: int = 20, *, batch_format: str = "default"):
+        for b in self.limit(batch_size).iter_batches(batch_size=batch_size, batch_format=batch_format):
+            return b
+        return {}
+
+    def show(self, limit: int = 20):
+        for r in self.take(limit):
+            print(r)
+
+    def count(self) -> int:
+        return int(sum(m["num_rows"] for m in self._metas()))
+
+    def schema(self, fetch_if_missing: bool = True):
+        from .._private.worker import get
+
+        for b, m in self._iter_refs():
+            blk = get(b)
+            acc = BlockAccessor(blk)
+            if acc.num_rows() == 0 and not acc.column_names():
+                continue
+            if hasattr(blk, "schema"):
+                s = blk.schema
+                return Schema(s.names, [str(t) for t in s.types])
+            return Schema(list(blk.keys()), [f"{v.dtype}{list(v.shape[1:]) if v.ndim > 1 else ''}"
+                                             for v in blk.values()])
+        return None
+
+    def columns(self, fetch_if_missing: bool = True):
+        s = self.schema()
+        return s.names if s else []
+
+    def num_blocks(self) -> int:
+        return len(self._refs())
+
+    def size_bytes(self) -> int:
+        return int(sum(m["size_bytes"] for m in self._metas()))
+
+    def materialize(self) -> "MaterializedDataset":
+        return MaterializedDataset(self._refs())
+
+    def to_pandas(self, limit: Optional[int] = None):
+        import pandas as pd
+
+        from .._private.worker import get
+
+        dfs = [BlockAccessor(get(b)).to_pandas() for b, _ in self._iter_refs()]
+        df = pd.concat(dfs, ignore_index=True) if dfs else pd.DataFrame()
+        if limit is not None and len(df) > limit:
+            raise ValueError(f"the dataset has more than the given limit of {limit} rows")
+        return df
+
+    def to_numpy_refs(self, *, column=None):
+        from .._private.worker import get, put
+
+        return [put(BlockAccessor(get(b)).to_numpy() if column is None else BlockAccessor(get(b)).to_numpy()[column])
+                for b, _ in self._refs()]
+
+    def to_arrow_refs(self):
+        from .._private.worker import get, put
+
+        return [put(BlockAccessor(get(b)).to_arrow()) for b, _ in self._refs()]
+
+    def to_pandas_refs(self):
+        from .._private.worker import get, put
+
+        return [put(BlockAccessor(get(b)).to_pandas()) for b, _ in self._refs()]
+
+    def get_internal_block_refs(self):
+        return [b for b, _ in self._refs()]
+
+    def to_torch(self, *, label_column=None, feature_columns=None, batch_size=1, **kw):
+        import torch
+
+        class _It(torch.utils.data.IterableDataset):
+            def __iter__(_s):
+                for b in self.iter_torch_batches(batch_size=batch_size):
+                    if label_column:
+                        y = b.pop(label_column)
+                        cols = feature_columns or list(b)
+                        yield torch.stack([b[c].float() for c in cols], dim=1), y
+                    else:
+                        yield b
+
+        return _It()
+
+    # ------------------------------------------------------------------ aggregations
+    def aggregate(self, *aggs):
+        return self.groupby(None).aggregate(*aggs).take(1)[0]
+
+    def sum(self, on=None, ignore_nulls=True):
+        return self._agg1("sum", on)
+
+    def min(self, on=None, ignore_nulls=True):
+        return self._agg1("min", on)
+
+    def max(self, on=None, ignore_nulls=True):
+        return self._agg1("max", on)
+
+    def mean(self, on=None, ignore_nulls=True):
+        return self._agg1("mean", on)
+
+    def std(self, on=None, ddof=1, ignore_nulls=True):
+        from .aggregate import Std
+
+        r = self.aggregate(Std(on, ddof=ddof))
+        return list(r.values())[0]
+
+    def unique(self, column: str) -> List:
+        vals = set()
+        for b in self.select_columns([column]).iter_batches(batch_format="numpy"):
+            vals.update(np.unique(b[column]).tolist())
+        return list(vals)
+
+    def _agg1(self, how, on):
+        from . import aggregate as A
+
+        cls = {"sum": A.Sum, "min": A.Min, "max": A.Max, "mean": A.Mean}[how]
+        if on is None:
+            on = self.columns()[0]
+        if isinstance(on, list):
+            r = self.aggregate(*[cls(c) for c in on])
+            return r
+        r = self.aggregate(cls(on))
+        return list(r.values())[0]
+
+    # ------------------------------------------------------------------ writes
+    def write_parquet(self, path: str, **kw):
+        self._write(path, "parquet")
+
+    def write_csv(self, path: str, **kw):
+        self._write(path, "csv")
+
+    def write_json(self, path: str, **kw):
+        self._write(path, "json")
+
+    def write_numpy(self, path: str, *, column: str = "data", **kw):
+        self._write(path, "npy", column=column)
+
+    def _write(self, path, fmt, column=None):
+        from .._private.worker import get
+
+        os.makedirs(path, exist_ok=True)
+        w = X._remote_fn(_write_block, {"num_cpus": 1})
+        refs = [w.remote(b, path, i, fmt, column)[0] for i, (b, _) in enumerate(self._refs())]
+        get(refs)
+
+    # ------------------------------------------------------------------ misc
+    def stats(self) -> str:
+        ms = self._metas()
+        return (f"Dataset: {len(ms)} blocks, {sum(m['num_rows'] for m in ms)} rows, "
+                f"{sum(m['size_bytes'] for m in ms) / 2**20:.2f} MiB")
+
+    def __repr__(self):
+        return f"Dataset(num_ops={len(self._ops)}, materialized={self._materialized is not None})"
+
+    def __len__(self):
+        raise AttributeError("Use ds.count() to compute the length of a distributed Dataset.")
+
+    def __iter__(self):
+        raise TypeError("`Dataset` objects aren't iterable. To iterate records, call `ds.iter_rows()` or "
+                        "`ds.iter_batches()`.")
+
+    def context(self):
+        from .context import DataContext
+
+        return DataContext.get_current()
+
+
+class MaterializedDataset(Dataset):
+    def __init__(self, refs):
+        super().__init__([("ref", b, m) for b, m in refs])
+        self._materialized = list(refs)
+
+
+# ---------------------------------------------------------------------------------- helpers
+def _compute(op, fn, compute, concurrency, ctor_args, ctor_kwargs, num_cpus, num_gpus, ray_remote_args):
+    is_class = inspect.isclass(fn)
+    use_actors = is_class or isinstance(compute, ActorPoolStrategy) or compute == "actors"
+    if use_actors:
+        size = 1
+        if isinstance(compute, ActorPoolStrategy):
+            size = compute.size
+            op["max_tasks_in_flight_per_actor"] = compute.max_tasks_in_flight_per_actor
+        elif concurrency is not None:
+            size = concurrency[-1] if isinstance(concurrency, tuple) else int(concurrency)
+        op["compute"] = "actors"
+        op["pool_size"] = max(1, size)
+        opts = {"num_cpus": 1 if num_cpus is None else num_cpus}
+        if num_gpus:
+            opts["num_gpus"] = num_gpus
+        for k, v in (ray_remote_args or {}).items():
+            if k in ("resources", "memory", "scheduling_strategy", "runtime_env", "max_restarts"):
+                opts[k] = v
+        op["actor_opts"] = opts
+        op["fn_constructor_args"] = tuple(ctor_args or ())
+        op["fn_constructor_kwargs"] = dict(ctor_kwargs or {})
+        if not is_class:
+            f = fn
+
+            class _Wrap:
+                def __init__(self):
+                    pass
+
+                def __call__(self, *a, **k):
+                    return f(*a, **k)
+
+            op["fn"] = _Wrap
+    else:
+        op["compute"] = "tasks"
+    return op
+
+
+def _task_opts(ops):
+    cpus = max([o.get("num_cpus") or 0 for o in ops] + [0]) or 1
+    gpus = max([o.get("num_gpus") or 0 for o in ops] + [0])
+    opts = {"num_cpus": cpus}
+    if gpus:
+        opts["num_gpus"] = gpus
+    for o in ops:
+        for k, v in (o.get("ray_remote_args") or {}).items():
+            if k in ("resources", "memory", "scheduling_strategy", "runtime_env", "max_retries"):
+                opts[k] = v
+    return opts
+
+
+def _repartition(refs, k, shuffle, seed):
+    from .._private.worker import get
+
+    if not refs:
+        return []
+    metas = get([m for _, m in refs])
+    if shuffle:
+        base = 0 if seed is None else int(seed)
+        args = [(k, base * 1000003 + i if seed is not None else None) for i in range(len(refs))]
+        return X.exchange(refs, k, X._split_random, args, X._reduce_concat,
+                          [{"shuffle_seed": (base + j) if seed is not None else int(np.random.randint(1 << 30))}
+                           for j in range(k)])
+    total = sum(m["num_rows"] for m in metas)
+    sizes = [total // k + (1 if i < total % k else 0) for i in range(k)]
+    return _repartition_to_sizes(refs, sizes, metas)
+
+
+def _repartition_to_sizes(refs, sizes, metas=None):
+    from .._private.worker import get
+
+    if metas is None:
+        metas = get([m for _, m in refs])
+    bounds = [0]
+    for s in sizes:
+        bounds.append(bounds[-1] + s)
+    starts = []
+    acc = 0
+    for m in metas:
+        starts.append(acc)
+        acc += m["num_rows"]
+    return X.exchange(refs, len(sizes), X._split_by_ranges, [(s, bounds) for s in starts], X._reduce_concat,
+                      [{} for _ in sizes])
+
+
+def _sort(refs, key, descending):
+    from .._private.worker import get
+
+    if not refs:
+        return []
+    k = len(refs)
+    sample_fn = X._remote_fn(_sample_keys, {"num_cpus": 1})
+    samples = get([sample_fn.remote(b, key)[0] for b, _ in refs])
+    allk = np.concatenate([s for s in samples if len(s)]) if any(len(s) for s in samples) else np.array([])
+    if len(allk) == 0:
+        return refs
+    qs = np.quantile(np.sort(allk), np.linspace(0, 1, k + 1)[1:-1]) if k > 1 else np.array([])
+    if descending:
+        qs = qs[::-1].copy()
+        bounds = np.sort(qs)
+    else:
+        bounds = qs
+    return X.exchange(refs, k, X._split_by_key_bounds, [(key, np.sort(bounds), descending) for _ in refs],
+                      X._reduce_concat, [{"sort_key": key, "descending": descending} for _ in range(k)])
+
+
+def _sample_keys(block, key):
+    d = BlockAccessor(block).to_numpy()
+    if key not in d or len(d[key]) == 0:
+        return np.array([]), {}
+    v = d[key]
+    idx = np.random.default_rng(0).choice(len(v), size=min(len(v), 64), replace=False)
+    return v[idx], {}
+
+
+def _zip_blocks(a, b):
+    da = BlockAccessor(a).to_numpy()
+    db = BlockAccessor(b).to_numpy()
+    out = dict(da)
+    for k, v in db.items():
+        out[k if k not in out else f"{k}_1"] = v
+    return out, X._meta(out)
+
+
+def _write_block(block, path, i, fmt, column):
+    acc = BlockAccessor(block)
+    if acc.num_rows() == 0:
+        return None, {}
+    fn = os.path.join(path, f"{i:06d}.{fmt}")
+    if fmt == "parquet":
+        import pyarrow.parquet as pq
+
+        pq.write_table(acc.to_arrow(), fn)
+    elif fmt == "csv":
+        acc.to_pandas().to_csv(fn, index=False)
+    elif fmt == "json":
+        acc.to_pandas().to_json(fn, orient="records", lines=True)
+    elif fmt == "npy":
+        np.save(fn, acc.to_numpy()[column])
+    return fn, {}

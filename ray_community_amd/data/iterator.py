@@ -1,0 +1,123 @@
+"""DataIterator (reference: ``python/ray/data/iterator.py``, ``_internal/block_batching``).
+
+Blocks are prefetched ``prefetch_batches`` ahead (their producing tasks keep running while the
+consumer works), re-batched to exactly ``batch_size`` rows, optionally locally shuffled, and — for
+``iter_torch_batches`` — copied host->device with non-blocking transfers from pinned staging.
+"""
+from __future__ import annotations
+
+import collections
+from typing import Any, Callable, Dict, Iterator, Optional
+
+import numpy as np
+
+from .block import BlockAccessor, concat_blocks
+
+
+class DataIterator:
+    def __init__(self, ds):
+        self._ds = ds
+
+    def _blocks(self, prefetch: int) -> Iterator:
+        from .._private.worker import get, wait
+
+        q = collections.deque()
+        it = self._ds._iter_refs()
+        done = False
+        while True:
+            while not done and len(q) < max(1, prefetch + 1):
+                try:
+                    q.append(next(it)[0])
+                except StopIteration:
+                    done = True
+            if not q:
+                return
+            yield get(q.popleft())
+
+    def iter_batches(self, *, prefetch_batches: int = 1, batch_size: Optional[int] = 256,
+                     batch_format: Optional[str] = "default", drop_last: bool = False,
+                     local_shuffle_buffer_size: Optional[int] = None, local_shuffle_seed: Optional[int] = None,
+                     _collate_fn=None) -> Iterator:
+        rng = np.random.default_rng(local_shuffle_seed)
+        buf = []
+        buf_rows = 0
+        min_rows = max(batch_size or 0, local_shuffle_buffer_size or 0)
+        for blk in self._blocks(prefetch_batches):
+            n = BlockAccessor(blk).num_rows()
+            if n == 0:
+                continue
+            if batch_size is None:
+                yield BlockAccessor(blk).to_batch(batch_format)
+                continue
+            buf.append(blk)
+            buf_rows += n
+            while buf_rows >= min_rows and buf_rows >= batch_size:
+                merged = concat_blocks(buf)
+                acc = BlockAccessor(merged)
+                if local_shuffle_buffer_size:
+                    merged = acc.take(rng.permutation(acc.num_rows()))
+                    acc = BlockAccessor(merged)
+                yield acc.slice(0, batch_size) if batch_format is None else BlockAccessor(
+                    acc.slice(0, batch_size)).to_batch(batch_format)
+                rest = acc.slice(batch_size, acc.num_rows())
+                buf = [rest]
+                buf_rows = acc.num_rows() - batch_size
+        if buf_rows > 0 and not drop_last:
+            merged = concat_blocks(buf)
+            acc = BlockAccessor(merged)
+            if local_shuffle_buffer_size:
+                merged = acc.take(rng.permutation(acc.num_rows()))
+                acc = BlockAccessor(merged)
+            while acc.num_rows() > 0:
+                k = min(batch_size, acc.num_rows())
+                yield BlockAccessor(acc.slice(0, k)).to_batch(batch_format)
+                merged = acc.slice(k, acc.num_rows())
+                acc = BlockAccessor(merged)
+
+    def iter_rows(self, *, prefetch_batches: int = 1) -> Iterator[Dict[str, Any]]:
+        for blk in self._blocks(prefetch_batches):
+            yield from BlockAccessor(blk).iter_rows()
+
+    def iter_torch_batches(self, *, prefetch_batches: int = 1, batch_size: Optional[int] = 256,
+                           dtypes=None, device: str = "auto", collate_fn: Optional[Callable] = None,
+                           drop_last: bool = False, local_shuffle_buffer_size=None, local_shuffle_seed=None,
+                           pin_memory: bool = True) -> Iterator:
+        import torch
+
+        if device == "auto":
+            from ..train.torch.train_loop_utils import get_device
+
+            dev = get_device() if torch.cuda.is_available() else torch.device("cpu")
+        else:
+            dev = torch.device(device) if device is not None else torch.device("cpu")
+        for b in self.iter_batches(prefetch_batches=prefetch_batches, batch_size=batch_size, batch_format="numpy",
+                                   drop_last=drop_last, local_shuffle_buffer_size=local_shuffle_buffer_size,
+                                   local_shuffle_seed=local_shuffle_seed):
+            if collate_fn is not None:
+                yield collate_fn(b)
+                continue
+            out = {}
+            for k, v in b.items():
+                if v.dtype == object:
+                    out[k] = v
+                    continue
+                t = torch.as_tensor(np.ascontiguousarray(v))
+                if dtypes is not None:
+                    dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes
+                    if dt is not None:
+                        t = t.to(dt)
+                if dev.type == "cuda":
+                    if pin_memory:
+                        t = t.pin_memory()
+                    t = t.to(dev, non_blocking=True)
+                out[k] = t
+            yield out
+
+    def to_tf(self, *a, **k):  # pragma: no cover
+        raise NotImplementedError("TensorFlow is not supported on this platform")
+
+    def materialize(self):
+        return self._ds.materialize()
+
+    def stats(self):
+        return self._ds.stats()
