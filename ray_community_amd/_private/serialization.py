@@ -16,9 +16,12 @@ Wire format (one contiguous region — either inline bytes or one shm-store obje
 from __future__ import annotations
 
 import io
+import itertools
+import os
 import pickle
 import struct
 import threading
+import weakref
 from typing import Any, List, Optional, Tuple
 
 import cloudpickle
@@ -97,9 +100,18 @@ def _reduce_cpu_tensor(t):
     return (_rebuild_np_torch, (arr, name, tuple(t.shape)))
 
 
-def _rebuild_gpu_tensor(rebuild_fn, args):
+_LOCAL_GPU: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+_LOCAL_GPU_SEQ = itertools.count()
+
+
+def _rebuild_gpu_tensor(rebuild_fn, args, owner=None):
     import torch
 
+    if owner is not None and owner[0] == os.getpid():
+        # HIP cannot open an IPC handle of the calling process's own allocation: reuse the tensor
+        t = _LOCAL_GPU.get(owner[1])
+        if t is not None:
+            return t
     try:
         # the HIP context must exist (and be current on the storage's device) before the IPC open
         torch.cuda.init()
@@ -120,7 +132,9 @@ def _reduce_gpu_tensor(t):
     if ctx is not None:
         ctx.gpu_tensors.append(t)
     fn, args = reduce_tensor(t)
-    return (_rebuild_gpu_tensor, (fn, args))
+    key = next(_LOCAL_GPU_SEQ)
+    _LOCAL_GPU[key] = t
+    return (_rebuild_gpu_tensor, (fn, args, (os.getpid(), key)))
 
 
 class _Pickler(cloudpickle.CloudPickler):

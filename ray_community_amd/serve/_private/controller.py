@@ -1,0 +1,243 @@
+"""Serve controller (reference: ``serve/_private/{controller,deployment_state,application_state,
+autoscaling_policy}.py``). A detached async actor owning every application's deployments:
+reconciles replica actors to the target count, health-checks them, applies user_config updates,
+and runs the autoscaling loop on the ongoing-request metric."""
+from __future__ import annotations
+
+import asyncio
+import math
+import time
+from typing import Any, Dict, List, Optional
+
+CONTROLLER_NAME = "SERVE_CONTROLLER_ACTOR"
+NAMESPACE = "serve"
+
+
+class _DeploymentState:
+    def __init__(self, app, name, spec):
+        self.app = app
+        self.name = name
+        self.spec = spec
+        self.replicas: Dict[str, Any] = {}  # tag -> actor handle
+        self.version = 0
+        self.target = spec["num_replicas"]
+        self.status = "UPDATING"
+        self.message = ""
+        self.last_scale = 0.0
+        self.counter = 0
+        self.unhealthy_since = {}
+
+
+class ServeController:
+    def __init__(self, http_options: Optional[Dict] = None):
+        self.apps: Dict[str, Dict[str, _DeploymentState]] = {}
+        self.app_meta: Dict[str, Dict] = {}
+        self.http_options = http_options or {}
+        self._loop_task = None
+        self.proxy = None
+        self.handle_queues: Dict[tuple, Dict[str, tuple]] = {}  # (app, dep) -> router id -> (n, ts)
+
+    async def _ensure_loop(self):
+        if self._loop_task is None:
+            self._loop_task = asyncio.ensure_future(self._control_loop())
+
+    # ------------------------------------------------------------------ deploy
+    async def deploy_application(self, app_name: str, deployments: List[Dict], ingress: str, route_prefix: Optional[str]):
+        await self._ensure_loop()
+        old = self.apps.get(app_name, {})
+        new = {}
+        for spec in deployments:
+            st = old.get(spec["name"])
+            if st is None:
+                st = _DeploymentState(app_name, spec["name"], spec)
+            else:
+                code_changed = st.spec["body_hash"] != spec["body_hash"] or st.spec["init_args_blob"] != \
+                    spec["init_args_blob"] or st.spec["actor_options"] != spec["actor_options"]
+                if code_changed:
+                    await self._stop_replicas(st, list(st.replicas))
+                elif spec.get("user_config") != st.spec.get("user_config"):
+                    from ..._private.worker import _core
+
+                    await asyncio.gather(*[r.reconfigure.remote(spec.get("user_config")) for r in st.replicas.values()])
+                st.spec = spec
+                st.status = "UPDATING"
+            st.target = spec["num_replicas"] if not spec.get("autoscaling_config") else max(
+                spec["autoscaling_config"].get("initial_replicas") or spec["autoscaling_config"].get("min_replicas", 1),
+                1 if not st.replicas else len(st.replicas))
+            new[spec["name"]] = st
+        for name, st in old.items():
+            if name not in new:
+                await self._stop_replicas(st, list(st.replicas))
+        self.apps[app_name] = new
+        self.app_meta[app_name] = {"ingress": ingress, "route_prefix": route_prefix, "status": "DEPLOYING",
+                                   "deployed_at": time.time()}
+        await self._reconcile_all()
+        return True
+
+    async def wait_app_running(self, app_name: str, timeout_s: float = 120.0):
+        deadline = time.time() + timeout_s
+        while time.time() < deadline:
+            await self._reconcile_all()
+            meta = self.app_meta.get(app_name)
+            if meta is None:
+                return "NOT_STARTED"
+            if meta["status"] in ("RUNNING", "DEPLOY_FAILED"):
+                return meta["status"]
+            await asyncio.sleep(0.05)
+        return self.app_meta.get(app_name, {}).get("status", "NOT_STARTED")
+
+    async def delete_application(self, app_name: str):
+        deps = self.apps.pop(app_name, {})
+        for st in deps.values():
+            await self._stop_replicas(st, list(st.replicas))
+        self.app_meta.pop(app_name, None)
+        return True
+
+    async def shutdown(self):
+        for app in list(self.apps):
+            await self.delete_application(app)
+        if self._loop_task is not None:
+            self._loop_task.cancel()
+        return True
+
+    # ------------------------------------------------------------------ replicas
+    async def _start_replica(self, st: _DeploymentState):
+        from ...actor import ActorClass
+        from .replica import ServeReplica
+
+        spec = st.spec
+        st.counter += 1
+        tag = f"{st.app}#{st.name}#{st.counter}"
+        opts = dict(spec["actor_options"])
+        mc = spec.get("max_ongoing_requests", 5)
+        opts["max_concurrency"] = max(mc, 1) + 4
+        opts.setdefault("num_cpus", 0)
+        cls = ActorClass(ServeReplica, opts)
+        r = cls.remote(st.app, st.name, tag, spec["body"], spec["init_args"], spec["init_kwargs"],
+                       spec.get("user_config"), spec["is_function"])
+        st.replicas[tag] = r
+        return tag, r
+
+    async def _stop_replicas(self, st, tags):
+        from ..._private.worker import kill
+
+        for t in tags:
+            r = st.replicas.pop(t, None)
+            if r is None:
+                continue
+            try:
+                await asyncio.wait_for(r.prepare_for_shutdown.remote(), 5)
+            except Exception:
+                pass
+            try:
+                kill(r)
+            except Exception:
+                pass
+
+    async def _reconcile_all(self):
+        for app, deps in list(self.apps.items()):
+            healthy_all = True
+            failed = False
+            for st in deps.values():
+                cur = len(st.replicas)
+                if cur < st.target:
+                    for _ in range(st.target - cur):
+                        await self._start_replica(st)
+                elif cur > st.target:
+                    await self._stop_replicas(st, list(st.replicas)[st.target:])
+                # readiness
+                ready = 0
+                for tag, r in list(st.replicas.items()):
+                    try:
+                        await asyncio.wait_for(r.check_health.remote(), 30)
+                        ready += 1
+                    except asyncio.TimeoutError:
+                        pass
+                    except Exception as e:  # noqa
+                        st.message = f"replica {tag} failed: {e}"
+                        st.replicas.pop(tag, None)
+                        failed = True
+                if ready >= st.target and st.target > 0:
+                    st.status = "HEALTHY"
+                elif failed:
+                    st.status = "UNHEALTHY"
+                    healthy_all = False
+                else:
+                    healthy_all = False
+            meta = self.app_meta.get(app)
+            if meta is not None:
+                if healthy_all:
+                    meta["status"] = "RUNNING"
+                elif failed and meta["status"] == "DEPLOYING":
+                    meta["status"] = "DEPLOY_FAILED"
+
+    async def _control_loop(self):
+        while True:
+            try:
+                await self._autoscale()
+                await self._reconcile_all()
+            except Exception:
+                pass
+            await asyncio.sleep(0.5)
+
+    async def _autoscale(self):
+        now = time.time()
+        for deps in self.apps.values():
+            for st in deps.values():
+                ac = st.spec.get("autoscaling_config")
+                if not ac or not st.replicas:
+                    continue
+                try:
+                    counts = await asyncio.gather(*[r.get_num_ongoing.remote() for r in st.replicas.values()])
+                except Exception:
+                    continue
+                now_q = time.time()
+                queued = sum(n for n, ts in self.handle_queues.get((st.app, st.name), {}).values()
+                             if now_q - ts < 30.0)
+                total = sum(counts) + queued
+                target_per = ac.get("target_ongoing_requests", ac.get("target_num_ongoing_requests_per_replica", 2))
+                desired = math.ceil(total / max(target_per, 1e-9)) if total > 0 else ac.get("min_replicas", 1)
+                desired = max(ac.get("min_replicas", 1), min(ac.get("max_replicas", 1), desired))
+                cur = st.target
+                if desired > cur and now - st.last_scale >= ac.get("upscale_delay_s", 0.0):
+                    st.target = desired
+                    st.last_scale = now
+                elif desired < cur and now - st.last_scale >= ac.get("downscale_delay_s", 5.0):
+                    st.target = desired
+                    st.last_scale = now
+
+    async def record_handle_queue(self, app_name: str, deployment: str, router_id: str, n: int):
+        self.handle_queues.setdefault((app_name, deployment), {})[router_id] = (n, time.time())
+        return True
+
+    # ------------------------------------------------------------------ queries
+    async def get_replicas(self, app_name: str, deployment: str):
+        st = self.apps.get(app_name, {}).get(deployment)
+        if st is None:
+            return None
+        return {"replicas": list(st.replicas.items()), "max_ongoing_requests": st.spec.get("max_ongoing_requests", 5),
+                "version": st.version}
+
+    async def get_ingress(self, app_name: str):
+        meta = self.app_meta.get(app_name)
+        return None if meta is None else meta["ingress"]
+
+    async def list_routes(self):
+        return {m["route_prefix"]: (app, m["ingress"]) for app, m in self.app_meta.items() if m["route_prefix"]}
+
+    async def status(self):
+        out = {}
+        for app, deps in self.apps.items():
+            meta = self.app_meta.get(app, {})
+            out[app] = {"status": meta.get("status"), "route_prefix": meta.get("route_prefix"),
+                        "deployments": {n: {"status": st.status, "replicas": len(st.replicas),
+                                            "target": st.target, "message": st.message}
+                                        for n, st in deps.items()}}
+        return out
+
+    async def set_proxy(self, info):
+        self.proxy = info
+        return True
+
+    async def get_proxy(self):
+        return self.proxy

@@ -1,0 +1,97 @@
+"""HTTP plumbing between the proxy and replicas (reference: ``serve/_private/http_util.py``,
+``proxy.py``). The proxy serialises each request to a plain dict; the replica either runs the
+deployment's ASGI app (``@serve.ingress(FastAPI)``) or calls ``__call__(request)`` with a
+Starlette ``Request``, and returns ``(status, headers, body)``."""
+from __future__ import annotations
+
+import inspect
+import json
+from typing import Any, Dict, List, Tuple
+
+
+def _to_response(result) -> Tuple[int, List, bytes]:
+    try:
+        from starlette.responses import Response
+    except ImportError:  # pragma: no cover
+        Response = None
+    if Response is not None and isinstance(result, Response):
+        return result.status_code, [(k.decode(), v.decode()) for k, v in result.raw_headers], result.body
+    if isinstance(result, (bytes, bytearray)):
+        return 200, [("content-type", "application/octet-stream")], bytes(result)
+    if isinstance(result, str):
+        return 200, [("content-type", "text/plain; charset=utf-8")], result.encode()
+    try:
+        import numpy as np
+
+        if isinstance(result, np.ndarray):
+            result = result.tolist()
+    except ImportError:
+        pass
+    return 200, [("content-type", "application/json")], json.dumps(result, default=_jsonable).encode()
+
+
+def _jsonable(o):
+    try:
+        import numpy as np
+
+        if isinstance(o, np.generic):
+            return o.item()
+        if isinstance(o, np.ndarray):
+            return o.tolist()
+    except ImportError:
+        pass
+    return str(o)
+
+
+def _scope(req: Dict) -> Dict:
+    return {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1", "method": req["method"],
+            "scheme": "http", "path": req["path"], "raw_path": req["path"].encode(),
+            "query_string": req.get("query_string", b""), "root_path": req.get("root_path", ""),
+            "headers": [(k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str) else v)
+                        for k, v in req.get("headers", [])],
+            "client": ("127.0.0.1", 0), "server": ("127.0.0.1", 8000)}
+
+
+async def run_asgi_or_call(replica, req: Dict):
+    obj = replica.obj
+    spec = getattr(type(obj), "_serve_ingress_spec", None) if not replica.is_function else None
+    if spec is not None:
+        app = getattr(replica, "_asgi_app", None)
+        if app is None:
+            from ..api import _build_ingress_app
+
+            app = replica._asgi_app = _build_ingress_app(spec, obj)
+        return await _run_asgi(app, req)
+    from starlette.requests import Request
+
+    body = req.get("body", b"")
+
+    async def receive():
+        return {"type": "http.request", "body": body, "more_body": False}
+
+    request = Request(_scope(req), receive)
+    res = await replica._call_user("__call__", (request,), {})
+    return _to_response(res)
+
+
+async def _run_asgi(app, req: Dict):
+    body = req.get("body", b"")
+    scope = _scope(req)
+    sent = {"status": 500, "headers": [], "body": b""}
+    done = {"v": False}
+
+    async def receive():
+        if done["v"]:
+            return {"type": "http.disconnect"}
+        done["v"] = True
+        return {"type": "http.request", "body": body, "more_body": False}
+
+    async def send(msg):
+        if msg["type"] == "http.response.start":
+            sent["status"] = msg["status"]
+            sent["headers"] = [(k.decode(), v.decode()) for k, v in msg.get("headers", [])]
+        elif msg["type"] == "http.response.body":
+            sent["body"] += msg.get("body", b"")
+
+    await app(scope, receive, send)
+    return sent["status"], sent["headers"], sent["body"]

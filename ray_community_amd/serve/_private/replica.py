@@ -1,0 +1,143 @@
+"""Serve replica actor (reference: ``python/ray/serve/_private/replica.py``).
+
+An async actor wrapping one instance of the user's deployment class (or function). Requests
+arrive as actor calls; sync user methods run on a thread pool so the event loop keeps
+accepting (and ``@serve.batch`` can coalesce) concurrent requests up to ``max_ongoing_requests``.
+"""
+from __future__ import annotations
+
+import asyncio
+import inspect
+import os
+import time
+import traceback
+from typing import Any, Dict, Optional
+
+_REPLICA_CTX = {}
+
+
+class ReplicaContext:
+    def __init__(self, app_name, deployment, replica_tag, servable_object=None):
+        self.app_name = app_name
+        self.deployment = deployment
+        self.replica_tag = replica_tag
+        self.replica_id = replica_tag
+        self.servable_object = servable_object
+
+
+class ServeReplica:
+    def __init__(self, app_name: str, deployment_name: str, replica_tag: str, body_blob: bytes, init_args, init_kwargs,
+                 user_config=None, is_function: bool = False):
+        from ..._private import serialization as ser
+        from ..handle import _resolve_handle_args
+
+        self.app_name = app_name
+        self.deployment_name = deployment_name
+        self.tag = replica_tag
+        body = ser.loads_function(body_blob)
+        init_args, init_kwargs = _resolve_handle_args(init_args, init_kwargs)
+        self.is_function = is_function
+        _REPLICA_CTX["ctx"] = ReplicaContext(app_name, deployment_name, replica_tag)
+        if is_function:
+            self.obj = body
+        else:
+            self.obj = body(*init_args, **init_kwargs)
+            if inspect.isawaitable(self.obj):
+                raise TypeError("constructor must not be async")
+        _REPLICA_CTX["ctx"].servable_object = self.obj
+        self.ongoing = 0
+        self.total = 0
+        self.started = time.time()
+        if user_config is not None:
+            self._reconfigure_sync(user_config)
+
+    def _reconfigure_sync(self, user_config):
+        fn = getattr(self.obj, "reconfigure", None)
+        if fn is None:
+            raise ValueError("user_config specified but deployment has no reconfigure() method")
+        r = fn(user_config)
+        if inspect.isawaitable(r):
+            asyncio.get_event_loop().run_until_complete(r) if not asyncio.get_event_loop().is_running() else None
+
+    async def reconfigure(self, user_config):
+        fn = getattr(self.obj, "reconfigure", None)
+        if fn is not None:
+            r = fn(user_config)
+            if inspect.isawaitable(r):
+                await r
+        return True
+
+    async def _call_user(self, method_name, args, kwargs, model_id=None):
+        from .. import multiplex
+
+        tok = multiplex._set_model_id(model_id)
+        try:
+            if self.is_function:
+                fn = self.obj
+            else:
+                fn = getattr(self.obj, method_name or "__call__")
+            if inspect.iscoroutinefunction(fn) or inspect.iscoroutinefunction(getattr(fn, "__call__", None)):
+                return await fn(*args, **kwargs)
+            if inspect.isasyncgenfunction(fn):
+                return [x async for x in fn(*args, **kwargs)]
+            loop = asyncio.get_running_loop()
+            import contextvars
+
+            ctx = contextvars.copy_context()
+            res = await loop.run_in_executor(None, lambda: ctx.run(fn, *args, **kwargs))
+            if inspect.isawaitable(res):
+                res = await res
+            if inspect.isgenerator(res):
+                res = list(res)
+            return res
+        finally:
+            multiplex._reset_model_id(tok)
+
+    async def handle_request(self, method_name, args, kwargs, meta=None):
+        from ..handle import _resolve_handle_args
+
+        meta = meta or {}
+        self.ongoing += 1
+        self.total += 1
+        try:
+            args, kwargs = _resolve_handle_args(args, kwargs)
+            from ..._private.core_worker import ObjectRef
+
+            # chained DeploymentResponses arrive as ObjectRefs: resolve them here, not in the caller
+            args = tuple([(await a) if isinstance(a, ObjectRef) else a for a in args])
+            kwargs = {k: ((await v) if isinstance(v, ObjectRef) else v) for k, v in kwargs.items()}
+            return await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
+        finally:
+            self.ongoing -= 1
+
+    async def handle_http(self, req: Dict):
+        """req: {method, path, query_string, headers, body, root_path}. Returns (status, headers, body)."""
+        self.ongoing += 1
+        self.total += 1
+        try:
+            from .http_util import run_asgi_or_call
+
+            return await run_asgi_or_call(self, req)
+        finally:
+            self.ongoing -= 1
+
+    async def get_num_ongoing(self):
+        return self.ongoing
+
+    async def check_health(self):
+        fn = getattr(self.obj, "check_health", None)
+        if fn is not None:
+            r = fn()
+            if inspect.isawaitable(r):
+                await r
+        return True
+
+    async def stats(self):
+        return {"ongoing": self.ongoing, "total": self.total, "pid": os.getpid(), "tag": self.tag}
+
+    async def prepare_for_shutdown(self):
+        deadline = time.time() + 5
+        while self.ongoing > 0 and time.time() < deadline:
+            await asyncio.sleep(0.05)
+        d = getattr(self.obj, "__del__", None)
+        return True

@@ -1,0 +1,306 @@
+"""Serve public API (reference: ``python/ray/serve/api.py``, ``deployment.py``)."""
+from __future__ import annotations
+
+import copy
+import hashlib
+import inspect
+import time
+from typing import Any, Callable, Dict, List, Optional, Union
+
+from .._private import serialization as ser
+from ._private.controller import CONTROLLER_NAME, NAMESPACE, ServeController
+from .handle import DeploymentHandle, _HandleSpec
+
+_STATE = {"controller": None, "proxy": None, "http": {"host": "127.0.0.1", "port": 8000}}
+
+_DEP_OPTS = {"name", "num_replicas", "ray_actor_options", "max_ongoing_requests", "max_concurrent_queries",
+             "autoscaling_config", "user_config", "health_check_period_s", "health_check_timeout_s",
+             "graceful_shutdown_wait_loop_s", "graceful_shutdown_timeout_s", "route_prefix", "version",
+             "max_queued_requests", "placement_group_bundles", "placement_group_strategy", "logging_config"}
+
+
+class Deployment:
+    def __init__(self, body, name: str, config: Dict):
+        self._body = body
+        self.name = name
+        self._config = config
+
+    @property
+    def func_or_class(self):
+        return self._body
+
+    @property
+    def num_replicas(self):
+        return self._config.get("num_replicas", 1)
+
+    @property
+    def user_config(self):
+        return self._config.get("user_config")
+
+    @property
+    def max_ongoing_requests(self):
+        return self._config.get("max_ongoing_requests", 5)
+
+    def options(self, **kw) -> "Deployment":
+        bad = set(kw) - _DEP_OPTS
+        if bad:
+            raise ValueError(f"invalid deployment options {bad}")
+        cfg = dict(self._config)
+        cfg.update(kw)
+        return Deployment(self._body, kw.get("name", self.name), cfg)
+
+    def bind(self, *args, **kwargs) -> "Application":
+        return Application(self, args, kwargs)
+
+    def __call__(self, *a, **k):
+        raise RuntimeError("Deployments cannot be constructed directly. Use `deployment.bind()` instead.")
+
+
+class Application:
+    def __init__(self, deployment: Deployment, args, kwargs):
+        self._deployment = deployment
+        self._args = args
+        self._kwargs = kwargs
+
+    def _collect(self, app_name, out: Dict[str, Dict]):
+        """Flatten the bound graph into deployment specs (children first)."""
+
+        def conv(x):
+            if isinstance(x, Application):
+                n = x._collect(app_name, out)
+                return _HandleSpec(app_name, n)
+            return x
+
+        args = tuple(conv(a) for a in self._args)
+        kwargs = {k: conv(v) for k, v in self._kwargs.items()}
+        d = self._deployment
+        name = d.name
+        if name in out and out[name]["_app"] is not self:
+            i = 1
+            while f"{name}_{i}" in out:
+                i += 1
+            name = f"{name}_{i}"
+        blob = ser.dumps_function(d._body)
+        cfg = d._config
+        init_blob = ser.serialize((args, kwargs)).to_bytes()
+        ac = cfg.get("autoscaling_config")
+        if ac is not None and not isinstance(ac, dict):
+            ac = dict(ac.__dict__)
+        out[name] = {"name": name, "body": blob, "body_hash": hashlib.sha1(blob).hexdigest(),
+                     "init_args": args, "init_kwargs": kwargs, "init_args_blob": hashlib.sha1(init_blob).hexdigest(),
+                     "is_function": not inspect.isclass(d._body),
+                     "num_replicas": 1 if cfg.get("num_replicas") in (None, "auto") else int(cfg["num_replicas"]),
+                     "actor_options": dict(cfg.get("ray_actor_options") or {}),
+                     "max_ongoing_requests": cfg.get("max_ongoing_requests") or cfg.get("max_concurrent_queries") or 5,
+                     "autoscaling_config": ac if ac else ({"min_replicas": 1, "max_replicas": 100,
+                                                           "target_ongoing_requests": 2}
+                                                          if cfg.get("num_replicas") == "auto" else None),
+                     "user_config": cfg.get("user_config"), "_app": self}
+        return name
+
+
+def deployment(_func_or_class=None, *, name: Optional[str] = None, num_replicas: Union[int, str, None] = None,
+               ray_actor_options: Optional[Dict] = None, max_ongoing_requests: Optional[int] = None,
+               max_concurrent_queries: Optional[int] = None, autoscaling_config=None, user_config=None,
+               health_check_period_s=None, health_check_timeout_s=None, graceful_shutdown_wait_loop_s=None,
+               graceful_shutdown_timeout_s=None, route_prefix=None, version=None, max_queued_requests=None,
+               placement_group_bundles=None, placement_group_strategy=None, logging_config=None):
+    cfg = {k: v for k, v in dict(num_replicas=num_replicas, ray_actor_options=ray_actor_options,
+                                 max_ongoing_requests=max_ongoing_requests or max_concurrent_queries,
+                                 autoscaling_config=autoscaling_config, user_config=user_config).items()
+           if v is not None}
+    if num_replicas is not None and autoscaling_config is not None and num_replicas != "auto":
+        raise ValueError("Manually setting num_replicas is not allowed when autoscaling_config is provided.")
+
+    def deco(body):
+        return Deployment(body, name or body.__name__, cfg)
+
+    return deco(_func_or_class) if _func_or_class is not None else deco
+
+
+# ------------------------------------------------------------------------------ controller
+def _get_controller():
+    from .._private import worker as w
+    from ..actor import ActorClass
+
+    if not w.is_initialized():
+        w.init()
+    c = _STATE["controller"]
+    if c is not None:
+        return c
+    try:
+        c = w.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+    except ValueError:
+        c = ActorClass(ServeController, {"name": CONTROLLER_NAME, "namespace": NAMESPACE, "lifetime": "detached",
+                                         "num_cpus": 0, "max_concurrency": 1000}).options(get_if_exists=True).remote()
+    _STATE["controller"] = c
+    return c
+
+
+def start(http_options: Optional[Dict] = None, detached: bool = True, proxy_location=None, **kw):
+    if http_options:
+        _STATE["http"].update({k: v for k, v in http_options.items() if k in ("host", "port")})
+    _get_controller()
+
+
+def _ensure_proxy():
+    from .._private import worker as w
+    from ..actor import ActorClass
+    from ._private.proxy import HTTPProxy
+
+    if _STATE["proxy"] is not None:
+        return
+    h = _STATE["http"]
+    try:
+        p = w.get_actor("SERVE_PROXY_ACTOR", namespace=NAMESPACE)
+    except ValueError:
+        p = ActorClass(HTTPProxy, {"name": "SERVE_PROXY_ACTOR", "namespace": NAMESPACE, "lifetime": "detached",
+                                   "num_cpus": 0, "max_concurrency": 100}).remote(h["host"], h["port"])
+    w.get(p.ready.remote())
+    _STATE["proxy"] = p
+
+
+def run(target: Union[Application, Deployment], *, name: str = "default", route_prefix: Optional[str] = "/",
+        blocking: bool = False, _blocking: bool = True, logging_config=None, http: bool = True,
+        **kw) -> DeploymentHandle:
+    from .._private import worker as w
+
+    if isinstance(target, Deployment):
+        target = target.bind()
+    if not isinstance(target, Application):
+        raise TypeError("serve.run expects an Application (deployment.bind(...))")
+    specs: Dict[str, Dict] = {}
+    ingress = target._collect(name, specs)
+    for s in specs.values():
+        s.pop("_app", None)
+    ctrl = _get_controller()
+    w.get(ctrl.deploy_application.remote(name, list(specs.values()), ingress, route_prefix))
+    status = w.get(ctrl.wait_app_running.remote(name, 300.0))
+    if status != "RUNNING":
+        st = w.get(ctrl.status.remote())
+        raise RuntimeError(f"Deploying app '{name}' failed: {st.get(name)}")
+    if http and route_prefix is not None:
+        _ensure_proxy()
+    handle = DeploymentHandle(ingress, name)
+    if blocking:
+        while True:
+            time.sleep(1)
+    return handle
+
+
+def delete(name: str, _blocking: bool = True):
+    from .._private import worker as w
+
+    w.get(_get_controller().delete_application.remote(name))
+
+
+def status():
+    from .._private import worker as w
+
+    return _ServeStatus(w.get(_get_controller().status.remote()))
+
+
+class _ServeStatus(dict):
+    @property
+    def applications(self):
+        return {k: _AppStatus(v) for k, v in self.items()}
+
+
+class _AppStatus(dict):
+    @property
+    def status(self):
+        return self["status"]
+
+    @property
+    def deployments(self):
+        return self["deployments"]
+
+
+def shutdown():
+    from .._private import worker as w
+
+    if not w.is_initialized():
+        return
+    try:
+        c = _STATE["controller"] or w.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+        w.get(c.shutdown.remote())
+        w.kill(c)
+    except Exception:
+        pass
+    try:
+        p = _STATE["proxy"] or w.get_actor("SERVE_PROXY_ACTOR", namespace=NAMESPACE)
+        w.get(p.shutdown.remote())
+        w.kill(p)
+    except Exception:
+        pass
+    _STATE["controller"] = None
+    _STATE["proxy"] = None
+    from .handle import _Router
+
+    _Router._routers.clear()
+
+
+def get_app_handle(name: str) -> DeploymentHandle:
+    from .._private import worker as w
+
+    ingress = w.get(_get_controller().get_ingress.remote(name))
+    if ingress is None:
+        raise ValueError(f"Application '{name}' does not exist.")
+    return DeploymentHandle(ingress, name)
+
+
+def get_deployment_handle(deployment_name: str, app_name: Optional[str] = None) -> DeploymentHandle:
+    return DeploymentHandle(deployment_name, app_name or "default")
+
+
+def get_replica_context():
+    from ._private.replica import _REPLICA_CTX
+
+    ctx = _REPLICA_CTX.get("ctx")
+    if ctx is None:
+        raise RuntimeError("`serve.get_replica_context()` may only be called from within a Serve replica.")
+    return ctx
+
+
+# ------------------------------------------------------------------------------ ingress
+def ingress(app):
+    """Class decorator serving a FastAPI app from the deployment (``@serve.ingress(app)``).
+
+    The FastAPI object itself is never shipped to replicas (its pydantic/starlette internals do
+    not survive pickling by value); instead the route table is captured as a picklable recipe and
+    each replica rebuilds an app whose class routes are bound to the replica's instance."""
+
+    def deco(cls):
+        cls._serve_ingress_spec = _capture_routes(app, cls)
+        return cls
+
+    return deco
+
+
+def _capture_routes(app, cls):
+    try:
+        from fastapi.routing import APIRoute
+    except ImportError:
+        raise ImportError("@serve.ingress requires fastapi")
+    meta = {k: getattr(app, k, None) for k in ("title", "version", "description")}
+    routes = []
+    for r in app.router.routes:
+        if not isinstance(r, APIRoute):
+            continue  # docs/openapi routes are recreated by the replica's FastAPI()
+        fn = r.endpoint
+        is_method = getattr(fn, "__qualname__", "").startswith(cls.__qualname__ + ".")
+        routes.append({"path": r.path, "endpoint": fn.__name__ if is_method else fn, "is_method": is_method,
+                       "methods": sorted(r.methods or ()), "name": r.name, "status_code": r.status_code,
+                       "response_model": r.response_model, "tags": list(r.tags or [])})
+    return {"meta": meta, "routes": routes}
+
+
+def _build_ingress_app(spec, instance):
+    from fastapi import FastAPI
+
+    app = FastAPI(**{k: v for k, v in spec["meta"].items() if v is not None})
+    for r in spec["routes"]:
+        ep = getattr(instance, r["endpoint"]) if r["is_method"] else r["endpoint"]
+        app.add_api_route(r["path"], ep, methods=r["methods"], name=r["name"], status_code=r["status_code"],
+                          response_model=r["response_model"], tags=r["tags"] or None)
+    return app

@@ -1,0 +1,295 @@
+"""Deployment handles + router (reference: ``serve/handle.py``, ``_private/router.py``,
+``_private/replica_scheduler/pow_2_scheduler.py``).
+
+Routing is power-of-two-choices on the caller's view of in-flight requests per replica, capped at
+``max_ongoing_requests`` (requests queue on the caller when every replica is saturated).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import concurrent.futures
+import random
+import threading
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+from .._private.core_worker import ObjectRef
+
+
+class _HandleSpec:
+    """Placeholder for a bound deployment inside another deployment's init args."""
+
+    def __init__(self, app_name, deployment_name):
+        self.app_name = app_name
+        self.deployment_name = deployment_name
+
+
+def _resolve_handle_args(args, kwargs):
+    def conv(x):
+        if isinstance(x, _HandleSpec):
+            return DeploymentHandle(x.deployment_name, x.app_name)
+        if isinstance(x, DeploymentResponse):
+            return x._to_object_ref_sync()
+        return x
+
+    return tuple(conv(a) for a in args), {k: conv(v) for k, v in kwargs.items()}
+
+
+class _Router:
+    """Per-(app, deployment) request router living in the caller's process.
+
+    ``submit`` never blocks: a request goes straight to a replica chosen by power-of-two-choices
+    when one has spare capacity, otherwise it waits in a local FIFO that is drained as replies
+    come back (or new replicas appear). The queue length is reported to the controller so the
+    autoscaler sees demand that has not reached any replica yet."""
+
+    _routers: Dict[Tuple[str, str], "_Router"] = {}
+    _lock = threading.Lock()
+
+    def __init__(self, app, dep):
+        self.app = app
+        self.dep = dep
+        self.id = f"{id(self):x}-{random.getrandbits(32):08x}"
+        self.replicas: List[Tuple[str, Any]] = []
+        self.inflight: Dict[str, int] = {}
+        self.max_ongoing = 5
+        self.last_refresh = 0.0
+        self.cv = threading.Condition()
+        self.queue: "collections.deque" = collections.deque()
+        self._reported = 0
+        self._drainer: Optional[threading.Thread] = None
+
+    @classmethod
+    def get(cls, app, dep):
+        with cls._lock:
+            r = cls._routers.get((app, dep))
+            if r is None:
+                r = _Router(app, dep)
+                cls._routers[(app, dep)] = r
+            return r
+
+    def _refresh(self, force=False, period=2.0):
+        now = time.time()
+        if not force and self.replicas and now - self.last_refresh < period:
+            return
+        from .api import _get_controller
+        from .._private.worker import get
+
+        info = get(_get_controller().get_replicas.remote(self.app, self.dep))
+        self.last_refresh = now
+        if info is None:
+            raise RuntimeError(f"Deployment {self.dep} of app {self.app} does not exist")
+        with self.cv:
+            self.replicas = info["replicas"]
+            self.max_ongoing = info["max_ongoing_requests"]
+            live = {t for t, _ in self.replicas}
+            for tag in live:
+                self.inflight.setdefault(tag, 0)
+            for tag in list(self.inflight):
+                if tag not in live:
+                    self.inflight.pop(tag)
+
+    def _pick_locked(self):
+        cands = [(t, a) for t, a in self.replicas if self.inflight.get(t, 0) < self.max_ongoing]
+        if not cands:
+            return None
+        pick = random.sample(cands, min(2, len(cands)))
+        tag, actor = min(pick, key=lambda x: self.inflight.get(x[0], 0))
+        self.inflight[tag] = self.inflight.get(tag, 0) + 1
+        return tag, actor
+
+    def choose(self, timeout_s=60.0):
+        """Blocking pick (used by callers that manage the call themselves)."""
+        deadline = time.time() + timeout_s
+        while True:
+            self._refresh()
+            with self.cv:
+                got = self._pick_locked()
+                if got is not None:
+                    return got
+                self.cv.wait(0.05)
+            if not self.replicas:
+                self._refresh(force=True)
+            if time.time() > deadline:
+                raise TimeoutError(f"no replica of {self.dep} available")
+
+    def submit(self, method: str, args, kwargs, meta, actor_method: str = "handle_request"):
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        self._refresh()
+        with self.cv:
+            self.queue.append((actor_method, method, args, kwargs, meta, fut))
+            self._drain_locked()
+            pending = bool(self.queue)
+        if pending:
+            self._ensure_drainer()
+        self._report()
+        return fut
+
+    def _drain_locked(self):
+        while self.queue:
+            got = self._pick_locked()
+            if got is None:
+                return
+            tag, actor = got
+            actor_method, method, args, kwargs, meta, fut = self.queue.popleft()
+            try:
+                if actor_method == "handle_request":
+                    ref = actor.handle_request.remote(method, args, kwargs, meta)
+                else:
+                    ref = getattr(actor, actor_method).remote(*args)
+            except Exception as e:  # noqa
+                self.inflight[tag] = max(0, self.inflight.get(tag, 0) - 1)
+                fut.set_exception(e)
+                continue
+            ref.future().add_done_callback(lambda f, tag=tag: self.done(tag))
+            fut.set_result((ref, tag))
+
+    def _ensure_drainer(self):
+        with self.cv:
+            if self._drainer is not None and self._drainer.is_alive():
+                return
+            self._drainer = threading.Thread(target=self._drain_loop, daemon=True, name=f"serve-router-{self.dep}")
+            self._drainer.start()
+
+    def _drain_loop(self):
+        while True:
+            with self.cv:
+                if not self.queue:
+                    self._drainer = None
+                    break
+                self.cv.wait(0.1)
+            try:
+                self._refresh(period=0.5)
+            except Exception:  # noqa
+                pass
+            with self.cv:
+                self._drain_locked()
+            self._report()
+        self._report()
+
+    def _report(self):
+        n = len(self.queue)
+        if n == self._reported:
+            return
+        self._reported = n
+        try:
+            from .api import _get_controller
+
+            _get_controller().record_handle_queue.remote(self.app, self.dep, self.id, n)
+        except Exception:  # noqa
+            pass
+
+    def done(self, tag):
+        with self.cv:
+            self.inflight[tag] = max(0, self.inflight.get(tag, 0) - 1)
+            self._drain_locked()
+            self.cv.notify_all()
+
+    def replica_died(self, tag):
+        with self.cv:
+            self.replicas = [(t, a) for t, a in self.replicas if t != tag]
+            self.inflight.pop(tag, None)
+        self.last_refresh = 0.0
+
+
+class DeploymentResponse:
+    """Future for one request; the underlying ObjectRef exists once the router assigned a replica."""
+
+    def __init__(self, fut: concurrent.futures.Future):
+        self._fut = fut
+
+    @property
+    def _ref(self) -> ObjectRef:
+        return self._fut.result()[0]
+
+    def result(self, *, timeout_s: Optional[float] = None):
+        from .._private.worker import get
+
+        t0 = time.time()
+        ref = self._fut.result(timeout=timeout_s)[0]
+        rem = None if timeout_s is None else max(0.0, timeout_s - (time.time() - t0))
+        return get(ref, timeout=rem)
+
+    async def _await(self):
+        ref, _ = await asyncio.wrap_future(self._fut)
+        return await ref
+
+    def __await__(self):
+        return self._await().__await__()
+
+    async def _to_object_ref(self):
+        return (await asyncio.wrap_future(self._fut))[0]
+
+    def _to_object_ref_sync(self):
+        return self._ref
+
+    def cancel(self):
+        from .._private.worker import cancel
+
+        if not self._fut.done():
+            self._fut.cancel()
+            return
+        cancel(self._ref)
+
+
+class DeploymentResponseGenerator:
+    def __init__(self, resp: DeploymentResponse):
+        self._resp = resp
+        self._items = None
+
+    def __iter__(self):
+        return iter(self._resp.result())
+
+    def __aiter__(self):
+        async def gen():
+            for x in await self._resp:
+                yield x
+
+        return gen()
+
+
+class DeploymentHandle:
+    def __init__(self, deployment_name: str, app_name: str = "default", *, method_name: str = "__call__",
+                 multiplexed_model_id: str = "", stream: bool = False):
+        self.deployment_name = deployment_name
+        self.app_name = app_name
+        self._method = method_name
+        self._model_id = multiplexed_model_id
+        self._stream = stream
+
+    def options(self, *, method_name: Optional[str] = None, multiplexed_model_id: Optional[str] = None,
+                stream: Optional[bool] = None, use_new_handle_api=None, **kw) -> "DeploymentHandle":
+        return DeploymentHandle(self.deployment_name, self.app_name,
+                                method_name=method_name or self._method,
+                                multiplexed_model_id=self._model_id if multiplexed_model_id is None else
+                                multiplexed_model_id,
+                                stream=self._stream if stream is None else stream)
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return self.options(method_name=name)
+
+    def remote(self, *args, **kwargs):
+        router = _Router.get(self.app_name, self.deployment_name)
+        args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
+        kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v) for k, v in kwargs.items()}
+        meta = {"multiplexed_model_id": self._model_id} if self._model_id else {}
+        resp = DeploymentResponse(router.submit(self._method, args, kwargs, meta))
+        return DeploymentResponseGenerator(resp) if self._stream else resp
+
+    def __reduce__(self):
+        return (DeploymentHandle, (self.deployment_name, self.app_name), {"_method": self._method,
+                                                                          "_model_id": self._model_id,
+                                                                          "_stream": self._stream})
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+
+    def __repr__(self):
+        return f"DeploymentHandle(deployment='{self.deployment_name}', app='{self.app_name}')"
+
+
+RayServeHandle = DeploymentHandle
+RayServeSyncHandle = DeploymentHandle
