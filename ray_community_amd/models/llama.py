@@ -37,6 +37,7 @@ class LlamaConfig:
     tie_embeddings: bool = False
     init_std: float = 0.02
     name: str = "llama"
+    attn_impl: str = "hip"  # "hip" (gfx950 flash attention kernels) | "sdpa" (torch SDPA / aotriton)
 
     @property
     def head_dim(self) -> int:
@@ -90,6 +91,9 @@ class Attention(nn.Module):
         T = B * S
         qkv = self.qkv(x)  # [T, (Hq+2Hk)*D]
         qkv = ops.apply_rope_(qkv, cs, S, Hq, Hk, D, positions)
+        if qkv.is_cuda and cfg.attn_impl == "hip" and ops.flash_attention_supported(S, D, Hq, Hk):
+            # gfx950 flash attention straight off the fused projection; backward fills dqkv directly
+            return self.o(ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
         q = qkv[:, : Hq * D].view(B, S, Hq, D).transpose(1, 2)
         k = qkv[:, Hq * D: (Hq + Hk) * D].view(B, S, Hk, D).transpose(1, 2)
         v = qkv[:, (Hq + Hk) * D:].view(B, S, Hk, D).transpose(1, 2)

@@ -28,6 +28,9 @@ __all__ = [
     "standardize_",
     "batched_concat",
     "image_normalize",
+    "flash_attention",
+    "flash_attention_qkv",
+    "flash_attention_supported",
     "kernels_available",
 ]
 
@@ -374,3 +377,108 @@ def image_normalize(u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), d
                                     ctypes.cast(sa, ctypes.c_void_p), 0 if dtype == torch.bfloat16 else 1,
                                     stream_ptr(u8.device)), "image_normalize")
     return out
+
+
+# --------------------------------------------------------------------------------- attention
+def flash_attention_supported(seq_len: int, head_dim: int, n_q_heads: int, n_kv_heads: int) -> bool:
+    """Shapes the gfx950 flash-attention kernels cover (others use torch SDPA)."""
+    return seq_len % 128 == 0 and head_dim in (64, 128) and n_kv_heads > 0 and n_q_heads % n_kv_heads == 0
+
+
+def _attn_fwd(q, k, v, o, lse, B, S, Hq, Hk, D, sq, sk, sv, so, scale, causal):
+    check(lib().rca_attn_fwd(q, k, v, o, lse, B, S, Hq, Hk, D, sq, sk, sv, so, scale, int(causal), stream_ptr()),
+          "rca_attn_fwd")
+
+
+def _attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, strides, scale, causal):
+    check(lib().rca_attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, *strides, scale, int(causal),
+                             stream_ptr()), "rca_attn_bwd")
+
+
+class _FlashAttnQKV(torch.autograd.Function):
+    """Attention straight off the fused qkv projection ``[B*S, (Hq+2Hk)*D]``; output ``[B*S, Hq*D]``.
+    The backward writes dQ/dK/dV into one fused ``dqkv`` gradient (no slicing copies)."""
+
+    @staticmethod
+    def forward(ctx, qkv, B, S, Hq, Hk, D, causal, scale):
+        W = (Hq + 2 * Hk) * D
+        o = torch.empty(B * S, Hq * D, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(B, Hq, S, device=qkv.device, dtype=torch.float32)
+        base, es = qkv.data_ptr(), qkv.element_size()
+        _attn_fwd(base, base + es * Hq * D, base + es * (Hq + Hk) * D, o.data_ptr(), lse.data_ptr(), B, S, Hq, Hk, D,
+                  W, W, W, Hq * D, scale, causal)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (B, S, Hq, Hk, D, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        B, S, Hq, Hk, D, causal, scale = ctx.cfg
+        do = do.contiguous()
+        W = (Hq + 2 * Hk) * D
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B, Hq, S, device=qkv.device, dtype=torch.float32)
+        base, gb, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+        _attn_bwd(base, base + es * Hq * D, base + es * (Hq + Hk) * D, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                  delta.data_ptr(), gb, gb + es * Hq * D, gb + es * (Hq + Hk) * D, B, S, Hq, Hk, D,
+                  (W, W, W, Hq * D, Hq * D, W, W, W), scale, causal)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def flash_attention_qkv(qkv, B: int, S: int, Hq: int, Hk: int, D: int, causal: bool = True, scale=None):
+    """Fused-qkv attention: ``qkv`` is ``[B*S, (Hq+2Hk)*D]`` (token-major, heads contiguous)."""
+    scale = float(D ** -0.5 if scale is None else scale)
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and flash_attention_supported(S, D, Hq, Hk):
+        return _FlashAttnQKV.apply(qkv.contiguous(), B, S, Hq, Hk, D, causal, scale)
+    q = qkv[:, : Hq * D].view(B, S, Hq, D)
+    k = qkv[:, Hq * D: (Hq + Hk) * D].view(B, S, Hk, D)
+    v = qkv[:, (Hq + Hk) * D:].view(B, S, Hk, D)
+    return ref.attention_ref(q, k, v, causal, scale).reshape(B * S, Hq * D)
+
+
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        B, S, Hq, D = q.shape
+        Hk = k.shape[2]
+        o = torch.empty(B, S, Hq, D, device=q.device, dtype=q.dtype)
+        lse = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+        _attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, Hq, Hk, D,
+                  q.stride(1), k.stride(1), v.stride(1), o.stride(1), scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.cfg = (causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        causal, scale = ctx.cfg
+        B, S, Hq, D = q.shape
+        Hk = k.shape[2]
+        do = do.contiguous()
+        dq = torch.empty(B, S, Hq, D, device=q.device, dtype=q.dtype)
+        dk = torch.empty(B, S, Hk, D, device=q.device, dtype=q.dtype)
+        dv = torch.empty(B, S, Hk, D, device=q.device, dtype=q.dtype)
+        delta = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+        _attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                  delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, S, Hq, Hk, D,
+                  (q.stride(1), k.stride(1), v.stride(1), o.stride(1), do.stride(1), dq.stride(1), dk.stride(1),
+                   dv.stride(1)), scale, causal)
+        return dq, dk, dv, None, None
+
+
+def _token_major_ok(t):
+    B, S, H, D = t.shape
+    return t.stride(3) == 1 and t.stride(2) == D and t.stride(0) == S * t.stride(1)
+
+
+def flash_attention(q, k, v, causal: bool = True, scale=None):
+    """Attention on ``[B, S, H, D]`` tensors (GQA when k/v have fewer heads). Returns ``[B, S, Hq, D]``."""
+    B, S, Hq, D = q.shape
+    Hk = k.shape[2]
+    scale = float(D ** -0.5 if scale is None else scale)
+    if (q.is_cuda and q.dtype == torch.bfloat16 and flash_attention_supported(S, D, Hq, Hk)
+            and all(_token_major_ok(t) for t in (q, k, v))):
+        return _FlashAttn.apply(q, k, v, causal, scale)
+    return ref.attention_ref(q, k, v, causal, scale)

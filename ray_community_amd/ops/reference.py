@@ -79,3 +79,20 @@ def image_normalize_ref(u8, mean, std, dtype=torch.bfloat16):
     m = torch.tensor(mean, dtype=torch.float32).view(1, 1, 1, -1)
     s = torch.tensor(std, dtype=torch.float32).view(1, 1, 1, -1)
     return ((x - m) / s).permute(0, 3, 1, 2).contiguous().to(dtype)
+
+
+def attention_ref(q, k, v, causal: bool = True, scale=None):
+    """fp32 attention on ``[B, S, H, D]`` tensors (GQA by head repetition); returns q's dtype."""
+    B, S, Hq, D = q.shape
+    Hk = k.shape[2]
+    scale = D ** -0.5 if scale is None else scale
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    if Hk != Hq:
+        kf = kf.repeat_interleave(Hq // Hk, dim=1)
+        vf = vf.repeat_interleave(Hq // Hk, dim=1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        m = torch.ones(S, k.shape[1], dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(m, float("-inf"))
+    o = torch.matmul(torch.softmax(s, dim=-1), vf)
+    return o.transpose(1, 2).to(q.dtype)

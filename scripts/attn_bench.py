@@ -1,9 +1,14 @@
-"""Attention backend microbenchmark on MI355X: SDPA flash (aotriton / ck) fwd+bwd at the
-Llama-3-8B bench shape (B=2, Hq=32, Hkv=8, S=4096, D=128, causal)."""
+"""Attention microbenchmark on MI355X at the Llama-3-8B bench shape (B=2, Hq=32, Hkv=8, S=4096,
+D=128, causal): the framework's gfx950 flash attention vs torch SDPA (aotriton)."""
+import os
+import sys
 import time
 
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ray_community_amd import ops  # noqa: E402
 
 
 def bench(fn, iters=10):
@@ -18,42 +23,31 @@ def bench(fn, iters=10):
 
 
 def main():
-    B, Hq, Hk, S, D = 2, 32, 8, 4096, 128
+    B, Hq, Hk, S, D = 2, 32, 8, int(os.environ.get("ATTN_S", 4096)), 128
     dev = "cuda"
-    q = torch.randn(B, Hq, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    k = torch.randn(B, Hk, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    v = torch.randn(B, Hk, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    do = torch.randn(B, Hq, S, D, device=dev, dtype=torch.bfloat16)
+    qkv = torch.randn(B * S, (Hq + 2 * Hk) * D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    do = torch.randn(B * S, Hq * D, device=dev, dtype=torch.bfloat16)
     flops_f = 4 * B * Hq * S * S * D / 2
-    libs = ["default"]
-    try:
-        print("preferred rocm fa lib:", torch.backends.cuda.preferred_rocm_fa_library())
-        libs = ["aotriton", "ck"]
-    except Exception as e:
-        print("no preferred_rocm_fa_library:", e)
-    for lib in libs:
-        try:
-            if lib != "default":
-                torch.backends.cuda.preferred_rocm_fa_library(lib)
-            for gqa in (True, False):
-                def fwd():
-                    if gqa:
-                        return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
-                    kk = k.repeat_interleave(Hq // Hk, dim=1)
-                    vv = v.repeat_interleave(Hq // Hk, dim=1)
-                    return F.scaled_dot_product_attention(q, kk, vv, is_causal=True)
 
-                def fb():
-                    o = fwd()
-                    o.backward(do)
+    def run(name, fwd):
+        def fb():
+            fwd().backward(do)
+        tf = bench(fwd)
+        tfb = bench(fb)
+        print(f"{name:10s}: fwd {tf:.3f} ms ({flops_f / tf / 1e9:.0f} TF)  fwd+bwd {tfb:.3f} ms "
+              f"(bwd {tfb - tf:.3f} ms, {2.5 * flops_f / (tfb - tf) / 1e9:.0f} TF)", flush=True)
 
-                with torch.nn.attention.sdpa_kernel(torch.nn.attention.SDPBackend.FLASH_ATTENTION):
-                    tf = bench(fwd)
-                    tfb = bench(fb)
-                print(f"{lib:9s} gqa={gqa}: fwd {tf:.2f} ms ({flops_f/tf/1e9:.0f} TF)  fwd+bwd {tfb:.2f} ms "
-                      f"(bwd {tfb-tf:.2f} ms, {2.5*flops_f/(tfb-tf)/1e9:.0f} TF)")
-        except Exception as e:
-            print(lib, "failed:", repr(e)[:300])
+    run("rca-hip", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
+
+    def sdpa():
+        q = qkv[:, : Hq * D].view(B, S, Hq, D).transpose(1, 2)
+        k = qkv[:, Hq * D: (Hq + Hk) * D].view(B, S, Hk, D).transpose(1, 2)
+        v = qkv[:, (Hq + Hk) * D:].view(B, S, Hk, D).transpose(1, 2)
+        return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True).transpose(1, 2).reshape(
+            B * S, Hq * D)
+
+    with torch.nn.attention.sdpa_kernel(torch.nn.attention.SDPBackend.FLASH_ATTENTION):
+        run("sdpa", sdpa)
 
 
 if __name__ == "__main__":

@@ -62,3 +62,24 @@ def test_swiglu_rope_cpu_shapes():
     # v heads untouched, position-0 rows unchanged
     assert torch.equal(out[:, 3 * 16:], qkv[:, 3 * 16:])
     assert torch.allclose(out[0], qkv[0])
+
+
+def test_attention_reference_matches_sdpa():
+    import torch.nn.functional as F
+
+    from ray_community_amd import ops
+    from ray_community_amd.ops import reference as ref
+
+    B, S, Hq, Hk, D = 2, 64, 4, 2, 32
+    q = torch.randn(B, S, Hq, D)
+    k = torch.randn(B, S, Hk, D)
+    v = torch.randn(B, S, Hk, D)
+    o = ref.attention_ref(q, k, v, True)
+    kk = k.repeat_interleave(2, dim=2)
+    vv = v.repeat_interleave(2, dim=2)
+    o2 = F.scaled_dot_product_attention(q.transpose(1, 2), kk.transpose(1, 2), vv.transpose(1, 2), is_causal=True)
+    assert torch.allclose(o, o2.transpose(1, 2), atol=1e-5)
+    # CPU tensors take the reference path of the public op
+    assert torch.allclose(ops.flash_attention(q, k, v, True), o)
+    qkv = torch.cat([q.reshape(B * S, -1), k.reshape(B * S, -1), v.reshape(B * S, -1)], dim=1)
+    assert torch.allclose(ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D), o.reshape(B * S, -1), atol=1e-6)
