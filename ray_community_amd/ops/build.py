@@ -18,6 +18,10 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_NAME = "libraca_kernels.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 ARCH = os.environ.get("RCA_OFFLOAD_ARCH", "gfx950")
+# Keep loop-carried MFMA accumulators in the accumulator file: without this hipcc copies every
+# AGPR-resident accumulator to VGPRs and back around each loop iteration once a kernel's live set
+# exceeds 256 VGPRs (the one-wave-per-SIMD attention dK/dV kernel: 574 v_accvgpr moves -> 26).
+EXTRA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
 
 
 def _hipcc() -> str:
@@ -38,6 +42,7 @@ def _digest() -> str:
             h.update(os.path.basename(p).encode())
             h.update(f.read())
     h.update(ARCH.encode())
+    h.update(" ".join(EXTRA_FLAGS).encode())
     return h.hexdigest()[:16]
 
 
@@ -59,7 +64,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     procs = []
     for src in _sources():
         obj = os.path.join(tmpdir, os.path.basename(src) + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj] + EXTRA_FLAGS
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), src))

@@ -26,6 +26,8 @@
 // examples (python/ray/train/examples, release/train_tests) — the reference itself has no kernel.
 #include "common.h"
 
+#include <type_traits>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -49,34 +51,35 @@ __device__ __forceinline__ f32x16 zero16() {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// LDS image of a [rows][D] bf16 tile: 16-byte chunk `ch` of row `row`, XOR-swizzled so that
-// (a) 16 lanes reading the same chunk of 16 consecutive rows (ds_read_b128 operand rows) and
-// (b) ds_read_b64_tr_b16 reading 4 rows x 32 columns per 32-lane half are both conflict-free.
+// LDS image of a [rows][D] bf16 tile (cdna_hip_programming.md T11 image (a)): 8-row x 32-column
+// subtiles of 512 B, chunk XOR-swizzled inside each 64-B row piece. Both operand reads the kernels
+// need are conflict-free on it and AFFINE in the loop indices, so every LDS read is one of two
+// per-lane base registers plus an immediate offset:
+//   row operand   (rows l32 + 32t, chunk 2kk + h):            rb[kk&1] + 4*G8*t + 512*(kk>>1)
+//   transposed op (rows R0 + 4h + q (+8), cols 32db+16g+4p):  tb[rd]   + G8*(R0/8 + rd) + 512*db
 template <int D>
-__device__ __forceinline__ int soff(int row, int ch) {
-  if constexpr (D == 128) {
-    return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
-  } else {
-    return row * 128 + ((ch ^ (((row & 1) << 2) | ((row >> 1) & 3))) << 4);
+struct Img {
+  static constexpr int G8 = D * 16;  // bytes per 8-row group
+  __device__ static __forceinline__ int off(int row, int ch) {
+    return G8 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
   }
+  __device__ static __forceinline__ int row_base(int l32, int h, int e) {
+    return G8 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 * e + h) ^ ((l32 >> 2) & 3));
+  }
+  __device__ static __forceinline__ int tr_base(int lane, int rd) {
+    const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    return 64 * (4 * h + q) + 16 * ((2 * g + (p >> 1)) ^ ((h + 2 * rd) & 3)) + 8 * (p & 1);
+  }
+};
+
+__device__ __forceinline__ bf16x8_t lds_b128(const char* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4*>(p));
 }
 
-template <int D>
-__device__ __forceinline__ bf16x8_t lds_row8(const char* base, int row, int ch) {
-  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4*>(base + soff<D>(row, ch)));
-}
-
-// Transposed 8-element operand: rows r0..r0+3 and r0+8..r0+11 of column `col` of the tile
-// (the k order of an MFMA operand taken from an accumulator: j -> 8*(j>>2) + (j&3)).
-// Each lane of a 16-lane group passes the address of row (r0 + (i>>2)), columns col0 + 4*(i&3).
-template <int D>
-__device__ __forceinline__ bf16x8_t lds_tr8(const char* base, int r0, int col0, int lane16) {
-  const int q = lane16 >> 2, p = lane16 & 3;
-  const int c = col0 + 4 * p;
-  const int off0 = soff<D>(r0 + q, c >> 3) + ((c & 4) << 1);
-  const int off1 = soff<D>(r0 + 8 + q, c >> 3) + ((c & 4) << 1);
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off0));
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off1));
+// transposed 8-element MFMA operand: two ds_read_b64_tr_b16 (k-steps j = 0..3 and 4..7)
+__device__ __forceinline__ bf16x8_t lds_tr8(const char* p0, const char* p1) {
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
   s16x8 r = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8_t, r);
 }
@@ -102,37 +105,80 @@ __device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, flo
 }
 
 // ---------------------------------------------------------------------------------------------
-// K/V tile staging (64 rows x D) through registers
+// [ROWS x D] tile staging HBM -> registers -> LDS. The per-lane parts of both addresses are
+// computed once; per tile only a wave-uniform base changes (global) or an immediate (LDS).
 template <int D, int ROWS>
-struct TileStage {
-  static constexpr int NCH = D / 8;
-  static constexpr int N = ROWS * NCH / kThreads;
+struct Stage {
+  static constexpr int NCH = D / 8, N = ROWS * NCH / kThreads, RPI = kThreads / NCH;
   u32x4 r[N];
-  __device__ __forceinline__ void load(const bf16_t* base, long stride, int row0, int tid) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int id = tid + kThreads * i, row = id / NCH, ch = id % NCH;
-      r[i] = *reinterpret_cast<const u32x4*>(base + (long)(row0 + row) * stride + ch * 8);
-    }
+  __amdgpu_buffer_rsrc_t rsrc;  // whole [rows x stride] extent of one (batch, head): wave-uniform
+  int voff, loff;
+  __device__ __forceinline__ void init(const bf16_t* base, long stride, int rows, int tid, int cols = D) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), (short)0,
+                                             (int)((long)(rows - 1) * stride * 2 + cols * 2), 0x00020000);
+    const int row = tid / NCH, ch = tid % NCH;
+    voff = (int)(row * stride * 2 + ch * 16);
+    loff = Img<D>::off(row, ch);
   }
-  __device__ __forceinline__ void store(char* lds, int tid) const {
+  __device__ __forceinline__ void load(int row0, long stride, int extra = 0) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int id = tid + kThreads * i, row = id / NCH, ch = id % NCH;
-      *reinterpret_cast<u32x4*>(lds + soff<D>(row, ch)) = r[i];
-    }
+    for (int i = 0; i < N; ++i)
+      r[i] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (int)((row0 + i * RPI) * stride * 2) + extra, 0));
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<u32x4*>(lds + loff + i * (RPI / 8) * Img<D>::G8) = r[i];
   }
 };
 
+template <int V>
+using IC = std::integral_constant<int, V>;
+
 // ---------------------------------------------------------------------------------------------
-// Forward
+// Cross-half (lane <-> lane^32) reductions on the VALU (v_permlane32_swap; no LDS round trip).
+__device__ __forceinline__ float xhalf_max(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// single v_max3_f32 (plain fmaxf on MFMA results gets canonicalising v_max pairs from hipcc)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ float max16(const f32x16& s, float init) {
+  float a = max3f(init, s[0], s[1]), b = max3f(s[2], s[3], s[4]);
+  a = max3f(a, s[5], s[6]);
+  b = max3f(b, s[7], s[8]);
+  a = max3f(a, s[9], s[10]);
+  b = max3f(b, s[11], s[12]);
+  a = max3f(a, s[13], s[14]);
+  return max3f(a, b, s[15]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward. Per 64-key tile each wave runs four clusters: K operand burst (16 x ds_read_b128 into
+// registers), S^T MFMAs (two independent 32-key chains), softmax on the VALU, V^T operand burst
+// (32 x ds_read_b64_tr_b16), P.V MFMAs. Two workgroups per CU put two waves on every SIMD, so one
+// wave's load/VALU clusters run beside the other's MFMA clusters. The loop is unrolled over the
+// 2-deep LDS ring so every LDS address is base register + immediate. The online-softmax rescale is
+// deferred (only when a row max grows by > 8 in log2 units: P <= 2^8, exact f32 accumulation)
+// and wave-uniform.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     bf16_t* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
     long so, float scale2) {
-  constexpr int BQ = 128, BK = 64, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE];
+  constexpr int BQ = 128, BK = 64, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2, G8 = Img<D>::G8;
+  constexpr float THR = 8.f;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
   const int nqb = S / BQ, BH = B * Hq;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -140,6 +186,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   const int bh = lid % BH, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int q0 = qb * BQ, qw0 = q0 + 32 * w, qrow = qw0 + l32;
+  const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
+  const int tb0 = Img<D>::tr_base(lane, 0), tb1 = Img<D>::tr_base(lane, 1);
 
   const bf16_t* Kb = K + (long)b * S * sk + (long)hk * D;
   const bf16_t* Vb = V + (long)b * S * sv + (long)hk * D;
@@ -154,83 +202,98 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   for (int i = 0; i < NDB; ++i) o[i] = zero16();
   float m = -INFINITY, lsum = 0.f;
 
-  const int nkv = CAUSAL ? (q0 + BQ) / BK : S / BK;
-  TileStage<D, BK> ks_, vs_;
-  ks_.load(Kb, sk, 0, tid);
-  vs_.load(Vb, sv, 0, tid);
-  ks_.store(smem[0][0], tid);
-  vs_.store(smem[0][1], tid);
+  const int ntile = CAUSAL ? (q0 + BQ) / BK : S / BK;  // always even (S % 128 == 0)
+  Stage<D, BK> kst, vst;
+  kst.init(Kb, sk, S, tid);
+  vst.init(Vb, sv, S, tid);
+  kst.load(0, sk);
+  vst.load(0, sv);
+  kst.store(smem);
+  vst.store(smem + TILE);
   __syncthreads();
 
-  for (int it = 0; it < nkv; ++it) {
+  auto tile = [&](auto bufc, int it) {
+    constexpr int buf = decltype(bufc)::value;
+    const char* Ks = smem + buf * 2 * TILE;
+    const char* Vs = Ks + TILE;
     const int kb = it * BK;
-    if (it + 1 < nkv) {
-      ks_.load(Kb, sk, kb + BK, tid);
-      vs_.load(Vb, sv, kb + BK, tid);
+    const bool more = it + 1 < ntile;
+    if (more) {
+      kst.load(kb + BK, sk);
+      vst.load(kb + BK, sv);
     }
-    const char* Ks = smem[it & 1][0];
-    const char* Vs = smem[it & 1][1];
     if (!CAUSAL || kb <= qw0 + 31) {
-      f32x16 s[2];
+      bf16x8_t fr[4 * NDB > 2 * NKS ? 4 * NDB : 2 * NKS];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        s[t] = zero16();
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) s[t] = mfma32(lds_row8<D>(Ks, 32 * t + l32, 2 * kk + h), qf[kk], s[t]);
+        for (int kk = 0; kk < NKS; ++kk)
+          fr[t * NKS + kk] = lds_b128(Ks + ((kk & 1) ? rb1 : rb0) + 4 * G8 * t + 512 * (kk >> 1));
+      f32x16 s0 = zero16(), s1 = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NKS; ++kk) {
+        s0 = mfma32(fr[kk], qf[kk], s0);
+        s1 = mfma32(fr[NKS + kk], qf[kk], s1);
       }
-      const bool diag = CAUSAL && (kb + BK - 1 > qw0);
-      float mt = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      if (CAUSAL && kb + BK - 1 > qw0) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float x = s[t][r] * scale2;
-          if (diag) {
-            const int key = kb + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-            x = key > qrow ? -INFINITY : x;
-          }
-          s[t][r] = x;
-          mt = fmaxf(mt, x);
+          const int kofs = kb - qw0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          s0[r] = kofs > l32 ? -INFINITY : s0[r];
+          s1[r] = kofs + 32 > l32 ? -INFINITY : s1[r];
         }
       }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m, mt);
-      const float alpha = fast_exp2(m - mn);
-      m = mn;
-      float ps = 0.f;
+      const float mts = xhalf_max(max16(s1, max16(s0, -INFINITY))) * scale2;
+      if (__builtin_amdgcn_ballot_w64(mts > m + THR) != 0) {
+        const float mn = fmaxf(m, mts);
+        const float a = mn == -INFINITY ? 1.f : fast_exp2(m - mn);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(s[t][r] - mn);
-          s[t][r] = p;
-          ps += p;
-        }
+        for (int i = 0; i < NDB; ++i) o[i] *= a;
+        lsum *= a;
+        m = mn;
       }
-      lsum = lsum * alpha + ps;
+      const float nm = -m;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
-      for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+      for (int r = 0; r < 16; r += 2) {
+        s0[r] = fast_exp2(fmaf(s0[r], scale2, nm));
+        s0[r + 1] = fast_exp2(fmaf(s0[r + 1], scale2, nm));
+        s1[r] = fast_exp2(fmaf(s1[r], scale2, nm));
+        s1[r + 1] = fast_exp2(fmaf(s1[r + 1], scale2, nm));
+        a0 += s0[r];
+        a1 += s0[r + 1];
+        a2 += s1[r];
+        a3 += s1[r + 1];
+      }
+      lsum += (a0 + a1) + (a2 + a3);
+      const bf16x8_t pf[4] = {acc_to_bf16(s0, 0), acc_to_bf16(s0, 1), acc_to_bf16(s1, 0), acc_to_bf16(s1, 1)};
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int half = 0; half < 2; ++half) {  // V^T burst in two halves: 32 operand VGPRs live
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8_t pf = acc_to_bf16(s[t], st);
+        for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
           for (int db = 0; db < NDB; ++db) {
-            const bf16x8_t vf = lds_tr8<D>(Vs, 32 * t + 16 * st + 4 * h, 32 * db + 16 * ((lane >> 4) & 1), lane & 15);
-            o[db] = mfma32(vf, pf, o[db]);
+            const int ts = 2 * half + t2;
+            fr[t2 * NDB + db] = lds_tr8(Vs + tb0 + G8 * (2 * ts) + 512 * db, Vs + tb1 + G8 * (2 * ts + 1) + 512 * db);
           }
-        }
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+          for (int db = 0; db < NDB; ++db) o[db] = mfma32(fr[t2 * NDB + db], pf[2 * half + t2], o[db]);
       }
     }
-    if (it + 1 < nkv) {
-      ks_.store(smem[(it + 1) & 1][0], tid);
-      vs_.store(smem[(it + 1) & 1][1], tid);
+    if (more) {
+      kst.store(smem + (buf ^ 1) * 2 * TILE);
+      vst.store(smem + (buf ^ 1) * 2 * TILE + TILE);
     }
     __syncthreads();
+  };
+  for (int it = 0; it < ntile; it += 2) {
+    tile(IC<0>{}, it);
+    tile(IC<1>{}, it + 1);
   }
 
-  const float lt = lsum + __shfl_xor(lsum, 32, 64);
+  const float lt = xhalf_sum(lsum);
   const float inv = 1.f / lt;
   bf16_t* Or = O + ((long)b * S + qrow) * so + (long)hq * D;
 #pragma unroll
@@ -277,15 +340,18 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_delta_kernel(const bf16_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// dQ (query-major; recomputes P and dP)
+// dQ (query-major twin of the forward: recomputes P from LSE and dP = dO.V^T, accumulates
+// dQ^T = K^T.dS^T in registers). 32-key tiles, 2-deep LDS ring (loop unrolled over it); per
+// tile: K-row burst -> S^T MFMAs, V-row burst -> dP^T MFMAs, dS on the VALU, K^T transposed
+// burst -> dQ^T MFMAs.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     bf16_t* __restrict__ dQ, int B, int S, int Hq, int Hk, long sq, long sk, long sv, long sdo, long sdq,
     float scale2, float scale) {
-  constexpr int BQ = 128, BK = 64, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE];
+  constexpr int BQ = 128, BK = 32, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2, G8 = Img<D>::G8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
   const int nqb = S / BQ, BH = B * Hq;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -293,6 +359,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
   const int bh = lid % BH, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int q0 = qb * BQ, qw0 = q0 + 32 * w, qrow = qw0 + l32;
+  const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
+  const int tb0 = Img<D>::tr_base(lane, 0), tb1 = Img<D>::tr_base(lane, 1);
 
   const bf16_t* Kb = K + (long)b * S * sk + (long)hk * D;
   const bf16_t* Vb = V + (long)b * S * sv + (long)hk * D;
@@ -305,64 +373,75 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
     qf[kk] = gload8(Qr + 16 * kk + 8 * h);
     gf[kk] = gload8(dOr + 16 * kk + 8 * h);
   }
-  const float lse = LSE[(long)bh * S + qrow];
+  const float nlse = -LSE[(long)bh * S + qrow];
   const float dlt = Delta[(long)bh * S + qrow];
 
   f32x16 dq[NDB];
 #pragma unroll
   for (int i = 0; i < NDB; ++i) dq[i] = zero16();
 
-  const int nkv = CAUSAL ? (q0 + BQ) / BK : S / BK;
-  TileStage<D, BK> ks_, vs_;
-  ks_.load(Kb, sk, 0, tid);
-  vs_.load(Vb, sv, 0, tid);
-  ks_.store(smem[0][0], tid);
-  vs_.store(smem[0][1], tid);
+  const int ntile = CAUSAL ? (q0 + BQ) / BK : S / BK;  // always even
+  Stage<D, BK> kst, vst;
+  kst.init(Kb, sk, S, tid);
+  vst.init(Vb, sv, S, tid);
+  kst.load(0, sk);
+  vst.load(0, sv);
+  kst.store(smem);
+  vst.store(smem + TILE);
   __syncthreads();
 
-  for (int it = 0; it < nkv; ++it) {
+  auto tile = [&](auto bufc, int it) {
+    constexpr int buf = decltype(bufc)::value;
+    const char* Ks = smem + buf * 2 * TILE;
+    const char* Vs = Ks + TILE;
     const int kb = it * BK;
-    if (it + 1 < nkv) {
-      ks_.load(Kb, sk, kb + BK, tid);
-      vs_.load(Vb, sv, kb + BK, tid);
+    const bool more = it + 1 < ntile;
+    if (more) {
+      kst.load(kb + BK, sk);
+      vst.load(kb + BK, sv);
     }
-    const char* Ks = smem[it & 1][0];
-    const char* Vs = smem[it & 1][1];
-    if (!CAUSAL || kb <= qw0 + 31) {
-      const bool diag = CAUSAL && (kb + BK - 1 > qw0);
+    if (!CAUSAL || kb <= qw0) {
+      bf16x8_t fr[2 * NKS];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f32x16 s = zero16(), dp = zero16();
+      for (int kk = 0; kk < NKS; ++kk) {
+        fr[kk] = lds_b128(Ks + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
+        fr[NKS + kk] = lds_b128(Vs + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
+      }
+      f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) {
-          s = mfma32(lds_row8<D>(Ks, 32 * t + l32, 2 * kk + h), qf[kk], s);
-          dp = mfma32(lds_row8<D>(Vs, 32 * t + l32, 2 * kk + h), gf[kk], dp);
-        }
+      for (int kk = 0; kk < NKS; ++kk) {
+        s = mfma32(fr[kk], qf[kk], s);
+        dp = mfma32(fr[NKS + kk], gf[kk], dp);
+      }
+      if (CAUSAL && kb == qw0) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = fast_exp2(s[r] * scale2 - lse);
-          if (diag) {
-            const int key = kb + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-            p = key > qrow ? 0.f : p;
-          }
-          s[r] = p * (dp[r] - dlt);  // dS^T (natural units, before the softmax scale)
-        }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8_t df = acc_to_bf16(s, st);
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            const bf16x8_t kf = lds_tr8<D>(Ks, 32 * t + 16 * st + 4 * h, 32 * db + 16 * ((lane >> 4) & 1), lane & 15);
-            dq[db] = mfma32(kf, df, dq[db]);
-          }
+          const int kofs = (r & 3) + 8 * (r >> 2) + 4 * h;
+          s[r] = kofs > l32 ? -INFINITY : s[r];
         }
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = fast_exp2(fmaf(s[r], scale2, nlse)) * (dp[r] - dlt);
+      const bf16x8_t d0 = acc_to_bf16(s, 0), d1 = acc_to_bf16(s, 1);
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+          fr[st * NDB + db] = lds_tr8(Ks + tb0 + G8 * (2 * st) + 512 * db, Ks + tb1 + G8 * (2 * st + 1) + 512 * db);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[db], d0, dq[db]);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[NDB + db], d1, dq[db]);
     }
-    if (it + 1 < nkv) {
-      ks_.store(smem[(it + 1) & 1][0], tid);
-      vs_.store(smem[(it + 1) & 1][1], tid);
+    if (more) {
+      kst.store(smem + (buf ^ 1) * 2 * TILE);
+      vst.store(smem + (buf ^ 1) * 2 * TILE + TILE);
     }
     __syncthreads();
+  };
+  for (int it = 0; it < ntile; it += 2) {
+    tile(IC<0>{}, it);
+    tile(IC<1>{}, it + 1);
   }
 
   bf16_t* dQr = dQ + ((long)b * S + qrow) * sdq + (long)hq * D;
@@ -377,16 +456,20 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV (key-major; sums the kv group's query heads in registers)
+// dK, dV (key-major; the kv group's query heads are summed in registers, no atomics). Query
+// slices of 32 rows stream through a 2-deep LDS ring (loop unrolled over it). Per slice: Q/dO row
+// burst -> S, dP MFMAs (key on the lane, two independent chains), P/dS on the VALU, dO^T/Q^T
+// transposed burst -> dV^T, dK^T MFMAs. One wave per SIMD (K, V fragments + both accumulators
+// stay in registers; build flag -amdgpu-mfma-vgpr-form keeps the accumulators out of copies).
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
     long sdo, long sdk, long sdv, float scale2, float scale) {
-  constexpr int BKV = 128, BQS = 32, NKS = D / 16, NDB = D / 32, SL = BQS * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2][2][SL];
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [buf][lse, delta][row]
+  constexpr int BKV = 128, BQS = 32, NKS = D / 16, NDB = D / 32, SL = BQS * D * 2, G8 = Img<D>::G8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * SL];
+  __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, delta][row]
 
   const int nkb = S / BKV, BHk = B * Hk, G = Hq / Hk;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -394,6 +477,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
   const int bhk = lid % BHk, b = bhk / Hk, hk = bhk % Hk;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int k0 = kbi * BKV, kw0 = k0 + 32 * w, key = kw0 + l32;
+  const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
+  const int tb0 = Img<D>::tr_base(lane, 0), tb1 = Img<D>::tr_base(lane, 1);
 
   bf16x8_t kf[NKS], vf[NKS];
   {
@@ -413,47 +498,57 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
   }
 
   const int qs0 = CAUSAL ? k0 : 0;
-  const int nsl = (S - qs0) / BQS;
-  const int total = G * nsl;
+  const int nsl = (S - qs0) / BQS;  // multiple of 4
+  const int total = G * nsl;        // even
 
-  TileStage<D, BQS> qs_, gs_;
+  Stage<D, BQS> qst, gst;
+  qst.init(Q + (long)b * S * sq + (long)hk * G * D, sq, S, tid, G * D);
+  gst.init(dO + (long)b * S * sdo + (long)hk * G * D, sdo, S, tid, G * D);
+  const float* rsrc = (tid < BQS ? LSE : Delta) + ((long)b * Hq + hk * G) * S + (tid & (BQS - 1));
   float rc = 0.f;
-  auto stage_load = [&](int idx) {
-    const int g = idx / nsl, sl = idx % nsl;
-    const int hq = hk * G + g, qa = qs0 + sl * BQS;
-    qs_.load(Q + (long)b * S * sq + (long)hq * D, sq, qa, tid);
-    gs_.load(dO + (long)b * S * sdo + (long)hq * D, sdo, qa, tid);
-    if (tid < 2 * BQS) {
-      const float* src = tid < BQS ? LSE : Delta;
-      rc = src[((long)b * Hq + hq) * S + qa + (tid & (BQS - 1))];
-    }
+  auto stage_load = [&](int g, int sl) {
+    const int qa = qs0 + sl * BQS;
+    qst.load(qa, sq, g * D * 2);  // head g of the kv group (the descriptor spans all G heads)
+    gst.load(qa, sdo, g * D * 2);
+    if (tid < 2 * BQS) rc = rsrc[(long)g * S + qa];
   };
   auto stage_store = [&](int buf) {
-    qs_.store(smem[buf][0], tid);
-    gs_.store(smem[buf][1], tid);
-    if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = rc;
+    qst.store(smem + buf * 2 * SL);
+    gst.store(smem + buf * 2 * SL + SL);
+    if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = tid < BQS ? -rc : rc;
   };
 
-  stage_load(0);
+  stage_load(0, 0);
   stage_store(0);
   __syncthreads();
 
-  for (int it = 0; it < total; ++it) {
-    const int sl = it % nsl;
+  auto slice = [&](auto bufc, int g, int sl) {
+    constexpr int buf = decltype(bufc)::value;
+    const char* Qs = smem + buf * 2 * SL;
+    const char* Gs = Qs + SL;
+    int gn = g, sn = sl + 1;
+    if (sn == nsl) {
+      sn = 0;
+      ++gn;
+    }
+    const bool more = gn < G;
+    if (more) stage_load(gn, sn);
     const int qa = qs0 + sl * BQS;
-    if (it + 1 < total) stage_load(it + 1);
-    const int buf = it & 1;
-    const char* Qs = smem[buf][0];
-    const char* Gs = smem[buf][1];
     if (!CAUSAL || qa + BQS - 1 >= kw0) {
-      const bool diag = CAUSAL && (qa < kw0 + 31);
+      bf16x8_t fr[4 * NDB > 2 * NKS ? 4 * NDB : 2 * NKS];
+#pragma unroll
+      for (int kk = 0; kk < NKS; ++kk) {
+        fr[kk] = lds_b128(Qs + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
+        fr[NKS + kk] = lds_b128(Gs + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
+      }
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int kk = 0; kk < NKS; ++kk) {
-        s = mfma32(lds_row8<D>(Qs, l32, 2 * kk + h), kf[kk], s);
-        dp = mfma32(lds_row8<D>(Gs, l32, 2 * kk + h), vf[kk], dp);
+        s = mfma32(fr[kk], kf[kk], s);
+        dp = mfma32(fr[NKS + kk], vf[kk], dp);
       }
-      // rows of the accumulators are query rows (r&3) + 8(r>>2) + 4h
+      const bool diag = CAUSAL && qa < kw0 + 31;
+      const int kq = key - qa - 4 * h;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const f32x4 l4 = *reinterpret_cast<const f32x4*>(&rowc[buf][0][8 * g4 + 4 * h]);
@@ -461,29 +556,41 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g4 + i;
-          float p = fast_exp2(s[r] * scale2 - l4[i]);
-          if (diag) {
-            const int q = qa + 8 * g4 + 4 * h + i;
-            p = key > q ? 0.f : p;
-          }
+          float p = fast_exp2(fmaf(s[r], scale2, l4[i]));
+          if (diag) p = kq > 8 * g4 + i ? 0.f : p;
           s[r] = p;
           dp[r] = p * (dp[r] - d4[i]);
         }
       }
+      const bf16x8_t pf0 = acc_to_bf16(s, 0), pf1 = acc_to_bf16(s, 1);
+      const bf16x8_t df0 = acc_to_bf16(dp, 0), df1 = acc_to_bf16(dp, 1);
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8_t pf = acc_to_bf16(s, st);
-        const bf16x8_t df = acc_to_bf16(dp, st);
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          const int col0 = 32 * db + 16 * ((lane >> 4) & 1);
-          dv[db] = mfma32(lds_tr8<D>(Gs, 16 * st + 4 * h, col0, lane & 15), pf, dv[db]);
-          dk[db] = mfma32(lds_tr8<D>(Qs, 16 * st + 4 * h, col0, lane & 15), df, dk[db]);
+          const int o0 = tb0 + G8 * (2 * st) + 512 * db, o1 = tb1 + G8 * (2 * st + 1) + 512 * db;
+          fr[(2 * st) * NDB + db] = lds_tr8(Gs + o0, Gs + o1);
+          fr[(2 * st + 1) * NDB + db] = lds_tr8(Qs + o0, Qs + o1);
         }
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        dv[db] = mfma32(fr[db], pf0, dv[db]);
+        dk[db] = mfma32(fr[NDB + db], df0, dk[db]);
+      }
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        dv[db] = mfma32(fr[2 * NDB + db], pf1, dv[db]);
+        dk[db] = mfma32(fr[3 * NDB + db], df1, dk[db]);
       }
     }
-    if (it + 1 < total) stage_store(buf ^ 1);
+    if (more) stage_store(buf ^ 1);
     __syncthreads();
+  };
+  for (int g = 0; g < G; ++g) {
+    for (int sl = 0; sl < nsl; sl += 2) {
+      slice(IC<0>{}, g, sl);
+      slice(IC<1>{}, g, sl + 1);
+    }
   }
 
   bf16_t* dKr = dK + ((long)b * S + key) * sdk + (long)hk * D;
