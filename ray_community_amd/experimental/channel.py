@@ -1,0 +1,124 @@
+"""Shared-memory channels for compiled DAGs (reference: ``python/ray/experimental/channel.py``).
+
+A channel is one POSIX shared-memory segment: a header of u64 words ``[write_seq, nbytes,
+ack[0..R)]`` followed by the payload. ``write`` waits until every reader has acknowledged the
+previous value, copies the pickled value in and publishes it by bumping ``write_seq`` (x86 keeps
+stores in order, and the header words are single aligned 8-byte stores). Readers poll
+``write_seq``; ``end_read`` acknowledges. No broker, no RPC: a driver->actor->actor->driver hop is
+a handful of memory copies. GPU tensors inside values travel as HIP IPC handles (the object
+serializer's GPU path), so HBM payloads are not copied either.
+"""
+from __future__ import annotations
+
+import pickle
+import time
+from multiprocessing import resource_tracker, shared_memory
+from typing import Any, Optional
+
+import numpy as np
+
+DEFAULT_BUFFER = 10 * 1024 * 1024
+
+
+class ChannelTimeoutError(TimeoutError):
+    pass
+
+
+class _Closed:
+    """Sentinel written into channels at teardown."""
+
+    def __reduce__(self):
+        return (_Closed, ())
+
+
+def _wait(cond, timeout: Optional[float]):
+    deadline = None if timeout is None else time.monotonic() + timeout
+    spins = 0
+    while not cond():
+        spins += 1
+        if spins < 2000:
+            continue
+        if deadline is not None and time.monotonic() > deadline:
+            raise ChannelTimeoutError("channel operation timed out")
+        time.sleep(0 if spins < 20000 else 50e-6)
+
+
+class Channel:
+    def __init__(self, buffer_size_bytes: Optional[int] = None, num_readers: int = 1, _name: Optional[str] = None):
+        self.num_readers = int(num_readers)
+        self.capacity = int(buffer_size_bytes or DEFAULT_BUFFER)
+        self._hdr_words = 2 + self.num_readers
+        self._data_off = ((self._hdr_words * 8 + 63) // 64) * 64
+        if _name is None:
+            self._shm = shared_memory.SharedMemory(create=True, size=self._data_off + self.capacity)
+            self._owner = True
+        else:
+            self._shm = shared_memory.SharedMemory(name=_name)
+            try:  # attached segments must not be unlinked by this process's resource tracker
+                resource_tracker.unregister(self._shm._name, "shared_memory")
+            except Exception:
+                pass
+            self._owner = False
+        self.name = self._shm.name
+        self._hdr = np.ndarray((self._hdr_words,), dtype=np.uint64, buffer=self._shm.buf, offset=0)
+        if self._owner:
+            self._hdr[:] = 0
+        self._read_seq = [0] * self.num_readers
+
+    def __reduce__(self):
+        return (_attach, (self.name, self.capacity, self.num_readers))
+
+    # ------------------------------------------------------------------ writer
+    def write(self, value: Any, timeout: Optional[float] = None):
+        data = pickle.dumps(value, protocol=5) if not isinstance(value, _Closed) else b"\x00CLOSED"
+        if len(data) > self.capacity:
+            raise ValueError(f"value of {len(data)} bytes exceeds the channel buffer ({self.capacity} bytes); "
+                             f"compile with a larger buffer_size_bytes")
+        hdr = self._hdr
+        seq = int(hdr[0])
+        _wait(lambda: all(int(hdr[2 + r]) >= seq for r in range(self.num_readers)), timeout)
+        self._shm.buf[self._data_off:self._data_off + len(data)] = data
+        hdr[1] = len(data)
+        hdr[0] = seq + 1
+
+    def close(self):
+        try:
+            self.write(_Closed(), timeout=5.0)
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ reader
+    def begin_read(self, reader: int = 0, timeout: Optional[float] = None) -> Any:
+        hdr = self._hdr
+        want = self._read_seq[reader] + 1
+        _wait(lambda: int(hdr[0]) >= want, timeout)
+        n = int(hdr[1])
+        data = bytes(self._shm.buf[self._data_off:self._data_off + n])
+        self._read_seq[reader] = want
+        if data == b"\x00CLOSED":
+            return _Closed()
+        return pickle.loads(data)
+
+    def end_read(self, reader: int = 0):
+        self._hdr[2 + reader] = self._read_seq[reader]
+
+    def read(self, reader: int = 0, timeout: Optional[float] = None) -> Any:
+        v = self.begin_read(reader, timeout)
+        self.end_read(reader)
+        return v
+
+    def destroy(self):
+        try:
+            self._hdr = None
+            self._shm.close()
+        except Exception:
+            pass
+        if self._owner:
+            try:
+                self._shm.unlink()
+            except Exception:
+                pass
+
+
+def _attach(name, capacity, num_readers):
+    return Channel(capacity, num_readers, _name=name)
