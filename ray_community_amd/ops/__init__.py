@@ -25,6 +25,7 @@ __all__ = [
     "cross_entropy",
     "grad_sumsq",
     "compute_gae",
+    "vtrace",
     "standardize_",
     "batched_concat",
     "image_normalize",
@@ -294,6 +295,31 @@ def compute_gae(rewards, values, terminateds, dones=None, gamma=0.99, lam=0.95, 
     if squeeze:
         adv, tgt = adv[0], tgt[0]
     return adv, tgt
+
+
+def vtrace(log_rhos, rewards, values, next_values, terminateds, dones=None, gamma=0.99, clip_rho_threshold=1.0,
+           clip_c_threshold=1.0, clip_pg_rho_threshold=1.0):
+    """V-trace targets over ``[B, T]`` fragments. Returns ``(vs, pg_advantages)`` (float32).
+
+    ``log_rhos`` = log pi(a|s) - log mu(a|s); ``next_values[b, t]`` = V(s_{t+1}) (used at episode
+    cuts and the fragment end); ``dones`` cuts the trace, ``terminateds`` zeroes the bootstrap.
+    """
+    if dones is None:
+        dones = terminateds
+    B, T = rewards.shape
+    if rewards.is_cuda:
+        dev = rewards.device
+        f = lambda x: x.to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
+        u8 = lambda x: x.to(device=dev, dtype=torch.uint8).contiguous()  # noqa: E731
+        lr, r, v, nv, te, do = f(log_rhos), f(rewards), f(values), f(next_values), u8(terminateds), u8(dones)
+        vs = torch.empty(B, T, device=dev, dtype=torch.float32)
+        pg = torch.empty_like(vs)
+        check(lib().rca_vtrace(lr.data_ptr(), r.data_ptr(), v.data_ptr(), nv.data_ptr(), te.data_ptr(), do.data_ptr(),
+                               vs.data_ptr(), pg.data_ptr(), B, T, float(gamma), float(clip_rho_threshold),
+                               float(clip_c_threshold), float(clip_pg_rho_threshold), stream_ptr(dev)), "vtrace")
+        return vs, pg
+    return ref.vtrace_ref(log_rhos, rewards, values, next_values, terminateds, dones, gamma, clip_rho_threshold,
+                          clip_c_threshold, clip_pg_rho_threshold)
 
 
 def _gae_cpu(rewards, values, terminateds, dones, gamma, lam, last_values, next_values):

@@ -34,6 +34,7 @@ _SIGS = {
                           c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
     "rca_gae": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                         c_float, c_float, c_int, c_void_p, c_void_p, c_float, c_void_p]),
+    "rca_vtrace": (c_int, [c_void_p] * 8 + [c_int, c_int, c_float, c_float, c_float, c_float, c_void_p]),
     "rca_standardize": (c_int, [c_void_p, c_ll, c_void_p, c_void_p, c_float, c_void_p]),
     "rca_batched_copy": (c_int, [c_void_p, c_int, c_void_p, c_ll, c_void_p]),
     "rca_attn_fwd": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_ll] * 4 + [c_float, c_int, c_void_p]),

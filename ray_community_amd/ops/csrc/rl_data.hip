@@ -71,6 +71,71 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
   }
 }
 
+// ----------------------------------------------------------------------------- V-trace
+// IMPALA off-policy targets (Espeholt et al. 2018; reference: rllib/algorithms/impala/vtrace_torch.py)
+// on env-major [B, T] fragments, one wave per trajectory. acc_t = vs_t - V_t obeys the same affine
+// right-to-left recurrence as GAE (acc_t = delta_t + k_t * acc_{t+1}), so the wave splits the row
+// into 64 chunks, scans the chunk maps across lanes and re-walks each chunk with its carry.
+//   rho_t = min(rho_bar, e^{logr_t}), c_t = min(c_bar, e^{logr_t}), disc_t = gamma * (1 - term_t)
+//   delta_t = rho_t (r_t + disc_t V'_t - V_t),  k_t = gamma c_t (1 - done_t)
+//   pg_t = min(pg_bar, e^{logr_t}) (r_t + disc_t vs'_t - V_t)
+// with V'_t = next_val[t] (value of s_{t+1}; exact at truncations) and vs'_t = vs_{t+1} inside an
+// episode, V'_t at a cut or at the fragment end.
+__global__ __launch_bounds__(256) void vtrace_kernel(const float* __restrict__ logr, const float* __restrict__ rew,
+                                                     const float* __restrict__ val, const float* __restrict__ nval,
+                                                     const unsigned char* __restrict__ term,
+                                                     const unsigned char* __restrict__ done, float* __restrict__ vs,
+                                                     float* __restrict__ pg, int B, int T, float gamma, float rho_bar,
+                                                     float c_bar, float pg_bar) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const long long base = (long long)row * T;
+  const int chunk = (T + 63) / 64;
+  const int t0 = lane * chunk;
+  const int t1 = min(T, t0 + chunk);
+  float a = 0.f, b = 1.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    const float ir = __expf(logr[base + t]);
+    const float disc = term[base + t] ? 0.f : gamma;
+    const float d = fminf(rho_bar, ir) * (rew[base + t] + disc * nval[base + t] - val[base + t]);
+    const float k = done[base + t] ? 0.f : gamma * fminf(c_bar, ir);
+    a = d + k * a;
+    b = k * b;
+  }
+  float ca = a, cb = b;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float ra = __shfl_down(ca, off, 64), rb = __shfl_down(cb, off, 64);
+    if (lane + off < 64) {
+      ca = ca + cb * ra;
+      cb = cb * rb;
+    }
+  }
+  float A = __shfl_down(ca, 1, 64);
+  if (lane == 63) A = 0.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    const float ir = __expf(logr[base + t]);
+    const float disc = term[base + t] ? 0.f : gamma;
+    const bool cut = done[base + t] || t + 1 >= T;
+    const float vs_next = cut ? nval[base + t] : val[base + t + 1] + A;
+    const float r = rew[base + t], v = val[base + t];
+    const float d = fminf(rho_bar, ir) * (r + disc * nval[base + t] - v);
+    const float k = done[base + t] ? 0.f : gamma * fminf(c_bar, ir);
+    A = d + k * A;
+    vs[base + t] = v + A;
+    pg[base + t] = fminf(pg_bar, ir) * (r + disc * vs_next - v);
+  }
+}
+
+RCA_API int rca_vtrace(const float* logr, const float* rew, const float* val, const float* nval,
+                       const unsigned char* term, const unsigned char* done, float* vs, float* pg, int B, int T,
+                       float gamma, float rho_bar, float c_bar, float pg_bar, hipStream_t stream) {
+  hipLaunchKernelGGL(vtrace_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, logr, rew, val, nval, term, done, vs, pg, B,
+                     T, gamma, rho_bar, c_bar, pg_bar);
+  return (int)hipGetLastError();
+}
+
 // stats[0] = mean, stats[1] = 1 / (std + eps)   (population std, as numpy.std)
 __global__ __launch_bounds__(256) void finalize_stats_kernel(const float* __restrict__ partial, int nb, long long n, float eps,
                                                              float* __restrict__ stats) {

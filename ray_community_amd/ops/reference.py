@@ -96,3 +96,28 @@ def attention_ref(q, k, v, causal: bool = True, scale=None):
         s = s.masked_fill(m, float("-inf"))
     o = torch.matmul(torch.softmax(s, dim=-1), vf)
     return o.transpose(1, 2).to(q.dtype)
+
+
+def vtrace_ref(log_rhos, rewards, values, next_values, terminateds, dones, gamma=0.99, clip_rho=1.0, clip_c=1.0,
+               clip_pg=1.0):
+    """Sequential fp32 V-trace (see ops/csrc/rl_data.hip vtrace_kernel for the recurrences)."""
+    lr, r, v, nv = (torch.as_tensor(x, dtype=torch.float32) for x in (log_rhos, rewards, values, next_values))
+    term = torch.as_tensor(terminateds).bool()
+    done = torch.as_tensor(dones).bool()
+    B, T = r.shape
+    ir = lr.exp()
+    rho, c, rpg = ir.clamp(max=clip_rho), ir.clamp(max=clip_c), ir.clamp(max=clip_pg)
+    disc = gamma * (~term).float()
+    vs = torch.zeros(B, T)
+    pg = torch.zeros(B, T)
+    acc = torch.zeros(B)
+    for t in range(T - 1, -1, -1):
+        cut = done[:, t] | (t + 1 >= T)
+        vnext_in = v[:, t + 1] + acc if t + 1 < T else nv[:, t]
+        vs_next = torch.where(cut, nv[:, t], vnext_in)
+        d = rho[:, t] * (r[:, t] + disc[:, t] * nv[:, t] - v[:, t])
+        k = gamma * c[:, t] * (~done[:, t]).float()
+        acc = d + k * acc
+        vs[:, t] = v[:, t] + acc
+        pg[:, t] = rpg[:, t] * (r[:, t] + disc[:, t] * vs_next - v[:, t])
+    return vs, pg

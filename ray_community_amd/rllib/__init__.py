@@ -1,8 +1,9 @@
-"""RLlib equivalent (reference: ``rllib/``): PPO / DQN (IMPALA / APPO in ``algorithms.impala``),
+"""RLlib equivalent (reference: ``rllib/``): PPO / DQN / IMPALA / APPO,
 vectorised env runners, GPU learners over RCCL, HIP GAE."""
-from .algorithms import DQN, PPO, Algorithm, AlgorithmConfig, DQNConfig, PPOConfig, get_algorithm_class
+from .algorithms import (APPO, DQN, IMPALA, PPO, Algorithm, AlgorithmConfig, APPOConfig, DQNConfig, IMPALAConfig,
+                         PPOConfig, get_algorithm_class)
 from .env import register_env
 from .policy.sample_batch import MultiAgentBatch, SampleBatch
 
-__all__ = ["PPO", "PPOConfig", "DQN", "DQNConfig", "Algorithm", "AlgorithmConfig", "SampleBatch", "MultiAgentBatch",
+__all__ = ["PPO", "PPOConfig", "IMPALA", "IMPALAConfig", "APPO", "APPOConfig", "DQN", "DQNConfig", "Algorithm", "AlgorithmConfig", "SampleBatch", "MultiAgentBatch",
            "register_env", "get_algorithm_class"]

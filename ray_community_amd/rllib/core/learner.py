@@ -165,6 +165,83 @@ class Learner:
                     "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr()})
         return out
 
+    # ------------------------------------------------------------------ IMPALA / APPO
+    def _vtrace_targets(self, b, N, T, logits, values):
+        """V-trace (HIP kernel) with the learner's current policy/values as the target."""
+        cfg = self.cfg
+        d = self.module.dist(logits)
+        act = b["actions"].reshape((N * T,) + tuple(b["actions"].shape[2:]))
+        logp = d.logp(act)
+        with torch.no_grad():
+            v = values.detach().reshape(N, T)
+            # V(s_{t+1}): the learner's own value of the next in-fragment state; the runner's bootstrap
+            # at episode cuts (terminal / truncated final obs) and at the fragment end.
+            done = (b["terminateds"] | b["truncateds"]).bool()
+            nv = b["next_vf_preds"].float().clone()
+            inner = ~done[:, :-1]
+            nv[:, :-1] = torch.where(inner, v[:, 1:], nv[:, :-1])
+            log_rhos = (logp.detach() - b["action_logp"].reshape(-1)).reshape(N, T)
+            vs, pg = ops.vtrace(log_rhos, b["rewards"].float(), v, nv, b["terminateds"], done,
+                                cfg.get("gamma", 0.99), cfg.get("vtrace_clip_rho_threshold", 1.0),
+                                cfg.get("vtrace_clip_c_threshold", 1.0), cfg.get("vtrace_clip_pg_rho_threshold", 1.0))
+        return d, logp, act, vs.reshape(-1), pg.reshape(-1)
+
+    def update_impala(self, batch: SampleBatch) -> Dict:
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        b = batch.to_device(self.device)
+        N, T = batch.fragment_shape
+        obs = b["obs"].reshape((N * T,) + tuple(b["obs"].shape[2:]))
+        logits, values = self.forward(obs)
+        d, logp, act, vs, pg = self._vtrace_targets(b, N, T, logits, values)
+        pi_loss = -(logp * pg).mean()
+        vf_loss = 0.5 * ((values - vs) ** 2).mean()
+        ent = d.entropy().mean()
+        loss = pi_loss + cfg.get("vf_loss_coeff", 0.5) * vf_loss - cfg.get("entropy_coeff", 0.01) * ent
+        gn = self._step(loss)
+        self.num_updates += 1
+        return {"policy_loss": float(pi_loss), "vf_loss": float(vf_loss), "entropy": float(ent),
+                "total_loss": float(loss), "grad_gnorm": float(gn) if gn is not None else float("nan"),
+                "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr()}
+
+    def update_appo(self, batch: SampleBatch) -> Dict:
+        """APPO: PPO-clip surrogate on V-trace advantages (reference: rllib/algorithms/appo/)."""
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        b = batch.to_device(self.device)
+        N, T = batch.fragment_shape
+        obs = b["obs"].reshape((N * T,) + tuple(b["obs"].shape[2:]))
+        with torch.no_grad():
+            logits0, values0 = self.forward(obs)
+            _, _, act, vs, pg = self._vtrace_targets(b, N, T, logits0, values0)
+        old_logp = b["action_logp"].reshape(-1)
+        old_logits = b["action_dist_inputs"].reshape(N * T, -1) if "action_dist_inputs" in b else None
+        clip = cfg.get("clip_param", 0.4)
+        stats = {"policy_loss": 0.0, "vf_loss": 0.0, "entropy": 0.0, "mean_kl": 0.0, "total_loss": 0.0}
+        epochs = int(cfg.get("num_epochs", 1))
+        for _ in range(epochs):
+            logits, values = self.forward(obs)
+            d = self.module.dist(logits)
+            ratio = torch.exp(d.logp(act) - old_logp)
+            surr = torch.min(ratio * pg, ratio.clamp(1 - clip, 1 + clip) * pg)
+            vf_loss = 0.5 * ((values - vs) ** 2).mean()
+            ent = d.entropy().mean()
+            loss = -surr.mean() + cfg.get("vf_loss_coeff", 0.5) * vf_loss - cfg.get("entropy_coeff", 0.01) * ent
+            kl = torch.zeros((), device=self.device)
+            if cfg.get("use_kl_loss", False) and old_logits is not None:
+                kl = self.module.dist(old_logits).kl(d).mean()
+                loss = loss + self.kl_coeff * kl
+            self._step(loss)
+            stats["policy_loss"] += float(-surr.mean())
+            stats["vf_loss"] += float(vf_loss)
+            stats["entropy"] += float(ent)
+            stats["mean_kl"] += float(kl)
+            stats["total_loss"] += float(loss)
+        out = {k: v / max(epochs, 1) for k, v in stats.items()}
+        self.num_updates += 1
+        out.update({"learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr(), "kl_coeff": self.kl_coeff})
+        return out
+
     # ------------------------------------------------------------------ DQN
     def update_dqn(self, batch: SampleBatch) -> Dict:
         cfg = self.cfg
@@ -204,7 +281,7 @@ class _LearnerActor:
         return True
 
     def update(self, kind, batch):
-        return self.learner.update_ppo(batch) if kind == "ppo" else self.learner.update_dqn(batch)
+        return getattr(self.learner, f"update_{kind}")(batch)
 
     def call(self, name, *args):
         return getattr(self.learner, name)(*args)
@@ -237,7 +314,7 @@ class LearnerGroup:
 
     def update(self, kind: str, batch: SampleBatch) -> Dict:
         if self.local is not None:
-            return self.local.update_ppo(batch) if kind == "ppo" else self.local.update_dqn(batch)
+            return getattr(self.local, f"update_{kind}")(batch)
         from ..._private.worker import get
 
         shards = _split(batch, self.n)

@@ -222,3 +222,18 @@ def test_llama_hip_matches_reference_path():
         a, b = p.grad.float().cpu(), g_cpu[n]
         rel = (a - b).norm() / (b.norm() + 1e-8)
         assert rel < 0.1, (n, rel.item())
+
+
+def test_vtrace_kernel_matches_reference():
+    from ray_community_amd.ops import reference as ref
+
+    torch.manual_seed(3)
+    B, T = 37, 203
+    lr = 0.5 * torch.randn(B, T)
+    r, v, nv = torch.randn(B, T), torch.randn(B, T), torch.randn(B, T)
+    term = torch.rand(B, T) < 0.03
+    done = term | (torch.rand(B, T) < 0.02)
+    vs_r, pg_r = ref.vtrace_ref(lr, r, v, nv, term, done, 0.97, 1.0, 0.9, 1.0)
+    vs, pg = ops.vtrace(lr.cuda(), r.cuda(), v.cuda(), nv.cuda(), term.cuda(), done.cuda(), 0.97, 1.0, 0.9, 1.0)
+    assert torch.allclose(vs.cpu(), vs_r, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(pg.cpu(), pg_r, atol=1e-4, rtol=1e-4)

@@ -113,3 +113,52 @@ def test_ppo_in_tune(shutdown_only, tmp_path):
     grid = tune.Tuner(PPO, param_space=cfg.to_dict(),
                       run_config=RunConfig(stop={"training_iteration": 2}, storage_path=str(tmp_path))).fit()
     assert grid.num_errors == 0 and grid[0].metrics["training_iteration"] == 2
+
+
+def test_vtrace_kernel_reference_properties():
+    # on-policy (log_rho = 0), no cuts: vs == n-step lambda=1 returns bootstrapped at the end
+    import torch
+
+    from ray_community_amd import ops
+
+    B, T, g = 3, 7, 0.9
+    torch.manual_seed(0)
+    r, v = torch.randn(B, T), torch.randn(B, T)
+    nv = torch.cat([v[:, 1:], torch.randn(B, 1)], 1)
+    z = torch.zeros(B, T, dtype=torch.bool)
+    vs, pg = ops.vtrace(torch.zeros(B, T), r, v, nv, z, z, g)
+    ret = nv[:, -1].clone()
+    for t in range(T - 1, -1, -1):
+        ret = r[:, t] + g * ret
+        assert torch.allclose(vs[:, t], ret, atol=1e-5)
+    vs_next = torch.cat([vs[:, 1:], nv[:, -1:]], 1)
+    assert torch.allclose(pg, r + g * vs_next - v, atol=1e-5)
+    # a termination cuts the trace and zeroes the bootstrap
+    term = z.clone()
+    term[:, 3] = True
+    vs2, _ = ops.vtrace(torch.zeros(B, T), r, v, nv, term, term, g)
+    assert torch.allclose(vs2[:, 3], r[:, 3], atol=1e-6)
+
+
+@pytest.mark.parametrize("algo", ["IMPALA", "APPO"])
+def test_impala_appo_cartpole_learn(shutdown_only, algo):
+    from ray_community_amd.rllib import APPOConfig, IMPALAConfig
+
+    ray.init(num_cpus=4)
+    cfg_cls = IMPALAConfig if algo == "IMPALA" else APPOConfig
+    config = (cfg_cls().environment("CartPole-v1")
+              .env_runners(num_env_runners=2, num_envs_per_env_runner=8, rollout_fragment_length=32)
+              .training(lr=1e-3, train_batch_size=512, vf_loss_coeff=0.5, entropy_coeff=0.0,
+                        model={"fcnet_hiddens": [64, 64]})
+              .debugging(seed=1))
+    if algo == "APPO":
+        config.training(num_epochs=2)
+    algo_ = config.build()
+    best = 0
+    for i in range(200):
+        r = algo_.train()
+        best = max(best, r["episode_reward_mean"])
+        if best > 100:
+            break
+    algo_.stop()
+    assert best > 100, best
