@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import itertools
+import threading
 from typing import Any, Callable, Iterable, List, Optional
 
 
@@ -24,6 +25,23 @@ class AsyncResult:
         self._error_callback = error_callback
         self._result = None
         self._done = False
+        self._lock = threading.Lock()
+        self._fired = False
+        if callback is not None or error_callback is not None:
+            # like multiprocessing's result-handler thread: callbacks fire on completion, not on get()
+            self._pending = len(refs)
+            for r in refs:
+                r.future().add_done_callback(self._on_done)
+
+    def _on_done(self, _fut):
+        with self._lock:
+            self._pending -= 1
+            if self._pending > 0:
+                return
+        try:
+            self.get(timeout=0)
+        except Exception:
+            pass
 
     def get(self, timeout=None):
         from .._private.worker import get
@@ -34,13 +52,18 @@ class AsyncResult:
                 flat = list(itertools.chain.from_iterable(out))
                 self._result = flat[0] if self._single else flat
                 self._done = True
-                if self._callback:
-                    self._callback(self._result)
+                self._fire(self._callback, self._result)
             except Exception as e:
-                if self._error_callback:
-                    self._error_callback(e)
+                self._fire(self._error_callback, e)
                 raise
         return self._result
+
+    def _fire(self, cb, arg):
+        with self._lock:
+            if self._fired or cb is None:
+                return
+            self._fired = True
+        cb(arg)
 
     def wait(self, timeout=None):
         from .._private.worker import wait
