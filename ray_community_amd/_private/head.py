@@ -935,7 +935,15 @@ class Head:
         for k, v in (renv.get("env_vars") or {}).items():
             env[str(k)] = str(v)
         if renv.get("working_dir"):
-            env["RCA_WORKING_DIR"] = str(renv["working_dir"])
+            from ..runtime_env import prepare_working_dir
+
+            try:
+                env["RCA_WORKING_DIR"] = prepare_working_dir(str(renv["working_dir"]), self.session_dir)
+            except Exception:
+                env["RCA_WORKING_DIR"] = str(renv["working_dir"])
+        if renv.get("pip") or renv.get("worker_process_setup_hook") or renv.get("_rca_setup_hook_blob"):
+            env["RCA_RUNTIME_ENV"] = json.dumps({k: renv[k] for k in ("pip", "worker_process_setup_hook",
+                                                                      "_rca_setup_hook_blob") if k in renv})
         if renv.get("py_modules"):
             env["RCA_PY_MODULES"] = json.dumps([str(p) for p in renv["py_modules"]])
         out_path = os.path.join(self.logs_dir, f"worker-{wid.hex()}.out")

@@ -124,7 +124,9 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
                     json.dump({"sock": head.sock_path, "pid": os.getpid(), "session": session}, f)
             except OSError:
                 pass
-        _state["runtime_env"] = runtime_env
+        from ..runtime_env import validate as _validate_env
+
+        _state["runtime_env"] = _validate_env(runtime_env)
         cw.set_global_core(core)
         return RayContext(_state)
 

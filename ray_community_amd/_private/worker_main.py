@@ -41,6 +41,25 @@ def _setup_paths():
 
 _setup_paths()
 
+
+def _setup_runtime_env():
+    """pip/conda requirement check + worker_process_setup_hook; the error (if any) fails every task."""
+    spec = os.environ.get("RCA_RUNTIME_ENV")
+    if not spec:
+        return None
+    try:
+        from ..runtime_env import apply_setup_hook, check_requirements
+
+        env = json.loads(spec)
+        check_requirements(env)
+        apply_setup_hook(env)
+        return None
+    except Exception as e:  # noqa
+        return e
+
+
+_ENV_ERROR = _setup_runtime_env()
+
 from .. import exceptions as exc  # noqa: E402
 from . import protocol as P  # noqa: E402
 from . import serialization as ser  # noqa: E402
@@ -172,6 +191,8 @@ class Worker:
         results = None
         try:
             try:
+                if _ENV_ERROR is not None:
+                    raise _ENV_ERROR
                 args, kwargs = self._resolve_args(spec)
                 if kind == "actor_creation":
                     cls = self._get_function(spec)

@@ -72,8 +72,10 @@ def build_strategy(opts: dict):
 def _merge_runtime_env(opts):
     from ._private.worker import _state
 
+    from .runtime_env import validate
+
     job_env = _state.get("runtime_env") or {}
-    env = opts.get("runtime_env")
+    env = validate(opts.get("runtime_env"))
     if not job_env and not env:
         return None
     out = dict(job_env)
