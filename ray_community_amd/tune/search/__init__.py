@@ -196,5 +196,13 @@ class Repeater(Searcher):
         return copy.deepcopy(self._current)
 
 
+def __getattr__(name):
+    if name in ("TPESearch", "OptunaSearch", "HyperOptSearch"):
+        from . import tpe
+
+        return getattr(tpe, name)
+    raise AttributeError(name)
+
+
 __all__ = ["Searcher", "BasicVariantGenerator", "ConcurrencyLimiter", "RandomSearch", "Repeater",
-           "generate_variants"]
+           "generate_variants", "TPESearch", "OptunaSearch", "HyperOptSearch"]

@@ -163,3 +163,36 @@ def test_with_parameters_and_run(ray_start_regular, tmp_path):
     ana = tune.run(tune.with_parameters(f, data=data), config={"k": tune.grid_search([1, 2])}, metric="s",
                    mode="max", storage_path=str(tmp_path))
     assert ana.best_config["k"] == 2
+
+
+def test_stoppers_unit():
+    from ray_community_amd.tune.stopper import (CombinedStopper, ExperimentPlateauStopper, MaximumIterationStopper,
+                                                TimeoutStopper, TrialPlateauStopper)
+
+    m = MaximumIterationStopper(3)
+    assert [m("t", {}) for _ in range(3)] == [False, False, True]
+    p = TrialPlateauStopper("x", std=0.01, num_results=3, grace_period=3)
+    assert [p("t", {"x": 1.0}) for _ in range(3)] == [False, False, True]
+    e = ExperimentPlateauStopper("x", top=2, std=0.0, mode="max")
+    e("a", {"x": 1.0})
+    e("b", {"x": 1.0})
+    assert e.stop_all()
+    t = TimeoutStopper(0)
+    assert t.stop_all()
+    assert CombinedStopper(MaximumIterationStopper(1), TimeoutStopper(100))("t", {})
+
+
+def test_tpe_search_finds_optimum(ray_start_regular, tmp_path):
+    from ray_community_amd import tune
+    from ray_community_amd.tune.search import ConcurrencyLimiter, TPESearch
+
+    def objective(config):
+        tune.report({"loss": (config["x"] - 3.0) ** 2 + (0 if config["opt"] == "adam" else 5)})
+
+    searcher = ConcurrencyLimiter(TPESearch(n_startup_trials=8, seed=0), max_concurrent=4)
+    grid = tune.Tuner(objective, param_space={"x": tune.uniform(-10, 10), "opt": tune.choice(["sgd", "adam"])},
+                      tune_config=tune.TuneConfig(metric="loss", mode="min", search_alg=searcher, num_samples=40),
+                      run_config=tune.RunConfig(storage_path=str(tmp_path), name="tpe")).fit()
+    best = grid.get_best_result()
+    assert best.metrics["loss"] < 1.0, best.metrics
+    assert best.config["opt"] == "adam"
