@@ -248,3 +248,11 @@ class PopulationBasedTrainingReplay(TrialScheduler):  # pragma: no cover
 
 __all__ = ["TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
            "MedianStoppingRule", "PopulationBasedTraining"]
+
+
+def __getattr__(name):
+    if name == "PB2":
+        from .pb2 import PB2
+
+        return PB2
+    raise AttributeError(name)

@@ -196,3 +196,26 @@ def test_tpe_search_finds_optimum(ray_start_regular, tmp_path):
     best = grid.get_best_result()
     assert best.metrics["loss"] < 1.0, best.metrics
     assert best.config["opt"] == "adam"
+
+
+def test_pb2(ray_start_regular, tmp_path):
+    from ray_community_amd.tune.schedulers.pb2 import PB2
+
+    def f(config):
+        v = 0.0
+        ck = tune.get_checkpoint()
+        if ck:
+            v = float(open(os.path.join(ck.path, "v")).read())
+        for i in range(12):
+            v += config["lr"]
+            with tempfile.TemporaryDirectory() as d:
+                open(os.path.join(d, "v"), "w").write(str(v))
+                tune.report({"v": v}, checkpoint=Checkpoint.from_directory(d))
+
+    pb2 = PB2(metric="v", mode="max", perturbation_interval=2, hyperparam_bounds={"lr": [0.0, 1.0]}, seed=0)
+    grid = tune.Tuner(f, param_space={"lr": tune.grid_search([0.01, 0.02, 0.5, 1.0])},
+                      tune_config=tune.TuneConfig(scheduler=pb2, max_concurrent_trials=4),
+                      run_config=RunConfig(storage_path=str(tmp_path))).fit()
+    assert grid.num_errors == 0
+    assert pb2.num_perturbations > 0
+    assert all(0.0 <= r.config["lr"] <= 1.0 for r in grid)
