@@ -1,0 +1,1 @@
+"""Hugging Face integrations (reference: ``python/ray/train/huggingface``)."""
