@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--device", default="cuda", help="cuda (the benchmark) | cpu (gloo rehearsal of the launch path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -43,12 +44,13 @@ def main():
     from ray_community_amd.train.torch import TorchTrainer
 
     loop_config = {"model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
-                   "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb}
+                   "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb,
+                   "device": args.device}
     # N=1: TorchTrainer runs the loop in a GPU worker actor of a local session.
     # N>1 under torchrun: TorchTrainer binds to the launcher's ranks (one process per GPU,
     # RCCL process group over xGMI) and runs this rank's share of the job.
     trainer = TorchTrainer(llama_train_loop_per_worker, train_loop_config=loop_config,
-                           scaling_config=ScalingConfig(num_workers=max(1, world), use_gpu=True),
+                           scaling_config=ScalingConfig(num_workers=max(1, world), use_gpu=args.device == "cuda"),
                            run_config=RunConfig(name="bench_llama", storage_path="/tmp/rca_bench"))
     result = trainer.fit()
     m = result.metrics

@@ -56,31 +56,34 @@ def llama_train_loop_per_worker(config: dict):
     bucket_cap_mb. Reports ``tokens_per_s`` (this worker) and ``ms_per_step``."""
     from . import report
 
+    dev_kind = config.get("device", "cuda")
+    device = None if dev_kind == "cuda" else torch.device(dev_kind)
+    sync = torch.cuda.synchronize if dev_kind == "cuda" else (lambda: None)
     steps = int(config.get("steps", 10))
     warmup = int(config.get("warmup", 3))
     seq_len = int(config.get("seq_len", 4096))
     mb = int(config.get("micro_batch", 2))
     net, ddp, opt, batch, step = build_llama_training(
         model=config.get("model", "llama3-8b"), seq_len=seq_len, micro_batch=mb, lr=config.get("lr", 3e-4),
-        bucket_cap_mb=config.get("bucket_cap_mb", 256.0), **config.get("model_overrides", {}))
+        bucket_cap_mb=config.get("bucket_cap_mb", 256.0), device=device, **config.get("model_overrides", {}))
     rank, world = _dist_info()
     data = [batch() for _ in range(2)]
     loss = None
     for i in range(warmup):
         loss = step(*data[i % 2])
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(steps):
         loss = step(*data[i % 2])
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
-    el_t = torch.tensor([el], device="cuda", dtype=torch.float64)
+    el_t = torch.tensor([el], device="cuda" if dev_kind == "cuda" else "cpu", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
@@ -91,7 +94,7 @@ def llama_train_loop_per_worker(config: dict):
         "ms_per_step": 1000.0 * el / max(steps, 1),
         "tokens_per_s": tokens / el if el > 0 else 0.0,
         "world_size": world,
-        "mem_gb": torch.cuda.max_memory_allocated() / 1e9,
+        "mem_gb": torch.cuda.max_memory_allocated() / 1e9 if dev_kind == "cuda" else 0.0,
         "flops_per_token": net.cfg.flops_per_token(seq_len),
     }
     report(metrics)

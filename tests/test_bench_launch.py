@@ -1,0 +1,23 @@
+"""The driver's multi-GPU launch path of bench.py (torchrun -> TorchTrainer external-launcher mode
+-> bucketed DDP), rehearsed on CPU with gloo and the tiny Llama preset."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_torchrun_two_ranks_cpu(tmp_path):
+    env = dict(os.environ)
+    env.pop("RCA_ADDRESS", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29541", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--model", "llama3-tiny", "--seq-len", "128", "--device", "cpu"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints exactly one JSON line
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
+    assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["higher_is_better"] is True
