@@ -1730,6 +1730,58 @@ class Head:
     def rpc_ping(self, caller):
         return "pong"
 
+    # ------------------------------------------------------------------ metrics
+    def rpc_metrics_push(self, caller, source, text):
+        if not hasattr(self, "_metrics_text"):
+            self._metrics_text = {}
+        self._metrics_text[source] = (time.time(), text)
+        return True
+
+    def rpc_metrics_text(self, caller):
+        """Prometheus exposition: built-in cluster gauges + the latest push of every process."""
+        from collections import Counter
+
+        lines = []
+
+        def gauge(name, help_, samples):
+            lines.append(f"# HELP {name} {help_}")
+            lines.append(f"# TYPE {name} gauge")
+            for tags, v in samples:
+                t = ",".join(f'{k}="{val}"' for k, val in tags.items())
+                lines.append(f"{name}{{{t}}} {v}" if t else f"{name} {v}")
+
+        total, avail = self.rpc_cluster_resources(caller), self.rpc_available_resources(caller)
+        gauge("rca_cluster_resources_total", "Total logical resources", [({"resource": k}, v) for k, v in total.items()])
+        gauge("rca_cluster_resources_available", "Available logical resources",
+              [({"resource": k}, v) for k, v in avail.items()])
+        st = self.store.stats()
+        gauge("rca_object_store_used_bytes", "Shared-memory object store bytes in use", [({}, st.get("used", 0))])
+        gauge("rca_object_store_capacity_bytes", "Object store capacity", [({}, st.get("capacity", 0))])
+        gauge("rca_object_store_spilled_bytes", "Bytes spilled to disk", [({}, self.spilled_bytes)])
+        tc = Counter(TASK_STATE_NAMES[t.state] for t in self.tasks.values())
+        gauge("rca_tasks", "Tasks by state", [({"state": k}, v) for k, v in tc.items()])
+        ac = Counter(a.state for a in self.actors.values())
+        gauge("rca_actors", "Actors by state", [({"state": k}, v) for k, v in ac.items()])
+        gauge("rca_workers", "Worker processes", [({"node_id": "all"}, len(self.workers))])
+        seen = set()
+        now = time.time()
+        for src, (t, text) in list(getattr(self, "_metrics_text", {}).items()):
+            if now - t > 300:
+                continue
+            for ln in text.splitlines():
+                if ln.startswith("#"):
+                    if ln in seen:
+                        continue
+                    seen.add(ln)
+                    lines.append(ln)
+                elif ln.strip():
+                    name, _, rest = ln.partition("{") if "{" in ln.split(" ")[0] else (ln.split(" ")[0], "", "")
+                    if rest:
+                        lines.append(f'{name}{{source="{src}",{rest}')
+                    else:
+                        lines.append(f'{ln.split(" ")[0]}{{source="{src}"}} {ln.split(" ", 1)[1]}')
+        return "\n".join(lines) + "\n"
+
     # ================================================================== timers
     def _add_timer(self, delay, fn):
         self.timers.append((time.time() + delay, fn))

@@ -118,6 +118,11 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
                               session_dir=session)
             head.driver_free_gpu_cb = core.free_gpu_objects
             _state.update(head=head, core=core, mode=SCRIPT_MODE, namespace=ns, address=head.sock_path)
+            if include_dashboard:
+                from .dashboard import Dashboard
+
+                _state["dashboard"] = Dashboard(head, dashboard_host or "127.0.0.1",
+                                                8265 if dashboard_port is None else int(dashboard_port))
             try:
                 os.makedirs(root, exist_ok=True)
                 with open(os.path.join(root, "latest_session.json"), "w") as f:
@@ -157,8 +162,11 @@ class RayContext(dict):
     def __init__(self, st):
         super().__init__(address=st.get("address"), node_id=st["core"].node_id if st["core"] else None,
                          namespace=st.get("namespace"))
+        dash = st.get("dashboard")
+        self.dashboard_url = dash.url if dash is not None else None
+        if dash is not None:
+            self["dashboard_url"] = self.dashboard_url
         self.address_info = dict(self)
-        self.dashboard_url = None
 
     def __enter__(self):
         return self
@@ -178,6 +186,12 @@ def shutdown(_exiting_interpreter: bool = False):
             return
         if _state["mode"] == WORKER_MODE:
             return
+        dash = _state.pop("dashboard", None)
+        if dash is not None:
+            try:
+                dash.stop()
+            except Exception:
+                pass
         core.shutdown()
         cw.set_global_core(None)
         _state.update(core=None, head=None, mode=None)

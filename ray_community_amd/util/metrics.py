@@ -17,6 +17,7 @@ class Metric:
     kind = "untyped"
 
     def __init__(self, name: str, description: str = "", tag_keys: Optional[Tuple[str, ...]] = None):
+        _ensure_pusher()
         if not name:
             raise ValueError("Empty name is not allowed. Please provide a metric name.")
         if tag_keys is not None and not isinstance(tag_keys, tuple):
@@ -120,3 +121,32 @@ def export_prometheus() -> str:
             t = ",".join(f'{k}="{val}"' for k, val in tags.items())
             lines.append(f"{name}{{{t}}} {v}" if t else f"{name} {v}")
     return "\n".join(lines) + "\n"
+
+
+# ------------------------------------------------------------------ push to the head
+_PUSHER = {"thread": None}
+
+
+def _ensure_pusher(period_s: float = 2.0):
+    """Every process that records metrics pushes its exposition text to the head (which serves
+    the cluster-wide ``/metrics`` of the dashboard)."""
+    if _PUSHER["thread"] is not None:
+        return
+    import os
+
+    def loop():
+        import time
+
+        src = f"{os.uname().nodename}:{os.getpid()}"
+        while True:
+            time.sleep(period_s)
+            try:
+                from .._private.worker import _core, is_initialized
+
+                if is_initialized():
+                    _core().client.call("metrics_push", src, export_prometheus())
+            except Exception:
+                pass
+
+    _PUSHER["thread"] = threading.Thread(target=loop, daemon=True, name="rca-metrics-push")
+    _PUSHER["thread"].start()

@@ -1,0 +1,45 @@
+"""Metrics export + dashboard JSON API (reference tests: python/ray/tests/test_metrics_agent.py,
+dashboard/tests)."""
+import json
+import time
+import urllib.request
+
+import ray_community_amd as ray
+
+
+def _get(url):
+    with urllib.request.urlopen(url, timeout=10) as r:
+        return r.read().decode()
+
+
+def test_dashboard_metrics_and_state(shutdown_only):
+    ctx = ray.init(num_cpus=2, include_dashboard=True, dashboard_port=0)
+    url = ctx.dashboard_url
+    assert url
+
+    @ray.remote
+    class Reporter:
+        def record(self):
+            from ray_community_amd.util.metrics import Counter, Gauge
+
+            c = Counter("rca_test_requests", description="requests", tag_keys=("route",))
+            c.inc(3.0, tags={"route": "/a"})
+            Gauge("rca_test_queue").set(7)
+            return True
+
+    r = Reporter.remote()
+    assert ray.get(r.record.remote())
+    deadline = time.time() + 20
+    text = ""
+    while time.time() < deadline:
+        text = _get(url + "/metrics")
+        if "rca_test_requests" in text:
+            break
+        time.sleep(0.5)
+    assert 'rca_test_requests{source=' in text and 'route="/a"' in text, text[-2000:]
+    assert "rca_cluster_resources_total" in text and "rca_object_store_capacity_bytes" in text
+    actors = json.loads(_get(url + "/api/actors"))
+    assert any(a["class_name"] == "Reporter" for a in actors)
+    status = json.loads(_get(url + "/api/cluster_status"))
+    assert status["total"]["CPU"] == 2.0
+    assert json.loads(_get(url + "/api/version"))["version"]
