@@ -25,7 +25,13 @@ def _appo():
     return APPO, APPOConfig()
 
 
-ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo}
+def _sac():
+    from .sac import SAC, SACConfig
+
+    return SAC, SACConfig()
+
+
+ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo, "SAC": _sac}
 
 
 def get_algorithm_class(name: str, return_config: bool = False):

@@ -18,7 +18,7 @@ import torch
 
 from ... import ops
 from ..policy.sample_batch import SampleBatch
-from .rl_module import RLModule
+from .rl_module import RLModule, make_module
 
 
 def _device(use_gpu: bool):
@@ -35,8 +35,7 @@ class Learner:
         seed = config.get("seed")
         if seed is not None:
             torch.manual_seed(int(seed))
-        self.module = RLModule(obs_space, act_space, config.get("model"), q_head=config.get("q_head", False)).to(
-            self.device)
+        self.module = make_module(config, obs_space, act_space).to(self.device)
         self.ddp = None
         import torch.distributed as dist
 
@@ -266,6 +265,55 @@ class Learner:
         self._step(loss)
         self.num_updates += 1
         return {"loss": loss.item(), "mean_q": qa.mean().item(), "mean_td_error": td.abs().mean().item()}
+
+    # ------------------------------------------------------------------ SAC
+    def update_sac(self, batch: SampleBatch) -> Dict:
+        """Twin-Q soft actor-critic step (reference: rllib/algorithms/sac/torch/sac_torch_learner.py)."""
+        cfg = self.cfg
+        m = self.module
+        if not hasattr(self, "_sac_opts"):
+            lr = cfg.get("lr", 3e-4)
+            olr = cfg.get("optimization_config") or {}
+            self._sac_opts = (
+                torch.optim.Adam(m.pi.parameters(), lr=olr.get("actor_learning_rate", lr)),
+                torch.optim.Adam(list(m.q1.parameters()) + list(m.q2.parameters()),
+                                 lr=olr.get("critic_learning_rate", lr)),
+                torch.optim.Adam([m.log_alpha], lr=olr.get("entropy_learning_rate", lr)))
+            te = cfg.get("target_entropy", "auto")
+            self._target_entropy = -float(m.act_dim) if te in (None, "auto") else float(te)
+        opt_pi, opt_q, opt_a = self._sac_opts
+        b = batch.to_device(self.device)
+        obs, nobs = b["obs"].float(), b["new_obs"].float()
+        u = m._unscale(b["actions"].float().reshape(obs.shape[0], -1))
+        r, term = b["rewards"].float(), b["terminateds"].float()
+        gamma = cfg.get("gamma", 0.99) ** cfg.get("n_step", 1)
+        alpha = m.log_alpha.exp().detach()
+        with torch.no_grad():
+            un, lpn = m.policy(nobs)
+            q1t, q2t = m.q(nobs, un, target=True)
+            y = r + gamma * (1 - term) * (torch.min(q1t, q2t) - alpha * lpn)
+        q1, q2 = m.q(obs, u)
+        q_loss = 0.5 * (((q1 - y) ** 2).mean() + ((q2 - y) ** 2).mean())
+        opt_q.zero_grad(set_to_none=True)
+        q_loss.backward()
+        gc = cfg.get("grad_clip")
+        if gc:
+            torch.nn.utils.clip_grad_norm_(list(m.q1.parameters()) + list(m.q2.parameters()), gc)
+        opt_q.step()
+        un, lp = m.policy(obs)
+        q1n, q2n = m.q(obs, un)
+        pi_loss = (alpha * lp - torch.min(q1n, q2n)).mean()
+        opt_pi.zero_grad(set_to_none=True)
+        pi_loss.backward()
+        opt_pi.step()
+        a_loss = -(m.log_alpha * (lp.detach() + self._target_entropy)).mean()
+        opt_a.zero_grad(set_to_none=True)
+        a_loss.backward()
+        opt_a.step()
+        m.polyak(cfg.get("tau", 5e-3))
+        self.num_updates += 1
+        return {"critic_loss": q_loss.item(), "actor_loss": pi_loss.item(), "alpha_loss": a_loss.item(),
+                "alpha_value": alpha.item(), "mean_q": q1.detach().mean().item()}
 
     def sync_target(self):
         if self.target is not None:

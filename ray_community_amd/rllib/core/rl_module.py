@@ -169,3 +169,13 @@ class RLModule(nn.Module):
 
     def set_state(self, state):
         self.load_state_dict(state)
+
+
+def make_module(config: Dict, observation_space, action_space):
+    """Module factory keyed by ``config['module_class']`` (``"actor_critic"`` default, ``"sac"``)."""
+    kind = config.get("module_class", "actor_critic")
+    if kind == "sac":
+        from .sac_module import SACModule
+
+        return SACModule(observation_space, action_space, config.get("model"))
+    return RLModule(observation_space, action_space, config.get("model"), q_head=config.get("q_head", False))

@@ -13,7 +13,7 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
-from ..core.rl_module import RLModule
+from ..core.rl_module import make_module
 from ..policy.sample_batch import SampleBatch
 from .envs import make_vector_env
 
@@ -30,8 +30,7 @@ class EnvRunner:
         self.env = make_vector_env(config["env"], config.get("num_envs_per_env_runner", 1), config.get("env_config"),
                                    seed=self.seed)
         self.N = self.env.num_envs
-        self.module = RLModule(self.env.observation_space, self.env.action_space, config.get("model"),
-                               q_head=config.get("q_head", False))
+        self.module = make_module(config, self.env.observation_space, self.env.action_space)
         self.module.eval()
         self.obs, _ = self.env.reset(seed=self.seed)
         self.ep_ret = np.zeros(self.N)
@@ -133,12 +132,20 @@ class EnvRunner:
         N = self.N
         T = max(1, int(num_steps) // N)
         out = {k: [] for k in ("obs", "actions", "rewards", "new_obs", "terminateds")}
+        continuous = not hasattr(self.module, "q_values")
+        space = self.env.action_space
         for _ in range(T):
-            q = self.module.q_values(torch.from_numpy(self.obs))
-            a = q.argmax(-1).numpy()
-            rnd = self._rng.random(N) < epsilon
-            if rnd.any():
-                a[rnd] = self._rng.integers(0, self.env.action_space.n, int(rnd.sum()))
+            if continuous:  # SAC: stochastic policy; epsilon = probability of a uniform random action
+                a = self.module.forward_exploration(torch.from_numpy(self.obs))[0].numpy().astype(np.float32)
+                rnd = self._rng.random(N) < epsilon
+                if rnd.any():
+                    a[rnd] = self._rng.uniform(space.low, space.high, size=(int(rnd.sum()),) + space.shape)
+            else:
+                q = self.module.q_values(torch.from_numpy(self.obs))
+                a = q.argmax(-1).numpy()
+                rnd = self._rng.random(N) < epsilon
+                if rnd.any():
+                    a[rnd] = self._rng.integers(0, space.n, int(rnd.sum()))
             nobs, r, te, tr, info = self.env.step(a)
             done = te | tr
             nxt = np.where(done.reshape((-1,) + (1,) * (nobs.ndim - 1)), info["final_obs"], nobs)

@@ -162,3 +162,23 @@ def test_impala_appo_cartpole_learn(shutdown_only, algo):
             break
     algo_.stop()
     assert best > 100, best
+
+
+def test_sac_pendulum_learns(shutdown_only):
+    from ray_community_amd.rllib import SACConfig
+
+    ray.init(num_cpus=2)
+    cfg = (SACConfig().environment("Pendulum-v1").env_runners(num_envs_per_env_runner=4, rollout_fragment_length=16)
+           .training(train_batch_size=128, num_steps_sampled_before_learning_starts=1000, training_intensity=1.0)
+           .reporting(metrics_num_episodes_for_smoothing=8).debugging(seed=0))
+    algo = cfg.build()
+    best = -1e9
+    for _ in range(150):
+        r = algo.train()
+        best = max(best, r["episode_reward_mean"])
+        if best > -400:
+            break
+    a = algo.compute_single_action(np.zeros(3, dtype=np.float32))
+    algo.stop()
+    assert best > -400, best
+    assert a.shape == (1,) and -2.0 <= float(a[0]) <= 2.0
