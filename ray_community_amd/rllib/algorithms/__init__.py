@@ -2,8 +2,9 @@ from .algorithm import Algorithm
 from .algorithm_config import AlgorithmConfig
 from .dqn import DQN, DQNConfig
 from .impala import APPO, IMPALA, APPOConfig, IMPALAConfig
+from .marwil import BC, MARWIL, BCConfig, MARWILConfig
 from .ppo import PPO, PPOConfig
 from .sac import SAC, SACConfig
 from .registry import ALGORITHMS, get_algorithm_class
 
-__all__ = ["Algorithm", "AlgorithmConfig", "PPO", "PPOConfig", "DQN", "DQNConfig", "IMPALA", "IMPALAConfig", "APPO", "APPOConfig", "SAC", "SACConfig", "get_algorithm_class", "ALGORITHMS"]
+__all__ = ["Algorithm", "AlgorithmConfig", "PPO", "PPOConfig", "DQN", "DQNConfig", "IMPALA", "IMPALAConfig", "APPO", "APPOConfig", "SAC", "SACConfig", "MARWIL", "MARWILConfig", "BC", "BCConfig", "get_algorithm_class", "ALGORITHMS"]

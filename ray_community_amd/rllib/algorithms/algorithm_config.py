@@ -18,6 +18,8 @@ class AlgorithmConfig:
         self.action_space = None
         # env runners
         self.num_env_runners = 0
+        self.input_ = "sampler"
+        self.output = None
         self.num_envs_per_env_runner = 1
         self.rollout_fragment_length: Any = "auto"
         self.batch_mode = "truncate_episodes"
@@ -136,7 +138,13 @@ class AlgorithmConfig:
             raise NotImplementedError("multi-agent training is not supported yet")
         return self
 
-    def offline_data(self, **kw):
+    def offline_data(self, *, input_=None, output=None, input_config=None, output_config=None, **kw):
+        """``input_``: directory / glob of JSON batches for offline algorithms (BC, MARWIL);
+        ``output``: directory the env runners write their sampled batches to."""
+        if input_ is not None:
+            self.input_ = input_
+        if output is not None:
+            self.output = output
         return self
 
     def callbacks(self, cb=None, **kw):

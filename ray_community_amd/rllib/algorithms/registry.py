@@ -31,7 +31,20 @@ def _sac():
     return SAC, SACConfig()
 
 
-ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo, "SAC": _sac}
+def _marwil():
+    from .marwil import MARWIL, MARWILConfig
+
+    return MARWIL, MARWILConfig()
+
+
+def _bc():
+    from .marwil import BC, BCConfig
+
+    return BC, BCConfig()
+
+
+ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo, "SAC": _sac, "MARWIL": _marwil,
+              "BC": _bc}
 
 
 def get_algorithm_class(name: str, return_config: bool = False):

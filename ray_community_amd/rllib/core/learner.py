@@ -266,6 +266,47 @@ class Learner:
         self.num_updates += 1
         return {"loss": loss.item(), "mean_q": qa.mean().item(), "mean_td_error": td.abs().mean().item()}
 
+    # ------------------------------------------------------------------ MARWIL / BC
+    def update_marwil(self, batch: SampleBatch) -> Dict:
+        cfg = self.cfg
+        b = batch.to_device(self.device)
+        if batch.fragment_shape is not None:
+            N, T = batch.fragment_shape
+            rew = b["rewards"].float()
+            term, trunc = b["terminateds"].bool(), b["truncateds"].bool()
+            nv = torch.zeros_like(rew)
+            if "next_vf_preds" in b:
+                boot = b["next_vf_preds"].float()
+                nv[:, -1] = boot[:, -1]
+                nv = torch.where(trunc, boot, nv)
+            ret, _ = ops.compute_gae(rew, torch.zeros_like(rew), term, term | trunc, cfg.get("gamma", 0.99), 1.0,
+                                     next_values=nv)
+            obs = b["obs"].reshape((N * T,) + tuple(b["obs"].shape[2:]))
+            act = b["actions"].reshape((N * T,) + tuple(b["actions"].shape[2:]))
+            ret = ret.reshape(-1)
+        else:
+            obs, act = b["obs"], b["actions"]
+            ret = b["returns"].float() if "returns" in b else b["rewards"].float()
+        logits, v = self.forward(obs)
+        logp = self.module.dist(logits).logp(act)
+        beta = float(cfg.get("beta", 1.0))
+        if beta > 0:
+            adv = (ret - v).detach()
+            if not hasattr(self, "_adv_c2"):
+                self._adv_c2 = float(cfg.get("moving_average_sqd_adv_norm_start", 100.0))
+            rate = float(cfg.get("moving_average_sqd_adv_norm_update_rate", 1e-8))
+            self._adv_c2 += rate * (float((adv ** 2).mean()) - self._adv_c2)
+            w = torch.exp(beta * adv / (self._adv_c2 ** 0.5 + 1e-8)).clamp(max=20.0)
+        else:
+            w = torch.ones_like(logp)
+        pi_loss = -(w * logp).mean()
+        vf_loss = 0.5 * ((ret - v) ** 2).mean()
+        loss = pi_loss + float(cfg.get("vf_coeff", 1.0)) * vf_loss
+        self._step(loss)
+        self.num_updates += 1
+        return {"policy_loss": pi_loss.item(), "vf_loss": vf_loss.item(), "total_loss": loss.item(),
+                "mean_logp": logp.detach().mean().item()}
+
     # ------------------------------------------------------------------ SAC
     def update_sac(self, batch: SampleBatch) -> Dict:
         """Twin-Q soft actor-critic step (reference: rllib/algorithms/sac/torch/sac_torch_learner.py)."""

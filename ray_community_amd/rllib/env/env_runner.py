@@ -124,6 +124,12 @@ class EnvRunner:
         if logits_buf is not None:
             b[SampleBatch.ACTION_DIST_INPUTS] = logits_buf
         b.fragment_shape = (N, T)
+        if self.cfg.get("output"):
+            if getattr(self, "_writer", None) is None:
+                from ..offline import JsonWriter
+
+                self._writer = JsonWriter(self.cfg["output"])
+            self._writer.write(b)
         return b
 
     @torch.no_grad()

@@ -182,3 +182,39 @@ def test_sac_pendulum_learns(shutdown_only):
     algo.stop()
     assert best > -400, best
     assert a.shape == (1,) and -2.0 <= float(a[0]) <= 2.0
+
+
+@pytest.mark.parametrize("algo", ["BC", "MARWIL"])
+def test_offline_bc_marwil_from_logged_ppo(shutdown_only, tmp_path, algo):
+    from ray_community_amd.rllib import BCConfig, MARWILConfig
+    from ray_community_amd.rllib.env.env_runner import EnvRunner
+
+    ray.init(num_cpus=4)
+    ppo = (PPOConfig().environment("CartPole-v1").env_runners(num_env_runners=2, num_envs_per_env_runner=8)
+           .training(lr=3e-4, train_batch_size=2048, minibatch_size=256, num_epochs=8, vf_loss_coeff=0.01,
+                     model={"fcnet_hiddens": [64, 64]}).debugging(seed=0))
+    teacher = ppo.build()
+    for _ in range(30):
+        if teacher.train()["episode_reward_mean"] > 150:
+            break
+    # log the teacher's behaviour to JSON
+    rd = ppo.runner_dict()
+    rd["output"] = str(tmp_path / "logged")
+    rd["num_envs_per_env_runner"] = 8
+    runner = EnvRunner(rd, 7)
+    runner.set_weights(teacher.get_weights(), 1)
+    for _ in range(4):
+        runner.sample(8 * 256)
+    runner._writer.close()
+    teacher.stop()
+
+    cfg_cls = BCConfig if algo == "BC" else MARWILConfig
+    cfg = (cfg_cls().environment("CartPole-v1").offline_data(input_=str(tmp_path / "logged"))
+           .training(lr=1e-3, train_batch_size=2048, model={"fcnet_hiddens": [64, 64]})
+           .evaluation(evaluation_interval=None, evaluation_duration=10).debugging(seed=0))
+    student = cfg.build()
+    for _ in range(60):
+        student.train()
+    ev = student.evaluate()
+    student.stop()
+    assert ev["episode_reward_mean"] > 100, ev
