@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..parallel.fused_linear import FusedWgradLinear
 
 
 @dataclass
@@ -82,8 +83,8 @@ class Attention(nn.Module):
         super().__init__()
         self.cfg = cfg
         D = cfg.head_dim
-        self.qkv = nn.Linear(cfg.hidden_size, (cfg.num_heads + 2 * cfg.num_kv_heads) * D, bias=False)
-        self.o = nn.Linear(cfg.num_heads * D, cfg.hidden_size, bias=False)
+        self.qkv = FusedWgradLinear(cfg.hidden_size, (cfg.num_heads + 2 * cfg.num_kv_heads) * D)
+        self.o = FusedWgradLinear(cfg.num_heads * D, cfg.hidden_size)
 
     def forward(self, x, cs, B, S, positions=None):
         cfg = self.cfg
@@ -105,8 +106,8 @@ class Attention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.gate_up = nn.Linear(cfg.hidden_size, 2 * cfg.intermediate_size, bias=False)
-        self.down = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+        self.gate_up = FusedWgradLinear(cfg.hidden_size, 2 * cfg.intermediate_size)
+        self.down = FusedWgradLinear(cfg.intermediate_size, cfg.hidden_size)
 
     def forward(self, x):
         return self.down(ops.swiglu(self.gate_up(x)))
@@ -128,7 +129,7 @@ class Llama(nn.Module):
         self.embed = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.num_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.norm_eps)
-        self.lm_head = None if cfg.tie_embeddings else nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False)
+        self.lm_head = None if cfg.tie_embeddings else FusedWgradLinear(cfg.hidden_size, cfg.vocab_size)
         self._cs = {}
         self.reset_parameters()
 
@@ -168,8 +169,9 @@ class Llama(nn.Module):
         return h  # [T, H], final-normed
 
     def logits(self, h):
-        w = self.embed.weight if self.lm_head is None else self.lm_head.weight
-        return F.linear(h, w)
+        if self.lm_head is not None:
+            return self.lm_head(h)
+        return F.linear(h, self.embed.weight)
 
     def forward(self, tokens, labels=None, positions=None):
         h = self.hidden_states(tokens, positions)

@@ -51,6 +51,7 @@ class DistributedDataParallel(nn.Module):
                     dist.broadcast(b, src=src, group=process_group)
             for p in self.flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                p._rca_grad_ready = self._on_grad  # fused-wgrad linears bypass AccumulateGrad
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
@@ -94,6 +95,8 @@ class DistributedDataParallel(nn.Module):
         """Launch any bucket whose grads never arrived (unused params) and wait for all."""
         if self.world <= 1:
             return
+        if any(w is None for w in self._works):
+            self.flat.finalize_fresh()
         for bi, w in enumerate(self._works):
             if w is None:
                 self._launch(bi)

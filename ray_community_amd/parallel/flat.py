@@ -95,9 +95,33 @@ class FlatParameters:
             for p in b.params:
                 self.param_bucket[id(p)] = b.index
         self.param_offset = {id(p): off for p, off in zip(self.params, offs)}
+        # Fused-wgrad linears (parallel/fused_linear.py) overwrite their gradient region on the first
+        # accumulation, so zero_grad only has to clear the tail holding everything else -- valid
+        # when all fused weights precede all other parameters in the layout.
+        self.fused = [p for p in self.params if getattr(p, "_rca_fused_wgrad", False) and self.grad_is_view]
+        fused_ids = {id(p) for p in self.fused}
+        first_other = next((i for i, p in enumerate(self.params) if id(p) not in fused_ids), len(self.params))
+        if self.fused and all(id(p) not in fused_ids for p in self.params[first_other:]):
+            self.zero_start = offs[first_other] if first_other < len(self.params) else o
+            for p in self.fused:
+                p._rca_flat_grad = True
+                p._rca_grad_fresh = True
+        else:
+            self.fused = []
+            self.zero_start = 0
+
+    def finalize_fresh(self):
+        """Zero the regions of fused weights that received no gradient since zero_grad."""
+        for p in self.fused:
+            if p._rca_grad_fresh:
+                off = self.param_offset[id(p)]
+                self.grad[off: off + p.numel()].zero_()
+                p._rca_grad_fresh = False
 
     def zero_grad(self):
-        self.grad.zero_()
+        self.grad[self.zero_start:].zero_()
+        for p in self.fused:
+            p._rca_grad_fresh = True
         if self.grad_is_view:
             for p, off in zip(self.params, self.offsets):
                 if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():

@@ -59,6 +59,7 @@ class FlatAdamW:
         bc1 = 1.0 - self.b1 ** t
         bc2 = 1.0 - self.b2 ** t
         flat = self.flat
+        flat.finalize_fresh()
         g = flat.grad
         clip = self.max_grad_norm if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
         if clip or self.track_grad_norm:

@@ -83,3 +83,39 @@ def test_attention_reference_matches_sdpa():
     assert torch.allclose(ops.flash_attention(q, k, v, True), o)
     qkv = torch.cat([q.reshape(B * S, -1), k.reshape(B * S, -1), v.reshape(B * S, -1)], dim=1)
     assert torch.allclose(ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D), o.reshape(B * S, -1), atol=1e-6)
+
+
+def test_fused_wgrad_linear_matches_autograd_with_accumulation():
+    import contextlib
+
+    from ray_community_amd.models import build_llama
+    from ray_community_amd.parallel import DistributedDataParallel, FlatAdamW
+
+    def run(fused):
+        torch.manual_seed(0)
+        net = build_llama("llama3-tiny", device="cpu", dtype=torch.float32)
+        if not fused:
+            for m in net.modules():
+                if getattr(getattr(m, "weight", None), "_rca_fused_wgrad", False):
+                    m.weight._rca_fused_wgrad = False
+        ddp = DistributedDataParallel(net)
+        assert (len(ddp.flat.fused) > 0) == fused
+        opt = FlatAdamW(ddp.flat, lr=1e-3)
+        torch.manual_seed(1)
+        tok = torch.randint(0, net.cfg.vocab_size, (2, 33))
+        losses = []
+        for i in range(4):
+            with ddp.no_sync() if i == 0 else contextlib.nullcontext():
+                loss = ddp(tok[:, :-1], tok[:, 1:])
+                loss.backward()
+            if i == 0:
+                continue
+            ddp.finish_gradient_sync()
+            opt.step()
+            opt.zero_grad()
+            losses.append(loss.item())
+        return losses, ddp.flat.data.clone()
+
+    (la, da), (lb, db) = run(True), run(False)
+    assert la == lb
+    assert torch.equal(da, db)
