@@ -92,6 +92,11 @@ __device__ __forceinline__ bf16x8_t acc_to_bf16(const f32x16& x, int s) {
   return r;
 }
 
+// Pin a register operand loaded from global memory: the asm "redefines" it after its load has
+// landed, so hipcc's loop-merged s_waitcnt bookkeeping stops treating it as pending inside the
+// main loop (otherwise every tile's first MFMAs wait vmcnt for the NEXT tile's staging loads).
+__device__ __forceinline__ void settle(bf16x8_t& v) { asm volatile("" : "+v"(v)); }
+
 __device__ __forceinline__ bf16x8_t gload8(const bf16_t* p) {
   return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4*>(p));
 }
@@ -196,6 +201,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   bf16x8_t qf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) qf[ks] = gload8(Qr + 16 * ks + 8 * h);
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) settle(qf[ks]);
 
   f32x16 o[NDB];
 #pragma unroll
@@ -223,63 +230,83 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
       vst.load(kb + BK, sv);
     }
     if (!CAUSAL || kb <= qw0 + 31) {
-      bf16x8_t fr[4 * NDB > 2 * NKS ? 4 * NDB : 2 * NKS];
+      // Two 32-key halves, software-pipelined: half 1's S^T MFMAs issue beside half 0's softmax
+      // VALU work, and half 0's P.V MFMAs beside half 1's row max.
+      auto qk = [&](int t, auto diagc) {
+        constexpr bool DIAG = decltype(diagc)::value;
+        bf16x8_t fr[NKS];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int kk = 0; kk < NKS; ++kk) fr[kk] = lds_b128(Ks + ((kk & 1) ? rb1 : rb0) + 4 * G8 * t + 512 * (kk >> 1));
+        f32x16 sx = zero16();
 #pragma unroll
-        for (int kk = 0; kk < NKS; ++kk)
-          fr[t * NKS + kk] = lds_b128(Ks + ((kk & 1) ? rb1 : rb0) + 4 * G8 * t + 512 * (kk >> 1));
-      f32x16 s0 = zero16(), s1 = zero16();
+        for (int kk = 0; kk < NKS; ++kk) sx = mfma32(fr[kk], qf[kk], sx);
+        if constexpr (DIAG) {
 #pragma unroll
-      for (int kk = 0; kk < NKS; ++kk) {
-        s0 = mfma32(fr[kk], qf[kk], s0);
-        s1 = mfma32(fr[NKS + kk], qf[kk], s1);
-      }
-      if (CAUSAL && kb + BK - 1 > qw0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kofs = kb - qw0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          s0[r] = kofs > l32 ? -INFINITY : s0[r];
-          s1[r] = kofs + 32 > l32 ? -INFINITY : s1[r];
+          for (int r = 0; r < 16; ++r) {
+            const int kofs = kb + 32 * t - qw0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            sx[r] = kofs > l32 ? -INFINITY : sx[r];
+          }
         }
-      }
-      const float mts = xhalf_max(max16(s1, max16(s0, -INFINITY))) * scale2;
-      if (__builtin_amdgcn_ballot_w64(mts > m + THR) != 0) {
-        const float mn = fmaxf(m, mts);
-        const float a = mn == -INFINITY ? 1.f : fast_exp2(m - mn);
+        return sx;
+      };
+      auto rescale = [&](float mt_raw) {
+        const float mts = mt_raw * scale2;
+        if (__builtin_amdgcn_ballot_w64(mts > m + THR) != 0) {
+          const float mn = fmaxf(m, mts);
+          const float a = mn == -INFINITY ? 1.f : fast_exp2(m - mn);
 #pragma unroll
-        for (int i = 0; i < NDB; ++i) o[i] *= a;
-        lsum *= a;
-        m = mn;
-      }
-      const float nm = -m;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+          for (int i = 0; i < NDB; ++i) o[i] *= a;
+          lsum *= a;
+          m = mn;
+        }
+      };
+      auto softmax = [&](f32x16& sx, bf16x8_t& p0, bf16x8_t& p1) {
+        const float nm = -m;
+        float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        s0[r] = fast_exp2(fmaf(s0[r], scale2, nm));
-        s0[r + 1] = fast_exp2(fmaf(s0[r + 1], scale2, nm));
-        s1[r] = fast_exp2(fmaf(s1[r], scale2, nm));
-        s1[r + 1] = fast_exp2(fmaf(s1[r + 1], scale2, nm));
-        a0 += s0[r];
-        a1 += s0[r + 1];
-        a2 += s1[r];
-        a3 += s1[r + 1];
-      }
-      lsum += (a0 + a1) + (a2 + a3);
-      const bf16x8_t pf[4] = {acc_to_bf16(s0, 0), acc_to_bf16(s0, 1), acc_to_bf16(s1, 0), acc_to_bf16(s1, 1)};
+        for (int r = 0; r < 16; r += 2) {
+          sx[r] = fast_exp2(fmaf(sx[r], scale2, nm));
+          sx[r + 1] = fast_exp2(fmaf(sx[r + 1], scale2, nm));
+          a0 += sx[r];
+          a1 += sx[r + 1];
+        }
+        lsum += a0 + a1;
+        p0 = acc_to_bf16(sx, 0);
+        p1 = acc_to_bf16(sx, 1);
+      };
+      auto pv = [&](int t, bf16x8_t p0, bf16x8_t p1) {
+        bf16x8_t fr[2 * NDB];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {  // V^T burst in two halves: 32 operand VGPRs live
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
+        for (int st = 0; st < 2; ++st)
 #pragma unroll
           for (int db = 0; db < NDB; ++db) {
-            const int ts = 2 * half + t2;
-            fr[t2 * NDB + db] = lds_tr8(Vs + tb0 + G8 * (2 * ts) + 512 * db, Vs + tb1 + G8 * (2 * ts + 1) + 512 * db);
+            const int ts = 2 * t + st;
+            fr[st * NDB + db] = lds_tr8(Vs + tb0 + G8 * (2 * ts) + 512 * db, Vs + tb1 + G8 * (2 * ts + 1) + 512 * db);
           }
 #pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
+        for (int db = 0; db < NDB; ++db) o[db] = mfma32(fr[db], p0, o[db]);
 #pragma unroll
-          for (int db = 0; db < NDB; ++db) o[db] = mfma32(fr[t2 * NDB + db], pf[2 * half + t2], o[db]);
+        for (int db = 0; db < NDB; ++db) o[db] = mfma32(fr[NDB + db], p1, o[db]);
+      };
+      // straight-line bodies (masked / unmasked) so each phase is one basic block the scheduler
+      // can interleave: half 1's S MFMAs with half 0's softmax, half 0's PV with half 1's max.
+      auto run = [&](auto diagc) {
+        f32x16 s0 = qk(0, diagc);
+        rescale(xhalf_max(max16(s0, -INFINITY)));
+        f32x16 s1 = qk(1, diagc);
+        bf16x8_t p00, p01;
+        softmax(s0, p00, p01);
+        const float mt1 = xhalf_max(max16(s1, -INFINITY));
+        pv(0, p00, p01);
+        rescale(mt1);
+        bf16x8_t p10, p11;
+        softmax(s1, p10, p11);
+        pv(1, p10, p11);
+      };
+      if (CAUSAL && kb + BK - 1 > qw0) {
+        run(std::integral_constant<bool, CAUSAL>{});
+      } else {
+        run(std::false_type{});
       }
     }
     if (more) {
@@ -372,6 +399,11 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
   for (int kk = 0; kk < NKS; ++kk) {
     qf[kk] = gload8(Qr + 16 * kk + 8 * h);
     gf[kk] = gload8(dOr + 16 * kk + 8 * h);
+  }
+#pragma unroll
+  for (int kk = 0; kk < NKS; ++kk) {
+    settle(qf[kk]);
+    settle(gf[kk]);
   }
   const float nlse = -LSE[(long)bh * S + qrow];
   const float dlt = Delta[(long)bh * S + qrow];
@@ -488,6 +520,11 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     for (int kk = 0; kk < NKS; ++kk) {
       kf[kk] = gload8(Kr + 16 * kk + 8 * h);
       vf[kk] = gload8(Vr + 16 * kk + 8 * h);
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKS; ++kk) {
+      settle(kf[kk]);
+      settle(vf[kk]);
     }
   }
   f32x16 dk[NDB], dv[NDB];
