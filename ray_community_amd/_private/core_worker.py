@@ -174,6 +174,10 @@ class DirectClient:
         with head.lock:
             res = getattr(head, "rpc_" + method)(self.key, *args, **kwargs)
         if res.__class__.__name__ == "Deferred":
+            if res.done:  # resolved inside the call (e.g. wait/get on ready objects)
+                if not res.ok:
+                    raise res.value
+                return res.value
             ev = threading.Event()
             res.add(lambda d: ev.set())
             ev.wait()
@@ -487,16 +491,19 @@ class CoreWorker:
         if isinstance(refs, ObjectRef):
             raise TypeError("wait() expected a list of ObjectRefs")
         refs = list(refs)
-        if len(set(r._id for r in refs)) != len(refs):
+        ids = [r._id for r in refs]
+        if len(set(ids)) != len(ids):
             raise ValueError("Wait requires a list of unique object refs.")
         if num_returns <= 0:
             raise ValueError("Invalid number of objects to return %d." % num_returns)
         if num_returns > len(refs):
             raise ValueError("num_returns cannot be greater than the number of objects provided.")
-        ready_ids = set(self.client.call("wait", [r._id for r in refs], num_returns, timeout, fetch_local))
-        ready = [r for r in refs if r._id in ready_ids][:num_returns]
-        rs = set(id(r) for r in ready)
-        not_ready = [r for r in refs if id(r) not in rs]
+        got = self.client.call("wait", ids, num_returns, timeout, fetch_local)
+        if len(got) > num_returns:
+            got = got[:num_returns]
+        rs = set(got)
+        ready = [r for r in refs if r._id in rs]
+        not_ready = [r for r in refs if r._id not in rs]
         return ready, not_ready
 
     # -------------------------------------------------------------- functions

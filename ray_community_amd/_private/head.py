@@ -669,24 +669,50 @@ class Head:
 
     def rpc_wait(self, caller, oids, num_returns, timeout=None, fetch_local=True):
         d = Deferred()
-        ready = [o for o in oids if (self.objects.get(o) is None or self.objects[o].state != PENDING)]
-        if len(ready) >= num_returns or timeout == 0:
-            d.resolve(ready[:num_returns] if len(ready) > num_returns else ready)
+        objs = self.objects
+        ready, pending = [], []
+        for o in oids:
+            e = objs.get(o)
+            if e is None or e.state != PENDING:
+                ready.append(o)
+                if len(ready) >= num_returns:  # result = the first num_returns ready, in order
+                    d.resolve(ready)
+                    return d
+            else:
+                pending.append(e)
+        if timeout == 0:
+            d.resolve(ready)
             return d
         rs = set(ready)
         order = list(ready)
 
-        def one(oid):
-            if d.done or oid in rs:
+        def detach():
+            # drop this wait's callbacks from objects still pending: repeated waits on a
+            # shrinking list (the common polling pattern) must not pile up dead callbacks
+            for e in pending:
+                if e.state == PENDING:
+                    try:
+                        e.waiters.remove(cb)
+                    except ValueError:
+                        pass
+
+        def cb(e):
+            if d.done or e.oid in rs:
                 return
-            rs.add(oid)
-            order.append(oid)
+            rs.add(e.oid)
+            order.append(e.oid)
             if len(order) >= num_returns:
                 d.resolve(order[:num_returns])
+                detach()
 
-        self._when_ready([o for o in oids if o not in rs], one)
+        for e in pending:
+            e.waiters.append(cb)
         if timeout is not None and not d.done:
-            self._add_timer(timeout, lambda: d.resolve(list(order)))
+            def expire():
+                if not d.done:
+                    d.resolve(list(order))
+                    detach()
+            self._add_timer(timeout, expire)
         self._maybe_block(caller, d)
         return d
 

@@ -1,0 +1,89 @@
+"""ResNet-50 (v1.5 bottleneck layout) for the "TorchTrainer ResNet-50 DDP bf16" benchmark config.
+
+Reference workload: ``release/nightly_tests/dataset/multi_node_train_benchmark.py:262-370``
+(torchvision ``resnet50(weights=None)``, SGD lr 0.1 momentum 0.9, 224x224 images, img/s) and the
+batch-inference / Serve ResNet workloads (``release/nightly_tests/dataset/gpu_batch_inference.py``,
+``release/serve_tests/workloads/serve_resnet_benchmark.py``). torchvision is not installed here, so
+the network is defined directly (same layer structure and parameter count: 25.56 M).
+
+MI355X layout: activations are NHWC (``channels_last``) end to end so MIOpen picks its NHWC
+implicit-GEMM convolutions on the matrix cores; compute in bf16 under autocast with fp32
+parameters (the optimizer keeps fp32 state); the stem's uint8 -> normalised bf16 NHWC
+conversion is the HIP ``image_normalize`` kernel when inputs arrive as raw pixels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, in_ch: int, width: int, stride: int = 1):
+        super().__init__()
+        out_ch = width * self.expansion
+        self.conv1 = nn.Conv2d(in_ch, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)  # v1.5: stride on the 3x3
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, out_ch, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(out_ch)
+        self.down = None
+        if stride != 1 or in_ch != out_ch:
+            self.down = nn.Sequential(nn.Conv2d(in_ch, out_ch, 1, stride=stride, bias=False), nn.BatchNorm2d(out_ch))
+
+    def forward(self, x):
+        idt = x if self.down is None else self.down(x)
+        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        y = F.relu(self.bn2(self.conv2(y)), inplace=True)
+        y = self.bn3(self.conv3(y))
+        return F.relu(y + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual: bool = False):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        blocks = []
+        in_ch = 64
+        for i, n in enumerate(layers):
+            width = 64 * 2 ** i
+            for j in range(n):
+                blocks.append(Bottleneck(in_ch, width, stride=2 if (j == 0 and i > 0) else 1))
+                in_ch = width * Bottleneck.expansion
+        self.blocks = nn.Sequential(*blocks)
+        self.fc = nn.Linear(in_ch, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        x = F.max_pool2d(x, 3, stride=2, padding=1)
+        x = self.blocks(x)
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes: int = 1000, device=None, channels_last: bool = True, **kw) -> ResNet:
+    m = ResNet((3, 4, 6, 3), num_classes=num_classes, **kw)
+    if device is not None:
+        m = m.to(device)
+    if channels_last:
+        m = m.to(memory_format=torch.channels_last)
+    return m
+
+
+def resnet_flops_per_image(image_size: int = 224) -> float:
+    """Forward multiply-add FLOPs (x2) of ResNet-50 at 224x224: 4.09 GMAC -> 8.2 GFLOP."""
+    return 2 * 4.09e9 * (image_size / 224) ** 2

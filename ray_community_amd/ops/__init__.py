@@ -388,20 +388,28 @@ def batched_concat(tensors, dim=0):
     return out
 
 
-def image_normalize(u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), dtype=torch.bfloat16):
-    """uint8 [N, H, W, C] -> normalised [N, C, H, W] (bf16 or f32) on the device of ``u8``."""
+def image_normalize(u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), dtype=torch.bfloat16,
+                    channels_last: bool = False):
+    """uint8 [N, H, W, C] -> normalised [N, C, H, W] (bf16 or f32) on the device of ``u8``.
+
+    ``channels_last=True`` returns the same logical NCHW tensor in NHWC memory (what MIOpen's
+    NHWC convolutions consume), written by a 16-byte-vectorised streaming kernel."""
     if not u8.is_cuda:
-        return ref.image_normalize_ref(u8, mean, std, dtype)
+        out = ref.image_normalize_ref(u8, mean, std, dtype)
+        return out.contiguous(memory_format=torch.channels_last) if channels_last else out
     import ctypes
 
     u8 = u8.contiguous()
     N, H, W, C = u8.shape
-    out = torch.empty(N, C, H, W, device=u8.device, dtype=dtype)
+    if channels_last:
+        out = torch.empty(N, H, W, C, device=u8.device, dtype=dtype).permute(0, 3, 1, 2)
+    else:
+        out = torch.empty(N, C, H, W, device=u8.device, dtype=dtype)
     ma = (ctypes.c_float * 4)(*[float(m) for m in mean])
     sa = (ctypes.c_float * 4)(*[float(s) for s in std])
     check(lib().rca_image_normalize(u8.data_ptr(), out.data_ptr(), N, H, W, C, ctypes.cast(ma, ctypes.c_void_p),
                                     ctypes.cast(sa, ctypes.c_void_p), 0 if dtype == torch.bfloat16 else 1,
-                                    stream_ptr(u8.device)), "image_normalize")
+                                    1 if channels_last else 0, stream_ptr(u8.device)), "image_normalize")
     return out
 
 

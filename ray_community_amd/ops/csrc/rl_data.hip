@@ -260,8 +260,54 @@ __global__ __launch_bounds__(256) void img_norm_kernel(const unsigned char* __re
   }
 }
 
+// channels_last output: out is [N, H, W, C] in memory, i.e. the input's element order, so the op is a
+// pure elementwise stream: each thread converts 16 consecutive bytes (one 16-B load) into 16 outputs
+// (two 16-B bf16 stores); the channel of element i is i % C.
+__global__ __launch_bounds__(256) void img_norm_nhwc_kernel(const unsigned char* __restrict__ in, void* __restrict__ out,
+                                                            long long n, int C, float m0, float m1, float m2, float m3,
+                                                            float s0, float s1, float s2, float s3, int out_dtype) {
+  const float mean[4] = {m0, m1, m2, m3};
+  const float inv[4] = {s0, s1, s2, s3};
+  const long long nvec = n / 16;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
+    const uint4 raw = reinterpret_cast<const uint4*>(in)[v];
+    const unsigned int w[4] = {raw.x, raw.y, raw.z, raw.w};
+    int c = (int)((v * 16) % C);
+    float f[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float b = (float)((w[j >> 2] >> ((j & 3) * 8)) & 0xffu);
+      f[j] = (b * (1.f / 255.f) - mean[c]) * inv[c];
+      c = (c + 1 == C) ? 0 : c + 1;
+    }
+    if (out_dtype == 0) {
+      uint4 o[2];
+      unsigned int* ow = reinterpret_cast<unsigned int*>(o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ow[j] = (unsigned int)f2bf(f[2 * j]) | ((unsigned int)f2bf(f[2 * j + 1]) << 16);
+      reinterpret_cast<uint4*>(out)[2 * v] = o[0];
+      reinterpret_cast<uint4*>(out)[2 * v + 1] = o[1];
+    } else {
+      float4* of = reinterpret_cast<float4*>(out) + 4 * v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) of[j] = make_float4(f[4 * j], f[4 * j + 1], f[4 * j + 2], f[4 * j + 3]);
+    }
+  }
+  // tail (n % 16 elements), one block
+  if (blockIdx.x == 0) {
+    for (long long i = nvec * 16 + threadIdx.x; i < n; i += blockDim.x) {
+      const int c = (int)(i % C);
+      const float val = ((float)in[i] * (1.f / 255.f) - mean[c]) * inv[c];
+      if (out_dtype == 0)
+        ((bf16_t*)out)[i] = f2bf(val);
+      else
+        ((float*)out)[i] = val;
+    }
+  }
+}
+
 RCA_API int rca_image_normalize(const void* in, void* out, long long N, int H, int W, int C, const float* mean,
-                                const float* stdv, int out_dtype, hipStream_t stream) {
+                                const float* stdv, int out_dtype, int channels_last, hipStream_t stream) {
   if (C < 1 || C > 4) return -1;
   float m[4] = {0, 0, 0, 0}, s[4] = {1, 1, 1, 1};
   for (int c = 0; c < C; ++c) {
@@ -269,6 +315,15 @@ RCA_API int rca_image_normalize(const void* in, void* out, long long N, int H, i
     s[c] = 1.f / stdv[c];
   }
   const long long npix = N * H * W;
+  if (channels_last) {
+    const long long n = npix * C;
+    long long gv = (n / 16 + 255) / 256;
+    if (gv > 8192) gv = 8192;
+    if (gv < 1) gv = 1;
+    hipLaunchKernelGGL(img_norm_nhwc_kernel, dim3((int)gv), dim3(256), 0, stream, (const unsigned char*)in, out, n, C, m[0], m[1],
+                       m[2], m[3], s[0], s[1], s[2], s[3], out_dtype);
+    return (int)hipGetLastError();
+  }
   long long g = (npix + 255) / 256;
   if (g > 2048) g = 2048;
   if (g < 1) g = 1;

@@ -2,6 +2,6 @@
 reference's reliance on torch DDP/FSDP (``python/ray/train/torch/train_loop_utils.py``)."""
 from .flat import FlatParameters
 from .ddp import DistributedDataParallel
-from .optim import FlatAdamW
+from .optim import FlatAdamW, FlatSGD
 
-__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW"]
+__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW", "FlatSGD"]

@@ -117,3 +117,59 @@ class FlatAdamW:
         if self.master_weights and sd.get("master") is not None:
             self.master.copy_(sd["master"])
             self.flat.data.copy_(self.master.to(self.flat.dtype))
+
+
+class FlatSGD:
+    """SGD with (Nesterov) momentum and weight decay over a ``FlatParameters`` buffer.
+
+    The whole model is one contiguous tensor, so the update is three streaming passes over the
+    flat buffers regardless of how many layers the model has (ResNet-50: 161 tensors -> 1).
+    ``grad_scale`` (1/world from DDP) is folded into the momentum update.
+    Reference semantics: ``torch.optim.SGD`` (momentum buffer initialised to the first gradient).
+    """
+
+    def __init__(self, flat: FlatParameters, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 0.0,
+                 nesterov: bool = False, lr_schedule=None):
+        self.flat = flat
+        self.lr = lr
+        self.momentum = momentum
+        self.wd = weight_decay
+        self.nesterov = nesterov
+        self.lr_schedule = lr_schedule
+        self.step_count = 0
+        self.buf = torch.zeros(flat.numel, dtype=flat.grad.dtype, device=flat.device) if momentum else None
+
+    @property
+    def param_groups(self):
+        return [{"lr": self.lr, "momentum": self.momentum, "weight_decay": self.wd}]
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0):
+        self.step_count += 1
+        lr = self.lr_schedule(self.step_count) if self.lr_schedule else self.lr
+        self.flat.finalize_fresh()
+        p, g = self.flat.data, self.flat.grad
+        if grad_scale != 1.0:
+            g.mul_(grad_scale)
+        if self.wd:
+            # decay only the matrices/conv kernels (the flat layout puts them first)
+            g[: self.flat.decay_end].add_(p[: self.flat.decay_end], alpha=self.wd)
+        d = g
+        if self.buf is not None:
+            if self.step_count == 1:
+                self.buf.copy_(g)
+            else:
+                self.buf.mul_(self.momentum).add_(g)
+            d = g.add(self.buf, alpha=self.momentum) if self.nesterov else self.buf
+        p.add_(d.to(p.dtype), alpha=-lr)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    def state_dict(self):
+        return {"step": self.step_count, "buf": self.buf, "lr": self.lr, "momentum": self.momentum, "wd": self.wd}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        if self.buf is not None and sd.get("buf") is not None:
+            self.buf.copy_(sd["buf"])

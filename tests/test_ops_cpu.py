@@ -119,3 +119,30 @@ def test_fused_wgrad_linear_matches_autograd_with_accumulation():
     (la, da), (lb, db) = run(True), run(False)
     assert la == lb
     assert torch.equal(da, db)
+
+
+def test_flat_sgd_matches_torch_sgd():
+    import copy
+
+    import torch.nn.functional as F
+
+    from ray_community_amd.models.resnet import ResNet
+    from ray_community_amd.parallel import DistributedDataParallel, FlatSGD
+
+    torch.manual_seed(0)
+    a = ResNet((1, 1, 1, 1), num_classes=5)
+    b = copy.deepcopy(a)
+    ddp = DistributedDataParallel(a)
+    fopt = FlatSGD(ddp.flat, lr=0.05, momentum=0.9)
+    topt = torch.optim.SGD(b.parameters(), lr=0.05, momentum=0.9)
+    x = torch.randn(4, 3, 32, 32)
+    y = torch.randint(0, 5, (4,))
+    for _ in range(3):
+        F.cross_entropy(ddp(x), y).backward()
+        fopt.step(ddp.grad_scale)
+        fopt.zero_grad()
+        F.cross_entropy(b(x), y).backward()
+        topt.step()
+        topt.zero_grad()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, atol=1e-5, rtol=1e-4), n

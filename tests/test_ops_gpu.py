@@ -183,6 +183,29 @@ def test_image_normalize():
     _close(out, r, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("shape", [(4, 17, 19, 3), (2, 224, 224, 3), (3, 5, 7, 4), (1, 3, 3, 1)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_image_normalize_channels_last(shape, dtype):
+    u8 = torch.randint(0, 256, shape, dtype=torch.uint8)
+    out = ops.image_normalize(u8.to(DEV), dtype=dtype, channels_last=True, mean=(0.4, 0.5, 0.6, 0.3)[: shape[3]],
+                              std=(0.2, 0.25, 0.3, 0.5)[: shape[3]])
+    assert out.shape == (shape[0], shape[3], shape[1], shape[2])
+    assert out.is_contiguous(memory_format=torch.channels_last) or shape[3] == 1
+    r = ref.image_normalize_ref(u8, (0.4, 0.5, 0.6, 0.3)[: shape[3]], (0.2, 0.25, 0.3, 0.5)[: shape[3]], torch.float32)
+    _close(out, r, atol=1e-5 if dtype == torch.float32 else 2e-2, rtol=1e-5 if dtype == torch.float32 else 1e-2)
+
+
+def test_resnet50_train_step_gpu():
+    from ray_community_amd.train.vision import build_resnet_training
+
+    net, ddp, opt, batch, step = build_resnet_training(batch_size=32, image_size=64, num_classes=10, lr=1e-3)
+    data = batch()
+    w0 = net.fc.weight.detach().clone()
+    losses = [float(step(*data)) for _ in range(4)]
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert not torch.equal(w0, net.fc.weight)
+
+
 def test_llama_tiny_train_step_gpu():
     from ray_community_amd.models import build_llama
     from ray_community_amd.parallel import DistributedDataParallel, FlatAdamW
