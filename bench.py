@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--parallel", default="auto", help="auto | ddp | zero (sharded AdamW; auto = zero for N>1)")
     ap.add_argument("--device", default="cuda", help="cuda (the benchmark) | cpu (gloo rehearsal of the launch path)")
     args = ap.parse_args()
 
@@ -44,7 +45,7 @@ def main():
     from ray_community_amd.train.torch import TorchTrainer
 
     loop_config = {"model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
-                   "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb,
+                   "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb, "parallel": args.parallel,
                    "device": args.device}
     # N=1: TorchTrainer runs the loop in a GPU worker actor of a local session.
     # N>1 under torchrun: TorchTrainer binds to the launcher's ranks (one process per GPU,
@@ -75,6 +76,8 @@ def main():
                 "parallelism": f"dp{world}",
                 "tokens_per_step": args.micro_batch * world * args.seq_len,
                 "optimizer": "AdamW fp32 master (fused HIP)",
+                "data_parallel": ("DDP: bucketed RCCL all-reduce" if m.get("parallel") == "ddp"
+                                  else "DDP with ZeRO-sharded AdamW: bucketed reduce-scatter + all-gather"),
             },
             "extra": {
                 "loss": round(m["loss"], 4),

@@ -3,5 +3,6 @@ reference's reliance on torch DDP/FSDP (``python/ray/train/torch/train_loop_util
 from .flat import FlatParameters
 from .ddp import DistributedDataParallel
 from .optim import FlatAdamW, FlatSGD
+from .fsdp import ShardedAdamW, ShardedDataParallel
 
-__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW", "FlatSGD"]
+__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW", "FlatSGD", "ShardedDataParallel", "ShardedAdamW"]

@@ -39,7 +39,11 @@ class Bucket:
 
 class FlatParameters:
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 256.0,
-                 no_decay: Callable[[str, torch.Tensor], bool] = default_no_decay, grad_dtype=None):
+                 no_decay: Callable[[str, torch.Tensor], bool] = default_no_decay, grad_dtype=None,
+                 bucket_align: int = ALIGN):
+        """``bucket_align``: every bucket starts and ends on a multiple of this many elements
+        (sharded data parallel uses world * ALIGN so each bucket splits into equal per-rank,
+        128-B aligned chunks for in-place reduce-scatter / all-gather)."""
         seen = set()
         named = []
         for name, p in module.named_parameters():
@@ -53,21 +57,43 @@ class FlatParameters:
         self.params = [p for _, p in decay + nodecay]
         if not self.params:
             raise ValueError("module has no trainable parameters")
+        if bucket_align % ALIGN:
+            raise ValueError(f"bucket_align must be a multiple of {ALIGN}")
         dev = self.params[0].device
         dtype = self.params[0].dtype
         self.dtype = dtype
         self.device = dev
-        offs = []
-        o = 0
-        for p in self.params:
-            offs.append(o)
-            o += _round_up(p.numel())
-        self.decay_end = sum(_round_up(p.numel()) for _, p in decay)
-        self.numel = o
-        self.offsets = offs
-        self.data = torch.zeros(o, dtype=dtype, device=dev)
         gdt = grad_dtype or dtype
-        self.grad = torch.zeros(o, dtype=gdt, device=dev)
+        esz = torch.empty((), dtype=gdt).element_size()
+        cap = max(1, int(bucket_cap_mb * 1024 * 1024 / esz))
+        # layout + buckets in one pass: contiguous ranges of the flat buffers; the no-decay tail
+        # always gets its own bucket(s) (tiny, all-reduced last)
+        offs: List[int] = []
+        bounds = []  # (start, end, params)
+        cur: List[nn.Parameter] = []
+        start = o = 0
+        n_decay = len(decay)
+        self.decay_end = None
+        for i, p in enumerate(self.params):
+            n = _round_up(p.numel())
+            if cur and (o + n - start > cap or i == n_decay):
+                end = _round_up(o, bucket_align)
+                bounds.append((start, end, cur))
+                cur, start, o = [], end, end
+            if i == n_decay:
+                self.decay_end = o
+            offs.append(o)
+            o += n
+            cur.append(p)
+        end = _round_up(o, bucket_align)
+        bounds.append((start, end, cur))
+        if self.decay_end is None:
+            self.decay_end = end
+        self.bucket_align = bucket_align
+        self.numel = end
+        self.offsets = offs
+        self.data = torch.zeros(end, dtype=dtype, device=dev)
+        self.grad = torch.zeros(end, dtype=gdt, device=dev)
         with torch.no_grad():
             for p, off in zip(self.params, offs):
                 n = p.numel()
@@ -76,20 +102,7 @@ class FlatParameters:
                 if gdt == dtype:
                     p.grad = self.grad[off: off + n].view_as(p)
         self.grad_is_view = gdt == dtype
-        # buckets: contiguous ranges of the flat gradient buffer
-        cap = max(1, int(bucket_cap_mb * 1024 * 1024 / self.grad.element_size()))
-        self.buckets: List[Bucket] = []
-        cur: List[nn.Parameter] = []
-        start = 0
-        for p, off in zip(self.params, offs):
-            end_p = off + _round_up(p.numel())
-            # the no-decay tail always gets its own bucket (tiny, all-reduced last)
-            if cur and (end_p - start > cap or off == self.decay_end):
-                self.buckets.append(Bucket(len(self.buckets), start, off, cur))
-                cur, start = [], off
-            cur.append(p)
-        if cur:
-            self.buckets.append(Bucket(len(self.buckets), start, o, cur))
+        self.buckets: List[Bucket] = [Bucket(i, s, e, ps) for i, (s, e, ps) in enumerate(bounds)]
         self.param_bucket = {}
         for b in self.buckets:
             for p in b.params:
@@ -102,7 +115,7 @@ class FlatParameters:
         fused_ids = {id(p) for p in self.fused}
         first_other = next((i for i, p in enumerate(self.params) if id(p) not in fused_ids), len(self.params))
         if self.fused and all(id(p) not in fused_ids for p in self.params[first_other:]):
-            self.zero_start = offs[first_other] if first_other < len(self.params) else o
+            self.zero_start = offs[first_other] if first_other < len(self.params) else end
             for p in self.fused:
                 p._rca_flat_grad = True
                 p._rca_grad_fresh = True

@@ -21,3 +21,4 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
     assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["higher_is_better"] is True
+    assert "ZeRO" in rec["config"]["data_parallel"]  # N>1 defaults to the sharded optimizer
