@@ -8,14 +8,32 @@ the network is defined directly (same layer structure and parameter count: 25.56
 
 MI355X layout: activations are NHWC (``channels_last``) end to end so MIOpen picks its NHWC
 implicit-GEMM convolutions on the matrix cores; compute in bf16 under autocast with fp32
-parameters (the optimizer keeps fp32 state); the stem's uint8 -> normalised bf16 NHWC
-conversion is the HIP ``image_normalize`` kernel when inputs arrive as raw pixels.
+parameters (the optimizer keeps fp32 state). Every BatchNorm with its ReLU (and the bottleneck's
+residual add) is ONE fused gfx950 kernel chain (``ops.batch_norm_act``: 3 launches forward,
+3 backward, NHWC 16-byte streams) instead of MIOpen BN + separate elementwise kernels; the
+stem's uint8 -> normalised bf16 NHWC conversion is the HIP ``image_normalize`` kernel.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from .. import ops
+
+
+def bn_act(bn: nn.BatchNorm2d, x, residual=None, relu=True):
+    """``act(bn(x) [+ residual])`` through the fused NHWC kernels (training mode) with the
+    module's own parameters and running statistics."""
+    mom = bn.momentum
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+        if mom is None:  # cumulative moving average, as nn.BatchNorm2d
+            mom = 1.0 / float(bn.num_batches_tracked)
+    return ops.batch_norm_act(x, bn.weight, bn.bias, bn.running_mean if bn.track_running_stats else None,
+                              bn.running_var if bn.track_running_stats else None,
+                              training=bn.training or not bn.track_running_stats, momentum=mom or 0.0,
+                              eps=bn.eps, residual=residual, relu=relu)
 
 
 class Bottleneck(nn.Module):
@@ -35,11 +53,10 @@ class Bottleneck(nn.Module):
             self.down = nn.Sequential(nn.Conv2d(in_ch, out_ch, 1, stride=stride, bias=False), nn.BatchNorm2d(out_ch))
 
     def forward(self, x):
-        idt = x if self.down is None else self.down(x)
-        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        y = F.relu(self.bn2(self.conv2(y)), inplace=True)
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt, inplace=True)
+        idt = x if self.down is None else bn_act(self.down[1], self.down[0](x), relu=False)
+        y = bn_act(self.bn1, self.conv1(x))
+        y = bn_act(self.bn2, self.conv2(y))
+        return bn_act(self.bn3, self.conv3(y), residual=idt)  # relu(bn3(conv3(y)) + identity), one kernel
 
 
 class ResNet(nn.Module):
@@ -68,7 +85,7 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x):
-        x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        x = bn_act(self.bn1, self.conv1(x))
         x = F.max_pool2d(x, 3, stride=2, padding=1)
         x = self.blocks(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -29,6 +29,7 @@ __all__ = [
     "standardize_",
     "batched_concat",
     "image_normalize",
+    "batch_norm_act",
     "flash_attention",
     "flash_attention_qkv",
     "flash_attention_supported",
@@ -411,6 +412,81 @@ def image_normalize(u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), d
                                     ctypes.cast(sa, ctypes.c_void_p), 0 if dtype == torch.bfloat16 else 1,
                                     1 if channels_last else 0, stream_ptr(u8.device)), "image_normalize")
     return out
+
+
+# --------------------------------------------------------------------------------- batch norm
+def bn_supported(x) -> bool:
+    """Shapes/layouts the fused NHWC BatchNorm kernels cover."""
+    if x.dim() != 4 or x.dtype != torch.bfloat16 or not x.is_cuda:
+        return False
+    C = x.shape[1]
+    return (C % 8 == 0 and 8 <= C <= 2048 and 256 % (C // 8) == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _rows(t):
+    N, C, H, W = t.shape
+    return N * H * W, C
+
+
+class _BatchNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu):
+        R, C = _rows(x)
+        L = lib()
+        dev = x.device
+        out = torch.empty_like(x, memory_format=torch.channels_last)
+        stats = torch.empty(4, C, device=dev, dtype=torch.float32)
+        ws = _workspace(dev, "bn", int(L.rca_bn_workspace(R, C)))
+        res = residual.contiguous(memory_format=torch.channels_last) if residual is not None else None
+        check(L.rca_bn_fwd(x.data_ptr(), res.data_ptr() if res is not None else 0, _p(weight), _p(bias),
+                           _p(running_mean), _p(running_var), stats.data_ptr(), ws.data_ptr(), out.data_ptr(), R, C,
+                           float(eps), float(momentum), 1 if relu else 0, stream_ptr(dev)), "bn_fwd")
+        ctx.save_for_backward(x, out, stats, weight)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.has_w = weight is not None
+        ctx.has_b = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, out, stats, weight = ctx.saved_tensors
+        R, C = _rows(x)
+        L = lib()
+        dev = x.device
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        dw = torch.empty(C, device=dev, dtype=torch.float32) if ctx.has_w else None
+        db = torch.empty(C, device=dev, dtype=torch.float32) if ctx.has_b else None
+        coef = torch.empty(3, C, device=dev, dtype=torch.float32)
+        ws = _workspace(dev, "bn", int(L.rca_bn_workspace(R, C)))
+        check(L.rca_bn_bwd(dy.data_ptr(), out.data_ptr(), x.data_ptr(), stats.data_ptr(), _p(weight), _p(dw), _p(db),
+                           coef.data_ptr(), ws.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else 0,
+                           R, C, 1 if ctx.relu else 0, stream_ptr(dev)), "bn_bwd")
+        return dx, dw, db, dres, None, None, None, None, None
+
+
+def batch_norm_act(x, weight, bias, running_mean=None, running_var=None, training: bool = True,
+                   momentum: float = 0.1, eps: float = 1e-5, residual=None, relu: bool = True):
+    """``act(batch_norm(x) [+ residual])`` for NCHW-logical tensors.
+
+    channels_last bf16 CUDA tensors in training mode run the fused gfx950 kernels
+    (``ops/csrc/batchnorm.hip``); everything else (CPU, eval mode, other layouts) uses the
+    PyTorch composition with identical semantics (batch statistics, biased variance for
+    normalisation, unbiased variance in the running estimate)."""
+    use_kernel = training and bn_supported(x) and (residual is None or residual.shape == x.shape)
+    if use_kernel and weight is not None and weight.dtype != torch.float32:
+        use_kernel = False
+    if not use_kernel:
+        y = torch.nn.functional.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+        if residual is not None:
+            y = y + residual
+        return torch.relu(y) if relu else y
+    if residual is not None and residual.dtype != x.dtype:
+        residual = residual.to(x.dtype)
+    return _BatchNormAct.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu)
 
 
 # --------------------------------------------------------------------------------- attention

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export RCA_NO_REBUILD=1
-timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ops.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -k "batch_norm or resnet or image" -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ops.log 2>&1
 rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/pytest_ops.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python bench_resnet.py --steps 20 --warmup 5 > gpurun_out/bench_resnet.log 2>&1 && tail -1 gpurun_out/bench_resnet.log || { tail -20 gpurun_out/bench_resnet.log; exit 1; }
 timeout -k 10 400 python bench_rllib.py > gpurun_out/bench_rllib.log 2>&1 && tail -1 gpurun_out/bench_rllib.log || { tail -20 gpurun_out/bench_rllib.log; exit 1; }
