@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""BASELINE.json config 5: Ray Data ``map_batches`` GPU preprocess -> Serve bf16 replica.
+
+    python bench_data_serve.py --gpus N --batches K --warmup W [--batch-size B]
+
+End-to-end offline-inference pipeline through the framework's own libraries:
+
+  ray.data.range(...)                         synthetic uint8 224x224x3 images (CPU read tasks)
+    .map_batches(PreprocessAndClassify,       GPU actor pool: ONE HIP kernel turns the uint8 NHWC
+                 num_gpus=0.25, concurrency)  batch into normalised bf16 (NCHW-logical, NHWC memory)
+                                              and hands the HBM tensor to ...
+  serve deployment Classifier (bf16)          ... a Serve replica (HIP IPC: zero-copy on the same
+                                              GPU, peer mapping over xGMI otherwise) running
+                                              ResNet-50 inference with BatchNorm folded into the
+                                              convolutions; only the int64 predictions go back.
+
+Throughput = images classified per second in steady state (blocks W+1..W+K of the output stream;
+actor start-up, MIOpen kernel selection and replica warm-up are outside the timed window).
+Random-init weights, synthetic images. One replica + two preprocess actors per GPU; N GPUs of one
+node run N replicas behind Serve's power-of-two-choices router. Prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+_POOL = {}
+
+
+def synth_images(batch, image_size: int):
+    """Read stage: uint8 NHWC images for the ids in this block (from a per-process random pool,
+    so the CPU cost is the block copy into the object store, as for decoded images)."""
+    import numpy as np
+
+    ids = batch["id"]
+    pool = _POOL.get(image_size)
+    if pool is None:
+        rng = np.random.default_rng(0)
+        pool = _POOL[image_size] = rng.integers(0, 256, (512, image_size, image_size, 3), dtype=np.uint8)
+    start = int(ids[0]) % len(pool)
+    n = len(ids)
+    if start + n <= len(pool):
+        imgs = pool[start: start + n]
+    else:
+        imgs = np.concatenate([pool[start:], pool[: n - (len(pool) - start)]])
+    return {"image": imgs, "id": ids}
+
+
+class Classifier:
+    """Serve replica: bf16 ResNet-50 inference on a device-resident NHWC batch."""
+
+    def __init__(self, model: str, image_size: int, batch_size: int, device: str):
+        import torch
+
+        from ray_community_amd.models.resnet import ResNet, fold_batchnorm, resnet50
+
+        self.dev = torch.device(device)
+        torch.manual_seed(0)
+        net = resnet50() if model == "resnet50" else ResNet((1, 1, 1, 1), num_classes=10)
+        net = fold_batchnorm(net.to(self.dev)).to(memory_format=torch.channels_last)
+        self.dtype = torch.bfloat16 if self.dev.type == "cuda" else torch.float32
+        self.net = net.to(self.dtype)
+        if self.dev.type == "cuda":
+            torch.backends.cudnn.benchmark = True
+            x = torch.randn(batch_size, 3, image_size, image_size, device=self.dev, dtype=self.dtype)
+            x = x.contiguous(memory_format=torch.channels_last)
+            for _ in range(3):  # MIOpen kernel selection for the serving shape
+                self(x)
+            torch.cuda.synchronize()
+
+    def __call__(self, x):
+        import torch
+
+        with torch.inference_mode():
+            x = x.to(self.dev, self.dtype, non_blocking=True)
+            return self.net(x).argmax(1).cpu().numpy()
+
+
+class PreprocessAndClassify:
+    """``map_batches`` actor: GPU normalise (HIP ``image_normalize``) -> Serve handle call."""
+
+    def __init__(self, app_name: str, device: str):
+        from ray_community_amd import serve
+        from ray_community_amd.data.gpu import ImageNormalize
+
+        self.cuda = device == "cuda"
+        self.norm = ImageNormalize(column="image", keep_on_device=True, channels_last=True,
+                                   dtype="bfloat16" if self.cuda else "float32")
+        self.handle = serve.get_app_handle(app_name)
+
+    def __call__(self, batch):
+        import torch
+
+        x = self.norm(batch)["image"]
+        if self.cuda:
+            torch.cuda.current_stream().synchronize()  # the replica reads it from another process
+        pred = self.handle.remote(x).result()
+        return {"pred": pred, "id": batch["id"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--batches", type=int, default=40, help="timed output blocks")
+    ap.add_argument("--warmup", type=int, default=6, help="untimed leading output blocks")
+    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--device", default="cuda", help="cuda (the benchmark) | cpu (plumbing rehearsal)")
+    ap.add_argument("--preprocess-actors-per-gpu", type=int, default=2)
+    a = ap.parse_args()
+
+    import ray_community_amd as ray
+    from ray_community_amd import serve
+
+    cuda = a.device == "cuda"
+    G = max(1, a.gpus)
+    ray.init(num_cpus=max(8, 4 * G + 4), num_gpus=G if cuda else 0)
+    try:
+        dep = serve.deployment(Classifier, name="Classifier", num_replicas=G, max_ongoing_requests=4,
+                               ray_actor_options={"num_gpus": 0.5 if cuda else 0, "num_cpus": 1})
+        serve.run(dep.bind(a.model, a.image_size, a.batch_size, a.device), name="classifier", route_prefix=None)
+
+        nblocks = a.warmup + a.batches
+        n = nblocks * a.batch_size
+        nact = a.preprocess_actors_per_gpu * G
+        ds = (ray.data.range(n, override_num_blocks=nblocks)
+              .map_batches(synth_images, batch_size=a.batch_size, fn_kwargs={"image_size": a.image_size})
+              .map_batches(PreprocessAndClassify, batch_size=a.batch_size, concurrency=nact,
+                           fn_constructor_kwargs={"app_name": "classifier", "device": a.device},
+                           num_gpus=0.5 / a.preprocess_actors_per_gpu if cuda else None, num_cpus=1))
+        stamps, seen, correct = [], 0, 0
+        for b in ds.iter_batches(batch_size=None, batch_format="numpy"):
+            stamps.append((time.perf_counter(), len(b["pred"])))
+            seen += len(b["pred"])
+            correct += int(((b["pred"] >= 0) & (b["pred"] < 1000)).all())
+        if len(stamps) <= a.warmup:
+            raise RuntimeError(f"pipeline produced {len(stamps)} blocks, need > {a.warmup}")
+        t0 = stamps[a.warmup - 1][0] if a.warmup > 0 else stamps[0][0]
+        timed = stamps[a.warmup:] if a.warmup > 0 else stamps[1:]
+        imgs = sum(k for _, k in timed)
+        dt = stamps[-1][0] - t0
+        assert seen == n, (seen, n)
+        print(json.dumps({
+            "metric": "data_to_serve_images_per_sec_resnet50_bf16", "value": round(imgs / dt, 1), "unit": "images/s",
+            "n_gpus": G, "steps": len(timed), "warmup": a.warmup, "ms_per_step": round(1e3 * dt / len(timed), 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if cuda else "fp32", "data": "synthetic uint8 images, random-init weights",
+            "config": {"model": a.model, "batch_size": a.batch_size, "image_size": a.image_size, "replicas": G,
+                       "preprocess_actors": nact,
+                       "pipeline": "ray.data map_batches(HIP image_normalize) -> serve handle (HIP IPC) -> "
+                                   "ResNet-50 bf16 (BN folded)"},
+            "extra": {"blocks": len(stamps), "images": seen}}), flush=True)
+    finally:
+        serve.shutdown()
+        ray.shutdown()
+
+
+if __name__ == "__main__":
+    main()

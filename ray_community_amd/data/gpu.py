@@ -12,7 +12,7 @@ import numpy as np
 
 class ImageNormalize:
     def __init__(self, column: str = "image", mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
-                 dtype: str = "bfloat16", keep_on_device: bool = False):
+                 dtype: str = "bfloat16", keep_on_device: bool = False, channels_last: bool = False):
         import torch
 
         self.column = column
@@ -20,6 +20,7 @@ class ImageNormalize:
         self.std = std
         self.dtype = getattr(torch, dtype)
         self.keep = keep_on_device
+        self.channels_last = channels_last  # NCHW-logical tensor in NHWC memory (MIOpen NHWC convs)
         self.device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
 
     def __call__(self, batch):
@@ -28,7 +29,7 @@ class ImageNormalize:
         from ..ops import image_normalize
 
         x = torch.from_numpy(np.ascontiguousarray(batch[self.column])).to(self.device, non_blocking=True)
-        y = image_normalize(x, self.mean, self.std, self.dtype)
+        y = image_normalize(x, self.mean, self.std, self.dtype, channels_last=self.channels_last)
         out = dict(batch)
         if self.keep:
             out[self.column] = y

@@ -24,7 +24,11 @@ from .. import ops
 
 def bn_act(bn: nn.BatchNorm2d, x, residual=None, relu=True):
     """``act(bn(x) [+ residual])`` through the fused NHWC kernels (training mode) with the
-    module's own parameters and running statistics."""
+    module's own parameters and running statistics. After ``fold_batchnorm`` the BN is an
+    ``nn.Identity`` (its affine map lives in the conv's weights/bias) and only the act remains."""
+    if isinstance(bn, nn.Identity):
+        y = x if residual is None else x + residual
+        return F.relu(y, inplace=True) if relu else y
     mom = bn.momentum
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
@@ -99,6 +103,35 @@ def resnet50(num_classes: int = 1000, device=None, channels_last: bool = True, *
     if channels_last:
         m = m.to(memory_format=torch.channels_last)
     return m
+
+
+@torch.no_grad()
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+    scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+    fused = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, stride=conv.stride,
+                      padding=conv.padding, dilation=conv.dilation, groups=conv.groups, bias=True)
+    fused = fused.to(device=conv.weight.device, dtype=conv.weight.dtype)
+    fused.weight.copy_((conv.weight.float() * scale.view(-1, 1, 1, 1)).to(conv.weight.dtype))
+    b0 = conv.bias.float() if conv.bias is not None else torch.zeros_like(bn.running_mean)
+    fused.bias.copy_(((b0 - bn.running_mean) * scale + bn.bias).to(conv.weight.dtype))
+    return fused.to(memory_format=torch.channels_last) if conv.weight.is_contiguous(
+        memory_format=torch.channels_last) else fused
+
+
+def fold_batchnorm(model: ResNet) -> ResNet:
+    """Inference graph: every eval-mode BatchNorm folded into the preceding convolution
+    (``w' = w * gamma / sqrt(var + eps)``, ``b' = (b - mean) * gamma / sqrt(var + eps) + beta``), so
+    a serving replica runs conv(+bias) -> ReLU / residual add only. Returns the model, modified in
+    place and switched to eval mode."""
+    model.eval()
+    model.conv1, model.bn1 = _fold(model.conv1, model.bn1), nn.Identity()
+    for blk in model.blocks:
+        for i in (1, 2, 3):
+            setattr(blk, f"conv{i}", _fold(getattr(blk, f"conv{i}"), getattr(blk, f"bn{i}")))
+            setattr(blk, f"bn{i}", nn.Identity())
+        if blk.down is not None:
+            blk.down = nn.Sequential(_fold(blk.down[0], blk.down[1]), nn.Identity())
+    return model
 
 
 def resnet_flops_per_image(image_size: int = 224) -> float:

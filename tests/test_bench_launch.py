@@ -22,3 +22,17 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
     assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["higher_is_better"] is True
     assert "ZeRO" in rec["config"]["data_parallel"]  # N>1 defaults to the sharded optimizer
+
+
+def test_bench_data_serve_pipeline_cpu(tmp_path):
+    """Config 5 plumbing: Data read -> map_batches actor pool -> Serve handle -> replica, on CPU."""
+    env = dict(os.environ)
+    env.pop("RCA_ADDRESS", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench_data_serve.py"), "--device", "cpu", "--model", "tiny",
+           "--image-size", "32", "--batch-size", "16", "--batches", "4", "--warmup", "2"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["steps"] == 4 and rec["extra"]["images"] == 6 * 16
