@@ -31,6 +31,12 @@ def _sac():
     return SAC, SACConfig()
 
 
+def _cql():
+    from .cql import CQL, CQLConfig
+
+    return CQL, CQLConfig()
+
+
 def _marwil():
     from .marwil import MARWIL, MARWILConfig
 
@@ -43,7 +49,7 @@ def _bc():
     return BC, BCConfig()
 
 
-ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo, "SAC": _sac, "MARWIL": _marwil,
+ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo, "SAC": _sac, "CQL": _cql, "MARWIL": _marwil,
               "BC": _bc}
 
 

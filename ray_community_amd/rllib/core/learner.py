@@ -356,6 +356,96 @@ class Learner:
         return {"critic_loss": q_loss.item(), "actor_loss": pi_loss.item(), "alpha_loss": a_loss.item(),
                 "alpha_value": alpha.item(), "mean_q": q1.detach().mean().item()}
 
+    # ------------------------------------------------------------------ CQL
+    def update_cql(self, batch: SampleBatch) -> Dict:
+        """Conservative Q-learning step (reference: rllib/algorithms/cql/cql_torch_policy.py): the
+        SAC losses plus, per critic, ``min_q_weight * (T * logsumexp(Q(s, a~{uniform, pi(s),
+        pi(s')}) / T - log-density) - Q(s, a_data))``; optional Lagrangian weight tuned to
+        ``lagrangian_thresh``; the actor clones the logged actions for the first ``bc_iters``
+        updates."""
+        cfg = self.cfg
+        m = self.module
+        if not hasattr(self, "_cql_opts"):
+            lr = cfg.get("lr", 3e-4)
+            olr = cfg.get("optimization_config") or {}
+            self._log_alpha_prime = torch.zeros((), device=self.device, requires_grad=True)
+            self._cql_opts = (
+                torch.optim.Adam(m.pi.parameters(), lr=olr.get("actor_learning_rate", lr)),
+                torch.optim.Adam(list(m.q1.parameters()) + list(m.q2.parameters()),
+                                 lr=olr.get("critic_learning_rate", lr)),
+                torch.optim.Adam([m.log_alpha], lr=olr.get("entropy_learning_rate", lr)),
+                torch.optim.Adam([self._log_alpha_prime], lr=olr.get("critic_learning_rate", lr)))
+            te = cfg.get("target_entropy", "auto")
+            self._target_entropy = -float(m.act_dim) if te in (None, "auto") else float(te)
+        opt_pi, opt_q, opt_a, opt_ap = self._cql_opts
+        b = batch.to_device(self.device)
+        obs, nobs = b["obs"].float(), b["new_obs"].float()
+        B = obs.shape[0]
+        u = m._unscale(b["actions"].float().reshape(B, -1)).clamp(-1.0, 1.0)
+        r, term = b["rewards"].float(), b["terminateds"].float()
+        gamma = cfg.get("gamma", 0.99) ** cfg.get("n_step", 1)
+        alpha = m.log_alpha.exp().detach()
+        K = int(cfg.get("num_actions", 10))
+        T = float(cfg.get("temperature", 1.0))
+        wq = float(cfg.get("min_q_weight", 5.0))
+        with torch.no_grad():
+            un, lpn = m.policy(nobs)
+            q1t, q2t = m.q(nobs, un, target=True)
+            y = r + gamma * (1 - term) * (torch.min(q1t, q2t) - alpha * lpn)
+            # the CQL action samples: uniform on [-1, 1]^A (log-density -A log 2), pi(.|s), pi(.|s')
+            obs_k = obs.repeat_interleave(K, 0)
+            nobs_k = nobs.repeat_interleave(K, 0)
+            u_rand = torch.rand(B * K, m.act_dim, device=obs.device) * 2 - 1
+            u_cur, lp_cur = m.policy(obs_k)
+            u_nxt, lp_nxt = m.policy(nobs_k)
+            lp_rand = -m.act_dim * math.log(2.0)
+        q1, q2 = m.q(obs, u)
+        bellman = 0.5 * (((q1 - y) ** 2).mean() + ((q2 - y) ** 2).mean())
+        xs = torch.cat([obs_k, obs_k, obs_k], 0)
+        us = torch.cat([u_rand, u_cur, u_nxt], 0)
+        dens = torch.cat([torch.full((B * K,), lp_rand, device=obs.device), lp_cur, lp_nxt], 0)
+        qs1, qs2 = m.q(xs, us)
+        pen = []
+        for qs, qd in ((qs1, q1), (qs2, q2)):
+            cat = (qs - dens).view(3, B, K).permute(1, 0, 2).reshape(B, 3 * K)
+            pen.append(wq * (T * torch.logsumexp(cat / T, dim=1).mean() - qd.mean()))
+        info = {}
+        if cfg.get("lagrangian", False):
+            ap = self._log_alpha_prime.exp().clamp(0.0, 1e6)
+            thresh = float(cfg.get("lagrangian_thresh", 5.0))
+            ap_loss = -0.5 * ap * ((pen[0].detach() - thresh) + (pen[1].detach() - thresh))
+            pen = [ap.detach() * (p - thresh) for p in pen]
+            opt_ap.zero_grad(set_to_none=True)
+            ap_loss.backward()
+            opt_ap.step()
+            info["alpha_prime_value"] = ap.item()
+        q_loss = bellman + pen[0] + pen[1]
+        opt_q.zero_grad(set_to_none=True)
+        q_loss.backward()
+        gc = cfg.get("grad_clip")
+        if gc:
+            torch.nn.utils.clip_grad_norm_(list(m.q1.parameters()) + list(m.q2.parameters()), gc)
+        opt_q.step()
+        un, lp = m.policy(obs)
+        if self.num_updates < int(cfg.get("bc_iters", 20000)):
+            pi_loss = (alpha * lp - m.logp_of(obs, u)).mean()
+        else:
+            q1n, q2n = m.q(obs, un)
+            pi_loss = (alpha * lp - torch.min(q1n, q2n)).mean()
+        opt_pi.zero_grad(set_to_none=True)
+        pi_loss.backward()
+        opt_pi.step()
+        a_loss = -(m.log_alpha * (lp.detach() + self._target_entropy)).mean()
+        opt_a.zero_grad(set_to_none=True)
+        a_loss.backward()
+        opt_a.step()
+        m.polyak(cfg.get("tau", 5e-3))
+        self.num_updates += 1
+        info.update({"critic_loss": q_loss.item(), "bellman_loss": bellman.item(), "cql_loss": (pen[0] + pen[1]).item(),
+                     "actor_loss": pi_loss.item(), "alpha_loss": a_loss.item(), "alpha_value": alpha.item(),
+                     "mean_q": q1.detach().mean().item()})
+        return info
+
     def sync_target(self):
         if self.target is not None:
             self.target.load_state_dict(self.module.state_dict())

@@ -61,11 +61,29 @@ class SACModule(nn.Module):
         logp = logp - (2 * (math.log(2.0) - z - nn.functional.softplus(-2 * z))).sum(-1)
         return u, logp
 
+    def logp_of(self, obs, u):
+        """Log-prob of given squashed actions ``u`` in (-1, 1) under the current policy (the
+        tanh-Gaussian density through atanh; used by CQL's behaviour-cloning warm-up)."""
+        x = obs.float().reshape(obs.shape[0], -1)
+        mean, log_std = self.pi(x).chunk(2, -1)
+        log_std = log_std.clamp(LOG_STD_MIN, LOG_STD_MAX)
+        u = u.clamp(-1 + 1e-6, 1 - 1e-6)
+        z = torch.atanh(u)
+        logp = (-0.5 * ((z - mean) / log_std.exp()) ** 2 - log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+        return logp - (2 * (math.log(2.0) - z - nn.functional.softplus(-2 * z))).sum(-1)
+
     def q(self, obs, u, target=False):
         x = torch.cat([obs.float().reshape(obs.shape[0], -1), u], -1)
         if target:
             return self.q1_t(x).squeeze(-1), self.q2_t(x).squeeze(-1)
         return self.q1(x).squeeze(-1), self.q2(x).squeeze(-1)
+
+    @torch.no_grad()
+    def forward(self, obs):
+        """(deterministic action, V(s) ~ min_i Q_i(s, mu(s))) — the value head on-policy samplers
+        bootstrap from."""
+        u, _ = self.policy(obs, deterministic=True)
+        return self._scale(u), torch.min(*self.q(obs, u))
 
     @torch.no_grad()
     def forward_inference(self, obs):

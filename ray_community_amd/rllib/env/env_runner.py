@@ -71,7 +71,8 @@ class EnvRunner:
         T = max(1, int(num_steps or self.cfg.get("rollout_fragment_length", 64) * self.N) // self.N)
         N = self.N
         obs_buf = np.empty((N, T) + self.obs.shape[1:], dtype=self.obs.dtype)
-        act_shape = () if self.module.dist_cls.__name__ == "Categorical" else self.env.action_space.shape
+        dist = getattr(self.module, "dist_cls", None)  # None: SAC-style module with its own squashed policy
+        act_shape = () if dist is not None and dist.__name__ == "Categorical" else self.env.action_space.shape
         acts = np.empty((N, T) + tuple(act_shape), dtype=np.int64 if act_shape == () else np.float32)
         logp = np.empty((N, T), dtype=np.float32)
         vf = np.empty((N, T), dtype=np.float32)
