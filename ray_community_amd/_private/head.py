@@ -221,6 +221,10 @@ class Head:
         self.driver_free_gpu_cb = None
         self.driver_task_cancel_cb = None
         self.shutting_down = False
+        from .memory_monitor import MemoryMonitor
+
+        self.memory_monitor = MemoryMonitor(self.config)
+        self._oom_log: collections.deque = collections.deque(maxlen=1000)
         # head node
         self.head_node_id = new_id().hex()
         self._add_node(self.head_node_id, resources, labels, is_head=True)
@@ -299,6 +303,7 @@ class Head:
             if self.timers:
                 self._fire_timers()
             self._reap_idle()
+            self.memory_monitor.poll(self)
 
     def wake(self):
         try:
@@ -1251,6 +1256,9 @@ class Head:
                 e.flags = FLAG_ERROR
         ts = w.task
         w.task = None
+        if getattr(w, "oom_killed", None):
+            reason = f"killed by the memory monitor (node memory usage {w.oom_killed[0]:.2f} >= " \
+                     f"threshold {w.oom_killed[1]:.2f})"
         if w.actor is not None:
             a = w.actor
             self._on_actor_worker_death(a, reason, ts)
@@ -1263,6 +1271,12 @@ class Head:
                 self._event(ts, "retry")
                 ts.state = T_WAIT_DEPS
                 self._enqueue(ts)
+            elif getattr(w, "oom_killed", None):
+                u, thr = w.oom_killed
+                self._fail_task(ts, exc.OutOfMemoryError(
+                    f"Task {ts.spec.get('name')} was killed by the memory monitor: node memory usage {u:.2f} "
+                    f"exceeded the threshold {thr:.2f} (memory_usage_threshold) and its retries are exhausted. "
+                    "Reduce the task's memory, lower its parallelism, or raise max_retries."))
             else:
                 self._fail_task(ts, exc.WorkerCrashedError(
                     f"The worker died unexpectedly while executing task {ts.spec.get('name')} ({reason})."))
