@@ -22,6 +22,7 @@ from typing import Any, Dict, List, Optional
 from .. import exceptions as exc
 from . import protocol as P
 from . import serialization as ser
+from ..util import tracing
 from .ids import new_id
 from .object_store import ObjectStore
 
@@ -550,6 +551,9 @@ class CoreWorker:
     def submit_spec(self, spec, deps=()):
         spec["parent"] = self.ctx.task_id
         spec["caller_node"] = self.node_id
+        trace = tracing.submission_context()
+        if trace is not None:
+            spec["trace"] = trace
         self.client.submit(spec)
 
     def shutdown(self):

@@ -225,6 +225,7 @@ class Head:
 
         self.memory_monitor = MemoryMonitor(self.config)
         self._oom_log: collections.deque = collections.deque(maxlen=1000)
+        self.spans: collections.deque = collections.deque(maxlen=int(self.config.get("max_spans", 200000)))
         # head node
         self.head_node_id = new_id().hex()
         self._add_node(self.head_node_id, resources, labels, is_head=True)
@@ -1113,6 +1114,9 @@ class Head:
         self._send(w, (P.EXECUTE, msg))
 
     def _on_task_done(self, w: WorkerState, tid, results, info):
+        sp = info.get("spans")
+        if sp:
+            self.spans.extend(sp)
         ts = self.tasks.get(tid)
         if w is not None and w.task is ts:
             w.task = None
@@ -1765,7 +1769,19 @@ class Head:
                 st, nm, p, nd = open_.pop(tid)
                 evs.append({"name": nm or "task", "cat": "task", "ph": "X", "ts": st * 1e6, "dur": (t - st) * 1e6,
                             "pid": nd or "node", "tid": p or 0, "args": {"task_id": tid.hex(), "state": what}})
+        for sp in self.spans:  # tracing spans and profile() events
+            evs.append({"name": sp["name"], "cat": sp.get("kind", "span"), "ph": "X", "ts": sp["start"] * 1e6,
+                        "dur": ((sp["end"] or sp["start"]) - sp["start"]) * 1e6, "pid": "spans", "tid": sp["pid"],
+                        "args": {"trace_id": sp["trace_id"], "span_id": sp["span_id"], "parent_id": sp["parent_id"],
+                                 **{k: str(v) for k, v in (sp.get("attributes") or {}).items()}}})
         return evs
+
+    def rpc_add_spans(self, caller, spans):
+        self.spans.extend(spans)
+        return True
+
+    def rpc_spans(self, caller):
+        return list(self.spans)
 
     def rpc_ping(self, caller):
         return "pong"

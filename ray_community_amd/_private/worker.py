@@ -132,6 +132,10 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
         from ..runtime_env import validate as _validate_env
 
         _state["runtime_env"] = _validate_env(runtime_env)
+        if kwargs.get("_tracing_startup_hook"):
+            from ..util import tracing
+
+            tracing.setup_tracing(kwargs["_tracing_startup_hook"])
         cw.set_global_core(core)
         return RayContext(_state)
 
@@ -186,6 +190,10 @@ def shutdown(_exiting_interpreter: bool = False):
             return
         if _state["mode"] == WORKER_MODE:
             return
+        from ..util import tracing
+
+        tracing.enable_tracing(False)
+        tracing.drain()
         dash = _state.pop("dashboard", None)
         if dash is not None:
             try:
@@ -286,6 +294,9 @@ def get_gpu_ids():
 
 
 def timeline(filename=None):
+    from ..util import tracing
+
+    tracing._flush_to_head()
     evs = _core().client.call("timeline")
     if filename:
         with open(filename, "w") as f:

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import asyncio
 import concurrent.futures
+import contextlib
 import ctypes
 import inspect
 import json
@@ -16,6 +17,7 @@ import os
 import queue
 import sys
 import threading
+import time
 import traceback
 
 
@@ -66,6 +68,7 @@ from . import serialization as ser  # noqa: E402
 from .core_worker import (CoreWorker, DynamicObjectRefGenerator, ObjectRef, SocketClient, _ErrorValue,  # noqa: E402
                           set_global_core)
 from .ids import new_id  # noqa: E402
+from ..util import tracing  # noqa: E402
 from .object_store import ObjectStore  # noqa: E402
 
 
@@ -189,6 +192,20 @@ class Worker:
         self.running[tid] = threading.get_ident()
         info = {}
         results = None
+        trace = spec.get("trace")
+        with (tracing.start_span(_span_name(spec), _span_attrs(spec), parent=trace, kind="server") if trace
+              else contextlib.nullcontext()) as span:
+            results, info = self._execute_body(spec, tid, kind, info)
+            if span is not None and info.get("error"):
+                span["status"] = "error"
+        spans = tracing.drain()
+        if spans:
+            info["spans"] = spans
+        self.client.send((P.TASK_DONE, tid, results, info))
+        self._keepalive = None
+
+    def _execute_body(self, spec, tid, kind, info):
+        results = None
         try:
             try:
                 if _ENV_ERROR is not None:
@@ -230,10 +247,7 @@ class Worker:
                 results, info = self._error_results(spec, e)
         finally:
             self.running.pop(tid, None)
-        self.client.send((P.TASK_DONE, tid, results, info))
-        self._keepalive = None
-        if kind == "actor_creation" and info.get("error"):
-            pass
+        return results, info
 
     def _error_results(self, spec, e, dep=False):
         if dep or isinstance(e, exc.RayTaskError):
@@ -329,6 +343,7 @@ class Worker:
         async with self.asem:
             tid = spec["tid"]
             self._set_ctx(spec)
+            t_start = time.time()
             info = {}
             try:
                 args, kwargs = self._resolve_args(spec)
@@ -375,6 +390,15 @@ class Worker:
                     results = [self._pack_one(rid, None) for rid in spec["return_ids"]]
                 else:
                     results, info = self._error_results(spec, e)
+            if spec.get("trace"):
+                tr = spec["trace"]
+                tracing._record({"trace_id": tr[0], "span_id": tracing._new_id(8), "parent_id": tr[1],
+                                 "name": _span_name(spec), "kind": "server", "start": t_start, "end": time.time(),
+                                 "pid": os.getpid(), "thread": 0, "attributes": _span_attrs(spec),
+                                 "status": "error" if info.get("error") else "ok"})
+            spans = tracing.drain()
+            if spans:
+                info["spans"] = spans
             self.client.send((P.TASK_DONE, tid, results, info))
 
 
@@ -382,6 +406,19 @@ class _DepError(Exception):
     def __init__(self, err):
         super().__init__(str(err))
         self.err = err
+
+
+def _span_name(spec):
+    kind = spec["kind"]
+    if kind == "actor_task":
+        return f"actor_method::{spec.get('name')}"
+    if kind == "actor_creation":
+        return f"actor_creation::{spec.get('class_name') or spec.get('name')}"
+    return f"task::{spec.get('name')}"
+
+
+def _span_attrs(spec):
+    return {"task_id": spec["tid"].hex(), "kind": spec["kind"], "pid": os.getpid()}
 
 
 def _is_exit_actor(e):

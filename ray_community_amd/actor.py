@@ -153,6 +153,11 @@ class ActorClass:
             core.registered_functions.add(fid)
         spec["parent"] = core.ctx.task_id
         spec["caller_node"] = core.node_id
+        from .util import tracing
+
+        trace = tracing.submission_context()
+        if trace is not None:
+            spec["trace"] = trace
         if name:
             core.client.call("submit", spec)
         else:

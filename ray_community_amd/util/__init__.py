@@ -13,7 +13,7 @@ def __getattr__(name):
     import importlib
 
     if name in ("collective", "queue", "actor_pool", "multiprocessing", "metrics", "state", "iter", "serialization",
-                "annotations", "timer"):
+                "annotations", "timer", "tracing"):
         return importlib.import_module("." + name, __name__)
     if name == "ActorPool":
         from .actor_pool import ActorPool
