@@ -83,6 +83,7 @@ class Worker:
         self.inbox: "queue.Queue" = queue.Queue()
         self.functions = {}
         self.actor = None
+        self._value_keepalive = {}
         self.actor_spec = None
         self.pool = None
         self.aloop = None
@@ -203,6 +204,7 @@ class Worker:
             info["spans"] = spans
         self.client.send((P.TASK_DONE, tid, results, info))
         self._keepalive = None
+        self._value_keepalive.pop(tid, None)
 
     def _execute_body(self, spec, tid, kind, info):
         results = None
@@ -230,6 +232,8 @@ class Worker:
                 else:
                     fn = self._get_function(spec)
                     value = fn(*args, **kwargs)
+                # refs nested in the value (ray.put inside the task) must outlive the TASK_DONE send
+                self._value_keepalive[tid] = value
                 results = self._pack_returns(spec, value)
             except _ActorExit:
                 info["actor_exit"] = True
