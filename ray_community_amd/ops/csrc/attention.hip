@@ -185,10 +185,12 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   constexpr float THR = 8.f;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
-  const int nqb = S / BQ, BH = B * Hq;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int qb = CAUSAL ? nqb - 1 - lid / BH : lid / BH;  // longest causal rows first
-  const int bh = lid % BH, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hk);
+  const int nqb = S / BQ, G = Hq / Hk;
+  // one (batch, kv head) per group: its G query heads x nqb query blocks share the K/V stream
+  int bhk, item;
+  xcd_group_map(blockIdx.x, B * Hk, G * nqb, bhk, item);
+  const int qr = item / G, b = bhk / Hk, hk = bhk % Hk, hq = hk * G + item % G, bh = b * Hq + hq;
+  const int qb = CAUSAL ? nqb - 1 - qr : qr;  // longest causal rows first
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int q0 = qb * BQ, qw0 = q0 + 32 * w, qrow = qw0 + l32;
   const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
@@ -380,10 +382,12 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
   constexpr int BQ = 128, BK = 32, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2, G8 = Img<D>::G8;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
-  const int nqb = S / BQ, BH = B * Hq;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int qb = CAUSAL ? nqb - 1 - lid / BH : lid / BH;
-  const int bh = lid % BH, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hk);
+  const int nqb = S / BQ, G = Hq / Hk;
+  // one (batch, kv head) per group: its G query heads x nqb query blocks share the K/V stream
+  int bhk, item;
+  xcd_group_map(blockIdx.x, B * Hk, G * nqb, bhk, item);
+  const int qr = item / G, b = bhk / Hk, hk = bhk % Hk, hq = hk * G + item % G, bh = b * Hq + hq;
+  const int qb = CAUSAL ? nqb - 1 - qr : qr;  // longest causal rows first
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int q0 = qb * BQ, qw0 = q0 + 32 * w, qrow = qw0 + l32;
   const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
@@ -503,10 +507,10 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * SL];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, delta][row]
 
-  const int nkb = S / BKV, BHk = B * Hk, G = Hq / Hk;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int kbi = CAUSAL ? lid / BHk : nkb - 1 - lid / BHk;  // causal: key block 0 sees every query
-  const int bhk = lid % BHk, b = bhk / Hk, hk = bhk % Hk;
+  const int nkb = S / BKV, G = Hq / Hk;
+  int bhk, kbi;
+  xcd_group_map(blockIdx.x, B * Hk, nkb, bhk, kbi);  // causal: key block 0 (sees every query) first
+  const int b = bhk / Hk, hk = bhk % Hk;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int k0 = kbi * BKV, kw0 = k0 + 32 * w, key = kw0 + l32;
   const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
@@ -555,21 +559,19 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = tid < BQS ? -rc : rc;
   };
 
-  stage_load(0, 0);
+  stage_load(0, nsl - 1);
   stage_store(0);
   __syncthreads();
 
-  auto slice = [&](auto bufc, int g, int sl) {
+  // Query slices are swept from the LAST one down to the key block (heads innermost), so the key
+  // blocks of one (batch, kv head) resident on an XCD read the same Q/dO slice at the same time.
+  auto slice = [&](auto bufc, int i) {
     constexpr int buf = decltype(bufc)::value;
     const char* Qs = smem + buf * 2 * SL;
     const char* Gs = Qs + SL;
-    int gn = g, sn = sl + 1;
-    if (sn == nsl) {
-      sn = 0;
-      ++gn;
-    }
-    const bool more = gn < G;
-    if (more) stage_load(gn, sn);
+    const int g = i % G, sl = nsl - 1 - i / G;
+    const bool more = i + 1 < total;
+    if (more) stage_load((i + 1) % G, nsl - 1 - (i + 1) / G);
     const int qa = qs0 + sl * BQS;
     if (!CAUSAL || qa + BQS - 1 >= kw0) {
       bf16x8_t fr[4 * NDB > 2 * NKS ? 4 * NDB : 2 * NKS];
@@ -623,11 +625,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     if (more) stage_store(buf ^ 1);
     __syncthreads();
   };
-  for (int g = 0; g < G; ++g) {
-    for (int sl = 0; sl < nsl; sl += 2) {
-      slice(IC<0>{}, g, sl);
-      slice(IC<1>{}, g, sl + 1);
-    }
+  for (int i = 0; i < total; i += 2) {
+    slice(IC<0>{}, i);
+    slice(IC<1>{}, i + 1);
   }
 
   bf16_t* dKr = dK + ((long)b * S + key) * sdk + (long)hk * D;

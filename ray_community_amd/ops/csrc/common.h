@@ -70,3 +70,21 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
+
+// XCD-grouped work mapping: a grid of ngroups x per workgroups where the `per` workgroups of one
+// group stream the same operand (e.g. the K/V or Q/dO of one (batch, kv-head)). When ngroups is a
+// multiple of 8, every group lives on ONE XCD (hardware deals block ids round-robin over the 8
+// XCDs) and its items are dispatched in item order there, so concurrently resident workgroups of a
+// group read the stream through one L2 instead of eight. Otherwise falls back to xcd_remap order
+// (item-major). Bijective in both cases.
+__device__ __forceinline__ void xcd_group_map(int bid, int ngroups, int per, int& group, int& item) {
+  if ((ngroups & 7) == 0) {
+    const int gpx = ngroups >> 3, xcd = bid & 7, slot = bid >> 3;
+    group = xcd * gpx + slot % gpx;
+    item = slot / gpx;
+  } else {
+    const int lid = xcd_remap(bid, ngroups * per);
+    group = lid % ngroups;
+    item = lid / ngroups;
+  }
+}
