@@ -26,6 +26,7 @@
 // examples (python/ray/train/examples, release/train_tests) — the reference itself has no kernel.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -493,17 +494,20 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
 
 // ---------------------------------------------------------------------------------------------
 // dK, dV (key-major; the kv group's query heads are summed in registers, no atomics). Query
-// slices of 32 rows stream through a 2-deep LDS ring (loop unrolled over it). Per slice: Q/dO row
-// burst -> S, dP MFMAs (key on the lane, two independent chains), P/dS on the VALU, dO^T/Q^T
-// transposed burst -> dV^T, dK^T MFMAs. One wave per SIMD (K, V fragments + both accumulators
-// stay in registers; build flag -amdgpu-mfma-vgpr-form keeps the accumulators out of copies).
-template <int D, bool CAUSAL>
+// slices of NH x 32 rows stream through a 2-deep LDS ring (loop unrolled over it). Per 32-row
+// half: Q/dO row burst -> S, dP MFMAs (key on the lane, two independent chains), P/dS on the VALU,
+// dO^T/Q^T transposed burst -> dV^T, dK^T MFMAs. With NH = 2 the halves are software-pipelined in
+// one basic block (half 1's S/dP MFMAs beside half 0's P/dS VALU work, half 0's dV/dK MFMAs beside
+// half 1's), and one barrier serves 64 query rows. One wave per SIMD (K, V fragments + both
+// accumulators stay in registers; build flag -amdgpu-mfma-vgpr-form keeps the accumulators out of
+// copies).
+template <int D, bool CAUSAL, int NH>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
     long sdo, long sdk, long sdv, float scale2, float scale) {
-  constexpr int BKV = 128, BQS = 32, NKS = D / 16, NDB = D / 32, SL = BQS * D * 2, G8 = Img<D>::G8;
+  constexpr int BKV = 128, BQS = 32 * NH, NKS = D / 16, NDB = D / 32, SL = BQS * D * 2, G8 = Img<D>::G8;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * SL];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, delta][row]
 
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
   }
 
   const int qs0 = CAUSAL ? k0 : 0;
-  const int nsl = (S - qs0) / BQS;  // multiple of 4
+  const int nsl = (S - qs0) / BQS;  // even (S - qs0 is a multiple of 128)
   const int total = G * nsl;        // even
 
   Stage<D, BQS> qst, gst;
@@ -569,57 +573,77 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     constexpr int buf = decltype(bufc)::value;
     const char* Qs = smem + buf * 2 * SL;
     const char* Gs = Qs + SL;
-    const int g = i % G, sl = nsl - 1 - i / G;
+    const int sl = nsl - 1 - i / G;
     const bool more = i + 1 < total;
     if (more) stage_load((i + 1) % G, nsl - 1 - (i + 1) / G);
     const int qa = qs0 + sl * BQS;
     if (!CAUSAL || qa + BQS - 1 >= kw0) {
-      bf16x8_t fr[4 * NDB > 2 * NKS ? 4 * NDB : 2 * NKS];
+      // S and dP of half t (rows 32t..32t+31 of the slice): row-operand burst + two MFMA chains
+      auto sdp = [&](int t, f32x16& s, f32x16& dp) {
+        bf16x8_t fr[2 * NKS];
 #pragma unroll
-      for (int kk = 0; kk < NKS; ++kk) {
-        fr[kk] = lds_b128(Qs + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
-        fr[NKS + kk] = lds_b128(Gs + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
-      }
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int kk = 0; kk < NKS; ++kk) {
-        s = mfma32(fr[kk], kf[kk], s);
-        dp = mfma32(fr[NKS + kk], vf[kk], dp);
-      }
-      const bool diag = CAUSAL && qa < kw0 + 31;
-      const int kq = key - qa - 4 * h;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&rowc[buf][0][8 * g4 + 4 * h]);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&rowc[buf][1][8 * g4 + 4 * h]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * g4 + i;
-          float p = fast_exp2(fmaf(s[r], scale2, l4[i]));
-          if (diag) p = kq > 8 * g4 + i ? 0.f : p;
-          s[r] = p;
-          dp[r] = p * (dp[r] - d4[i]);
+        for (int kk = 0; kk < NKS; ++kk) {
+          const int o = ((kk & 1) ? rb1 : rb0) + 4 * G8 * t + 512 * (kk >> 1);
+          fr[kk] = lds_b128(Qs + o);
+          fr[NKS + kk] = lds_b128(Gs + o);
         }
-      }
-      const bf16x8_t pf0 = acc_to_bf16(s, 0), pf1 = acc_to_bf16(s, 1);
-      const bf16x8_t df0 = acc_to_bf16(dp, 0), df1 = acc_to_bf16(dp, 1);
+        s = zero16();
+        dp = zero16();
 #pragma unroll
-      for (int st = 0; st < 2; ++st)
+        for (int kk = 0; kk < NKS; ++kk) {
+          s = mfma32(fr[kk], kf[kk], s);
+          dp = mfma32(fr[NKS + kk], vf[kk], dp);
+        }
+      };
+      // P = exp2(S*c - lse), dS = P * (dP - delta) on the VALU (causal mask on the diagonal)
+      auto pds = [&](int t, f32x16& s, f32x16& dp) {
+        const bool diag = CAUSAL && qa + 32 * t < kw0 + 31;
+        const int kq = key - qa - 32 * t - 4 * h;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(&rowc[buf][0][32 * t + 8 * g4 + 4 * h]);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&rowc[buf][1][32 * t + 8 * g4 + 4 * h]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * g4 + j;
+            float p = fast_exp2(fmaf(s[r], scale2, l4[j]));
+            if (diag) p = kq > 8 * g4 + j ? 0.f : p;
+            s[r] = p;
+            dp[r] = p * (dp[r] - d4[j]);
+          }
+        }
+      };
+      // dV^T += dO^T P^T, dK^T += Q^T dS^T for half t: transposed burst + MFMAs
+      auto acc = [&](int t, const f32x16& s, const f32x16& dp) {
+        const bf16x8_t pf0 = acc_to_bf16(s, 0), pf1 = acc_to_bf16(s, 1);
+        const bf16x8_t df0 = acc_to_bf16(dp, 0), df1 = acc_to_bf16(dp, 1);
+        bf16x8_t fr[4 * NDB];
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int db = 0; db < NDB; ++db) {
+            const int o0 = tb0 + G8 * (4 * t + 2 * st) + 512 * db, o1 = tb1 + G8 * (4 * t + 2 * st + 1) + 512 * db;
+            fr[(2 * st) * NDB + db] = lds_tr8(Gs + o0, Gs + o1);
+            fr[(2 * st + 1) * NDB + db] = lds_tr8(Qs + o0, Qs + o1);
+          }
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          const int o0 = tb0 + G8 * (2 * st) + 512 * db, o1 = tb1 + G8 * (2 * st + 1) + 512 * db;
-          fr[(2 * st) * NDB + db] = lds_tr8(Gs + o0, Gs + o1);
-          fr[(2 * st + 1) * NDB + db] = lds_tr8(Qs + o0, Qs + o1);
+          dv[db] = mfma32(fr[db], pf0, dv[db]);
+          dk[db] = mfma32(fr[NDB + db], df0, dk[db]);
         }
 #pragma unroll
-      for (int db = 0; db < NDB; ++db) {
-        dv[db] = mfma32(fr[db], pf0, dv[db]);
-        dk[db] = mfma32(fr[NDB + db], df0, dk[db]);
-      }
+        for (int db = 0; db < NDB; ++db) {
+          dv[db] = mfma32(fr[2 * NDB + db], pf1, dv[db]);
+          dk[db] = mfma32(fr[3 * NDB + db], df1, dk[db]);
+        }
+      };
+      f32x16 s[NH], dp[NH];
 #pragma unroll
-      for (int db = 0; db < NDB; ++db) {
-        dv[db] = mfma32(fr[2 * NDB + db], pf1, dv[db]);
-        dk[db] = mfma32(fr[3 * NDB + db], df1, dk[db]);
+      for (int t = 0; t < NH; ++t) sdp(t, s[t], dp[t]);
+#pragma unroll
+      for (int t = 0; t < NH; ++t) {
+        pds(t, s[t], dp[t]);
+        acc(t, s[t], dp[t]);
       }
     }
     if (more) stage_store(buf ^ 1);
@@ -660,8 +684,17 @@ void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t*
   const long threads = rows * (D / 8);
   hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((threads + kThreads - 1) / kThreads), dim3(kThreads), 0, st, o,
                      dout, delta, B, S, Hq, so, sdo);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C>), dim3(B * Hk * (S / 128)), dim3(kThreads), 0, st, q, k, v, dout,
-                     lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
+  // RCA_ATTN_DKDV_NH=1 selects the unpipelined 32-row-slice variant (A/B measurements)
+  static const int nh = [] {
+    const char* e = getenv("RCA_ATTN_DKDV_NH");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  if (nh == 1)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 1>), dim3(B * Hk * (S / 128)), dim3(kThreads), 0, st, q, k, v,
+                       dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 2>), dim3(B * Hk * (S / 128)), dim3(kThreads), 0, st, q, k, v,
+                       dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3(B * Hq * (S / 128)), dim3(kThreads), 0, st, q, k, v, dout, lse,
                      delta, dq, B, S, Hq, Hk, sq, sk, sv, sdo, sdq, scale2, scale);
 }
