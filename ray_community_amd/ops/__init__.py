@@ -135,6 +135,25 @@ def swiglu(gu):
     return ref.swiglu_ref(gu)
 
 
+def transpose_supported(x) -> bool:
+    """2-D bf16 CUDA tensor, unit inner stride, both dims multiples of 64, 16-B aligned rows."""
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.bfloat16 and x.stride(1) == 1 and x.shape[0] % 64 == 0
+            and x.shape[1] % 64 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
+def transpose(x, out=None):
+    """``x.t().contiguous()`` for a 2-D bf16 tensor: one LDS-tiled pass at HBM rate on the GPU
+    (torch's generic permute copy runs at a fraction of it). CPU / unsupported shapes: torch."""
+    if not transpose_supported(x):
+        return x.t().contiguous() if out is None else out.copy_(x.t())
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C, R), device=x.device, dtype=x.dtype)
+    check(lib().rca_transpose_bf16(x.data_ptr(), out.data_ptr(), R, C, x.stride(0), stream_ptr(x.device)),
+          "transpose_bf16")
+    return out
+
+
 # ----------------------------------------------------------------------------------- RoPE
 class _RoPE(torch.autograd.Function):
     @staticmethod

@@ -123,3 +123,50 @@ RCA_API int rca_rope(void* qkv, const void* cs, const int* pos, long long T, int
                      T, S, nheads_rot, row_stride, D, backward ? -1.f : 1.f);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// bf16 transpose out[C, R] = in[R, C] (row stride ldi, output contiguous), 64 x 64 tiles staged
+// through LDS: 16-B global loads along C, 16-B global stores along R (every output row piece is a
+// full 128-B line). The LDS tile rows are padded to 66 elements (33 dwords), so the eight lanes
+// that gather one output chunk (8 input rows apart) hit eight different banks. Feeds the
+// reduction-contiguous operand layouts of the backward GEMMs (parallel/fused_linear.py).
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                             int R, int C, long ldi) {
+  constexpr int TP = 66;
+  __shared__ unsigned tile32[64 * TP / 2];
+  bf16_t* tile = reinterpret_cast<bf16_t*>(tile32);
+  const int tilesC = C >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = (bid / tilesC) << 6, c0 = (bid % tilesC) << 6;
+  const int t = threadIdx.x, ch = t & 7, rr = t >> 3;
+  u32x4 v[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+    v[p] = *reinterpret_cast<const u32x4*>(in + (long)(r0 + rr + 32 * p) * ldi + c0 + ch * 8);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    unsigned* dst = tile32 + ((rr + 32 * p) * TP + ch * 8) / 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = v[p][i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = rr + 32 * p;
+    u32x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (unsigned)tile[(ch * 8 + 2 * i) * TP + c] | ((unsigned)tile[(ch * 8 + 2 * i + 1) * TP + c] << 16);
+    *reinterpret_cast<u32x4*>(out + (long)(c0 + c) * R + r0 + ch * 8) = o;
+  }
+}
+
+RCA_API int rca_transpose_bf16(const void* in, void* out, int R, int C, long long ldi, hipStream_t stream) {
+  if (R <= 0 || C <= 0 || (R & 63) || (C & 63) || (ldi & 7) || ldi < C) return -1;
+  if (((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return -3;
+  const long long tiles = (long long)(R >> 6) * (C >> 6);
+  if (tiles >= (1LL << 31)) return -2;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, (const bf16_t*)in,
+                     (bf16_t*)out, R, C, (long)ldi);
+  return (int)hipGetLastError();
+}

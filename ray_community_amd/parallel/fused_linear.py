@@ -10,9 +10,16 @@ AccumulateGrad hooks would have done is notified directly (``_rca_grad_ready``).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from .. import ops
+
+# RCA_BWD_TRANSPOSED=0 keeps the plain (transposed-operand) GEMM calls, for A/B measurements
+_TRANSPOSED = os.environ.get("RCA_BWD_TRANSPOSED", "1") != "0"
 
 
 class _LinearWgradIntoFlat(torch.autograd.Function):
@@ -26,17 +33,29 @@ class _LinearWgradIntoFlat(torch.autograd.Function):
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
         w = ctx.weight
-        gx = torch.matmul(gy, w) if ctx.needs_input_grad[0] else None
         g2 = gy.reshape(-1, gy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
+        # Reduction-contiguous operands: both backward products have their reduction dim as the
+        # OUTER dim of one (dgrad: W) or both (wgrad: gy, x) operands, which hipBLASLt runs at
+        # 0.93-1.33 PF/s at the 8B shapes; on transposed copies the same products run at
+        # 1.29-1.58 PF/s (scripts/gemm_layout.py). The copies come from one HBM-rate HIP pass each.
+        tr = _TRANSPOSED and ops.transpose_supported(g2) and ops.transpose_supported(x2) and ops.transpose_supported(w)
+        if ctx.needs_input_grad[0]:
+            gx = F.linear(gy, ops.transpose(w)) if tr else torch.matmul(gy, w)
+        else:
+            gx = None
+        if tr:
+            a, b = ops.transpose(g2), ops.transpose(x2).t()
+        else:
+            a, b = g2.t(), x2
         view = w.grad
         if view is None or not getattr(w, "_rca_flat_grad", False) or view.dtype != g2.dtype:
-            return gx, torch.mm(g2.t(), x2).to(w.dtype)  # plain autograd accumulation
+            return gx, torch.mm(a, b).to(w.dtype)  # plain autograd accumulation
         if getattr(w, "_rca_grad_fresh", False):
-            torch.mm(g2.t(), x2, out=view)
+            torch.mm(a, b, out=view)
             w._rca_grad_fresh = False
         else:
-            view.addmm_(g2.t(), x2)
+            view.addmm_(a, b)
         cb = getattr(w, "_rca_grad_ready", None)
         if cb is not None:
             cb(w)

@@ -334,3 +334,32 @@ def test_batch_norm_act_matches_fp32(N, C, H, W, relu, with_res):
     _close(b.grad, br.grad, atol=5e-2 * (N * H * W) ** 0.5, rtol=2e-2, msg="dbeta")
     if with_res:
         _close(rk.grad, rr.grad, atol=3e-2, rtol=3e-2, msg="dres")
+
+
+@pytest.mark.parametrize("R,C,pad", [(64, 64, 0), (256, 192, 0), (8192, 448, 64), (128, 4096, 8)])
+def test_transpose_bf16(R, C, pad):
+    torch.manual_seed(0)
+    base = torch.randn(R, C + pad, device=DEV, dtype=torch.bfloat16)
+    x = base[:, :C]
+    out = ops.transpose(x)
+    assert out.shape == (C, R) and out.is_contiguous()
+    assert torch.equal(out, x.t().contiguous())
+
+
+def test_fused_wgrad_linear_transposed_backward_matches_fp32():
+    """dgrad/wgrad through the transposed-operand GEMMs vs an fp32 autograd reference."""
+    from ray_community_amd.parallel.fused_linear import FusedWgradLinear
+
+    torch.manual_seed(0)
+    lin = FusedWgradLinear(256, 384, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(2, 64, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    gy = torch.randn(2, 64, 384, device=DEV, dtype=torch.bfloat16)
+    lin.weight._rca_flat_grad = True
+    lin.weight.grad = torch.zeros_like(lin.weight)
+    lin.weight._rca_grad_fresh = True
+    lin(x).backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = lin.weight.detach().float().requires_grad_(True)
+    torch.nn.functional.linear(xr, wr).backward(gy.float())
+    _close(x.grad, xr.grad, atol=0.15, rtol=2e-2, msg="dgrad")
+    _close(lin.weight.grad, wr.grad, atol=0.15, rtol=2e-2, msg="wgrad")
