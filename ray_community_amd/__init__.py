@@ -43,7 +43,7 @@ def remote(*args, **kwargs):
 
 
 _LAZY = {"util", "train", "tune", "data", "serve", "rllib", "dag", "air", "experimental", "models", "ops", "parallel",
-         "cluster_utils", "job_submission", "workflow", "runtime_env", "autoscaler", "utils"}
+         "cluster_utils", "job_submission", "workflow", "runtime_env", "autoscaler", "utils", "job_config", "scripts"}
 
 
 def __getattr__(name):

@@ -81,6 +81,12 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             if ignore_reinit_error:
                 return RayContext(_state)
             raise RuntimeError("Maybe you called init() twice by accident? Use ignore_reinit_error=True.")
+        if job_config is not None:
+            if namespace is None and job_config.ray_namespace is not None:
+                namespace = job_config.ray_namespace
+            if runtime_env is None and job_config.runtime_env:
+                runtime_env = job_config.runtime_env
+        _state["job_config"] = job_config
         if address is None:
             address = os.environ.get("RAY_ADDRESS") or os.environ.get("RCA_ADDRESS")
         if address in ("local", None):

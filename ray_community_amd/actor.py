@@ -125,6 +125,12 @@ class ActorClass:
             except ValueError:
                 pass
         lifetime = opts.get("lifetime")
+        if lifetime is None:
+            from ._private.worker import _state as _wstate
+
+            jc = _wstate.get("job_config")
+            if jc is not None and getattr(jc, "default_actor_lifetime", None) == "detached":
+                lifetime = "detached"
         if lifetime not in (None, "detached", "non_detached"):
             raise ValueError("actor `lifetime` argument must be one of 'detached', 'non_detached' and 'None'.")
         fid = self._ensure_exported(core)

@@ -1,0 +1,453 @@
+"""Command-line interface (reference: ``python/ray/scripts/scripts.py`` — the ``ray`` CLI, and
+``python/ray/util/state/state_cli.py`` / ``dashboard/modules/job/cli.py`` for ``list``,
+``summary`` and ``job``).
+
+    python -m ray_community_amd start --head [--num-cpus N] [--num-gpus N] [--block]
+    python -m ray_community_amd status | stop [--force] | timeline [--output F] | memory
+    python -m ray_community_amd list actors|tasks|objects|nodes|workers|placement-groups|jobs
+    python -m ray_community_amd summary tasks|actors|objects
+    python -m ray_community_amd job submit [--submission-id ID] [--no-wait] -- <entrypoint ...>
+    python -m ray_community_amd job status|logs|stop|delete <id> | job list
+    python -m ray_community_amd microbenchmark | healthcheck
+
+Single-node design: ``start --head`` runs the session's head (scheduler, object store, worker
+pool) in a detached process that owns it until ``stop``; every other command and every
+``init(address="auto")`` driver connects to it over its unix socket, located through
+``<temp-dir>/latest_session.json``. ``stop`` signals exactly the head process it started (pid
+recorded in that file) and the head shuts its worker processes down.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+from typing import List, Optional
+
+DEFAULT_ROOT = "/tmp/rca"
+
+
+def _root(args) -> str:
+    return getattr(args, "temp_dir", None) or os.environ.get("RCA_TEMP_DIR") or DEFAULT_ROOT
+
+
+def _session_file(root: str) -> str:
+    return os.path.join(root, "latest_session.json")
+
+
+def _read_session(root: str) -> Optional[dict]:
+    try:
+        with open(_session_file(root)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+        return True
+    except OSError:
+        return False
+
+
+def _connect(args):
+    import ray_community_amd as ray
+
+    addr = getattr(args, "address", None) or "auto"
+    if addr == "auto":
+        os.environ.setdefault("RCA_TEMP_DIR", _root(args))
+        sess = _read_session(_root(args))
+        if not sess or not os.path.exists(sess.get("sock", "")):
+            raise SystemExit(f"no running session under {_root(args)} (start one with `start --head`)")
+    ray.init(address=addr, namespace="_rca_cli", log_to_driver=False)
+    return ray
+
+
+# ------------------------------------------------------------------------------------- start/stop
+def _run_head(args) -> int:
+    """Foreground head: init() a local session and serve until SIGTERM/SIGINT."""
+    import threading
+
+    import ray_community_amd as ray
+
+    os.environ["RCA_TEMP_DIR"] = _root(args)
+    res = json.loads(args.resources) if args.resources else None
+    ray.init(num_cpus=args.num_cpus, num_gpus=args.num_gpus, resources=res, namespace="",
+             include_dashboard=args.include_dashboard, dashboard_port=args.dashboard_port,
+             object_store_memory=args.object_store_memory, _temp_dir=_root(args))
+    stop = threading.Event()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda *_: stop.set())
+    sess = _read_session(_root(args)) or {}
+    print(json.dumps({"address": sess.get("sock"), "pid": os.getpid(), "session": sess.get("session")}), flush=True)
+    while not stop.wait(0.5):
+        pass
+    ray.shutdown()
+    try:
+        cur = _read_session(_root(args))
+        if cur and cur.get("pid") == os.getpid():
+            os.unlink(_session_file(_root(args)))
+    except OSError:
+        pass
+    return 0
+
+
+def cmd_start(args) -> int:
+    if not args.head:
+        print("only single-node sessions are supported: use `start --head`", file=sys.stderr)
+        return 2
+    root = _root(args)
+    cur = _read_session(root)
+    if cur and _alive(int(cur.get("pid", -1))) and os.path.exists(cur.get("sock", "")):
+        print(f"a session is already running (pid {cur['pid']}, address {cur['sock']}); run `stop` first",
+              file=sys.stderr)
+        return 1
+    if args.block:
+        return _run_head(args)
+    os.makedirs(root, exist_ok=True)
+    log = open(os.path.join(root, "head.out"), "ab")
+    cmd = [sys.executable, "-m", "ray_community_amd.scripts.scripts", "_run_head", "--temp-dir", root]
+    for flag in ("num_cpus", "num_gpus", "resources", "dashboard_port", "object_store_memory"):
+        v = getattr(args, flag)
+        if v is not None:
+            cmd += ["--" + flag.replace("_", "-"), str(v)]
+    if args.include_dashboard:
+        cmd.append("--include-dashboard")
+    env = dict(os.environ, RCA_TEMP_DIR=root)
+    proc = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                            start_new_session=True, env=env)
+    deadline = time.time() + args.timeout
+    while time.time() < deadline:
+        sess = _read_session(root)
+        if sess and sess.get("pid") == proc.pid and os.path.exists(sess.get("sock", "")):
+            print(f"Started head (pid {proc.pid}).\n  address: {sess['sock']}\n"
+                  f"  connect with: init(address=\"auto\")  (RCA_TEMP_DIR={root})")
+            return 0
+        if proc.poll() is not None:
+            print(f"head exited with code {proc.returncode}; see {os.path.join(root, 'head.out')}", file=sys.stderr)
+            return 1
+        time.sleep(0.1)
+    print("timed out waiting for the head to come up", file=sys.stderr)
+    return 1
+
+
+def cmd_stop(args) -> int:
+    root = _root(args)
+    sess = _read_session(root)
+    if not sess or not _alive(int(sess.get("pid", -1))):
+        print("no running session")
+        try:
+            os.unlink(_session_file(root))
+        except OSError:
+            pass
+        return 0
+    pid = int(sess["pid"])
+    os.kill(pid, signal.SIGTERM)
+    deadline = time.time() + args.grace_period
+    while time.time() < deadline and _alive(pid):
+        time.sleep(0.1)
+    if _alive(pid):
+        if not args.force:
+            print(f"head (pid {pid}) still running after {args.grace_period}s; use --force", file=sys.stderr)
+            return 1
+        os.kill(pid, signal.SIGKILL)
+    try:
+        os.unlink(_session_file(root))
+    except OSError:
+        pass
+    print(f"Stopped head (pid {pid}).")
+    return 0
+
+
+# ------------------------------------------------------------------------------------- inspection
+def _fmt_res(d: dict) -> str:
+    out = []
+    for k in sorted(d):
+        v = d[k]
+        if k in ("memory", "object_store_memory"):
+            out.append(f"{k}: {v / 2**30:.1f} GiB")
+        elif not k.startswith("node:"):
+            out.append(f"{k}: {v:g}")
+    return ", ".join(out)
+
+
+def cmd_status(args) -> int:
+    ray = _connect(args)
+    try:
+        nodes = ray.nodes()
+        total, avail = ray.cluster_resources(), ray.available_resources()
+        print("======== Cluster status ========")
+        print(f"Nodes: {sum(1 for n in nodes if n.get('Alive', True))} alive / {len(nodes)} total")
+        for n in nodes:
+            print(f"  {n.get('NodeID', '?')[:12]}  alive={n.get('Alive', True)}  {_fmt_res(n.get('Resources', {}))}")
+        print("Usage:")
+        for k in sorted(total):
+            if k.startswith("node:"):
+                continue
+            used = total[k] - avail.get(k, 0.0)
+            if k in ("memory", "object_store_memory"):
+                print(f"  {used / 2**30:.2f}/{total[k] / 2**30:.2f} GiB {k}")
+            else:
+                print(f"  {used:g}/{total[k]:g} {k}")
+        if args.json:
+            print(json.dumps({"nodes": nodes, "total": total, "available": avail}, default=str))
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def cmd_healthcheck(args) -> int:
+    try:
+        ray = _connect(args)
+    except Exception as e:  # noqa: BLE001
+        print(f"unhealthy: {e}", file=sys.stderr)
+        return 1
+    ok = bool(ray.nodes())
+    ray.shutdown()
+    print("healthy" if ok else "unhealthy")
+    return 0 if ok else 1
+
+
+_LISTS = {"actors": "list_actors", "tasks": "list_tasks", "objects": "list_objects", "nodes": "list_nodes",
+          "workers": "list_workers", "placement-groups": "list_placement_groups"}
+
+
+def _parse_filters(fs: List[str]):
+    out = []
+    for f in fs or []:
+        for op in ("!=", "="):
+            if op in f:
+                k, v = f.split(op, 1)
+                out.append((k.strip(), op, v.strip()))
+                break
+        else:
+            raise SystemExit(f"bad filter {f!r} (use key=value or key!=value)")
+    return out
+
+
+def _print_rows(rows, fmt: str):
+    if fmt == "json":
+        print(json.dumps(rows, indent=2, default=str))
+        return
+    if not rows:
+        print("(none)")
+        return
+    cols = [c for c in rows[0].keys() if not isinstance(rows[0][c], (dict, list))][:8]
+    width = {c: max(len(c), *(len(str(r.get(c, ""))[:40]) for r in rows)) for c in cols}
+    print("  ".join(c.upper().ljust(width[c]) for c in cols))
+    for r in rows:
+        print("  ".join(str(r.get(c, ""))[:40].ljust(width[c]) for c in cols))
+
+
+def cmd_list(args) -> int:
+    ray = _connect(args)
+    try:
+        if args.resource == "jobs":
+            from ..job_submission import JobSubmissionClient
+
+            rows = [dict(vars(j)) if not isinstance(j, dict) else j for j in JobSubmissionClient().list_jobs()]
+            rows = [{k: (str(v) if hasattr(v, "value") else v) for k, v in r.items()} for r in rows]
+        else:
+            from ..util import state
+
+            rows = getattr(state, _LISTS[args.resource])(filters=_parse_filters(args.filter), limit=args.limit,
+                                                          detail=args.detail)
+            rows = [r if isinstance(r, dict) else dict(vars(r)) for r in rows]
+        _print_rows(rows, args.format)
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def cmd_summary(args) -> int:
+    ray = _connect(args)
+    try:
+        from ..util import state
+
+        out = getattr(state, f"summarize_{args.resource}")()
+        print(json.dumps(out, indent=2, default=str))
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def cmd_memory(args) -> int:
+    ray = _connect(args)
+    try:
+        from ..util import state
+
+        stats = state.object_store_stats()
+        print("======== Object store ========")
+        print(json.dumps(stats, indent=2, default=str))
+        objs = state.list_objects(limit=args.limit)
+        print(f"======== Objects ({len(objs)}) ========")
+        _print_rows([o if isinstance(o, dict) else dict(vars(o)) for o in objs], "table")
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def cmd_timeline(args) -> int:
+    ray = _connect(args)
+    try:
+        path = args.output or os.path.join(_root(args), f"timeline-{time.strftime('%Y-%m-%d_%H-%M-%S')}.json")
+        ray.timeline(filename=path)
+        print(f"Trace file written to {path} (open in chrome://tracing or Perfetto).")
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def cmd_microbenchmark(args) -> int:
+    from .._private import ray_perf
+
+    results = ray_perf.run(window=args.window, rounds=args.rounds, pattern=args.filter)
+    ray_perf.report(results, out=args.out)
+    return 0
+
+
+# ------------------------------------------------------------------------------------- jobs
+def cmd_job(args) -> int:
+    ray = _connect(args)
+    try:
+        from ..job_submission import JobSubmissionClient
+
+        c = JobSubmissionClient()
+        if args.job_cmd == "submit":
+            ep = args.entrypoint
+            if ep and ep[0] == "--":
+                ep = ep[1:]
+            if not ep:
+                print("missing entrypoint", file=sys.stderr)
+                return 2
+            renv = json.loads(args.runtime_env_json) if args.runtime_env_json else None
+            sid = c.submit_job(entrypoint=" ".join(ep), submission_id=args.submission_id, runtime_env=renv)
+            print(f"Job '{sid}' submitted successfully")
+            if args.no_wait:
+                return 0
+            st = c.wait_until_finish(sid, timeout_s=args.timeout)
+            sys.stdout.write(c.get_job_logs(sid))
+            print(f"Job '{sid}' {st}")
+            return 0 if str(st) == "SUCCEEDED" else 1
+        if args.job_cmd == "status":
+            print(c.get_job_status(args.job_id))
+        elif args.job_cmd == "logs":
+            sys.stdout.write(c.get_job_logs(args.job_id))
+        elif args.job_cmd == "stop":
+            print("stopped" if c.stop_job(args.job_id) else "not running")
+        elif args.job_cmd == "delete":
+            print("deleted" if c.delete_job(args.job_id) else "not found")
+        elif args.job_cmd == "list":
+            for j in c.list_jobs():
+                d = j if isinstance(j, dict) else vars(j)
+                print(json.dumps({k: str(v) for k, v in d.items()}))
+    finally:
+        ray.shutdown()
+    return 0
+
+
+# ------------------------------------------------------------------------------------- parser
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="ray", description="ray_community_amd command-line interface")
+    sub = p.add_subparsers(dest="cmd", required=True)
+
+    def head_opts(sp):
+        sp.add_argument("--num-cpus", type=int, default=None)
+        sp.add_argument("--num-gpus", type=int, default=None)
+        sp.add_argument("--resources", default=None, help='JSON, e.g. \'{"special": 2}\'')
+        sp.add_argument("--object-store-memory", type=int, default=None)
+        sp.add_argument("--include-dashboard", action="store_true")
+        sp.add_argument("--dashboard-port", type=int, default=None)
+        sp.add_argument("--temp-dir", default=None)
+
+    sp = sub.add_parser("start", help="start a head session")
+    sp.add_argument("--head", action="store_true")
+    sp.add_argument("--block", action="store_true", help="run in the foreground")
+    sp.add_argument("--timeout", type=float, default=60.0)
+    head_opts(sp)
+    sp.set_defaults(fn=cmd_start)
+
+    sp = sub.add_parser("_run_head")
+    head_opts(sp)
+    sp.set_defaults(fn=_run_head)
+
+    sp = sub.add_parser("stop", help="stop the running session")
+    sp.add_argument("--force", action="store_true")
+    sp.add_argument("--grace-period", type=float, default=10.0)
+    sp.add_argument("--temp-dir", default=None)
+    sp.set_defaults(fn=cmd_stop)
+
+    def conn_opts(sp):
+        sp.add_argument("--address", default=None)
+        sp.add_argument("--temp-dir", default=None)
+
+    sp = sub.add_parser("status", help="nodes and resource usage")
+    sp.add_argument("--json", action="store_true")
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_status)
+
+    sp = sub.add_parser("healthcheck")
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_healthcheck)
+
+    sp = sub.add_parser("list", help="state API listing")
+    sp.add_argument("resource", choices=sorted(list(_LISTS) + ["jobs"]))
+    sp.add_argument("--filter", action="append", default=[])
+    sp.add_argument("--limit", type=int, default=100)
+    sp.add_argument("--detail", action="store_true")
+    sp.add_argument("--format", choices=["table", "json"], default="table")
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_list)
+
+    sp = sub.add_parser("summary", help="state API summaries")
+    sp.add_argument("resource", choices=["tasks", "actors", "objects"])
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_summary)
+
+    sp = sub.add_parser("memory", help="object store usage and objects")
+    sp.add_argument("--limit", type=int, default=100)
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_memory)
+
+    sp = sub.add_parser("timeline", help="dump a chrome trace of task events")
+    sp.add_argument("--output", default=None)
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_timeline)
+
+    sp = sub.add_parser("microbenchmark", help="core task/actor/object microbenchmarks")
+    sp.add_argument("--window", type=float, default=1.0)
+    sp.add_argument("--rounds", type=int, default=2)
+    sp.add_argument("--filter", default="")
+    sp.add_argument("--out", default=None)
+    sp.set_defaults(fn=cmd_microbenchmark)
+
+    sp = sub.add_parser("job", help="job submission")
+    jsub = sp.add_subparsers(dest="job_cmd", required=True)
+    js = jsub.add_parser("submit")
+    js.add_argument("--submission-id", default=None)
+    js.add_argument("--runtime-env-json", default=None)
+    js.add_argument("--no-wait", action="store_true")
+    js.add_argument("--timeout", type=float, default=3600.0)
+    js.add_argument("entrypoint", nargs=argparse.REMAINDER)
+    conn_opts(js)
+    for name in ("status", "logs", "stop", "delete"):
+        jx = jsub.add_parser(name)
+        jx.add_argument("job_id")
+        conn_opts(jx)
+    jl = jsub.add_parser("list")
+    conn_opts(jl)
+    sp.set_defaults(fn=cmd_job)
+    return p
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = build_parser().parse_args(argv)
+    return int(args.fn(args) or 0)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

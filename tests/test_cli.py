@@ -1,0 +1,91 @@
+"""CLI: start --head / status / list / summary / job submit / timeline / stop (reference:
+python/ray/tests/test_cli.py, dashboard/modules/job/tests/test_cli_integration.py)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cli(tmp, *args, timeout=90):
+    env = dict(os.environ, RCA_TEMP_DIR=str(tmp), PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    return subprocess.run([sys.executable, "-m", "ray_community_amd", *args], env=env, capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT)
+
+
+def test_cli_session_lifecycle(tmp_path):
+    r = _cli(tmp_path, "start", "--head", "--num-cpus", "2", "--resources", '{"special": 3}')
+    assert r.returncode == 0, r.stderr
+    try:
+        sess = json.loads((tmp_path / "latest_session.json").read_text())
+        assert os.path.exists(sess["sock"])
+        assert _cli(tmp_path, "start", "--head").returncode == 1  # already running
+        r = _cli(tmp_path, "status")
+        assert r.returncode == 0 and "2 CPU" in r.stdout and "special" in r.stdout, r.stdout + r.stderr
+        r = _cli(tmp_path, "list", "nodes", "--format", "json")
+        assert r.returncode == 0 and json.loads(r.stdout)[0]["state"] == "ALIVE"
+        r = _cli(tmp_path, "job", "submit", "--", "python", "-c", "'print(6*7)'")
+        assert r.returncode == 0 and "42" in r.stdout and "SUCCEEDED" in r.stdout, r.stdout + r.stderr
+        r = _cli(tmp_path, "list", "jobs", "--format", "json")
+        assert r.returncode == 0 and json.loads(r.stdout)[0]["status"] == "SUCCEEDED"
+        r = _cli(tmp_path, "summary", "tasks")
+        assert r.returncode == 0 and "cluster" in r.stdout
+        out = tmp_path / "tl.json"
+        assert _cli(tmp_path, "timeline", "--output", str(out)).returncode == 0
+        assert isinstance(json.loads(out.read_text()), list)
+        assert _cli(tmp_path, "healthcheck").returncode == 0
+    finally:
+        r = _cli(tmp_path, "stop", "--force")
+    assert r.returncode == 0 and "Stopped" in r.stdout
+    assert not (tmp_path / "latest_session.json").exists()
+    r = _cli(tmp_path, "status")
+    assert r.returncode != 0 and "no running session" in r.stderr
+
+
+def test_cli_driver_connects_with_address_auto(tmp_path):
+    assert _cli(tmp_path, "start", "--head", "--num-cpus", "2").returncode == 0
+    try:
+        code = ("import ray_community_amd as ray; ray.init(address='auto');"
+                "f = ray.remote(lambda x: x * 2); print('OUT', ray.get(f.remote(21)), ray.cluster_resources()['CPU'])")
+        env = dict(os.environ, RCA_TEMP_DIR=str(tmp_path), PYTHONPATH=ROOT)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=90)
+        assert "OUT 42 2.0" in r.stdout, r.stdout + r.stderr
+    finally:
+        _cli(tmp_path, "stop", "--force")
+
+
+@pytest.mark.parametrize("argv", [["--help"], ["list", "--help"], ["job", "submit", "--help"]])
+def test_cli_help(argv, tmp_path):
+    r = _cli(tmp_path, *argv)
+    assert r.returncode == 0 and "usage" in r.stdout.lower()
+
+
+def test_job_config_namespace_runtime_env_and_lifetime(shutdown_only):
+    import ray_community_amd as ray
+    from ray_community_amd.job_config import JobConfig
+
+    jc = JobConfig(runtime_env={"env_vars": {"JC_VAR": "on"}}, ray_namespace="jcns", metadata={"team": "a"})
+    jc.set_default_actor_lifetime("detached")
+    assert JobConfig.from_json(jc._serialize()).metadata == {"team": "a"}
+    ray.init(num_cpus=2, job_config=jc)
+    assert ray.get_runtime_context().namespace == "jcns"
+
+    @ray.remote
+    def env():
+        return os.environ.get("JC_VAR")
+
+    assert ray.get(env.remote()) == "on"
+
+    @ray.remote
+    class A:
+        def ping(self):
+            return 1
+
+    a = A.options(name="jc_actor").remote()
+    assert ray.get(a.ping.remote()) == 1
+    assert ray.get(ray.get_actor("jc_actor", namespace="jcns").ping.remote()) == 1
+    with pytest.raises(ValueError):
+        jc.set_default_actor_lifetime("forever")
