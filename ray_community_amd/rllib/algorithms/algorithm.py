@@ -59,6 +59,12 @@ class Algorithm(Trainable):
         ld.update(self._runner_extra())
         self.learner_group = LearnerGroup(ld, self.obs_space, self.act_space)
         self._sync_weights()
+        from .callbacks import build as _build_callbacks
+
+        self.callbacks = _build_callbacks(getattr(cfg, "_callbacks", None))
+        self._custom_metrics = []
+        if self.callbacks is not None:
+            self.callbacks.on_algorithm_init(algorithm=self)
 
     def _runner_extra(self):
         return {}
@@ -91,6 +97,7 @@ class Algorithm(Trainable):
         if self.remote_runners:
             ms += get([r.get_metrics.remote() for r in self.remote_runners])
         eps = [e for m in ms for e in m["episodes"]]
+        self._custom_metrics = [c for m in ms for c in m.get("custom_metrics", ())]
         for e in eps:
             self._recent.append(e)
         self._episodes_total += len(eps)
@@ -131,12 +138,28 @@ class Algorithm(Trainable):
                               "episode_return_min": res["episode_reward_min"],
                               "episode_len_mean": res["episode_len_mean"],
                               "num_episodes": len(eps)}
+        if self._custom_metrics:
+            from .callbacks import aggregate_custom_metrics
+
+            res["custom_metrics"] = aggregate_custom_metrics(self._custom_metrics)
+            res["env_runners"]["custom_metrics"] = res["custom_metrics"]
         iv = self.config.evaluation_interval
         if iv and self._iteration % iv == 0:
             res["evaluation"] = self.evaluate()
+        if getattr(self, "callbacks", None) is not None:
+            self.callbacks.on_train_result(algorithm=self, result=res)
         return res
 
     def evaluate(self) -> Dict:
+        cb = getattr(self, "callbacks", None)
+        if cb is not None:
+            cb.on_evaluate_start(algorithm=self)
+        out = self._evaluate()
+        if cb is not None:
+            cb.on_evaluate_end(algorithm=self, evaluation_metrics=out)
+        return out
+
+    def _evaluate(self) -> Dict:
         cfg = self.config
         rd = cfg.runner_dict()
         rd.update(self._runner_extra())
@@ -200,6 +223,8 @@ class Algorithm(Trainable):
         self._timesteps_total = st["timesteps_total"]
         self._load_extra_state(st.get("extra") or {})
         self._sync_weights()
+        if getattr(self, "callbacks", None) is not None:
+            self.callbacks.on_checkpoint_loaded(algorithm=self)
 
     def _extra_state(self):
         return {}

@@ -147,9 +147,18 @@ class AlgorithmConfig:
             self.output = output
         return self
 
-    def callbacks(self, cb=None, **kw):
-        self._callbacks = cb
+    def callbacks(self, callbacks_class=None, **kw):
+        """A ``DefaultCallbacks`` subclass (or a list of them, see ``make_multi_callbacks``)."""
+        self._callbacks = callbacks_class if callbacks_class is not None else kw.get("cb")
         return self
+
+    @property
+    def callbacks_class(self):
+        return getattr(self, "_callbacks", None)
+
+    @callbacks_class.setter
+    def callbacks_class(self, v):
+        self._callbacks = v
 
     # ------------------------------------------------------------------ misc
     def copy(self, copy_frozen=None):
@@ -195,4 +204,5 @@ class AlgorithmConfig:
     def runner_dict(self) -> Dict:
         d = self.to_dict()
         d["rollout_fragment_length"] = self.get_rollout_fragment_length()
+        d["callbacks_class"] = getattr(self, "_callbacks", None)
         return d

@@ -40,6 +40,17 @@ class EnvRunner:
         self.steps_sampled = 0
         self.weights_version = -1
         self._rng = np.random.default_rng(self.seed)
+        from ..algorithms.callbacks import Episode, build, overrides
+
+        self._Episode = Episode
+        self.callbacks = build(config.get("callbacks_class"))
+        self._cb_step = overrides(self.callbacks, "on_episode_step")
+        self.new_custom_metrics = []
+        if self.callbacks is not None:
+            self.callbacks.on_environment_created(env_runner=self, env=self.env, env_context=config.get("env_config"))
+            self._eps = [Episode(i) for i in range(self.N)]
+            for i, ep in enumerate(self._eps):
+                self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i)
 
     def spaces(self):
         return self.env.observation_space, self.env.action_space
@@ -53,15 +64,28 @@ class EnvRunner:
     def get_weights(self):
         return self.module.get_state()
 
-    def _track(self, rew, term, trunc):
+    def _track(self, rew, term, trunc, info=None):
         self.ep_ret += rew
         self.ep_len += 1
         done = term | trunc
+        cb = self.callbacks
+        if cb is not None and self._cb_step:
+            for i, ep in enumerate(self._eps):
+                ep.total_reward, ep.length, ep.last_info = float(self.ep_ret[i]), int(self.ep_len[i]), info
+                cb.on_episode_step(episode=ep, env_runner=self, env_index=i)
         if done.any():
             for i in np.nonzero(done)[0]:
                 ep = (float(self.ep_ret[i]), int(self.ep_len[i]))
                 self.completed.append(ep)
                 self.new_episodes.append(ep)
+                if cb is not None:
+                    e = self._eps[i]
+                    e.total_reward, e.length = ep
+                    cb.on_episode_end(episode=e, env_runner=self, env_index=int(i))
+                    if e.custom_metrics:
+                        self.new_custom_metrics.append(dict(e.custom_metrics))
+                    self._eps[i] = self._Episode(int(i))
+                    cb.on_episode_start(episode=self._eps[i], env_runner=self, env_index=int(i))
             self.ep_ret[done] = 0
             self.ep_len[done] = 0
 
@@ -105,7 +129,7 @@ class EnvRunner:
             if tr.any():
                 idx = np.nonzero(tr)[0]
                 trunc_fix.append((t, idx, info["final_obs"][idx]))
-            self._track(r, te, tr)
+            self._track(r, te, tr, info)
             self.obs = nobs
         last_v = self.module.forward(torch.from_numpy(self.obs))[1].numpy()
         next_vf = np.empty_like(vf)
@@ -131,6 +155,8 @@ class EnvRunner:
 
                 self._writer = JsonWriter(self.cfg["output"])
             self._writer.write(b)
+        if self.callbacks is not None:
+            self.callbacks.on_sample_end(env_runner=self, samples=b)
         return b
 
     @torch.no_grad()
@@ -161,16 +187,19 @@ class EnvRunner:
             out["rewards"].append(r)
             out["new_obs"].append(nxt)
             out["terminateds"].append(te)
-            self._track(r, te, tr)
+            self._track(r, te, tr, info)
             self.obs = nobs
         self.steps_sampled += N * T
-        return SampleBatch({k: np.concatenate(v, axis=0) if k in ("obs", "new_obs") else np.concatenate(v) for k, v
-                            in out.items()})
+        b = SampleBatch({k: np.concatenate(v, axis=0) if k in ("obs", "new_obs") else np.concatenate(v) for k, v
+                         in out.items()})
+        if self.callbacks is not None:
+            self.callbacks.on_sample_end(env_runner=self, samples=b)
+        return b
 
     def get_metrics(self) -> Dict:
-        eps = self.new_episodes
-        self.new_episodes = []
-        return {"episodes": eps, "num_env_steps_sampled": self.steps_sampled}
+        eps, cms = self.new_episodes, self.new_custom_metrics
+        self.new_episodes, self.new_custom_metrics = [], []
+        return {"episodes": eps, "num_env_steps_sampled": self.steps_sampled, "custom_metrics": cms}
 
     def ping(self):
         return "ok"

@@ -279,3 +279,55 @@ def test_cql_offline_conservative_and_clones(shutdown_only, tmp_path, lagrangian
     ev = algo.evaluate()
     algo.stop()
     assert "episode_reward_mean" in ev
+
+
+class _CountingCallbacks(ray.rllib.algorithms.DefaultCallbacks):
+    def on_algorithm_init(self, *, algorithm, **kw):
+        algorithm._cb_init = True
+
+    def on_episode_start(self, *, episode, env_runner=None, env_index=0, **kw):
+        episode.user_data["steps"] = 0
+
+    def on_episode_step(self, *, episode, env_runner=None, env_index=0, **kw):
+        episode.user_data["steps"] += 1
+
+    def on_episode_end(self, *, episode, env_runner=None, env_index=0, **kw):
+        assert episode.user_data["steps"] == episode.length
+        episode.custom_metrics["len_seen"] = episode.user_data["steps"]
+
+    def on_sample_end(self, *, env_runner=None, samples=None, **kw):
+        env_runner._cb_samples = getattr(env_runner, "_cb_samples", 0) + 1
+
+    def on_train_result(self, *, algorithm, result, **kw):
+        result["callback_ok"] = True
+
+    def on_evaluate_end(self, *, algorithm, evaluation_metrics, **kw):
+        evaluation_metrics["eval_cb"] = 1
+
+
+class _Second(ray.rllib.algorithms.DefaultCallbacks):
+    def on_train_result(self, *, algorithm, result, **kw):
+        result["second"] = result.get("callback_ok", False)
+
+
+@pytest.mark.parametrize("remote", [0, 1])
+def test_rllib_callbacks_hooks_and_custom_metrics(shutdown_only, remote):
+    from ray_community_amd.rllib.algorithms import make_multi_callbacks
+
+    ray.init(num_cpus=3)
+    cfg = (PPOConfig().environment("CartPole-v1").env_runners(num_env_runners=remote, num_envs_per_env_runner=4)
+           .training(train_batch_size=1024, minibatch_size=256, num_epochs=1)
+           .evaluation(evaluation_interval=1, evaluation_duration=2)
+           .callbacks(make_multi_callbacks([_CountingCallbacks, _Second])).debugging(seed=0))
+    algo = cfg.build()
+    try:
+        assert getattr(algo, "_cb_init", False) is True
+        r = algo.train()
+        assert r["callback_ok"] and r["second"]
+        cm = r["custom_metrics"]
+        assert cm["len_seen_min"] >= 1 and cm["len_seen_mean"] == pytest.approx(r["episode_len_mean"], rel=0.5)
+        assert r["evaluation"]["eval_cb"] == 1
+        if not remote:
+            assert algo.local_runner._cb_samples >= 1
+    finally:
+        algo.stop()
