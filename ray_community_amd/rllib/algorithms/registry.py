@@ -49,8 +49,14 @@ def _bc():
     return BC, BCConfig()
 
 
+def _dreamerv3():
+    from .dreamerv3 import DreamerV3, DreamerV3Config
+
+    return DreamerV3, DreamerV3Config()
+
+
 ALGORITHMS = {"PPO": _ppo, "DQN": _dqn, "IMPALA": _impala, "APPO": _appo, "SAC": _sac, "CQL": _cql, "MARWIL": _marwil,
-              "BC": _bc}
+              "BC": _bc, "DreamerV3": _dreamerv3}
 
 
 def get_algorithm_class(name: str, return_config: bool = False):
