@@ -61,6 +61,8 @@ class LlamaConfig:
 
 PRESETS = {
     "llama3-8b": LlamaConfig(name="llama3-8b"),
+    "llama3-70b": LlamaConfig(hidden_size=8192, intermediate_size=28672, num_layers=80, num_heads=64, num_kv_heads=8,
+                              name="llama3-70b"),
     "llama3-1b": LlamaConfig(hidden_size=2048, intermediate_size=8192, num_layers=16, num_heads=32, num_kv_heads=8,
                              tie_embeddings=True, name="llama3-1b"),
     "llama3-tiny": LlamaConfig(vocab_size=1024, hidden_size=256, intermediate_size=512, num_layers=2, num_heads=4,
