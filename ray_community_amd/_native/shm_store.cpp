@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <pybind11/pybind11.h>
@@ -444,7 +445,40 @@ struct PinnedView {
   }
 };
 
+// Large-object copy into the segment with several threads (reference: the Plasma client's
+// `memcopy_threads` / src/ray/util/memory.cc parallel memcopy): one core's memcpy tops out well
+// below the socket's bandwidth, and the first touch of fresh shm pages faults them in, which
+// then also runs in parallel. Chunks are page aligned.
+static void parallel_memcpy(uint8_t* dst, const uint8_t* src, size_t n, int threads) {
+  constexpr size_t kMin = 8u << 20;
+  if (threads <= 1 || n < kMin) {
+    memcpy(dst, src, n);
+    return;
+  }
+  threads = (int)std::min<size_t>((size_t)threads, n / (kMin / 4));
+  const size_t chunk = ((n + threads - 1) / threads + 4095) & ~(size_t)4095;
+  std::vector<std::thread> ts;
+  for (int t = 1; t < threads; ++t) {
+    const size_t off = chunk * t;
+    if (off >= n) break;
+    const size_t len = std::min(chunk, n - off);
+    ts.emplace_back([=] { memcpy(dst + off, src + off, len); });
+  }
+  memcpy(dst, src, std::min(chunk, n));
+  for (auto& th : ts) th.join();
+}
+
 void register_store(py::module_& m) {
+  m.def(
+      "copy_into",
+      [](py::buffer dst, py::buffer src, int threads) {
+        py::buffer_info di = dst.request(true), si = src.request();
+        const size_t n = (size_t)si.size * si.itemsize;
+        if (n > (size_t)di.size * di.itemsize) throw std::out_of_range("copy_into: destination too small");
+        py::gil_scoped_release rel;
+        parallel_memcpy((uint8_t*)di.ptr, (const uint8_t*)si.ptr, n, threads);
+      },
+      py::arg("dst"), py::arg("src"), py::arg("threads") = 4);
   py::class_<PinnedView>(m, "PinnedView", py::buffer_protocol())
       .def_buffer([](PinnedView& v) -> py::buffer_info {
         return py::buffer_info((void*)(v.store->address() + v.offset), 1, py::format_descriptor<uint8_t>::format(), 1,

@@ -163,6 +163,24 @@ def _dumps(value, buffers: list) -> bytes:
     return f.getvalue()
 
 
+_BULK = 8 << 20  # buffers this large are copied by the native multi-threaded memcpy
+# drivers copy with up to half the cores; worker processes (many of them put at once) copy alone
+_COPY_THREADS = int(os.environ.get("RCA_MEMCOPY_THREADS", 1 if os.environ.get("RCA_WORKER_ID") else
+                                   max(1, min(8, (os.cpu_count() or 2) // 2))))
+_COPY_FN = []
+
+
+def _bulk_copy():
+    if not _COPY_FN:
+        try:
+            from .._native import load
+
+            _COPY_FN.append(getattr(load(), "copy_into", None))
+        except Exception:  # native core unavailable: plain slice assignment
+            _COPY_FN.append(None)
+    return _COPY_FN[0]
+
+
 class Serialized:
     """A serialised value: inband pickle + raw out-of-band buffers, ready to be written."""
 
@@ -195,7 +213,11 @@ class Serialized:
         off = _pad(off + len(self.inband))
         for b, n in zip(self.buffers, self._lens):
             if n:
-                mv[off:off + n] = b.cast("B") if b.format != "B" or b.ndim != 1 else b
+                src = b.cast("B") if b.format != "B" or b.ndim != 1 else b
+                if n >= _BULK and _bulk_copy() is not None:
+                    _bulk_copy()(mv[off:off + n], src, _COPY_THREADS)
+                else:
+                    mv[off:off + n] = src
             off = _pad(off + n)
 
     def to_bytes(self) -> bytes:
