@@ -399,7 +399,7 @@ class Head:
         if kind == "worker":
             w = self.workers.get(ident)
             if w is None or w.dead:
-                cc.conn.send((P.EXIT,))
+                self._send(cc.conn, (P.EXIT,))  # a late/stale worker; it may already be gone
                 return
             cc.worker = w
             self.start_failures = 0
@@ -721,6 +721,21 @@ class Head:
             self._add_timer(timeout, expire)
         self._maybe_block(caller, d)
         return d
+
+    def rpc_object_locations(self, caller, oids):
+        """{oid: {"node_ids": [...], "object_size": n}} for known objects (reference:
+        ``experimental/locations.py``): objects in the node's shm store (or spilled from it) report
+        that node; small inline objects live in their owner's memory and report no node."""
+        out = {}
+        for o in oids:
+            e = self.objects.get(o)
+            if e is None or e.state == PENDING:
+                continue
+            kind = e.desc[0] if e.desc else None
+            nodes = [self.head_node_id.hex() if isinstance(self.head_node_id, bytes) else self.head_node_id] \
+                if kind in ("shm", "spill") else []
+            out[o] = {"node_ids": nodes, "object_size": int(e.size or 0)}
+        return out
 
     def rpc_object_ready(self, caller, oid):
         e = self.objects.get(oid)

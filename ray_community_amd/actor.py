@@ -119,6 +119,10 @@ class ActorClass:
             raise TypeError(f"name must be None or a string, got {type(name)}")
         if name == "":
             raise ValueError("Actor name cannot be an empty string.")
+        if ns is not None and not isinstance(ns, str):
+            raise TypeError(f"namespace must be None or a string, got {type(ns)}")
+        if opts.get("get_if_exists") and not name:
+            raise ValueError("The actor name must be specified to use `get_if_exists`.")
         if opts.get("get_if_exists") and name:
             try:
                 return get_actor(name, namespace=ns)

@@ -173,7 +173,8 @@ class _RoPE(torch.autograd.Function):
         saved = ctx.saved_tensors
         cs = saved[0]
         pos = saved[1] if has_pos else None
-        g = g.contiguous().clone()
+        if not getattr(g, "_rca_owned_grad", False) or not g.is_contiguous():
+            g = g.contiguous().clone()  # never rotate a gradient buffer someone else may still read
         check(lib().rca_rope(g.data_ptr(), cs.data_ptr(), _p(pos), g.shape[0], seq_len, n_rot, g.stride(0), D, 1,
                              stream_ptr(g.device)), "rope_bwd")
         return g, None, None, None, None, None
@@ -552,6 +553,7 @@ class _FlashAttnQKV(torch.autograd.Function):
         _attn_bwd(base, base + es * Hq * D, base + es * (Hq + Hk) * D, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
                   delta.data_ptr(), gb, gb + es * Hq * D, gb + es * (Hq + Hk) * D, B, S, Hq, Hk, D,
                   (W, W, W, Hq * D, Hq * D, W, W, W), scale, causal)
+        dqkv._rca_owned_grad = True  # fresh buffer: the RoPE backward may rotate it in place
         return dqkv, None, None, None, None, None, None, None
 
 

@@ -280,3 +280,35 @@ def test_asyncio_driver_await(ray_start_regular):
 
     assert asyncio.run(main()) == 5
     assert f.remote().future().result() == 5
+
+
+def test_get_if_exists_and_object_locations(shutdown_only):
+    """reference: python/ray/tests/test_get_or_create_actor.py, test_get_locations.py"""
+    import numpy as np
+
+    from ray_community_amd.experimental import get_object_locations
+
+    ray.init(num_cpus=1)
+
+    @ray.remote
+    class A:
+        def pid(self):
+            import os
+
+            return os.getpid()
+
+    for ns in [None, "test"]:
+        a = A.options(name="x", namespace=ns, get_if_exists=True).remote()
+        b = A.options(name="x", namespace=ns, get_if_exists=True).remote()
+        assert ray.get(a.pid.remote()) == ray.get(b.pid.remote())
+    with pytest.raises(TypeError):
+        A.options(name=object(), get_if_exists=True).remote()
+    with pytest.raises(TypeError):
+        A.options(name="x", namespace=object(), get_if_exists=True).remote()
+    with pytest.raises(ValueError):
+        A.options(num_cpus=1, get_if_exists=True).remote()
+
+    small, big = ray.put(1), ray.put(np.zeros(1 << 20))
+    locs = get_object_locations([small, big])
+    assert locs[small]["node_ids"] == [] and locs[big]["object_size"] >= 8 << 20
+    assert locs[big]["node_ids"] == [ray.get_runtime_context().get_node_id()]
