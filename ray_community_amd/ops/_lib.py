@@ -57,8 +57,9 @@ def lib():
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        path = _build.LIB_PATH
-        if not os.path.exists(path) or (_build.is_stale() and os.environ.get("RCA_NO_REBUILD") != "1"):
+        path = os.environ.get("RCA_KERNEL_LIB") or _build.LIB_PATH  # override: A/B builds of the library
+        if path == _build.LIB_PATH and (not os.path.exists(path) or (_build.is_stale() and
+                                                                   os.environ.get("RCA_NO_REBUILD") != "1")):
             try:
                 _build.build()
             except Exception as e:  # pragma: no cover - only on broken toolchains

@@ -22,6 +22,8 @@ ARCH = os.environ.get("RCA_OFFLOAD_ARCH", "gfx950")
 # AGPR-resident accumulator to VGPRs and back around each loop iteration once a kernel's live set
 # exceeds 256 VGPRs (the one-wave-per-SIMD attention dK/dV kernel: 574 v_accvgpr moves -> 26).
 EXTRA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+# per-file overrides: the one-wave-per-SIMD dK/dV kernel keeps its accumulators in AGPRs
+FILE_FLAGS = {"attention_dkdv.hip": []}
 
 
 def _hipcc() -> str:
@@ -43,6 +45,7 @@ def _digest() -> str:
             h.update(f.read())
     h.update(ARCH.encode())
     h.update(" ".join(EXTRA_FLAGS).encode())
+    h.update(repr(sorted(FILE_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -64,7 +67,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     procs = []
     for src in _sources():
         obj = os.path.join(tmpdir, os.path.basename(src) + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj] + EXTRA_FLAGS
+        flags = FILE_FLAGS.get(os.path.basename(src), EXTRA_FLAGS)
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj] + flags
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), src))

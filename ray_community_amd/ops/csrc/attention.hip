@@ -24,150 +24,15 @@
 //                accumulates dQ^T = K^T.dS^T in registers: deterministic, no float atomics.
 // Reference behaviour: torch SDPA / flash-attention semantics as used by the reference's Train
 // examples (python/ray/train/examples, release/train_tests) — the reference itself has no kernel.
-#include "common.h"
+#include "attention_common.h"
 
-#include <cstdlib>
-#include <type_traits>
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+// dK/dV lives in attention_dkdv.hip (its own register-form flags)
+void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
+                          const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
+                          long sq, long sk, long sv, long sdo, long sdk, long sdv, float scale2, float scale,
+                          hipStream_t st);
 
 namespace {
-
-constexpr int kThreads = 256;
-
-__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-// LDS image of a [rows][D] bf16 tile (cdna_hip_programming.md T11 image (a)): 8-row x 32-column
-// subtiles of 512 B, chunk XOR-swizzled inside each 64-B row piece. Both operand reads the kernels
-// need are conflict-free on it and AFFINE in the loop indices, so every LDS read is one of two
-// per-lane base registers plus an immediate offset:
-//   row operand   (rows l32 + 32t, chunk 2kk + h):            rb[kk&1] + 4*G8*t + 512*(kk>>1)
-//   transposed op (rows R0 + 4h + q (+8), cols 32db+16g+4p):  tb[rd]   + G8*(R0/8 + rd) + 512*db
-template <int D>
-struct Img {
-  static constexpr int G8 = D * 16;  // bytes per 8-row group
-  __device__ static __forceinline__ int off(int row, int ch) {
-    return G8 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
-  }
-  __device__ static __forceinline__ int row_base(int l32, int h, int e) {
-    return G8 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 * e + h) ^ ((l32 >> 2) & 3));
-  }
-  __device__ static __forceinline__ int tr_base(int lane, int rd) {
-    const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
-    return 64 * (4 * h + q) + 16 * ((2 * g + (p >> 1)) ^ ((h + 2 * rd) & 3)) + 8 * (p & 1);
-  }
-};
-
-__device__ __forceinline__ bf16x8_t lds_b128(const char* p) {
-  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4*>(p));
-}
-
-// transposed 8-element MFMA operand: two ds_read_b64_tr_b16 (k-steps j = 0..3 and 4..7)
-__device__ __forceinline__ bf16x8_t lds_tr8(const char* p0, const char* p1) {
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-  s16x8 r = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8_t, r);
-}
-
-// registers 8s..8s+7 of an accumulator -> bf16 MFMA operand (k-step s)
-__device__ __forceinline__ bf16x8_t acc_to_bf16(const f32x16& x, int s) {
-  bf16x8_t r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[8 * s + j];
-  return r;
-}
-
-// Pin a register operand loaded from global memory: the asm "redefines" it after its load has
-// landed, so hipcc's loop-merged s_waitcnt bookkeeping stops treating it as pending inside the
-// main loop (otherwise every tile's first MFMAs wait vmcnt for the NEXT tile's staging loads).
-__device__ __forceinline__ void settle(bf16x8_t& v) { asm volatile("" : "+v"(v)); }
-
-__device__ __forceinline__ bf16x8_t gload8(const bf16_t* p) {
-  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4*>(p));
-}
-
-// store 4 consecutive fp32 as bf16 (8 bytes)
-__device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, float d) {
-  uint2 v;
-  v.x = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
-  v.y = (unsigned)f2bf(c) | ((unsigned)f2bf(d) << 16);
-  *reinterpret_cast<uint2*>(p) = v;
-}
-
-// ---------------------------------------------------------------------------------------------
-// [ROWS x D] tile staging HBM -> registers -> LDS. The per-lane parts of both addresses are
-// computed once; per tile only a wave-uniform base changes (global) or an immediate (LDS).
-template <int D, int ROWS>
-struct Stage {
-  static constexpr int NCH = D / 8, N = ROWS * NCH / kThreads, RPI = kThreads / NCH;
-  u32x4 r[N];
-  __amdgpu_buffer_rsrc_t rsrc;  // whole [rows x stride] extent of one (batch, head): wave-uniform
-  int voff, loff;
-  __device__ __forceinline__ void init(const bf16_t* base, long stride, int rows, int tid, int cols = D) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), (short)0,
-                                             (int)((long)(rows - 1) * stride * 2 + cols * 2), 0x00020000);
-    const int row = tid / NCH, ch = tid % NCH;
-    voff = (int)(row * stride * 2 + ch * 16);
-    loff = Img<D>::off(row, ch);
-  }
-  __device__ __forceinline__ void load(int row0, long stride, int extra = 0) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      r[i] = __builtin_bit_cast(
-          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (int)((row0 + i * RPI) * stride * 2) + extra, 0));
-  }
-  __device__ __forceinline__ void store(char* lds) const {
-#pragma unroll
-    for (int i = 0; i < N; ++i) *reinterpret_cast<u32x4*>(lds + loff + i * (RPI / 8) * Img<D>::G8) = r[i];
-  }
-};
-
-template <int V>
-using IC = std::integral_constant<int, V>;
-
-// ---------------------------------------------------------------------------------------------
-// Cross-half (lane <-> lane^32) reductions on the VALU (v_permlane32_swap; no LDS round trip).
-__device__ __forceinline__ float xhalf_max(float v) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xhalf_sum(float v) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// single v_max3_f32 (plain fmaxf on MFMA results gets canonicalising v_max pairs from hipcc)
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-__device__ __forceinline__ float max16(const f32x16& s, float init) {
-  float a = max3f(init, s[0], s[1]), b = max3f(s[2], s[3], s[4]);
-  a = max3f(a, s[5], s[6]);
-  b = max3f(b, s[7], s[8]);
-  a = max3f(a, s[9], s[10]);
-  b = max3f(b, s[11], s[12]);
-  a = max3f(a, s[13], s[14]);
-  return max3f(a, b, s[15]);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Forward. Per 64-key tile each wave runs four clusters: K operand burst (16 x ds_read_b128 into
@@ -492,181 +357,6 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// dK, dV (key-major; the kv group's query heads are summed in registers, no atomics). Query
-// slices of NH x 32 rows stream through a 2-deep LDS ring (loop unrolled over it). Per 32-row
-// half: Q/dO row burst -> S, dP MFMAs (key on the lane, two independent chains), P/dS on the VALU,
-// dO^T/Q^T transposed burst -> dV^T, dK^T MFMAs. With NH = 2 the halves are software-pipelined in
-// one basic block (half 1's S/dP MFMAs beside half 0's P/dS VALU work, half 0's dV/dK MFMAs beside
-// half 1's), and one barrier serves 64 query rows. One wave per SIMD (K, V fragments + both
-// accumulators stay in registers; build flag -amdgpu-mfma-vgpr-form keeps the accumulators out of
-// copies).
-template <int D, bool CAUSAL, int NH>
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
-    long sdo, long sdk, long sdv, float scale2, float scale) {
-  constexpr int BKV = 128, BQS = 32 * NH, NKS = D / 16, NDB = D / 32, SL = BQS * D * 2, G8 = Img<D>::G8;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * SL];
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, delta][row]
-
-  const int nkb = S / BKV, G = Hq / Hk;
-  int bhk, kbi;
-  xcd_group_map(blockIdx.x, B * Hk, nkb, bhk, kbi);  // causal: key block 0 (sees every query) first
-  const int b = bhk / Hk, hk = bhk % Hk;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int k0 = kbi * BKV, kw0 = k0 + 32 * w, key = kw0 + l32;
-  const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
-  const int tb0 = Img<D>::tr_base(lane, 0), tb1 = Img<D>::tr_base(lane, 1);
-
-  bf16x8_t kf[NKS], vf[NKS];
-  {
-    const bf16_t* Kr = K + ((long)b * S + key) * sk + (long)hk * D;
-    const bf16_t* Vr = V + ((long)b * S + key) * sv + (long)hk * D;
-#pragma unroll
-    for (int kk = 0; kk < NKS; ++kk) {
-      kf[kk] = gload8(Kr + 16 * kk + 8 * h);
-      vf[kk] = gload8(Vr + 16 * kk + 8 * h);
-    }
-#pragma unroll
-    for (int kk = 0; kk < NKS; ++kk) {
-      settle(kf[kk]);
-      settle(vf[kk]);
-    }
-  }
-  f32x16 dk[NDB], dv[NDB];
-#pragma unroll
-  for (int i = 0; i < NDB; ++i) {
-    dk[i] = zero16();
-    dv[i] = zero16();
-  }
-
-  const int qs0 = CAUSAL ? k0 : 0;
-  const int nsl = (S - qs0) / BQS;  // even (S - qs0 is a multiple of 128)
-  const int total = G * nsl;        // even
-
-  Stage<D, BQS> qst, gst;
-  qst.init(Q + (long)b * S * sq + (long)hk * G * D, sq, S, tid, G * D);
-  gst.init(dO + (long)b * S * sdo + (long)hk * G * D, sdo, S, tid, G * D);
-  const float* rsrc = (tid < BQS ? LSE : Delta) + ((long)b * Hq + hk * G) * S + (tid & (BQS - 1));
-  float rc = 0.f;
-  auto stage_load = [&](int g, int sl) {
-    const int qa = qs0 + sl * BQS;
-    qst.load(qa, sq, g * D * 2);  // head g of the kv group (the descriptor spans all G heads)
-    gst.load(qa, sdo, g * D * 2);
-    if (tid < 2 * BQS) rc = rsrc[(long)g * S + qa];
-  };
-  auto stage_store = [&](int buf) {
-    qst.store(smem + buf * 2 * SL);
-    gst.store(smem + buf * 2 * SL + SL);
-    if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = tid < BQS ? -rc : rc;
-  };
-
-  stage_load(0, nsl - 1);
-  stage_store(0);
-  __syncthreads();
-
-  // Query slices are swept from the LAST one down to the key block (heads innermost), so the key
-  // blocks of one (batch, kv head) resident on an XCD read the same Q/dO slice at the same time.
-  auto slice = [&](auto bufc, int i) {
-    constexpr int buf = decltype(bufc)::value;
-    const char* Qs = smem + buf * 2 * SL;
-    const char* Gs = Qs + SL;
-    const int sl = nsl - 1 - i / G;
-    const bool more = i + 1 < total;
-    if (more) stage_load((i + 1) % G, nsl - 1 - (i + 1) / G);
-    const int qa = qs0 + sl * BQS;
-    if (!CAUSAL || qa + BQS - 1 >= kw0) {
-      // S and dP of half t (rows 32t..32t+31 of the slice): row-operand burst + two MFMA chains
-      auto sdp = [&](int t, f32x16& s, f32x16& dp) {
-        bf16x8_t fr[2 * NKS];
-#pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) {
-          const int o = ((kk & 1) ? rb1 : rb0) + 4 * G8 * t + 512 * (kk >> 1);
-          fr[kk] = lds_b128(Qs + o);
-          fr[NKS + kk] = lds_b128(Gs + o);
-        }
-        s = zero16();
-        dp = zero16();
-#pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) {
-          s = mfma32(fr[kk], kf[kk], s);
-          dp = mfma32(fr[NKS + kk], vf[kk], dp);
-        }
-      };
-      // P = exp2(S*c - lse), dS = P * (dP - delta) on the VALU (causal mask on the diagonal)
-      auto pds = [&](int t, f32x16& s, f32x16& dp) {
-        const bool diag = CAUSAL && qa + 32 * t < kw0 + 31;
-        const int kq = key - qa - 32 * t - 4 * h;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(&rowc[buf][0][32 * t + 8 * g4 + 4 * h]);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&rowc[buf][1][32 * t + 8 * g4 + 4 * h]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = 4 * g4 + j;
-            float p = fast_exp2(fmaf(s[r], scale2, l4[j]));
-            if (diag) p = kq > 8 * g4 + j ? 0.f : p;
-            s[r] = p;
-            dp[r] = p * (dp[r] - d4[j]);
-          }
-        }
-      };
-      // dV^T += dO^T P^T, dK^T += Q^T dS^T for half t: transposed burst + MFMAs
-      auto acc = [&](int t, const f32x16& s, const f32x16& dp) {
-        const bf16x8_t pf0 = acc_to_bf16(s, 0), pf1 = acc_to_bf16(s, 1);
-        const bf16x8_t df0 = acc_to_bf16(dp, 0), df1 = acc_to_bf16(dp, 1);
-        bf16x8_t fr[4 * NDB];
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            const int o0 = tb0 + G8 * (4 * t + 2 * st) + 512 * db, o1 = tb1 + G8 * (4 * t + 2 * st + 1) + 512 * db;
-            fr[(2 * st) * NDB + db] = lds_tr8(Gs + o0, Gs + o1);
-            fr[(2 * st + 1) * NDB + db] = lds_tr8(Qs + o0, Qs + o1);
-          }
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-          dv[db] = mfma32(fr[db], pf0, dv[db]);
-          dk[db] = mfma32(fr[NDB + db], df0, dk[db]);
-        }
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-          dv[db] = mfma32(fr[2 * NDB + db], pf1, dv[db]);
-          dk[db] = mfma32(fr[3 * NDB + db], df1, dk[db]);
-        }
-      };
-      f32x16 s[NH], dp[NH];
-#pragma unroll
-      for (int t = 0; t < NH; ++t) sdp(t, s[t], dp[t]);
-#pragma unroll
-      for (int t = 0; t < NH; ++t) {
-        pds(t, s[t], dp[t]);
-        acc(t, s[t], dp[t]);
-      }
-    }
-    if (more) stage_store(buf ^ 1);
-    __syncthreads();
-  };
-  for (int i = 0; i < total; i += 2) {
-    slice(IC<0>{}, i);
-    slice(IC<1>{}, i + 1);
-  }
-
-  bf16_t* dKr = dK + ((long)b * S + key) * sdk + (long)hk * D;
-  bf16_t* dVr = dV + ((long)b * S + key) * sdv + (long)hk * D;
-#pragma unroll
-  for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      store4(dKr + 32 * db + 8 * g + 4 * h, dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale,
-             dk[db][4 * g + 2] * scale, dk[db][4 * g + 3] * scale);
-      store4(dVr + 32 * db + 8 * g + 4 * h, dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]);
-    }
-  }
-}
-
 template <int D, bool C>
 void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                 int Hk, long sq, long sk, long sv, long so, float scale2, hipStream_t st) {
@@ -684,17 +374,8 @@ void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t*
   const long threads = rows * (D / 8);
   hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((threads + kThreads - 1) / kThreads), dim3(kThreads), 0, st, o,
                      dout, delta, B, S, Hq, so, sdo);
-  // RCA_ATTN_DKDV_NH=1 selects the unpipelined 32-row-slice variant (A/B measurements)
-  static const int nh = [] {
-    const char* e = getenv("RCA_ATTN_DKDV_NH");
-    return e && atoi(e) == 1 ? 1 : 2;
-  }();
-  if (nh == 1)
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 1>), dim3(B * Hk * (S / 128)), dim3(kThreads), 0, st, q, k, v,
-                       dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
-  else
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 2>), dim3(B * Hk * (S / 128)), dim3(kThreads), 0, st, q, k, v,
-                       dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
+  rca_attn_launch_dkdv(D, C, q, k, v, dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale,
+                       st);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3(B * Hq * (S / 128)), dim3(kThreads), 0, st, q, k, v, dout, lse,
                      delta, dq, B, S, Hq, Hk, sq, sk, sv, sdo, sdq, scale2, scale);
 }
