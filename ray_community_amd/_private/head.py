@@ -28,6 +28,7 @@ from typing import Any, Callable, Dict, List, Optional, Set
 
 from .. import exceptions as exc
 from . import protocol as P
+from .gc_tuning import tune_gc
 from .ids import new_id
 from .object_store import ObjectStore, default_store_capacity, native
 from .serialization import FLAG_ERROR, serialize
@@ -192,6 +193,7 @@ class Head:
         self.logs_dir = os.path.join(session_dir, "logs")
         os.makedirs(self.logs_dir, exist_ok=True)
         self.config = dict(system_config or {})
+        tune_gc(self.config)
         self.namespace = namespace
         self.job_id = job_id or new_id()
         self.sched = native().Scheduler(float(self.config.get("scheduler_spread_threshold", 0.5)))

@@ -430,6 +430,9 @@ def _is_exit_actor(e):
 
 
 def main():
+    from .gc_tuning import tune_gc
+
+    tune_gc()
     w = Worker()
     try:
         w.loop()
