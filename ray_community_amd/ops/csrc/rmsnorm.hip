@@ -192,6 +192,110 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_reg(const bf16_t* __restrict_
   }
 }
 
+// Backward for H = 2048 * CPW (Llama hidden sizes 2048/4096). The per-wave LDS dw slices of
+// rmsnorm_bwd_reg cost 4*H*4 B per block (64 KB at H=4096 -> 2 waves/SIMD) and the generic
+// two-pass loop keeps only ~3 loads in flight per wave. Here a block walks rows TWO at a time and
+// its 4 waves split the columns (wave w owns H/4): each lane keeps its 8*CPW columns' dw partial in
+// VGPRs, both rows' s/dy stay packed in VGPRs (4*CPW 16-B loads in flight per lane), and the row
+// dot products are combined across the 4 waves through 8 LDS floats (double-buffered by
+// iteration parity: one barrier per row pair). No cross-wave dw fold is needed: every column has
+// one owner lane, which writes its block partial directly (fixed order: bitwise reproducible).
+template <int CPW>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_split(const bf16_t* __restrict__ s, const bf16_t* __restrict__ dy,
+                                                         const bf16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                         const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                         float* __restrict__ dw_part, int rows, int H) {
+  __shared__ float dots[2][2][4];  // [parity][row of pair][wave]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cbase = wid * CPW * 64 + lane;  // u32x4 column index of chunk 0 (chunk stride 64)
+  float acc[CPW][8];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  float wf[CPW][8];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) unpack8(wr[cbase + i * 64], wf[i]);
+  const float invH = 1.f / (float)H;
+  int parity = 0;
+  for (int r0 = blockIdx.x * 2; r0 < rows; r0 += gridDim.x * 2, parity ^= 1) {
+    const bool two = r0 + 1 < rows;
+    u32x4 ps[2][CPW], pg[2][CPW];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = two ? r0 + k : r0;
+      const u32x4* sr = reinterpret_cast<const u32x4*>(s + (size_t)row * H);
+      const u32x4* gr = reinterpret_cast<const u32x4*>(dy + (size_t)row * H);
+#pragma unroll
+      for (int i = 0; i < CPW; ++i) {
+        ps[k][i] = __builtin_nontemporal_load(sr + cbase + i * 64);
+        pg[k][i] = __builtin_nontemporal_load(gr + cbase + i * 64);
+      }
+    }
+    float rr[2], dot[2] = {0.f, 0.f};
+    rr[0] = rstd[r0];
+    rr[1] = two ? rstd[r0 + 1] : 0.f;  // a missing second row contributes nothing to dw
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int i = 0; i < CPW; ++i) {
+        float sv[8], gv[8];
+        unpack8(ps[k][i], sv);
+        unpack8(pg[k][i], gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dot[k] += sv[j] * wf[i][j] * gv[j];
+          acc[i][j] += gv[j] * bf2f(f2bf(sv[j] * rr[k]));
+        }
+      }
+    }
+    dot[0] = wave_sum(dot[0]);
+    dot[1] = wave_sum(dot[1]);
+    if (lane == 0) {
+      dots[parity][0][wid] = dot[0];
+      dots[parity][1][wid] = dot[1];
+    }
+    __syncthreads();
+    // opaque: stops the compiler keeping pass-1's unpacked fp32 rows (2x the packed VGPRs) alive
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int i = 0; i < CPW; ++i) asm volatile("" : "+v"(ps[k][i]), "+v"(pg[k][i]));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && !two) break;
+      const int row = r0 + k;
+      const float d = dots[parity][k][0] + dots[parity][k][1] + dots[parity][k][2] + dots[parity][k][3];
+      const float r = rr[k];
+      const float c = d * r * r * r * invH;
+      u32x4* xr = reinterpret_cast<u32x4*>(dx + (size_t)row * H);
+      const u32x4* drr = dres ? reinterpret_cast<const u32x4*>(dres + (size_t)row * H) : nullptr;
+#pragma unroll
+      for (int i = 0; i < CPW; ++i) {
+        float sv[8], gv[8], o[8];
+        unpack8(ps[k][i], sv);
+        unpack8(pg[k][i], gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r * wf[i][j] * gv[j] - c * sv[j];
+        if (drr) {
+          float t[8];
+          unpack8(__builtin_nontemporal_load(drr + cbase + i * 64), t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += t[j];
+        }
+        xr[cbase + i * 64] = pack8(o);
+      }
+    }
+  }
+  f32x4* out = reinterpret_cast<f32x4*>(dw_part + (size_t)blockIdx.x * H);
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    out[(cbase + i * 64) * 2] = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+    out[(cbase + i * 64) * 2 + 1] = f32x4{acc[i][4], acc[i][5], acc[i][6], acc[i][7]};
+  }
+}
+
 __global__ __launch_bounds__(256) void rmsnorm_bwd_generic(const bf16_t* __restrict__ s, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, const float* __restrict__ rstd,
                                                            const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
@@ -300,8 +404,8 @@ RCA_API int rca_rmsnorm_fwd(const void* x, const void* res, const void* w, void*
 
 // returns the number of blocks used for dw partials; dw_part must hold nb*H floats (nb <= 512)
 RCA_API int rca_rmsnorm_bwd_blocks(int rows) {
-  int nb = (rows + 15) / 16;  // >= 4 rows per wave
-  if (nb > 512) nb = 512;
+  int nb = (rows + 7) / 8;  // >= 2 rows per wave
+  if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
   return nb;
 }
@@ -310,9 +414,13 @@ RCA_API int rca_rmsnorm_bwd(const void* s, const void* dy, const void* w, const 
                             float* dw_part, void* dw_bf16, float* dw_f32, int accumulate, int rows, int H,
                             hipStream_t stream) {
   if (H % 8 != 0) return -1;
-  const int nb = rca_rmsnorm_bwd_blocks(rows);
+  // dw_part holds rca_rmsnorm_bwd_blocks(rows) rows; the LDS-slice kernels (2 blocks/CU resident)
+  // use at most 512 of them, the column-split kernel all (>= 4 waves/SIMD, 2 row pairs per block)
+  int nb = rca_rmsnorm_bwd_blocks(rows);
+  const bool split = H == 2048 || H == 4096;  // CPW=4 (H=8192) needs 256 VGPRs: generic
+  if (!split && nb > 512) nb = 512;
   dim3 block(256), grid(nb);
-  const size_t lds = (size_t)4 * H * sizeof(float);
+  const size_t lds = split ? 0 : (size_t)4 * H * sizeof(float);
   if (lds > 160 * 1024) return -2;
   auto S = (const bf16_t*)s;
   auto G = (const bf16_t*)dy;
@@ -322,6 +430,8 @@ RCA_API int rca_rmsnorm_bwd(const void* s, const void* dy, const void* w, const 
   switch (H) {
     case 512: hipLaunchKernelGGL(rmsnorm_bwd_reg<1>, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H); break;
     case 1024: hipLaunchKernelGGL(rmsnorm_bwd_reg<2>, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H); break;
+    case 2048: hipLaunchKernelGGL(rmsnorm_bwd_split<1>, grid, block, 0, stream, S, G, W, rstd, DR, DX, dw_part, rows, H); break;
+    case 4096: hipLaunchKernelGGL(rmsnorm_bwd_split<2>, grid, block, 0, stream, S, G, W, rstd, DR, DX, dw_part, rows, H); break;
     // wider rows: the register-cached variant drops to 1-2 waves/SIMD; the two-pass generic
     // kernel (second pass served from L2) keeps 7 waves/SIMD
     default: hipLaunchKernelGGL(rmsnorm_bwd_generic, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H);

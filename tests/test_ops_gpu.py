@@ -22,11 +22,11 @@ def test_kernel_library_loads():
     assert L.rca_rmsnorm_bwd_blocks(100) >= 1
 
 
-@pytest.mark.parametrize("H", [512, 1024, 4096, 640, 8192])
+@pytest.mark.parametrize("H,rows", [(512, 300), (1024, 300), (2048, 301), (4096, 300), (4096, 8203), (640, 300),
+                                    (8192, 300)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_rmsnorm_fwd_bwd(H, with_res):
+def test_rmsnorm_fwd_bwd(H, rows, with_res):
     torch.manual_seed(0)
-    rows = 300
     x = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
     r = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
@@ -50,7 +50,13 @@ def test_rmsnorm_fwd_bwd(H, with_res):
         y.backward(gy)
         yr.backward(gy.float())
     _close(x.grad, xr.grad, atol=5e-2, rtol=3e-2, msg="dx")
-    _close(w.grad, wr.grad, atol=0.5, rtol=3e-2, msg="dw")
+    # dw sums `rows` terms whose bf16 roundings (s, s*rstd) the fp32 reference skips: that error
+    # grows like sqrt(rows); the rounding-matched fp64 sum below pins the reduction itself
+    _close(w.grad, wr.grad, atol=0.5 * max(1.0, (rows / 300) ** 0.5), rtol=3e-2, msg="dw")
+    s16 = (x.detach().float() + r.detach().float()).bfloat16().float() if with_res else x.detach().float()
+    rs = torch.rsqrt(s16.pow(2).mean(-1, keepdim=True) + 1e-5)
+    dw_m = (gy.double() * (s16 * rs).bfloat16().double()).sum(0)
+    _close(w.grad, dw_m.float(), atol=0.05, rtol=1e-2, msg="dw (rounding-matched)")
     if with_res:
         _close(r.grad, rr.grad, atol=5e-2, rtol=3e-2, msg="dres")
 
