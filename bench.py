@@ -3,9 +3,13 @@
 
     python bench.py --gpus N --steps K --warmup W
 
-N=1: runs in-process. N>1: launched by the driver as
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N ... bench.py --gpus N ...
-one rank per GPU, process group over RCCL (xGMI). The worker function is the framework's Train
+Two launch modes, same worker function:
+  * self-launched (no torchrun): ``TorchTrainer(num_workers=N, use_gpu=True)`` starts N GPU
+    worker actors in a local session; each sees the union of the group's GPUs in
+    ``HIP_VISIBLE_DEVICES`` and joins an RCCL process group (``train/torch/config.py``);
+  * under ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` (the
+    driver's multi-GPU launch): TorchTrainer binds to the launcher's ranks instead.
+Either way ``n_gpus`` is the process group's world size and must equal ``--gpus``. The worker function is the framework's Train
 loop (``ray_community_amd.train.llm.llama_train_loop_per_worker``): full forward + backward +
 bucketed DDP all-reduce + fused AdamW step inside the timed region, bf16 compute, fp32 master
 weights, random-init Llama-3-8B weights, synthetic tokens. Weak scaling (fixed per-GPU batch).
@@ -32,12 +36,19 @@ def main():
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
-    ap.add_argument("--parallel", default="auto", help="auto | ddp | zero (sharded AdamW; auto = zero for N>1)")
+    ap.add_argument("--parallel", default="ddp", choices=["ddp", "zero", "auto"],
+                    help="ddp (replicated AdamW after bucketed all-reduce) | zero (ZeRO-1/2 sharded AdamW) | "
+                         "auto (zero for N>1)")
+    ap.add_argument("--grad-reduce-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="dtype of the gradient collective (fp32 = torch DDP-under-AMP parity)")
     ap.add_argument("--device", default="cuda", help="cuda (the benchmark) | cpu (gloo rehearsal of the launch path)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    external = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    world = int(os.environ["WORLD_SIZE"]) if external else args.gpus
+    rank = int(os.environ.get("RANK", "0")) if external else 0
+    if external and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
 
     import ray_community_amd as ray
     from ray_community_amd.train import RunConfig, ScalingConfig
@@ -46,15 +57,19 @@ def main():
 
     loop_config = {"model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                    "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb, "parallel": args.parallel,
-                   "device": args.device}
-    # N=1: TorchTrainer runs the loop in a GPU worker actor of a local session.
-    # N>1 under torchrun: TorchTrainer binds to the launcher's ranks (one process per GPU,
-    # RCCL process group over xGMI) and runs this rank's share of the job.
+                   "grad_reduce_dtype": args.grad_reduce_dtype, "device": args.device}
+    if not external and args.device == "cpu":
+        ray.init(num_cpus=max(2, args.gpus), include_dashboard=False)
+    # self-launched: TorchTrainer starts N worker actors (one per GPU, RCCL group over xGMI);
+    # under torchrun it binds to the launcher's ranks and runs this rank's share of the job.
     trainer = TorchTrainer(llama_train_loop_per_worker, train_loop_config=loop_config,
                            scaling_config=ScalingConfig(num_workers=max(1, world), use_gpu=args.device == "cuda"),
                            run_config=RunConfig(name="bench_llama", storage_path="/tmp/rca_bench"))
     result = trainer.fit()
     m = result.metrics
+    if int(m["world_size"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but training ran on a process group of {m['world_size']}")
+    world = int(m["world_size"])
     if rank == 0:
         out = {
             "metric": "ray_train_tokens_per_sec_llama3_8b_ddp",
@@ -74,9 +89,12 @@ def main():
                 "global_batch": args.micro_batch * world,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{world}",
+                "parallel_mode": m.get("parallel"),
+                "grad_reduce_dtype": m.get("grad_reduce_dtype"),
+                "launch": "torchrun" if external else "TorchTrainer worker actors",
                 "tokens_per_step": args.micro_batch * world * args.seq_len,
                 "optimizer": "AdamW fp32 master (fused HIP)",
-                "data_parallel": ("DDP: bucketed RCCL all-reduce" if m.get("parallel") == "ddp"
+                "data_parallel": ("DDP: bucketed RCCL all-reduce, replicated fused AdamW" if m.get("parallel") == "ddp"
                                   else "DDP with ZeRO-sharded AdamW: bucketed reduce-scatter + all-gather"),
             },
             "extra": {
@@ -86,7 +104,7 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if external:
         import torch.distributed as dist
 
         if dist.is_initialized():

@@ -21,6 +21,7 @@ import shutil
 import socket
 import subprocess
 import sys
+import tempfile
 import threading
 import time
 import traceback
@@ -28,7 +29,7 @@ from typing import Any, Callable, Dict, List, Optional, Set
 
 from .. import exceptions as exc
 from . import protocol as P
-from .gc_tuning import tune_gc
+from .gc_tuning import restore_gc, tune_gc
 from .ids import new_id
 from .object_store import ObjectStore, default_store_capacity, native
 from .serialization import FLAG_ERROR, serialize
@@ -193,7 +194,9 @@ class Head:
         self.logs_dir = os.path.join(session_dir, "logs")
         os.makedirs(self.logs_dir, exist_ok=True)
         self.config = dict(system_config or {})
-        tune_gc(self.config)
+        # in-process head (local ray.init inside the user's driver): raise the threshold only,
+        # no freeze, and put the driver's setting back at shutdown
+        self._prev_gc = tune_gc(self.config, freeze=False)
         self.namespace = namespace
         self.job_id = job_id or new_id()
         self.sched = native().Scheduler(float(self.config.get("scheduler_spread_threshold", 0.5)))
@@ -233,6 +236,8 @@ class Head:
         self._add_node(self.head_node_id, resources, labels, is_head=True)
         # network
         self.sock_path = os.path.join(session_dir, "head.sock")
+        if len(self.sock_path.encode()) > 100:  # sun_path is 108 bytes: fall back to a short name
+            self.sock_path = os.path.join(tempfile.gettempdir(), f"rca-{new_id().hex()[-12:]}.sock")
         if os.path.exists(self.sock_path):
             os.unlink(self.sock_path)
         self.listener = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -1918,6 +1923,8 @@ class Head:
         self.store.unlink()
         if self.config.get("cleanup_session_dir", True):
             shutil.rmtree(self.spill_dir, ignore_errors=True)
+        restore_gc(self._prev_gc)
+        self._prev_gc = None
 
 
 class ClientConn:

@@ -9,7 +9,8 @@ MI355X-first layout choices:
   * HIP cross-entropy writing dlogits in place over the 128k-vocab logits;
   * activations kept resident (no recomputation) — 288 GB HBM holds a full 8B replica with
     fp32 master weights + AdamW states + seq-4096 activations per GPU.
-GEMMs are plain library GEMMs (hipBLASLt via torch). Attention uses PyTorch's fused SDPA.
+Attention is the framework's own MFMA flash-attention HIP kernels (``ops.attention``: causal,
+GQA, XCD-grouped workgroup order); GEMMs are hipBLASLt via torch.
 """
 from __future__ import annotations
 

@@ -85,7 +85,7 @@ class _RMSNorm(torch.autograd.Function):
         ds2 = ds.contiguous().view(-1, H) if ds is not None else None
         dx = torch.empty_like(s)
         L = lib()
-        nb = L.rca_rmsnorm_bwd_blocks(rows)
+        nb = L.rca_rmsnorm_bwd_blocks(rows, H)
         part = torch.empty(nb, H, device=s.device, dtype=torch.float32)
         dw = torch.empty_like(w)
         check(L.rca_rmsnorm_bwd(s.data_ptr(), dy2.data_ptr(), w.data_ptr(), rstd.data_ptr(), _p(ds2), dx.data_ptr(),

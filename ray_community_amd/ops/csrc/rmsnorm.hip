@@ -403,9 +403,17 @@ RCA_API int rca_rmsnorm_fwd(const void* x, const void* res, const void* w, void*
 }
 
 // returns the number of blocks used for dw partials; dw_part must hold nb*H floats (nb <= 512)
-RCA_API int rca_rmsnorm_bwd_blocks(int rows) {
-  int nb = (rows + 7) / 8;  // >= 2 rows per wave
-  if (nb > 1024) nb = 1024;
+static inline bool rmsnorm_bwd_split(int H) { return H == 2048 || H == 4096; }
+
+// Number of workgroups (= rows of the fp32 dw partials buffer) rca_rmsnorm_bwd launches for
+// (rows, H): the column-split kernel (H = 2048/4096) runs up to 1024 blocks of 2 row pairs each
+// (>= 4 waves/SIMD); the LDS-slice kernels keep 2 blocks/CU resident, so at most 512 blocks of
+// >= 16 rows.
+RCA_API int rca_rmsnorm_bwd_blocks(int rows, int H) {
+  const bool split = rmsnorm_bwd_split(H);
+  int nb = split ? (rows + 7) / 8 : (rows + 15) / 16;
+  const int cap = split ? 1024 : 512;
+  if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return nb;
 }
@@ -414,11 +422,9 @@ RCA_API int rca_rmsnorm_bwd(const void* s, const void* dy, const void* w, const 
                             float* dw_part, void* dw_bf16, float* dw_f32, int accumulate, int rows, int H,
                             hipStream_t stream) {
   if (H % 8 != 0) return -1;
-  // dw_part holds rca_rmsnorm_bwd_blocks(rows) rows; the LDS-slice kernels (2 blocks/CU resident)
-  // use at most 512 of them, the column-split kernel all (>= 4 waves/SIMD, 2 row pairs per block)
-  int nb = rca_rmsnorm_bwd_blocks(rows);
-  const bool split = H == 2048 || H == 4096;  // CPW=4 (H=8192) needs 256 VGPRs: generic
-  if (!split && nb > 512) nb = 512;
+  // dw_part holds rca_rmsnorm_bwd_blocks(rows, H) rows, one per launched block
+  const int nb = rca_rmsnorm_bwd_blocks(rows, H);
+  const bool split = rmsnorm_bwd_split(H);  // CPW=4 (H=8192) needs 256 VGPRs: generic
   dim3 block(256), grid(nb);
   const size_t lds = split ? 0 : (size_t)4 * H * sizeof(float);
   if (lds > 160 * 1024) return -2;

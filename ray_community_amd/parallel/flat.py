@@ -102,6 +102,9 @@ class FlatParameters:
                 if gdt == dtype:
                     p.grad = self.grad[off: off + n].view_as(p)
         self.grad_is_view = gdt == dtype
+        # wider buffer the data-parallel wrappers reduce into (fp32 gradient reduction); when set,
+        # optimizers read their gradients from it instead of ``grad``
+        self.reduced_grad: Optional[torch.Tensor] = None
         self.buckets: List[Bucket] = [Bucket(i, s, e, ps) for i, (s, e, ps) in enumerate(bounds)]
         self.param_bucket = {}
         for b in self.buckets:
@@ -139,6 +142,11 @@ class FlatParameters:
             for p, off in zip(self.params, self.offsets):
                 if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
                     p.grad = self.grad[off: off + p.numel()].view_as(p)
+
+    @property
+    def step_grad(self) -> torch.Tensor:
+        """The gradient buffer an optimizer step should read."""
+        return self.reduced_grad if self.reduced_grad is not None else self.grad
 
     def param_slices(self, name_filter: Optional[Callable[[str], bool]] = None):
         for n, p, off in zip(self.names, self.params, self.offsets):

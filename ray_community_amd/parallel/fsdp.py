@@ -37,13 +37,18 @@ from .flat import ALIGN, FlatParameters
 
 
 class ShardedDataParallel(nn.Module):
-    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0, broadcast_buffers=True):
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0, broadcast_buffers=True,
+                 reduce_dtype=None):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.flat = FlatParameters(module, bucket_cap_mb=bucket_cap_mb, bucket_align=ALIGN * self.world)
+        # fp32 gradient reduction: see DistributedDataParallel(reduce_dtype=...)
+        self.reduce_dtype = reduce_dtype or self.flat.grad.dtype
+        if self.world > 1 and self.reduce_dtype != self.flat.grad.dtype:
+            self.flat.reduced_grad = torch.zeros(self.flat.numel, dtype=self.reduce_dtype, device=self.flat.device)
         self._sync = True
         self._rs: List[Optional[object]] = [None] * len(self.flat.buckets)
         self._ag: List[Optional[object]] = [None] * len(self.flat.buckets)
@@ -87,8 +92,11 @@ class ShardedDataParallel(nn.Module):
     def _launch_rs(self, bi):
         b = self.flat.buckets[bi]
         s, e = self.shard_range(bi)
-        self._rs[bi] = dist.reduce_scatter_tensor(self.flat.grad[s:e], self.flat.grad[b.start: b.end],
-                                                  group=self.pg, async_op=True)
+        g = self.flat.grad
+        if self.flat.reduced_grad is not None:
+            g = self.flat.reduced_grad
+            g[b.start: b.end].copy_(self.flat.grad[b.start: b.end])
+        self._rs[bi] = dist.reduce_scatter_tensor(g[s:e], g[b.start: b.end], group=self.pg, async_op=True)
 
     def finish_gradient_sync(self):
         """Reduce-scatter buckets whose grads never arrived (unused params) and wait for all."""
@@ -208,7 +216,7 @@ class ShardedAdamW:
         lr = self.current_lr()
         bc1, bc2 = 1.0 - self.b1 ** t, 1.0 - self.b2 ** t
         flat.finalize_fresh()
-        g = flat.grad
+        g = flat.step_grad
         clip = self.max_grad_norm if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
         if clip:
             ops.grad_sumsq([g[s:e] for _, s, e, _, _ in self.chunks], out=self._sumsq)

@@ -60,7 +60,7 @@ class FlatAdamW:
         bc2 = 1.0 - self.b2 ** t
         flat = self.flat
         flat.finalize_fresh()
-        g = flat.grad
+        g = flat.step_grad
         clip = self.max_grad_norm if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
         if clip or self.track_grad_norm:
             ops.grad_sumsq([g], out=self._sumsq)
@@ -148,7 +148,7 @@ class FlatSGD:
         self.step_count += 1
         lr = self.lr_schedule(self.step_count) if self.lr_schedule else self.lr
         self.flat.finalize_fresh()
-        p, g = self.flat.data, self.flat.grad
+        p, g = self.flat.data, self.flat.step_grad
         if grad_scale != 1.0:
             g.mul_(grad_scale)
         if self.wd:

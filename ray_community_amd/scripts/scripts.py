@@ -79,6 +79,9 @@ def _run_head(args) -> int:
     ray.init(num_cpus=args.num_cpus, num_gpus=args.num_gpus, resources=res, namespace="",
              include_dashboard=args.include_dashboard, dashboard_port=args.dashboard_port,
              object_store_memory=args.object_store_memory, _temp_dir=_root(args))
+    from .._private.gc_tuning import tune_gc
+
+    tune_gc()  # this process is a dedicated head: freeze the startup heap too
     stop = threading.Event()
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, lambda *_: stop.set())

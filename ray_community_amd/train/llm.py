@@ -22,10 +22,13 @@ def _dist_info():
 
 
 def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4, bucket_cap_mb=256.0,
-                         device=None, seed=1234, max_grad_norm=1.0, parallel="auto", **model_overrides):
-    """``parallel``: "ddp" (replicated AdamW after a bucketed all-reduce), "zero" (reduce-scatter,
-    sharded AdamW, all-gather overlapped with the next forward — parallel/fsdp.py) or "auto"
-    (zero when world > 1: the AdamW pass, ~9 % of a 1-GPU step, shrinks by 1/world)."""
+                         device=None, seed=1234, max_grad_norm=1.0, parallel="ddp", grad_reduce_dtype="bf16",
+                         **model_overrides):
+    """``parallel``: "ddp" (replicated AdamW after a bucketed all-reduce; the default, as the
+    headline metric is DDP), "zero" (reduce-scatter, sharded AdamW, all-gather overlapped with the
+    next forward — parallel/fsdp.py) or "auto" (zero when world > 1: the AdamW pass, ~9 % of a
+    1-GPU step, shrinks by 1/world). ``grad_reduce_dtype``: "bf16" (gradients reduced in the
+    compute dtype) or "fp32" (widened to fp32 before the collective, torch-DDP-under-AMP parity)."""
     from ..models import build_llama
     from ..parallel import DistributedDataParallel, FlatAdamW, ShardedAdamW, ShardedDataParallel
 
@@ -33,13 +36,14 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
     rank, world = _dist_info()
     if parallel == "auto":
         parallel = "zero" if world > 1 else "ddp"
+    rdt = {"bf16": None, "fp32": torch.float32}[grad_reduce_dtype]
     torch.manual_seed(seed)
     net = build_llama(model, device=device, max_seq_len=max(seq_len, 256), **model_overrides)
     if parallel == "zero":
-        ddp = ShardedDataParallel(net, bucket_cap_mb=bucket_cap_mb)
+        ddp = ShardedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt)
         opt = ShardedAdamW(ddp, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
     elif parallel == "ddp":
-        ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb)
+        ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt)
         opt = FlatAdamW(ddp.flat, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
     else:
         raise ValueError(f"unknown parallel mode {parallel!r}")
@@ -77,7 +81,8 @@ def llama_train_loop_per_worker(config: dict):
     mb = int(config.get("micro_batch", 2))
     net, ddp, opt, batch, step = build_llama_training(
         model=config.get("model", "llama3-8b"), seq_len=seq_len, micro_batch=mb, lr=config.get("lr", 3e-4),
-        bucket_cap_mb=config.get("bucket_cap_mb", 256.0), device=device, parallel=config.get("parallel", "auto"),
+        bucket_cap_mb=config.get("bucket_cap_mb", 256.0), device=device, parallel=config.get("parallel", "ddp"),
+        grad_reduce_dtype=config.get("grad_reduce_dtype", "bf16"),
         **config.get("model_overrides", {}))
     rank, world = _dist_info()
     data = [batch() for _ in range(2)]
@@ -110,6 +115,7 @@ def llama_train_loop_per_worker(config: dict):
         "mem_gb": torch.cuda.max_memory_allocated() / 1e9 if dev_kind == "cuda" else 0.0,
         "flops_per_token": net.cfg.flops_per_token(seq_len),
         "parallel": net.parallel_mode,
+        "grad_reduce_dtype": config.get("grad_reduce_dtype", "bf16"),
     }
     report(metrics)
     return metrics

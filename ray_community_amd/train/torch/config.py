@@ -52,11 +52,12 @@ def _setup_torch_process_group(rank, world_size, local_rank, local_world_size, n
     if device_index is not None and torch.cuda.is_available():
         torch.cuda.set_device(device_index)
         kw["device_id"] = torch.device("cuda", device_index)
-    if world_size > 1 or True:
-        if dist.is_initialized():
-            dist.destroy_process_group()
-        dist.init_process_group(backend=backend, init_method=f"tcp://{addr}:{port}", rank=rank,
-                                world_size=world_size, timeout=timedelta(seconds=timeout_s), **kw)
+    # a process group is formed even for world_size 1 so train loops can call collectives
+    # (barrier / all_reduce of metrics) unconditionally
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    dist.init_process_group(backend=backend, init_method=f"tcp://{addr}:{port}", rank=rank,
+                            world_size=world_size, timeout=timedelta(seconds=timeout_s), **kw)
     return True
 
 

@@ -65,3 +65,36 @@ def test_flash_attention_long_causal_rows():
     o = ops.flash_attention(q, k, v, True)
     o_ref = ref.attention_ref(q, k, v, True)
     assert _err(o, o_ref) < 2e-2
+
+
+# Shapes of the production path: B*Hk a multiple of 8 takes the XCD-grouped workgroup order of
+# xcd_group_map (ops/csrc/common.h) in the fwd, dQ and dK/dV kernels -- the Llama-3-8B bench
+# shape is (B=2, S=4096, Hq=32, Hk=8, D=128), B*Hk = 16. dK/dV runs its default 64-row
+# pipelined-slice variant (RCA_ATTN_DKDV_NH unset).
+@pytest.mark.parametrize("B,S,Hq,Hk,D,causal", [
+    (2, 1024, 32, 8, 128, True),
+    (2, 1024, 32, 8, 128, False),
+    (1, 4096, 32, 8, 128, True),
+    (2, 512, 16, 8, 64, True),
+    (1, 1024, 32, 8, 64, False),
+])
+def test_flash_attention_xcd_grouped_fwd_bwd(B, S, Hq, Hk, D, causal):
+    assert (B * Hk) % 8 == 0
+    q, k, v = _mk(B, S, Hq, D, 21), _mk(B, S, Hk, D, 22), _mk(B, S, Hk, D, 23)
+    do = _mk(B, S, Hq, D, 24)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    o_ref = ref.attention_ref(qr, kr, vr, causal)
+    o_ref.backward(do.float())
+    o_ref = o_ref.detach()
+    q.requires_grad_(True)
+    k.requires_grad_(True)
+    v.requires_grad_(True)
+    o = ops.flash_attention(q, k, v, causal)
+    o.backward(do)
+    torch.cuda.synchronize()
+    assert _err(o, o_ref) < 2e-2
+    assert _err(q.grad, qr.grad) < 3e-2
+    assert _err(k.grad, kr.grad) < 3e-2
+    assert _err(v.grad, vr.grad) < 3e-2
+    # every (batch, kv-head) group is covered: no head left unwritten
+    assert torch.isfinite(q.grad).all() and k.grad.float().abs().amax(dim=(1, 3)).min() > 0

@@ -19,7 +19,7 @@ def _close(a, b, atol, rtol=0.0, msg=""):
 
 def test_kernel_library_loads():
     L = ops.lib()
-    assert L.rca_rmsnorm_bwd_blocks(100) >= 1
+    assert L.rca_rmsnorm_bwd_blocks(100, 4096) >= 1
 
 
 @pytest.mark.parametrize("H,rows", [(512, 300), (1024, 300), (2048, 301), (4096, 300), (4096, 8203), (640, 300),
@@ -369,3 +369,29 @@ def test_fused_wgrad_linear_transposed_backward_matches_fp32():
     torch.nn.functional.linear(xr, wr).backward(gy.float())
     _close(x.grad, xr.grad, atol=0.15, rtol=2e-2, msg="dgrad")
     _close(lin.weight.grad, wr.grad, atol=0.15, rtol=2e-2, msg="wgrad")
+
+
+def test_llama_8b_width_two_layers_matches_fp32_cpu():
+    """Two decoder layers at Llama-3-8B width (H=4096, 32 q / 8 kv heads, FFN 14336, RoPE 5e5):
+    the bf16 GPU path (HIP attention on its XCD-grouped branch, B*Hk=16; HIP RMSNorm/RoPE/SwiGLU/CE;
+    fused-wgrad linears) vs the fp32 CPU reference path with the same weights."""
+    from ray_community_amd.models import build_llama
+
+    torch.manual_seed(0)
+    net = build_llama("llama3-8b", device="cpu", dtype=torch.float32, num_layers=2, vocab_size=8192)
+    assert net.cfg.hidden_size == 4096 and net.cfg.num_heads == 32 and net.cfg.num_kv_heads == 8
+    toks = torch.randint(0, 8192, (2, 257))
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    loss_cpu = net(toks[:, :-1], toks[:, 1:])
+    loss_cpu.backward()
+    g_cpu = {n: p.grad.clone() for n, p in net.named_parameters()}
+    net.zero_grad()
+    gnet = net.to(DEV, torch.bfloat16)
+    loss_gpu = gnet(toks[:, :-1].to(DEV), toks[:, 1:].to(DEV))
+    loss_gpu.backward()
+    torch.cuda.synchronize()
+    assert abs(loss_gpu.item() - loss_cpu.item()) < 1e-2 * abs(loss_cpu.item())
+    for n, p in gnet.named_parameters():
+        a, b = p.grad.float().cpu(), g_cpu[n]
+        rel = (a - b).norm() / (b.norm() + 1e-8)
+        assert rel < 0.1, (n, rel.item())
