@@ -41,6 +41,8 @@ def main():
                          "auto (zero for N>1)")
     ap.add_argument("--grad-reduce-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="dtype of the gradient collective (fp32 = torch DDP-under-AMP parity)")
+    ap.add_argument("--overlap-optimizer", action="store_true",
+                    help="run the AdamW update per bucket on a side stream, overlapped with the next forward")
     ap.add_argument("--device", default="cuda", help="cuda (the benchmark) | cpu (gloo rehearsal of the launch path)")
     args = ap.parse_args()
 
@@ -57,7 +59,8 @@ def main():
 
     loop_config = {"model": args.model, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                    "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb, "parallel": args.parallel,
-                   "grad_reduce_dtype": args.grad_reduce_dtype, "device": args.device}
+                   "grad_reduce_dtype": args.grad_reduce_dtype, "device": args.device,
+                   "overlap_optimizer": args.overlap_optimizer}
     if not external and args.device == "cpu":
         ray.init(num_cpus=max(2, args.gpus), include_dashboard=False)
     # self-launched: TorchTrainer starts N worker actors (one per GPU, RCCL group over xGMI);
