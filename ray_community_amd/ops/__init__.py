@@ -154,6 +154,42 @@ def transpose(x, out=None):
     return out
 
 
+# ----------------------------------------------------------------------------------- GEMM
+def _gemm_operand_ok(t) -> bool:
+    return (t.is_cuda and t.dim() == 2 and t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0)
+
+
+def gemm_supported(M: int, N: int, K: int, *tensors) -> bool:
+    """Shapes the hand-written gfx950 GEMM (ops/csrc/gemm.hip) takes: M, N multiples of 256, K of
+    64, bf16 CUDA operands with unit inner stride and 16-B aligned rows."""
+    return M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and M > 0 and N > 0 and K > 0 and all(
+        _gemm_operand_ok(t) for t in tensors)
+
+
+def gemm(a, b, a_kmajor: bool = False, b_kmajor: bool = False, out=None, accumulate: bool = False):
+    """``C[M][N] (+)= sum_k A(m,k) B(n,k)`` on the gfx950 MFMA GEMM.
+
+    ``a`` is ``[M][K]`` (``a_kmajor=False``) or ``[K][M]`` (True); ``b`` is ``[N][K]`` or ``[K][N]``.
+    So ``gemm(x, w)`` = ``x @ w.T`` (linear forward), ``gemm(dy, w, b_kmajor=True)`` = ``dy @ w``
+    (dgrad) and ``gemm(dy, x, True, True)`` = ``dy.T @ x`` (wgrad), all without transposed copies.
+    """
+    M, K = (a.shape[1], a.shape[0]) if a_kmajor else a.shape
+    N, Kb = (b.shape[1], b.shape[0]) if b_kmajor else b.shape
+    if K != Kb:
+        raise ValueError(f"gemm: reduction dims differ ({K} vs {Kb})")
+    if out is None:
+        if accumulate:
+            raise ValueError("gemm: accumulate needs out")
+        out = torch.empty((M, N), device=a.device, dtype=torch.bfloat16)
+    if not gemm_supported(M, N, K, a, b, out) or tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm: unsupported operands M={M} N={N} K={K}")
+    check(lib().rca_gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                              out.stride(0), int(a_kmajor), int(b_kmajor), int(accumulate), stream_ptr(a.device)),
+          "gemm_bf16")
+    return out
+
+
 # ----------------------------------------------------------------------------------- RoPE
 class _RoPE(torch.autograd.Function):
     @staticmethod

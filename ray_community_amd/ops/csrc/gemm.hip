@@ -1,0 +1,344 @@
+// bf16 GEMM for gfx950 (MI355X) on MFMA 16x16x32, with either operand stored k-contiguous or
+// k-outer, so the training backward reads W, dY and X in their natural layouts:
+//
+//   C[M][N] (+)= sum_k A(m, k) * B(n, k)
+//   A: "row"  = A[m][k] (k contiguous, lda = row stride)     | "kmaj" = A[k][m] (m contiguous)
+//   B: "row"  = B[n][k]                                       | "kmaj" = B[k][n]
+//
+//   forward   y  = x W^T      A = x  [T][K] row,   B = W  [N][K] row
+//   dgrad     dx = dy W       A = dy [T][N] row,   B = W  [N][K] kmaj   (k = N)
+//   wgrad     dW = dy^T x     A = dy [T][N] kmaj,  B = x  [T][K] kmaj   (k = T)
+//
+// Structure (cdna_hip_programming.md §5): 256x256x64 block tile, 8 waves (2 M x 4 N), 128x64
+// per wave = 8x4 accumulators of v_mfma_f32_16x16x32_bf16; global->LDS by global_load_lds 16 B
+// per lane (no VGPR staging), two LDS stages (2 x 64 KB); the LDS images are lane-linear with
+// the bank swizzle applied to the per-lane SOURCE address and undone on the read:
+//   * k-contiguous tile [256][64]: 128-B rows, chunk' = chunk ^ ((row >> 1) & 7) -> the 16 rows a
+//     16-lane ds_read_b128 group touches cover all 16 bank slots;
+//   * k-outer tile [64][256]: 512-B k-rows read by ds_read_b64_tr_b16 (hardware transpose: lane
+//     i of a 16-lane group gets column i of 4 k-rows), 16-B chunk' = chunk ^ s(k) with
+//     s(k) = 2 * ((k & 3) | ((k >> 3) & 1) << 2): the 8 k-rows one 32-lane half reads land on 8
+//     distinct even chunk pairs.
+// The MFMA's "A" operand is the B tile and its "B" operand the A tile, so a lane's 4 accumulator
+// registers are 4 CONSECUTIVE n of one m: 8-byte bf16x4 stores in the epilogue.
+// Workgroup order: XCD remap (each XCD gets a contiguous range) then GROUP_M=8 grouped tiles, so
+// the ~32 blocks co-resident on one XCD share A and B panels through that XCD's L2.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
+
+constexpr int BM = 256, BN = 256, NTHR = 512;
+constexpr int GROUP_M = 8;
+
+__device__ __forceinline__ int kswz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+// Stage one 256 x BK operand tile into a lane-linear LDS image (BK/16 global_load_lds per thread).
+template <bool KMAJ, int BK>
+__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* dst,
+                                           int wid, int lane) {
+  constexpr int CPR = BK / 8;  // 16-B chunks per k-contiguous row
+  constexpr int RSH = CPR == 8 ? 1 : 2;  // rows sharing a 256-B bank row differ in (row >> RSH)
+#pragma unroll
+  for (int i = 0; i < BK / 16; ++i) {
+    const int blk = i * 8 + wid;          // 1 KB block of the image this wave instruction fills
+    const int p = blk * 64 + lane;        // 16-B chunk index in the image
+    const bf16_t* src;
+    if constexpr (!KMAJ) {                // [256 outer][CPR chunks]
+      const int row = p / CPR, c = (p % CPR) ^ ((row >> RSH) & (CPR - 1));
+      src = g + (long)(o0 + row) * ld + k0 + c * 8;
+    } else {                              // [BK k][32 chunks]
+      const int kr = p >> 5, c = (p & 31) ^ kswz(kr);
+      src = g + (long)(k0 + kr) * ld + o0 + c * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(dst + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// MFMA operand fragment: 16 outer indices (ob*16 + lane&15) x 8 k (kk*32 + 8*(lane>>4) + 0..7).
+template <bool KMAJ, int BK>
+__device__ __forceinline__ bf16x8_t load_frag(const lds_char* t, int ob, int kk, int lane) {
+  constexpr int CPR = BK / 8;
+  constexpr int RSH = CPR == 8 ? 1 : 2;
+  if constexpr (!KMAJ) {
+    const int row = ob * 16 + (lane & 15);
+    const int c = (kk * 4 + (lane >> 4)) ^ ((row >> RSH) & (CPR - 1));
+    s16x8 v = *(const lds_s16x8*)(t + row * (BK * 2) + c * 16);
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int k1 = kk * 32 + 8 * g + q, k2 = k1 + 4;
+    const int c = ob * 2 + (p >> 1), h = (p & 1) * 8;
+    s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + k1 * 512 + ((c ^ kswz(k1)) << 4) + h));
+    s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + k2 * 512 + ((c ^ kswz(k2)) << 4) + h));
+    s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// NS-stage ring of BK-deep stages; NS-1 stages in flight. One raw s_barrier per stage: the
+// counted vmcnt retires exactly the stage about to be read (the later stages stay in flight
+// ACROSS the barrier -- __syncthreads() would drain them), the barrier publishes every wave's
+// DMA, and the stage refilled right after it was last read one stage earlier by all waves.
+template <bool AK, bool BKM, bool ACC, int BK, int NS>
+__global__ __launch_bounds__(NTHR) void gemm_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                         bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                         long ldb, long ldc) {
+  constexpr int TILE_BYTES = 256 * BK * 2;
+  constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+  constexpr int LOADS = 2 * (BK / 16);  // glds per thread per stage
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+
+  // tile order: XCD-contiguous ranges, GROUP_M-row groups inside
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int lin = xcd_remap(blockIdx.x, nwg);
+  const int gsz = GROUP_M * ntn, grp = lin / gsz, fm = grp * GROUP_M;
+  const int gm = min(ntm - fm, GROUP_M), r = lin % gsz;
+  const int m0 = (fm + r % gm) * BM, n0 = (r / gm) * BN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) {
+    if (s < nt) {
+      lds_char* buf = smem + s * STAGE_BYTES;
+      stage_tile<AK, BK>(A, lda, m0, s * BK, buf, wid, lane);
+      stage_tile<BKM, BK>(B, ldb, n0, s * BK, buf + TILE_BYTES, wid, lane);
+    }
+  }
+
+  for (int t = 0; t < nt; ++t) {
+    if (t + NS - 1 <= nt) wait_vmcnt<(NS - 2) * LOADS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + NS - 1 < nt) {
+      const int s = t + NS - 1;
+      lds_char* buf = smem + (s % NS) * STAGE_BYTES;
+      stage_tile<AK, BK>(A, lda, m0, s * BK, buf, wid, lane);
+      stage_tile<BKM, BK>(B, ldb, n0, s * BK, buf + TILE_BYTES, wid, lane);
+    }
+    const lds_char* ta = smem + (t % NS) * STAGE_BYTES;
+    const lds_char* tb = ta + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8_t bf[4], af[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = load_frag<BKM, BK>(tb, wn * 4 + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = load_frag<AK, BK>(ta, wm * 8 + i, kk, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // epilogue: acc[i][j] reg r = C[m0 + wm*128 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      unsigned long long* dst = (unsigned long long*)(C + m * ldc + n);
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if constexpr (ACC) {
+        const unsigned long long old = *dst;
+        v0 += bf2f((bf16_t)(old & 0xffff));
+        v1 += bf2f((bf16_t)((old >> 16) & 0xffff));
+        v2 += bf2f((bf16_t)((old >> 32) & 0xffff));
+        v3 += bf2f((bf16_t)((old >> 48) & 0xffff));
+      }
+      const unsigned long long o = (unsigned long long)f2bf(v0) | ((unsigned long long)f2bf(v1) << 16) |
+                                   ((unsigned long long)f2bf(v2) << 32) | ((unsigned long long)f2bf(v3) << 48);
+      *dst = o;
+    }
+  }
+}
+
+// Software-pipelined variant (BK=64, two LDS stages): the fragments of the NEXT 32-deep k-step
+// are read from LDS while the MFMAs of the current one run (two register fragment sets, 96 VGPRs,
+// + 128 accumulators), so LDS latency and bandwidth hide under the MFMA pipe:
+//   [glds tile t+1] [read k1(t) || MFMA k0(t)] [lgkm(0) vmcnt(0) barrier] [read k0(t+1) || MFMA k1(t)]
+// Every ds_read retires before the barrier, so the refill of a stage after the next barrier can
+// never overtake a slow reader.
+template <bool AK, bool BKM>
+__device__ __forceinline__ void load_set(const lds_char* ta, const lds_char* tb, int kk, int wm, int wn, int lane,
+                                         bf16x8_t (&af)[8], bf16x8_t (&bf)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bf[j] = load_frag<BKM, 64>(tb, wn * 4 + j, kk, lane);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) af[i] = load_frag<AK, 64>(ta, wm * 8 + i, kk, lane);
+}
+
+__device__ __forceinline__ void mfma_set(f32x4 (&acc)[8][4], const bf16x8_t (&af)[8], const bf16x8_t (&bf)[4]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <bool AK, bool BKM, bool ACC>
+__global__ __launch_bounds__(NTHR) void gemm_bf16_sp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                            bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                            long ldb, long ldc) {
+  constexpr int BK = 64;
+  constexpr int TILE_BYTES = 256 * BK * 2;
+  constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int lin = xcd_remap(blockIdx.x, nwg);
+  const int gsz = GROUP_M * ntn, grp = lin / gsz, fm = grp * GROUP_M;
+  const int gm = min(ntm - fm, GROUP_M), r = lin % gsz;
+  const int m0 = (fm + r % gm) * BM, n0 = (r / gm) * BN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t ax[8], bx[4], ay[8], by[4];
+
+  const int nt = K / BK;
+  stage_tile<AK, BK>(A, lda, m0, 0, smem, wid, lane);
+  stage_tile<BKM, BK>(B, ldb, n0, 0, smem + TILE_BYTES, wid, lane);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  load_set<AK, BKM>(smem, smem + TILE_BYTES, 0, wm, wn, lane, ax, bx);
+  for (int t = 0; t < nt; ++t) {
+    const lds_char* ta = smem + (t & 1) * STAGE_BYTES;
+    const lds_char* tb = ta + TILE_BYTES;
+    const bool more = t + 1 < nt;
+    lds_char* na = smem + ((t + 1) & 1) * STAGE_BYTES;
+    if (more) {
+      stage_tile<AK, BK>(A, lda, m0, (t + 1) * BK, na, wid, lane);
+      stage_tile<BKM, BK>(B, ldb, n0, (t + 1) * BK, na + TILE_BYTES, wid, lane);
+    }
+    load_set<AK, BKM>(ta, tb, 1, wm, wn, lane, ay, by);
+    mfma_set(acc, ax, bx);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) load_set<AK, BKM>(na, na + TILE_BYTES, 0, wm, wn, lane, ax, bx);
+    mfma_set(acc, ay, by);
+  }
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      unsigned long long* dst = (unsigned long long*)(C + m * ldc + n);
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if constexpr (ACC) {
+        const unsigned long long old = *dst;
+        v0 += bf2f((bf16_t)(old & 0xffff));
+        v1 += bf2f((bf16_t)((old >> 16) & 0xffff));
+        v2 += bf2f((bf16_t)((old >> 32) & 0xffff));
+        v3 += bf2f((bf16_t)((old >> 48) & 0xffff));
+      }
+      *dst = (unsigned long long)f2bf(v0) | ((unsigned long long)f2bf(v1) << 16) |
+             ((unsigned long long)f2bf(v2) << 32) | ((unsigned long long)f2bf(v3) << 48);
+    }
+  }
+}
+
+template <bool AK, bool BKM, bool ACC>
+int launch_sp(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+              hipStream_t st) {
+  auto kern = gemm_bf16_sp_kernel<AK, BKM, ACC>;
+  constexpr int smem = 2 * 2 * 256 * 64 * 2;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NTHR), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+template <bool AK, bool BKM, bool ACC, int BK, int NS>
+int launch(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc, hipStream_t st) {
+  auto kern = gemm_bf16_kernel<AK, BKM, ACC, BK, NS>;
+  constexpr int smem = NS * 2 * 256 * BK * 2;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  if (K % BK) return -1;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NTHR), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+// Measured on MI355X (scripts/gemm_bench.py, 8B training shapes, random operands; round 2):
+//   variant 1 (BK=64, 2 stages)      fwd 1.06-1.20 PF, dgrad 0.91-0.97, wgrad 0.71-0.93
+//   BK=32 x 3/4 stages (removed)     fwd 0.82-1.04,    dgrad 0.66-0.73, wgrad 0.60-0.74
+//   variant 2 (software-pipelined)   256 VGPRs + 12-60 B/lane scratch: register-bound as written
+// hipBLASLt on the same shapes: 1.41-1.61 PF (fwd), 1.21-1.50 incl. transposed copies (bwd).
+template <bool AK, bool BKM, bool ACC>
+int launch_variant(int variant, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
+                   long ldc, hipStream_t st) {
+  if (variant == 2) return launch_sp<AK, BKM, ACC>(A, B, C, M, N, K, lda, ldb, ldc, st);
+  return launch<AK, BKM, ACC, 64, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
+}
+
+}  // namespace
+
+// Shape contract (checked here and by the Python wrapper): M % 256 == 0, N % 256 == 0,
+// K % 64 == 0; leading dimensions multiples of 8 elements and 16-B aligned base pointers.
+// a_kmaj / b_kmaj select the k-outer layouts; accumulate adds into C (bf16 read-modify-write).
+static int gemm_variant() {
+  static const int v = [] {
+    const char* e = getenv("RCA_GEMM_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+RCA_API int rca_gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, long long lda, long long ldb,
+                          long long ldc, int a_kmaj, int b_kmaj, int accumulate, hipStream_t st) {
+  if (M % BM || N % BN || K % 64 || M <= 0 || N <= 0 || K <= 0) return -1;
+  if ((lda | ldb | ldc) & 7) return -2;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -2;
+  const int v = gemm_variant();
+#define RCA_G(a, b, c) return launch_variant<a, b, c>(v, A, B, C, M, N, K, lda, ldb, ldc, st)
+  if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G(false, false, true); RCA_G(false, false, false); }
+  if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G(false, true, true); RCA_G(false, true, false); }
+  if (a_kmaj && b_kmaj) { if (accumulate) RCA_G(true, true, true); RCA_G(true, true, false); }
+  if (accumulate) RCA_G(true, false, true);
+  RCA_G(true, false, false);
+#undef RCA_G
+}

@@ -435,3 +435,28 @@ def test_flat_adamw_overlapped_with_forward_matches_serial():
     assert torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
     fl = nets[1][1].flat
     assert fl.grad[fl.zero_start:].abs().max().item() == 0  # zeroed behind the update
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(False, False), (False, True), (True, True), (True, False)])
+def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj):
+    """ops.gemm (hand-written gfx950 MFMA GEMM, LDS-DMA staging, swizzled row / transposed-read
+    operand images, XCD-grouped tile order) vs an fp32 torch reference, all four operand
+    layouts, plain and accumulating epilogues; asymmetric operands (integer-valued rows/cols
+    mixed with noise) so a transposed output or operand cannot pass."""
+    torch.manual_seed(M + N + K)
+    a = torch.randn(K, M, device=DEV) if a_kmaj else torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV) if b_kmaj else torch.randn(N, K, device=DEV)
+    a = (a + torch.arange(a.shape[1], device=DEV) * 0.01).to(torch.bfloat16)
+    b = (b - torch.arange(b.shape[0], device=DEV)[:, None] * 0.003).to(torch.bfloat16)
+    af = a.float().t() if a_kmaj else a.float()
+    bf = b.float() if b_kmaj else b.float().t()
+    ref = af @ bf
+    out = ops.gemm(a, b, a_kmaj, b_kmaj)
+    torch.cuda.synchronize()
+    tol = 2e-2 * ref.abs().max().item()
+    assert (out.float() - ref).abs().max().item() < tol
+    base = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    acc = base.clone()
+    ops.gemm(a, b, a_kmaj, b_kmaj, out=acc, accumulate=True)
+    assert (acc.float() - (ref + base.float())).abs().max().item() < tol
