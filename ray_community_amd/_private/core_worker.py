@@ -83,6 +83,9 @@ class ObjectRef:
         ctx = ser.current_context()
         if ctx is not None:
             ctx.contained.append(self._id)
+        c = _core
+        if c is not None and self._id in c.owned.objs:
+            c.owned.publish(self._id)  # a caller-owned result escapes this process
         return (_rebuild_ref, (self._id,))
 
     # futures / asyncio integration
@@ -168,7 +171,7 @@ class DirectClient:
 
     def __init__(self, head):
         self.head = head
-        self.key = "driver"
+        self.key = "driver"  # this process's holder key at the head
 
     def call(self, method, *args, **kwargs):
         head = self.head
@@ -227,7 +230,7 @@ class DirectClient:
 class SocketClient:
     """Framed RPC client over the head's Unix socket (workers and external drivers)."""
 
-    def __init__(self, sock_path, kind, ident, on_message=None):
+    def __init__(self, sock_path, kind, ident, on_message=None, register_extra=None):
         s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         s.connect(sock_path)
         self.conn = P.Connection(s)
@@ -236,6 +239,7 @@ class SocketClient:
         self._lock = threading.Lock()
         self.on_message = on_message
         self.kind = kind
+        self.key = ("w:" + ident.hex()) if kind == "worker" else ("client:" + ident.hex())
         self._closed = False
         self._adds: List[bytes] = []
         self._removes: List[bytes] = []
@@ -246,7 +250,7 @@ class SocketClient:
             self._pending[0] = f
         self._reader = threading.Thread(target=self._read_loop, name="rca-client-reader", daemon=True)
         self._reader.start()
-        self.conn.send((P.REGISTER, kind, ident, os.getpid()))
+        self.conn.send((P.REGISTER, kind, ident, os.getpid(), register_extra))
         if kind == "client":
             self.hello = f.result(timeout=30)
         self._flusher = threading.Thread(target=self._flush_loop, name="rca-ref-flush", daemon=True)
@@ -359,6 +363,12 @@ class CoreWorker:
         self.assigned_resources = {}
         self.current_actor = None
         self._shutdown = False
+        from .direct_transport import OwnedTable
+
+        self.owned = OwnedTable(self)
+        self.channels: Dict[bytes, Any] = {}
+        self._chan_lock = threading.Lock()
+        self.direct_actor_calls = os.environ.get("RCA_DIRECT_ACTOR_CALLS", "1") != "0"
 
     # -------------------------------------------------------------- reference counting
     def ref_add(self, oid):
@@ -366,6 +376,8 @@ class CoreWorker:
             n = self._refs.get(oid, 0)
             self._refs[oid] = n + 1
         if n == 0:
+            if oid in self.owned.objs and self.owned.revive(oid):
+                return
             self.client.ref_delta((oid,), ())
 
     def ref_remove(self, oid):
@@ -378,6 +390,8 @@ class CoreWorker:
             else:
                 self._refs[oid] = n
         if n == 0:
+            if oid in self.owned.objs and not self.owned.drop(oid):
+                return  # a caller-owned result the head never heard of
             self.client.ref_delta((), (oid,))
 
     def ref_remove_server_pin(self, oid):
@@ -459,7 +473,7 @@ class CoreWorker:
         if not refs:
             return []
         oids = [r._id for r in refs]
-        descs = self.client.call("get", oids, timeout)
+        descs = self._get_descs(oids, timeout)
         out = []
         for oid, d in zip(oids, descs):
             v = self._materialize(oid, d)
@@ -470,8 +484,45 @@ class CoreWorker:
             out.append(v)
         return out[0] if single else out
 
+    def _get_descs(self, oids, timeout):
+        """Descriptors for ``oids``: caller-owned results from the local table (no head round
+        trip), the rest from the head."""
+        owned = self.owned.objs
+        local = [o for o in oids if o in owned]
+        if not local:
+            return self.client.call("get", oids, timeout)
+        deadline = None if timeout is None else time.monotonic() + timeout
+        remote = [o for o in oids if o not in owned]
+        got = {}
+        if remote:
+            for o, d in zip(remote, self.client.call("get", remote, timeout)):
+                got[o] = d
+        blocking = self.mode == "worker" and any(owned.get(o) is not None and owned[o].desc is None for o in local)
+        if blocking:
+            self.client.send((P.BLOCKED, True))
+        try:
+            for o, d in zip(local, self.owned.wait_descs(local, deadline)):
+                got[o] = d
+        finally:
+            if blocking:
+                self.client.send((P.BLOCKED, False))
+        return [got[o] for o in oids]
+
     def as_future(self, ref) -> concurrent.futures.Future:
         out = concurrent.futures.Future()
+        if ref._id in self.owned.objs:
+            def ready(d, oid=ref._id):
+                try:
+                    v = self._materialize(oid, d)
+                    if isinstance(v, _ErrorValue):
+                        out.set_exception(v.as_exception())
+                    else:
+                        out.set_result(v)
+                except BaseException as e:  # noqa
+                    out.set_exception(e)
+
+            self.owned.on_ready(ref._id, ready)
+            return out
         f = self.client.call_async("get", [ref._id], None)
 
         def done(fut):
@@ -499,7 +550,15 @@ class CoreWorker:
             raise ValueError("Invalid number of objects to return %d." % num_returns)
         if num_returns > len(refs):
             raise ValueError("num_returns cannot be greater than the number of objects provided.")
-        got = self.client.call("wait", ids, num_returns, timeout, fetch_local)
+        owned = self.owned.objs
+        local = [o for o in ids if o in owned]
+        if local and len(local) == len(ids):
+            deadline = None if timeout is None else time.monotonic() + timeout
+            got = self.owned.wait_ready(ids, num_returns, deadline)
+        else:
+            for o in local:  # mixed with head-managed refs: let the head track them all
+                self.owned.publish(o)
+            got = self.client.call("wait", ids, num_returns, timeout, fetch_local)
         if len(got) > num_returns:
             got = got[:num_returns]
         rs = set(got)
@@ -554,10 +613,48 @@ class CoreWorker:
         trace = tracing.submission_context()
         if trace is not None:
             spec["trace"] = trace
+        owned = self.owned.objs
+        for a in spec["args"]:
+            if a[0] == "r" and a[1] in owned:
+                self.owned.publish(a[1])  # the head schedules this task: it must know its inputs
         self.client.submit(spec)
+
+    def submit_actor_task(self, spec, deps):
+        """Actor calls go straight to the actor's worker (``direct_transport.ActorChannel``);
+        generator methods keep the head-routed path."""
+        if not self.direct_actor_calls or spec.get("generator") is not None:
+            return self.submit_spec(spec, deps)
+        spec["parent"] = self.ctx.task_id
+        spec["caller_node"] = self.node_id
+        spec["owner_key"] = self.client.key
+        trace = tracing.submission_context()
+        if trace is not None:
+            spec["trace"] = trace
+        aid = spec["actor_id"]
+        ch = self.channels.get(aid)
+        if ch is None:
+            from .direct_transport import ActorChannel
+
+            with self._chan_lock:
+                ch = self.channels.get(aid)
+                if ch is None:
+                    ch = ActorChannel(self, aid)
+                    self.channels[aid] = ch
+        ch.submit(spec, list(deps))
+
+    def cancel(self, oid, force=False, recursive=True):
+        e = self.owned.objs.get(oid)
+        if e is not None:
+            if e.desc is not None or e.channel is None:
+                return False
+            return e.channel.cancel(e.tid, force)
+        return self.client.call("cancel", oid, force, recursive)
 
     def shutdown(self):
         self._shutdown = True
+        for ch in list(self.channels.values()):
+            ch.close()
+        self.channels.clear()
 
 
 class _ErrorValue:

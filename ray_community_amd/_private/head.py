@@ -145,6 +145,7 @@ class ActorState:
         self.creation_task: Optional[TaskState] = None
         self.pid = None
         self.killed = False
+        self.addr_waiters: List[tuple] = []  # (Deferred, min incarnation) of direct-call channels
 
 
 class WorkerState:
@@ -166,6 +167,7 @@ class WorkerState:
         self.dead = False
         self.gpu_objects: Set[bytes] = set()
         self.out = collections.deque()
+        self.direct_addr: Optional[str] = None
 
 
 class NodeState:
@@ -218,6 +220,8 @@ class Head:
         self.functions: Dict[bytes, bytes] = {}
         self.events: collections.deque = collections.deque(maxlen=int(self.config.get("task_events_max", 100000)))
         self.finished_tasks: collections.deque = collections.deque(maxlen=10000)
+        # records of directly transported actor calls (state API / timeline), batched by workers
+        self.direct_tasks: collections.deque = collections.deque(maxlen=int(self.config.get("direct_task_records", 10000)))
         self.timers: List[tuple] = []
         self.spilled_bytes = 0
         self.num_spilled = 0
@@ -396,6 +400,8 @@ class Head:
             self._on_gen_item(msg[1], msg[2], msg[3])
         elif t == P.BLOCKED:
             self._on_blocked(cc.worker, msg[1])
+        elif t == P.DIRECT_EVENTS:
+            self._on_direct_events(cc.worker, msg[1])
         elif t == P.REGISTER:
             self._on_register(cc, msg)
         elif t == P.LOG:
@@ -411,6 +417,8 @@ class Head:
             cc.worker = w
             self.start_failures = 0
             w.conn = cc.conn
+            extra = msg[4] if len(msg) > 4 and isinstance(msg[4], dict) else {}
+            w.direct_addr = extra.get("direct_addr")
             w.pid = pid
             w.state = "idle"
             node = self.nodes[w.node_id]
@@ -642,7 +650,7 @@ class Head:
                 pass
 
     # -------------------------------------------------------------- get / wait
-    def rpc_get(self, caller, oids, timeout=None):
+    def rpc_get(self, caller, oids, timeout=None, _block=True):
         d = Deferred()
         remaining = {o for o in oids}
         for oid in oids:
@@ -666,7 +674,8 @@ class Head:
         if timeout is not None and not d.done:
             self._add_timer(timeout, lambda: d.resolve(exc.GetTimeoutError(
                 f"Get timed out: some object(s) not ready after {timeout}s."), ok=False))
-        self._maybe_block(caller, d)
+        if _block:
+            self._maybe_block(caller, d)
         return d
 
     def _maybe_block(self, caller, d):
@@ -1191,6 +1200,7 @@ class Head:
                 for d in a.ready_waiters:
                     d.resolve(True)
                 a.ready_waiters = []
+                self._flush_addr_waiters(a)
                 self._pump_actor(a)
             return
         if kind == "actor_task":
@@ -1383,18 +1393,23 @@ class Head:
         w = self.workers.get(a.worker)
         if w is None or w.dead:
             return
-        while a.queue:
-            ts = a.queue[0]
+        # per-caller order: a call with unresolved dependencies holds back only the LATER calls
+        # of the same caller; other callers' calls proceed
+        blocked = set()
+        rest = collections.deque()
+        q = a.queue
+        while q:
+            ts = q.popleft()
             if ts.cancelled:
-                a.queue.popleft()
                 continue
-            if ts.deps:
-                # keep submission order: later calls wait behind an unresolved earlier call
-                return
-            a.queue.popleft()
+            if ts.deps or ts.owner in blocked:
+                blocked.add(ts.owner)
+                rest.append(ts)
+                continue
             a.inflight[ts.tid] = ts
             ts.node = a.node
             self._dispatch_actor_task(w, ts)
+        a.queue = rest
 
     def _dispatch_actor_task(self, w, ts):
         spec = ts.spec
@@ -1462,6 +1477,7 @@ class Head:
             for d in a.ready_waiters:
                 d.resolve(exc.ActorDiedError(a.aid, self._actor_death_msg(a)), ok=False)
             a.ready_waiters = []
+            self._flush_addr_waiters(a)
 
     def _actor_death_msg(self, a):
         if a is None:
@@ -1531,6 +1547,79 @@ class Head:
         else:
             a.ready_waiters.append(d)
         return d
+
+    # -------------------------------------------------------------- direct actor calls
+    def rpc_actor_address(self, caller, aid, min_incarnation=0):
+        """Direct-call endpoint of an actor: resolves to (socket path, incarnation) once the actor
+        is ALIVE in an incarnation >= ``min_incarnation`` (a caller whose stream broke asks for
+        the next one), or fails with ActorDiedError once it is dead for good."""
+        d = Deferred()
+        a = self.actors.get(aid)
+        if a is None:
+            d.resolve(exc.ActorDiedError(aid, "The actor is dead (unknown actor)."), ok=False)
+            return d
+        a.addr_waiters.append((d, min_incarnation))
+        self._flush_addr_waiters(a)
+        return d
+
+    def _flush_addr_waiters(self, a):
+        if not a.addr_waiters:
+            return
+        keep = []
+        for d, inc in a.addr_waiters:
+            if d.done:
+                continue
+            if a.state == A_DEAD:
+                d.resolve(exc.ActorDiedError(a.aid, self._actor_death_msg(a)), ok=False)
+                continue
+            w = self.workers.get(a.worker) if a.worker else None
+            if a.state == A_ALIVE and a.num_restarts >= inc and w is not None and not w.dead and w.direct_addr:
+                d.resolve((w.direct_addr, a.num_restarts))
+            else:
+                keep.append((d, inc))
+        a.addr_waiters = keep
+
+    def rpc_object_descs(self, caller, oids):
+        """Descriptors of ``oids`` once all are ready (like ``get`` but without lending the
+        caller's CPU: a direct-call submitter resolving the arguments of a queued call)."""
+        return self.rpc_get(caller, oids, None, _block=False)
+
+    def rpc_declare_object(self, caller, oid):
+        """A caller-owned (direct-call) result whose ref escaped before its value arrived."""
+        e = self._obj(oid)
+        e.holders.add(caller)
+        return True
+
+    def rpc_put_owned(self, caller, items, owner_key):
+        """An actor worker registers direct-call results the head must manage (shm, GPU, nested
+        refs) on behalf of the calling process ``owner_key`` before replying to it."""
+        gpu_owner = bytes.fromhex(caller[2:]) if caller.startswith("w:") else None
+        w = self.workers.get(gpu_owner) if gpu_owner else None
+        for oid, desc, contained, is_gpu, flags in items:
+            e = self._obj(oid)
+            e.holders.add(owner_key)
+            owner = None
+            if is_gpu and w is not None:
+                owner = gpu_owner
+                w.gpu_objects.add(oid)
+            self._set_ready(e, tuple(desc), contained, owner, flags)
+        return True
+
+    def rpc_actor_exit(self, caller):
+        """``exit_actor()`` / ``__ray_terminate__`` inside a directly called actor."""
+        w = self.workers.get(bytes.fromhex(caller[2:])) if caller.startswith("w:") else None
+        if w is not None and w.actor is not None:
+            self._kill_actor(w.actor, no_restart=True, reason="exit_actor() called", graceful=True)
+        return True
+
+    def _on_direct_events(self, w, records):
+        pid = w.pid if w is not None else None
+        node = w.node_id if w is not None else None
+        wid = w.wid if w is not None else None
+        for tid, name, aid, start, end, failed, etype in records:
+            self.direct_tasks.append((tid, name, aid, start, end, failed, etype, wid, node))
+            self.events.append((start, tid, "running", name, pid, node))
+            self.events.append((end, tid, "failed" if failed else "finished", name, pid, node))
 
     def rpc_actor_info(self, caller, aid):
         a = self.actors.get(aid)
@@ -1750,7 +1839,13 @@ class Head:
                         "start_time_ms": int(ts.times.get("start", 0) * 1000),
                         "end_time_ms": int(ts.times.get("end", 0) * 1000),
                         "func_or_class_name": ts.spec.get("name")})
-        return out
+        for tid, name, aid, start, end, failed, etype, wid, node in list(self.direct_tasks)[-limit:]:
+            out.append({"task_id": tid.hex(), "name": name, "state": "FAILED" if failed else "FINISHED",
+                        "type": "ACTOR_TASK", "node_id": node, "worker_id": wid.hex() if wid else None,
+                        "actor_id": aid.hex() if aid else None, "required_resources": {}, "error_type": etype,
+                        "attempt_number": 0, "start_time_ms": int(start * 1000), "end_time_ms": int(end * 1000),
+                        "func_or_class_name": name})
+        return out[-limit:]
 
     def rpc_list_actors(self, caller):
         out = []

@@ -28,6 +28,12 @@ EXIT = 22
 CANCEL = 23        # (CANCEL, task_id, force)
 FREE_GPU = 24      # (FREE_GPU, [object_ids])
 PING = 25
+# worker -> head: batched records of directly transported actor calls
+DIRECT_EVENTS = 30  # (DIRECT_EVENTS, [(tid, name, actor_id, start, end, failed, error_type)])
+# caller <-> actor worker (direct transport, _private/direct_transport.py)
+DEXEC = 40         # (DEXEC, task_spec_dict)              caller -> actor worker
+DDONE = 41         # (DDONE, task_id, [desc], head_managed) actor worker -> caller
+DCANCEL = 42       # (DCANCEL, task_id, force)             caller -> actor worker
 
 
 def dumps(msg) -> bytes:

@@ -272,13 +272,17 @@ def cancel(object_ref, *, force: bool = False, recursive: bool = True):
         object_ref = object_ref._main
     if not isinstance(object_ref, ObjectRef):
         raise TypeError("cancel() only supports ObjectRefs")
-    return _core().client.call("cancel", object_ref._id, force, recursive)
+    return _core().cancel(object_ref._id, force, recursive)
 
 
 def free(object_refs, local_only=False):
     if isinstance(object_refs, ObjectRef):
         object_refs = [object_refs]
-    _core().client.call("free", [r._id for r in object_refs])
+    core = _core()
+    for r in object_refs:
+        if r._id in core.owned.objs:
+            core.owned.publish(r._id)
+    core.client.call("free", [r._id for r in object_refs])
 
 
 # ---------------------------------------------------------------------------------- cluster

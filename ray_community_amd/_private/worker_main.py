@@ -90,7 +90,12 @@ class Worker:
         self.asem = None
         self.running = {}  # tid -> thread ident
         self.exiting = False
-        self.client = SocketClient(env["RCA_HEAD_SOCK"], "worker", self.wid, on_message=self._on_message)
+        from .direct_transport import DirectServer
+
+        # direct-call endpoint: callers of an actor hosted here push their calls to this socket
+        self.direct = DirectServer(self, env.get("RCA_SESSION_DIR", ""), self.wid)
+        self.client = SocketClient(env["RCA_HEAD_SOCK"], "worker", self.wid, on_message=self._on_message,
+                                   register_extra={"direct_addr": self.direct.path})
         self.store = ObjectStore(env["RCA_STORE"])
         self.core = CoreWorker("worker", self.client, self.store, env["RCA_NODE_ID"], bytes.fromhex(env["RCA_JOB_ID"]),
                                env.get("RCA_NAMESPACE", ""), worker_id=self.wid, session_dir=env.get("RCA_SESSION_DIR", ""))
@@ -107,13 +112,7 @@ class Worker:
     def _on_message(self, msg):
         t = msg[0]
         if t == P.EXECUTE:
-            spec = msg[1]
-            if self.aloop is not None and spec["kind"] == "actor_task":
-                asyncio.run_coroutine_threadsafe(self._run_async(spec), self.aloop)
-            elif self.pool is not None and spec["kind"] == "actor_task":
-                self.pool.submit(self._execute, spec)
-            else:
-                self.inbox.put(spec)
+            self._dispatch_spec(msg[1])
         elif t == P.EXIT:
             self.exiting = True
             self.inbox.put(None)
@@ -121,6 +120,40 @@ class Worker:
             self._cancel(msg[1], msg[2])
         elif t == P.FREE_GPU:
             self.core.free_gpu_objects(msg[1])
+
+    def _dispatch_spec(self, spec):
+        """Route a task (from the head, or a direct actor call) to its executor."""
+        if self.aloop is not None and spec["kind"] == "actor_task":
+            asyncio.run_coroutine_threadsafe(self._run_async(spec), self.aloop)
+        elif self.pool is not None and spec["kind"] == "actor_task":
+            self.pool.submit(self._execute, spec)
+        else:
+            self.inbox.put(spec)
+
+    def _finish(self, spec, results, info, t_start):
+        """Report a finished task: to the head, or -- for a direct actor call -- to the caller."""
+        if info.get("actor_exit"):
+            self.actor_exited = True
+        conn = spec.get("_reply")
+        tid = spec["tid"]
+        if conn is None:
+            self.client.send((P.TASK_DONE, tid, results, info))
+            return
+        # results the head has to manage (shm / GPU / nested refs) are registered before replying
+        head_managed = any(r[0] != "inline" or r[3] or r[5] for r in results)
+        if head_managed:
+            self.client.call("put_owned", [(rid, r[0:3], r[3], r[5], r[4]) for rid, r in
+                                           zip(spec["return_ids"], results)], spec["owner_key"])
+        try:
+            conn.send((P.DDONE, tid, [(r[0], r[1], r[2], r[4]) for r in results], head_managed))
+        except OSError:
+            pass
+        if info.get("spans"):
+            self.client.call_async("add_spans", info["spans"])
+        self.direct.record(spec, t_start, time.time(), info)
+        if info.get("actor_exit"):
+            self.direct.flush()
+            self.client.call_async("actor_exit")
 
     def _cancel(self, tid, force):
         if force:
@@ -144,9 +177,11 @@ class Worker:
 
     def _exit(self):
         try:
+            self.direct.flush()
             self.client.flush_refs()
         except Exception:
             pass
+        self.direct.close()
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(0)
@@ -189,6 +224,7 @@ class Worker:
     def _execute(self, spec):
         tid = spec["tid"]
         kind = spec["kind"]
+        t_start = time.time()
         self._set_ctx(spec)
         self.running[tid] = threading.get_ident()
         info = {}
@@ -202,7 +238,7 @@ class Worker:
         spans = tracing.drain()
         if spans:
             info["spans"] = spans
-        self.client.send((P.TASK_DONE, tid, results, info))
+        self._finish(spec, results, info, t_start)
         self._keepalive = None
         self._value_keepalive.pop(tid, None)
 
@@ -220,6 +256,10 @@ class Worker:
                     value = None
                 elif kind == "actor_task":
                     method = spec["method"]
+                    if getattr(self, "actor_exited", False):
+                        # calls queued behind exit_actor() / __ray_terminate__ never run
+                        raise _DepError(exc.ActorDiedError(self.core.actor_id, "The actor exited (exit_actor() "
+                                                                               "or __ray_terminate__)."))
                     if method == "__ray_terminate__":
                         raise _ActorExit()
                     if method == "__ray_ready__":
@@ -350,6 +390,9 @@ class Worker:
             t_start = time.time()
             info = {}
             try:
+                if getattr(self, "actor_exited", False):
+                    raise _DepError(exc.ActorDiedError(self.core.actor_id, "The actor exited (exit_actor() "
+                                                                           "or __ray_terminate__)."))
                 args, kwargs = self._resolve_args(spec)
                 method = spec["method"]
                 if method == "__ray_terminate__":
@@ -403,7 +446,7 @@ class Worker:
             spans = tracing.drain()
             if spans:
                 info["spans"] = spans
-            self.client.send((P.TASK_DONE, tid, results, info))
+            self._finish(spec, results, info, t_start)
 
 
 class _DepError(Exception):
@@ -430,6 +473,10 @@ def _is_exit_actor(e):
 
 
 def main():
+    import faulthandler
+    import signal
+
+    faulthandler.register(signal.SIGUSR1, all_threads=True)  # stack dump of a stuck worker: kill -USR1 <pid>
     from .gc_tuning import tune_gc
 
     tune_gc()

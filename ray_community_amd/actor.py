@@ -260,7 +260,7 @@ class ActorHandle:
         with core._ref_lock:
             for r in rids:
                 core._refs[r] = core._refs.get(r, 0) + 1
-        core.submit_spec(spec, deps)
+        core.submit_actor_task(spec, deps)
         if generator == "streaming":
             return ObjectRefGenerator(tid, refs[0])
         if nret == 0:

@@ -220,3 +220,112 @@ def test_actor_gpu_assignment_without_gpus(ray_start_regular):
 def test_ready(ray_start_regular):
     c = Counter.remote()
     assert ray.get(c.__ray_ready__.remote()) is True
+
+
+# ----------------------------------------------------------------------------- direct transport
+def test_per_caller_ordering_with_unresolved_dependency(ray_start_regular):
+    """An earlier call with an unresolved ObjectRef argument holds back only the same caller's
+    later calls (submission order kept); another caller's calls are not blocked behind it."""
+
+    @ray.remote
+    class Log:
+        def __init__(self):
+            self.seen = []
+
+        def add(self, tag, *_dep):
+            self.seen.append(tag)
+            return tag
+
+        def seen_list(self):
+            return list(self.seen)
+
+    @ray.remote
+    def slow(x):
+        time.sleep(1.5)
+        return x
+
+    @ray.remote
+    def other_caller(log):
+        return ray.get(log.add.remote("B1"))
+
+    log = Log.remote()
+    ray.get(log.seen_list.remote())
+    dep = slow.remote(0)
+    a1 = log.add.remote("A1", dep)   # blocked on dep
+    a2 = log.add.remote("A2")        # same caller: must run after A1
+    t0 = time.time()
+    assert ray.get(other_caller.remote(log)) == "B1"  # different caller: not blocked by A1
+    assert time.time() - t0 < 1.3
+    assert ray.get([a1, a2]) == ["A1", "A2"]
+    seen = ray.get(log.seen_list.remote())
+    assert seen.index("B1") < seen.index("A1") < seen.index("A2")
+
+
+def test_direct_results_escape_to_tasks_and_puts(ray_start_regular):
+    """Caller-owned results of direct actor calls passed on (as task args, nested in a put, in
+    wait() mixed with head-managed refs) are published to the head transparently."""
+    c = Counter.remote(100)
+
+    @ray.remote
+    def plus(x, y):
+        return x + y
+
+    @ray.remote
+    def unwrap(lst):
+        return ray.get(lst[0])
+
+    r = c.inc.remote()           # pending while we pass it on
+    assert ray.get(plus.remote(r, 1)) == 102
+    nested = ray.put([c.inc.remote()])
+    assert ray.get(unwrap.remote(nested)) == 102
+    r2 = c.inc.remote()
+    p = plus.remote(1, 2)
+    ready, _ = ray.wait([r2, p], num_returns=2, timeout=30)
+    assert len(ready) == 2 and ray.get(r2) == 103
+
+
+def test_direct_call_retried_after_actor_restart(ray_start_regular):
+    """The stream to a restarting actor breaks: in-flight calls with max_task_retries are re-sent
+    to the new incarnation, calls without retries fail with ActorDiedError."""
+
+    @ray.remote(max_restarts=1, max_task_retries=1)
+    class Flaky:
+        def __init__(self):
+            self.calls = 0
+
+        def pid(self):
+            return os.getpid()
+
+        def die_once(self, marker):
+            if not os.path.exists(marker):
+                open(marker, "w").close()
+                os._exit(1)
+            return "survived"
+
+    import tempfile
+
+    marker = os.path.join(tempfile.mkdtemp(), "m")
+    f = Flaky.remote()
+    pid0 = ray.get(f.pid.remote())
+    assert ray.get(f.die_once.remote(marker), timeout=60) == "survived"
+    assert ray.get(f.pid.remote()) != pid0
+    g = Flaky.options(max_task_retries=0).remote()
+    marker2 = os.path.join(tempfile.mkdtemp(), "m")
+    with pytest.raises(exc.RayActorError):
+        ray.get(g.die_once.remote(marker2), timeout=60)
+
+
+def test_direct_calls_visible_in_state_api_and_timeline(ray_start_regular):
+    from ray_community_amd.util import state
+
+    c = Counter.remote()
+    ray.get([c.inc.remote() for _ in range(5)])
+    deadline = time.time() + 10
+    names = []
+    while time.time() < deadline:
+        names = [t["name"] for t in state.list_tasks() if t["type"] == "ACTOR_TASK"]
+        if names.count("Counter.inc") >= 5:
+            break
+        time.sleep(0.2)
+    assert names.count("Counter.inc") >= 5
+    assert any(e["name"] == "Counter.inc" for e in ray.timeline())
