@@ -357,7 +357,6 @@ class CoreWorker:
         self._ref_lock = threading.Lock()
         self.ctx = TaskContext()
         self.registered_functions = set()
-        self.gpu_pins: Dict[bytes, list] = {}
         self.actor_id = None
         self.gpu_ids = ()
         self.assigned_resources = {}
@@ -402,7 +401,20 @@ class CoreWorker:
         return self._refs.get(oid, 0)
 
     # -------------------------------------------------------------- objects
-    def _store_serialized(self, oid, s: ser.Serialized):
+    def gpu_info(self, oid):
+        """HBM accounting record of a GPU object this process owns (None for host objects)."""
+        from .gpu_store import local_store
+
+        return local_store().info(oid)
+
+    def _store_serialized(self, oid, s: ser.Serialized, copy_gpu: bool = True):
+        if s.gpu_tensors:
+            # CUDA tensors stay in HBM, owned by this process's GPU object store; the wire bytes
+            # (host parts + IPC export table) travel inline
+            from .gpu_store import local_store
+
+            b = local_store().add(oid, s, copy=copy_gpu and os.environ.get("RCA_GPU_PUT_COPY", "1") != "0")
+            return ("inline", b, len(b))
         if s.total_size <= INLINE_THRESHOLD:
             b = s.to_bytes()
             return ("inline", b, len(b))
@@ -424,19 +436,32 @@ class CoreWorker:
             raise TypeError("Calling put() on an ObjectRef is not allowed.")
         oid = new_id()
         s = ser.serialize(value)
+        is_gpu = bool(s.gpu_tensors)
         desc = self._store_serialized(oid, s)
-        if s.gpu_tensors:
-            self.gpu_pins[oid] = s.gpu_tensors
         ref = ObjectRef(oid, _register=False)
         with self._ref_lock:
             self._refs[oid] = self._refs.get(oid, 0) + 1
-        self.client.call("put", oid, desc, s.contained, bool(s.gpu_tensors), s.flags) if self.mode != "driver" else \
-            self.client.call("put", oid, desc, s.contained, bool(s.gpu_tensors), s.flags)
+        self.client.call("put", oid, desc, s.contained, self.gpu_info(oid) if is_gpu else False, s.flags)
         return ref
 
     def free_gpu_objects(self, oids):
-        for o in oids:
-            self.gpu_pins.pop(o, None)
+        from .gpu_store import local_store
+
+        local_store().free(oids)
+
+    def gpu_command(self, cmd, oids):
+        """The head asks this owner to spill GPU objects to pinned host memory or restore them."""
+        from .gpu_store import local_store
+
+        st = local_store()
+        if cmd == "spill":
+            done = [o for o in oids if st.spill(o)]
+            self.client.call_async("gpu_spilled", done)
+        elif cmd == "restore":
+            for o in oids:
+                b = st.restore(o)
+                self.client.call_async("gpu_restored", o, ("inline", b, len(b)) if b is not None else None,
+                                       self.gpu_info(o))
 
     def _materialize(self, oid, desc):
         kind, data, size, flags = desc
@@ -506,14 +531,34 @@ class CoreWorker:
         finally:
             if blocking:
                 self.client.send((P.BLOCKED, False))
+        # GPU objects are managed by the head (spill / restore / owner death): ask it
+        gpu = [o for o in local if got[o][3] & ser.FLAG_GPU]
+        if gpu:
+            rem = None if deadline is None else max(0.0, deadline - time.monotonic())
+            for o, d in zip(gpu, self.client.call("get", gpu, rem)):
+                got[o] = d
         return [got[o] for o in oids]
 
     def as_future(self, ref) -> concurrent.futures.Future:
         out = concurrent.futures.Future()
         if ref._id in self.owned.objs:
             def ready(d, oid=ref._id):
+                if d[3] & ser.FLAG_GPU:  # GPU objects: current descriptor from the head
+                    g = self.client.call_async("get", [oid], None)
+                    g.add_done_callback(lambda f: _finish(f, oid))
+                    return
                 try:
                     v = self._materialize(oid, d)
+                    if isinstance(v, _ErrorValue):
+                        out.set_exception(v.as_exception())
+                    else:
+                        out.set_result(v)
+                except BaseException as e:  # noqa
+                    out.set_exception(e)
+
+            def _finish(f, oid):
+                try:
+                    v = self._materialize(oid, f.result()[0])
                     if isinstance(v, _ErrorValue):
                         out.set_exception(v.as_exception())
                     else:
@@ -582,7 +627,7 @@ class CoreWorker:
                 continue
             s = ser.serialize(a)
             if s.gpu_tensors:
-                # GPU tensors passed by value become GPU objects owned by this process
+                # GPU tensors passed by value become GPU objects owned by this process (snapshot)
                 ref = self._put_serialized(s)
                 out.append(("r", ref._id))
                 deps.append(ref)
@@ -598,13 +643,12 @@ class CoreWorker:
 
     def _put_serialized(self, s):
         oid = new_id()
+        is_gpu = bool(s.gpu_tensors)
         desc = self._store_serialized(oid, s)
-        if s.gpu_tensors:
-            self.gpu_pins[oid] = s.gpu_tensors
         ref = ObjectRef(oid, _register=False)
         with self._ref_lock:
             self._refs[oid] = self._refs.get(oid, 0) + 1
-        self.client.call("put", oid, desc, s.contained, bool(s.gpu_tensors), s.flags)
+        self.client.call("put", oid, desc, s.contained, self.gpu_info(oid) if is_gpu else False, s.flags)
         return ref
 
     def submit_spec(self, spec, deps=()):

@@ -261,6 +261,8 @@ class ActorChannel:
                 continue
             oid = a[1]
             e = self.core.owned.get_entry(oid)
+            if e is not None and e.desc is not None and e.desc[3] & ser.FLAG_GPU:
+                e = None  # GPU objects: the head hands out current descriptors (spill / restore)
             if e is not None:
                 if e.desc is not None:
                     args[i] = ("d", oid, e.desc)
@@ -270,25 +272,32 @@ class ActorChannel:
             else:
                 head_ids.append((i, oid))
         if head_ids:
+            self._resolve_at_head(call, head_ids)
+
+    def _resolve_at_head(self, call, head_ids):
+        with self.lock:
             call.unresolved += 1
-            fut = self.core.client.call_async("object_descs", [o for _, o in head_ids])
+        fut = self.core.client.call_async("object_descs", [o for _, o in head_ids])
 
-            def done(f, call=call, head_ids=head_ids):  # runs on the _bg pool, never the head thread
-                try:
-                    descs = f.result()
-                except BaseException as e:  # noqa
-                    descs = [error_desc(e if isinstance(e, exc.RayError) else exc.RaySystemError(str(e)))] * len(head_ids)
-                with self.lock:
-                    for (i, oid), d in zip(head_ids, descs):
-                        call.resolved_args[i] = ("d", oid, d)
-                    call.unresolved -= 1
-                self._pump_locked()
+        def done(f, call=call, head_ids=head_ids):  # runs on the _bg pool, never the head thread
+            try:
+                descs = f.result()
+            except BaseException as e:  # noqa
+                descs = [error_desc(e if isinstance(e, exc.RayError) else exc.RaySystemError(str(e)))] * len(head_ids)
+            with self.lock:
+                for (i, oid), d in zip(head_ids, descs):
+                    call.resolved_args[i] = ("d", oid, d)
+                call.unresolved -= 1
+            self._pump_locked()
 
-            fut.add_done_callback(lambda f, done=done: _bg(done, f))
+        fut.add_done_callback(lambda f, done=done: _bg(done, f))
 
     def _dep_done(self, call, i, oid, desc):
+        if desc[3] & ser.FLAG_GPU:  # a GPU result: fetch its current descriptor from the head
+            self._resolve_at_head(call, [(i, oid)])
         with self.lock:
-            call.resolved_args[i] = ("d", oid, desc)
+            if not desc[3] & ser.FLAG_GPU:
+                call.resolved_args[i] = ("d", oid, desc)
             call.unresolved -= 1
         _bg(self._pump_locked)
 

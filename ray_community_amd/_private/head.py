@@ -77,7 +77,7 @@ class Deferred:
 
 class ObjEntry:
     __slots__ = ("oid", "state", "desc", "holders", "pins", "waiters", "contained", "task", "gpu_owner", "size",
-                 "flags", "created")
+                 "flags", "created", "gpu")
 
     def __init__(self, oid, task=None):
         self.oid = oid
@@ -92,6 +92,7 @@ class ObjEntry:
         self.size = 0
         self.flags = 0
         self.created = time.time()
+        self.gpu = None  # GPU object accounting: {"nbytes", "gpus", "state", "last", "maps": {reader: n}}
 
 
 class TaskState:
@@ -228,6 +229,14 @@ class Head:
         self.num_restored = 0
         self.driver_gpu_objects: Set[bytes] = set()
         self.driver_free_gpu_cb = None
+        self.driver_gpu_cmd_cb = None
+        # GPU object store accounting (per physical GPU), see _private/gpu_store.py
+        self.gpu_budget = int(self.config.get("gpu_object_store_memory") or _default_gpu_budget())
+        self.gpu_usage: Dict[str, int] = {}
+        self.gpu_objects: Dict[bytes, ObjEntry] = {}
+        self.gpu_spilled_bytes = 0
+        self.gpu_num_spilled = 0
+        self.gpu_num_restored = 0
         self.driver_task_cancel_cb = None
         self.shutting_down = False
         from .memory_monitor import MemoryMonitor
@@ -515,6 +524,7 @@ class Head:
                 except OSError:
                     pass
         if e.gpu_owner is not None:
+            self._gpu_unaccount(e)
             self._free_gpu_object(e.gpu_owner, e.oid)
         e.desc = None
         for c in e.contained:
@@ -533,6 +543,8 @@ class Head:
 
     def _drop_holder_everywhere(self, key):
         for e in list(self.objects.values()):
+            if e.gpu is not None:
+                e.gpu["maps"].pop(key, None)
             if key in e.holders:
                 e.holders.discard(key)
                 self._maybe_free(e)
@@ -542,9 +554,11 @@ class Head:
                 hs.discard(key)
                 self._maybe_kill_unreferenced(a)
 
-    def _set_ready(self, e: ObjEntry, desc, contained=(), gpu_owner=None, flags=0):
+    def _set_ready(self, e: ObjEntry, desc, contained=(), gpu_owner=None, flags=0, gpu_info=None):
         if e.state == FREED:
             return
+        if gpu_owner is not None and isinstance(gpu_info, dict):
+            self._gpu_account(e, gpu_info)
         e.desc = desc
         e.flags = flags
         e.size = desc[2] or 0
@@ -586,6 +600,11 @@ class Head:
         if d[0] == "spill" and self.config.get("restore_spilled", True):
             self._restore(e)
             d = e.desc
+        g = e.gpu
+        if g is not None:
+            g["last"] = time.time()
+            if caller != self._gpu_owner_key(e):  # the reader maps the owner's HBM until it unmaps
+                g["maps"][caller] = g["maps"].get(caller, 0) + 1
         return (d[0], d[1], d[2], e.flags)
 
     # -------------------------------------------------------------- put
@@ -601,8 +620,124 @@ class Head:
                 w = self.workers.get(owner)
                 if w is not None:
                     w.gpu_objects.add(oid)
-        self._set_ready(e, tuple(desc), contained, owner, flags)
+        self._set_ready(e, tuple(desc), contained, owner, flags, gpu_info=is_gpu)
         return True
+
+    # -------------------------------------------------------------- GPU object store (HBM budget)
+    def _gpu_owner_key(self, e):
+        o = e.gpu_owner
+        return None if o is None else (DRIVER if o == DRIVER else "w:" + o.hex())
+
+    def _gpu_account(self, e, info):
+        e.gpu = {"nbytes": int(info.get("nbytes", 0)), "gpus": list(info.get("gpus") or ["0"]), "state": "hbm",
+                 "last": time.time(), "maps": {}, "counted": True}
+        self.gpu_objects[e.oid] = e
+        share = e.gpu["nbytes"] // max(1, len(e.gpu["gpus"]))
+        for g in e.gpu["gpus"]:
+            self.gpu_usage[g] = self.gpu_usage.get(g, 0) + share
+        for g in e.gpu["gpus"]:
+            self._gpu_enforce_budget(g)
+
+    def _gpu_unaccount(self, e):
+        g = e.gpu
+        if g is None:
+            return
+        self.gpu_objects.pop(e.oid, None)
+        if g["counted"]:
+            share = g["nbytes"] // max(1, len(g["gpus"]))
+            for d in g["gpus"]:
+                self.gpu_usage[d] = max(0, self.gpu_usage.get(d, 0) - share)
+        e.gpu = None
+
+    def _gpu_enforce_budget(self, gpu):
+        budget = self.gpu_budget
+        if not budget or self.gpu_usage.get(gpu, 0) <= budget:
+            return
+        over = self.gpu_usage[gpu] - budget
+        # least recently used, not mapped by any reader, resident on this GPU
+        cands = sorted((e for e in self.gpu_objects.values() if e.gpu["state"] == "hbm" and gpu in e.gpu["gpus"]
+                        and e.state == READY and not any(e.gpu["maps"].values())), key=lambda e: e.gpu["last"])
+        by_owner: Dict[Any, List[bytes]] = {}
+        for e in cands:
+            if over <= 0:
+                break
+            e.gpu["state"] = "spilling"
+            by_owner.setdefault(e.gpu_owner, []).append(e.oid)
+            over -= e.gpu["nbytes"] // max(1, len(e.gpu["gpus"]))
+        for owner, oids in by_owner.items():
+            self._gpu_command(owner, "spill", oids)
+
+    def _gpu_command(self, owner, cmd, oids):
+        if owner == DRIVER:
+            if self.driver_gpu_cmd_cb is not None:
+                threading.Thread(target=self.driver_gpu_cmd_cb, args=(cmd, oids), daemon=True).start()
+            return
+        w = self.workers.get(owner)
+        if w is not None and not w.dead:
+            self._send(w, (P.GPU_CMD, cmd, oids))
+
+    def rpc_gpu_spilled(self, caller, oids):
+        for oid in oids:
+            e = self.objects.get(oid)
+            if e is None or e.gpu is None or not e.gpu["counted"]:
+                continue
+            if e.gpu["state"] == "spilling":
+                e.gpu["state"] = "host"
+            e.gpu["counted"] = False
+            share = e.gpu["nbytes"] // max(1, len(e.gpu["gpus"]))
+            for d in e.gpu["gpus"]:
+                self.gpu_usage[d] = max(0, self.gpu_usage.get(d, 0) - share)
+            self.gpu_spilled_bytes += e.gpu["nbytes"]
+            self.gpu_num_spilled += 1
+        return True
+
+    def _gpu_request_restore(self, e):
+        if e.gpu["state"] == "restoring":
+            return
+        e.gpu["state"] = "restoring"
+        e.state = PENDING  # readers wait on the restore like on a producing task
+        self._gpu_command(e.gpu_owner, "restore", [e.oid])
+
+    def rpc_gpu_restored(self, caller, oid, desc, info):
+        e = self.objects.get(oid)
+        if e is None or e.gpu is None or e.gpu["state"] != "restoring":
+            return False
+        if desc is None:
+            self._set_error(e, exc.ObjectLostError(oid.hex()))
+            return False
+        g = e.gpu
+        g["state"] = "hbm"
+        g["last"] = time.time()
+        if not g["counted"]:
+            g["counted"] = True
+            share = g["nbytes"] // max(1, len(g["gpus"]))
+            for d in g["gpus"]:
+                self.gpu_usage[d] = self.gpu_usage.get(d, 0) + share
+        self.gpu_num_restored += 1
+        e.desc = tuple(desc)
+        e.state = READY
+        ws, e.waiters = e.waiters, []
+        for cb in ws:
+            cb(e)
+        for d in g["gpus"]:
+            self._gpu_enforce_budget(d)
+        return True
+
+    def rpc_gpu_unmapped(self, caller, oid):
+        e = self.objects.get(oid)
+        if e is not None and e.gpu is not None:
+            n = e.gpu["maps"].get(caller, 0) - 1
+            if n > 0:
+                e.gpu["maps"][caller] = n
+            else:
+                e.gpu["maps"].pop(caller, None)
+        return True
+
+    def rpc_gpu_store_stats(self, caller):
+        return {"budget_per_gpu": self.gpu_budget, "usage": dict(self.gpu_usage), "objects": len(self.gpu_objects),
+                "spilled_bytes": self.gpu_spilled_bytes, "num_spilled": self.gpu_num_spilled,
+                "num_restored": self.gpu_num_restored,
+                "on_host": sum(1 for e in self.gpu_objects.values() if e.gpu["state"] == "host")}
 
     def rpc_make_room(self, caller, nbytes):
         """Spill LRU objects until ``nbytes`` could fit (best effort). Returns freed bytes."""
@@ -655,6 +790,8 @@ class Head:
         remaining = {o for o in oids}
         for oid in oids:
             e = self.objects.get(oid)
+            if e is not None and e.state == READY and e.gpu is not None and e.gpu["state"] != "hbm":
+                self._gpu_request_restore(e)  # spilled to pinned host: back into HBM first
             if e is not None and e.state == PENDING:
                 continue
             remaining.discard(oid)
@@ -1183,7 +1320,7 @@ class Head:
             owner = w.wid if (is_gpu and w is not None) else None
             if owner is not None:
                 w.gpu_objects.add(rid)
-            self._set_ready(e, tuple(desc), contained, owner, flags)
+            self._set_ready(e, tuple(desc), contained, owner, flags, gpu_info=is_gpu)
         if spec.get("generator") == "streaming":
             ts.gen_done = True
             self._flush_gen_waiters(ts)
@@ -1286,10 +1423,16 @@ class Head:
         # GPU objects owned by the worker are lost
         for oid in list(w.gpu_objects):
             e = self.objects.get(oid)
-            if e is not None and e.state == READY:
+            if e is not None and e.state in (READY, PENDING) and (e.state == READY or e.gpu is not None):
+                self._gpu_unaccount(e)
                 e.gpu_owner = None
                 e.desc = ("inline", serialize(exc.OwnerDiedError(oid.hex()), error=True).to_bytes(), 0)
                 e.flags = FLAG_ERROR
+                if e.state == PENDING:  # readers were waiting on a restore from the dead owner
+                    e.state = READY
+                    ws, e.waiters = e.waiters, []
+                    for cb in ws:
+                        cb(e)
         ts = w.task
         w.task = None
         if getattr(w, "oom_killed", None):
@@ -1602,7 +1745,7 @@ class Head:
             if is_gpu and w is not None:
                 owner = gpu_owner
                 w.gpu_objects.add(oid)
-            self._set_ready(e, tuple(desc), contained, owner, flags)
+            self._set_ready(e, tuple(desc), contained, owner, flags, gpu_info=is_gpu)
         return True
 
     def rpc_actor_exit(self, caller):
@@ -2038,6 +2181,24 @@ class ClientConn:
 
     def send(self, msg):
         self.conn.send(msg)
+
+
+def _default_gpu_budget() -> int:
+    """30 % of one GPU's HBM (read from sysfs: no HIP initialisation in the head), 0 = unlimited."""
+    env = os.environ.get("RCA_GPU_OBJECT_STORE_MEMORY")
+    if env:
+        return int(float(env))
+    try:
+        import glob
+
+        for f in sorted(glob.glob("/sys/class/drm/card*/device/mem_info_vram_total")):
+            with open(f) as fh:
+                v = int(fh.read().strip())
+            if v > 0:
+                return int(v * 0.3)
+    except (OSError, ValueError):
+        pass
+    return 0
 
 
 def _parent_visible_devices():

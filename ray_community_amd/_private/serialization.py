@@ -8,10 +8,11 @@ Wire format (one contiguous region — either inline bytes or one shm-store obje
   raw (64-B aligned) and deserialised as zero-copy views of the shm object.
 * ObjectRefs inside a value are recorded (``SerializationContext.contained``) so the head keeps
   them alive while the container lives (borrowing).
-* CUDA tensors are NOT copied through the host: they are exported as HIP IPC handles
-  (``torch.multiprocessing.reductions.reduce_tensor``) — the consumer maps the producer's HBM
-  (same GPU: zero-copy; another GPU on the node: peer mapping over xGMI) and the producer keeps
-  the allocation pinned until the object is freed.
+* CUDA tensors are NOT copied through the host: they become persistent-id slots of the pickle,
+  the owning process keeps them in its GPU object store (``_private/gpu_store.py``) and the wire
+  bytes carry a table of HIP IPC export records as the last out-of-band buffer (``FLAG_GPU``);
+  readers map the owner's HBM (same GPU: zero-copy; another GPU of the node: peer mapping over
+  xGMI).
 """
 from __future__ import annotations
 
@@ -100,44 +101,19 @@ def _reduce_cpu_tensor(t):
     return (_rebuild_np_torch, (arr, name, tuple(t.shape)))
 
 
-_LOCAL_GPU: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
-_LOCAL_GPU_SEQ = itertools.count()
-
-
-def _rebuild_gpu_tensor(rebuild_fn, args, owner=None):
-    import torch
-
-    if owner is not None and owner[0] == os.getpid():
-        # HIP cannot open an IPC handle of the calling process's own allocation: reuse the tensor
-        t = _LOCAL_GPU.get(owner[1])
-        if t is not None:
-            return t
-    try:
-        # the HIP context must exist (and be current on the storage's device) before the IPC open
-        torch.cuda.init()
-        dev = args[6] if len(args) > 6 and isinstance(args[6], int) else torch.cuda.current_device()
-        if dev >= torch.cuda.device_count():
-            dev = torch.cuda.current_device()
-        with torch.cuda.device(dev):
-            torch.cuda.current_stream().synchronize()
-            return rebuild_fn(*args)
-    except Exception as e:  # pragma: no cover - depends on device visibility
-        raise RuntimeError(f"could not map GPU object into this process (HIP IPC): {e}") from e
-
-
-def _reduce_gpu_tensor(t):
-    from torch.multiprocessing.reductions import reduce_tensor
-
-    ctx = current_context()
-    if ctx is not None:
-        ctx.gpu_tensors.append(t)
-    fn, args = reduce_tensor(t)
-    key = next(_LOCAL_GPU_SEQ)
-    _LOCAL_GPU[key] = t
-    return (_rebuild_gpu_tensor, (fn, args, (os.getpid(), key)))
-
-
 class _Pickler(cloudpickle.CloudPickler):
+    def persistent_id(self, obj):
+        # CUDA tensors become slots resolved against the object's GPU export table
+        t = type(obj)
+        if getattr(t, "__module__", "").startswith("torch") and t.__name__ in ("Tensor", "Parameter"):
+            if obj.is_cuda:
+                ctx = current_context()
+                if ctx is None:
+                    raise TypeError("CUDA tensors can only be serialized into objects")
+                ctx.gpu_tensors.append(obj)
+                return ("rca_gpu", len(ctx.gpu_tensors) - 1)
+        return None
+
     def reducer_override(self, obj):
         t = type(obj)
         if t in _CUSTOM:
@@ -147,9 +123,7 @@ class _Pickler(cloudpickle.CloudPickler):
         if mod.startswith("torch") and t.__name__ in ("Tensor", "Parameter"):
             import torch
 
-            if isinstance(obj, torch.Tensor):
-                if obj.is_cuda:
-                    return _reduce_gpu_tensor(obj)
+            if isinstance(obj, torch.Tensor) and not obj.is_cuda:
                 r = _reduce_cpu_tensor(obj)
                 if r is not None:
                     return r
@@ -225,6 +199,18 @@ class Serialized:
         self.write_into(memoryview(buf))
         return bytes(buf)
 
+    def to_bytes_with_table(self, table: bytes) -> bytes:
+        """Wire bytes of a GPU object: the host parts plus the IPC export table as the last
+        out-of-band buffer (``FLAG_GPU``)."""
+        t = Serialized(self.inband, [], self.flags | FLAG_GPU, self.contained, [])
+        t.buffers = list(self.buffers) + [memoryview(table)]
+        t._lens = list(self._lens) + [len(table)]
+        size = _pad(_HDR.size + 8 * len(t.buffers)) + _pad(len(t.inband))
+        for n in t._lens:
+            size += _pad(n)
+        t.total_size = size
+        return t.to_bytes()
+
 
 def serialize(value: Any, error: bool = False) -> Serialized:
     ctx = SerializationContext()
@@ -261,6 +247,13 @@ def parse(mv) -> Tuple[int, bytes, list]:
 
 def deserialize(mv) -> Tuple[Any, int]:
     flags, inband, bufs = parse(mv)
+    if flags & FLAG_GPU:
+        from .gpu_store import decode_table, import_tensor
+
+        tensors = [import_tensor(r) for r in decode_table(bufs[-1])]
+        up = pickle.Unpickler(io.BytesIO(inband), buffers=bufs[:-1])
+        up.persistent_load = lambda pid: tensors[pid[1]]
+        return up.load(), flags
     value = pickle.loads(inband, buffers=bufs)
     return value, flags
 

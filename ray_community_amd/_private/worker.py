@@ -123,6 +123,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             core = CoreWorker("driver", client, head.store, head.head_node_id, head.job_id, ns,
                               session_dir=session)
             head.driver_free_gpu_cb = core.free_gpu_objects
+            head.driver_gpu_cmd_cb = core.gpu_command
             _state.update(head=head, core=core, mode=SCRIPT_MODE, namespace=ns, address=head.sock_path)
             if include_dashboard:
                 from .dashboard import Dashboard

@@ -120,6 +120,8 @@ class Worker:
             self._cancel(msg[1], msg[2])
         elif t == P.FREE_GPU:
             self.core.free_gpu_objects(msg[1])
+        elif t == P.GPU_CMD:
+            threading.Thread(target=self.core.gpu_command, args=(msg[1], msg[2]), daemon=True).start()
 
     def _dispatch_spec(self, spec):
         """Route a task (from the head, or a direct actor call) to its executor."""
@@ -144,12 +146,12 @@ class Worker:
         if head_managed:
             self.client.call("put_owned", [(rid, r[0:3], r[3], r[5], r[4]) for rid, r in
                                            zip(spec["return_ids"], results)], spec["owner_key"])
+        if info.get("spans"):  # tracing on: spans reach the head before the caller sees the result
+            self.client.call("add_spans", info["spans"])
         try:
             conn.send((P.DDONE, tid, [(r[0], r[1], r[2], r[4]) for r in results], head_managed))
         except OSError:
             pass
-        if info.get("spans"):
-            self.client.call_async("add_spans", info["spans"])
         self.direct.record(spec, t_start, time.time(), info)
         if info.get("actor_exit"):
             self.direct.flush()
@@ -320,10 +322,10 @@ class Worker:
 
     def _pack_one(self, oid, value):
         s = ser.serialize(value)
+        is_gpu = bool(s.gpu_tensors)
         desc = self.core._store_serialized(oid, s)
-        if s.gpu_tensors:
-            self.core.gpu_pins[oid] = s.gpu_tensors
-        return (desc[0], desc[1], desc[2], s.contained, s.flags, bool(s.gpu_tensors))
+        gpu = self.core.gpu_info(oid) if is_gpu else False
+        return (desc[0], desc[1], desc[2], s.contained, s.flags | (ser.FLAG_GPU if is_gpu else 0), gpu)
 
     def _pack_returns(self, spec, value):
         rids = spec["return_ids"]
