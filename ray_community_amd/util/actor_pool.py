@@ -1,117 +1,145 @@
-"""ActorPool (reference: ``python/ray/util/actor_pool.py``)."""
+"""ActorPool: spread work over a fixed set of actors (API of ``python/ray/util/actor_pool.py``).
+
+Bookkeeping here is a ticket scheme: every submitted item takes the next ticket number; an
+item waits in ``_backlog`` until an actor is idle; ``_running`` maps the object ref that signals
+an item's completion to its ticket. Results are handed out either in ticket order (``get_next``)
+or in completion order (``get_next_unordered``); a ticket consumed out of order is remembered in
+``_taken`` so ordered retrieval skips it.
+"""
 from __future__ import annotations
 
-from typing import Any, Callable, List
+import collections
+from dataclasses import dataclass, field
+from typing import Any, Callable, Deque, Dict, Iterable, List, Optional, Set, Tuple
+
+
+@dataclass
+class _Ticket:
+    number: int
+    actor: Any
+    result: Any                       # what ``fn`` returned (an ObjectRef or a list of them)
+
+    @property
+    def signal(self):
+        """The ref whose readiness marks this item done."""
+        return self.result[0] if isinstance(self.result, list) else self.result
+
+
+@dataclass
+class _State:
+    idle: Deque[Any] = field(default_factory=collections.deque)
+    backlog: Deque[Tuple[Callable, Any]] = field(default_factory=collections.deque)
+    running: Dict[Any, _Ticket] = field(default_factory=dict)      # signal ref -> ticket
+    by_number: Dict[int, _Ticket] = field(default_factory=dict)
+    taken: Set[int] = field(default_factory=set)
+    issued: int = 0
+    next_ordered: int = 0
 
 
 class ActorPool:
     def __init__(self, actors: list):
-        from .._private.worker import get, wait  # noqa
+        self._s = _State(idle=collections.deque(actors))
 
-        self._idle_actors = list(actors)
-        self._future_to_actor = {}
-        self._index_to_future = {}
-        self._next_task_index = 0
-        self._next_return_index = 0
-        self._pending_submits = []
+    # ------------------------------------------------------------------ submission
+    def submit(self, fn: Callable[[Any, Any], Any], value):
+        """Schedule ``fn(actor, value)`` on an idle actor, or queue it until one frees up."""
+        s = self._s
+        if not s.idle:
+            s.backlog.append((fn, value))
+            return
+        actor = s.idle.popleft()
+        t = _Ticket(s.issued, actor, fn(actor, value))
+        s.issued += 1
+        s.running[t.signal] = t
+        s.by_number[t.number] = t
 
-    def map(self, fn: Callable[[Any, Any], Any], values):
+    def _release(self, actor):
+        s = self._s
+        s.idle.append(actor)
+        if s.backlog:
+            fn, value = s.backlog.popleft()
+            self.submit(fn, value)
+
+    def _drain_ready(self):
+        """Discard already-finished results before a new map() so it starts from a clean slate."""
         while self.has_next():
             try:
                 self.get_next_unordered(timeout=0)
             except TimeoutError:
-                break
+                return
+
+    # ------------------------------------------------------------------ map
+    def map(self, fn: Callable[[Any, Any], Any], values: Iterable):
+        self._drain_ready()
         for v in values:
             self.submit(fn, v)
+        return (self.get_next() for _ in iter(self.has_next, False))
 
-        def gen():
-            while self.has_next():
-                yield self.get_next()
-
-        return gen()
-
-    def map_unordered(self, fn, values):
-        while self.has_next():
-            try:
-                self.get_next_unordered(timeout=0)
-            except TimeoutError:
-                break
+    def map_unordered(self, fn: Callable[[Any, Any], Any], values: Iterable):
+        self._drain_ready()
         for v in values:
             self.submit(fn, v)
+        return (self.get_next_unordered() for _ in iter(self.has_next, False))
 
-        def gen():
-            while self.has_next():
-                yield self.get_next_unordered()
-
-        return gen()
-
-    def submit(self, fn, value):
-        if self._idle_actors:
-            actor = self._idle_actors.pop()
-            future = fn(actor, value)
-            key = future if not isinstance(future, list) else future[0]
-            self._future_to_actor[key] = (self._next_task_index, actor)
-            self._index_to_future[self._next_task_index] = future
-            self._next_task_index += 1
-        else:
-            self._pending_submits.append((fn, value))
-
+    # ------------------------------------------------------------------ retrieval
     def has_next(self) -> bool:
-        return bool(self._future_to_actor)
+        return bool(self._s.running)
 
-    def get_next(self, timeout=None, ignore_if_timedout=False):
-        from .._private.worker import get, wait
-        from ..exceptions import GetTimeoutError
+    def _finish(self, t: _Ticket):
+        from .._private.worker import get
 
+        s = self._s
+        s.running.pop(t.signal, None)
+        s.by_number.pop(t.number, None)
+        self._release(t.actor)
+        return get(t.result)
+
+    def get_next(self, timeout: Optional[float] = None, ignore_if_timedout: bool = False):
+        """The result of the oldest outstanding item (submission order)."""
+        from .._private.worker import wait
+
+        s = self._s
         if not self.has_next():
             raise StopIteration("No more results to get")
-        if self._next_return_index >= self._next_task_index:
+        while s.next_ordered in s.taken:
+            s.taken.discard(s.next_ordered)
+            s.next_ordered += 1
+        t = s.by_number.get(s.next_ordered)
+        if t is None:
             raise ValueError("It is not allowed to call get_next() after get_next_unordered().")
-        future = self._index_to_future[self._next_return_index]
-        key = future if not isinstance(future, list) else future[0]
         if timeout is not None:
-            res, _ = wait([key], timeout=timeout)
-            if not res:
-                if ignore_if_timedout:
-                    del self._index_to_future[self._next_return_index]
-                    self._next_return_index += 1
+            ready, _ = wait([t.signal], timeout=timeout)
+            if not ready:
+                if ignore_if_timedout:  # give up on this item: ordered retrieval moves past it
+                    s.next_ordered += 1
                 raise TimeoutError("Timed out waiting for result")
-        del self._index_to_future[self._next_return_index]
-        self._next_return_index += 1
-        i, a = self._future_to_actor.pop(key)
-        self._return_actor(a)
-        return get(future)
+        s.next_ordered += 1
+        return self._finish(t)
 
-    def get_next_unordered(self, timeout=None, ignore_if_timedout=False):
-        from .._private.worker import get, wait
+    def get_next_unordered(self, timeout: Optional[float] = None, ignore_if_timedout: bool = False):
+        """The result of whichever outstanding item finishes first."""
+        from .._private.worker import wait
 
+        s = self._s
         if not self.has_next():
             raise StopIteration("No more results to get")
-        res, _ = wait(list(self._future_to_actor), num_returns=1, timeout=timeout)
-        if not res:
+        ready, _ = wait(list(s.running), num_returns=1, timeout=timeout)
+        if not ready:
             raise TimeoutError("Timed out waiting for result")
-        future = res[0]
-        i, a = self._future_to_actor.pop(future)
-        self._return_actor(a)
-        del self._index_to_future[i]
-        self._next_return_index = max(self._next_return_index, i + 1)
-        return get(future)
+        t = s.running[ready[0]]
+        if t.number >= s.next_ordered:
+            s.taken.add(t.number)
+        return self._finish(t)
 
-    def _return_actor(self, actor):
-        self._idle_actors.append(actor)
-        if self._pending_submits:
-            self.submit(*self._pending_submits.pop(0))
-
-    def has_free(self):
-        return len(self._idle_actors) > 0 and len(self._pending_submits) == 0
+    # ------------------------------------------------------------------ pool membership
+    def has_free(self) -> bool:
+        return bool(self._s.idle) and not self._s.backlog
 
     def pop_idle(self):
-        if self.has_free():
-            return self._idle_actors.pop()
-        return None
+        return self._s.idle.popleft() if self.has_free() else None
 
     def push(self, actor):
-        busy = [a for _, a in self._future_to_actor.values()]
-        if actor in self._idle_actors or actor in busy:
+        s = self._s
+        if actor in s.idle or any(t.actor is actor or t.actor == actor for t in s.running.values()):
             raise ValueError("Actor already belongs to current ActorPool")
-        self._return_actor(actor)
+        self._release(actor)

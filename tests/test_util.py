@@ -25,6 +25,73 @@ def test_actor_pool(ray_start_regular):
     assert not pool.has_next()
 
 
+def test_actor_pool_backlog_ordering_and_membership(ray_start_regular):
+    from ray_community_amd.util import ActorPool
+
+    @ray.remote
+    class Sleeper:
+        def run(self, x):
+            time.sleep(0.3 if x == 0 else 0.01)
+            return x
+
+    a, b = Sleeper.remote(), Sleeper.remote()
+    pool = ActorPool([a, b])
+    for v in range(5):  # 2 run, 3 wait in the backlog for an idle actor
+        pool.submit(lambda act, v: act.run.remote(v), v)
+    assert not pool.has_free() and pool.pop_idle() is None
+    first = pool.get_next_unordered()
+    assert first != 0  # item 0 is the slow one
+    rest = [pool.get_next() for _ in range(4)]  # ordered retrieval skips the ticket already taken
+    assert sorted([first] + rest) == list(range(5)) and rest == sorted(rest)
+    assert pool.has_free()
+    idle = pool.pop_idle()
+    assert idle is not None
+    other = b if idle is a else a
+    with pytest.raises(ValueError):
+        pool.push(other)  # still a member of the pool
+    pool.push(idle)
+    with pytest.raises(StopIteration):
+        pool.get_next()
+    pool.submit(lambda act, v: act.run.remote(v), 0)
+    with pytest.raises(TimeoutError):
+        pool.get_next(timeout=0.01)
+
+
+def test_queue_bounded_blocking_and_async(ray_start_regular):
+    from ray_community_amd.util.queue import Empty, Full, Queue
+
+    q = Queue(maxsize=2)
+    q.put(1)
+    q.put(2)
+    assert q.full() and len(q) == 2
+    with pytest.raises(Full):
+        q.put(3, block=False)
+    with pytest.raises(Full):
+        q.put(3, timeout=0.1)
+    with pytest.raises(Full):
+        q.put_nowait_batch([3, 4])
+
+    @ray.remote
+    def late_consumer(q):
+        time.sleep(0.3)
+        return q.get()
+
+    r = late_consumer.remote(q)
+    q.put(3, timeout=10)  # blocks until the consumer frees a slot
+    assert ray.get(r) == 1 and q.get_nowait_batch(2) == [2, 3]
+    with pytest.raises(Empty):
+        q.get_nowait_batch(1)
+
+    @ray.remote
+    class User:
+        async def roundtrip(self, q):
+            await q.put_async("x")
+            return await q.get_async(timeout=5)
+
+    assert ray.get(User.remote().roundtrip.remote(q)) == "x"
+    q.shutdown()
+
+
 def test_queue(ray_start_regular):
     from ray_community_amd.util.queue import Empty, Queue
 
