@@ -77,7 +77,7 @@ class Deferred:
 
 class ObjEntry:
     __slots__ = ("oid", "state", "desc", "holders", "pins", "waiters", "contained", "task", "gpu_owner", "size",
-                 "flags", "created", "gpu")
+                 "flags", "created", "gpu", "node")
 
     def __init__(self, oid, task=None):
         self.oid = oid
@@ -93,6 +93,7 @@ class ObjEntry:
         self.flags = 0
         self.created = time.time()
         self.gpu = None  # GPU object accounting: {"nbytes", "gpus", "state", "last", "maps": {reader: n}}
+        self.node = None  # node whose store holds the value (lost with the node)
 
 
 class TaskState:
@@ -221,6 +222,10 @@ class Head:
         self.functions: Dict[bytes, bytes] = {}
         self.events: collections.deque = collections.deque(maxlen=int(self.config.get("task_events_max", 100000)))
         self.finished_tasks: collections.deque = collections.deque(maxlen=10000)
+        # lineage of reconstructable task outputs: tid -> [spec, owner, attempts left]; bounded LRU
+        self.lineage: "collections.OrderedDict[bytes, list]" = collections.OrderedDict()
+        self.lineage_max = int(self.config.get("max_lineage_entries", 100000))
+        self.num_reconstructions = 0
         # records of directly transported actor calls (state API / timeline), batched by workers
         self.direct_tasks: collections.deque = collections.deque(maxlen=int(self.config.get("direct_task_records", 10000)))
         self.timers: List[tuple] = []
@@ -299,6 +304,10 @@ class Head:
             for w in list(self.workers.values()):
                 if w.node_id == node_id and not w.dead:
                     self._kill_worker(w)
+            # objects in the node's store are gone with it: reconstruct from lineage or fail
+            for e in [e for e in self.objects.values() if e.node == node_id and e.state == READY and e.desc
+                      and e.desc[0] in ("shm", "spill")]:
+                self._lose_object(e)
             self._schedule()
 
     # ================================================================== main loop
@@ -623,6 +632,77 @@ class Head:
         self._set_ready(e, tuple(desc), contained, owner, flags, gpu_info=is_gpu)
         return True
 
+    # -------------------------------------------------------------- lineage reconstruction
+    def _record_lineage(self, ts):
+        """Keep the spec of a finished retryable task so its outputs can be recomputed if lost
+        (reference ``src/ray/core_worker/object_recovery_manager.cc``). Bounded LRU: an evicted
+        entry makes a later loss fail with ObjectReconstructionFailedLineageEvictedError."""
+        spec = ts.spec
+        ent = self.lineage.get(ts.tid)
+        if ent is None:
+            self.lineage[ts.tid] = [spec, ts.owner, int(spec.get("max_retries", 0))]
+        self.lineage.move_to_end(ts.tid)
+        while len(self.lineage) > self.lineage_max:
+            self.lineage.popitem(last=False)
+
+    def _lose_object(self, e):
+        """A READY object's value is gone (its node died / its spill file vanished)."""
+        if e.desc and e.desc[0] == "shm":
+            self.store.delete(e.oid)
+        tid = e.task
+        ent = self.lineage.get(tid) if tid else None
+        if ent is None:
+            err = (exc.ObjectReconstructionFailedLineageEvictedError(e.oid.hex()) if tid and tid in self.tasks
+                   else exc.ObjectLostError(e.oid.hex()))
+            self._fail_lost(e, err)
+            return
+        if ent[2] == 0:
+            self._fail_lost(e, exc.ObjectReconstructionFailedMaxAttemptsExceededError(e.oid.hex()))
+            return
+        self._reconstruct(tid)
+
+    def _fail_lost(self, e, err):
+        b = serialize(err, error=True).to_bytes()
+        e.desc = ("inline", b, len(b))
+        e.flags = FLAG_ERROR
+
+    def _reconstruct(self, tid):
+        """Re-execute the producing task (same task id and return ids); readers of its outputs
+        wait on them as on any pending object. Lost inputs are reconstructed first."""
+        ent = self.lineage.get(tid)
+        if ent is None:
+            return
+        ts_old = self.tasks.get(tid)
+        if ts_old is not None and ts_old.state not in (T_FINISHED, T_FAILED, T_CANCELLED):
+            return  # already being recomputed
+        spec, owner, left = ent
+        if left > 0:
+            ent[2] = left - 1
+        self.num_reconstructions += 1
+        for rid in spec["return_ids"]:
+            e = self.objects.get(rid)
+            if e is not None and e.state == READY:
+                if e.desc and e.desc[0] == "shm":
+                    self.store.delete(rid)
+                for c in e.contained:
+                    self._unpin(c)
+                e.contained = []
+                e.state = PENDING
+                e.desc = None
+        for a in spec["args"]:
+            if a[0] == "r":
+                d = self.objects.get(a[1])
+                if d is not None and d.state == READY and d.desc and d.desc[0] in ("shm", "spill") and \
+                        d.node is not None and not self.nodes.get(d.node, NodeState("x", {})).alive:
+                    self._lose_object(d)
+        self._event(ts_old or TaskState(tid, spec, owner), "reconstruct")
+        re_spec = dict(spec)
+        re_spec["max_retries"] = 0
+        self._submit(re_spec, owner)
+
+    def rpc_lineage_stats(self, caller):
+        return {"entries": len(self.lineage), "reconstructions": self.num_reconstructions}
+
     # -------------------------------------------------------------- GPU object store (HBM budget)
     def _gpu_owner_key(self, e):
         o = e.gpu_owner
@@ -771,6 +851,7 @@ class Head:
             with open(path, "rb") as f:
                 data = f.read()
         except OSError:
+            self._lose_object(e)  # the spill file is gone: reconstruct from lineage or fail
             return
         ok = self.store.put_bytes(e.oid, data)
         if not ok:
@@ -1308,6 +1389,8 @@ class Head:
         ts.state = T_FAILED if failed else T_FINISHED
         ts.times["end"] = time.time()
         ts.error_type = info.get("error_type")
+        if kind == "task" and not failed and spec.get("max_retries", 0) != 0 and spec.get("generator") is None:
+            self._record_lineage(ts)
         self._event(ts, "failed" if failed else "finished", worker=w)
         gpu_owner = ("w:" + w.wid.hex()) if w is not None else None
         for rid, res in zip(spec["return_ids"], results):
@@ -1320,6 +1403,7 @@ class Head:
             owner = w.wid if (is_gpu and w is not None) else None
             if owner is not None:
                 w.gpu_objects.add(rid)
+            e.node = ts.node
             self._set_ready(e, tuple(desc), contained, owner, flags, gpu_info=is_gpu)
         if spec.get("generator") == "streaming":
             ts.gen_done = True

@@ -155,6 +155,14 @@ class ObjectReconstructionFailedError(ObjectLostError):
     pass
 
 
+class ObjectReconstructionFailedMaxAttemptsExceededError(ObjectReconstructionFailedError):
+    pass
+
+
+class ObjectReconstructionFailedLineageEvictedError(ObjectReconstructionFailedError):
+    pass
+
+
 class ObjectStoreFullError(RayError):
     pass
 
