@@ -22,7 +22,8 @@ if HERE not in sys.path:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--learners", type=int, default=0, help="0 = one local GPU learner in the driver")
+    ap.add_argument("--learners", type=int, default=None,
+                    help="GPU learner actors (default: one per visible GPU; 0 = a local learner in the driver)")
     ap.add_argument("--runners", type=int, default=None)
     ap.add_argument("--envs-per-runner", type=int, default=16)
     ap.add_argument("--train-batch", type=int, default=8192)
@@ -41,6 +42,8 @@ def main():
     ncpu = len(os.sched_getaffinity(0))
     runners = args.runners if args.runners is not None else max(1, min(16, ncpu - 2))
     ngpu = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if args.learners is None:
+        args.learners = ngpu
     ray.init(num_cpus=max(ncpu, runners + 2), num_gpus=ngpu)
     cfg = (PPOConfig().environment(args.env)
            .env_runners(num_env_runners=runners, num_envs_per_env_runner=args.envs_per_runner)

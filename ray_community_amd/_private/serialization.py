@@ -21,6 +21,7 @@ import itertools
 import os
 import pickle
 import struct
+import sys
 import threading
 import weakref
 from typing import Any, List, Optional, Tuple
@@ -101,11 +102,23 @@ def _reduce_cpu_tensor(t):
     return (_rebuild_np_torch, (arr, name, tuple(t.shape)))
 
 
+_TENSOR_TYPES: frozenset = frozenset()
+
+
+def _tensor_types() -> frozenset:
+    global _TENSOR_TYPES
+    if not _TENSOR_TYPES and "torch" in sys.modules:
+        import torch
+
+        _TENSOR_TYPES = frozenset({torch.Tensor, torch.nn.Parameter})
+    return _TENSOR_TYPES
+
+
 class _Pickler(cloudpickle.CloudPickler):
     def persistent_id(self, obj):
-        # CUDA tensors become slots resolved against the object's GPU export table
-        t = type(obj)
-        if getattr(t, "__module__", "").startswith("torch") and t.__name__ in ("Tensor", "Parameter"):
+        # CUDA tensors become slots resolved against the object's GPU export table (called for
+        # every pickled object: one set lookup on the hot path)
+        if type(obj) in _tensor_types():
             if obj.is_cuda:
                 ctx = current_context()
                 if ctx is None:
@@ -119,14 +132,10 @@ class _Pickler(cloudpickle.CloudPickler):
         if t in _CUSTOM:
             ser, des = _CUSTOM[t]
             return (_rebuild_custom, (des, ser(obj)))
-        mod = getattr(t, "__module__", "")
-        if mod.startswith("torch") and t.__name__ in ("Tensor", "Parameter"):
-            import torch
-
-            if isinstance(obj, torch.Tensor) and not obj.is_cuda:
-                r = _reduce_cpu_tensor(obj)
-                if r is not None:
-                    return r
+        if t in _tensor_types() and not obj.is_cuda:
+            r = _reduce_cpu_tensor(obj)
+            if r is not None:
+                return r
         return super().reducer_override(obj)
 
 

@@ -20,6 +20,8 @@ from .algorithm_config import AlgorithmConfig
 
 class Algorithm(Trainable):
     _default_config_cls = AlgorithmConfig
+    multi_agent = False      # set in setup() from the config
+    learner_groups = None
 
     def __init__(self, config: Optional[AlgorithmConfig] = None, env=None, **kw):
         if isinstance(config, dict):
@@ -45,19 +47,35 @@ class Algorithm(Trainable):
         cfg = self.config
         rd = cfg.runner_dict()
         rd.update(self._runner_extra())
-        self.local_runner = EnvRunner(rd, 0)
-        self.obs_space, self.act_space = self.local_runner.spaces()
+        self.multi_agent = cfg.is_multi_agent
+        runner_cls = EnvRunner
+        if self.multi_agent:
+            from ..env.multi_agent_env_runner import MultiAgentEnvRunner
+
+            runner_cls = MultiAgentEnvRunner
+        self.local_runner = runner_cls(rd, 0)
         self.remote_runners = []
         if cfg.num_env_runners > 0:
             from ...actor import ActorClass
 
-            cls = ActorClass(EnvRunner, {"num_cpus": cfg.num_cpus_per_env_runner})
+            cls = ActorClass(runner_cls, {"num_cpus": cfg.num_cpus_per_env_runner})
             self.remote_runners = [cls.remote(rd, i + 1) for i in range(cfg.num_env_runners)]
         from ..core.learner import LearnerGroup
 
         ld = cfg.to_dict()
         ld.update(self._runner_extra())
-        self.learner_group = LearnerGroup(ld, self.obs_space, self.act_space)
+        if self.multi_agent:
+            # one learner group (RLModule + optimizer, possibly several GPU learners) per policy
+            sp = self.local_runner.spaces()
+            self.learner_groups = {p: LearnerGroup(ld, *sp[p]) for p in self.local_runner.modules}
+            self.policies_to_train = list(cfg.policies_to_train or self.learner_groups)
+            first = next(iter(self.learner_groups))
+            self.obs_space, self.act_space = sp[first]
+            self.learner_group = self.learner_groups[first]
+        else:
+            self.obs_space, self.act_space = self.local_runner.spaces()
+            self.learner_group = LearnerGroup(ld, self.obs_space, self.act_space)
+            self.learner_groups = None
         self._sync_weights()
         from .callbacks import build as _build_callbacks
 
@@ -73,22 +91,24 @@ class Algorithm(Trainable):
     def _sync_weights(self):
         from ..._private.worker import get, put
 
-        st = self.learner_group.get_weights()
+        st = ({p: g.get_weights() for p, g in self.learner_groups.items()} if self.multi_agent
+              else self.learner_group.get_weights())
         self._weights_version += 1
         self.local_runner.set_weights(st, self._weights_version)
         if self.remote_runners:
             ref = put(st)
             get([r.set_weights.remote(ref, self._weights_version) for r in self.remote_runners])
 
-    def _sample(self, steps_total: int) -> SampleBatch:
+    def _sample_fragments(self, steps_total: int) -> List[SampleBatch]:
         from ..._private.worker import get
 
         if self.remote_runners:
             per = max(1, steps_total // len(self.remote_runners))
-            batches = get([r.sample.remote(per) for r in self.remote_runners])
-        else:
-            batches = [self.local_runner.sample(steps_total)]
-        return concat_samples(batches)
+            return get([r.sample.remote(per) for r in self.remote_runners])
+        return [self.local_runner.sample(steps_total)]
+
+    def _sample(self, steps_total: int) -> SampleBatch:
+        return concat_samples(self._sample_fragments(steps_total))
 
     def _collect_metrics(self):
         from ..._private.worker import get
@@ -98,6 +118,13 @@ class Algorithm(Trainable):
             ms += get([r.get_metrics.remote() for r in self.remote_runners])
         eps = [e for m in ms for e in m["episodes"]]
         self._custom_metrics = [c for m in ms for c in m.get("custom_metrics", ())]
+        if self.multi_agent:
+            if not hasattr(self, "_policy_recent"):
+                self._policy_recent = {}
+            for m in ms:
+                for p, rets in m.get("policy_returns", {}).items():
+                    dq = self._policy_recent.setdefault(p, deque(maxlen=self.config.metrics_num_episodes_for_smoothing))
+                    dq.extend(rets)
         for e in eps:
             self._recent.append(e)
         self._episodes_total += len(eps)
@@ -130,8 +157,11 @@ class Algorithm(Trainable):
             "num_env_steps_sampled": self._timesteps_total,
             "num_env_steps_sampled_this_iter": info.pop("_steps_this_iter", 0),
             "time_this_iter_s": dt,
-            "info": {"learner": {"default_policy": info}},
+            "info": {"learner": info if self.multi_agent else {"default_policy": info}},
         }
+        if self.multi_agent:
+            res["policy_reward_mean"] = {p: float(np.mean(d)) for p, d in getattr(self, "_policy_recent", {}).items()
+                                         if d}
         res["env_steps_per_sec"] = res["num_env_steps_sampled_this_iter"] / dt if dt > 0 else 0.0
         res["env_runners"] = {"episode_return_mean": res["episode_reward_mean"],
                               "episode_return_max": res["episode_reward_max"],
@@ -180,10 +210,15 @@ class Algorithm(Trainable):
                 "env_runners": {"episode_return_mean": float(np.mean(rets)) if rets else float("nan")},
                 "num_episodes": len(eps)}
 
-    def compute_single_action(self, observation, explore: bool = False, **kw):
+    def compute_single_action(self, observation, explore: bool = False, policy_id=None, **kw):
         obs = torch.as_tensor(np.asarray(observation)[None])
-        m = self.local_runner.module
-        m.set_state(self.learner_group.get_weights())
+        if self.multi_agent:
+            pid = policy_id or next(iter(self.learner_groups))
+            m = self.local_runner.modules[pid]
+            m.set_state(self.learner_groups[pid].get_weights())
+        else:
+            m = self.local_runner.module
+            m.set_state(self.learner_group.get_weights())
         if explore:
             a, _, _, _ = m.forward_exploration(obs)
         else:
@@ -196,16 +231,24 @@ class Algorithm(Trainable):
         m.set_state(self.learner_group.get_weights())
         return m
 
-    def get_weights(self):
+    def get_weights(self, policies=None):
+        if self.multi_agent:
+            return {p: g.get_weights() for p, g in self.learner_groups.items() if policies is None or p in policies}
         return self.learner_group.get_weights()
 
     def set_weights(self, w):
-        self.learner_group.call("set_weights", w)
+        if self.multi_agent:
+            for p, st in w.items():
+                self.learner_groups[p].call("set_weights", st)
+        else:
+            self.learner_group.call("set_weights", w)
         self._sync_weights()
 
     def save_checkpoint(self, checkpoint_dir: str):
         os.makedirs(checkpoint_dir, exist_ok=True)
-        st = {"learner": self.learner_group.call("get_state"), "iteration": self._iteration,
+        learner = ({p: g.call("get_state") for p, g in self.learner_groups.items()} if self.multi_agent
+                   else self.learner_group.call("get_state"))
+        st = {"learner": learner, "iteration": self._iteration, "multi_agent": self.multi_agent,
               "timesteps_total": self._timesteps_total, "config": self.config.to_dict(),
               "extra": self._extra_state()}
         with open(os.path.join(checkpoint_dir, "algorithm_state.pkl"), "wb") as f:
@@ -218,7 +261,11 @@ class Algorithm(Trainable):
         path = checkpoint if isinstance(checkpoint, str) else getattr(checkpoint, "path", checkpoint)
         with open(os.path.join(path, "algorithm_state.pkl"), "rb") as f:
             st = pickle.load(f)
-        self.learner_group.call("set_state", st["learner"])
+        if st.get("multi_agent"):
+            for p, ls in st["learner"].items():
+                self.learner_groups[p].call("set_state", ls)
+        else:
+            self.learner_group.call("set_state", st["learner"])
         self._iteration = st["iteration"]
         self._timesteps_total = st["timesteps_total"]
         self._load_extra_state(st.get("extra") or {})
@@ -261,7 +308,8 @@ class Algorithm(Trainable):
             except Exception:
                 pass
         self.remote_runners = []
-        self.learner_group.shutdown()
+        for g in (self.learner_groups.values() if self.multi_agent else [self.learner_group]):
+            g.shutdown()
 
     cleanup = stop
 

@@ -46,6 +46,10 @@ class AlgorithmConfig:
         # misc
         self.seed = None
         self.metrics_num_episodes_for_smoothing = 100
+        # multi-agent
+        self.policies = None                 # {policy_id: None | PolicySpec | (cls, obs_space, act_space, cfg)}
+        self.policy_mapping_fn = None        # (agent_id, episode, worker, **kw) -> policy_id
+        self.policies_to_train = None
         self.min_sample_timesteps_per_iteration = 0
 
     # ------------------------------------------------------------------ builder methods
@@ -133,10 +137,28 @@ class AlgorithmConfig:
     def api_stack(self, **kw):
         return self
 
-    def multi_agent(self, **kw):
-        if kw.get("policies") and len(kw["policies"]) > 1:
-            raise NotImplementedError("multi-agent training is not supported yet")
+    def multi_agent(self, *, policies=None, policy_mapping_fn=None, policies_to_train=None, **kw):
+        """Several policies, each with its own RLModule and learner group; agents are bound to
+        policies by ``policy_mapping_fn(agent_id, episode, worker)`` (reference:
+        ``AlgorithmConfig.multi_agent``). ``policies`` may be a set/list of ids or a dict of ids to
+        ``None`` / ``PolicySpec`` / ``(cls, obs_space, act_space, config)``."""
+        if policies is not None:
+            self.policies = {p: None for p in policies} if isinstance(policies, (set, list, tuple)) else dict(policies)
+        if policy_mapping_fn is not None:
+            self.policy_mapping_fn = policy_mapping_fn
+        if policies_to_train is not None:
+            self.policies_to_train = list(policies_to_train)
         return self
+
+    @property
+    def is_multi_agent(self) -> bool:
+        from ..env.multi_agent_env import MultiAgentEnv, _MA_REGISTRY
+
+        if self.policies:
+            return True
+        e = self.env
+        return (isinstance(e, str) and e in _MA_REGISTRY) or isinstance(e, MultiAgentEnv) or \
+            (isinstance(e, type) and issubclass(e, MultiAgentEnv))
 
     def offline_data(self, *, input_=None, output=None, input_config=None, output_config=None, **kw):
         """``input_``: directory / glob of JSON batches for offline algorithms (BC, MARWIL);

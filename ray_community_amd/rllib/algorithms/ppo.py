@@ -44,10 +44,17 @@ class PPO(Algorithm):
 
     def training_step(self) -> Dict:
         cfg = self.config
-        batch = self._sample(cfg.train_batch_size)
-        n = batch.count
+        if self.multi_agent:
+            batch = self._sample(cfg.train_batch_size)
+            n = batch.count
+            info = {p: self.learner_groups[p].update("ppo", batch.policy_batches[p])
+                    for p in self.policies_to_train if p in batch.policy_batches}
+        else:
+            # runner fragments go to the learner(s) as they are: stacked on the GPU, not the host
+            frags = self._sample_fragments(cfg.train_batch_size)
+            n = sum(f.count for f in frags)
+            info = self.learner_group.update("ppo", frags)
         self._timesteps_total += n
-        info = self.learner_group.update("ppo", batch)
         self._sync_weights()
         info["_steps_this_iter"] = n
         return info

@@ -79,7 +79,12 @@ class Learner:
         return pts[-1][1]
 
     def _step(self, loss):
-        self.opt.zero_grad(set_to_none=True)
+        if self.ddp is not None:
+            # gradients must stay views into DDP's flat buffer (the all-reduce runs on it);
+            # set_to_none would make backward allocate detached .grad tensors
+            self.ddp.zero_grad()
+        else:
+            self.opt.zero_grad(set_to_none=True)
         loss.backward()
         gc = self.cfg.get("grad_clip")
         gn = None
@@ -91,11 +96,30 @@ class Learner:
         return gn
 
     # ------------------------------------------------------------------ PPO
+    def _dist_group(self):
+        import torch.distributed as dist
+
+        return self.ddp is not None and dist.is_initialized() and dist.get_world_size() > 1
+
+    def _allreduce_sum(self, t):
+        """Sum over the learner group (no-op for a single learner)."""
+        if self._dist_group():
+            import torch.distributed as dist
+
+            dist.all_reduce(t)
+        return t
+
     def update_ppo(self, batch: SampleBatch) -> Dict:
+        """Clipped-surrogate PPO over the batch resident on this learner's device.
+
+        ``loss_mask`` (optional, multi-agent padding): rows with mask 0 carry no loss and are left
+        out of the advantage statistics. With several learners the advantage mean/std and the
+        reported statistics are reduced over the whole group (each learner holds an env-axis
+        shard), so N learners take exactly the step one learner would on the full batch."""
         cfg = self.cfg
         t0 = time.perf_counter()
-        b = batch.to_device(self.device)
-        N, T = batch.fragment_shape
+        b = _to_device_batch(batch, self.device)
+        N, T = b.fragment_shape
         rew, vf, nvf = b["rewards"], b["vf_preds"], b["next_vf_preds"]
         term, trunc = b["terminateds"], b["truncateds"]
         done = term | trunc
@@ -108,7 +132,17 @@ class Learner:
             adv = adv - vf
         adv = adv.reshape(-1).contiguous()
         vt = vt.reshape(-1)
-        ops.standardize_(adv)
+        mask = b["loss_mask"].reshape(-1).float() if "loss_mask" in b else None
+        if mask is None and not self._dist_group():
+            ops.standardize_(adv)
+        else:  # masked and/or group-wide statistics
+            m = mask if mask is not None else torch.ones_like(adv)
+            st = torch.stack([m.sum(), (adv * m).sum(), (adv * adv * m).sum()]).double()
+            self._allreduce_sum(st)
+            cnt = st[0].clamp(min=1.0)
+            mean = st[1] / cnt
+            var = (st[2] / cnt - mean * mean).clamp(min=0.0)
+            adv = ((adv - mean.float()) / (var.sqrt().float() + 1e-4)) * m
         obs = b["obs"].reshape((N * T,) + tuple(b["obs"].shape[2:]))
         act = b["actions"].reshape((N * T,) + tuple(b["actions"].shape[2:]))
         old_logp = b["action_logp"].reshape(-1)
@@ -124,10 +158,15 @@ class Learner:
         count = 0
         gen = torch.Generator(device=self.device)
         gen.manual_seed(1234 + self.num_updates)
+
+        def mean(x, w):
+            return x.mean() if w is None else (x * w).sum() / w.sum().clamp(min=1.0)
+
         for _ in range(epochs):
             perm = torch.randperm(n, device=self.device, generator=gen)
             for i in range(0, n - mb + 1, mb):
                 idx = perm[i: i + mb]
+                w = mask[idx] if mask is not None else None
                 logits, v = self.forward(obs[idx])
                 d = self.module.dist(logits)
                 lp = d.logp(act[idx])
@@ -137,21 +176,30 @@ class Learner:
                 vf_err = (v - vt[idx]) ** 2
                 vf_loss = vf_err.clamp(0, vclip) if vclip else vf_err
                 ent = d.entropy()
-                loss = -surr.mean() + vf_coeff * vf_loss.mean() - ent_coeff * ent.mean()
+                pi_term, vf_term, ent_term = mean(surr, w), mean(vf_loss, w), mean(ent, w)
+                loss = -pi_term + vf_coeff * vf_term - ent_coeff * ent_term
                 if use_kl:
-                    kl = self.module.dist(old_logits[idx]).kl(d).mean()
+                    kl = mean(self.module.dist(old_logits[idx]).kl(d), w)
                     if self.kl_coeff > 0:
                         loss = loss + self.kl_coeff * kl
                 else:
                     kl = torch.zeros((), device=self.device)
                 self._step(loss)
-                stats["policy_loss"] += -surr.mean().detach()
-                stats["vf_loss"] += vf_loss.mean().detach()
-                stats["entropy"] += ent.mean().detach()
+                stats["policy_loss"] += -pi_term.detach()
+                stats["vf_loss"] += vf_term.detach()
+                stats["entropy"] += ent_term.detach()
                 stats["mean_kl"] += kl.detach()
                 stats["total_loss"] += loss.detach()
                 count += 1
-        out = {k: float(v) / max(count, 1) for k, v in stats.items()}
+        keys = list(stats)
+        vec = torch.stack([torch.as_tensor(stats[k], device=self.device, dtype=torch.float64) for k in keys])
+        vec = vec / max(count, 1)
+        if self._dist_group():  # every learner adapts kl_coeff from the same group-wide KL
+            import torch.distributed as dist
+
+            self._allreduce_sum(vec)
+            vec = vec / dist.get_world_size()
+        out = {k: float(v) for k, v in zip(keys, vec.tolist())}
         if use_kl:
             kt = cfg.get("kl_target", 0.01)
             if out["mean_kl"] > 2.0 * kt:
@@ -451,19 +499,27 @@ class Learner:
             self.target.load_state_dict(self.module.state_dict())
 
 
-class _LearnerActor:
-    def __init__(self):
-        self.learner = None
+def _learner_actor_cls():
+    from ...train._internal.worker_group import _TrainWorker
 
-    def build(self, config, obs_space, act_space, use_gpu):
-        self.learner = Learner(config, obs_space, act_space, use_gpu)
-        return True
+    class _LearnerActor(_TrainWorker):
+        """A Train worker (node info, process-group setup via the torch backend) hosting a Learner."""
 
-    def update(self, kind, batch):
-        return getattr(self.learner, f"update_{kind}")(batch)
+        def __init__(self):
+            super().__init__()
+            self.learner = None
 
-    def call(self, name, *args):
-        return getattr(self.learner, name)(*args)
+        def build(self, config, obs_space, act_space, use_gpu):
+            self.learner = Learner(config, obs_space, act_space, use_gpu)
+            return True
+
+        def update(self, kind, batch):
+            return getattr(self.learner, f"update_{kind}")(batch)
+
+        def call(self, name, *args):
+            return getattr(self.learner, name)(*args)
+
+    return _LearnerActor
 
 
 class LearnerGroup:
@@ -485,7 +541,7 @@ class LearnerGroup:
         from ..._private.worker import get
 
         res = {"CPU": 1, "GPU": gpus} if gpus else {"CPU": 1}
-        self.wg = WorkerGroup(self.n, res, "PACK", actor_cls=_LearnerActor)
+        self.wg = WorkerGroup(self.n, res, "PACK", actor_cls=_learner_actor_cls())
         sc = ScalingConfig(num_workers=self.n, use_gpu=gpus > 0, resources_per_worker=res)
         _TorchBackend().on_start(self.wg, TorchConfig(), sc)
         get([w.build.remote(config, obs_space, act_space, gpus > 0) for w in self.wg.workers])
@@ -520,7 +576,25 @@ class LearnerGroup:
             self.wg.shutdown()
 
 
-def _split(batch: SampleBatch, n: int) -> List[SampleBatch]:
+def _to_device_batch(batch, device) -> SampleBatch:
+    """One device-resident train batch. A list of runner fragments is copied host->device
+    fragment by fragment and stacked ON THE DEVICE (``concat_samples`` -> HIP ``batched_concat``,
+    one launch per column), so the driver never concatenates the rollouts on the host."""
+    if isinstance(batch, (list, tuple)):
+        from ..policy.sample_batch import concat_samples
+
+        return concat_samples([b.to_device(device) for b in batch if b is not None and b.count > 0])
+    return batch.to_device(device)
+
+
+def _split(batch, n: int) -> List:
+    if isinstance(batch, (list, tuple)):
+        if len(batch) >= n and len(batch) % n == 0:  # whole runner fragments per learner
+            k = len(batch) // n
+            return [list(batch[i * k: (i + 1) * k]) for i in range(n)]
+        from ..policy.sample_batch import concat_samples
+
+        batch = concat_samples(list(batch))
     if batch.fragment_shape is not None:
         N, T = batch.fragment_shape
         per = [N // n + (1 if i < N % n else 0) for i in range(n)]

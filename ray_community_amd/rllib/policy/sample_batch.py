@@ -161,9 +161,21 @@ def _cat(xs):
 
 
 class MultiAgentBatch:
+    """Per-policy SampleBatches of one sampling round (reference ``MultiAgentBatch``)."""
+
     def __init__(self, policy_batches: Dict[str, SampleBatch], env_steps: int):
         self.policy_batches = policy_batches
         self._env_steps = env_steps
+        self.fragment_shape = None
+
+    def __getitem__(self, pid):
+        return self.policy_batches[pid]
+
+    def __contains__(self, pid):
+        return pid in self.policy_batches
+
+    def __len__(self):
+        return self._env_steps
 
     @property
     def count(self):

@@ -376,3 +376,67 @@ def test_dreamerv3_world_model_learns_and_checkpoints(shutdown_only, tmp_path):
     r = pend.train()
     assert np.isfinite(r["info"]["learner"]["default_policy"]["actor_loss"])
     assert np.asarray(pend.compute_single_action(np.zeros(3, dtype=np.float32))).shape == (1,)
+
+
+def test_multi_agent_ppo_two_policies_learn(shutdown_only):
+    """Two CartPole agents stepping simultaneously in one MultiAgentEnv, mapped to two separate
+    policies (own RLModule + learner each): both learn."""
+    from ray_community_amd.rllib.env.multi_agent_env import MultiAgentEnv, make_multi_agent
+
+    ray.init(num_cpus=4)
+    env = make_multi_agent("CartPole-v1")({"num_agents": 2})
+    assert isinstance(env, MultiAgentEnv) and env.possible_agents == ["agent_0", "agent_1"]
+    obs, _ = env.reset(seed=0)
+    assert set(obs) == {"agent_0", "agent_1"}
+    config = (PPOConfig().environment("MultiAgentCartPole", env_config={"num_agents": 2})
+              .env_runners(num_env_runners=1, num_envs_per_env_runner=8)
+              .multi_agent(policies={"p0", "p1"}, policy_mapping_fn=lambda aid, *a, **k: "p" + aid[-1])
+              .training(lr=3e-4, train_batch_size=2048, minibatch_size=256, num_epochs=8, vf_loss_coeff=0.01,
+                        model={"fcnet_hiddens": [64, 64]})
+              .debugging(seed=0))
+    algo = config.build()
+    best = {"p0": 0.0, "p1": 0.0}
+    for _ in range(30):
+        r = algo.train()
+        for p, v in r.get("policy_reward_mean", {}).items():
+            best[p] = max(best[p], v)
+        if min(best.values()) > 100:
+            break
+    assert min(best.values()) > 100, best
+    assert set(r["info"]["learner"]) == {"p0", "p1"}
+    w = algo.get_weights()
+    assert set(w) == {"p0", "p1"} and not all(torch.equal(w["p0"][k], w["p1"][k]) for k in w["p0"])
+    assert algo.compute_single_action(np.zeros(4, dtype=np.float32), policy_id="p1") in (0, 1)
+    algo.stop()
+
+
+def test_two_learners_take_the_single_learner_step(shutdown_only):
+    """num_learners=2 (gloo process group, DDP gradient all-reduce, group-wide advantage
+    statistics) updates the weights exactly like one learner on the whole batch."""
+    from ray_community_amd.rllib.core.learner import LearnerGroup
+    from ray_community_amd.rllib.env.env_runner import EnvRunner
+
+    ray.init(num_cpus=4)
+    cfg = (PPOConfig().environment("CartPole-v1").env_runners(num_envs_per_env_runner=8)
+           .training(lr=1e-3, train_batch_size=512, minibatch_size=512, num_epochs=1, use_kl_loss=False,
+                     model={"fcnet_hiddens": [32, 32]}).debugging(seed=3))
+    # Adam's first step is lr * g / (|g| + eps): a large eps keeps it a smooth function of the
+    # gradient, so fp32 summation-order differences between 1 and 2 learners stay tiny
+    cfg.adam_epsilon = 1e-3
+    runner = EnvRunner(cfg.runner_dict(), 0)
+    batch = runner.sample(512)
+    obs_sp, act_sp = runner.spaces()
+    d1 = cfg.to_dict()
+    one = LearnerGroup(d1, obs_sp, act_sp)
+    d2 = dict(d1, num_learners=2)
+    two = LearnerGroup(d2, obs_sp, act_sp)
+    w0 = {k: v.clone() for k, v in one.get_weights().items()}
+    assert all(torch.equal(w0[k], two.get_weights()[k]) for k in w0)
+    s1 = one.update("ppo", batch)
+    s2 = two.update("ppo", batch)
+    wa, wb = one.get_weights(), two.get_weights()
+    for k in wa:
+        assert not torch.equal(wa[k], w0[k]) or k.endswith("bias"), k  # the step did move the weights
+        assert torch.allclose(wa[k], wb[k], atol=2e-6, rtol=1e-4), k
+    assert abs(s1["policy_loss"] - s2["policy_loss"]) < 1e-5
+    two.shutdown()
