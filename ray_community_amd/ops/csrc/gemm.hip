@@ -39,15 +39,16 @@ constexpr int GROUP_M = 8;
 
 __device__ __forceinline__ int kswz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
 
-// Stage one 256 x BK operand tile into a lane-linear LDS image (BK/16 global_load_lds per thread).
-template <bool KMAJ, int BK>
+// Stage one 256 x BK operand tile into a lane-linear LDS image: 256*BK*2/1024 one-KB blocks, one
+// global_load_lds (64 lanes x 16 B) each, dealt round-robin over the NW waves.
+template <bool KMAJ, int BK, int NW = 8>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* dst,
                                            int wid, int lane) {
   constexpr int CPR = BK / 8;  // 16-B chunks per k-contiguous row
   constexpr int RSH = CPR == 8 ? 1 : 2;  // rows sharing a 256-B bank row differ in (row >> RSH)
 #pragma unroll
-  for (int i = 0; i < BK / 16; ++i) {
-    const int blk = i * 8 + wid;          // 1 KB block of the image this wave instruction fills
+  for (int i = 0; i < (BK / 2) / NW; ++i) {
+    const int blk = i * NW + wid;         // 1 KB block of the image this wave instruction fills
     const int p = blk * 64 + lane;        // 16-B chunk index in the image
     const bf16_t* src;
     if constexpr (!KMAJ) {                // [256 outer][CPR chunks]
@@ -179,115 +180,6 @@ __global__ __launch_bounds__(NTHR) void gemm_bf16_kernel(const bf16_t* __restric
   }
 }
 
-// Software-pipelined variant (BK=64, two LDS stages): the fragments of the NEXT 32-deep k-step
-// are read from LDS while the MFMAs of the current one run (two register fragment sets, 96 VGPRs,
-// + 128 accumulators), so LDS latency and bandwidth hide under the MFMA pipe:
-//   [glds tile t+1] [read k1(t) || MFMA k0(t)] [lgkm(0) vmcnt(0) barrier] [read k0(t+1) || MFMA k1(t)]
-// Every ds_read retires before the barrier, so the refill of a stage after the next barrier can
-// never overtake a slow reader.
-template <bool AK, bool BKM>
-__device__ __forceinline__ void load_set(const lds_char* ta, const lds_char* tb, int kk, int wm, int wn, int lane,
-                                         bf16x8_t (&af)[8], bf16x8_t (&bf)[4]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bf[j] = load_frag<BKM, 64>(tb, wn * 4 + j, kk, lane);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) af[i] = load_frag<AK, 64>(ta, wm * 8 + i, kk, lane);
-}
-
-__device__ __forceinline__ void mfma_set(f32x4 (&acc)[8][4], const bf16x8_t (&af)[8], const bf16x8_t (&bf)[4]) {
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
-}
-
-template <bool AK, bool BKM, bool ACC>
-__global__ __launch_bounds__(NTHR) void gemm_bf16_sp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                            bf16_t* __restrict__ C, int M, int N, int K, long lda,
-                                                            long ldb, long ldc) {
-  constexpr int BK = 64;
-  constexpr int TILE_BYTES = 256 * BK * 2;
-  constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char* smem = (lds_char*)smem_raw;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
-  const int lin = xcd_remap(blockIdx.x, nwg);
-  const int gsz = GROUP_M * ntn, grp = lin / gsz, fm = grp * GROUP_M;
-  const int gm = min(ntm - fm, GROUP_M), r = lin % gsz;
-  const int m0 = (fm + r % gm) * BM, n0 = (r / gm) * BN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8_t ax[8], bx[4], ay[8], by[4];
-
-  const int nt = K / BK;
-  stage_tile<AK, BK>(A, lda, m0, 0, smem, wid, lane);
-  stage_tile<BKM, BK>(B, ldb, n0, 0, smem + TILE_BYTES, wid, lane);
-  wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-  load_set<AK, BKM>(smem, smem + TILE_BYTES, 0, wm, wn, lane, ax, bx);
-  for (int t = 0; t < nt; ++t) {
-    const lds_char* ta = smem + (t & 1) * STAGE_BYTES;
-    const lds_char* tb = ta + TILE_BYTES;
-    const bool more = t + 1 < nt;
-    lds_char* na = smem + ((t + 1) & 1) * STAGE_BYTES;
-    if (more) {
-      stage_tile<AK, BK>(A, lda, m0, (t + 1) * BK, na, wid, lane);
-      stage_tile<BKM, BK>(B, ldb, n0, (t + 1) * BK, na + TILE_BYTES, wid, lane);
-    }
-    load_set<AK, BKM>(ta, tb, 1, wm, wn, lane, ay, by);
-    mfma_set(acc, ax, bx);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (more) load_set<AK, BKM>(na, na + TILE_BYTES, 0, wm, wn, lane, ax, bx);
-    mfma_set(acc, ay, by);
-  }
-
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const long m = m0 + wm * 128 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      unsigned long long* dst = (unsigned long long*)(C + m * ldc + n);
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      if constexpr (ACC) {
-        const unsigned long long old = *dst;
-        v0 += bf2f((bf16_t)(old & 0xffff));
-        v1 += bf2f((bf16_t)((old >> 16) & 0xffff));
-        v2 += bf2f((bf16_t)((old >> 32) & 0xffff));
-        v3 += bf2f((bf16_t)((old >> 48) & 0xffff));
-      }
-      *dst = (unsigned long long)f2bf(v0) | ((unsigned long long)f2bf(v1) << 16) |
-             ((unsigned long long)f2bf(v2) << 32) | ((unsigned long long)f2bf(v3) << 48);
-    }
-  }
-}
-
-template <bool AK, bool BKM, bool ACC>
-int launch_sp(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
-              hipStream_t st) {
-  auto kern = gemm_bf16_sp_kernel<AK, BKM, ACC>;
-  constexpr int smem = 2 * 2 * 256 * 64 * 2;
-  static bool attr = [&] {
-    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
-  }();
-  if (!attr) return -3;
-  const int nwg = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NTHR), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
-                     lda, ldb, ldc);
-  return (int)hipGetLastError();
-}
-
 template <bool AK, bool BKM, bool ACC, int BK, int NS>
 int launch(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc, hipStream_t st) {
   auto kern = gemm_bf16_kernel<AK, BKM, ACC, BK, NS>;
@@ -304,14 +196,17 @@ int launch(const void* A, const void* B, void* C, int M, int N, int K, long lda,
 }
 
 // Measured on MI355X (scripts/gemm_bench.py, 8B training shapes, random operands; round 2):
-//   variant 1 (BK=64, 2 stages)      fwd 1.06-1.20 PF, dgrad 0.91-0.97, wgrad 0.71-0.93
-//   BK=32 x 3/4 stages (removed)     fwd 0.82-1.04,    dgrad 0.66-0.73, wgrad 0.60-0.74
-//   variant 2 (software-pipelined)   256 VGPRs + 12-60 B/lane scratch: register-bound as written
-// hipBLASLt on the same shapes: 1.41-1.61 PF (fwd), 1.21-1.50 incl. transposed copies (bwd).
+//   BK=64, 2 stages, 8 waves of 128x64 (kept)   fwd 1.03-1.18 PF, dgrad 0.90-0.96, wgrad 0.71-0.91
+//   BK=32 x 3/4 stages                           fwd 0.82-1.04,    dgrad 0.66-0.73, wgrad 0.60-0.74
+//   8 waves, next-k fragments prefetched         256 VGPRs + 12-60 B/lane scratch (register-bound)
+//   4 waves (1/SIMD) of 128x128, prefetched      fwd 0.81-1.01,    dgrad 0.75-0.80, wgrad 0.62-0.77
+// hipBLASLt on the same shapes: 1.41-1.61 PF (fwd), 1.21-1.50 incl. transposed copies (bwd), so
+// the model keeps hipBLASLt; this kernel is the natural-layout path (no transposed copies,
+// deterministic, no stream-K atomics) for the next round's 8-phase schedule.
 template <bool AK, bool BKM, bool ACC>
 int launch_variant(int variant, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
                    long ldc, hipStream_t st) {
-  if (variant == 2) return launch_sp<AK, BKM, ACC>(A, B, C, M, N, K, lda, ldb, ldc, st);
+  (void)variant;
   return launch<AK, BKM, ACC, 64, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
 }
 
