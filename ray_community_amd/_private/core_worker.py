@@ -138,12 +138,18 @@ class ObjectRefGenerator:
     def __aiter__(self):
         return self
 
+    def _next_or_none(self):
+        try:
+            return self._next_sync(None)
+        except StopIteration:  # cannot cross an executor future: signal the end with None
+            return None
+
     async def __anext__(self):
         loop = asyncio.get_running_loop()
-        try:
-            return await loop.run_in_executor(None, self._next_sync, None)
-        except StopIteration:
+        ref = await loop.run_in_executor(None, self._next_or_none)
+        if ref is None:
             raise StopAsyncIteration
+        return ref
 
     def completed(self):
         return self._main

@@ -331,7 +331,7 @@ class Worker:
         rids = spec["return_ids"]
         gen = spec.get("generator")
         if gen == "streaming":
-            n = 0
+            n = spec.get("_streamed", 0)  # items already streamed by an async generator
             it = value
             if inspect.isgenerator(it) or hasattr(it, "__next__") or hasattr(it, "__iter__"):
                 for item in it:
@@ -418,10 +418,22 @@ class Worker:
                         self._async_tasks.pop(tid, None)
                         self.running.pop(tid, None)
                 elif inspect.isasyncgen(value):
-                    items = []
-                    async for x in value:
-                        items.append(x)
-                    value = iter(items)
+                    if spec.get("generator") == "streaming":
+                        # stream each item to the caller as the coroutine produces it
+                        loop = asyncio.get_running_loop()
+                        n = 0
+                        async for x in value:
+                            oid = new_id()
+                            r = await loop.run_in_executor(None, self._pack_one, oid, x)
+                            self.client.send((P.GEN_ITEM, spec["tid"], n, r + (oid,)))
+                            n += 1
+                        value = iter(())
+                        spec = dict(spec, _streamed=n)
+                    else:
+                        items = []
+                        async for x in value:
+                            items.append(x)
+                        value = iter(items)
                 loop = asyncio.get_running_loop()
                 results = await loop.run_in_executor(None, self._pack_returns, spec, value)
             except _ActorExit:

@@ -95,3 +95,78 @@ async def _run_asgi(app, req: Dict):
 
     await app(scope, receive, send)
     return sent["status"], sent["headers"], sent["body"]
+
+
+async def stream_asgi_or_call(replica, req: Dict):
+    """Async generator of response messages: ("start", status, headers), ("body", chunk)*."""
+    import asyncio
+
+    obj = replica.obj
+    spec = getattr(type(obj), "_serve_ingress_spec", None) if not replica.is_function else None
+    if spec is not None:
+        app = getattr(replica, "_asgi_app", None)
+        if app is None:
+            from ..api import _build_ingress_app
+
+            app = replica._asgi_app = _build_ingress_app(spec, obj)
+        q: asyncio.Queue = asyncio.Queue()
+        body = req.get("body", b"")
+        got = {"v": False}
+
+        async def receive():
+            if got["v"]:
+                await asyncio.sleep(3600)  # no more request body: park like a real server
+            got["v"] = True
+            return {"type": "http.request", "body": body, "more_body": False}
+
+        async def send(msg):
+            await q.put(msg)
+
+        async def run():
+            try:
+                await app(_scope(req), receive, send)
+            finally:
+                await q.put(None)
+
+        task = asyncio.ensure_future(run())
+        try:
+            while True:
+                msg = await q.get()
+                if msg is None:
+                    break
+                if msg["type"] == "http.response.start":
+                    yield ("start", msg["status"], [(k.decode(), v.decode()) for k, v in msg.get("headers", [])])
+                elif msg["type"] == "http.response.body":
+                    if msg.get("body"):
+                        yield ("body", msg["body"])
+        finally:
+            await task
+        return
+    from starlette.requests import Request
+
+    body = req.get("body", b"")
+
+    async def receive2():
+        return {"type": "http.request", "body": body, "more_body": False}
+
+    request = Request(_scope(req), receive2)
+    res = await replica._invoke_user("__call__", (request,), {})
+    try:
+        from starlette.responses import StreamingResponse
+    except ImportError:  # pragma: no cover
+        StreamingResponse = None
+    if StreamingResponse is not None and isinstance(res, StreamingResponse):
+        yield ("start", res.status_code, [(k.decode(), v.decode()) for k, v in res.raw_headers])
+        async for chunk in res.body_iterator:
+            yield ("body", chunk.encode() if isinstance(chunk, str) else chunk)
+        return
+    if inspect.isgenerator(res) or inspect.isasyncgen(res):
+        from .replica import _aiter
+
+        yield ("start", 200, [("content-type", "text/plain; charset=utf-8")])
+        async for chunk in _aiter(res):
+            yield ("body", chunk.encode() if isinstance(chunk, str) else bytes(chunk))
+        return
+    status, headers, out = _to_response(res)
+    yield ("start", status, headers)
+    yield ("body", out)

@@ -77,18 +77,30 @@ class HTTPProxy:
                "root_path": root}
         from ..handle import _Router
 
+        started = False
         try:
             router = _Router.get(app_name, ingress)
             loop = asyncio.get_running_loop()
-            fut = await loop.run_in_executor(None, router.submit, None, (req,), {}, {}, "handle_http")
-            ref, _ = await asyncio.wrap_future(fut)
-            status, headers, out = await ref
+            fut = await loop.run_in_executor(None, router.submit, None, (req,), {}, {}, "handle_http_stream")
+            gen, _ = await asyncio.wrap_future(fut)
+            # streamed response: each message is forwarded the moment the replica produces it
+            async for ref in gen:
+                msg = await ref
+                if msg[0] == "start":
+                    await send({"type": "http.response.start", "status": msg[1],
+                                "headers": [(k.encode(), v.encode()) for k, v in msg[2]]})
+                    started = True
+                else:
+                    await send({"type": "http.response.body", "body": msg[1], "more_body": True})
+            await gen.completed()  # surfaces a replica-side failure
         except Exception as e:  # noqa
-            await _respond(send, 500, f"Internal Server Error: {e}".encode())
+            if not started:
+                await _respond(send, 500, f"Internal Server Error: {e}".encode())
+                return
+        if not started:
+            await _respond(send, 500, b"Internal Server Error: empty response")
             return
-        await send({"type": "http.response.start", "status": status,
-                    "headers": [(k.encode(), v.encode()) for k, v in headers]})
-        await send({"type": "http.response.body", "body": out})
+        await send({"type": "http.response.body", "body": b"", "more_body": False})
 
     def shutdown(self):
         if self._server is not None:

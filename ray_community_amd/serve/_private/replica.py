@@ -16,6 +16,23 @@ from typing import Any, Dict, Optional
 _REPLICA_CTX = {}
 
 
+async def _aiter(res):
+    """Iterate a sync or async generator (a plain value yields once)."""
+    if inspect.isasyncgen(res):
+        async for x in res:
+            yield x
+    elif inspect.isgenerator(res):
+        loop = asyncio.get_running_loop()
+        done = object()
+        while True:  # pull sync generator items on a thread: the event loop keeps serving
+            x = await loop.run_in_executor(None, next, res, done)
+            if x is done:
+                break
+            yield x
+    else:
+        yield res
+
+
 class ReplicaContext:
     def __init__(self, app_name, deployment, replica_tag, servable_object=None):
         self.app_name = app_name
@@ -67,26 +84,31 @@ class ServeReplica:
                 await r
         return True
 
+    async def _invoke_user(self, method_name, args, kwargs):
+        """Call the user's method: coroutines awaited, sync code on the thread pool (the event
+        loop keeps serving), generators returned unconsumed."""
+        fn = self.obj if self.is_function else getattr(self.obj, method_name or "__call__")
+        if inspect.iscoroutinefunction(fn) or inspect.iscoroutinefunction(getattr(fn, "__call__", None)):
+            return await fn(*args, **kwargs)
+        if inspect.isasyncgenfunction(fn):
+            return fn(*args, **kwargs)
+        loop = asyncio.get_running_loop()
+        import contextvars
+
+        ctx = contextvars.copy_context()
+        res = await loop.run_in_executor(None, lambda: ctx.run(fn, *args, **kwargs))
+        if inspect.isawaitable(res):
+            res = await res
+        return res
+
     async def _call_user(self, method_name, args, kwargs, model_id=None):
         from .. import multiplex
 
         tok = multiplex._set_model_id(model_id)
         try:
-            if self.is_function:
-                fn = self.obj
-            else:
-                fn = getattr(self.obj, method_name or "__call__")
-            if inspect.iscoroutinefunction(fn) or inspect.iscoroutinefunction(getattr(fn, "__call__", None)):
-                return await fn(*args, **kwargs)
-            if inspect.isasyncgenfunction(fn):
-                return [x async for x in fn(*args, **kwargs)]
-            loop = asyncio.get_running_loop()
-            import contextvars
-
-            ctx = contextvars.copy_context()
-            res = await loop.run_in_executor(None, lambda: ctx.run(fn, *args, **kwargs))
-            if inspect.isawaitable(res):
-                res = await res
+            res = await self._invoke_user(method_name, args, kwargs)
+            if inspect.isasyncgen(res):
+                return [x async for x in res]
             if inspect.isgenerator(res):
                 res = list(res)
             return res
@@ -107,6 +129,38 @@ class ServeReplica:
             args = tuple([(await a) if isinstance(a, ObjectRef) else a for a in args])
             kwargs = {k: ((await v) if isinstance(v, ObjectRef) else v) for k, v in kwargs.items()}
             return await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
+        finally:
+            self.ongoing -= 1
+
+    async def handle_request_stream(self, method_name, args, kwargs, meta=None):
+        """Generator counterpart of ``handle_request`` for ``handle.options(stream=True)``:
+        items of a (sync or async) generator method are streamed back one by one."""
+        from ..handle import _resolve_handle_args
+        from .. import multiplex
+
+        meta = meta or {}
+        self.ongoing += 1
+        self.total += 1
+        tok = multiplex._set_model_id(meta.get("multiplexed_model_id"))
+        try:
+            args, kwargs = _resolve_handle_args(args, kwargs)
+            res = await self._invoke_user(method_name, args, kwargs)
+            async for x in _aiter(res):
+                yield x
+        finally:
+            multiplex._reset_model_id(tok)
+            self.ongoing -= 1
+
+    async def handle_http_stream(self, req: Dict):
+        """Streaming HTTP: yields ("start", status, headers) then ("body", chunk) messages as the
+        deployment produces them (ASGI apps, ``StreamingResponse``, generator ``__call__``)."""
+        self.ongoing += 1
+        self.total += 1
+        try:
+            from .http_util import stream_asgi_or_call
+
+            async for msg in stream_asgi_or_call(self, req):
+                yield msg
         finally:
             self.ongoing -= 1
 

@@ -14,7 +14,7 @@ import threading
 import time
 from typing import Any, Dict, List, Optional, Tuple
 
-from .._private.core_worker import ObjectRef
+from .._private.core_worker import ObjectRef, ObjectRefGenerator
 
 
 class _HandleSpec:
@@ -134,15 +134,16 @@ class _Router:
             tag, actor = got
             actor_method, method, args, kwargs, meta, fut = self.queue.popleft()
             try:
-                if actor_method == "handle_request":
-                    ref = actor.handle_request.remote(method, args, kwargs, meta)
+                if actor_method in ("handle_request", "handle_request_stream"):
+                    ref = getattr(actor, actor_method).remote(method, args, kwargs, meta)
                 else:
                     ref = getattr(actor, actor_method).remote(*args)
             except Exception as e:  # noqa
                 self.inflight[tag] = max(0, self.inflight.get(tag, 0) - 1)
                 fut.set_exception(e)
                 continue
-            ref.future().add_done_callback(lambda f, tag=tag: self.done(tag))
+            done_ref = ref.completed() if isinstance(ref, ObjectRefGenerator) else ref
+            done_ref.future().add_done_callback(lambda f, tag=tag: self.done(tag))
             fut.set_result((ref, tag))
 
     def _ensure_drainer(self):
@@ -234,19 +235,34 @@ class DeploymentResponse:
 
 
 class DeploymentResponseGenerator:
-    def __init__(self, resp: DeploymentResponse):
-        self._resp = resp
-        self._items = None
+    """Streaming response of ``handle.options(stream=True)``: items arrive one by one as the
+    replica's generator yields them (an ObjectRefGenerator underneath)."""
+
+    def __init__(self, fut: concurrent.futures.Future):
+        self._fut = fut
+
+    def _gen(self):
+        return self._fut.result()[0]
 
     def __iter__(self):
-        return iter(self._resp.result())
+        from .._private.worker import get
+
+        for ref in self._gen():
+            yield get(ref)
 
     def __aiter__(self):
         async def gen():
-            for x in await self._resp:
-                yield x
+            g = (await asyncio.wrap_future(self._fut))[0]
+            async for ref in g:
+                yield await ref
 
         return gen()
+
+    def cancel(self):
+        from .._private.worker import cancel
+
+        if self._fut.done():
+            cancel(self._gen()._main)
 
 
 class DeploymentHandle:
@@ -276,8 +292,10 @@ class DeploymentHandle:
         args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
         kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v) for k, v in kwargs.items()}
         meta = {"multiplexed_model_id": self._model_id} if self._model_id else {}
-        resp = DeploymentResponse(router.submit(self._method, args, kwargs, meta))
-        return DeploymentResponseGenerator(resp) if self._stream else resp
+        if self._stream:
+            return DeploymentResponseGenerator(router.submit(self._method, args, kwargs, meta,
+                                                             actor_method="handle_request_stream"))
+        return DeploymentResponse(router.submit(self._method, args, kwargs, meta))
 
     def __reduce__(self):
         return (DeploymentHandle, (self.deployment_name, self.app_name), {"_method": self._method,

@@ -179,3 +179,48 @@ def test_multiplexing(serve_instance):
     assert h.options(multiplexed_model_id="a").remote().result() == ("model-a", 1)
     assert h.options(multiplexed_model_id="a").remote().result() == ("model-a", 1)
     assert h.options(multiplexed_model_id="b").remote().result() == ("model-b", 2)
+
+
+def test_streaming_http_and_handle(serve_instance):
+    """Responses stream chunk by chunk: a generator __call__ over HTTP (the first chunk arrives
+    before the generator finishes), a FastAPI StreamingResponse, and handle.options(stream=True)."""
+    import time as _time
+
+    from fastapi import FastAPI
+    from fastapi.responses import StreamingResponse
+
+    @serve.deployment
+    class Ticker:
+        def __call__(self, request):
+            def gen():
+                for i in range(3):
+                    yield f"tick{i}\n"
+                    _time.sleep(0.4)
+            return gen()
+
+        def count(self, n):
+            for i in range(n):
+                yield i
+
+    h = serve.run(Ticker.bind(), name="ticker", route_prefix="/ticker")
+    t0 = _time.time()
+    with requests.get("http://127.0.0.1:18123/ticker", stream=True, timeout=30) as r:
+        it = r.iter_lines()
+        first = next(it)
+        t_first = _time.time() - t0
+        rest = list(it)
+    assert first == b"tick0" and rest == [b"tick1", b"tick2"]
+    assert t_first < 0.7  # the whole response takes >= 0.8 s
+    assert list(h.options(method_name="count", stream=True).remote(4)) == [0, 1, 2, 3]
+
+    app = FastAPI()
+
+    @serve.deployment
+    @serve.ingress(app)
+    class Api:
+        @app.get("/s")
+        def s(self):
+            return StreamingResponse(iter([b"a", b"b", b"c"]), media_type="text/plain")
+
+    serve.run(Api.bind(), name="sapi", route_prefix="/sapi")
+    assert requests.get("http://127.0.0.1:18123/sapi/s", timeout=30).content == b"abc"
