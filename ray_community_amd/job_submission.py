@@ -191,9 +191,57 @@ def _to_info(d: Dict) -> JobInfo:
     return JobInfo(**{k: v for k, v in d.items() if k in fields})
 
 
+def _job_manager(create: bool = True):
+    """The session's detached JobManager actor (created on first use)."""
+    from ._private import worker as w
+    from .actor import ActorClass
+
+    try:
+        return w.get_actor(_MANAGER, namespace=_NS)
+    except ValueError:
+        if not create:
+            raise
+        core = w._core()
+        logs = os.path.join(core.session_dir or "/tmp/rca", "logs")
+        addr = w._state.get("address")
+        return ActorClass(JobManager, {"name": _MANAGER, "namespace": _NS, "lifetime": "detached",
+                                       "num_cpus": 0, "max_concurrency": 64,
+                                       "get_if_exists": True}).remote(addr, logs)
+
+
+def _jsonable_job(d: Dict) -> Dict:
+    out = dict(d)
+    for k, v in out.items():
+        if isinstance(v, enum.Enum):
+            out[k] = v.value
+    return out
+
+
 class JobSubmissionClient:
+    """Submit and manage jobs.
+
+    ``address="http://host:8265"`` talks to the dashboard's job REST API (reference
+    ``dashboard/modules/job/job_head.py``: ``POST /api/jobs/``, ``GET /api/jobs/{id}``,
+    ``POST /api/jobs/{id}/stop``, ``DELETE /api/jobs/{id}``, ``GET /api/jobs/{id}/logs``); any other
+    address (a session socket, ``"auto"``, ``None``) joins the session and drives the JobManager
+    actor directly.
+    """
+
     def __init__(self, address: Optional[str] = None, create_cluster_if_needed: bool = False, cookies=None,
                  metadata=None, headers=None, verify=None):
+        self._http = None
+        if address and address.startswith(("http://", "https://")):
+            import requests
+
+            self._http = address.rstrip("/")
+            self._session = requests.Session()
+            if headers:
+                self._session.headers.update(headers)
+            if cookies:
+                self._session.cookies.update(cookies)
+            r = self._session.get(self._http + "/api/version", timeout=10)
+            r.raise_for_status()
+            return
         from ._private import worker as w
 
         if not w.is_initialized():
@@ -201,18 +249,18 @@ class JobSubmissionClient:
                 w.init(address=address if address != "auto" else None, ignore_reinit_error=True)
             else:
                 w.init(address=None if address in (None, "auto", "local") else address, ignore_reinit_error=True)
-        from .actor import ActorClass
-
-        try:
-            self._mgr = w.get_actor(_MANAGER, namespace=_NS)
-        except ValueError:
-            core = w._core()
-            logs = os.path.join(core.session_dir or "/tmp/rca", "logs")
-            addr = w._state.get("address")
-            self._mgr = ActorClass(JobManager, {"name": _MANAGER, "namespace": _NS, "lifetime": "detached",
-                                                "num_cpus": 0, "max_concurrency": 64,
-                                                "get_if_exists": True}).remote(addr, logs)
+        self._mgr = _job_manager()
         self._get = w.get
+
+    # ------------------------------------------------------------------ HTTP transport
+    def _req(self, method: str, path: str, **kw):
+        r = self._session.request(method, self._http + path, timeout=60, **kw)
+        if r.status_code == 404:
+            raise RuntimeError(r.json().get("error", f"{path} not found") if r.headers.get(
+                "content-type", "").startswith("application/json") else f"{path} not found")
+        if r.status_code >= 400:
+            raise RuntimeError(f"{method} {path} failed ({r.status_code}): {r.text}")
+        return r.json()
 
     def submit_job(self, *, entrypoint: str, job_id: Optional[str] = None, runtime_env: Optional[Dict] = None,
                    metadata: Optional[Dict[str, str]] = None, submission_id: Optional[str] = None,
@@ -222,10 +270,18 @@ class JobSubmissionClient:
 
         res = {"entrypoint_num_cpus": entrypoint_num_cpus, "entrypoint_num_gpus": entrypoint_num_gpus,
                "entrypoint_resources": entrypoint_resources}
+        if self._http:
+            body = {"entrypoint": entrypoint, "submission_id": submission_id or job_id,
+                    "runtime_env": runtime_env, "metadata": metadata, **res}
+            return self._req("POST", "/api/jobs/", json=body)["submission_id"]
         return self._get(self._mgr.submit.remote(entrypoint, submission_id or job_id, validate(runtime_env),
                                                  metadata, res))
 
     def get_job_info(self, job_id: str) -> JobInfo:
+        if self._http:
+            d = self._req("GET", f"/api/jobs/{job_id}")
+            d["status"] = JobStatus(d["status"])
+            return _to_info(d)
         d = self._get(self._mgr.info.remote(job_id))
         if d is None:
             raise RuntimeError(f"Job {job_id} does not exist.")
@@ -235,9 +291,17 @@ class JobSubmissionClient:
         return self.get_job_info(job_id).status
 
     def list_jobs(self) -> List[JobDetails]:
+        if self._http:
+            out = []
+            for d in self._req("GET", "/api/jobs/"):
+                d["status"] = JobStatus(d["status"])
+                out.append(_to_info(d))
+            return out
         return [_to_info(d) for d in self._get(self._mgr.list.remote())]
 
     def get_job_logs(self, job_id: str) -> str:
+        if self._http:
+            return self._req("GET", f"/api/jobs/{job_id}/logs")["logs"]
         out = self._get(self._mgr.logs.remote(job_id, 0))
         if out is None:
             raise RuntimeError(f"Job {job_id} does not exist.")
@@ -246,22 +310,34 @@ class JobSubmissionClient:
     async def tail_job_logs(self, job_id: str) -> AsyncIterator[str]:
         offset = 0
         while True:
-            chunk = await self._mgr.logs.remote(job_id, offset)
+            if self._http:
+                loop = asyncio.get_running_loop()
+                d = await loop.run_in_executor(None, lambda: self._req("GET", f"/api/jobs/{job_id}/logs",
+                                                                       params={"offset": offset}))
+                chunk = d["logs"]
+                info = await loop.run_in_executor(None, lambda: self._req("GET", f"/api/jobs/{job_id}"))
+            else:
+                chunk = await self._mgr.logs.remote(job_id, offset)
+                info = await self._mgr.info.remote(job_id)
             if chunk:
                 offset += len(chunk.encode())
                 yield chunk
-            info = await self._mgr.info.remote(job_id)
             if info is None or JobStatus(info["status"]).is_terminal():
-                rest = await self._mgr.logs.remote(job_id, offset)
+                rest = (self._req("GET", f"/api/jobs/{job_id}/logs", params={"offset": offset})["logs"]
+                        if self._http else await self._mgr.logs.remote(job_id, offset))
                 if rest:
                     yield rest
                 return
             await asyncio.sleep(0.1)
 
     def stop_job(self, job_id: str) -> bool:
+        if self._http:
+            return self._req("POST", f"/api/jobs/{job_id}/stop")["stopped"]
         return self._get(self._mgr.stop.remote(job_id))
 
     def delete_job(self, job_id: str) -> bool:
+        if self._http:
+            return self._req("DELETE", f"/api/jobs/{job_id}")["deleted"]
         return self._get(self._mgr.delete.remote(job_id))
 
     def wait_until_finish(self, job_id: str, timeout_s: float = 600) -> JobStatus:

@@ -47,3 +47,29 @@ def test_job_lifecycle(shutdown_only, tmp_path):
         return "".join([c async for c in client.tail_job_logs(tail)])
 
     assert "two" in asyncio.run(collect())
+
+
+def test_job_rest_api_over_http(shutdown_only, tmp_path):
+    """JobSubmissionClient("http://127.0.0.1:<dashboard port>") drives the dashboard's job REST API
+    (POST /api/jobs/, GET /api/jobs/{id}[/logs], POST /api/jobs/{id}/stop, DELETE /api/jobs/{id})."""
+    import requests
+
+    ctx = ray.init(num_cpus=2, include_dashboard=True, dashboard_port=0)
+    url = ctx.dashboard_url
+    client = JobSubmissionClient(url)
+    sid = client.submit_job(entrypoint=f"{sys.executable} -c \"print('hello from http job')\"",
+                            metadata={"via": "rest"})
+    assert client.wait_until_finish(sid, 120) == JobStatus.SUCCEEDED
+    assert "hello from http job" in client.get_job_logs(sid)
+    assert client.get_job_info(sid).metadata == {"via": "rest"}
+    slow = client.submit_job(entrypoint="sleep 30", submission_id="rest-sleeper")
+    assert slow == "rest-sleeper" and client.get_job_status(slow) == JobStatus.RUNNING
+    with pytest.raises(RuntimeError):
+        client.delete_job(slow)  # not terminal yet
+    assert client.stop_job(slow)
+    assert client.wait_until_finish(slow, 30) == JobStatus.STOPPED
+    assert {j.submission_id for j in client.list_jobs()} >= {sid, slow}
+    assert client.delete_job(slow)
+    assert requests.get(f"{url}/api/jobs/rest-sleeper", timeout=10).status_code == 404
+    r = requests.post(f"{url}/api/jobs/", json={"entrypoint": "true", "submission_id": sid}, timeout=10)
+    assert r.status_code == 400  # duplicate submission id
