@@ -36,9 +36,9 @@ def main():
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
-    ap.add_argument("--parallel", default="ddp", choices=["ddp", "zero", "auto"],
+    ap.add_argument("--parallel", default="ddp", choices=["ddp", "zero", "fsdp", "auto"],
                     help="ddp (replicated AdamW after bucketed all-reduce) | zero (ZeRO-1/2 sharded AdamW) | "
-                         "auto (zero for N>1)")
+                         "fsdp (ZeRO-3: parameters sharded, per-block all-gather) | auto (zero for N>1)")
     ap.add_argument("--grad-reduce-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="dtype of the gradient collective (fp32 = torch DDP-under-AMP parity)")
     ap.add_argument("--overlap-optimizer", action="store_true",
@@ -97,8 +97,11 @@ def main():
                 "launch": "torchrun" if external else "TorchTrainer worker actors",
                 "tokens_per_step": args.micro_batch * world * args.seq_len,
                 "optimizer": "AdamW fp32 master (fused HIP)",
-                "data_parallel": ("DDP: bucketed RCCL all-reduce, replicated fused AdamW" if m.get("parallel") == "ddp"
-                                  else "DDP with ZeRO-sharded AdamW: bucketed reduce-scatter + all-gather"),
+                "data_parallel": {
+                    "ddp": "DDP: bucketed RCCL all-reduce, replicated fused AdamW",
+                    "zero": "DDP with ZeRO-sharded AdamW: bucketed reduce-scatter + all-gather",
+                    "fsdp": "ZeRO-3: per-block all-gather of sharded weights, reduce-scatter of grads",
+                }.get(m.get("parallel"), m.get("parallel")),
             },
             "extra": {
                 "loss": round(m["loss"], 4),

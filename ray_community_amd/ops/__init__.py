@@ -298,7 +298,11 @@ def grad_sumsq(tensors, out=None):
         return torch.zeros((), dtype=torch.float32)
     dev = tensors[0].device
     if not tensors[0].is_cuda:
-        return sum(t.float().pow(2).sum() for t in tensors)
+        s = sum(t.float().pow(2).sum() for t in tensors)
+        if out is None:
+            return s
+        out.reshape(-1)[0] = s
+        return out
     out = torch.zeros(1, device=dev, dtype=torch.float32) if out is None else out
     part = _workspace(dev, "sumsq", 1024)
     L = lib()

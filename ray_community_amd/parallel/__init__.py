@@ -4,5 +4,7 @@ from .flat import FlatParameters
 from .ddp import DistributedDataParallel
 from .optim import FlatAdamW, FlatSGD
 from .fsdp import ShardedAdamW, ShardedDataParallel
+from .fully_sharded import FullyShardedAdamW, FullyShardedDataParallel, estimate_memory_gb
 
-__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW", "FlatSGD", "ShardedDataParallel", "ShardedAdamW"]
+__all__ = ["FlatParameters", "DistributedDataParallel", "FlatAdamW", "FlatSGD", "ShardedDataParallel", "ShardedAdamW",
+           "FullyShardedDataParallel", "FullyShardedAdamW", "estimate_memory_gb"]

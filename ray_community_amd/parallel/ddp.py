@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .flat import FlatParameters
+from .flat import FlatParameters, register_grad_ready
 
 
 class DistributedDataParallel(nn.Module):
@@ -56,9 +56,7 @@ class DistributedDataParallel(nn.Module):
             if broadcast_buffers:
                 for b in module.buffers():
                     dist.broadcast(b, src=src, group=process_group)
-            for p in self.flat.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-                p._rca_grad_ready = self._on_grad  # fused-wgrad linears bypass AccumulateGrad
+            self._hooks += register_grad_ready(self.flat.params, self._on_grad)
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):

@@ -25,6 +25,34 @@ def _round_up(n, a=ALIGN):
     return (n + a - 1) // a * a
 
 
+def register_grad_ready(params, fn) -> list:
+    """Call ``fn(p)`` exactly once per backward when ``p``'s gradient is final.
+
+    Two sources report readiness: the post-accumulate-grad hook (AccumulateGrad), and the
+    fused-wgrad linears (``parallel/fused_linear.py``), which write dW straight into the flat
+    buffer and call ``p._rca_grad_ready``. The engine still runs the leaf's AccumulateGrad node
+    (with an undefined gradient) after such a backward, so its hook fires too; the callback marks
+    the parameter so that the hook call that follows is swallowed instead of counted twice.
+    """
+
+    def on_accumulate(p):
+        if getattr(p, "_rca_grad_counted", False):
+            p._rca_grad_counted = False
+            return
+        fn(p)
+
+    def on_fused(p):
+        p._rca_grad_counted = True
+        fn(p)
+
+    handles = []
+    for p in params:
+        handles.append(p.register_post_accumulate_grad_hook(on_accumulate))
+        p._rca_grad_ready = on_fused
+        p._rca_grad_counted = False
+    return handles
+
+
 def default_no_decay(name: str, p: torch.Tensor) -> bool:
     return p.dim() < 2 or name.endswith(".bias")
 

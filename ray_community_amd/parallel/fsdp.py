@@ -33,7 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import ops
-from .flat import ALIGN, FlatParameters
+from .flat import ALIGN, FlatParameters, register_grad_ready
 
 
 class ShardedDataParallel(nn.Module):
@@ -60,9 +60,7 @@ class ShardedDataParallel(nn.Module):
             if broadcast_buffers:
                 for b in module.buffers():
                     dist.broadcast(b, src=src, group=process_group)
-            for p in self.flat.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-                p._rca_grad_ready = self._on_grad
+            self._hooks += register_grad_ready(self.flat.params, self._on_grad)
         # forward pre-hooks: wait for the all-gathers of the buckets this module's own params live in
         self._module_buckets: Dict[int, List[int]] = {}
         for m in module.modules():

@@ -26,7 +26,9 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
                          overlap_optimizer=False, **model_overrides):
     """``parallel``: "ddp" (replicated AdamW after a bucketed all-reduce; the default, as the
     headline metric is DDP), "zero" (reduce-scatter, sharded AdamW, all-gather overlapped with the
-    next forward — parallel/fsdp.py) or "auto" (zero when world > 1: the AdamW pass, ~9 % of a
+    next forward — parallel/fsdp.py), "fsdp" (ZeRO-3: parameters sharded too, each block's weights
+    all-gathered just in time and freed after use -- parallel/fully_sharded.py; what lets
+    ``llama3-70b`` train on 8 GPUs) or "auto" (zero when world > 1: the AdamW pass, ~9 % of a
     1-GPU step, shrinks by 1/world). ``grad_reduce_dtype``: "bf16" (gradients reduced in the
     compute dtype) or "fp32" (widened to fp32 before the collective, torch-DDP-under-AMP parity).
     ``overlap_optimizer`` (DDP): the HBM-bound AdamW update runs bucket by bucket on a side stream
@@ -34,7 +36,8 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
     8B step it measured 368 vs 366 ms serial -- the forward's 256-VGPR GEMM workgroups fill every
     SIMD, so AdamW waves cannot be co-resident and only time-slice with them."""
     from ..models import build_llama
-    from ..parallel import DistributedDataParallel, FlatAdamW, ShardedAdamW, ShardedDataParallel
+    from ..parallel import (DistributedDataParallel, FlatAdamW, FullyShardedAdamW, FullyShardedDataParallel,
+                            ShardedAdamW, ShardedDataParallel)
 
     device = device or torch.device("cuda", torch.cuda.current_device())
     rank, world = _dist_info()
@@ -46,6 +49,9 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
     if parallel == "zero":
         ddp = ShardedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt)
         opt = ShardedAdamW(ddp, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
+    elif parallel == "fsdp":
+        ddp = FullyShardedDataParallel(net, reduce_dtype=rdt)
+        opt = FullyShardedAdamW(ddp, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
     elif parallel == "ddp":
         ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt)
         opt = FlatAdamW(ddp.flat, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)

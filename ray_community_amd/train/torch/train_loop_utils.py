@@ -36,7 +36,10 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True, parallel_
 
     ``parallel_strategy``: ``"ddp"`` (default) = the framework's bucketed RCCL DDP with flat
     gradient buckets (``ray_community_amd.parallel.DistributedDataParallel``); ``"torch_ddp"`` =
-    ``torch.nn.parallel.DistributedDataParallel``; ``"fsdp"`` = torch FSDP; ``None`` = no wrap.
+    ``torch.nn.parallel.DistributedDataParallel``; ``"fsdp"`` = torch FSDP; ``"zero3"`` = the
+    framework's ZeRO-3 (``parallel.FullyShardedDataParallel``: per-block RCCL all-gather /
+    reduce-scatter over flat shards; step it with ``parallel.FullyShardedAdamW`` and call
+    ``finish_gradient_sync()`` after backward); ``None`` = no wrap.
     """
     kw = dict(parallel_strategy_kwargs or {})
     if wrap_ddp is False:
@@ -57,6 +60,10 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True, parallel_
         if dev.type == "cuda":
             kw.setdefault("device_ids", [dev.index])
         return TDDP(model, **kw)
+    if parallel_strategy == "zero3":
+        from ...parallel import FullyShardedDataParallel
+
+        return FullyShardedDataParallel(model, **kw)
     if parallel_strategy == "fsdp":
         from torch.distributed.fsdp import FullyShardedDataParallel as FSDP
 

@@ -27,7 +27,8 @@ def _model(seed=0):
 def _worker(rank, world, port, mode, steps, out_dir, bucket_mb):
     import torch.distributed as dist
 
-    from ray_community_amd.parallel import DistributedDataParallel, FlatAdamW, ShardedAdamW, ShardedDataParallel
+    from ray_community_amd.parallel import (DistributedDataParallel, FlatAdamW, FullyShardedAdamW,
+                                            FullyShardedDataParallel, ShardedAdamW, ShardedDataParallel)
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -38,6 +39,9 @@ def _worker(rank, world, port, mode, steps, out_dir, bucket_mb):
     if mode == "zero":
         wrap = ShardedDataParallel(net, bucket_cap_mb=bucket_mb)
         opt = ShardedAdamW(wrap, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
+    elif mode.startswith("fsdp"):
+        wrap = FullyShardedDataParallel(net, reduce_dtype=torch.float32 if mode == "fsdp_f32" else None)
+        opt = FullyShardedAdamW(wrap, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
     else:
         wrap = DistributedDataParallel(net, bucket_cap_mb=bucket_mb)
         opt = FlatAdamW(wrap.flat, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
@@ -49,8 +53,9 @@ def _worker(rank, world, port, mode, steps, out_dir, bucket_mb):
         opt.zero_grad()
     if mode == "zero":
         wrap.wait_all_gathers()
+    sd = wrap.state_dict() if mode.startswith("fsdp") else net.state_dict()  # fsdp: collective gather
     if rank == 0:
-        torch.save({k: v.detach().clone() for k, v in net.state_dict().items()}, os.path.join(out_dir, f"{mode}.pt"))
+        torch.save({k: v.detach().clone() for k, v in sd.items()}, os.path.join(out_dir, f"{mode}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -72,11 +77,14 @@ def _single(steps, world):
     return {k: v.detach().clone() for k, v in net.state_dict().items()}
 
 
-@pytest.mark.parametrize("mode", ["ddp", "zero"])
-def test_data_parallel_matches_single_process(tmp_path, mode):
+@pytest.mark.parametrize("mode,bucket_mb", [("ddp", 0.05), ("ddp", 256.0), ("zero", 0.05), ("zero", 256.0),
+                                            ("fsdp", None), ("fsdp_f32", None)])
+def test_data_parallel_matches_single_process(tmp_path, mode, bucket_mb):
     world, steps = 2, 3
-    # tiny buckets -> many buckets, padding and out-of-order gathers are exercised
-    mp.spawn(_worker, args=(world, _port(), mode, steps, str(tmp_path), 0.05), nprocs=world, join=True)
+    # tiny buckets -> many buckets, padding and out-of-order gathers are exercised; one big bucket
+    # -> a bucket must wait for every gradient in it (fused-wgrad callback + AccumulateGrad hook
+    # both report a weight: counted once)
+    mp.spawn(_worker, args=(world, _port(), mode, steps, str(tmp_path), bucket_mb), nprocs=world, join=True)
     got = torch.load(os.path.join(tmp_path, f"{mode}.pt"), weights_only=True)
     ref = _single(steps, world)
     for k in ref:
