@@ -43,6 +43,8 @@ def main():
                     help="dtype of the gradient collective (fp32 = torch DDP-under-AMP parity)")
     ap.add_argument("--overlap-optimizer", action="store_true",
                     help="run the AdamW update per bucket on a side stream, overlapped with the next forward")
+    ap.add_argument("--fused-ce", type=int, default=None, choices=[0, 1],
+                    help="1: chunked lm_head + one-pass HIP cross-entropy (no T x V logits); default: model preset")
     ap.add_argument("--device", default="cuda", help="cuda (the benchmark) | cpu (gloo rehearsal of the launch path)")
     args = ap.parse_args()
 
@@ -61,6 +63,8 @@ def main():
                    "steps": args.steps, "warmup": args.warmup, "bucket_cap_mb": args.bucket_mb, "parallel": args.parallel,
                    "grad_reduce_dtype": args.grad_reduce_dtype, "device": args.device,
                    "overlap_optimizer": args.overlap_optimizer}
+    if args.fused_ce is not None:
+        loop_config["model_overrides"] = {"fused_ce": bool(args.fused_ce)}
     if not external and args.device == "cpu":
         ray.init(num_cpus=max(2, args.gpus), include_dashboard=False)
     # self-launched: TorchTrainer starts N worker actors (one per GPU, RCCL group over xGMI);

@@ -6,7 +6,8 @@ MI355X-first layout choices:
   * fused gate|up projection feeding the HIP SwiGLU kernel;
   * residual add fused into the following RMSNorm (HIP kernel emits both the new residual
     stream and the normalised activations; its backward adds the residual gradient);
-  * HIP cross-entropy writing dlogits in place over the 128k-vocab logits;
+  * HIP cross-entropy writing dlogits in place over the 128k-vocab logits, or (``fused_ce``)
+    lm_head + CE fused chunk by chunk so the T x 128k logits are never materialised;
   * activations kept resident (no recomputation) — 288 GB HBM holds a full 8B replica with
     fp32 master weights + AdamW states + seq-4096 activations per GPU.
 Attention is the framework's own MFMA flash-attention HIP kernels (``ops.attention``: causal,
@@ -40,6 +41,8 @@ class LlamaConfig:
     init_std: float = 0.02
     name: str = "llama"
     attn_impl: str = "hip"  # "hip" (gfx950 flash attention kernels) | "sdpa" (torch SDPA / aotriton)
+    fused_ce: bool = False  # chunked lm_head + one-pass HIP CE (parallel/fused_linear.py): no T x V logits
+    ce_chunk: int = 0       # tokens per fused-CE chunk (0: <= 1 GiB of logits per chunk)
 
     @property
     def head_dim(self) -> int:
@@ -178,6 +181,12 @@ class Llama(nn.Module):
 
     def forward(self, tokens, labels=None, positions=None):
         h = self.hidden_states(tokens, positions)
+        if labels is not None and self.cfg.fused_ce and h.is_cuda:
+            if self.lm_head is not None:  # through the module call so wrapper hooks still fire
+                return self.lm_head(h, labels=labels.reshape(-1), ce_chunk=self.cfg.ce_chunk)
+            from ..parallel.fused_linear import linear_cross_entropy
+
+            return linear_cross_entropy(h, self.embed.weight, labels.reshape(-1), chunk_tokens=self.cfg.ce_chunk)
         logits = self.logits(h)
         if labels is None:
             return logits.view(*tokens.shape, -1)

@@ -278,6 +278,24 @@ def cross_entropy(logits, labels, ignore_index: int = -100, reduction: str = "me
     return rows.sum() / n
 
 
+def ce_fused_(logits, labels, gscale, ignore_index: int = -100):
+    """One-pass HIP cross-entropy over 2-D bf16 ``logits``: returns per-row losses (fp32) and
+    overwrites ``logits`` with ``gscale * (softmax - onehot)`` (ignored rows -> 0). ``gscale`` is
+    a 1-element fp32 device tensor. Needs V % 8 == 0 and V <= 131072."""
+    T, V = logits.shape
+    assert logits.is_contiguous() and logits.dtype == torch.bfloat16
+    labels = labels.contiguous().to(torch.int64)
+    loss = torch.empty(T, device=logits.device, dtype=torch.float32)
+    lse = torch.empty(T, device=logits.device, dtype=torch.float32)
+    check(lib().rca_ce_fused(logits.data_ptr(), labels.data_ptr(), gscale.data_ptr(), loss.data_ptr(), lse.data_ptr(),
+                             T, V, ignore_index, stream_ptr(logits.device)), "ce_fused")
+    return loss
+
+
+def ce_fused_supported(V: int) -> bool:
+    return V % 8 == 0 and 0 < V <= 131072
+
+
 # ----------------------------------------------------------------------------------- grad norm
 _WS = {}
 

@@ -32,6 +32,7 @@ _SIGS = {
     "rca_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rca_ce_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_ll, c_void_p]),
     "rca_ce_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_ll, c_int, c_ll, c_void_p]),
+    "rca_ce_fused": (c_int, [c_void_p] * 5 + [c_ll, c_int, c_ll, c_void_p]),
     "rca_sumsq": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "rca_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float, c_float,
                           c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),

@@ -116,6 +116,108 @@ RCA_API int rca_ce_bwd(const void* logits, const long long* labels, const float*
   return (int)hipGetLastError();
 }
 
+// One-pass fused cross-entropy forward + backward for the fused linear-CE path: the row stays
+// in VGPRs (NPT 16-B vectors per thread, 1024 threads -> up to 131072 bf16 logits), so HBM sees
+// exactly one read and one write of the logits: (max, sum-exp) online per lane, one block
+// merge, then dlogits = g * (softmax - onehot) written over the logits. g = gscale[0] (a
+// device scalar, e.g. 1 / #valid labels: no host sync) or 0 for ignored rows. The label logit
+// is read before the block barrier, i.e. before any thread overwrites the row.
+template <int NPT>
+__global__ __launch_bounds__(1024) void ce_fused_kernel(bf16_t* __restrict__ logits, const long long* __restrict__ labels,
+                                                        const float* __restrict__ gscale, float* __restrict__ loss,
+                                                        float* __restrict__ lse_out, int V, long long ignore_index) {
+  __shared__ float sm[16], ss[16], bc[2];
+  const long long row = blockIdx.x;
+  bf16_t* x = logits + row * (long long)V;
+  const int nv = V >> 3;
+  const long long lab = labels[row];
+  const bool ign = (lab == ignore_index || lab < 0 || lab >= V);
+  float xlab = 0.f;
+  if (threadIdx.x == 0 && !ign) xlab = bf2f(x[lab]);
+  u32x4* xv = reinterpret_cast<u32x4*>(x);
+  u32x4 r[NPT];
+  float m = -INFINITY, s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int c = threadIdx.x + i * 1024;
+    if (c < nv) {
+      r[i] = __builtin_nontemporal_load(xv + c);
+      float f[8];
+      unpack8(r[i], f);
+      float vm = f[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) vm = fmaxf(vm, f[j]);
+      const float mn = fmaxf(m, vm);
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += __expf(f[j] - mn);
+      s = s * __expf(m - mn) + acc;
+      m = mn;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const float mn = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+    m = mn;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[wid] = m;
+    ss[wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = -INFINITY;
+    for (int i = 0; i < 16; ++i) M = fmaxf(M, sm[i]);
+    float S = 0.f;
+    for (int i = 0; i < 16; ++i) S += (sm[i] == -INFINITY) ? 0.f : ss[i] * __expf(sm[i] - M);
+    const float lse = M + __logf(S);
+    bc[0] = lse;
+    bc[1] = ign ? 0.f : gscale[0];
+    lse_out[row] = lse;
+    loss[row] = ign ? 0.f : lse - xlab;
+  }
+  __syncthreads();
+  const float L = bc[0], g = bc[1];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int c = threadIdx.x + i * 1024;
+    if (c < nv) {
+      float f[8];
+      unpack8(r[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p = __expf(f[j] - L);
+        if ((long long)(c * 8 + j) == lab) p -= 1.f;
+        f[j] = g * p;
+      }
+      xv[c] = pack8(f);
+    }
+  }
+}
+
+// Contract: V % 8 == 0, V <= 131072, 16-B aligned rows. Returns -1 when the shape is not covered.
+RCA_API int rca_ce_fused(void* logits, const long long* labels, const float* gscale, float* loss, float* lse,
+                         long long T, int V, long long ignore_index, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if ((V & 7) || V <= 0 || ((uintptr_t)logits & 15)) return -1;
+  const int nv = V >> 3;
+  const int npt = (nv + 1023) / 1024;
+#define RCA_CE(N)                                                                                          \
+  hipLaunchKernelGGL(ce_fused_kernel<N>, dim3((unsigned)T), dim3(1024), 0, stream, (bf16_t*)logits, labels, gscale, \
+                     loss, lse, V, ignore_index);                                                          \
+  return (int)hipGetLastError()
+  if (npt <= 1) { RCA_CE(1); }
+  if (npt <= 2) { RCA_CE(2); }
+  if (npt <= 4) { RCA_CE(4); }
+  if (npt <= 8) { RCA_CE(8); }
+  if (npt <= 16) { RCA_CE(16); }
+#undef RCA_CE
+  return -1;
+}
+
 // ----------------------------------------------------------------------------- grad norm
 // partial[b] = sum of squares of this block's grid-stride share; dtype 0 = bf16, 1 = f32
 template <int DT>

@@ -35,31 +35,129 @@ class _LinearWgradIntoFlat(torch.autograd.Function):
         w = ctx.weight
         g2 = gy.reshape(-1, gy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
-        # Reduction-contiguous operands: both backward products have their reduction dim as the
-        # OUTER dim of one (dgrad: W) or both (wgrad: gy, x) operands, which hipBLASLt runs at
-        # 0.93-1.33 PF/s at the 8B shapes; on transposed copies the same products run at
-        # 1.29-1.58 PF/s (scripts/gemm_layout.py). The copies come from one HBM-rate HIP pass each.
-        tr = _TRANSPOSED and ops.transpose_supported(g2) and ops.transpose_supported(x2) and ops.transpose_supported(w)
+        tr = _use_transposed(g2, x2, w)
         if ctx.needs_input_grad[0]:
             gx = F.linear(gy, ops.transpose(w)) if tr else torch.matmul(gy, w)
         else:
             gx = None
-        if tr:
-            a, b = ops.transpose(g2), ops.transpose(x2).t()
-        else:
-            a, b = g2.t(), x2
-        view = w.grad
-        if view is None or not getattr(w, "_rca_flat_grad", False) or view.dtype != g2.dtype:
-            return gx, torch.mm(a, b).to(w.dtype)  # plain autograd accumulation
-        if getattr(w, "_rca_grad_fresh", False):
-            torch.mm(a, b, out=view)
-            w._rca_grad_fresh = False
-        else:
-            view.addmm_(a, b)
-        cb = getattr(w, "_rca_grad_ready", None)
-        if cb is not None:
-            cb(w)
+        view = _flat_view(w, g2.dtype)
+        if view is None:
+            return gx, _wgrad(g2, x2, tr).to(w.dtype)  # plain autograd accumulation
+        _wgrad(g2, x2, tr, out=view, accumulate=not _take_fresh(w))
+        _notify(w)
         return gx, None
+
+
+def _use_transposed(g2, x2, w) -> bool:
+    # Reduction-contiguous operands: both backward products have their reduction dim as the
+    # OUTER dim of one (dgrad: W) or both (wgrad: gy, x) operands, which hipBLASLt runs at
+    # 0.93-1.33 PF/s at the 8B shapes; on transposed copies the same products run at
+    # 1.29-1.58 PF/s (scripts/gemm_layout.py). The copies come from one HBM-rate HIP pass each.
+    return _TRANSPOSED and ops.transpose_supported(g2) and ops.transpose_supported(x2) and ops.transpose_supported(w)
+
+
+def _wgrad(g2, x2, tr, out=None, accumulate=False):
+    """dW = g2^T @ x2 (into ``out``, accumulating when asked)."""
+    if tr:
+        a, b = ops.transpose(g2), ops.transpose(x2).t()
+    else:
+        a, b = g2.t(), x2
+    if out is None:
+        return torch.mm(a, b)
+    if accumulate:
+        return out.addmm_(a, b)
+    return torch.mm(a, b, out=out)
+
+
+def _flat_view(w, dtype):
+    """``w.grad`` when it is a fused-wgrad view into a flat gradient buffer of ``dtype``."""
+    view = w.grad
+    if view is None or not getattr(w, "_rca_flat_grad", False) or view.dtype != dtype:
+        return None
+    return view
+
+
+def _take_fresh(w) -> bool:
+    fresh = getattr(w, "_rca_grad_fresh", False)
+    if fresh:
+        w._rca_grad_fresh = False
+    return fresh
+
+
+def _notify(w):
+    cb = getattr(w, "_rca_grad_ready", None)
+    if cb is not None:
+        cb(w)
+
+
+class _FusedLinearCrossEntropy(torch.autograd.Function):
+    """mean CE(h @ W^T, labels) with the logits produced and consumed chunk by chunk.
+
+    The loss is the last op of the step, so its gradients are computed in FORWARD while each
+    logits chunk is hot: lm_head GEMM (hipBLASLt) -> one-pass HIP CE kernel that overwrites the
+    chunk with ``(softmax - onehot) / n_valid`` -> dgrad (dh chunk) and wgrad (accumulated dW)
+    GEMMs. Backward only scales by the incoming gradient (a device scalar: no host sync).
+    Peak extra memory: one ``chunk x V`` bf16 logits buffer + dW, instead of the full ``T x V``
+    logits plus their gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, h, weight, labels, ignore_index, chunk):
+        T, H = h.shape
+        V = weight.shape[0]
+        labels = labels.reshape(-1)
+        valid = labels != ignore_index
+        inv_n = (1.0 / valid.sum().clamp_min(1).float()).reshape(1)
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        rows = torch.empty(T, device=h.device, dtype=torch.float32)
+        dh = torch.empty_like(h) if need_h else None
+        dw = torch.empty_like(weight) if need_w else None
+        buf = torch.empty(min(chunk, T), V, device=h.device, dtype=h.dtype)
+        wt = ops.transpose(weight) if (need_h and _TRANSPOSED and ops.transpose_supported(weight)) else None
+        for i, c0 in enumerate(range(0, T, chunk)):
+            c1 = min(T, c0 + chunk)
+            hc, lg = h[c0:c1], buf[: c1 - c0]
+            torch.mm(hc, weight.t(), out=lg)
+            rows[c0:c1] = ops.ce_fused_(lg, labels[c0:c1], inv_n, ignore_index)
+            if need_h:
+                if wt is not None:
+                    torch.mm(lg, wt.t(), out=dh[c0:c1])
+                else:
+                    torch.mm(lg, weight, out=dh[c0:c1])
+            if need_w:
+                _wgrad(lg, hc, _use_transposed(lg, hc, weight), out=dw, accumulate=i > 0)
+        ctx.save_for_backward(dh, dw)
+        ctx.weight = weight
+        return rows.sum() * inv_n[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        dh, dw = ctx.saved_tensors
+        w = ctx.weight
+        gh = dh.mul_(g) if dh is not None else None
+        if dw is None:
+            return gh, None, None, None, None
+        view = _flat_view(w, dw.dtype)
+        if view is None:
+            return gh, dw.mul_(g), None, None, None
+        if _take_fresh(w):
+            torch.mul(dw, g, out=view)
+        else:
+            view.addcmul_(dw, g.reshape(1, 1).to(dw.dtype))
+        _notify(w)
+        return gh, None, None, None, None
+
+
+def linear_cross_entropy(h, weight, labels, ignore_index: int = -100, chunk_tokens: int = 0):
+    """Mean cross-entropy of ``h @ weight.T`` against ``labels`` without materialising the full
+    logits (GPU: chunked, fused HIP CE; CPU: the plain PyTorch reference).
+    ``chunk_tokens`` = 0 picks chunks of <= 1 GiB of bf16 logits."""
+    V = weight.shape[0]
+    if not h.is_cuda or not ops.ce_fused_supported(V) or h.dtype != torch.bfloat16:
+        return F.cross_entropy(F.linear(h, weight).float(), labels.reshape(-1), ignore_index=ignore_index)
+    if chunk_tokens <= 0:
+        chunk_tokens = max(256, (1 << 30) // (2 * V) // 256 * 256)
+    return _FusedLinearCrossEntropy.apply(h.contiguous(), weight, labels, ignore_index, int(chunk_tokens))
 
 
 class FusedWgradLinear(nn.Linear):
@@ -71,7 +169,11 @@ class FusedWgradLinear(nn.Linear):
         super().__init__(in_features, out_features, bias=False, device=device, dtype=dtype)
         self.weight._rca_fused_wgrad = True
 
-    def forward(self, x):
+    def forward(self, x, labels=None, ignore_index: int = -100, ce_chunk: int = 0):
+        """``labels`` given: returns the mean cross-entropy of ``x @ W^T`` through the fused,
+        chunked linear + CE path (the full logits are never materialised)."""
+        if labels is not None:
+            return linear_cross_entropy(x, self.weight, labels, ignore_index, ce_chunk)
         if torch.is_grad_enabled() and self.weight.requires_grad and getattr(self.weight, "_rca_flat_grad", False):
             return _LinearWgradIntoFlat.apply(x, self.weight)
         return F.linear(x, self.weight)

@@ -156,7 +156,7 @@ def test_bench_fsdp_two_workers_cpu(tmp_path):
 
 @pytest.mark.gpu
 def test_fsdp_world1_gpu_matches_ddp():
-    """bf16 on the GPU through the fused HIP AdamW: ZeRO-3 at world 1 == DDP + FlatAdamW."""
+    """bf16 on the GPU through the fused HIP AdamW: ZeRO-3 at world 1 ~= DDP + FlatAdamW."""
     from ray_community_amd.models import build_llama
     from ray_community_amd.parallel import (DistributedDataParallel, FlatAdamW, FullyShardedAdamW,
                                             FullyShardedDataParallel)
@@ -182,5 +182,10 @@ def test_fsdp_world1_gpu_matches_ddp():
         torch.cuda.synchronize()
         sd = w.state_dict() if mode == "fsdp" else {k: v.detach().cpu() for k, v in net.state_dict().items()}
         out.append(sd)
+    # not bitwise: the embedding backward accumulates with atomics and the grad-norm sum runs over
+    # a different buffer layout -> last-bit gradient differences, which AdamW can turn into at most
+    # ~2 * lr per step on near-zero-gradient elements, plus one bf16 ulp of the rounded weight
     for k in out[0]:
-        assert torch.equal(out[0][k].cpu(), out[1][k].cpu()), k
+        a, b = out[0][k].float().cpu(), out[1][k].float().cpu()
+        d = (a - b).abs()
+        assert (d <= 3 * 2 * 1e-3 + a.abs() * 2 ** -7).all() and d.mean() < 1e-4, (k, d.max(), d.mean())
