@@ -137,7 +137,18 @@ def _remote_fn(f, opts):
     return RemoteFunction(f, {"num_returns": 2, **opts})
 
 
-def source_stage(inputs, window: int) -> Iterator[Tuple[Any, Any]]:
+def _admit(rm, op, q) -> bool:
+    """May ``op`` launch another task now? With nothing queued for downstream it waits for
+    capacity instead of stalling the pipeline (resource_manager.py)."""
+    if rm is None or rm.can_submit(op):
+        return True
+    if q:
+        return False
+    rm.wait_for_capacity(op)
+    return True
+
+
+def source_stage(inputs, window: int, rm=None, op=None) -> Iterator[Tuple[Any, Any]]:
     """inputs: list of ("ref", block_ref, meta_ref_or_None) or ("read", fn)."""
     rf = None
     q = collections.deque()
@@ -153,34 +164,47 @@ def source_stage(inputs, window: int) -> Iterator[Tuple[Any, Any]]:
             if x[0] == "ref":
                 q.append((x[1], x[2]))
             else:
+                if not _admit(rm, op, q):
+                    it = itertools.chain([x], it)
+                    break
                 if rf is None:
                     rf = _remote_fn(_read_task, {"num_cpus": 1})
                 b, m = rf.remote(x[1])
+                if rm is not None:
+                    rm.on_submit(op, m)
                 q.append((b, m))
         if not q:
             return
         yield q.popleft()
 
 
-def task_map_stage(upstream, ops, window: int, remote_opts: Dict) -> Iterator:
+def task_map_stage(upstream, ops, window: int, remote_opts: Dict, rm=None, op=None) -> Iterator:
     rf = _remote_fn(_run_chain, remote_opts)
     q = collections.deque()
     exhausted = False
+    held = None  # upstream output pulled but not yet admitted (pulling may launch upstream work)
     while True:
         while not exhausted and len(q) < window:
-            try:
-                b, _ = next(upstream)
-            except StopIteration:
-                exhausted = True
+            if held is None:
+                try:
+                    held = next(upstream)
+                except StopIteration:
+                    exhausted = True
+                    break
+            if not _admit(rm, op, q):
                 break
-            q.append(rf.remote(b, ops))
+            b, held = held[0], None
+            refs = rf.remote(b, ops)
+            if rm is not None:
+                rm.on_submit(op, refs[1])
+            q.append(refs)
         if not q:
             return
         yield tuple(q.popleft())
 
 
 def actor_map_stage(upstream, op, ops_before, ops_after, pool_size: int, actor_opts: Dict,
-                    max_in_flight: int = 4) -> Iterator:
+                    max_in_flight: int = 4, rm=None, rm_op=None) -> Iterator:
     from ..._private.worker import kill, wait
     from ...actor import ActorClass
 
@@ -202,6 +226,8 @@ def actor_map_stage(upstream, op, ops_before, ops_after, pool_size: int, actor_o
                     exhausted = True
                     break
                 refs = actors[i].process.options(num_returns=2).remote(b)
+                if rm is not None:
+                    rm.on_submit(rm_op, refs[1])
                 load[i] += 1
                 q.append((i, refs))
             if not q:

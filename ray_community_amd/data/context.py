@@ -5,8 +5,18 @@ import threading
 from dataclasses import dataclass, field
 
 
+def _no_limits():
+    from ._internal.resource_manager import ExecutionResources
+
+    return ExecutionResources()
+
+
 @dataclass
 class ExecutionOptions:
+    """``resource_limits``: caps for the streaming executor (``ExecutionResources(cpu=, gpu=,
+    object_store_memory=)``; None = the cluster's CPUs/GPUs and
+    ``object_store_memory_limit_fraction`` of its object store)."""
+    resource_limits: object = field(default_factory=_no_limits)
     preserve_order: bool = True
     locality_with_output: bool = False
     verbose_progress: bool = False
@@ -19,6 +29,9 @@ class DataContext:
     execution_options: ExecutionOptions = field(default_factory=ExecutionOptions)
     enable_progress_bars: bool = False
     use_push_based_shuffle: bool = False
+    object_store_memory_limit_fraction: float = 0.5
+    op_resource_reservation_ratio: float = 0.5
+    last_execution_stats: object = None  # ResourceManager.stats() of the most recent execution
 
     _current = None
     _lock = threading.Lock()

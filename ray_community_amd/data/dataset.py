@@ -74,19 +74,37 @@ class Dataset:
         _ensure_init()
         if self._materialized is not None:
             return iter(self._materialized)
+        from .context import DataContext
+        from ._internal.resource_manager import ResourceManager
+
+        ctx = DataContext.get_current()
+        rm = ResourceManager.from_context(ctx)
+        ctx.last_execution_stats = rm
+        self._exec_rm = rm
         window = max(2, 2 * _cpus())
-        it = X.source_stage(self._inputs, window)
+        it = X.source_stage(self._inputs, window, rm, rm.register("Read", cpu=1))
+
+        def task_stage(it, ops):
+            opts = _task_opts(ops)
+            caps = [o.get("concurrency") for o in ops if isinstance(o.get("concurrency"), int)]
+            name = "->".join(_op_name(o) for o in ops)
+            st = rm.register(name, cpu=opts.get("num_cpus", 1) or 0, gpu=opts.get("num_gpus", 0) or 0,
+                             concurrency_cap=min(caps) if caps else None)
+            return X.task_map_stage(it, ops, window, opts, rm, st)
+
         pending_tasks: List[Dict] = []
         for op in self._ops:
             if op["kind"] in _MAP_KINDS and op.get("compute") != "actors":
                 pending_tasks.append(op)
                 continue
             if pending_tasks:
-                it = X.task_map_stage(it, pending_tasks, window, _task_opts(pending_tasks))
+                it = task_stage(it, pending_tasks)
                 pending_tasks = []
             if op["kind"] in _MAP_KINDS:  # actor pool stage
+                st = rm.register(_op_name(op) + "(actors)", concurrency_cap=op["pool_size"] *
+                                 op.get("max_tasks_in_flight_per_actor", 4))
                 it = X.actor_map_stage(it, op, [], [], op["pool_size"], op["actor_opts"],
-                                       op.get("max_tasks_in_flight_per_actor", 4))
+                                       op.get("max_tasks_in_flight_per_actor", 4), rm, st)
             elif op["kind"] == "limit":
                 it = X.limit_stage(it, op["n"])
             elif op["kind"] == "alltoall":
@@ -95,7 +113,7 @@ class Dataset:
             else:
                 raise ValueError(op["kind"])
         if pending_tasks:
-            it = X.task_map_stage(it, pending_tasks, window, _task_opts(pending_tasks))
+            it = task_stage(it, pending_tasks)
         return it
 
     def _refs(self) -> List[Tuple[Any, Any]]:
@@ -444,8 +462,23 @@ class Dataset:
     # ------------------------------------------------------------------ misc
     def stats(self) -> str:
         ms = self._metas()
-        return (f"Dataset: {len(ms)} blocks, {sum(m['num_rows'] for m in ms)} rows, "
-                f"{sum(m['size_bytes'] for m in ms) / 2**20:.2f} MiB")
+        out = (f"Dataset: {len(ms)} blocks, {sum(m['num_rows'] for m in ms)} rows, "
+               f"{sum(m['size_bytes'] for m in ms) / 2**20:.2f} MiB")
+        rm = getattr(self, "_exec_rm", None)
+        if rm is not None:
+            st = rm.stats()
+            for o in st["ops"]:
+                out += (f"\n  Operator {o['name']}: {o['tasks']} tasks, peak {o['peak_running']} concurrent, "
+                        f"backpressured {o['backpressured']}x, {o['output_bytes'] / 2**20:.2f} MiB out")
+        return out
+
+    def _execution_stats(self) -> Optional[Dict]:
+        """Resource-manager counters of this dataset's last execution (limits, peaks, per op)."""
+        rm = getattr(self, "_exec_rm", None)
+        if rm is None:
+            return None
+        rm.poll()
+        return rm.stats()
 
     def __repr__(self):
         return f"Dataset(num_ops={len(self._ops)}, materialized={self._materialized is not None})"
@@ -470,6 +503,13 @@ class MaterializedDataset(Dataset):
 
 
 # ---------------------------------------------------------------------------------- helpers
+def _op_name(op) -> str:
+    fn = op.get("fn")
+    n = getattr(fn, "__name__", None) or type(fn).__name__ if fn is not None else None
+    k = {"map_batches": "MapBatches", "map": "Map", "flat_map": "FlatMap", "filter": "Filter"}.get(op["kind"], op["kind"])
+    return f"{k}({n})" if n else k
+
+
 def _compute(op, fn, compute, concurrency, ctor_args, ctor_kwargs, num_cpus, num_gpus, ray_remote_args):
     is_class = inspect.isclass(fn)
     use_actors = is_class or isinstance(compute, ActorPoolStrategy) or compute == "actors"
@@ -504,6 +544,8 @@ def _compute(op, fn, compute, concurrency, ctor_args, ctor_kwargs, num_cpus, num
             op["fn"] = _Wrap
     else:
         op["compute"] = "tasks"
+        if isinstance(concurrency, int):
+            op["concurrency"] = concurrency  # task-pool concurrency cap (backpressure policy)
     return op
 
 
