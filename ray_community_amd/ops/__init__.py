@@ -29,6 +29,7 @@ __all__ = [
     "standardize_",
     "batched_concat",
     "image_normalize",
+    "crop_resize_normalize",
     "batch_norm_act",
     "flash_attention",
     "flash_attention_qkv",
@@ -489,6 +490,40 @@ def image_normalize(u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), d
     check(lib().rca_image_normalize(u8.data_ptr(), out.data_ptr(), N, H, W, C, ctypes.cast(ma, ctypes.c_void_p),
                                     ctypes.cast(sa, ctypes.c_void_p), 0 if dtype == torch.bfloat16 else 1,
                                     1 if channels_last else 0, stream_ptr(u8.device)), "image_normalize")
+    return out
+
+
+def crop_resize_normalize(u8, boxes, size, flips=None, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
+                          dtype=torch.bfloat16, channels_last: bool = False):
+    """Fused per-image crop -> bilinear resize -> optional h-flip -> normalise (one HIP pass).
+
+    ``u8``: uint8 [N, H, W, C]; ``boxes``: int [N, 4] = (y0, x0, h, w); ``flips``: bool/uint8 [N]
+    or None; ``size``: (Ho, Wo). Returns [N, C, Ho, Wo] (channels_last: same logical shape in
+    NHWC memory) on ``u8``'s device."""
+    Ho, Wo = (size, size) if isinstance(size, int) else tuple(size)
+    N, H, W, C = u8.shape
+    bx = torch.as_tensor(boxes, dtype=torch.int32).reshape(N, 4)
+    if ((bx[:, 0] < 0) | (bx[:, 1] < 0) | (bx[:, 2] < 1) | (bx[:, 3] < 1) | (bx[:, 0] + bx[:, 2] > H)
+            | (bx[:, 1] + bx[:, 3] > W)).any():
+        raise ValueError("crop boxes must lie inside the images")
+    if not u8.is_cuda:
+        out = ref.crop_resize_normalize_ref(u8, bx, flips, (Ho, Wo), mean, std, dtype)
+        return out.contiguous(memory_format=torch.channels_last) if channels_last else out
+    import ctypes
+
+    u8 = u8.contiguous()
+    bxd = bx.to(u8.device)
+    fl = None if flips is None else torch.as_tensor(flips).to(device=u8.device, dtype=torch.uint8).contiguous()
+    if channels_last:
+        out = torch.empty(N, Ho, Wo, C, device=u8.device, dtype=dtype).permute(0, 3, 1, 2)
+    else:
+        out = torch.empty(N, C, Ho, Wo, device=u8.device, dtype=dtype)
+    ma = (ctypes.c_float * 4)(*[float(m) for m in mean])
+    sa = (ctypes.c_float * 4)(*[float(s) for s in std])
+    check(lib().rca_crop_resize_normalize(u8.data_ptr(), out.data_ptr(), bxd.data_ptr(), _p(fl), N, H, W, C, Ho, Wo,
+                                          ctypes.cast(ma, ctypes.c_void_p), ctypes.cast(sa, ctypes.c_void_p),
+                                          0 if dtype == torch.bfloat16 else 1, 1 if channels_last else 0,
+                                          stream_ptr(u8.device)), "crop_resize_normalize")
     return out
 
 

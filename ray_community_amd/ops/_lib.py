@@ -43,6 +43,7 @@ _SIGS = {
     "rca_batched_copy": (c_int, [c_void_p, c_int, c_void_p, c_ll, c_void_p]),
     "rca_attn_fwd": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_ll] * 4 + [c_float, c_int, c_void_p]),
     "rca_attn_bwd": (c_int, [c_void_p] * 10 + [c_int] * 5 + [c_ll] * 8 + [c_float, c_int, c_void_p]),
+    "rca_crop_resize_normalize": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "rca_bn_workspace": (c_ll, [c_ll, c_int]),
     "rca_bn_fwd": (c_int, [c_void_p] * 9 + [c_ll, c_int, c_float, c_float, c_int, c_void_p]),
     "rca_bn_apply": (c_int, [c_void_p] * 4 + [c_ll, c_int, c_int, c_void_p]),

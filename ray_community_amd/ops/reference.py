@@ -81,6 +81,24 @@ def image_normalize_ref(u8, mean, std, dtype=torch.bfloat16):
     return ((x - m) / s).permute(0, 3, 1, 2).contiguous().to(dtype)
 
 
+def crop_resize_normalize_ref(u8, boxes, flips, size, mean, std, dtype=torch.float32):
+    """Per image: crop box (y0, x0, h, w) -> bilinear resize (align_corners=False) -> optional
+    horizontal flip -> /255, mean/std. uint8 [N, H, W, C] -> [N, C, Ho, Wo]."""
+    import torch.nn.functional as F
+
+    outs = []
+    m = torch.tensor(mean, dtype=torch.float32).view(-1, 1, 1)
+    s = torch.tensor(std, dtype=torch.float32).view(-1, 1, 1)
+    for n in range(u8.shape[0]):
+        y0, x0, h, w = (int(v) for v in boxes[n])
+        crop = u8[n, y0:y0 + h, x0:x0 + w, :].float().permute(2, 0, 1)[None]
+        r = F.interpolate(crop, size=tuple(size), mode="bilinear", align_corners=False, antialias=False)[0]
+        if flips is not None and bool(flips[n]):
+            r = r.flip(-1)
+        outs.append((r / 255.0 - m) / s)
+    return torch.stack(outs).to(dtype)
+
+
 def attention_ref(q, k, v, causal: bool = True, scale=None):
     """fp32 attention on ``[B, S, H, D]`` tensors (GQA by head repetition); returns q's dtype."""
     B, S, Hq, D = q.shape
