@@ -234,11 +234,14 @@ class DirectClient:
 
 
 class SocketClient:
-    """Framed RPC client over the head's Unix socket (workers and external drivers)."""
+    """Framed RPC client over the head's Unix socket (workers and external drivers), or over a
+    pre-connected stream socket (``sock``: the TCP link of a ``ray://`` remote driver)."""
 
-    def __init__(self, sock_path, kind, ident, on_message=None, register_extra=None):
-        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
-        s.connect(sock_path)
+    def __init__(self, sock_path, kind, ident, on_message=None, register_extra=None, sock=None):
+        if sock is None:
+            sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            sock.connect(sock_path)
+        s = sock
         self.conn = P.Connection(s)
         self._req = itertools.count(1)
         self._pending: Dict[int, concurrent.futures.Future] = {}

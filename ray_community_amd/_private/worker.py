@@ -92,7 +92,12 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
         if address in ("local", None):
             address = None
         ns = namespace if namespace is not None else ("" if address else "anon_" + os.urandom(4).hex())
-        if address is not None:
+        if address is not None and address.startswith("ray://"):
+            from ..util.client import connect as _client_connect
+
+            core, addr = _client_connect(address, ns)
+            _state.update(head=None, core=core, mode=SCRIPT_MODE, namespace=ns, address=addr, client_mode=True)
+        elif address is not None:
             sock = _resolve_address(address)
             ident = os.urandom(20)
             client = SocketClient(sock, "client", ident)
@@ -201,6 +206,12 @@ def shutdown(_exiting_interpreter: bool = False):
 
         tracing.enable_tracing(False)
         tracing.drain()
+        for srv in _state.pop("client_servers", []) or []:
+            try:
+                srv.stop()
+            except Exception:
+                pass
+        _state.pop("client_mode", None)
         dash = _state.pop("dashboard", None)
         if dash is not None:
             try:

@@ -82,6 +82,10 @@ def _run_head(args) -> int:
     from .._private.gc_tuning import tune_gc
 
     tune_gc()  # this process is a dedicated head: freeze the startup heap too
+    if getattr(args, "ray_client_server_port", None):
+        from ..util.client.server import serve
+
+        serve(f"{args.ray_client_server_host}:{args.ray_client_server_port}")
     stop = threading.Event()
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, lambda *_: stop.set())
@@ -114,7 +118,8 @@ def cmd_start(args) -> int:
     os.makedirs(root, exist_ok=True)
     log = open(os.path.join(root, "head.out"), "ab")
     cmd = [sys.executable, "-m", "ray_community_amd.scripts.scripts", "_run_head", "--temp-dir", root]
-    for flag in ("num_cpus", "num_gpus", "resources", "dashboard_port", "object_store_memory"):
+    for flag in ("num_cpus", "num_gpus", "resources", "dashboard_port", "object_store_memory",
+                 "ray_client_server_port", "ray_client_server_host"):
         v = getattr(args, flag)
         if v is not None:
             cmd += ["--" + flag.replace("_", "-"), str(v)]
@@ -366,6 +371,9 @@ def build_parser() -> argparse.ArgumentParser:
         sp.add_argument("--include-dashboard", action="store_true")
         sp.add_argument("--dashboard-port", type=int, default=None)
         sp.add_argument("--temp-dir", default=None)
+        sp.add_argument("--ray-client-server-port", type=int, default=None,
+                        help="serve ray:// drivers on this TCP port (reference default 10001)")
+        sp.add_argument("--ray-client-server-host", default="127.0.0.1")
 
     sp = sub.add_parser("start", help="start a head session")
     sp.add_argument("--head", action="store_true")
