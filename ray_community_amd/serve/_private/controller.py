@@ -222,6 +222,10 @@ class ServeController:
         meta = self.app_meta.get(app_name)
         return None if meta is None else meta["ingress"]
 
+    async def list_applications(self):
+        """{application name: ingress deployment} of every deployed application (gRPC routing)."""
+        return {app: m["ingress"] for app, m in self.app_meta.items()}
+
     async def list_routes(self):
         return {m["route_prefix"]: (app, m["ingress"]) for app, m in self.app_meta.items() if m["route_prefix"]}
 

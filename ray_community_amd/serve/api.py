@@ -11,7 +11,8 @@ from .._private import serialization as ser
 from ._private.controller import CONTROLLER_NAME, NAMESPACE, ServeController
 from .handle import DeploymentHandle, _HandleSpec
 
-_STATE = {"controller": None, "proxy": None, "http": {"host": "127.0.0.1", "port": 8000}}
+_STATE = {"controller": None, "proxy": None, "http": {"host": "127.0.0.1", "port": 8000}, "grpc": None,
+          "grpc_proxy": None}
 
 _DEP_OPTS = {"name", "num_replicas", "ray_actor_options", "max_ongoing_requests", "max_concurrent_queries",
              "autoscaling_config", "user_config", "health_check_period_s", "health_check_timeout_s",
@@ -137,10 +138,40 @@ def _get_controller():
     return c
 
 
-def start(http_options: Optional[Dict] = None, detached: bool = True, proxy_location=None, **kw):
+def start(http_options: Optional[Dict] = None, detached: bool = True, proxy_location=None, grpc_options=None, **kw):
+    """``grpc_options``: ``serve.config.gRPCOptions`` or a dict with ``port`` (and ``host``) and
+    ``grpc_servicer_functions`` (``add_<Service>Servicer_to_server`` callables or import paths)."""
     if http_options:
-        _STATE["http"].update({k: v for k, v in http_options.items() if k in ("host", "port")})
+        if not isinstance(http_options, dict):
+            http_options = {"host": getattr(http_options, "host", None), "port": getattr(http_options, "port", None)}
+        _STATE["http"].update({k: v for k, v in http_options.items() if k in ("host", "port") and v is not None})
+    if grpc_options is not None:
+        if not isinstance(grpc_options, dict):
+            grpc_options = {"host": getattr(grpc_options, "host", "127.0.0.1"), "port": grpc_options.port,
+                            "grpc_servicer_functions": list(grpc_options.grpc_servicer_functions)}
+        _STATE["grpc"] = {"host": grpc_options.get("host", "127.0.0.1"), "port": int(grpc_options.get("port", 9000)),
+                          "grpc_servicer_functions": list(grpc_options.get("grpc_servicer_functions", []))}
     _get_controller()
+    if _STATE["grpc"] is not None:
+        _ensure_grpc_proxy()
+
+
+def _ensure_grpc_proxy():
+    from .._private import worker as w
+    from ..actor import ActorClass
+    from ._private.grpc_proxy import gRPCProxy
+
+    if _STATE["grpc_proxy"] is not None or _STATE["grpc"] is None:
+        return
+    g = _STATE["grpc"]
+    try:
+        p = w.get_actor("SERVE_GRPC_PROXY_ACTOR", namespace=NAMESPACE)
+    except ValueError:
+        p = ActorClass(gRPCProxy, {"name": "SERVE_GRPC_PROXY_ACTOR", "namespace": NAMESPACE, "lifetime": "detached",
+                                   "num_cpus": 0, "max_concurrency": 100}).remote(
+            g["host"], g["port"], g["grpc_servicer_functions"])
+    _STATE["grpc_info"] = w.get(p.ready.remote())
+    _STATE["grpc_proxy"] = p
 
 
 def _ensure_proxy():
@@ -181,6 +212,8 @@ def run(target: Union[Application, Deployment], *, name: str = "default", route_
         raise RuntimeError(f"Deploying app '{name}' failed: {st.get(name)}")
     if http and route_prefix is not None:
         _ensure_proxy()
+    if _STATE["grpc"] is not None:
+        _ensure_grpc_proxy()
     handle = DeploymentHandle(ingress, name)
     if blocking:
         while True:
@@ -233,8 +266,19 @@ def shutdown():
         w.kill(p)
     except Exception:
         pass
+    try:
+        g = _STATE["grpc_proxy"]
+        if g is None and _STATE["grpc"] is not None:
+            g = w.get_actor("SERVE_GRPC_PROXY_ACTOR", namespace=NAMESPACE)
+        if g is not None:
+            w.get(g.shutdown.remote())
+            w.kill(g)
+    except Exception:
+        pass
     _STATE["controller"] = None
     _STATE["proxy"] = None
+    _STATE["grpc_proxy"] = None
+    _STATE["grpc"] = None
     from .handle import _Router
 
     _Router._routers.clear()
