@@ -12,6 +12,10 @@ model in ``torch.nn.parallel.DistributedDataParallel``. Here DDP is the framewor
     per-link bound, so a handful of large messages beats NVSwitch-style 25 MB buckets;
   * averaging is NOT a separate pass: the all-reduce is a SUM and ``grad_scale`` (1/world)
     is folded into the fused AdamW kernel;
+  * ``precompute_grad_norm``: each finished (and reduced) bucket's sum of squares is taken on a
+    side stream during the rest of backward, so the optimizer's global-norm clip needs no
+    extra pass over the gradients after backward (the 8B step's 16 GB read, ~3 ms, leaves the
+    critical path);
   * ``reduce_dtype=torch.float32`` (torch-DDP-under-AMP parity): each finished bf16 bucket is
     widened into a persistent fp32 reduce buffer (``flat.reduced_grad``, 4 B/param -- 32 GB for
     8B params, cheap against 288 GB of HBM) and all-reduced in fp32 (2x the wire bytes); the
@@ -32,7 +36,7 @@ from .flat import FlatParameters, register_grad_ready
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0, broadcast_buffers=True,
                  flat: Optional[FlatParameters] = None, average_in_optimizer: bool = True,
-                 auto_finalize: bool = False, reduce_dtype=None):
+                 auto_finalize: bool = False, reduce_dtype=None, precompute_grad_norm: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -50,12 +54,18 @@ class DistributedDataParallel(nn.Module):
         self.reduce_dtype = reduce_dtype or self.flat.grad.dtype
         if self.world > 1 and self.reduce_dtype != self.flat.grad.dtype:
             self.flat.reduced_grad = torch.zeros(self.flat.numel, dtype=self.reduce_dtype, device=self.flat.device)
+        self._norm = None
+        if precompute_grad_norm and self.flat.device.type == "cuda":
+            dev = self.flat.device
+            self._norm = {"stream": torch.cuda.Stream(device=dev), "sumsq": torch.zeros(1, device=dev),
+                          "partial": torch.empty(1024, device=dev), "n": 0, "done": torch.cuda.Event()}
         if self.world > 1:
             src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
             dist.broadcast(self.flat.data, src=src, group=process_group)
             if broadcast_buffers:
                 for b in module.buffers():
                     dist.broadcast(b, src=src, group=process_group)
+        if self.world > 1 or self._norm is not None:
             self._hooks += register_grad_ready(self.flat.params, self._on_grad)
 
     # ------------------------------------------------------------------ hooks
@@ -70,6 +80,23 @@ class DistributedDataParallel(nn.Module):
         if self._pending[bi] == 0:
             self._launch(bi)
 
+    def _launch_norm(self, bi, view):
+        """Sum of squares of a finished bucket, accumulated on the norm side stream."""
+        from ..ops._lib import check, lib
+
+        nm = self._norm
+        side = nm["stream"]
+        side.wait_stream(torch.cuda.current_stream(self.flat.device))
+        w = self._works[bi]
+        with torch.cuda.stream(side):
+            if w is not None:
+                w.wait()  # the side stream waits for the bucket's collective
+            self.flat.finalize_fresh_range(self.flat.buckets[bi])
+            dt = 0 if view.dtype == torch.bfloat16 else 1
+            check(lib().rca_sumsq(view.data_ptr(), view.numel(), dt, nm["partial"].data_ptr(), nm["sumsq"].data_ptr(),
+                                  1 if nm["n"] else 0, side.cuda_stream), "sumsq")
+        nm["n"] += 1
+
     def _launch(self, bi):
         b = self.flat.buckets[bi]
         view = self.flat.grad[b.start: b.end]
@@ -77,9 +104,12 @@ class DistributedDataParallel(nn.Module):
             wide = self.flat.reduced_grad[b.start: b.end]
             wide.copy_(view)
             view = wide
-        if not self.average_in_optimizer:
-            view.div_(self.world)
-        self._works[bi] = dist.all_reduce(view, group=self.pg, async_op=True)
+        if self.world > 1:
+            if not self.average_in_optimizer:
+                view.div_(self.world)
+            self._works[bi] = dist.all_reduce(view, group=self.pg, async_op=True)
+        if self._norm is not None:
+            self._launch_norm(bi, view)
 
     def forward(self, *args, **kwargs):
         if self._sync:
@@ -103,6 +133,13 @@ class DistributedDataParallel(nn.Module):
     def finish_gradient_sync(self):
         """Launch any bucket whose grads never arrived (unused params) and wait for all."""
         if self.world <= 1:
+            if self._norm is not None:
+                for bi in range(len(self.flat.buckets)):
+                    if self._pending[bi] > 0:  # unused params: their (zeroed) bucket still counts
+                        self.flat.finalize_fresh()
+                        self._launch(bi)
+                self._publish_norm()
+            self._pending = [len(b.params) for b in self.flat.buckets]
             return
         if any(w is None for w in self._works):
             self.flat.finalize_fresh()
@@ -114,6 +151,18 @@ class DistributedDataParallel(nn.Module):
                 w.wait()
             self._works[bi] = None
         self._pending = [len(b.params) for b in self.flat.buckets]
+        self._publish_norm()
+
+    def _publish_norm(self):
+        nm = self._norm
+        if nm is None or nm["n"] == 0:
+            return
+        if nm["n"] < len(self.flat.buckets):
+            nm["n"] = 0
+            return  # partial (e.g. no_sync micro-batches): the optimizer computes the norm itself
+        torch.cuda.current_stream(self.flat.device).wait_stream(nm["stream"])
+        self.flat.precomputed_sumsq = nm["sumsq"]
+        nm["n"] = 0
 
     @property
     def grad_scale(self) -> float:

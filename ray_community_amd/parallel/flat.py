@@ -133,6 +133,9 @@ class FlatParameters:
         # wider buffer the data-parallel wrappers reduce into (fp32 gradient reduction); when set,
         # optimizers read their gradients from it instead of ``grad``
         self.reduced_grad: Optional[torch.Tensor] = None
+        # device scalar: sum of squares of this step's final gradients, taken by the DDP wrapper
+        # bucket by bucket during backward; consumed (and cleared) by the optimizer step
+        self.precomputed_sumsq: Optional[torch.Tensor] = None
         self.buckets: List[Bucket] = [Bucket(i, s, e, ps) for i, (s, e, ps) in enumerate(bounds)]
         self.param_bucket = {}
         for b in self.buckets:
@@ -153,6 +156,14 @@ class FlatParameters:
         else:
             self.fused = []
             self.zero_start = 0
+
+    def finalize_fresh_range(self, bucket):
+        """``finalize_fresh`` restricted to one bucket's parameters."""
+        for p in bucket.params:
+            if getattr(p, "_rca_grad_fresh", False) and getattr(p, "_rca_flat_grad", False):
+                off = self.param_offset[id(p)]
+                self.grad[off: off + p.numel()].zero_()
+                p._rca_grad_fresh = False
 
     def finalize_fresh(self):
         """Zero the regions of fused weights that received no gradient since zero_grad."""

@@ -120,8 +120,12 @@ class FlatAdamW:
         flat.finalize_fresh()
         g = flat.step_grad
         clip = self.max_grad_norm if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
+        pre, flat.precomputed_sumsq = flat.precomputed_sumsq, None
         if clip or self.track_grad_norm:
-            ops.grad_sumsq([g], out=self._sumsq)
+            if pre is not None and pre.device == self._sumsq.device:
+                self._sumsq.copy_(pre)  # taken during backward (DistributedDataParallel precompute_grad_norm)
+            else:
+                ops.grad_sumsq([g], out=self._sumsq)
             self.last_grad_norm = self._sumsq  # sqrt taken lazily by grad_norm()
         self._grad_scale = grad_scale
         segs = [(0, flat.decay_end, self.wd), (flat.decay_end, flat.numel, 0.0)]

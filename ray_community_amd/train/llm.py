@@ -53,7 +53,8 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
         ddp = FullyShardedDataParallel(net, reduce_dtype=rdt)
         opt = FullyShardedAdamW(ddp, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
     elif parallel == "ddp":
-        ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt)
+        ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt,
+                                      precompute_grad_norm=max_grad_norm is not None and max_grad_norm > 0)
         opt = FlatAdamW(ddp.flat, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
         if overlap_optimizer:
             opt.overlap_with_forward(net)
