@@ -364,6 +364,7 @@ class CoreWorker:
         self.session_dir = session_dir
         self._refs: Dict[bytes, int] = {}
         self._ref_lock = threading.Lock()
+        self._ready_known = set()  # head-managed objects a wait() saw ready (dropped with the last ref)
         self.ctx = TaskContext()
         self.registered_functions = set()
         self.actor_id = None
@@ -398,6 +399,7 @@ class CoreWorker:
             else:
                 self._refs[oid] = n
         if n == 0:
+            self._ready_known.discard(oid)
             if oid in self.owned.objs and not self.owned.drop(oid):
                 return  # a caller-owned result the head never heard of
             self.client.ref_delta((), (oid,))
@@ -612,7 +614,15 @@ class CoreWorker:
         else:
             for o in local:  # mixed with head-managed refs: let the head track them all
                 self.owned.publish(o)
-            got = self.client.call("wait", ids, num_returns, timeout, fetch_local)
+            # objects seen ready by an earlier wait stay ready while referenced: polling a shrinking
+            # list (``ready, rest = wait(rest)``) is answered locally after one head round trip
+            rk = self._ready_known
+            known = [o for o in ids if o in rk]
+            if len(known) >= num_returns:
+                got = known
+            else:
+                got = self.client.call("wait", ids, num_returns, timeout, fetch_local, True)
+                rk.update(got)
         if len(got) > num_returns:
             got = got[:num_returns]
         rs = set(got)

@@ -907,7 +907,9 @@ class Head:
         self._on_blocked(w, True)
         d.add(lambda _d, w=w: self._on_blocked(w, False))
 
-    def rpc_wait(self, caller, oids, num_returns, timeout=None, fetch_local=True):
+    def rpc_wait(self, caller, oids, num_returns, timeout=None, fetch_local=True, all_ready=False):
+        """``all_ready``: when enough objects are already ready, return EVERY ready one (in input
+        order) so the caller can answer its next waits on the same list locally."""
         d = Deferred()
         objs = self.objects
         ready, pending = [], []
@@ -915,11 +917,14 @@ class Head:
             e = objs.get(o)
             if e is None or e.state != PENDING:
                 ready.append(o)
-                if len(ready) >= num_returns:  # result = the first num_returns ready, in order
+                if len(ready) >= num_returns and not all_ready:  # the first num_returns ready, in order
                     d.resolve(ready)
                     return d
             else:
                 pending.append(e)
+        if len(ready) >= num_returns:
+            d.resolve(ready)
+            return d
         if timeout == 0:
             d.resolve(ready)
             return d
