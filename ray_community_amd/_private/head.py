@@ -2013,6 +2013,42 @@ class Head:
                     tot[k] += v
         return dict(tot)
 
+    # ================================================================== autoscaler load
+    def rpc_resource_demands(self, caller):
+        """Unmet demand for the autoscaler: resource shapes of queued (not yet scheduled) tasks and
+        actors, and the bundles of pending placement groups (``[{res: amount}, ...]`` per group)."""
+        tasks = []
+        for ts in self.task_keys.values():
+            if ts.cancelled or ts.state in (T_CANCELLED,):
+                continue
+            d = {k: v for k, v in (ts.demand or {}).items() if v > 0 and "_group_" not in k and not k.startswith("node:")}
+            if d:
+                tasks.append(d)
+        pgs = []
+        for pg_id in self.pending_pgs:
+            pg = self.pgs.get(pg_id)
+            if pg is not None and pg["state"] == "PENDING":
+                pgs.append({"strategy": pg["strategy"],
+                            "bundles": [{k: float(v) for k, v in b.items() if v > 0} for b in pg["bundles"]]})
+        return {"tasks": tasks, "placement_groups": pgs}
+
+    def rpc_node_load(self, caller):
+        """Per alive node: totals, availability and whether any worker is executing work."""
+        totals, avail = self.sched.totals(), self.sched.available()
+        busy = collections.Counter()
+        for w in self.workers.values():
+            if not w.dead and (w.task is not None or w.actor is not None):
+                busy[w.node_id] += 1
+        out = []
+        for nid, n in self.nodes.items():
+            if not n.alive:
+                continue
+            clean = lambda r: {k: v for k, v in r.items() if "_group_" not in k and not k.startswith("node:")}  # noqa
+            out.append({"node_id": nid, "is_head": n.is_head, "labels": dict(n.labels or {}),
+                        "total": clean(totals.get(nid, n.resources)), "available": clean(avail.get(nid, {})),
+                        "busy_workers": busy[nid]})
+        return out
+
     def rpc_nodes(self, caller):
         totals = self.sched.totals()
         out = []

@@ -82,6 +82,14 @@ def _run_head(args) -> int:
     from .._private.gc_tuning import tune_gc
 
     tune_gc()  # this process is a dedicated head: freeze the startup heap too
+    asc = None
+    if getattr(args, "autoscaling_config", None):
+        import yaml
+
+        from ..autoscaler import StandardAutoscaler
+
+        with open(args.autoscaling_config) as f:
+            asc = StandardAutoscaler(yaml.safe_load(f)).start()
     if getattr(args, "ray_client_server_port", None):
         from ..util.client.server import serve
 
@@ -93,6 +101,8 @@ def _run_head(args) -> int:
     print(json.dumps({"address": sess.get("sock"), "pid": os.getpid(), "session": sess.get("session")}), flush=True)
     while not stop.wait(0.5):
         pass
+    if asc is not None:
+        asc.stop()
     ray.shutdown()
     try:
         cur = _read_session(_root(args))
@@ -119,7 +129,7 @@ def cmd_start(args) -> int:
     log = open(os.path.join(root, "head.out"), "ab")
     cmd = [sys.executable, "-m", "ray_community_amd.scripts.scripts", "_run_head", "--temp-dir", root]
     for flag in ("num_cpus", "num_gpus", "resources", "dashboard_port", "object_store_memory",
-                 "ray_client_server_port", "ray_client_server_host"):
+                 "ray_client_server_port", "ray_client_server_host", "autoscaling_config"):
         v = getattr(args, flag)
         if v is not None:
             cmd += ["--" + flag.replace("_", "-"), str(v)]
@@ -374,6 +384,9 @@ def build_parser() -> argparse.ArgumentParser:
         sp.add_argument("--ray-client-server-port", type=int, default=None,
                         help="serve ray:// drivers on this TCP port (reference default 10001)")
         sp.add_argument("--ray-client-server-host", default="127.0.0.1")
+        sp.add_argument("--autoscaling-config", default=None,
+                        help="YAML with available_node_types/min_workers/max_workers/idle_timeout_minutes: run the "
+                             "autoscaler over virtual nodes in the head process")
 
     sp = sub.add_parser("start", help="start a head session")
     sp.add_argument("--head", action="store_true")
