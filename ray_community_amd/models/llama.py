@@ -116,7 +116,13 @@ class MLP(nn.Module):
         self.down = FusedWgradLinear(cfg.intermediate_size, cfg.hidden_size)
 
     def forward(self, x):
-        return self.down(ops.swiglu(self.gate_up(x)))
+        gu = self.gate_up(x)
+        if gu.is_cuda and torch.is_grad_enabled() and getattr(self.down.weight, "_rca_flat_grad", False):
+            # SwiGLU also writes act^T (the down projection's wgrad operand) and, in backward,
+            # d(gate|up)^T for the gate_up wgrad: two transpose passes per layer folded away
+            act, act_t = ops.swiglu(gu, with_transposed=True)
+            return self.down(act, x_t=act_t)
+        return self.down(ops.swiglu(gu))
 
 
 class Block(nn.Module):

@@ -105,35 +105,88 @@ def rms_norm(x, weight, eps: float = 1e-5, residual=None):
 
 
 # ----------------------------------------------------------------------------------- SwiGLU
+# Transposed gradient side channel: a backward kernel that already has a gradient tile in
+# registers can also emit its transpose (one extra write instead of a later read + write
+# transpose pass). The consumer -- the weight GEMM of the linear that produced the forward input
+# (parallel/fused_linear.py) -- looks the transposed copy up by the gradient's storage pointer.
+_GRAD_T = {}
+
+
+def put_grad_transposed(g, gT):
+    import weakref
+
+    for k in [k for k, (r, _) in _GRAD_T.items() if r() is None]:  # producers' grads already freed
+        del _GRAD_T[k]
+    _GRAD_T[(g.data_ptr(), tuple(g.shape))] = (weakref.ref(g), gT)
+
+
+def pop_grad_transposed(g):
+    """The transposed copy a producer registered for gradient ``g`` (None if there is none). A
+    match needs the registered gradient to be alive (then its storage cannot have been reused)."""
+    if not _GRAD_T:
+        return None
+    hit = _GRAD_T.pop((g.data_ptr(), tuple(g.shape)), None)
+    if hit is None or hit[0]() is None:
+        return None
+    return hit[1]
+
+
+def _swiglu_tr_ok(gu) -> bool:
+    return gu.dim() == 2 and gu.shape[0] % 64 == 0 and (gu.shape[1] // 2) % 64 == 0 and gu.is_contiguous()
+
+
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, with_t):
         gu = gu.contiguous()
         F2 = gu.shape[-1]
         F = F2 // 2
         T = gu.numel() // F2
         out = torch.empty(*gu.shape[:-1], F, device=gu.device, dtype=gu.dtype)
-        check(lib().rca_swiglu_fwd(gu.data_ptr(), out.data_ptr(), T, F, stream_ptr(gu.device)), "swiglu_fwd")
+        ctx.tr = bool(with_t) and _swiglu_tr_ok(gu)
         ctx.save_for_backward(gu)
-        return out
+        ctx.set_materialize_grads(False)  # out^T gets no gradient: no [F, T] zero tensor per layer
+        if ctx.tr:
+            out_t = torch.empty(F, T, device=gu.device, dtype=gu.dtype)
+            check(lib().rca_swiglu_fwd_tr(gu.data_ptr(), out.data_ptr(), out_t.data_ptr(), T, F,
+                                          stream_ptr(gu.device)), "swiglu_fwd_tr")
+            ctx.mark_non_differentiable(out_t)
+            return out, out_t
+        check(lib().rca_swiglu_fwd(gu.data_ptr(), out.data_ptr(), T, F, stream_ptr(gu.device)), "swiglu_fwd")
+        return out, None
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, dout, _dout_t=None):
         (gu,) = ctx.saved_tensors
+        if dout is None:
+            return None, None
         F2 = gu.shape[-1]
         T = gu.numel() // F2
         dgu = torch.empty_like(gu)
         dout = dout.contiguous()
-        check(lib().rca_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), T, F2 // 2, stream_ptr(gu.device)),
-              "swiglu_bwd")
-        return dgu
+        if ctx.tr:
+            dgu_t = torch.empty(F2, T, device=gu.device, dtype=gu.dtype)
+            check(lib().rca_swiglu_bwd_tr(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), dgu_t.data_ptr(), T,
+                                          F2 // 2, stream_ptr(gu.device)), "swiglu_bwd_tr")
+            put_grad_transposed(dgu, dgu_t)
+        else:
+            check(lib().rca_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), T, F2 // 2,
+                                       stream_ptr(gu.device)), "swiglu_bwd")
+        return dgu, None
 
 
-def swiglu(gu):
-    """silu(gu[..., :F]) * gu[..., F:] for the fused gate|up projection output."""
+def swiglu(gu, with_transposed: bool = False):
+    """silu(gu[..., :F]) * gu[..., F:] for the fused gate|up projection output.
+
+    ``with_transposed=True`` (2-D, T and F multiples of 64, GPU) returns ``(out, out^T)``: the
+    transposed copy feeds the next linear's weight gradient, and the backward registers the
+    transposed input gradient for the producing linear (``pop_grad_transposed``). Otherwise
+    ``(out, None)`` is returned in that mode."""
     if gu.is_cuda:
-        return _SwiGLU.apply(gu)
-    return ref.swiglu_ref(gu)
+        out, out_t = _SwiGLU.apply(gu, with_transposed)
+        return (out, out_t) if with_transposed else out
+    out = ref.swiglu_ref(gu)
+    return (out, None) if with_transposed else out
 
 
 def transpose_supported(x) -> bool:

@@ -60,6 +60,93 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// SwiGLU with a transposed copy of its output(s) for the backward weight GEMMs (the wgrad of the
+// next linear needs its input reduction-contiguous: [F, T]). One 64 (tokens) x 64 (features)
+// tile per workgroup: the row-major result is stored directly, the tile is staged through LDS
+// (rows padded to 66 elements: conflict-free column gathers, as transpose_bf16_kernel) and
+// stored again transposed -- the transposed copy costs one extra write instead of a separate
+// read + write transpose pass.
+__device__ __forceinline__ void tile_put8(unsigned* tile32, int row, int col8, const float* v) {
+  constexpr int TP = 66;
+  unsigned* dst = tile32 + (row * TP + col8) / 2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dst[i] = (unsigned)f2bf(v[2 * i]) | ((unsigned)f2bf(v[2 * i + 1]) << 16);
+}
+
+// out_t[c0 + c][r0 .. r0+63] <- tile column c (64 rows), 8 rows per lane-chunk
+__device__ __forceinline__ void tile_store_t(const unsigned* tile32, bf16_t* out_t, long ldt, int r0, int c0, int t) {
+  constexpr int TP = 66;
+  const bf16_t* tile = reinterpret_cast<const bf16_t*>(tile32);
+  const int ch = t & 7, rr = t >> 3;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = rr + 32 * p;
+    u32x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (unsigned)tile[(ch * 8 + 2 * i) * TP + c] | ((unsigned)tile[(ch * 8 + 2 * i + 1) * TP + c] << 16);
+    *reinterpret_cast<u32x4*>(out_t + (long)(c0 + c) * ldt + r0 + ch * 8) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_fwd_tr_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out,
+                                                            bf16_t* __restrict__ out_t, int T, int F) {
+  __shared__ unsigned tile32[64 * 66 / 2];
+  const int tilesF = F >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = (bid / tilesF) << 6, c0 = (bid % tilesF) << 6;
+  const int t = threadIdx.x, ch = t & 7, rr = t >> 3;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = rr + 32 * p;
+    const bf16_t* row = gu + (long)(r0 + r) * 2 * F;
+    float g[8], u[8], o[8];
+    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + c0 + ch * 8)), g);
+    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + F + c0 + ch * 8)), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(silu_f(g[j]))) * u[j];
+    *reinterpret_cast<u32x4*>(out + (long)(r0 + r) * F + c0 + ch * 8) = pack8(o);
+    tile_put8(tile32, r, ch * 8, o);
+  }
+  __syncthreads();
+  tile_store_t(tile32, out_t, T, r0, c0, t);
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_tr_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dout,
+                                                            bf16_t* __restrict__ dgu, bf16_t* __restrict__ dgu_t, int T,
+                                                            int F) {
+  __shared__ unsigned tg[64 * 66 / 2], tu[64 * 66 / 2];
+  const int tilesF = F >> 6;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = (bid / tilesF) << 6, c0 = (bid % tilesF) << 6;
+  const int t = threadIdx.x, ch = t & 7, rr = t >> 3;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = rr + 32 * p;
+    const bf16_t* row = gu + (long)(r0 + r) * 2 * F;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(*reinterpret_cast<const u32x4*>(row + c0 + ch * 8), g);
+    unpack8(*reinterpret_cast<const u32x4*>(row + F + c0 + ch * 8), u);
+    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dout + (long)(r0 + r) * F + c0 + ch * 8)), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.f / (1.f + __expf(-g[j]));
+      const float si = g[j] * sg;
+      du[j] = d[j] * bf2f(f2bf(si));
+      dg[j] = d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg));
+    }
+    bf16_t* orow = dgu + (long)(r0 + r) * 2 * F;
+    *reinterpret_cast<u32x4*>(orow + c0 + ch * 8) = pack8(dg);
+    *reinterpret_cast<u32x4*>(orow + F + c0 + ch * 8) = pack8(du);
+    tile_put8(tg, r, ch * 8, dg);
+    tile_put8(tu, r, ch * 8, du);
+  }
+  __syncthreads();
+  tile_store_t(tg, dgu_t, T, r0, c0, t);      // rows [0, F) of dgu^T: the gate half
+  tile_store_t(tu, dgu_t, T, r0, F + c0, t);  // rows [F, 2F): the up half
+}
+
 // RoPE in place on the first (Hq + Hk) heads of each row of qkv: [T, (Hq + 2*Hk) * D].
 // Token t has position pos[t] if pos != nullptr else (t % S). cs: [max_pos, D/2] float2 (cos, sin).
 // sign = +1 forward, -1 backward (rotation by -theta is the adjoint).
@@ -111,6 +198,24 @@ RCA_API int rca_swiglu_bwd(const void* gu, const void* dout, void* dgu, long lon
   if (T * (F / 8) >= (1LL << 31)) return -2;
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8), 256)), dim3(256), 0, stream, (const bf16_t*)gu,
                      (const bf16_t*)dout, (bf16_t*)dgu, T, F);
+  return (int)hipGetLastError();
+}
+
+// Contract: T % 64 == 0, F % 64 == 0, 16-B aligned buffers; out_t is [F, T] (fwd) / dgu_t [2F, T] (bwd).
+RCA_API int rca_swiglu_fwd_tr(const void* gu, void* out, void* out_t, int T, int F, hipStream_t stream) {
+  if ((T & 63) || (F & 63) || T <= 0 || F <= 0) return -1;
+  const long long tiles = (long long)(T >> 6) * (F >> 6);
+  hipLaunchKernelGGL(swiglu_fwd_tr_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, (const bf16_t*)gu,
+                     (bf16_t*)out, (bf16_t*)out_t, T, F);
+  return (int)hipGetLastError();
+}
+
+RCA_API int rca_swiglu_bwd_tr(const void* gu, const void* dout, void* dgu, void* dgu_t, int T, int F,
+                              hipStream_t stream) {
+  if ((T & 63) || (F & 63) || T <= 0 || F <= 0) return -1;
+  const long long tiles = (long long)(T >> 6) * (F >> 6);
+  hipLaunchKernelGGL(swiglu_bwd_tr_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, (const bf16_t*)gu,
+                     (const bf16_t*)dout, (bf16_t*)dgu, (bf16_t*)dgu_t, T, F);
   return (int)hipGetLastError();
 }
 

@@ -24,44 +24,55 @@ _TRANSPOSED = os.environ.get("RCA_BWD_TRANSPOSED", "1") != "0"
 
 class _LinearWgradIntoFlat(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
-        ctx.save_for_backward(x)
+    def forward(ctx, x, weight, x_t):
+        # x_t: the input already transposed ([K, T], by its producer): saved instead of x, which
+        # backward only needs for the weight gradient
+        ctx.save_for_backward(x_t if x_t is not None else x)
+        ctx.has_t = x_t is not None
         ctx.weight = weight
         return F.linear(x, weight)
 
     @staticmethod
     def backward(ctx, gy):
-        (x,) = ctx.saved_tensors
+        (xs,) = ctx.saved_tensors
         w = ctx.weight
         g2 = gy.reshape(-1, gy.shape[-1])
-        x2 = x.reshape(-1, x.shape[-1])
-        tr = _use_transposed(g2, x2, w)
+        g_t = ops.pop_grad_transposed(g2)
+        if ctx.has_t:
+            x_t, x2 = xs, None
+        else:
+            x_t, x2 = None, xs.reshape(-1, xs.shape[-1])
+        tr = _use_transposed(g2, x2, w, x_t)
         if ctx.needs_input_grad[0]:
             gx = F.linear(gy, ops.transpose(w)) if tr else torch.matmul(gy, w)
         else:
             gx = None
         view = _flat_view(w, g2.dtype)
         if view is None:
-            return gx, _wgrad(g2, x2, tr).to(w.dtype)  # plain autograd accumulation
-        _wgrad(g2, x2, tr, out=view, accumulate=not _take_fresh(w))
+            return gx, _wgrad(g2, x2, tr, g_t=g_t, x_t=x_t).to(w.dtype), None
+        _wgrad(g2, x2, tr, out=view, accumulate=not _take_fresh(w), g_t=g_t, x_t=x_t)
         _notify(w)
-        return gx, None
+        return gx, None, None
 
 
-def _use_transposed(g2, x2, w) -> bool:
+def _use_transposed(g2, x2, w, x_t=None) -> bool:
     # Reduction-contiguous operands: both backward products have their reduction dim as the
     # OUTER dim of one (dgrad: W) or both (wgrad: gy, x) operands, which hipBLASLt runs at
     # 0.93-1.33 PF/s at the 8B shapes; on transposed copies the same products run at
     # 1.29-1.58 PF/s (scripts/gemm_layout.py). The copies come from one HBM-rate HIP pass each.
-    return _TRANSPOSED and ops.transpose_supported(g2) and ops.transpose_supported(x2) and ops.transpose_supported(w)
+    x_ok = (x_t is not None and x_t.is_cuda and x_t.is_contiguous()) or (x2 is not None and ops.transpose_supported(x2))
+    return _TRANSPOSED and ops.transpose_supported(g2) and x_ok and ops.transpose_supported(w)
 
 
-def _wgrad(g2, x2, tr, out=None, accumulate=False):
-    """dW = g2^T @ x2 (into ``out``, accumulating when asked)."""
+def _wgrad(g2, x2, tr, out=None, accumulate=False, g_t=None, x_t=None):
+    """dW = g2^T @ x2 (into ``out``, accumulating when asked). ``g_t`` / ``x_t``: transposed
+    copies a producer already wrote (no transpose pass for them)."""
     if tr:
-        a, b = ops.transpose(g2), ops.transpose(x2).t()
+        a = g_t if g_t is not None else ops.transpose(g2)
+        b = (x_t if x_t is not None else ops.transpose(x2)).t()
     else:
-        a, b = g2.t(), x2
+        a = g2.t() if g_t is None else g_t
+        b = x2 if x_t is None else x_t.t()
     if out is None:
         return torch.mm(a, b)
     if accumulate:
@@ -169,11 +180,12 @@ class FusedWgradLinear(nn.Linear):
         super().__init__(in_features, out_features, bias=False, device=device, dtype=dtype)
         self.weight._rca_fused_wgrad = True
 
-    def forward(self, x, labels=None, ignore_index: int = -100, ce_chunk: int = 0):
+    def forward(self, x, labels=None, ignore_index: int = -100, ce_chunk: int = 0, x_t=None):
         """``labels`` given: returns the mean cross-entropy of ``x @ W^T`` through the fused,
-        chunked linear + CE path (the full logits are never materialised)."""
+        chunked linear + CE path (the full logits are never materialised). ``x_t``: ``x``
+        already transposed by its producer (saved for the weight gradient instead of ``x``)."""
         if labels is not None:
             return linear_cross_entropy(x, self.weight, labels, ignore_index, ce_chunk)
         if torch.is_grad_enabled() and self.weight.requires_grad and getattr(self.weight, "_rca_flat_grad", False):
-            return _LinearWgradIntoFlat.apply(x, self.weight)
+            return _LinearWgradIntoFlat.apply(x, self.weight, x_t)
         return F.linear(x, self.weight)
