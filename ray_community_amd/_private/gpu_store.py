@@ -144,6 +144,18 @@ class _Mapped:
             pass
 
 
+def _dense_layout(t) -> bool:
+    """Dense layouts the store keeps as they are (a permutation of a contiguous block):
+    row-major and channels-last; anything else is snapshotted row-major."""
+    import torch
+
+    if t.is_contiguous():
+        return True
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return True
+    return t.dim() == 5 and t.is_contiguous(memory_format=torch.channels_last_3d)
+
+
 def import_tensor(rec):
     import torch
 
@@ -156,8 +168,11 @@ def import_tensor(rec):
         dev = torch.cuda.current_device()
     torch.cuda.init()
     m = _Mapped(rec, dev)
-    raw = torch.as_tensor(m, device=f"cuda:{dev}")
-    return raw.view(getattr(torch, rec["dtype"])).view(rec["shape"])
+    raw = torch.as_tensor(m, device=f"cuda:{dev}").view(getattr(torch, rec["dtype"]))
+    # dense record: same bytes, the exporter's strides (e.g. channels-last activations keep their
+    # memory format, so the consumer's kernels see the layout the producer chose)
+    stride = rec.get("stride")
+    return raw.as_strided(tuple(rec["shape"]), tuple(stride)) if stride else raw.view(rec["shape"])
 
 
 # ====================================================================== owner side
@@ -207,9 +222,13 @@ class GpuObjectStore:
         owned = []
         for t in serialized.gpu_tensors:
             c = t.detach()
+            dense = _dense_layout(c)
             if copy:
-                c = c.clone(memory_format=torch.contiguous_format)
-            elif not c.is_contiguous():
+                # keep a dense layout (row-major or channels-last) as it is: a consumer that gets
+                # NCHW bytes for an NHWC producer would silently run different (slower) kernels
+                c = c.clone(memory_format=torch.preserve_format) if dense else c.clone(
+                    memory_format=torch.contiguous_format)
+            elif not dense:
                 c = c.contiguous()
             owned.append(c)
         if owned:
@@ -247,7 +266,7 @@ class GpuObjectStore:
             for t in e.tensors:
                 s = self._side_stream(t.device)
                 s.wait_stream(torch.cuda.current_stream(t.device))
-                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                h = torch.empty_strided(t.shape, t.stride(), dtype=t.dtype, pin_memory=True)
                 with torch.cuda.stream(s):
                     h.copy_(t, non_blocking=True)
                     ev = torch.cuda.Event()
@@ -279,7 +298,7 @@ class GpuObjectStore:
                     dev = torch.cuda.current_device() if dev is None else dev
                     s = self._side_stream(torch.device("cuda", dev))
                     with torch.cuda.stream(s):
-                        d = torch.empty(h.shape, dtype=h.dtype, device=f"cuda:{dev}")
+                        d = torch.empty_strided(h.shape, h.stride(), dtype=h.dtype, device=f"cuda:{dev}")
                         d.copy_(h, non_blocking=True)
                     s.synchronize()
                     out.append(d)

@@ -16,7 +16,7 @@ from typing import Any, Dict, Optional
 _REPLICA_CTX = {}
 
 
-async def _aiter(res):
+async def _aiter(res, executor=None):
     """Iterate a sync or async generator (a plain value yields once)."""
     if inspect.isasyncgen(res):
         async for x in res:
@@ -24,8 +24,8 @@ async def _aiter(res):
     elif inspect.isgenerator(res):
         loop = asyncio.get_running_loop()
         done = object()
-        while True:  # pull sync generator items on a thread: the event loop keeps serving
-            x = await loop.run_in_executor(None, next, res, done)
+        while True:  # pull sync generator items on the user-code thread: the event loop keeps serving
+            x = await loop.run_in_executor(executor, next, res, done)
             if x is done:
                 break
             yield x
@@ -55,10 +55,18 @@ class ServeReplica:
         init_args, init_kwargs = _resolve_handle_args(init_args, init_kwargs)
         self.is_function = is_function
         _REPLICA_CTX["ctx"] = ReplicaContext(app_name, deployment_name, replica_tag)
+        # ONE user-code thread (reference: replica.py ``_user_code_event_loop_thread``): the
+        # constructor and every sync method run on it. Besides matching the reference's
+        # semantics this keeps per-thread GPU library state warm: MIOpen / hipBLASLt handles are
+        # per host thread, so a model warmed up in __init__ on thread A and served from a pool
+        # thread B would pay kernel loading again (seconds per new thread for a ResNet-50).
+        import concurrent.futures
+
+        self._user_exec = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="serve-user")
         if is_function:
             self.obj = body
         else:
-            self.obj = body(*init_args, **init_kwargs)
+            self.obj = self._user_exec.submit(lambda: body(*init_args, **init_kwargs)).result()
             if inspect.isawaitable(self.obj):
                 raise TypeError("constructor must not be async")
         _REPLICA_CTX["ctx"].servable_object = self.obj
@@ -66,7 +74,7 @@ class ServeReplica:
         self.total = 0
         self.started = time.time()
         if user_config is not None:
-            self._reconfigure_sync(user_config)
+            self._user_exec.submit(self._reconfigure_sync, user_config).result()
 
     def _reconfigure_sync(self, user_config):
         fn = getattr(self.obj, "reconfigure", None)
@@ -96,7 +104,7 @@ class ServeReplica:
         import contextvars
 
         ctx = contextvars.copy_context()
-        res = await loop.run_in_executor(None, lambda: ctx.run(fn, *args, **kwargs))
+        res = await loop.run_in_executor(self._user_exec, lambda: ctx.run(fn, *args, **kwargs))
         if inspect.isawaitable(res):
             res = await res
         return res
@@ -145,7 +153,7 @@ class ServeReplica:
         try:
             args, kwargs = _resolve_handle_args(args, kwargs)
             res = await self._invoke_user(method_name, args, kwargs)
-            async for x in _aiter(res):
+            async for x in _aiter(res, self._user_exec):
                 yield x
         finally:
             multiplex._reset_model_id(tok)

@@ -144,3 +144,30 @@ def test_gpu_object_owner_death_is_object_lost(ray_gpu):
     time.sleep(1.0)
     with pytest.raises(exc.ObjectLostError):
         ray.get(r2, timeout=30)
+
+
+@pytest.mark.gpu
+def test_gpu_object_keeps_channels_last_layout():
+    """A channels-last activation handed to another GPU actor arrives channels-last (same
+    strides, same values): NCHW bytes would silently switch the consumer's conv kernels."""
+    import torch
+
+    import ray_community_amd as ray
+
+    ray.init(num_cpus=4, num_gpus=1)
+    try:
+        @ray.remote(num_gpus=0.25)
+        class Reader:
+            def check(self, x):
+                return (x.is_contiguous(memory_format=torch.channels_last), tuple(x.stride()),
+                        x.float().sum().item())
+
+        x = torch.randn(4, 3, 16, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        r = Reader.remote()
+        cl, stride, s = ray.get(r.check.remote(x))
+        assert cl and stride == tuple(x.stride())
+        assert abs(s - x.float().sum().item()) < 1e-2
+        ref = ray.put(x)
+        assert ray.get(r.check.remote(ref))[1] == tuple(x.stride())
+    finally:
+        ray.shutdown()
