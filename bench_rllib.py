@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--env", default="ALE/Pong-v5")
+    ap.add_argument("--runner-gpu-share", type=float, default=0.5,
+                    help="fraction of each GPU given to env-runner policy inference (0: runners infer on CPU); "
+                         "the learner on that GPU gets the rest")
     args = ap.parse_args()
 
     import torch
@@ -45,13 +48,16 @@ def main():
     if args.learners is None:
         args.learners = ngpu
     ray.init(num_cpus=max(ncpu, runners + 2), num_gpus=ngpu)
+    share = args.runner_gpu_share if ngpu else 0.0
+    per_runner = share * ngpu / runners if share > 0 else 0
     cfg = (PPOConfig().environment(args.env)
-           .env_runners(num_env_runners=runners, num_envs_per_env_runner=args.envs_per_runner)
+           .env_runners(num_env_runners=runners, num_envs_per_env_runner=args.envs_per_runner,
+                        num_gpus_per_env_runner=per_runner)
            .training(lr=2.5e-4, train_batch_size=args.train_batch, minibatch_size=args.minibatch,
                      num_epochs=args.epochs, clip_param=0.1, vf_clip_param=10.0, entropy_coeff=0.01,
                      kl_coeff=0.5, lambda_=0.95, gamma=0.99, model={"vf_share_layers": True}))
     if args.learners > 0:
-        cfg.learners(num_learners=args.learners, num_gpus_per_learner=1 if ngpu else 0)
+        cfg.learners(num_learners=args.learners, num_gpus_per_learner=(1.0 - share) if ngpu else 0)
     else:
         cfg.resources(num_gpus=1 if ngpu else 0)
     algo = cfg.build()
@@ -70,7 +76,7 @@ def main():
            "higher_is_better": True, "vs_baseline": None, "data": "SyntheticAtari (84x84x4 uint8, Discrete(6))",
            "config": {"env_runners": runners, "envs_per_runner": args.envs_per_runner,
                       "train_batch_size": args.train_batch, "minibatch": args.minibatch, "epochs": args.epochs,
-                      "learners": args.learners},
+                      "learners": args.learners, "runner_gpu_share": share},
            "extra": {"learner_time_s": last["info"]["learner"]["default_policy"].get("learner_time_s"),
                      "iter_time_s": dt / max(1, args.iters)}}
     print(json.dumps(out), flush=True)

@@ -53,12 +53,16 @@ class Algorithm(Trainable):
             from ..env.multi_agent_env_runner import MultiAgentEnvRunner
 
             runner_cls = MultiAgentEnvRunner
-        self.local_runner = runner_cls(rd, 0)
+        # the local runner (index 0) never takes the runners' GPU share
+        self.local_runner = runner_cls(dict(rd, num_gpus_per_env_runner=0), 0)
         self.remote_runners = []
         if cfg.num_env_runners > 0:
             from ...actor import ActorClass
 
-            cls = ActorClass(runner_cls, {"num_cpus": cfg.num_cpus_per_env_runner})
+            opts = {"num_cpus": cfg.num_cpus_per_env_runner}
+            if getattr(cfg, "num_gpus_per_env_runner", 0):
+                opts["num_gpus"] = cfg.num_gpus_per_env_runner
+            cls = ActorClass(runner_cls, opts)
             self.remote_runners = [cls.remote(rd, i + 1) for i in range(cfg.num_env_runners)]
         from ..core.learner import LearnerGroup
 

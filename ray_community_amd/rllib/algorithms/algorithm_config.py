@@ -24,6 +24,7 @@ class AlgorithmConfig:
         self.rollout_fragment_length: Any = "auto"
         self.batch_mode = "truncate_episodes"
         self.num_cpus_per_env_runner = 1
+        self.num_gpus_per_env_runner = 0  # > 0: the runner's RLModule runs its inference on that GPU share
         self.explore = True
         # training
         self.gamma = 0.99
@@ -63,10 +64,11 @@ class AlgorithmConfig:
         return self
 
     def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None, rollout_fragment_length=None,
-                    batch_mode=None, num_cpus_per_env_runner=None, explore=None, **kw):
+                    batch_mode=None, num_cpus_per_env_runner=None, num_gpus_per_env_runner=None, explore=None, **kw):
         for k, v in dict(num_env_runners=num_env_runners, num_envs_per_env_runner=num_envs_per_env_runner,
                          rollout_fragment_length=rollout_fragment_length, batch_mode=batch_mode,
-                         num_cpus_per_env_runner=num_cpus_per_env_runner, explore=explore).items():
+                         num_cpus_per_env_runner=num_cpus_per_env_runner,
+                         num_gpus_per_env_runner=num_gpus_per_env_runner, explore=explore).items():
             if v is not None:
                 setattr(self, k, v)
         return self

@@ -32,6 +32,12 @@ class EnvRunner:
         self.N = self.env.num_envs
         self.module = make_module(config, self.env.observation_space, self.env.action_space)
         self.module.eval()
+        # GPU inference (num_gpus_per_env_runner > 0): the module lives on the runner's GPU share,
+        # observations go up once per step and ONE packed [N, 3 + A] tensor comes back
+        self.device = torch.device("cpu")
+        if float(config.get("num_gpus_per_env_runner", 0) or 0) > 0 and torch.cuda.is_available():
+            self.device = torch.device("cuda", torch.cuda.current_device())
+            self.module.to(self.device)
         self.obs, _ = self.env.reset(seed=self.seed)
         self.ep_ret = np.zeros(self.N)
         self.ep_len = np.zeros(self.N, dtype=np.int64)
@@ -89,6 +95,22 @@ class EnvRunner:
             self.ep_ret[done] = 0
             self.ep_len[done] = 0
 
+    def _to_host(self, a, lp, v, logits):
+        """One device->host copy per step for the policy outputs (discrete actions travel as f32)."""
+        if a.dim() != 1 or a.dtype not in (torch.int64, torch.int32):
+            return a.cpu(), lp.cpu(), v.cpu(), None if logits is None else logits.cpu()
+        cols = [a.float().unsqueeze(1), lp.float().unsqueeze(1), v.float().unsqueeze(1)]
+        if logits is not None:
+            cols.append(logits.float())
+        h = torch.cat(cols, 1).cpu()
+        return h[:, 0].long(), h[:, 1], h[:, 2], (h[:, 3:] if logits is not None else None)
+
+    def _value(self, obs):
+        o = torch.from_numpy(obs)
+        if self.device.type == "cuda":
+            o = o.to(self.device, non_blocking=True)
+        return self.module.forward(o)[1].float().cpu().numpy()
+
     @torch.no_grad()
     def sample(self, num_steps: Optional[int] = None, explore: bool = True) -> SampleBatch:
         """On-policy fragment of T = num_steps // N steps per sub-env (PPO / IMPALA)."""
@@ -105,14 +127,19 @@ class EnvRunner:
         trunc = np.empty((N, T), dtype=bool)
         logits_buf = None
         trunc_fix = []  # (t, env indices, final obs)
+        gpu = self.device.type == "cuda"
         for t in range(T):
             o = torch.from_numpy(self.obs)
+            if gpu:
+                o = o.to(self.device, non_blocking=True)
             if explore:
                 a, lp, v, logits = self.module.forward_exploration(o)
             else:
                 a, v = self.module.forward_inference(o)
-                lp = torch.zeros(N)
+                lp = torch.zeros(N, device=o.device)
                 logits = None
+            if gpu:
+                a, lp, v, logits = self._to_host(a, lp, v, logits)
             if logits is not None:
                 if logits_buf is None:
                     logits_buf = np.empty((N, T, logits.shape[-1]), dtype=np.float32)
@@ -131,13 +158,13 @@ class EnvRunner:
                 trunc_fix.append((t, idx, info["final_obs"][idx]))
             self._track(r, te, tr, info)
             self.obs = nobs
-        last_v = self.module.forward(torch.from_numpy(self.obs))[1].numpy()
+        last_v = self._value(self.obs)
         next_vf = np.empty_like(vf)
         next_vf[:, :-1] = vf[:, 1:]
         next_vf[:, -1] = last_v
         if trunc_fix:
             fo = np.concatenate([x[2] for x in trunc_fix], axis=0)
-            fv = self.module.forward(torch.from_numpy(fo))[1].numpy()
+            fv = self._value(fo)
             k = 0
             for t, idx, _ in trunc_fix:
                 next_vf[idx, t] = fv[k: k + len(idx)]
