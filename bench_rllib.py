@@ -49,7 +49,14 @@ def main():
         args.learners = ngpu
     ray.init(num_cpus=max(ncpu, runners + 2), num_gpus=ngpu)
     share = args.runner_gpu_share if ngpu else 0.0
-    per_runner = share * ngpu / runners if share > 0 else 0
+    if share > 0 and args.runners is None and runners > 12 * ngpu:
+        # GPU-inference runners each open the device: keep <= 12 per GPU (+ learner, driver) and
+        # the same total number of vectorised envs
+        total_envs = runners * args.envs_per_runner
+        runners = 12 * ngpu
+        args.envs_per_runner = -(-total_envs // runners)
+    # resources are fixed-point 1e-4 units: round the per-runner share DOWN so runners + learner fit
+    per_runner = int(share * ngpu / runners * 1e4) / 1e4 if share > 0 else 0
     cfg = (PPOConfig().environment(args.env)
            .env_runners(num_env_runners=runners, num_envs_per_env_runner=args.envs_per_runner,
                         num_gpus_per_env_runner=per_runner)
@@ -60,9 +67,21 @@ def main():
         cfg.learners(num_learners=args.learners, num_gpus_per_learner=(1.0 - share) if ngpu else 0)
     else:
         cfg.resources(num_gpus=1 if ngpu else 0)
+    import threading
+
+    t_start = time.perf_counter()
+    stop = threading.Event()
+
+    def heartbeat():  # long first-iteration kernel builds (MIOpen) must not look like a hang
+        while not stop.wait(30):
+            print(f"[bench_rllib] still running ({time.perf_counter() - t_start:.0f} s)", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     algo = cfg.build()
-    for _ in range(args.warmup):
+    print(f"[bench_rllib] built in {time.perf_counter() - t_start:.1f} s", file=sys.stderr, flush=True)
+    for i in range(args.warmup):
         algo.train()
+        print(f"[bench_rllib] warmup {i} done at {time.perf_counter() - t_start:.1f} s", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     steps = 0
     last = None
@@ -79,6 +98,7 @@ def main():
                       "learners": args.learners, "runner_gpu_share": share},
            "extra": {"learner_time_s": last["info"]["learner"]["default_policy"].get("learner_time_s"),
                      "iter_time_s": dt / max(1, args.iters)}}
+    stop.set()
     print(json.dumps(out), flush=True)
     algo.stop()
     ray.shutdown()
