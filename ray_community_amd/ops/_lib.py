@@ -28,6 +28,7 @@ _SIGS = {
     "rca_swiglu_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p]),
     "rca_swiglu_fwd_tr": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "rca_swiglu_bwd_tr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "rca_probe_hwid": (c_int, [c_void_p, c_void_p]),
     "rca_gemm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int,
                               c_void_p]),
     "rca_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_ll, c_void_p]),

@@ -219,6 +219,22 @@ RCA_API int rca_swiglu_bwd_tr(const void* gu, const void* dout, void* dgu, void*
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Placement probe: where did this workgroup run? out[0] = XCC id (HW_REG_XCC_ID), out[1] = the
+// raw HW_REG_HW_ID word (CU / SH / SE fields). Used to map hipExtStreamCreateWithCUMask bits to
+// XCDs before partitioning CUs between concurrent streams (parallel/optim.py).
+__global__ void probe_hwid_kernel(int* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    out[0] = (int)__builtin_amdgcn_s_getreg((3 << 11) | 20);   // XCC_ID[3:0]
+    out[1] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+  }
+}
+
+RCA_API int rca_probe_hwid(int* out, hipStream_t stream) {
+  hipLaunchKernelGGL(probe_hwid_kernel, dim3(1), dim3(64), 0, stream, out);
+  return (int)hipGetLastError();
+}
+
 RCA_API int rca_rope(void* qkv, const void* cs, const int* pos, long long T, int S, int nheads_rot, int row_stride,
                      int D, int backward, hipStream_t stream) {
   if (D % 16) return -1;
