@@ -100,7 +100,14 @@ struct Stage {
   __device__ __forceinline__ void init(const bf16_t* base, long stride, int rows, int tid, int cols = D) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), (short)0,
                                              (int)((long)(rows - 1) * stride * 2 + cols * 2), 0x00020000);
-    const int row = tid / NCH, ch = tid % NCH;
+    // thread -> (row, chunk): each 8-lane group of a ds_write_b128 (the unit that conflicts,
+    // bank = (a/4) mod 32) stores chunks 0-3 of TWO consecutive rows, i.e. 8 distinct 16-B slots
+    // of a 128-B bank window in the image; row-major tid / NCH put chunks 0-3 and 4-7 of one row
+    // in a group, which alias (512-B subtile stride) -> 2-way conflicts on every staging store.
+    // Global loads stay coalesced (each wave covers whole 2*NCH*16-B row pairs).
+    constexpr int LG = NCH == 16 ? 2 : (NCH == 8 ? 1 : 0);  // log2(NCH / 4)
+    const int ch = (tid & 3) | (((tid >> 3) & ((NCH >> 2) - 1)) << 2);
+    const int row = ((tid >> 2) & 1) | ((tid >> (3 + LG)) << 1);
     voff = (int)(row * stride * 2 + ch * 16);
     loff = Img<D>::off(row, ch);
   }
