@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     long sdo, long sdk, long sdv, float scale2, float scale) {
   constexpr int BKV = 128, BQS = 32 * NH, NKS = D / 16, NDB = D / 32, SL = BQS * D * 2, G8 = Img<D>::G8;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * SL];
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, delta][row]
+  __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, -delta][row]
 
   const int nkb = S / BKV, G = Hq / Hk;
   int bhk, kbi;
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
   auto stage_store = [&](int buf) {
     qst.store(smem + buf * 2 * SL);
     gst.store(smem + buf * 2 * SL + SL);
-    if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = tid < BQS ? -rc : rc;
+    if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = -rc;  // -lse, -delta
   };
 
   stage_load(0, nsl - 1);
@@ -95,7 +95,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
     if (more) stage_load((i + 1) % G, nsl - 1 - (i + 1) / G);
     const int qa = qs0 + sl * BQS;
     if (!CAUSAL || qa + BQS - 1 >= kw0) {
-      // S and dP of half t (rows 32t..32t+31 of the slice): row-operand burst + two MFMA chains
+      // S and dP of half t (rows 32t..32t+31 of the slice): row-operand burst + two MFMA chains.
+      // dP's chain starts from -delta (the row constant as the initial accumulator: dS = P * dP'
+      // needs no subtraction afterwards)
       auto sdp = [&](int t, f32x16& s, f32x16& dp) {
         bf16x8_t fr[2 * NKS];
 #pragma unroll
@@ -105,28 +107,37 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
           fr[NKS + kk] = lds_b128(Gs + o);
         }
         s = zero16();
-        dp = zero16();
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&rowc[buf][1][32 * t + 8 * g4 + 4 * h]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dp[4 * g4 + j] = d4[j];
+        }
 #pragma unroll
         for (int kk = 0; kk < NKS; ++kk) {
           s = mfma32(fr[kk], kf[kk], s);
           dp = mfma32(fr[NKS + kk], vf[kk], dp);
         }
       };
-      // P = exp2(S*c - lse), dS = P * (dP - delta) on the VALU (causal mask on the diagonal)
-      auto pds = [&](int t, f32x16& s, f32x16& dp) {
-        const bool diag = CAUSAL && qa + 32 * t < kw0 + 31;
+      // P = exp2(S*c - lse), dS = P * (dP - delta) on the VALU. The causal mask is compiled only
+      // into the diagonal variant (DIAG): a runtime `if` here became an unconditional
+      // compare + select per element (64 VALU per slice) on every off-diagonal slice.
+      auto pds = [&](int t, f32x16& s, f32x16& dp, auto diagc) {
+        constexpr bool DIAG = decltype(diagc)::value;
+        const bool diag = DIAG && qa + 32 * t < kw0 + 31;
         const int kq = key - qa - 32 * t - 4 * h;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const f32x4 l4 = *reinterpret_cast<const f32x4*>(&rowc[buf][0][32 * t + 8 * g4 + 4 * h]);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&rowc[buf][1][32 * t + 8 * g4 + 4 * h]);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g4 + j;
             float p = fast_exp2(fmaf(s[r], scale2, l4[j]));
-            if (diag) p = kq > 8 * g4 + j ? 0.f : p;
+            if constexpr (DIAG) {
+              if (diag) p = kq > 8 * g4 + j ? 0.f : p;
+            }
             s[r] = p;
-            dp[r] = p * (dp[r] - d4[j]);
+            dp[r] = p * dp[r];
           }
         }
       };
@@ -154,13 +165,20 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
           dk[db] = mfma32(fr[3 * NDB + db], df1, dk[db]);
         }
       };
-      f32x16 s[NH], dp[NH];
+      auto body = [&](auto diagc) {
+        f32x16 s[NH], dp[NH];
 #pragma unroll
-      for (int t = 0; t < NH; ++t) sdp(t, s[t], dp[t]);
+        for (int t = 0; t < NH; ++t) sdp(t, s[t], dp[t]);
 #pragma unroll
-      for (int t = 0; t < NH; ++t) {
-        pds(t, s[t], dp[t]);
-        acc(t, s[t], dp[t]);
+        for (int t = 0; t < NH; ++t) {
+          pds(t, s[t], dp[t], diagc);
+          acc(t, s[t], dp[t]);
+        }
+      };
+      if (CAUSAL && qa < kw0 + 31) {
+        body(std::integral_constant<bool, CAUSAL>{});
+      } else {
+        body(std::false_type{});
       }
     }
     if (more) stage_store(buf ^ 1);
