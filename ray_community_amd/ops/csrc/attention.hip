@@ -276,7 +276,14 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
     settle(gf[kk]);
   }
   const float nlse = -LSE[(long)bh * S + qrow];
-  const float dlt = Delta[(long)bh * S + qrow];
+  // -delta as the dP chain's initial accumulator (one query per lane: a constant vector built
+  // once), so dS = P * dP' needs no per-tile subtraction
+  f32x16 ndlt;
+  {
+    const float d = -Delta[(long)bh * S + qrow];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ndlt[i] = d;
+  }
 
   f32x16 dq[NDB];
 #pragma unroll
@@ -302,20 +309,24 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
       kst.load(kb + BK, sk);
       vst.load(kb + BK, sv);
     }
-    if (!CAUSAL || kb <= qw0) {
+    // one straight-line body per variant (the diagonal tile's mask is compiled only into DIAG):
+    // a runtime branch between the S/dP MFMAs and the VALU split the tile into basic blocks the
+    // scheduler could not interleave
+    auto run = [&](auto diagc) {
+      constexpr bool DIAG = decltype(diagc)::value;
       bf16x8_t fr[2 * NKS];
 #pragma unroll
       for (int kk = 0; kk < NKS; ++kk) {
         fr[kk] = lds_b128(Ks + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
         fr[NKS + kk] = lds_b128(Vs + ((kk & 1) ? rb1 : rb0) + 512 * (kk >> 1));
       }
-      f32x16 s = zero16(), dp = zero16();
+      f32x16 s = zero16(), dp = ndlt;
 #pragma unroll
       for (int kk = 0; kk < NKS; ++kk) {
         s = mfma32(fr[kk], qf[kk], s);
         dp = mfma32(fr[NKS + kk], gf[kk], dp);
       }
-      if (CAUSAL && kb == qw0) {
+      if constexpr (DIAG) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int kofs = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
         }
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = fast_exp2(fmaf(s[r], scale2, nlse)) * (dp[r] - dlt);
+      for (int r = 0; r < 16; ++r) s[r] = fast_exp2(fmaf(s[r], scale2, nlse)) * dp[r];
       const bf16x8_t d0 = acc_to_bf16(s, 0), d1 = acc_to_bf16(s, 1);
 #pragma unroll
       for (int st = 0; st < 2; ++st)
@@ -334,6 +345,11 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
       for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[db], d0, dq[db]);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[NDB + db], d1, dq[db]);
+    };
+    if (CAUSAL && kb == qw0) {
+      run(std::integral_constant<bool, CAUSAL>{});
+    } else if (!CAUSAL || kb < qw0) {
+      run(std::false_type{});
     }
     if (more) {
       kst.store(smem + (buf ^ 1) * 2 * TILE);
