@@ -203,35 +203,50 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// delta = rowsum(dO * O) (fp32), [B, Hq, S]
+// delta = rowsum(dO * O) (fp32), [B, Hq, S]. One wave per RPW consecutive OUTPUT rows
+// ((b, hq, s) order, so the stores are one contiguous burst): LPR = D/8 lanes per row, RPS rows
+// per load step, 4 steps unrolled with all 8 loads issued before the first use (memory-level
+// parallelism: the one-row-per-16-lanes version ran at ~2.5 TB/s), 32-bit index math.
 template <int D>
 __global__ __launch_bounds__(kThreads) void attn_bwd_delta_kernel(const bf16_t* __restrict__ O,
                                                                   const bf16_t* __restrict__ dO,
                                                                   float* __restrict__ delta, int B, int S, int Hq,
                                                                   long so, long sdo) {
-  constexpr int LPR = D / 8;  // lanes per (token, head) row
-  const long gid = (long)blockIdx.x * kThreads + threadIdx.x;
-  const long row = gid / LPR;  // = (b*S + s)*Hq + hq
-  const int c = gid % LPR;
-  const long total = (long)B * S * Hq;
-  float acc = 0.f;
-  if (row < total) {
-    const long tok = row / Hq;
-    const int hq = row % Hq;
+  constexpr int LPR = D / 8, RPS = 64 / LPR, U = 4, RPW = RPS * U;
+  const int lane = threadIdx.x & 63;
+  const int total = B * S * Hq;
+  const int base = (blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * RPW;
+  const int c = lane % LPR, r = lane / LPR;
+  u32x4 va[U], vg[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int row = base + u * RPS + r;  // = (b * Hq + hq) * S + s
+    if (row < total) {
+      const int s_ = row % S, bh = row / S;
+      const long tok = (long)(bh / Hq) * S + s_;
+      const int hq = bh % Hq;
+      va[u] = *reinterpret_cast<const u32x4*>(O + tok * so + hq * D + c * 8);
+      vg[u] = *reinterpret_cast<const u32x4*>(dO + tok * sdo + hq * D + c * 8);
+    } else {
+      va[u] = vg[u] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  float out = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
     float a[8], g[8];
-    unpack8(*reinterpret_cast<const u32x4*>(O + tok * so + (long)hq * D + c * 8), a);
-    unpack8(*reinterpret_cast<const u32x4*>(dO + tok * sdo + (long)hq * D + c * 8), g);
+    unpack8(va[u], a);
+    unpack8(vg[u], g);
+    float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += a[i] * g[i];
-  }
 #pragma unroll
-  for (int off = LPR / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if (row < total && c == 0) {
-    const long tok = row / Hq;
-    const int hq = row % Hq;
-    const long b = tok / S, s = tok % S;
-    delta[((b * Hq) + hq) * S + s] = acc;
+    for (int off = LPR / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    // lane L < RPW collects row L = u * RPS + (L % RPS) from lane (L % RPS) * LPR
+    const float v = __shfl(acc, (lane % RPS) * LPR, 64);
+    if (lane / RPS == u) out = v;
   }
+  if (lane < RPW && base + lane < total) delta[base + lane] = out;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -386,10 +401,10 @@ void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t*
                 const float* lse, float* delta, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
                 long sq, long sk, long sv, long so, long sdo, long sdq, long sdk, long sdv, float scale2, float scale,
                 hipStream_t st) {
-  const long rows = (long)B * S * Hq;
-  const long threads = rows * (D / 8);
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((threads + kThreads - 1) / kThreads), dim3(kThreads), 0, st, o,
-                     dout, delta, B, S, Hq, so, sdo);
+  const long rows = (long)B * S * Hq;  // < 2^31 (shapes_ok)
+  const long rows_per_block = (kThreads / 64) * 4 * (64 / (D / 8));
+  hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((rows + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
+                     st, o, dout, delta, B, S, Hq, so, sdo);
   rca_attn_launch_dkdv(D, C, q, k, v, dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale,
                        st);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3(B * Hq * (S / 128)), dim3(kThreads), 0, st, q, k, v, dout, lse,
@@ -397,7 +412,8 @@ void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t*
 }
 
 bool shapes_ok(int B, int S, int Hq, int Hk, int D) {
-  return B > 0 && S > 0 && S % 128 == 0 && Hk > 0 && Hq % Hk == 0 && (D == 64 || D == 128);
+  return B > 0 && S > 0 && S % 128 == 0 && Hk > 0 && Hq % Hk == 0 && (D == 64 || D == 128) &&
+         (long)B * S * Hq < (1L << 31);
 }
 
 }  // namespace
