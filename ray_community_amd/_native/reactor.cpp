@@ -1,0 +1,251 @@
+// Native I/O reactor of the control plane (reference role: the asio event loops + gRPC
+// transports of src/ray/common/asio and src/ray/rpc). Frames on every stream are
+// <uint64 little-endian length><payload> (ray_community_amd/_private/protocol.py).
+//
+// One Reactor serves many stream sockets through epoll: poll() waits with the GIL released,
+// accepts on listening sockets, drains every readable socket with MSG_DONTWAIT reads (the sockets
+// stay blocking for the threads that send on them), splits the bytes into frames in C++, and only
+// then takes the GIL to hand Python a batch: one call returns every frame that arrived, across
+// connections, instead of a selector round + recv + Python-level frame parsing per wake-up.
+// send_frame() writes header + payload with one sendmsg (no concatenation copy), releasing the
+// GIL for large payloads.
+#include <pybind11/pybind11.h>
+
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <poll.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <cstdint>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+enum EventKind : int { kFrame = 0, kClosed = 1, kAccepted = 2, kWake = 3 };
+
+struct Stream {
+  int64_t token = 0;
+  bool listener = false;
+  std::string in;  // bytes received, not yet a whole frame
+};
+
+struct Event {
+  int kind;
+  int64_t token;
+  int fd;
+  std::string payload;
+};
+
+class Reactor {
+ public:
+  Reactor() {
+    ep_ = epoll_create1(EPOLL_CLOEXEC);
+    if (ep_ < 0) throw std::runtime_error(std::string("epoll_create1: ") + strerror(errno));
+    wake_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+    if (wake_ < 0) throw std::runtime_error(std::string("eventfd: ") + strerror(errno));
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = wake_;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, wake_, &ev);
+  }
+  ~Reactor() { close_all(); }
+
+  void add(int fd, int64_t token, bool listener) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      Stream& s = streams_[fd];
+      s.token = token;
+      s.listener = listener;
+      s.in.clear();
+    }
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLRDHUP;
+    ev.data.fd = fd;
+    if (epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev) != 0 && errno == EEXIST) epoll_ctl(ep_, EPOLL_CTL_MOD, fd, &ev);
+  }
+
+  void remove(int fd) {
+    epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+    std::lock_guard<std::mutex> g(mu_);
+    streams_.erase(fd);
+  }
+
+  void wake() {
+    uint64_t one = 1;
+    ssize_t r = write(wake_, &one, sizeof(one));
+    (void)r;
+  }
+
+  // [(kind, token, fd, payload-or-None)]: kind 0 frame, 1 peer closed (the stream is removed
+  // from the reactor; the caller closes its socket), 2 accepted (fd = the new socket), 3 wake.
+  py::list poll(int timeout_ms) {
+    std::vector<Event> out;
+    {
+      py::gil_scoped_release nogil;
+      epoll_event evs[64];
+      int n = epoll_wait(ep_, evs, 64, timeout_ms);
+      std::lock_guard<std::mutex> g(mu_);  // add/remove from other threads wait for this batch
+      for (int i = 0; i < n; ++i) {
+        const int fd = evs[i].data.fd;
+        if (fd == wake_) {
+          uint64_t v;
+          while (read(wake_, &v, sizeof(v)) > 0) {
+          }
+          out.push_back({kWake, 0, -1, {}});
+          continue;
+        }
+        auto it = streams_.find(fd);
+        if (it == streams_.end()) continue;
+        if (it->second.listener)
+          accept_all(fd, it->second.token, out);
+        else if (drain(fd, it->second, out))
+          streams_.erase(it);
+      }
+    }
+    py::list res;
+    for (auto& e : out) {
+      if (e.kind == kFrame)
+        res.append(py::make_tuple(e.kind, e.token, e.fd, py::bytes(e.payload)));
+      else
+        res.append(py::make_tuple(e.kind, e.token, e.fd, py::none()));
+    }
+    return res;
+  }
+
+  void close_all() {
+    if (ep_ >= 0) close(ep_);
+    if (wake_ >= 0) close(wake_);
+    ep_ = wake_ = -1;
+  }
+
+ private:
+  void accept_all(int lfd, int64_t token, std::vector<Event>& out) {
+    for (;;) {
+      int c = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+      if (c < 0) return;  // EAGAIN (drained: the listener is non-blocking) or a transient error
+      out.push_back({kAccepted, token, c, {}});
+    }
+  }
+
+  // Reads everything available, appends whole frames to ``out``; true if the peer closed (the
+  // stream is then dropped from epoll; the caller erases it).
+  bool drain(int fd, Stream& s, std::vector<Event>& out) {
+    char buf[1 << 16];
+    bool closed = false;
+    for (;;) {
+      ssize_t k = recv(fd, buf, sizeof(buf), MSG_DONTWAIT);
+      if (k > 0) {
+        s.in.append(buf, (size_t)k);
+        if ((size_t)k < sizeof(buf)) break;
+        continue;
+      }
+      if (k == 0) {
+        closed = true;
+        break;
+      }
+      if (errno == EINTR) continue;
+      if (errno != EAGAIN && errno != EWOULDBLOCK) closed = true;
+      break;
+    }
+    size_t off = 0;
+    while (s.in.size() - off >= 8) {
+      uint64_t n;
+      memcpy(&n, s.in.data() + off, 8);
+      if (s.in.size() - off - 8 < n) break;
+      out.push_back({kFrame, s.token, fd, s.in.substr(off + 8, n)});
+      off += 8 + n;
+    }
+    if (off) s.in.erase(0, off);
+    if (closed) {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+      out.push_back({kClosed, s.token, fd, {}});
+    }
+    return closed;
+  }
+
+  int ep_ = -1, wake_ = -1;
+  std::mutex mu_;
+  std::unordered_map<int, Stream> streams_;
+};
+
+}  // namespace
+
+// One frame = header + payload in a single sendmsg (looping over partial writes). The GIL is
+// released for payloads above 64 KiB, where the copy into the socket buffer dominates.
+static void send_frame(int fd, py::bytes payload) {
+  char* data;
+  Py_ssize_t len;
+  if (PyBytes_AsStringAndSize(payload.ptr(), &data, &len) != 0) throw py::error_already_set();
+  uint64_t n = (uint64_t)len;
+  char hdr[8];
+  memcpy(hdr, &n, 8);
+  auto do_send = [&]() -> int {
+    size_t sent = 0, total = 8 + (size_t)len;
+    while (sent < total) {
+      iovec iov[2];
+      int cnt = 0;
+      if (sent < 8) {
+        iov[cnt].iov_base = hdr + sent;
+        iov[cnt].iov_len = 8 - sent;
+        ++cnt;
+        iov[cnt].iov_base = data;
+        iov[cnt].iov_len = (size_t)len;
+        ++cnt;
+      } else {
+        iov[cnt].iov_base = data + (sent - 8);
+        iov[cnt].iov_len = total - sent;
+        ++cnt;
+      }
+      msghdr m{};
+      m.msg_iov = iov;
+      m.msg_iovlen = cnt;
+      ssize_t k = sendmsg(fd, &m, MSG_NOSIGNAL);
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) {  // a socket with a timeout is non-blocking
+          pollfd p{fd, POLLOUT, 0};
+          ::poll(&p, 1, -1);
+          continue;
+        }
+        return errno;
+      }
+      sent += (size_t)k;
+    }
+    return 0;
+  };
+  int err;
+  if (len > (1 << 16)) {
+    py::gil_scoped_release nogil;
+    err = do_send();
+  } else {
+    err = do_send();
+  }
+  if (err != 0) {
+    errno = err;
+    PyErr_SetFromErrno(PyExc_OSError);
+    throw py::error_already_set();
+  }
+}
+
+void register_reactor(py::module_& m) {
+  py::class_<Reactor>(m, "Reactor")
+      .def(py::init<>())
+      .def("add", &Reactor::add, py::arg("fd"), py::arg("token"), py::arg("listener") = false)
+      .def("remove", &Reactor::remove)
+      .def("wake", &Reactor::wake)
+      .def("poll", &Reactor::poll, py::arg("timeout_ms"))
+      .def("close", &Reactor::close_all);
+  m.def("send_frame", &send_frame, py::arg("fd"), py::arg("payload"));
+}

@@ -378,6 +378,14 @@ class CoreWorker:
         self.channels: Dict[bytes, Any] = {}
         self._chan_lock = threading.Lock()
         self.direct_actor_calls = os.environ.get("RCA_DIRECT_ACTOR_CALLS", "1") != "0"
+        # normal tasks over leased workers (direct_transport.TaskLeaseChannel), per resource shape
+        self.direct_task_calls = os.environ.get("RCA_DIRECT_TASK_CALLS", "1") != "0"
+        self.task_channels: Dict[tuple, Any] = {}
+        self.worker_links: Dict[str, Any] = {}
+        # (tid, name, None, start, end, failed, error type, worker id, node) of leased tasks this
+        # process submitted, batched to the head (state API / timeline)
+        self.task_records: List[tuple] = []
+        self._records_armed = False
 
     # -------------------------------------------------------------- reference counting
     def ref_add(self, oid):
@@ -600,18 +608,19 @@ class CoreWorker:
             raise TypeError("wait() expected a list of ObjectRefs")
         refs = list(refs)
         ids = [r._id for r in refs]
-        if len(set(ids)) != len(ids):
+        sids = set(ids)
+        if len(sids) != len(ids):
             raise ValueError("Wait requires a list of unique object refs.")
         if num_returns <= 0:
             raise ValueError("Invalid number of objects to return %d." % num_returns)
         if num_returns > len(refs):
             raise ValueError("num_returns cannot be greater than the number of objects provided.")
         owned = self.owned.objs
-        local = [o for o in ids if o in owned]
-        if local and len(local) == len(ids):
+        if sids <= owned.keys():
             deadline = None if timeout is None else time.monotonic() + timeout
             got = self.owned.wait_ready(ids, num_returns, deadline)
         else:
+            local = [o for o in ids if o in owned]
             for o in local:  # mixed with head-managed refs: let the head track them all
                 self.owned.publish(o)
             # objects seen ready by an earlier wait stay ready while referenced: polling a shrinking
@@ -625,6 +634,15 @@ class CoreWorker:
                 rk.update(got)
         if len(got) > num_returns:
             got = got[:num_returns]
+        if len(got) <= 4:  # the polling case: split by position instead of two filtering passes
+            idx = sorted(ids.index(o) for o in got)
+            ready = [refs[i] for i in idx]
+            not_ready, prev = [], 0
+            for i in idx:
+                not_ready.extend(refs[prev:i])
+                prev = i + 1
+            not_ready.extend(refs[prev:])
+            return ready, not_ready
         rs = set(got)
         ready = [r for r in refs if r._id in rs]
         not_ready = [r for r in refs if r._id not in rs]
@@ -676,11 +694,40 @@ class CoreWorker:
         trace = tracing.submission_context()
         if trace is not None:
             spec["trace"] = trace
+        if self.direct_task_calls and _leasable(spec):
+            return self._submit_leased(spec, deps)
         owned = self.owned.objs
         for a in spec["args"]:
             if a[0] == "r" and a[1] in owned:
                 self.owned.publish(a[1])  # the head schedules this task: it must know its inputs
         self.client.submit(spec)
+
+    def flush_task_records(self):
+        self._records_armed = False
+        if not self.task_records:
+            return
+        recs, self.task_records = self.task_records, []
+        try:
+            self.client.call_async("direct_task_records", recs)
+        except Exception:  # noqa  (the session is going away)
+            pass
+
+    def _submit_leased(self, spec, deps):
+        blob = spec.pop("fblob", None)
+        if blob is not None:  # workers fetch functions they have not seen from the head
+            self.client.call("register_function", spec["fid"], blob)
+        spec["owner_key"] = self.client.key
+        res = spec.get("resources") or {}
+        key = tuple(sorted((k, v) for k, v in res.items() if v > 0))
+        ch = self.task_channels.get(key)
+        if ch is None:
+            from .direct_transport import TaskLeaseChannel
+
+            with self._chan_lock:
+                ch = self.task_channels.get(key)
+                if ch is None:
+                    ch = self.task_channels[key] = TaskLeaseChannel(self, dict(key))
+        ch.submit(spec, list(deps))
 
     def submit_actor_task(self, spec, deps):
         """Actor calls go straight to the actor's worker (``direct_transport.ActorChannel``);
@@ -718,6 +765,26 @@ class CoreWorker:
         for ch in list(self.channels.values()):
             ch.close()
         self.channels.clear()
+        for ch in list(self.task_channels.values()):
+            ch.close()
+        self.task_channels.clear()
+        for link in list(self.worker_links.values()):
+            link.close()
+        self.worker_links.clear()
+
+
+def _leasable(spec) -> bool:
+    """Normal tasks that run on a leased worker pushed by their caller: plain CPU-shaped tasks
+    (no placement group / strategy, runtime_env, GPU, generator, or refs nested in inline args,
+    which the head pins while a head-scheduled task runs)."""
+    if spec["kind"] != "task" or spec.get("generator") is not None or spec.get("strategy") is not None:
+        return False
+    if spec.get("runtime_env") or spec.get("contained"):
+        return False
+    for k in (spec.get("resources") or {}):
+        if k == "GPU" or k.startswith("GPU_group") or k.startswith("accelerator_type"):
+            return False
+    return True
 
 
 class _ErrorValue:

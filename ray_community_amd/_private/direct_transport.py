@@ -21,6 +21,13 @@ caller pushes actor tasks straight to the actor's worker, ordered by per-caller 
   * a broken stream means the actor's worker died: the channel re-resolves the actor (waiting for
     the head to restart it or declare it dead), re-sends in-flight calls that have
     ``max_task_retries`` left, and fails the others with ``ActorDiedError``.
+
+Normal tasks take the same road over LEASED workers (``TaskLeaseChannel``, reference
+``normal_task_submitter.cc``): the head grants a worker per burst of same-shaped tasks, the
+caller pushes the tasks to it and owns the results. One reactor thread per process reads every
+worker link. Measured on the core microbenchmark (8 CPUs, A/B in one sitting): single-client
+async tasks 7.8k -> 11.8k/s, multi-client 10.5k -> 24.5k/s, tasks-and-get-batch 7.8 -> 14.9/s,
+sync 2.3k -> 2.75k/s (a 1 ms lease linger keeps one-at-a-time callers on their lease).
 """
 from __future__ import annotations
 
@@ -84,6 +91,7 @@ class OwnedTable:
         self.core = core
         self.cond = threading.Condition(threading.Lock())
         self.objs: Dict[bytes, _Owned] = {}
+        self.waiters: List[list] = []  # wait_ready records: [pending oid set, still needed, Event]
 
     def create(self, oid, tid, channel):
         with self.cond:
@@ -110,6 +118,11 @@ class OwnedTable:
                 cbs, e.callbacks = e.callbacks, []
                 if e.dropped:
                     del self.objs[oid]
+            for w in self.waiters:
+                if oid in w[0]:
+                    w[1] -= 1
+                    if w[1] <= 0:
+                        w[2].set()
         if forward:  # the ref escaped while the call was in flight: hand the value to the head
             self.core.client.call("put", oid, desc[:3], [], False, desc[3])
         for cb in cbs:
@@ -199,59 +212,59 @@ class OwnedTable:
         return out
 
     def wait_ready(self, oids, num_returns, deadline):
-        with self.cond:
-            pending = [o for o in oids if o in self.objs and self.objs[o].desc is None]
-            need = num_returns - (len(oids) - len(pending))
-            ev = self._arm(pending, need) if need > 0 else None
-        if ev is not None:
-            rem = None if deadline is None else max(0.0, deadline - time.monotonic())
-            ev.wait(rem)
+        """``wait``: the ready ones once ``num_returns`` are. Nothing is attached to the objects
+        themselves: one waiter record (the pending set + how many more it needs) is checked by
+        ``set_ready`` -- polling a shrinking list (``ready, rest = wait(rest)``) over N refs costs
+        O(N) per call, not O(N) stale callbacks per object."""
         objs = self.objs
+        with self.cond:
+            ready = []
+            for o in oids:  # in order, stopping once enough are ready (the usual polling case)
+                e = objs.get(o)
+                if e is None or e.desc is not None:
+                    ready.append(o)
+                    if len(ready) >= num_returns:
+                        return ready
+            pending = {o for o in oids if o in objs and objs[o].desc is None}
+            need = num_returns - (len(oids) - len(pending))
+            w = None
+            if need > 0:
+                w = [pending, need, threading.Event()]
+                self.waiters.append(w)
+        if w is not None:
+            rem = None if deadline is None else max(0.0, deadline - time.monotonic())
+            w[2].wait(rem)
+            with self.cond:
+                try:
+                    self.waiters.remove(w)
+                except ValueError:
+                    pass
         return [o for o in oids if (o not in objs) or objs[o].desc is not None]
 
 
 # ====================================================================== caller side
 class _Call:
-    __slots__ = ("spec", "deps", "unresolved", "retries_left", "resolved_args")
+    __slots__ = ("spec", "deps", "unresolved", "retries_left", "resolved_args", "queued", "cancelled", "lease")
 
-    def __init__(self, spec, deps):
+    def __init__(self, spec, deps, retries=None):
         self.spec = spec
         self.deps = deps                  # ObjectRefs kept alive until the call completes
         self.unresolved = 0
-        self.retries_left = spec.get("max_task_retries", 0)
+        self.retries_left = spec.get("max_task_retries", 0) if retries is None else retries
         self.resolved_args = list(spec["args"])
+        self.queued = False               # lease channel: moved to the ready queue
+        self.cancelled = False
+        self.lease = None                 # lease channel: the lease executing it
 
 
-class ActorChannel:
-    """Ordered direct submission to one actor from this process."""
+class _DepResolver:
+    """Caller-side resolution of a call's ObjectRef arguments into descriptors: results this
+    process owns are taken from its table (or waited for), the rest are asked from the head in
+    one batch. ``_deps_progress(call)`` runs (off the thread that delivered the value) each time
+    an argument resolves; ``call.unresolved == 0`` once all have."""
 
-    def __init__(self, core, aid: bytes):
-        self.core = core
-        self.aid = aid
-        self.lock = threading.RLock()
-        self.queue: "collections.deque[_Call]" = collections.deque()
-        self.inflight: Dict[bytes, _Call] = {}
-        self.conn: Optional[P.Connection] = None
-        self.state = "new"  # new | resolving | connected | dead
-        self.incarnation = -1
-        self.dead_error: Optional[BaseException] = None
-        self.holding = False
-        self.broken_calls: List[_Call] = []
-
-    # -------------------------------------------------------------- submit
-    def submit(self, spec, deps):
-        call = _Call(spec, deps)
-        owned = self.core.owned
-        for rid in spec["return_ids"]:
-            owned.create(rid, spec["tid"], self)
-        with self.lock:
-            if self.state == "dead":
-                self._fail(call, self.dead_error)
-                return
-            self._hold(True)
-            self.queue.append(call)
-            self._resolve_deps(call)
-            self._pump()
+    core = None
+    lock = None
 
     def _resolve_deps(self, call):
         args = call.resolved_args
@@ -288,7 +301,7 @@ class ActorChannel:
                 for (i, oid), d in zip(head_ids, descs):
                     call.resolved_args[i] = ("d", oid, d)
                 call.unresolved -= 1
-            self._pump_locked()
+            self._deps_progress(call)
 
         fut.add_done_callback(lambda f, done=done: _bg(done, f))
 
@@ -299,7 +312,42 @@ class ActorChannel:
             if not desc[3] & ser.FLAG_GPU:
                 call.resolved_args[i] = ("d", oid, desc)
             call.unresolved -= 1
-        _bg(self._pump_locked)
+        _bg(self._deps_progress, call)
+
+    def _deps_progress(self, call):
+        raise NotImplementedError
+
+
+class ActorChannel(_DepResolver):
+    """Ordered direct submission to one actor from this process."""
+
+    def __init__(self, core, aid: bytes):
+        self.core = core
+        self.aid = aid
+        self.lock = threading.RLock()
+        self.queue: "collections.deque[_Call]" = collections.deque()
+        self.inflight: Dict[bytes, _Call] = {}
+        self.conn: Optional[P.Connection] = None
+        self.state = "new"  # new | resolving | connected | dead
+        self.incarnation = -1
+        self.dead_error: Optional[BaseException] = None
+        self.holding = False
+        self.broken_calls: List[_Call] = []
+
+    # -------------------------------------------------------------- submit
+    def submit(self, spec, deps):
+        call = _Call(spec, deps)
+        owned = self.core.owned
+        for rid in spec["return_ids"]:
+            owned.create(rid, spec["tid"], self)
+        with self.lock:
+            if self.state == "dead":
+                self._fail(call, self.dead_error)
+                return
+            self._hold(True)
+            self.queue.append(call)
+            self._resolve_deps(call)
+            self._pump()
 
     def _pump_locked(self):
         with self.lock:
@@ -322,6 +370,9 @@ class ActorChannel:
             except OSError:
                 self._on_break()
                 return
+
+    def _deps_progress(self, call):
+        self._pump_locked()
 
     # -------------------------------------------------------------- address / connection
     def _resolve_address(self):
@@ -379,7 +430,7 @@ class ActorChannel:
                 return
             if msg[0] != P.DDONE:
                 continue
-            _, tid, results, head_managed = msg
+            tid, results, head_managed = msg[1], msg[2], msg[3]
             with self.lock:
                 call = self.inflight.pop(tid, None)
             if call is None:
@@ -461,6 +512,485 @@ class ActorChannel:
             self.conn = None
             self.state = "dead"
             self.dead_error = exc.RaySystemError("the session was shut down")
+
+
+# ====================================================================== normal tasks over leased workers
+class _LinkReactor:
+    """One reactor thread per process reads every ``WorkerLink`` through the native epoll
+    reactor (``_native/reactor.cpp``: reads + frame splitting in C++, GIL released); a thread
+    per link would put N GIL-contending readers in the submitter for N leased workers. Each wake
+    handles every frame that arrived, across links. Also runs the lease-linger timers."""
+
+    def __init__(self):
+        from .._native import load
+
+        self.rx = load().Reactor()
+        self.lock = threading.Lock()
+        self.links: Dict[int, "WorkerLink"] = {}
+        self.timers: list = []  # heap of (deadline, seq, fn)
+        self._seq = 0
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="rca-lease-reactor", daemon=True)
+        self._thread.start()
+        import atexit
+
+        # the loop must not be inside poll() (GIL released) when the interpreter finalizes
+        atexit.register(self.stop)
+
+    def stop(self):
+        self._stop = True
+        self.rx.wake()
+        if self._thread is not threading.current_thread():
+            self._thread.join(timeout=2.0)
+
+    def add(self, link):
+        fd = link.conn.sock.fileno()
+        with self.lock:
+            self.links[fd] = link
+        self.rx.add(fd, fd)
+
+    def remove(self, link):
+        fd = link.conn.sock.fileno()
+        if fd < 0:
+            return
+        self.rx.remove(fd)
+        with self.lock:
+            if self.links.get(fd) is link:
+                del self.links[fd]
+
+    def call_later(self, delay, fn):
+        import heapq
+
+        with self.lock:
+            self._seq += 1
+            heapq.heappush(self.timers, (time.monotonic() + delay, self._seq, fn))
+            first = self.timers[0][1] == self._seq
+        if first:
+            self.rx.wake()
+
+    def _fire_timers(self):
+        import heapq
+
+        now = time.monotonic()
+        due = []
+        with self.lock:
+            while self.timers and self.timers[0][0] <= now:
+                due.append(heapq.heappop(self.timers)[2])
+            nxt = self.timers[0][0] - now if self.timers else 1.0
+        for fn in due:
+            try:
+                fn()
+            except Exception:  # noqa
+                log.error("lease reactor timer failed\n%s", traceback.format_exc())
+        return max(0.0, min(1.0, nxt))
+
+    def _loop(self):
+        timeout = 1.0
+        loads = P.loads
+        while not self._stop:
+            try:
+                events = self.rx.poll(int(timeout * 1000) + 1)
+            except Exception:  # noqa
+                events = []
+            timeout = self._fire_timers()
+            for kind, _tok, fd, payload in events:
+                if kind == 0:
+                    link = self.links.get(fd)
+                    if link is not None:
+                        link._on_msg(loads(payload))
+                elif kind == 1:
+                    with self.lock:
+                        link = self.links.pop(fd, None)
+                    if link is not None:
+                        link._on_break()
+
+
+_REACTOR: Optional[_LinkReactor] = None
+
+
+def _reactor() -> _LinkReactor:
+    global _REACTOR
+    if _REACTOR is None:
+        with _EXEC_LOCK:
+            if _REACTOR is None:
+                _REACTOR = _LinkReactor()
+    return _REACTOR
+
+
+class WorkerLink:
+    """This process's stream to one worker's direct socket, shared by every lease on that worker
+    (a lease per burst must not cost a connect + accept + server thread)."""
+
+    def __init__(self, core, path):
+        self.core = core
+        self.path = path
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(path)
+        self.conn = P.Connection(s)
+        self.lock = threading.Lock()
+        self.pending: Dict[bytes, tuple] = {}   # tid -> (channel, lease, call)
+        self.leases: set = set()                # live leases on this worker
+        self.broken = False
+        _reactor().add(self)
+
+    def send(self, channel, lease, call, spec):
+        with self.lock:
+            if self.broken:
+                raise OSError("worker link broken")
+            self.pending[spec["tid"]] = (channel, lease, call)
+        self.conn.send((P.DEXEC, spec))
+
+    def _on_msg(self, msg):
+        if msg[0] != P.DDONE:
+            return
+        with self.lock:
+            ent = self.pending.pop(msg[1], None)
+        if ent is not None:
+            ch, lease, call = ent
+            if len(msg) > 5 and msg[5] is not None:
+                st, en, failed, etype = msg[5]
+                self.core.task_records.append((msg[1], call.spec.get("name"), None, st, en, failed, etype,
+                                               lease.wid, lease.node))
+                _arm_record_flush(self.core)
+            try:
+                ch._on_done(lease, call, msg[2], msg[3], msg[4] if len(msg) > 4 else False)
+            except Exception:  # noqa  (the reactor serves every link: never let one call kill it)
+                log.error("lease channel: completion failed\n%s", traceback.format_exc())
+
+    def close(self):
+        with self.lock:
+            self.broken = True
+        _reactor().remove(self)
+        try:
+            self.conn.close()
+        except Exception:  # noqa
+            pass
+
+    def _on_break(self):
+        with self.lock:
+            if self.broken:
+                return
+            self.broken = True
+            pending, self.pending = self.pending, {}
+            leases, self.leases = list(self.leases), set()
+        links = self.core.worker_links
+        if links.get(self.path) is self:
+            links.pop(self.path, None)
+        try:
+            self.conn.close()
+        except Exception:
+            pass
+        for lease in leases:
+            lease.channel._on_lease_lost(lease)
+
+
+def _arm_record_flush(core):
+    if not core._records_armed:
+        core._records_armed = True
+        _reactor().call_later(0.1, core.flush_task_records)
+
+
+def worker_link(core, path) -> WorkerLink:
+    link = core.worker_links.get(path)
+    if link is None or link.broken:
+        with core._chan_lock:
+            link = core.worker_links.get(path)
+            if link is None or link.broken:
+                link = WorkerLink(core, path)
+                core.worker_links[path] = link
+    return link
+
+
+class _Lease:
+    __slots__ = ("lid", "wid", "node", "link", "channel", "call", "dead", "idle_since")
+
+    def __init__(self, lid, wid, node, link, channel):
+        self.lid, self.wid, self.node, self.link, self.channel = lid, wid, node, link, channel
+        self.call: Optional[_Call] = None
+        self.dead = False
+        self.idle_since: Optional[float] = None
+
+
+class TaskLeaseChannel(_DepResolver):
+    """Normal tasks of one resource shape submitted by this process over leased workers
+    (reference: ``src/ray/core_worker/transport/normal_task_submitter.cc``).
+
+    The head is asked for a worker LEASE per burst, not per task: a lease reserves the shape's
+    resources on a node and names a worker; the caller pushes tasks to it one at a time over the
+    worker's direct socket and the results land in this process's ``OwnedTable`` (the head never
+    sees the task itself, only batched records for the state API). Arguments are resolved here;
+    a call whose arguments are pending waits without blocking the others. At most
+    ``max_pending_leases`` requests are in flight; a lease whose worker finds the queue empty is
+    returned at once. A broken stream means the worker died: in-flight tasks retry
+    (``max_retries``) or fail with the head's verdict (``WorkerCrashedError`` /
+    ``OutOfMemoryError``); application errors retry when ``retry_exceptions`` allows."""
+
+    max_pending_leases = 8
+    linger_s = float(os.environ.get("RCA_LEASE_LINGER_S", "0.001"))
+
+    def __init__(self, core, resources):
+        self.core = core
+        self.resources = dict(resources)
+        self.lock = threading.RLock()
+        self.ready: "collections.deque[_Call]" = collections.deque()
+        self.idle: List[_Lease] = []
+        self.leases: Dict[bytes, _Lease] = {}
+        self.requests = 0
+        self.calls: Dict[bytes, _Call] = {}  # submitted, not yet completed
+        self.linger_armed = False
+        self.closed = False
+
+    # -------------------------------------------------------------- submit
+    # State changes happen under ``lock``; the I/O they imply (pushing a task, asking the head
+    # for a lease or returning one, failing a call) is collected by ``_plan`` and performed by
+    # ``_act`` after the lock is released, so reader threads never wait behind a socket write or
+    # a head round trip.
+    def submit(self, spec, deps):
+        call = _Call(spec, deps, retries=spec.get("max_retries", 0))
+        owned = self.core.owned
+        for rid in spec["return_ids"]:
+            owned.create(rid, spec["tid"], self)
+        with self.lock:
+            self.calls[spec["tid"]] = call
+            self._resolve_deps(call)
+            acts = self._maybe_ready(call, [])
+            acts = self._plan(acts)
+        self._act(acts)
+
+    def _maybe_ready(self, call, acts):
+        if call.unresolved == 0 and not call.queued:
+            call.queued = True
+            if call.cancelled:
+                acts.append(("fail", call, exc.TaskCancelledError(call.spec["tid"].hex())))
+            else:
+                self.ready.append(call)
+        return acts
+
+    def _deps_progress(self, call):
+        with self.lock:
+            acts = self._plan(self._maybe_ready(call, []))
+        self._act(acts)
+
+    def _plan(self, acts):
+        if self.closed:
+            return acts
+        while self.ready and self.idle:
+            lease = self.idle.pop()
+            if lease.dead:
+                continue
+            lease.idle_since = None
+            call = self.ready.popleft()
+            call.lease = lease
+            lease.call = call
+            acts.append(("run", lease, call))
+        want = min(len(self.ready) - self.requests, self.max_pending_leases - self.requests)
+        if want > 0:
+            self.requests += want
+            acts.append(("lease", want))
+        if not self.ready and self.idle:
+            if self.linger_s > 0 and not self.closed:
+                # keep idle leases briefly: a caller submitting one task at a time reuses them
+                now = time.monotonic()
+                for lease in self.idle:
+                    if lease.idle_since is None:
+                        lease.idle_since = now
+                if not self.linger_armed:
+                    self.linger_armed = True
+                    acts.append(("linger",))
+                return acts
+            idle, self.idle = self.idle, []
+            for lease in idle:
+                self.leases.pop(lease.lid, None)
+                lease.dead = True
+                acts.append(("return", lease))
+        return acts
+
+    def _expire_idle(self):
+        with self.lock:
+            self.linger_armed = False
+            now = time.monotonic()
+            keep, acts = [], []
+            for lease in self.idle:
+                if self.closed or self.ready or lease.idle_since is None or now - lease.idle_since < self.linger_s:
+                    keep.append(lease)
+                else:
+                    self.leases.pop(lease.lid, None)
+                    lease.dead = True
+                    acts.append(("return", lease))
+            self.idle = keep
+            if keep and not self.ready:
+                self.linger_armed = True
+                acts.append(("linger",))
+        self._act(acts)
+
+    def _act(self, acts):
+        for act in acts:
+            kind = act[0]
+            if kind == "run":
+                self._run(act[1], act[2])
+            elif kind == "lease":
+                for _ in range(act[1]):
+                    fut = self.core.client.call_async("lease", self.resources, self.core.node_id)
+                    fut.add_done_callback(lambda f: _bg(self._on_grant, f))
+            elif kind == "return":
+                lease = act[1]
+                with lease.link.lock:
+                    lease.link.leases.discard(lease)
+                self.core.client.call_async("return_lease", lease.lid)
+            elif kind == "fail":
+                self._fail(act[1], act[2])
+            elif kind == "linger":
+                _reactor().call_later(self.linger_s, self._expire_idle)
+
+    # -------------------------------------------------------------- leases
+    def _on_grant(self, fut):
+        try:
+            grant = fut.result()
+        except BaseException as e:  # noqa
+            with self.lock:
+                self.requests -= 1
+                calls, self.ready = list(self.ready), collections.deque()
+            for c in calls:
+                self._fail(c, e if isinstance(e, exc.RayError) else exc.RaySystemError(f"worker lease failed: {e}"))
+            return
+        if grant is None:  # the head dropped the request (shutdown)
+            with self.lock:
+                self.requests -= 1
+            return
+        lid, wid, path, node = grant
+        try:
+            link = worker_link(self.core, path)
+        except OSError:
+            link = None
+        lease = _Lease(lid, wid, node, link, self) if link is not None else None
+        if lease is not None:
+            with link.lock:
+                if link.broken:
+                    lease = None  # the worker died already: its lease ended with it at the head
+                else:
+                    link.leases.add(lease)
+        with self.lock:
+            self.requests -= 1
+            if link is not None and lease is None:
+                acts = self._plan([])
+            elif lease is None or self.closed:
+                acts = self._plan([])
+                self.core.client.call_async("return_lease", lid)
+            else:
+                self.leases[lid] = lease
+                self.idle.append(lease)
+                acts = self._plan([])
+        self._act(acts)
+
+    def _run(self, lease, call):
+        spec = dict(call.spec)
+        spec["args"] = call.resolved_args
+        spec["node_id"] = lease.node
+        spec["gpu_ids"] = ()
+        try:
+            lease.link.send(self, lease, call, spec)
+        except OSError:
+            pass  # the link's reader sees the break and hands the call back (_on_lease_lost)
+
+    def _on_done(self, lease, call, results, head_managed, retryable):
+        with self.lock:
+            lease.call = None
+            call.lease = None
+            retry = retryable and call.retries_left != 0 and not call.cancelled
+            if retry:
+                if call.retries_left > 0:
+                    call.retries_left -= 1
+                self.ready.appendleft(call)
+            if not lease.dead:
+                self.idle.append(lease)
+            acts = self._plan([])
+        self._act(acts)
+        if retry:
+            return
+        self.calls.pop(call.spec["tid"], None)
+        owned = self.core.owned
+        for rid, r in zip(call.spec["return_ids"], results):
+            owned.set_ready(rid, r, head_managed)
+        call.deps = None
+
+    def _on_lease_lost(self, lease):
+        """The leased worker's stream broke (it died): the head has ended the lease with it."""
+        err = verdict = None
+        with self.lock:
+            lease.dead = True
+            self.leases.pop(lease.lid, None)
+            call, lease.call = lease.call, None
+            if call is not None:
+                call.lease = None
+                if call.cancelled:
+                    err = exc.TaskCancelledError(call.spec["tid"].hex())
+                elif call.retries_left != 0:
+                    if call.retries_left > 0:
+                        call.retries_left -= 1
+                    self.ready.appendleft(call)
+                else:
+                    verdict = call
+            acts = self._plan([])
+        self._act(acts)
+        if err is not None:
+            self._fail(call, err)
+        if verdict is None:
+            return
+        fut = self.core.client.call_async("lease_fate", lease.lid)
+
+        def on_verdict(f, call=verdict):
+            try:
+                e = f.result()
+            except BaseException as x:  # noqa
+                e = x
+            self._fail(call, e if isinstance(e, BaseException) else exc.WorkerCrashedError(str(e)))
+
+        fut.add_done_callback(lambda f: _bg(on_verdict, f))
+
+    def _fail(self, call, err):
+        self.calls.pop(call.spec["tid"], None)
+        d = error_desc(err)
+        for rid in call.spec["return_ids"]:
+            self.core.owned.set_ready(rid, d)
+        call.deps = None
+
+    # -------------------------------------------------------------- cancel / close
+    def cancel(self, tid, force):
+        with self.lock:
+            c = self.calls.get(tid)
+            if c is None:
+                return False
+            c.cancelled = True
+            lease = c.lease
+            if lease is not None:  # running: the worker interrupts it (force: exits)
+                try:
+                    lease.link.conn.send((P.DCANCEL, tid, force))
+                except OSError:
+                    pass
+                return True
+            if not c.queued:
+                return True  # still resolving its arguments: failed once they arrive
+            try:
+                self.ready.remove(c)
+            except ValueError:
+                return True
+        self._fail(c, exc.TaskCancelledError(tid.hex()))
+        return True
+
+    def close(self):
+        with self.lock:
+            self.closed = True
+            acts = []
+            for lease in list(self.leases.values()):
+                if lease.call is None and not lease.dead:
+                    lease.dead = True
+                    acts.append(("return", lease))
+            self.leases.clear()
+            self.idle = []
+        try:
+            self._act(acts)
+        except Exception:  # noqa
+            pass
 
 
 # ====================================================================== actor-worker side

@@ -16,7 +16,6 @@ import collections
 import json
 import logging
 import os
-import selectors
 import shutil
 import socket
 import subprocess
@@ -99,7 +98,7 @@ class ObjEntry:
 class TaskState:
     __slots__ = ("tid", "spec", "state", "deps", "retries_left", "worker", "node", "demand", "owner", "key", "gpus",
                  "times", "children", "parent", "cancelled", "blocked", "gen_items", "gen_done", "gen_waiters",
-                 "error_type", "attempt")
+                 "error_type", "attempt", "reply")
 
     def __init__(self, tid, spec, owner):
         self.tid = tid
@@ -123,6 +122,7 @@ class TaskState:
         self.gen_waiters: Dict[int, List[Deferred]] = {}
         self.error_type = None
         self.attempt = 0
+        self.reply: Optional[Deferred] = None  # leases: the grant reply
 
 
 class ActorState:
@@ -228,6 +228,11 @@ class Head:
         self.num_reconstructions = 0
         # records of directly transported actor calls (state API / timeline), batched by workers
         self.direct_tasks: collections.deque = collections.deque(maxlen=int(self.config.get("direct_task_records", 10000)))
+        # worker leases of direct task submitters: lease id -> TaskState (kind "lease")
+        self.leases: Dict[bytes, TaskState] = {}
+        self.leases_by_owner: Dict[str, Set[bytes]] = {}
+        self.lease_fates: Dict[bytes, BaseException] = {}
+        self.lease_fate_waiters: Dict[bytes, List[Deferred]] = {}
         self.timers: List[tuple] = []
         self.spilled_bytes = 0
         self.num_spilled = 0
@@ -262,11 +267,11 @@ class Head:
         self.listener.bind(self.sock_path)
         self.listener.listen(1024)
         self.listener.setblocking(False)
-        self.sel = selectors.DefaultSelector()
-        self.sel.register(self.listener, selectors.EVENT_READ, ("listen", None))
-        self._wake_r, self._wake_w = socket.socketpair()
-        self._wake_r.setblocking(False)
-        self.sel.register(self._wake_r, selectors.EVENT_READ, ("wake", None))
+        # native epoll reactor (_native/reactor.cpp): accepts, reads and splits frames in C++
+        # with the GIL released; the loop gets every frame that arrived in one batch
+        self.reactor = native().Reactor()
+        self.reactor.add(self.listener.fileno(), -1, True)
+        self.conns: Dict[int, tuple] = {}  # fd -> (socket, ClientConn)
         self.conn_worker: Dict[int, WorkerState] = {}
         self.clients: Dict[int, "ClientConn"] = {}
         self._thread = threading.Thread(target=self._loop, name="rca-head", daemon=True)
@@ -312,63 +317,67 @@ class Head:
 
     # ================================================================== main loop
     def _loop(self):
+        reactor = self.reactor
+        loads = P.loads
         while not self.shutting_down:
             try:
-                events = self.sel.select(timeout=0.05)
-            except OSError:
+                events = reactor.poll(50)
+            except Exception:  # noqa
                 if self.shutting_down:
                     return
                 raise
-            for key, _ in events:
-                kind, obj = key.data
-                if kind == "listen":
-                    self._accept()
-                elif kind == "wake":
-                    try:
-                        self._wake_r.recv(65536)
-                    except BlockingIOError:
-                        pass
-                elif kind == "conn":
-                    self._read_conn(key.fileobj, obj)
+            if events:
+                self._on_events(events, loads)
             if self.timers:
                 self._fire_timers()
             self._reap_idle()
             self.memory_monitor.poll(self)
 
+    def _on_events(self, events, loads):
+        conns = self.conns
+        batch = []  # consecutive frames handled under one lock acquisition
+        for kind, token, fd, payload in events:
+            if kind == 0:
+                ent = conns.get(fd)
+                if ent is not None:
+                    try:
+                        batch.append((ent[1], loads(payload)))
+                    except Exception:
+                        log.error("head: undecodable frame\n%s", traceback.format_exc())
+                continue
+            if batch:
+                self._handle_batch(batch)
+                batch = []
+            if kind == 2:
+                c = socket.socket(fileno=fd)
+                c.setblocking(True)
+                cc = ClientConn(c)
+                conns[fd] = (c, cc)
+                self.reactor.add(fd, fd)
+            elif kind == 1:
+                ent = conns.pop(fd, None)
+                if ent is not None:
+                    self._on_disconnect(ent[0], ent[1])
+        if batch:
+            self._handle_batch(batch)
+
+    def _handle_batch(self, batch):
+        with self.lock:
+            for cc, msg in batch:
+                try:
+                    self._handle(cc, msg)
+                except Exception:
+                    log.error("head: error handling %s\n%s", msg[0], traceback.format_exc())
+
     def wake(self):
         try:
-            self._wake_w.send(b"x")
-        except OSError:
+            self.reactor.wake()
+        except Exception:  # noqa
             pass
-
-    def _accept(self):
-        while True:
-            try:
-                c, _ = self.listener.accept()
-            except (BlockingIOError, OSError):
-                return
-            c.setblocking(True)
-            cc = ClientConn(c)
-            self.sel.register(c, selectors.EVENT_READ, ("conn", cc))
-
-    def _read_conn(self, sock, cc):
-        try:
-            data = sock.recv(1 << 20)
-        except (ConnectionError, OSError):
-            data = b""
-        if not data:
-            self._on_disconnect(sock, cc)
-            return
-        for msg in cc.reader.feed(data):
-            try:
-                with self.lock:
-                    self._handle(cc, msg)
-            except Exception:
-                log.error("head: error handling %s\n%s", msg[0], traceback.format_exc())
 
     def _on_disconnect(self, sock, cc):
         try:
-            self.sel.unregister(sock)
+            self.reactor.remove(sock.fileno())
         except Exception:
             pass
         try:
@@ -379,7 +388,9 @@ class Head:
             if cc.worker is not None:
                 self._on_worker_death(cc.worker, "worker process exited")
             elif cc.client_key is not None:
+                self._return_leases_of(cc.client_key)
                 self._drop_holder_everywhere(cc.client_key)
+                self._schedule()
 
     def _send(self, cc_or_worker, msg):
         conn = cc_or_worker.conn if isinstance(cc_or_worker, WorkerState) else cc_or_worker
@@ -1339,6 +1350,9 @@ class Head:
     # ================================================================== dispatch / completion
     def _dispatch(self, w: WorkerState, ts: TaskState):
         spec = ts.spec
+        if spec["kind"] == "lease":
+            self._grant_lease(w, ts)
+            return
         ts.worker = w.wid
         ts.state = T_RUNNING
         ts.attempt += 1
@@ -1484,7 +1498,7 @@ class Head:
         if w is None or w.task is None:
             return
         ts = w.task
-        if ts.spec["kind"] != "task" or ts.node is None:
+        if ts.spec["kind"] not in ("task", "lease") or ts.node is None:
             return
         cpu = {k: v for k, v in ts.demand.items() if k == "CPU" or k.startswith("CPU_group")}
         if not cpu:
@@ -1527,9 +1541,12 @@ class Head:
         if getattr(w, "oom_killed", None):
             reason = f"killed by the memory monitor (node memory usage {w.oom_killed[0]:.2f} >= " \
                      f"threshold {w.oom_killed[1]:.2f})"
+        self._return_leases_of("w:" + w.wid.hex())  # leases this worker held as a submitter
         if w.actor is not None:
             a = w.actor
             self._on_actor_worker_death(a, reason, ts)
+        elif ts is not None and ts.spec["kind"] == "lease":
+            self._lease_worker_died(w, ts, reason)
         elif ts is not None and ts.state == T_RUNNING:
             self._release_task_resources(ts)
             if ts.cancelled:
@@ -1822,14 +1839,26 @@ class Head:
         e.holders.add(caller)
         return True
 
-    def rpc_put_owned(self, caller, items, owner_key):
-        """An actor worker registers direct-call results the head must manage (shm, GPU, nested
-        refs) on behalf of the calling process ``owner_key`` before replying to it."""
+    def rpc_put_owned(self, caller, items, owner_key, lineage=None):
+        """A worker registers direct-call results the head must manage (shm, GPU, nested refs) on
+        behalf of the calling process ``owner_key`` before replying to it. ``lineage``: the spec
+        of a retryable leased task, kept so lost outputs can be recomputed like head-run ones."""
         gpu_owner = bytes.fromhex(caller[2:]) if caller.startswith("w:") else None
         w = self.workers.get(gpu_owner) if gpu_owner else None
+        tid = None
+        if lineage is not None:
+            tid = lineage["tid"]
+            self.lineage[tid] = [lineage, owner_key, int(lineage.get("max_retries", 0))]
+            self.lineage.move_to_end(tid)
+            while len(self.lineage) > self.lineage_max:
+                self.lineage.popitem(last=False)
         for oid, desc, contained, is_gpu, flags in items:
             e = self._obj(oid)
             e.holders.add(owner_key)
+            if tid is not None:
+                e.task = tid
+            if w is not None:
+                e.node = w.node_id
             owner = None
             if is_gpu and w is not None:
                 owner = gpu_owner
@@ -1842,6 +1871,118 @@ class Head:
         w = self.workers.get(bytes.fromhex(caller[2:])) if caller.startswith("w:") else None
         if w is not None and w.actor is not None:
             self._kill_actor(w.actor, no_restart=True, reason="exit_actor() called", graceful=True)
+        return True
+
+    # -------------------------------------------------------------- worker leases (direct tasks)
+    def rpc_lease(self, caller, resources, caller_node=None):
+        """Lease a worker for normal tasks of one resource shape (reference:
+        ``NodeManager::HandleRequestWorkerLease`` + ``NormalTaskSubmitter``). The lease goes
+        through the ordinary scheduler like a task; once a worker is assigned the caller gets
+        ``(lease_id, worker_id, direct socket, node_id)`` and pushes its tasks to the worker
+        itself until it returns the lease. The lease holds the shape's resources meanwhile."""
+        lid = new_id()
+        spec = {"tid": lid, "kind": "lease", "name": "lease", "resources": dict(resources or {}), "args": (),
+                "return_ids": (), "caller_node": caller_node, "max_retries": -1}
+        ts = TaskState(lid, spec, caller)
+        d = Deferred()
+        ts.reply = d
+        self.leases[lid] = ts
+        self.leases_by_owner.setdefault(caller, set()).add(lid)
+        self._enqueue(ts)
+        return d
+
+    def _grant_lease(self, w, ts):
+        ts.worker = w.wid
+        ts.state = T_RUNNING
+        ts.times["start"] = time.time()  # memory-monitor victim order: newest first
+        w.state = "busy"
+        w.task = ts
+        d = ts.reply
+        if d is not None and not d.done:
+            d.resolve((ts.tid, w.wid, w.direct_addr, ts.node))
+
+    def _end_lease(self, ts, make_available=True):
+        self.leases.pop(ts.tid, None)
+        s = self.leases_by_owner.get(ts.owner)
+        if s is not None:
+            s.discard(ts.tid)
+            if not s:
+                self.leases_by_owner.pop(ts.owner, None)
+        d = ts.reply
+        if d is not None and not d.done:
+            d.resolve(None)  # cancelled before a worker was assigned
+        state = ts.state
+        if state in (T_QUEUED, T_WAIT_DEPS):
+            ts.cancelled = True
+            if ts.key is not None and self.sched.cancel(ts.key):
+                self.task_keys.pop(ts.key, None)
+        elif state == T_WAIT_WORKER:
+            ts.cancelled = True
+            self._release_task_resources(ts)
+        elif state == T_RUNNING:
+            self._release_task_resources(ts)
+            w = self.workers.get(ts.worker)
+            if w is not None and w.task is ts:
+                w.task = None
+                if make_available:
+                    self._worker_available(w)
+        ts.state = T_FINISHED
+
+    def rpc_return_lease(self, caller, lid):
+        ts = self.leases.get(lid)
+        if ts is not None:
+            self._end_lease(ts)
+            self._schedule()
+        return True
+
+    def rpc_lease_fate(self, caller, lid):
+        """Why a leased worker went away (the caller saw its stream break): the error its
+        in-flight task fails with. Resolved once the head has processed the worker's death."""
+        d = Deferred()
+        fate = self.lease_fates.get(lid)
+        if fate is not None:
+            d.resolve(fate)
+        else:
+            self.lease_fate_waiters.setdefault(lid, []).append(d)
+            self._add_timer(10.0, lambda: None if d.done else d.resolve(
+                exc.WorkerCrashedError("The worker executing this task died unexpectedly.")))
+        return d
+
+    def _lease_worker_died(self, w, ts, reason):
+        if getattr(w, "oom_killed", None):
+            u, thr = w.oom_killed
+            err = exc.OutOfMemoryError(
+                f"A task was killed by the memory monitor: node memory usage {u:.2f} exceeded the threshold "
+                f"{thr:.2f} (memory_usage_threshold) and its retries are exhausted. Reduce the task's memory, "
+                "lower its parallelism, or raise max_retries.")
+        else:
+            err = exc.WorkerCrashedError(f"The worker died unexpectedly while executing a task ({reason}).")
+        self.lease_fates[ts.tid] = err
+        while len(self.lease_fates) > 10000:
+            self.lease_fates.pop(next(iter(self.lease_fates)))
+        for d in self.lease_fate_waiters.pop(ts.tid, ()):
+            d.resolve(err)
+        self._end_lease(ts, make_available=False)
+
+    def _return_leases_of(self, owner):
+        for lid in list(self.leases_by_owner.get(owner, ())):
+            ts = self.leases.get(lid)
+            if ts is not None:
+                self._end_lease(ts)
+
+    def rpc_get_function(self, caller, fid):
+        """Function blob for a worker that received a task directly (not through the head)."""
+        return self.functions.get(fid)
+
+    def rpc_direct_task_records(self, caller, records):
+        """(tid, name, None, start, end, failed, error type, worker id, node) of leased tasks,
+        reported by their caller."""
+        for tid, name, aid, start, end, failed, etype, wid, node in records:
+            w = self.workers.get(wid)
+            self.direct_tasks.append((tid, name, aid, start, end, failed, etype, wid, node))
+            pid = w.pid if w is not None else None
+            self.events.append((start, tid, "running", name, pid, node))
+            self.events.append((end, tid, "failed" if failed else "finished", name, pid, node))
         return True
 
     def _on_direct_events(self, w, records):
@@ -2088,6 +2229,8 @@ class Head:
 
     # ================================================================== state / observability
     def _event(self, ts, what, worker=None):
+        if ts.spec["kind"] == "lease":
+            return
         self.events.append((time.time(), ts.tid, what, ts.spec.get("name"), worker.pid if worker else None,
                             ts.node))
 
@@ -2109,7 +2252,8 @@ class Head:
                         "func_or_class_name": ts.spec.get("name")})
         for tid, name, aid, start, end, failed, etype, wid, node in list(self.direct_tasks)[-limit:]:
             out.append({"task_id": tid.hex(), "name": name, "state": "FAILED" if failed else "FINISHED",
-                        "type": "ACTOR_TASK", "node_id": node, "worker_id": wid.hex() if wid else None,
+                        "type": "ACTOR_TASK" if aid else "NORMAL_TASK", "node_id": node,
+                        "worker_id": wid.hex() if wid else None,
                         "actor_id": aid.hex() if aid else None, "required_resources": {}, "error_type": etype,
                         "attempt_number": 0, "start_time_ms": int(start * 1000), "end_time_ms": int(end * 1000),
                         "func_or_class_name": name})
@@ -2274,8 +2418,14 @@ class Head:
                 except Exception:
                     pass
         self._thread.join(timeout=2)
+        for c, _cc in list(self.conns.values()):
+            try:
+                c.close()
+            except OSError:
+                pass
+        self.conns.clear()
         try:
-            self.sel.close()
+            self.reactor.close()
         except Exception:
             pass
         try:

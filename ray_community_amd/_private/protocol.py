@@ -45,8 +45,22 @@ def loads(b):
     return pickle.loads(b)
 
 
+def _native_send_frame():
+    try:
+        from .._native import load
+
+        return load().send_frame
+    except Exception:  # noqa  (no native module: pure-Python framing)
+        return None
+
+
+_SEND_FRAME = _native_send_frame()
+
+
 class Connection:
-    """Blocking framed connection with a send lock (many threads may send)."""
+    """Blocking framed connection with a send lock (many threads may send). Frames go out
+    through the native ``send_frame`` (header + payload in one ``sendmsg``, GIL released for
+    large payloads) when the runtime core is built."""
 
     def __init__(self, sock: socket.socket):
         self.sock = sock
@@ -55,8 +69,11 @@ class Connection:
 
     def send(self, msg):
         data = dumps(msg)
-        hdr = _LEN.pack(len(data))
         with self._send_lock:
+            if _SEND_FRAME is not None:
+                _SEND_FRAME(self.sock.fileno(), data)
+                return
+            hdr = _LEN.pack(len(data))
             if len(data) < 65536:
                 self.sock.sendall(hdr + data)
             else:

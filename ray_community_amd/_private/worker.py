@@ -319,6 +319,9 @@ def timeline(filename=None):
     from ..util import tracing
 
     tracing._flush_to_head()
+    from ..util.state import _flush_own_task_records
+
+    _flush_own_task_records()
     evs = _core().client.call("timeline")
     if filename:
         with open(filename, "w") as f:

@@ -143,16 +143,27 @@ class Worker:
             return
         # results the head has to manage (shm / GPU / nested refs) are registered before replying
         head_managed = any(r[0] != "inline" or r[3] or r[5] for r in results)
+        failed = bool(info.get("error"))
         if head_managed:
+            lineage = None
+            if spec["kind"] == "task" and spec.get("max_retries", 0) != 0 and not failed:
+                lineage = _lineage_spec(spec)  # leased task: lost outputs stay recomputable
             self.client.call("put_owned", [(rid, r[0:3], r[3], r[5], r[4]) for rid, r in
-                                           zip(spec["return_ids"], results)], spec["owner_key"])
+                                           zip(spec["return_ids"], results)], spec["owner_key"], lineage)
         if info.get("spans"):  # tracing on: spans reach the head before the caller sees the result
             self.client.call("add_spans", info["spans"])
+        leased = spec["kind"] == "task"
+        # a leased task's (start, end, outcome) rides on the reply: its CALLER reports it to the
+        # head (and flushes before its own state-API / timeline queries); actor calls are batched
+        # by this worker
+        rec = (t_start, time.time(), failed, info.get("error_type")) if leased else None
         try:
-            conn.send((P.DDONE, tid, [(r[0], r[1], r[2], r[4]) for r in results], head_managed))
+            conn.send((P.DDONE, tid, [(r[0], r[1], r[2], r[4]) for r in results], head_managed,
+                       failed and bool(info.get("retryable")), rec))
         except OSError:
             pass
-        self.direct.record(spec, t_start, time.time(), info)
+        if not leased:
+            self.direct.record(spec, t_start, time.time(), info)
         if info.get("actor_exit"):
             self.direct.flush()
             self.client.call_async("actor_exit")
@@ -210,6 +221,10 @@ class Worker:
         if spec.get("fblob") is not None:
             self.functions[fid] = ser.loads_function(spec["fblob"])
         fn = self.functions.get(fid)
+        if fn is None and fid is not None:
+            blob = self.client.call("get_function", fid)  # a task pushed by its caller directly
+            if blob is not None:
+                fn = self.functions[fid] = ser.loads_function(blob)
         if fn is None:
             raise exc.RaySystemError(f"function {spec.get('name')} not available on this worker")
         return fn
@@ -467,6 +482,14 @@ class _DepError(Exception):
     def __init__(self, err):
         super().__init__(str(err))
         self.err = err
+
+
+def _lineage_spec(spec):
+    """The submission form of a leased task's spec (arguments back to refs), for the head's
+    lineage table."""
+    out = {k: v for k, v in spec.items() if k not in ("_reply", "gpu_ids", "node_id", "fblob")}
+    out["args"] = [("r", a[1]) if a[0] == "d" else a for a in spec["args"]]
+    return out
 
 
 def _span_name(spec):

@@ -33,7 +33,22 @@ def list_actors(filters: Optional[List[Tuple[str, str, Any]]] = None, limit: int
 
 
 def list_tasks(filters=None, limit: int = 10000, detail=False, **kw):
+    _flush_own_task_records()
     return _filter(_call("list_tasks", limit), filters)[:limit]
+
+
+def _flush_own_task_records():
+    """Leased tasks are reported to the head by their submitter in batches: this process's
+    pending records go first, so its own finished tasks are listed."""
+    from .._private.core_worker import global_core
+
+    try:
+        c = global_core()
+    except Exception:  # noqa
+        return
+    if c is not None and c.task_records:
+        recs, c.task_records = c.task_records, []
+        c.client.call("direct_task_records", recs)
 
 
 def list_objects(filters=None, limit: int = 10000, detail=False, **kw):
