@@ -137,12 +137,12 @@ __device__ __forceinline__ float xhalf_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// single v_max3_f32 (plain fmaxf on MFMA results gets canonicalising v_max pairs from hipcc)
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// max of three in plain C: hipcc emits one v_max3_f32 per call on MFMA results (no canonicalising
+// v_max pairs) AND counts the MFMA -> VALU read hazard wait states. An inline-asm v_max3 here was
+// issued with NO wait states behind the S^T MFMA chain (the hazard recognizer does not look into
+// asm operands), so it read stale accumulator VGPRs: a timing-dependent row max, i.e. a
+// run-to-run nondeterministic forward.
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 __device__ __forceinline__ float max16(const f32x16& s, float init) {
   float a = max3f(init, s[0], s[1]), b = max3f(s[2], s[3], s[4]);

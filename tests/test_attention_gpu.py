@@ -98,3 +98,22 @@ def test_flash_attention_xcd_grouped_fwd_bwd(B, S, Hq, Hk, D, causal):
     assert _err(v.grad, vr.grad) < 3e-2
     # every (batch, kv-head) group is covered: no head left unwritten
     assert torch.isfinite(q.grad).all() and k.grad.float().abs().amax(dim=(1, 3)).min() > 0
+
+
+@pytest.mark.parametrize("B,S,Hq,Hk,D", [(2, 128, 4, 2, 64), (2, 1024, 32, 8, 128), (1, 512, 16, 8, 64)])
+def test_flash_attention_bitwise_deterministic(B, S, Hq, Hk, D):
+    """Forward and backward are bitwise reproducible run to run (no float atomics, no hazards):
+    an inline-asm v_max3 that read the S^T MFMA accumulators without the MFMA->VALU wait states
+    once made the forward's row max (and so the output rounding) timing dependent."""
+    q, k, v = _mk(B, S, Hq, D, 31), _mk(B, S, Hk, D, 32), _mk(B, S, Hk, D, 33)
+    do = _mk(B, S, Hq, D, 34)
+    runs = []
+    for _ in range(4):
+        qq, kk, vv = (t.clone().requires_grad_(True) for t in (q, k, v))
+        o = ops.flash_attention(qq, kk, vv, True)
+        o.backward(do)
+        runs.append((o.detach(), qq.grad, kk.grad, vv.grad))
+    torch.cuda.synchronize()
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
