@@ -22,6 +22,10 @@ def shapes(T=8192, H=4096, I=14336, V=128256, kv=1024):
         out.append((f"{name}.fwd", "fwd", T, K, N))
         out.append((f"{name}.dgrad", "dgrad", T, K, N))
         out.append((f"{name}.wgrad", "wgrad", T, K, N))
+        # the layouts the training step issues with RCA_BWD_TRANSPOSED=1 (parallel/fused_linear.py):
+        # dgrad = F.linear(gy, W^T) and wgrad = gy^T @ (x^T)^T on producer-transposed copies
+        out.append((f"{name}.dgrad_tr", "dgrad_tr", T, K, N))
+        out.append((f"{name}.wgrad_tr", "wgrad_tr", T, K, N))
     return out
 
 
@@ -34,6 +38,12 @@ def make(kind, T, K, N, dev):
         return lambda: F.linear(x, w)
     if kind == "dgrad":
         return lambda: torch.matmul(gy, w)
+    if kind == "dgrad_tr":
+        wt = w.t().contiguous()
+        return lambda: F.linear(gy, wt)
+    if kind == "wgrad_tr":
+        gt, xt = gy.t().contiguous(), x.t().contiguous()
+        return lambda: torch.mm(gt, xt.t(), out=dw)
     return lambda: torch.mm(gy.t(), x, out=dw)
 
 
@@ -66,6 +76,7 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--out", default="gpurun_out/gemm_tuned.csv")
     ap.add_argument("--tokens", type=int, default=8192)
+    ap.add_argument("--tune-ms", type=int, default=30, help="TunableOp time budget per candidate solution")
     ap.add_argument("--table", default=None, help="compare default vs an existing tuned table (no tuning)")
     a = ap.parse_args()
     dev = "cuda"
@@ -92,7 +103,7 @@ def main():
         tun.set_filename(a.out)
         if os.path.exists(a.out):
             tun.read_file(a.out)  # resume: shapes already in the table are not re-tuned
-        tun.set_max_tuning_duration(12)
+        tun.set_max_tuning_duration(a.tune_ms)
         tun.set_max_tuning_iterations(10)
         for name, kind, T, K, N in shapes(a.tokens):
             fn = make(kind, T, K, N, dev)
@@ -112,7 +123,8 @@ def main():
         t0, t1 = res[name]
         tot0 += t0
         tot1 += t1 or t0
-        m, n, k = {"fwd": (T, N, K), "dgrad": (T, K, N), "wgrad": (N, K, T)}[kind]
+        m, n, k = {"fwd": (T, N, K), "dgrad": (T, K, N), "wgrad": (N, K, T), "dgrad_tr": (T, K, N),
+                   "wgrad_tr": (N, K, T)}[kind]
         s1 = f"{1e3 * t1:9.3f} {fl / t1 / 1e12:7.0f}" if t1 else ""
         print(f"{name:16s} {f'{m}x{n}x{k}':>22s} {1e3 * t0:10.3f} {fl / t0 / 1e12:7.0f} {s1}", flush=True)
     print(f"per-layer-set total: default {1e3 * tot0:.2f} ms, tuned {1e3 * tot1:.2f} ms")
