@@ -183,7 +183,11 @@ class Reactor {
 }  // namespace
 
 // One frame = header + payload in a single sendmsg (looping over partial writes). The GIL is
-// released for payloads above 64 KiB, where the copy into the socket buffer dominates.
+// released for payloads above 64 KiB, where the copy into the socket buffer dominates, and for ANY
+// frame the moment the socket is full: a small frame is first tried with MSG_DONTWAIT under the GIL
+// and, if the peer is not draining, the rest is written with the GIL released. (Blocking with the
+// GIL held would stop this process's own reader threads -- the ones that drain the peer's replies
+// -- and deadlock two processes that pipeline calls at each other.)
 static void send_frame(int fd, py::bytes payload) {
   char* data;
   Py_ssize_t len;
@@ -191,8 +195,10 @@ static void send_frame(int fd, py::bytes payload) {
   uint64_t n = (uint64_t)len;
   char hdr[8];
   memcpy(hdr, &n, 8);
-  auto do_send = [&]() -> int {
-    size_t sent = 0, total = 8 + (size_t)len;
+  const size_t total = 8 + (size_t)len;
+  size_t sent = 0;
+  // returns 0 when done, EAGAIN when `stop_when_full` and the socket is full, else an errno
+  auto do_send = [&](bool stop_when_full) -> int {
     while (sent < total) {
       iovec iov[2];
       int cnt = 0;
@@ -211,11 +217,12 @@ static void send_frame(int fd, py::bytes payload) {
       msghdr m{};
       m.msg_iov = iov;
       m.msg_iovlen = cnt;
-      ssize_t k = sendmsg(fd, &m, MSG_NOSIGNAL);
+      ssize_t k = sendmsg(fd, &m, MSG_NOSIGNAL | (stop_when_full ? MSG_DONTWAIT : 0));
       if (k < 0) {
         if (errno == EINTR) continue;
-        if (errno == EAGAIN || errno == EWOULDBLOCK) {  // a socket with a timeout is non-blocking
-          pollfd p{fd, POLLOUT, 0};
+        if (errno == EAGAIN || errno == EWOULDBLOCK) {
+          if (stop_when_full) return EAGAIN;
+          pollfd p{fd, POLLOUT, 0};  // a socket with a timeout is non-blocking: wait for room
           ::poll(&p, 1, -1);
           continue;
         }
@@ -225,12 +232,10 @@ static void send_frame(int fd, py::bytes payload) {
     }
     return 0;
   };
-  int err;
-  if (len > (1 << 16)) {
+  int err = len > (1 << 16) ? EAGAIN : do_send(true);
+  if (err == EAGAIN) {
     py::gil_scoped_release nogil;
-    err = do_send();
-  } else {
-    err = do_send();
+    err = do_send(false);
   }
   if (err != 0) {
     errno = err;

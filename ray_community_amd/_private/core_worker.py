@@ -68,7 +68,11 @@ class ObjectRef:
         return self._id.hex()
 
     def task_id(self):
-        return None
+        """``TaskID`` of the task that returns this object (None for ``put`` objects)."""
+        from .ids import TaskID, task_id_of
+
+        t = task_id_of(self._id)
+        return TaskID(t) if t is not None else None
 
     def __hash__(self):
         return hash(self._id)

@@ -8,6 +8,7 @@ from __future__ import annotations
 import json
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from urllib.parse import parse_qs, urlparse
 
 
 class Dashboard:
@@ -66,6 +67,13 @@ class Dashboard:
                     if self._jobs("GET"):
                         return
                     path = self.path.split("?")[0].rstrip("/")
+                    query = parse_qs(urlparse(self.path).query)
+                    if path in ("", "/index.html"):
+                        return self._send(200, _INDEX_HTML, "text/html; charset=utf-8")
+                    if path == "/api/logs/file":
+                        lines = dash._call("get_log", (query.get("filename") or [None])[0], None, None, None, None,
+                                           int((query.get("lines") or ["-1"])[0]))
+                        return self._send(200, "\n".join(lines), "text/plain; charset=utf-8")
                     if path == "/metrics":
                         return self._send(200, dash._call("metrics_text"), "text/plain; version=0.0.4")
                     routes = {"/api/version": lambda: {"version": _version(), "ray_compatible": "3.0.0.dev0"},
@@ -77,7 +85,10 @@ class Dashboard:
                               "/api/objects": lambda: dash._call("list_objects"),
                               "/api/workers": lambda: dash._call("list_workers"),
                               "/api/object_store": lambda: dash._call("store_stats"),
-                              "/api/timeline": lambda: dash._call("timeline")}
+                              "/api/timeline": lambda: dash._call("timeline"),
+                              "/api/logs": lambda: dash._call("list_logs", None, None),
+                              "/api/cluster_events": lambda: dash._call("cluster_events"),
+                              "/api/placement_groups": lambda: list(dash._call("pg_table", None).values())}
                     if path in routes:
                         return self._send(200, json.dumps(routes[path](), default=str), "application/json")
                     return self._send(404, "not found", "text/plain")
@@ -143,3 +154,46 @@ def _version():
     from .. import __version__
 
     return __version__
+
+
+# One self-contained overview page (reference: the dashboard's React client, dashboard/client/):
+# cluster resources, nodes, actors, recent tasks, workers, jobs, events and worker logs, refreshed
+# from the /api/* routes above every two seconds.
+_INDEX_HTML = """<!doctype html><html><head><meta charset="utf-8"><title>ray_community_amd dashboard</title>
+<style>body{font:13px sans-serif;margin:16px;color:#222}h2{margin:18px 0 6px;font-size:15px}
+table{border-collapse:collapse;width:100%}td,th{border:1px solid #ddd;padding:3px 6px;text-align:left;
+vertical-align:top}th{background:#f3f3f3}pre{background:#f7f7f7;padding:8px;max-height:300px;overflow:auto}
+.bar{display:flex;gap:24px}.k{color:#666}</style></head><body>
+<h1>ray_community_amd</h1><div class="bar" id="res"></div>
+<h2>Nodes</h2><div id="nodes"></div><h2>Actors</h2><div id="actors"></div>
+<h2>Recent tasks</h2><div id="tasks"></div><h2>Workers</h2><div id="workers"></div>
+<h2>Jobs</h2><div id="jobs"></div><h2>Cluster events</h2><div id="events"></div>
+<h2>Logs</h2><div id="logs"></div><pre id="logview"></pre>
+<script>
+function esc(v){return String(v===null||v===undefined?"":(typeof v==="object"?JSON.stringify(v):v))
+ .replace(/[&<>]/g,c=>({"&":"&amp;","<":"&lt;",">":"&gt;"}[c]))}
+function table(rows,cols){if(!rows||!rows.length)return "<i>none</i>";
+ return "<table><tr>"+cols.map(c=>"<th>"+c+"</th>").join("")+"</tr>"+rows.map(r=>"<tr>"+cols.map(
+ c=>"<td>"+esc(r[c])+"</td>").join("")+"</tr>").join("")+"</table>"}
+async function j(u){const r=await fetch(u);return r.ok?r.json():null}
+async function showLog(f){const r=await fetch("/api/logs/file?lines=200&filename="+encodeURIComponent(f));
+ document.getElementById("logview").textContent=await r.text()}
+async function refresh(){
+ const cs=await j("/api/cluster_status");if(cs){document.getElementById("res").innerHTML=Object.keys(cs.total)
+  .filter(k=>!k.startsWith("node:")).map(k=>"<div><span class=k>"+esc(k)+"</span> "+esc(cs.available[k]||0)+" / "
+  +esc(cs.total[k])+"</div>").join("")}
+ document.getElementById("nodes").innerHTML=table(await j("/api/nodes"),["NodeID","Alive","IsHead","Resources"]);
+ document.getElementById("actors").innerHTML=table(await j("/api/actors"),["actor_id","class_name","state","name",
+  "pid","num_restarts","death_cause"]);
+ const t=(await j("/api/tasks"))||[];document.getElementById("tasks").innerHTML=table(t.slice(-50).reverse(),
+  ["task_id","name","state","type","worker_id","error_type"]);
+ document.getElementById("workers").innerHTML=table(await j("/api/workers"),["worker_id","pid","state","is_actor",
+  "gpu_ids","log_file"]);
+ document.getElementById("jobs").innerHTML=table(await j("/api/jobs/"),["submission_id","status","entrypoint",
+  "message"]);
+ const ev=(await j("/api/cluster_events"))||[];document.getElementById("events").innerHTML=table(ev.slice(-30)
+  .reverse(),["severity","source_type","message"]);
+ const lg=(await j("/api/logs"))||{};document.getElementById("logs").innerHTML=Object.values(lg).flat().map(
+  f=>"<a href='#' onclick='showLog(\\""+esc(f)+"\\");return false'>"+esc(f)+"</a>").join(" &middot; ")}
+refresh();setInterval(refresh,2000);
+</script></body></html>"""

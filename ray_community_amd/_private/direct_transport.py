@@ -333,6 +333,11 @@ class ActorChannel(_DepResolver):
         self.dead_error: Optional[BaseException] = None
         self.holding = False
         self.broken_calls: List[_Call] = []
+        # frames are queued under ``lock`` (submission order) and written outside it by
+        # ``_flush``: a send blocked on a full socket must never hold ``lock``, which the reader
+        # thread needs to retire completions -- otherwise caller and actor both stop reading
+        self.outbox: "collections.deque[tuple]" = collections.deque()
+        self.send_lock = threading.Lock()
 
     # -------------------------------------------------------------- submit
     def submit(self, spec, deps):
@@ -348,10 +353,30 @@ class ActorChannel(_DepResolver):
             self.queue.append(call)
             self._resolve_deps(call)
             self._pump()
+        self._flush()
 
     def _pump_locked(self):
         with self.lock:
             self._pump()
+        self._flush()
+
+    def _flush(self):
+        """Write queued frames in order (never called with ``lock`` held)."""
+        while self.outbox:
+            with self.send_lock:
+                while True:
+                    try:
+                        conn, msg = self.outbox.popleft()
+                    except IndexError:
+                        break
+                    try:
+                        conn.send(msg)
+                    except OSError:
+                        # frames of a dead connection: its in-flight calls are resent or failed
+                        # by the reconnect path (_on_break -> _on_address)
+                        with self.lock:
+                            if self.conn is conn:
+                                self._on_break()
 
     def _pump(self):
         if self.state == "new":
@@ -365,11 +390,7 @@ class ActorChannel(_DepResolver):
             spec = dict(call.spec)
             spec["args"] = call.resolved_args
             self.inflight[spec["tid"]] = call
-            try:
-                self.conn.send((P.DEXEC, spec))
-            except OSError:
-                self._on_break()
-                return
+            self.outbox.append((self.conn, (P.DEXEC, spec)))
 
     def _deps_progress(self, call):
         self._pump_locked()
@@ -417,6 +438,7 @@ class ActorChannel(_DepResolver):
                 self.queue.appendleft(call)
             threading.Thread(target=self._read_loop, args=(conn,), name="rca-direct-reader", daemon=True).start()
             self._pump()
+        self._flush()
 
     def _read_loop(self, conn):
         owned = self.core.owned
@@ -479,12 +501,12 @@ class ActorChannel(_DepResolver):
                     self._fail(c, exc.TaskCancelledError(tid.hex()))
                     self._maybe_release()
                     return True
-            if tid in self.inflight and self.conn is not None:
-                try:
-                    self.conn.send((P.DCANCEL, tid, False))
-                except OSError:
-                    pass
-                return True
+            queued = tid in self.inflight and self.conn is not None
+            if queued:
+                self.outbox.append((self.conn, (P.DCANCEL, tid, False)))
+        if queued:
+            self._flush()
+            return True
         return False
 
     # -------------------------------------------------------------- actor lifetime

@@ -29,6 +29,7 @@ from typing import Any, Callable, Dict, List, Optional, Set
 from .. import exceptions as exc
 from . import protocol as P
 from .gc_tuning import restore_gc, tune_gc
+from .log_monitor import LogMonitor, read_log
 from .ids import new_id
 from .object_store import ObjectStore, default_store_capacity, native
 from .serialization import FLAG_ERROR, serialize
@@ -253,6 +254,8 @@ class Head:
 
         self.memory_monitor = MemoryMonitor(self.config)
         self._oom_log: collections.deque = collections.deque(maxlen=1000)
+        # cluster events for the state API (node added/removed, worker died, OOM kills)
+        self.cluster_events: collections.deque = collections.deque(maxlen=10000)
         self.spans: collections.deque = collections.deque(maxlen=int(self.config.get("max_spans", 200000)))
         # head node
         self.head_node_id = new_id().hex()
@@ -276,6 +279,11 @@ class Head:
         self.clients: Dict[int, "ClientConn"] = {}
         self._thread = threading.Thread(target=self._loop, name="rca-head", daemon=True)
         self._thread.start()
+        # worker stdout/stderr -> drivers (log_to_driver); see _private/log_monitor.py
+        self.log_monitor = LogMonitor(self._describe_worker_logs, self.lock,
+                                      float(self.config.get("log_monitor_interval_s", 0.1)))
+        if self.config.get("log_monitor", True):
+            self.log_monitor.start()
         prestart = int(self.config.get("prestart_workers", min(2, int(resources.get("CPU", 1)))))
         with self.lock:
             for _ in range(prestart):
@@ -290,6 +298,7 @@ class Head:
             res["node:__internal_head__"] = 1.0
         self.sched.add_node(node_id, res)
         self.nodes[node_id] = NodeState(node_id, res, labels, is_head)
+        self._cluster_event("INFO", "NODE", f"node {node_id[:8]} added", node_id=node_id)
         return node_id
 
     def add_node(self, resources: dict, labels=None) -> str:
@@ -306,6 +315,7 @@ class Head:
                 return
             node.alive = False
             self.sched.remove_node(node_id)
+            self._cluster_event("ERROR", "NODE", f"node {node_id[:8]} removed", node_id=node_id)
             for w in list(self.workers.values()):
                 if w.node_id == node_id and not w.dead:
                     self._kill_worker(w)
@@ -388,6 +398,8 @@ class Head:
             if cc.worker is not None:
                 self._on_worker_death(cc.worker, "worker process exited")
             elif cc.client_key is not None:
+                if getattr(cc, "log_sink", None) is not None:
+                    self.log_monitor.remove_sink(cc.log_sink)
                 self._return_leases_of(cc.client_key)
                 self._drop_holder_everywhere(cc.client_key)
                 self._schedule()
@@ -455,6 +467,10 @@ class Head:
             self._worker_available(w)
         else:  # client driver
             cc.client_key = "client:" + ident.hex()
+            extra = msg[4] if len(msg) > 4 and isinstance(msg[4], dict) else {}
+            if extra.get("log_to_driver"):
+                cc.log_sink = lambda batches, cc=cc: self._send(cc, (P.LOG_BATCH, batches))
+                self.log_monitor.add_sink(cc.log_sink)
             cc.conn.send((P.REPLY, 0, True, {"store": self.store_name, "node_id": self.head_node_id,
                                               "job_id": self.job_id, "namespace": self.namespace,
                                               "session_dir": self.session_dir}))
@@ -1511,10 +1527,25 @@ class Head:
             ts.blocked = False
             self.sched.acquire(ts.node, cpu, True)
 
+    def _cluster_event(self, severity, source, message, **fields):
+        ev = {"event_id": new_id().hex(), "time": time.time(), "severity": severity, "source_type": source,
+              "message": message}
+        ev.update(fields)
+        self.cluster_events.append(ev)
+
+    def rpc_cluster_events(self, caller):
+        return list(self.cluster_events)
+
     def _on_worker_death(self, w: WorkerState, reason):
         if w.dead:
             return
         w.dead = True
+        if not self.shutting_down:
+            oom = getattr(w, "oom_killed", None)
+            self._cluster_event("ERROR" if oom else "WARNING", "WORKER",
+                                f"worker {w.wid.hex()[:8]} (pid {w.pid}) died: "
+                                f"{'killed by the memory monitor' if oom else reason}",
+                                node_id=w.node_id, pid=w.pid, worker_id=w.wid.hex())
         node = self.nodes.get(w.node_id)
         if w.state == "starting" and node is not None:
             node.starting[w.env_key] = max(0, node.starting[w.env_key] - 1)
@@ -2280,7 +2311,75 @@ class Head:
 
     def rpc_list_workers(self, caller):
         return [{"worker_id": w.wid.hex(), "pid": w.pid, "node_id": w.node_id, "state": w.state,
-                 "is_actor": w.actor is not None, "gpu_ids": list(w.gpus)} for w in self.workers.values()]
+                 "is_actor": w.actor is not None, "gpu_ids": list(w.gpus), "worker_type": "WORKER",
+                 "is_alive": not w.dead, "runtime_env": json.loads(w.env_key[0]) if w.env_key[0] else {},
+                 "log_file": os.path.basename(getattr(w, "log_path", "") or "")}
+                for w in self.workers.values()]
+
+    # ------------------------------------------------------------------ worker logs
+    def _describe_worker_logs(self):
+        out = {}
+        for w in self.workers.values():
+            path = getattr(w, "log_path", None)
+            if path is None:
+                continue
+            if w.actor is not None:
+                label = w.actor.spec.get("class_name")
+            elif w.task is not None:
+                label = w.task.spec.get("name")
+            else:
+                label = None
+            out[w.wid] = (path, w.pid, label, w.node_id, not w.dead)
+        return out
+
+    def rpc_list_logs(self, caller, node_id=None, glob=None):
+        """``{node_id: [file names]}`` of the session's log directory (reference: ``list_logs``)."""
+        import fnmatch
+
+        try:
+            names = sorted(os.listdir(self.logs_dir))
+        except OSError:
+            names = []
+        if glob:
+            names = [n for n in names if fnmatch.fnmatch(n, glob)]
+        by_node = collections.defaultdict(list)
+        owner = {os.path.basename(getattr(w, "log_path", "") or ""): w.node_id for w in self.workers.values()}
+        for n in names:
+            by_node[owner.get(n, self.head_node_id)].append(n)
+        if node_id is not None:
+            return {node_id: by_node.get(node_id, [])}
+        return dict(by_node)
+
+    def rpc_get_log(self, caller, filename=None, actor_id=None, task_id=None, pid=None, worker_id=None, tail=-1):
+        """Lines of one worker log, located by file name, actor, task, worker id or pid."""
+        path = None
+        if filename is not None:
+            path = os.path.join(self.logs_dir, os.path.basename(filename))
+        else:
+            if task_id is not None and worker_id is None:
+                ts = self.tasks.get(bytes.fromhex(task_id)) if isinstance(task_id, str) else self.tasks.get(task_id)
+                if ts is not None and ts.worker is not None:
+                    worker_id = ts.worker.hex()
+                else:
+                    for rec in self.direct_tasks:
+                        if rec[0].hex() == task_id and rec[7] is not None:
+                            worker_id = rec[7].hex()
+                if worker_id is None:
+                    raise ValueError(f"no worker is known for task {task_id}")
+            if actor_id is not None:
+                a = self.actors.get(bytes.fromhex(actor_id) if isinstance(actor_id, str) else actor_id)
+                if a is None:
+                    raise ValueError(f"actor {actor_id} not found")
+                pid = a.pid
+            for w in self.workers.values():
+                if (worker_id is not None and w.wid.hex() == worker_id) or (pid is not None and w.pid == pid):
+                    path = getattr(w, "log_path", None)
+                    break
+            if path is None and worker_id is not None:
+                path = os.path.join(self.logs_dir, f"worker-{worker_id}.out")
+        if path is None or not os.path.exists(path):
+            raise ValueError("log file not found")
+        return read_log(path, tail)
 
     def rpc_store_stats(self, caller):
         s = dict(self.store.stats())
@@ -2418,6 +2517,7 @@ class Head:
                 except Exception:
                     pass
         self._thread.join(timeout=2)
+        self.log_monitor.stop()  # drains what the workers wrote before they exited
         for c, _cc in list(self.conns.values()):
             try:
                 c.close()
@@ -2448,6 +2548,7 @@ class ClientConn:
         self.reader = P.FrameReader()
         self.worker: Optional[WorkerState] = None
         self.client_key: Optional[str] = None
+        self.log_sink = None
 
     def key(self):
         if self.worker is not None:

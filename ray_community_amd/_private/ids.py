@@ -30,6 +30,21 @@ def new_id() -> bytes:
     return _PREFIX + struct.pack("<Q", next(_COUNTER))
 
 
+def return_ids(tid: bytes, n: int) -> list:
+    """Object ids of a task's ``n`` returns: the task id's first 16 bytes + a 1-based index
+    (reference: ``ObjectID::FromIndex``). ``new_id`` values keep bytes 16..20 zero (< 2**32 ids
+    per process), so these never collide with a put id or another task's returns."""
+    head = tid[:16]
+    return [head + struct.pack("<I", i + 1) for i in range(n)]
+
+
+def task_id_of(oid: bytes):
+    """The id of the task that returns ``oid`` (None for ``put`` objects)."""
+    if len(oid) == ID_LEN and oid[16:] != b"\0\0\0\0":
+        return oid[:16] + b"\0\0\0\0"
+    return None
+
+
 class BaseID:
     __slots__ = ("_b",)
     size = ID_LEN

@@ -29,6 +29,7 @@ CANCEL = 23        # (CANCEL, task_id, force)
 FREE_GPU = 24      # (FREE_GPU, [object_ids])
 PING = 25
 GPU_CMD = 26       # (GPU_CMD, "spill" | "restore", [object_ids])  head -> GPU-object owner
+LOG_BATCH = 27     # (LOG_BATCH, [{pid, label, node, lines}])       head -> log_to_driver drivers
 # worker -> head: batched records of directly transported actor calls
 DIRECT_EVENTS = 30  # (DIRECT_EVENTS, [(tid, name, actor_id, start, end, failed, error_type)])
 # caller <-> actor worker (direct transport, _private/direct_transport.py)

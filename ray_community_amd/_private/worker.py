@@ -95,12 +95,13 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
         if address is not None and address.startswith("ray://"):
             from ..util.client import connect as _client_connect
 
-            core, addr = _client_connect(address, ns)
+            core, addr = _client_connect(address, ns, log_to_driver)
             _state.update(head=None, core=core, mode=SCRIPT_MODE, namespace=ns, address=addr, client_mode=True)
         elif address is not None:
             sock = _resolve_address(address)
             ident = os.urandom(20)
-            client = SocketClient(sock, "client", ident)
+            client = SocketClient(sock, "client", ident, on_message=_driver_push_handler(log_to_driver),
+                                  register_extra={"log_to_driver": bool(log_to_driver)})
             hello = client.hello
             from .object_store import ObjectStore
 
@@ -124,6 +125,10 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             head = Head(session, res, object_store_memory=object_store_memory, namespace=ns, system_config=sysconf,
                         labels=labels)
             res["object_store_memory"] = float(head.store_capacity)
+            if log_to_driver:
+                from .log_monitor import print_batches
+
+                head.log_monitor.add_sink(print_batches)
             client = DirectClient(head)
             core = CoreWorker("driver", client, head.store, head.head_node_id, head.job_id, ns,
                               session_dir=session)
@@ -150,6 +155,19 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
             tracing.setup_tracing(kwargs["_tracing_startup_hook"])
         cw.set_global_core(core)
         return RayContext(_state)
+
+
+def _driver_push_handler(log_to_driver):
+    """Head -> driver pushes on a socket driver: forwarded worker log lines."""
+    from . import protocol as P
+
+    def on_message(msg):
+        if msg[0] == P.LOG_BATCH and log_to_driver:
+            from .log_monitor import print_batches
+
+            print_batches(msg[1])
+
+    return on_message
 
 
 def _mem_bytes():

@@ -68,6 +68,7 @@ from . import serialization as ser  # noqa: E402
 from .core_worker import (CoreWorker, DynamicObjectRefGenerator, ObjectRef, SocketClient, _ErrorValue,  # noqa: E402
                           set_global_core)
 from .ids import new_id  # noqa: E402
+from .log_monitor import LOG_LABEL_MARK  # noqa: E402
 from ..util import tracing  # noqa: E402
 from .object_store import ObjectStore  # noqa: E402
 
@@ -78,6 +79,7 @@ class _ActorExit(BaseException):
 
 class Worker:
     def __init__(self):
+        self._log_label = None  # last task / actor label announced to the log monitor
         env = os.environ
         self.wid = bytes.fromhex(env["RCA_WORKER_ID"])
         self.inbox: "queue.Queue" = queue.Queue()
@@ -241,6 +243,15 @@ class Worker:
     def _execute(self, spec):
         tid = spec["tid"]
         kind = spec["kind"]
+        if kind != "actor_task":
+            label = spec.get("class_name") if kind == "actor_creation" else spec.get("name")
+            if label and label != self._log_label:
+                # tells the head's log monitor what this worker's next lines belong to
+                self._log_label = label
+                try:
+                    os.write(1, f"{LOG_LABEL_MARK}{label}\n".encode())
+                except OSError:
+                    pass
         t_start = time.time()
         self._set_ctx(spec)
         self.running[tid] = threading.get_ident()

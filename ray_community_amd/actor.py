@@ -7,7 +7,7 @@ from typing import Any, Dict, Optional
 from . import exceptions as exc
 from ._private import serialization as ser
 from ._private.core_worker import ObjectRef, ObjectRefGenerator
-from ._private.ids import new_id
+from ._private.ids import new_id, return_ids
 from .remote_function import _merge_runtime_env, build_resources, build_strategy
 
 _ACTOR_OPTIONS = {"num_cpus", "num_gpus", "memory", "resources", "accelerator_type", "max_restarts",
@@ -248,7 +248,7 @@ class ActorHandle:
             nret = int(num_returns)
         enc, kw_names, contained, deps = core.encode_args(args, kwargs)
         tid = new_id()
-        rids = [new_id() for _ in range(nret)]
+        rids = return_ids(tid, nret)
         spec = {
             "tid": tid, "kind": "actor_task", "actor_id": self._actor_id, "method": name,
             "name": mo.get("name") or f"{self._meta.get('class_name', 'Actor')}.{name}", "args": enc,

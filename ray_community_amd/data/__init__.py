@@ -5,6 +5,9 @@ from .context import DataContext, DatasetContext
 from .dataset import ActorPoolStrategy, Dataset, MaterializedDataset, Schema, TaskPoolStrategy
 from .grouped_data import GroupedData
 from .iterator import DataIterator
+from .datasource import (Datasink, from_arrow_refs, from_pandas_refs, read_parquet_bulk, read_sql, read_tfrecords,
+                         read_webdataset)
+from .random_access_dataset import RandomAccessDataset
 from .read_api import (Datasource, from_arrow, from_huggingface, from_items, from_numpy, from_numpy_refs, from_pandas,
                        from_torch, range, range_tensor, read_binary_files, read_csv, read_datasource, read_images,
                        read_json, read_numpy, read_parquet, read_text)
@@ -14,4 +17,5 @@ __all__ = ["Dataset", "MaterializedDataset", "DataIterator", "GroupedData", "Act
            "from_numpy", "from_numpy_refs", "from_pandas", "from_arrow", "from_torch", "from_huggingface",
            "read_parquet", "read_csv", "read_json", "read_text", "read_numpy", "read_binary_files", "read_images",
            "read_datasource", "Datasource", "AggregateFn", "Count", "Sum", "Min", "Max", "Mean", "Std", "AbsMax",
-           "Unique"]
+           "Unique", "Datasink", "read_sql", "read_webdataset", "read_tfrecords", "read_parquet_bulk",
+           "from_pandas_refs", "from_arrow_refs", "RandomAccessDataset"]

@@ -451,6 +451,51 @@ class Dataset:
     def write_numpy(self, path: str, *, column: str = "data", **kw):
         self._write(path, "npy", column=column)
 
+    def write_datasink(self, datasink, *, ray_remote_args=None, concurrency=None):
+        from .datasource import write_datasink
+
+        write_datasink(self, datasink, ray_remote_args=ray_remote_args, concurrency=concurrency)
+
+    def write_sql(self, sql: str, connection_factory, **kw):
+        from .datasource import SQLDatasink
+
+        self.write_datasink(SQLDatasink(sql, connection_factory))
+
+    def write_images(self, path: str, column: str, file_format: str = "png", **kw):
+        from .datasource import ImageDatasink
+
+        self.write_datasink(ImageDatasink(path, column, file_format))
+
+    def write_webdataset(self, path: str, **kw):
+        from .datasource import WebDatasetDatasink
+
+        self.write_datasink(WebDatasetDatasink(path))
+
+    def write_tfrecords(self, path: str, **kw):
+        from .datasource import TFRecordDatasink
+
+        self.write_datasink(TFRecordDatasink(path))
+
+    def to_random_access_dataset(self, key: str, num_workers: Optional[int] = None):
+        from .random_access_dataset import RandomAccessDataset
+
+        return RandomAccessDataset(self, key, num_workers or 4)
+
+    def input_files(self) -> List[str]:
+        """Files the dataset's read stage reads (empty for in-memory datasets)."""
+        out = []
+        for st in self._inputs or []:
+            fn = st[1] if isinstance(st, tuple) and len(st) > 1 and st[0] == "read" else None
+            p = getattr(fn, "path", None)
+            if isinstance(p, str) and p not in out:
+                out.append(p)
+        return out
+
+    def copy(self) -> "Dataset":
+        import copy as _copy
+
+        return _copy.copy(self)
+
     def _write(self, path, fmt, column=None):
         from .._private.worker import get
 

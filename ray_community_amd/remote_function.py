@@ -7,7 +7,7 @@ from typing import Any, Dict, Optional
 
 from ._private import serialization as ser
 from ._private.core_worker import ObjectRef, ObjectRefGenerator
-from ._private.ids import new_id
+from ._private.ids import new_id, return_ids
 
 _TASK_OPTIONS = {"num_cpus", "num_gpus", "memory", "resources", "accelerator_type", "num_returns", "max_retries",
                  "retry_exceptions", "scheduling_strategy", "runtime_env", "name", "max_calls", "placement_group",
@@ -157,7 +157,7 @@ class RemoteFunction:
             generator, nret = "streaming", 1
         enc, kw_names, contained, deps = core.encode_args(args, kwargs)
         tid = new_id()
-        rids = [new_id() for _ in range(nret)]
+        rids = return_ids(tid, nret)
         spec = {
             "tid": tid, "kind": "task", "fid": fid, "name": opts.get("name") or self._name, "args": enc,
             "kw_names": kw_names, "return_ids": rids, "resources": build_resources(opts, 1),

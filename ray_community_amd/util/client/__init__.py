@@ -52,7 +52,7 @@ class RemoteCoreWorker(CoreWorker):
         return super()._materialize(oid, desc)
 
 
-def connect(address: str, namespace: str):
+def connect(address: str, namespace: str, log_to_driver: bool = True):
     """Open the TCP link, register as a client driver and build its core worker."""
     import os
 
@@ -60,7 +60,10 @@ def connect(address: str, namespace: str):
     s = socket.create_connection((host, port), timeout=30)
     s.settimeout(None)
     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-    client = SocketClient(None, "client", os.urandom(20), sock=s)
+    from ..._private.worker import _driver_push_handler
+
+    client = SocketClient(None, "client", os.urandom(20), sock=s, on_message=_driver_push_handler(log_to_driver),
+                          register_extra={"log_to_driver": bool(log_to_driver)})
     hello = client.hello
     core = RemoteCoreWorker("client", client, None, hello["node_id"], hello["job_id"], namespace,
                             session_dir=hello.get("session_dir", ""))

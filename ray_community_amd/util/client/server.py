@@ -49,7 +49,11 @@ class _Session:
             if msg[0] != P.REGISTER or msg[1] != "client":
                 return
             ident = msg[2]
-            self.head = SocketClient(self.server.head_address, "client", ident)
+            extra = msg[4] if len(msg) > 4 and isinstance(msg[4], dict) else {}
+            # worker log lines the head pushes are relayed to the remote driver as they are
+            relay = (lambda m: self._push(m)) if extra.get("log_to_driver") else None
+            self.head = SocketClient(self.server.head_address, "client", ident, on_message=relay,
+                                     register_extra={"log_to_driver": bool(extra.get("log_to_driver"))})
             hello = dict(self.head.hello)
             store_name = hello.pop("store", None)
             if store_name:
@@ -96,6 +100,13 @@ class _Session:
                 self._reply(rid, False, e)
 
         fut.add_done_callback(done)
+
+    def _push(self, msg):
+        if msg[0] == P.LOG_BATCH:
+            try:
+                self.remote.send(msg)
+            except OSError:
+                pass
 
     def _reply(self, rid, ok, val):
         try:

@@ -2,7 +2,8 @@
 from __future__ import annotations
 
 from collections import Counter
-from typing import Any, Dict, List, Optional, Tuple
+import os
+from typing import Any, Dict, Iterator, List, Optional, Tuple
 
 
 def _call(method, *args):
@@ -11,18 +12,32 @@ def _call(method, *args):
     return _core().client.call(method, *args)
 
 
+_PREDICATES = ("=", "==", "!=")
+
+
+def _match(v, val) -> bool:
+    if isinstance(v, bool) or isinstance(val, bool):
+        return str(v).lower() == str(val).lower()
+    return str(v) == str(val)
+
+
 def _filter(rows, filters):
+    """AND of ``(key, predicate, value)`` filters; predicates ``=`` / ``!=`` as in the reference
+    (``util/state/common.py`` ``ListApiOptions``), values compared as strings (booleans
+    case-insensitively, so ``("is_detached", "=", "true")`` works from the CLI too)."""
     if not filters:
         return rows
+    for f in filters:
+        if len(f) != 3 or f[1] not in _PREDICATES:
+            raise ValueError(f"Unsupported filter {f!r}: use (key, '=' | '!=', value)")
     out = []
     for r in rows:
         ok = True
         for key, op, val in filters:
-            v = r.get(key)
-            if op in ("=", "==") and str(v) != str(val):
+            eq = _match(r.get(key), val)
+            if (op == "!=") == eq:
                 ok = False
-            elif op == "!=" and str(v) == str(val):
-                ok = False
+                break
         if ok:
             out.append(r)
     return out
@@ -69,6 +84,76 @@ def list_placement_groups(filters=None, limit: int = 10000, detail=False, **kw):
     return _filter(list(_call("pg_table", None).values()), filters)[:limit]
 
 
+def list_jobs(filters=None, limit: int = 10000, detail=False, **kw):
+    """The driver job of this session plus submitted jobs (job submission manager), reference
+    ``list_jobs`` fields: ``job_id``/``submission_id``, ``type``, ``status``, ``entrypoint``."""
+    from .._private.worker import _core
+
+    core = _core()
+    rows = [{"job_id": core.job_id.hex() if isinstance(core.job_id, bytes) else str(core.job_id),
+             "submission_id": None, "type": "DRIVER", "status": "RUNNING", "entrypoint": "",
+             "driver_info": {"pid": os.getpid()}}]
+    try:
+        from ..job_submission import _job_manager
+        from .._private.worker import get
+
+        mgr = _job_manager(create=False)
+        for d in get(mgr.list.remote(), timeout=10):
+            st = d.get("status")
+            rows.append({"job_id": d.get("submission_id"), "submission_id": d.get("submission_id"),
+                         "type": "SUBMISSION", "status": getattr(st, "value", st),
+                         "entrypoint": d.get("entrypoint"), "message": d.get("message"),
+                         "start_time": d.get("start_time"), "end_time": d.get("end_time"),
+                         "metadata": d.get("metadata")})
+    except Exception:  # noqa  (no job has been submitted in this session)
+        pass
+    return _filter(rows, filters)[:limit]
+
+
+def list_runtime_envs(filters=None, limit: int = 10000, detail=False, **kw):
+    """Distinct runtime environments of the live workers (one row per env, with its worker count)."""
+    rows = {}
+    for w in _call("list_workers"):
+        key = str(w.get("runtime_env") or {})
+        r = rows.setdefault(key, {"runtime_env": w.get("runtime_env") or {}, "success": True, "ref_cnt": 0})
+        r["ref_cnt"] += 1
+    return _filter(list(rows.values()), filters)[:limit]
+
+
+def list_cluster_events(filters=None, limit: int = 10000, detail=False, **kw):
+    """Node / worker / OOM-kill events recorded by the head (reference: ``list_cluster_events``)."""
+    return _filter(_call("cluster_events"), filters)[:limit]
+
+
+def list_logs(node_id: Optional[str] = None, glob_filter: Optional[str] = None, **kw) -> Dict[str, List[str]]:
+    """``{node_id: [log file names]}`` (worker stdout/stderr files ``worker-<id>.out``)."""
+    return _call("list_logs", node_id, glob_filter)
+
+
+def get_log(filename: Optional[str] = None, actor_id: Optional[str] = None, task_id: Optional[str] = None,
+            pid: Optional[int] = None, node_id: Optional[str] = None, tail: int = -1, follow: bool = False,
+            interval: float = 0.5, worker_id: Optional[str] = None, **kw) -> Iterator[str]:
+    """Yield the lines of one worker log, found by file name, actor id, task id, worker id or pid
+    (reference: ``util/state/api.py`` ``get_log``). ``follow=True`` keeps yielding new lines."""
+    import time
+
+    if task_id is not None:
+        _flush_own_task_records()  # leased tasks: the worker that ran it is in this process's records
+    lines = _call("get_log", filename, actor_id, task_id, pid, worker_id, tail)
+    yield from lines
+    if not follow:
+        return
+    seen = len(_call("get_log", filename, actor_id, task_id, pid, worker_id, -1))
+    while True:
+        time.sleep(interval)
+        try:
+            cur = _call("get_log", filename, actor_id, task_id, pid, worker_id, -1)
+        except Exception:  # noqa  (the worker is gone)
+            return
+        yield from cur[seen:]
+        seen = len(cur)
+
+
 def get_actor(id: str):
     for a in list_actors():
         if a["actor_id"] == id:
@@ -77,10 +162,32 @@ def get_actor(id: str):
 
 
 def get_task(id: str):
+    """The latest attempt of a task (reference returns the attempt list's last entry)."""
+    hit = None
     for t in list_tasks():
         if t["task_id"] == id:
-            return t
-    return None
+            hit = t
+    return hit
+
+
+def get_node(id: str):
+    return next((n for n in list_nodes() if n["node_id"] == id), None)
+
+
+def get_worker(id: str):
+    return next((w for w in list_workers() if w["worker_id"] == id), None)
+
+
+def get_placement_group(id: str):
+    return next((p for p in list_placement_groups() if p.get("placement_group_id") == id), None)
+
+
+def get_job(id: str):
+    return next((j for j in list_jobs() if id in (j["job_id"], j.get("submission_id"))), None)
+
+
+def get_objects(id: str):
+    return [o for o in list_objects() if o["object_id"] == id]
 
 
 def summarize_tasks(**kw) -> Dict[str, Any]:

@@ -43,3 +43,29 @@ def test_dashboard_metrics_and_state(shutdown_only):
     status = json.loads(_get(url + "/api/cluster_status"))
     assert status["total"]["CPU"] == 2.0
     assert json.loads(_get(url + "/api/version"))["version"]
+
+
+def test_dashboard_overview_page_logs_and_events(shutdown_only):
+    ctx = ray.init(num_cpus=2, include_dashboard=True, dashboard_port=0, log_to_driver=False)
+    url = ctx.dashboard_url
+
+    @ray.remote
+    def noisy():
+        print("dashboard-log-line")
+        return 1
+
+    ray.get(noisy.remote())
+    page = _get(url + "/")
+    assert "<html" in page and "/api/actors" in page and "showLog" in page
+    logs = json.loads(_get(url + "/api/logs"))
+    files = [f for fs in logs.values() for f in fs]
+    assert files
+    deadline = time.time() + 10
+    text = ""
+    while time.time() < deadline and "dashboard-log-line" not in text:
+        text = "".join(_get(url + f"/api/logs/file?filename={f}&lines=50") for f in files)
+        time.sleep(0.1)
+    assert "dashboard-log-line" in text
+    ev = json.loads(_get(url + "/api/cluster_events"))
+    assert any(e["source_type"] == "NODE" for e in ev)
+    assert json.loads(_get(url + "/api/placement_groups")) == []

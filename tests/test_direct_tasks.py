@@ -196,3 +196,33 @@ def test_leased_output_is_reconstructed_when_its_node_dies(ray_start_cluster, tm
     out = ray.get(refs[1], timeout=60)  # recomputed on the new node from its lineage
     assert int(out[-1]) == 6
     assert open(runs).read().count("x") >= 3
+
+
+def test_pipelined_actor_calls_do_not_deadlock_on_full_sockets(shutdown_only):
+    """Tens of thousands of direct actor calls submitted without waiting fill the caller->actor
+    socket. The caller must keep reading replies while a send is blocked: the native frame writer
+    once blocked with the GIL held (and the channel sent under its lock), freezing the reader
+    thread, so caller and actor both stopped reading (core microbenchmark 1:1 actor calls async)."""
+    import threading
+
+    ray.init(num_cpus=2, include_dashboard=False)
+
+    @ray.remote
+    class Echo:
+        def v(self, x=b"ok"):
+            return x
+
+    a = Echo.remote()
+    ray.get(a.v.remote())
+    done = []
+
+    def work():
+        for _ in range(6):
+            refs = [a.v.remote(b"x" * 200) for _ in range(4000)]
+            assert ray.get(refs, timeout=120)[-1] == b"x" * 200
+        done.append(True)
+
+    t = threading.Thread(target=work, daemon=True)
+    t.start()
+    t.join(150)
+    assert done, "pipelined actor calls stalled"
