@@ -42,6 +42,65 @@ def remote(*args, **kwargs):
     return lambda obj: make(obj, kwargs)
 
 
+class Language:
+    """Task/actor languages (reference: ``ray.Language``). Only PYTHON workers exist here."""
+    PYTHON = 0
+    JAVA = 1
+    CPP = 2
+
+
+def _cross_language(kind):
+    def unsupported(*a, **k):
+        raise NotImplementedError(f"{kind}: cross-language (Java/C++) workers are not part of ray_community_amd; "
+                                  "only Python tasks and actors are supported")
+    return unsupported
+
+
+java_function = _cross_language("java_function")
+java_actor_class = _cross_language("java_actor_class")
+cpp_function = _cross_language("cpp_function")
+
+
+def show_in_dashboard(message: str, key: str = "", dtype: str = "text"):
+    """Attach a message to the current actor/task, shown in its state-API record (``list_actors``
+    ``repr``/dashboard): reference ``ray.show_in_dashboard``."""
+    from ._private.worker import _core
+
+    core = _core()
+    aid = getattr(core, "actor_id", None)
+    if aid is None:
+        return
+    try:
+        core.client.call("actor_annotate", aid, key or "message", str(message))
+    except Exception:  # noqa
+        pass
+
+
+def client(address: str = None):
+    """``ray.client("host:port").namespace(..).connect()`` builder for Ray Client sessions."""
+    return ClientBuilder(address)
+
+
+class ClientBuilder:
+    def __init__(self, address=None):
+        self._address = address
+        self._kw = {}
+
+    def namespace(self, ns):
+        self._kw["namespace"] = ns
+        return self
+
+    def env(self, runtime_env):
+        self._kw["runtime_env"] = runtime_env
+        return self
+
+    def connect(self):
+        addr = self._address or ""
+        if addr and not addr.startswith("ray://"):
+            addr = "ray://" + addr
+        return init(address=addr or None, **self._kw)
+
+
 _LAZY = {"util", "train", "tune", "data", "serve", "rllib", "dag", "air", "experimental", "models", "ops", "parallel",
          "cluster_utils", "job_submission", "workflow", "runtime_env", "autoscaler", "utils", "job_config", "scripts"}
 
@@ -60,5 +119,6 @@ __all__ = [
     "get_runtime_context", "ObjectRef", "ObjectRefGenerator", "DynamicObjectRefGenerator", "ActorHandle",
     "ActorClass", "RemoteFunction", "exceptions", "exit_actor", "LOCAL_MODE", "SCRIPT_MODE", "WORKER_MODE",
     "ActorID", "TaskID", "NodeID", "JobID", "ObjectID", "WorkerID", "FunctionID", "PlacementGroupID", "UniqueID",
-    "ActorClassID",
+    "ActorClassID", "Language", "java_function", "java_actor_class", "cpp_function", "show_in_dashboard",
+    "client", "ClientBuilder",
 ]

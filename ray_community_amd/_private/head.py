@@ -2296,8 +2296,18 @@ class Head:
             out.append({"actor_id": a.aid.hex(), "class_name": a.spec.get("class_name"), "state": a.state,
                         "name": a.name or "", "namespace": a.namespace, "pid": a.pid, "node_id": a.node,
                         "num_restarts": a.num_restarts, "death_cause": a.death_cause,
-                        "is_detached": a.detached, "required_resources": a.spec.get("resources")})
+                        "is_detached": a.detached, "required_resources": a.spec.get("resources"),
+                        "annotations": dict(getattr(a, "annotations", None) or {})})
         return out
+
+    def rpc_actor_annotate(self, caller, aid, key, message):
+        """``ray.show_in_dashboard`` from inside an actor: a message kept on its state record."""
+        a = self.actors.get(aid)
+        if a is not None:
+            if getattr(a, "annotations", None) is None:
+                a.annotations = {}
+            a.annotations[key] = message
+        return True
 
     def rpc_list_objects(self, caller):
         out = []

@@ -281,6 +281,65 @@ def cmd_list(args) -> int:
     return 0
 
 
+def cmd_logs(args) -> int:
+    """``logs`` (list files) / ``logs <file>`` / ``logs --actor-id|--task-id|--pid`` [--tail N] [--follow]."""
+    ray = _connect(args)
+    try:
+        from ..util import state
+
+        if not (args.filename or args.actor_id or args.task_id or args.pid):
+            for node, files in state.list_logs(glob_filter=args.glob).items():
+                print(f"node {node}:")
+                for f in files:
+                    print(f"  {f}")
+            return 0
+        for line in state.get_log(filename=args.filename, actor_id=args.actor_id, task_id=args.task_id,
+                                  pid=args.pid, tail=args.tail, follow=args.follow):
+            print(line, flush=True)
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def cmd_debug(args) -> int:
+    """List the session's remote breakpoints (util.pdb.set_trace) and attach to one: this
+    terminal's lines go to the breakpoint's pdb, its output comes back."""
+    import select
+    import socket as _socket
+
+    ray = _connect(args)
+    try:
+        from ..util.pdb import list_breakpoints
+
+        bps = list_breakpoints()
+    finally:
+        ray.shutdown()
+    if not bps:
+        print("No active breakpoints.")
+        return 0
+    for i, b in enumerate(bps):
+        print(f"{i}: pid {b['pid']} at {b['host']}:{b['port']}")
+    idx = args.index if args.index is not None else (0 if len(bps) == 1 else int(input("Enter breakpoint index: ")))
+    b = bps[idx]
+    conn = _socket.create_connection((b["host"], b["port"]))
+    try:
+        while True:
+            r, _, _ = select.select([conn, sys.stdin], [], [])
+            if conn in r:
+                data = conn.recv(65536)
+                if not data:
+                    return 0
+                sys.stdout.write(data.decode("utf-8", "replace"))
+                sys.stdout.flush()
+            if sys.stdin in r:
+                line = sys.stdin.readline()
+                if not line:
+                    return 0
+                conn.sendall(line.encode())
+    finally:
+        conn.close()
+
+
 def cmd_summary(args) -> int:
     ray = _connect(args)
     try:
@@ -426,6 +485,22 @@ def build_parser() -> argparse.ArgumentParser:
     sp.add_argument("--format", choices=["table", "json"], default="table")
     conn_opts(sp)
     sp.set_defaults(fn=cmd_list)
+
+    sp = sub.add_parser("logs", help="list worker log files or print one (by file, actor, task or pid)")
+    sp.add_argument("filename", nargs="?")
+    sp.add_argument("--actor-id")
+    sp.add_argument("--task-id")
+    sp.add_argument("--pid", type=int)
+    sp.add_argument("--glob")
+    sp.add_argument("--tail", type=int, default=-1)
+    sp.add_argument("--follow", action="store_true")
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_logs)
+
+    sp = sub.add_parser("debug", help="attach to a remote breakpoint (ray_community_amd.util.pdb)")
+    sp.add_argument("--index", type=int)
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_debug)
 
     sp = sub.add_parser("summary", help="state API summaries")
     sp.add_argument("resource", choices=["tasks", "actors", "objects"])

@@ -57,6 +57,25 @@ def test_cli_driver_connects_with_address_auto(tmp_path):
         _cli(tmp_path, "stop", "--force")
 
 
+def test_cli_logs_and_debug(tmp_path):
+    assert _cli(tmp_path, "start", "--head", "--num-cpus", "2").returncode == 0
+    try:
+        code = ("import ray_community_amd as ray; ray.init(address='auto', log_to_driver=False);"
+                "f = ray.remote(lambda: print('cli-log-marker') or 1); ray.get(f.remote())")
+        env = dict(os.environ, RCA_TEMP_DIR=str(tmp_path), PYTHONPATH=ROOT)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=90)
+        assert r.returncode == 0, r.stderr
+        r = _cli(tmp_path, "logs")
+        assert r.returncode == 0 and "worker-" in r.stdout, r.stdout + r.stderr
+        files = [ln.strip() for ln in r.stdout.splitlines() if ln.strip().startswith("worker-")]
+        hits = [_cli(tmp_path, "logs", f, "--tail", "5").stdout for f in files]
+        assert any("cli-log-marker" in h for h in hits)
+        r = _cli(tmp_path, "debug")
+        assert r.returncode == 0 and "No active breakpoints" in r.stdout
+    finally:
+        _cli(tmp_path, "stop", "--force")
+
+
 @pytest.mark.parametrize("argv", [["--help"], ["list", "--help"], ["job", "submit", "--help"]])
 def test_cli_help(argv, tmp_path):
     r = _cli(tmp_path, *argv)
