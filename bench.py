@@ -65,8 +65,11 @@ def main():
                    "overlap_optimizer": args.overlap_optimizer}
     if args.fused_ce is not None:
         loop_config["model_overrides"] = {"fused_ce": bool(args.fused_ce)}
+    # workers' own output stays in their log files: stdout carries exactly one JSON line
     if not external and args.device == "cpu":
-        ray.init(num_cpus=max(2, args.gpus), include_dashboard=False)
+        ray.init(num_cpus=max(2, args.gpus), include_dashboard=False, log_to_driver=False)
+    elif not external:
+        ray.init(include_dashboard=False, log_to_driver=False)
     # self-launched: TorchTrainer starts N worker actors (one per GPU, RCCL group over xGMI);
     # under torchrun it binds to the launcher's ranks and runs this rank's share of the job.
     trainer = TorchTrainer(llama_train_loop_per_worker, train_loop_config=loop_config,

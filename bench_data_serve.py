@@ -122,7 +122,7 @@ def main():
 
     cuda = a.device == "cuda"
     G = max(1, a.gpus)
-    ray.init(num_cpus=max(8, 4 * G + 4), num_gpus=G if cuda else 0)
+    ray.init(num_cpus=max(8, 4 * G + 4), num_gpus=G if cuda else 0, log_to_driver=False)
     try:
         dep = serve.deployment(Classifier, name="Classifier", num_replicas=G, max_ongoing_requests=4,
                                ray_actor_options={"num_gpus": 0.5 if cuda else 0, "num_cpus": 1})

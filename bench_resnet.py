@@ -34,6 +34,8 @@ def main():
     from ray_community_amd.train.torch import TorchTrainer
     from ray_community_amd.train.vision import resnet_train_loop_per_worker
 
+    if world <= 1:
+        ray.init(include_dashboard=False, log_to_driver=False)  # stdout: one JSON line
     cfg = {"batch_size": a.batch_size, "image_size": a.image_size, "steps": a.steps, "warmup": a.warmup,
            "device": a.device}
     trainer = TorchTrainer(resnet_train_loop_per_worker, train_loop_config=cfg,

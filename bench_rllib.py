@@ -49,7 +49,7 @@ def main():
     ngpu = torch.cuda.device_count() if torch.cuda.is_available() else 0
     if args.learners is None:
         args.learners = ngpu
-    ray.init(num_cpus=max(ncpu, runners + 2), num_gpus=ngpu)
+    ray.init(num_cpus=max(ncpu, runners + 2), num_gpus=ngpu, log_to_driver=False)
     share = args.runner_gpu_share if ngpu else 0.0
     if share > 0 and args.runners is None and runners > 12 * ngpu:
         # GPU-inference runners each open the device: keep <= 12 per GPU (+ learner, driver) and

@@ -1023,7 +1023,7 @@ class DirectServer:
         self.worker = worker
         path = os.path.join(session_dir or "/tmp", f"d-{wid.hex()[-16:]}.sock")
         if len(path.encode()) > 100:
-            path = os.path.join("/tmp", f"rca-d-{wid.hex()[-16:]}.sock")
+            path = os.path.join("/tmp", f"rca-d-{os.urandom(8).hex()}.sock")
         if os.path.exists(path):
             os.unlink(path)
         self.path = path

@@ -206,7 +206,9 @@ class Head:
         self.job_id = job_id or new_id()
         self.sched = native().Scheduler(float(self.config.get("scheduler_spread_threshold", 0.5)))
         cap = object_store_memory or default_store_capacity()
-        self.store_name = "/rca_" + new_id().hex()[-16:]
+        # random, not derived from new_id(): its last bytes are a per-process counter, so two
+        # sessions on one machine would pick the same segment name and unlink each other's store
+        self.store_name = "/rca_" + os.urandom(8).hex()
         self.store = ObjectStore(self.store_name, cap, create=True)
         self.store_capacity = cap
         self.objects: Dict[bytes, ObjEntry] = {}
@@ -263,7 +265,7 @@ class Head:
         # network
         self.sock_path = os.path.join(session_dir, "head.sock")
         if len(self.sock_path.encode()) > 100:  # sun_path is 108 bytes: fall back to a short name
-            self.sock_path = os.path.join(tempfile.gettempdir(), f"rca-{new_id().hex()[-12:]}.sock")
+            self.sock_path = os.path.join(tempfile.gettempdir(), f"rca-{os.urandom(6).hex()}.sock")
         if os.path.exists(self.sock_path):
             os.unlink(self.sock_path)
         self.listener = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
@@ -2335,8 +2337,8 @@ class Head:
                 continue
             if w.actor is not None:
                 label = w.actor.spec.get("class_name")
-            elif w.task is not None:
-                label = w.task.spec.get("name")
+            elif w.task is not None and w.task.spec.get("kind") != "lease":
+                label = w.task.spec.get("name")  # (a leased worker announces its tasks itself)
             else:
                 label = None
             out[w.wid] = (path, w.pid, label, w.node_id, not w.dead)

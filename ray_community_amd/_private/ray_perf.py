@@ -141,7 +141,7 @@ def run(window: float = 2.0, rounds: int = 4, pattern: str = "", scale: float = 
     """Run the suite. ``scale`` < 1 shrinks batch sizes (CI); the ops/s definition is unchanged."""
     t = _Timer(window, rounds, pattern)
     ncpu = max(2, multiprocessing.cpu_count())
-    ray.init(num_cpus=ncpu)
+    ray.init(num_cpus=ncpu, log_to_driver=False)
     try:
         value = ray.put(0)
         t("single client get calls (Plasma Store)", lambda: ray.get(value))
@@ -234,7 +234,7 @@ def run(window: float = 2.0, rounds: int = 4, pattern: str = "", scale: float = 
     finally:
         ray.shutdown()
 
-    ray.init(num_cpus=ncpu, resources={"custom": 100})
+    ray.init(num_cpus=ncpu, resources={"custom": 100}, log_to_driver=False)
     try:
         from ..util.placement_group import placement_group, remove_placement_group
 

@@ -478,3 +478,81 @@ def read_parquet_bulk(paths, *, columns=None, **kw) -> Dataset:
     from .read_api import read_parquet
 
     return read_parquet(paths, columns=columns, **kw)
+
+
+# ============================================================================ file datasinks / ReadTask
+class ReadTask:
+    """A read unit for ``Datasource.get_read_tasks``: a zero-arg callable producing blocks plus its
+    metadata (reference ``datasource/datasource.py``). Returning a list/iterator of blocks is
+    allowed; they are concatenated into one block."""
+
+    def __init__(self, read_fn: Callable[[], Iterable[Any]], metadata: Any = None):
+        self._read_fn = read_fn
+        self.metadata = metadata
+
+    def __call__(self):
+        from .block import concat_blocks
+
+        out = self._read_fn()
+        if isinstance(out, (dict,)) or hasattr(out, "num_rows") or hasattr(out, "columns"):
+            return out
+        blocks = list(out)
+        return concat_blocks(blocks) if len(blocks) != 1 else blocks[0]
+
+
+class _FileDatasink(Datasink):
+    def __init__(self, path: str, *, file_format: str = "bin", **kw):
+        self.path, self.file_format = path, file_format
+
+    def on_write_start(self):
+        os.makedirs(self.path, exist_ok=True)
+
+
+class RowBasedFileDatasink(_FileDatasink):
+    """One file per ROW: subclasses implement ``write_row_to_file(row, file)``."""
+
+    def write_row_to_file(self, row: Dict[str, Any], file):
+        raise NotImplementedError
+
+    def write(self, blocks, ctx):
+        n = 0
+        for b in blocks:
+            for j, row in enumerate(BlockAccessor(b).iter_rows()):
+                with open(os.path.join(self.path, f"{ctx.task_idx:06d}_{j:06d}.{self.file_format}"), "wb") as f:
+                    self.write_row_to_file(row, f)
+                n += 1
+        return n
+
+
+class BlockBasedFileDatasink(_FileDatasink):
+    """One file per BLOCK: subclasses implement ``write_block_to_file(block_accessor, file)``."""
+
+    def write_block_to_file(self, block: BlockAccessor, file):
+        raise NotImplementedError
+
+    def write(self, blocks, ctx):
+        n = 0
+        for j, b in enumerate(blocks):
+            acc = BlockAccessor(b)
+            if acc.num_rows() == 0:
+                continue
+            with open(os.path.join(self.path, f"{ctx.task_idx:06d}_{j:06d}.{self.file_format}"), "wb") as f:
+                self.write_block_to_file(acc, f)
+            n += acc.num_rows()
+        return n
+
+
+def _absent(lib):
+    def f(*a, **k):
+        raise ImportError(f"{lib} is not installed in this environment; convert to pandas/arrow/numpy first")
+    return f
+
+
+from_dask = _absent("dask")
+from_mars = _absent("mars")
+from_modin = _absent("modin")
+from_spark = _absent("pyspark")
+from_tf = _absent("tensorflow")
+read_mongo = _absent("pymongo")
+read_bigquery = _absent("google-cloud-bigquery")
+read_databricks_tables = _absent("databricks-sql-connector")

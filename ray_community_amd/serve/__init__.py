@@ -17,7 +17,23 @@ class AutoscalingConfig:
         self.downscale_delay_s = downscale_delay_s
 
 
+class HTTPOptions:
+    """HTTP proxy options for ``serve.start(http_options=HTTPOptions(...))`` (reference
+    ``serve/config.py``): ``host``/``port`` are used by the proxy; the rest are accepted."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 8000, root_path: str = "", location: str = "HeadOnly",
+                 request_timeout_s=None, keep_alive_timeout_s: int = 5, **kw):
+        self.host, self.port, self.root_path, self.location = host, port, root_path, location
+        self.request_timeout_s = request_timeout_s
+        self.keep_alive_timeout_s = keep_alive_timeout_s
+
+
+def _run(target, *, name: str = "default", route_prefix="/", _blocking: bool = True, **kw):
+    """Internal alias of ``serve.run`` (the reference exports it for its own tooling)."""
+    return run(target, name=name, route_prefix=route_prefix, blocking=False, **kw)
+
+
 __all__ = ["deployment", "run", "delete", "shutdown", "start", "status", "ingress", "batch", "multiplexed",
            "get_multiplexed_model_id", "get_replica_context", "get_app_handle", "get_deployment_handle",
            "Deployment", "Application", "DeploymentHandle", "DeploymentResponse", "DeploymentResponseGenerator",
-           "AutoscalingConfig"]
+           "AutoscalingConfig", "HTTPOptions", "_run"]

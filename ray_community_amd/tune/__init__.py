@@ -14,6 +14,9 @@ from .search import BasicVariantGenerator, ConcurrencyLimiter, Searcher
 from .search.sample import (choice, grid_search, lograndint, loguniform, qlograndint, qloguniform, qrandint, qrandn,
                             quniform, randint, randn, sample_from, uniform)
 from .tuner import ResultGrid, Stopper, Trainable, TuneConfig, Tuner
+from .registry import (CLIReporter, Experiment, JupyterNotebookReporter, PlacementGroupFactory, ProgressReporter,
+                       ResumeConfig, create_scheduler, create_searcher, register_env, register_trainable,
+                       run_experiments)
 
 
 def report(metrics: Optional[Dict] = None, *, checkpoint=None, **kwargs):
@@ -38,6 +41,8 @@ def get_context():
 
 
 def with_resources(trainable, resources):
+    if isinstance(resources, PlacementGroupFactory):
+        resources = resources.required_resources
     if callable(resources) and not isinstance(resources, dict):
         raise NotImplementedError("resource functions are not supported; pass a dict")
     res = {}
@@ -83,9 +88,13 @@ def with_parameters(trainable, **kwargs):
 def run(run_or_experiment, *, name=None, metric=None, mode=None, stop=None, config=None, resources_per_trial=None,
         num_samples=1, storage_path=None, search_alg=None, scheduler=None, checkpoint_config=None,
         max_failures=0, max_concurrent_trials=None, time_budget_s=None, callbacks=None, verbose=None,
-        fail_fast=False, raise_on_failed_trial=True, **kwargs) -> "ExperimentAnalysis":
+        fail_fast=False, raise_on_failed_trial=True, progress_reporter=None, **kwargs) -> "ExperimentAnalysis":
     """Legacy functional API: returns an ExperimentAnalysis."""
-    t = run_or_experiment
+    from .registry import resolve_trainable
+
+    t = resolve_trainable(run_or_experiment)
+    if progress_reporter is not None:
+        callbacks = list(callbacks or []) + [progress_reporter]
     if resources_per_trial:
         t = with_resources(t, resources_per_trial)
     tuner = Tuner(t, param_space=config or {},
@@ -152,4 +161,6 @@ __all__ = ["Tuner", "TuneConfig", "ResultGrid", "Trainable", "Stopper", "report"
            "ASHAScheduler", "AsyncHyperBandScheduler", "HyperBandScheduler", "MedianStoppingRule",
            "PopulationBasedTraining", "FIFOScheduler", "TrialScheduler", "BasicVariantGenerator",
            "ConcurrencyLimiter", "Searcher", "Checkpoint", "RunConfig", "CheckpointConfig", "FailureConfig",
-           "Result", "Callback", "ExperimentAnalysis", "TuneError"]
+           "Result", "Callback", "ExperimentAnalysis", "TuneError", "register_env", "register_trainable",
+           "run_experiments", "Experiment", "CLIReporter", "JupyterNotebookReporter", "ProgressReporter",
+           "create_searcher", "create_scheduler", "PlacementGroupFactory", "ResumeConfig"]

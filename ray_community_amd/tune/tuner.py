@@ -636,7 +636,9 @@ def _jsonable(d):
 class Tuner:
     def __init__(self, trainable=None, *, param_space: Optional[Dict] = None, tune_config: Optional[TuneConfig] = None,
                  run_config: Optional[RunConfig] = None, _restored_trials=None, _exp_dir=None):
-        self.trainable = trainable
+        from .registry import resolve_trainable
+
+        self.trainable = resolve_trainable(trainable)  # a name from tune.register_trainable works too
         self.param_space = param_space or {}
         self.tune_config = tune_config or TuneConfig()
         from ..train.data_parallel_trainer import BaseTrainer
@@ -650,9 +652,16 @@ class Tuner:
     def fit(self) -> ResultGrid:
         name = self.run_config.name or f"{_tname(self.trainable)}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
         exp_dir = self._exp_dir or os.path.join(os.path.expanduser(self.run_config.storage_path), name)
-        ctrl = TuneController(self.trainable, self.param_space, self.tune_config, self.run_config, exp_dir,
-                              self._restored)
-        return ctrl.run()
+        rc = self.run_config
+        rep = getattr(rc, "progress_reporter", None)
+        if rep is not None and rep not in (rc.callbacks or []):
+            rc.callbacks = list(rc.callbacks or []) + [rep]
+        ctrl = TuneController(self.trainable, self.param_space, self.tune_config, rc, exp_dir, self._restored)
+        grid = ctrl.run()
+        for cb in (rc.callbacks or []):
+            if hasattr(cb, "on_experiment_end"):
+                cb.on_experiment_end(trials=ctrl.trials)
+        return grid
 
     def get_results(self) -> ResultGrid:
         return self.fit()

@@ -312,3 +312,23 @@ def test_get_if_exists_and_object_locations(shutdown_only):
     locs = get_object_locations([small, big])
     assert locs[small]["node_ids"] == [] and locs[big]["object_size"] >= 8 << 20
     assert locs[big]["node_ids"] == [ray.get_runtime_context().get_node_id()]
+
+
+def test_concurrent_sessions_get_distinct_store_segments(tmp_path):
+    """Two sessions in two processes on one machine: each has its own shm segment, so one
+    shutting down never unlinks the other's store (names once came from the per-process id counter)."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import ray_community_amd as ray\n"
+            "from ray_community_amd._private import worker\n"
+            "ray.init(num_cpus=1, include_dashboard=False)\n"
+            "print('STORE', worker._state['head'].store_name)\n"
+            "ray.shutdown()\n") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = []
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        names += [ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("STORE")]
+    assert len(names) == 2 and names[0] != names[1]
