@@ -4,7 +4,12 @@ from .algorithms import (APPO, BC, CQL, DQN, IMPALA, MARWIL, PPO, BCConfig, MARW
                          PPOConfig, SAC, SACConfig, CQLConfig, get_algorithm_class)
 from .env import MultiAgentEnv, make_multi_agent, register_env
 from .policy import PolicySpec
+from .policy.policy import Policy, TFPolicy, TorchPolicy
+from .env.envs import VectorEnv
+from .env.external_env import BaseEnv, ExternalEnv
+from .env.env_runner import EnvRunner as RolloutWorker  # old-stack name of the sampling actor
 from .policy.sample_batch import MultiAgentBatch, SampleBatch
 
 __all__ = ["PPO", "PPOConfig", "IMPALA", "IMPALAConfig", "APPO", "APPOConfig", "SAC", "SACConfig", "CQL", "CQLConfig", "MARWIL", "MARWILConfig", "BC", "BCConfig", "DQN", "DQNConfig", "Algorithm", "AlgorithmConfig", "SampleBatch", "MultiAgentBatch",
-           "register_env", "get_algorithm_class", "MultiAgentEnv", "make_multi_agent", "PolicySpec"]
+           "register_env", "get_algorithm_class", "MultiAgentEnv", "make_multi_agent", "PolicySpec",
+           "Policy", "TorchPolicy", "TFPolicy", "RolloutWorker", "BaseEnv", "VectorEnv", "ExternalEnv"]

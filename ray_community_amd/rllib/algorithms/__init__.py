@@ -10,4 +10,6 @@ from .ppo import PPO, PPOConfig
 from .sac import SAC, SACConfig
 from .registry import ALGORITHMS, get_algorithm_class
 
-__all__ = ["Algorithm", "AlgorithmConfig", "DefaultCallbacks", "RLlibCallback", "make_multi_callbacks", "PPO", "PPOConfig", "DQN", "DQNConfig", "DreamerV3", "DreamerV3Config", "IMPALA", "IMPALAConfig", "APPO", "APPOConfig", "SAC", "SACConfig", "CQL", "CQLConfig", "MARWIL", "MARWILConfig", "BC", "BCConfig", "get_algorithm_class", "ALGORITHMS"]
+Impala, ImpalaConfig = IMPALA, IMPALAConfig  # the reference exports both spellings
+
+__all__ = ["Impala", "ImpalaConfig", "Algorithm", "AlgorithmConfig", "DefaultCallbacks", "RLlibCallback", "make_multi_callbacks", "PPO", "PPOConfig", "DQN", "DQNConfig", "DreamerV3", "DreamerV3Config", "IMPALA", "IMPALAConfig", "APPO", "APPOConfig", "SAC", "SACConfig", "CQL", "CQLConfig", "MARWIL", "MARWILConfig", "BC", "BCConfig", "get_algorithm_class", "ALGORITHMS"]

@@ -180,3 +180,12 @@ def prepare_working_dir(path: str, session_dir: str) -> str:
 
 
 __all__ = ["RuntimeEnv", "RuntimeEnvConfig", "RuntimeEnvSetupError"]
+
+
+def mpi_init():
+    """The reference's MPI runtime-env hook (``runtime_env/mpi.py``); MPI workers are not part of
+    this runtime, so this only checks that an MPI launch is not expected."""
+    import os as _os
+
+    if _os.environ.get("OMPI_COMM_WORLD_SIZE") or _os.environ.get("PMI_SIZE"):
+        raise NotImplementedError("MPI-launched workers are not supported; use torch.distributed / RCCL")

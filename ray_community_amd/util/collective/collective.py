@@ -214,8 +214,93 @@ def allreduce(tensor, group_name: str = "default", op=ReduceOp.SUM):
     _group(group_name).allreduce([tensor], op)
 
 
+# ---- multi-GPU-per-process variants (reference collective.py *_multigpu). A process here drives one
+# GPU, but the list forms are kept: the local tensors are combined first, one collective runs on
+# the combined tensor, and the result is copied back to every local tensor.
+def nccl_available() -> bool:
+    torch, dist = _torch()
+    return bool(dist.is_nccl_available() and torch.cuda.is_available())
+
+
+def gloo_available() -> bool:
+    _, dist = _torch()
+    return bool(dist.is_gloo_available())
+
+
+def _local_sum(tensor_list, op=ReduceOp.SUM):
+    acc = tensor_list[0].clone()
+    for t in tensor_list[1:]:
+        t = t.to(acc.device)
+        if op in (ReduceOp.SUM, ReduceOp.AVG):
+            acc += t
+        elif op == ReduceOp.PRODUCT:
+            acc *= t
+        elif op == ReduceOp.MIN:
+            acc = acc.minimum(t)
+        elif op == ReduceOp.MAX:
+            acc = acc.maximum(t)
+    return acc
+
+
 def allreduce_multigpu(tensor_list, group_name: str = "default", op=ReduceOp.SUM):
-    _group(group_name).allreduce(list(tensor_list), op)
+    tensor_list = list(tensor_list)
+    acc = _local_sum(tensor_list, ReduceOp.SUM if op == ReduceOp.AVG else op)
+    _group(group_name).allreduce([acc], op)
+    if op == ReduceOp.AVG and len(tensor_list) > 1:
+        acc /= len(tensor_list)
+    for t in tensor_list:
+        t.copy_(acc)
+
+
+def reduce_multigpu(tensor_list, dst_rank: int = 0, dst_tensor: int = 0, group_name: str = "default",
+                    op=ReduceOp.SUM):
+    tensor_list = list(tensor_list)
+    g = _group(group_name)
+    acc = _local_sum(tensor_list, op)
+    g.reduce([acc], dst_rank, op)
+    if g.rank == dst_rank:
+        tensor_list[dst_tensor].copy_(acc)
+
+
+def broadcast_multigpu(tensor_list, src_rank: int = 0, src_tensor: int = 0, group_name: str = "default"):
+    tensor_list = list(tensor_list)
+    g = _group(group_name)
+    t = tensor_list[src_tensor] if g.rank == src_rank else tensor_list[0]
+    g.broadcast([t], src_rank)
+    for x in tensor_list:
+        if x is not t:
+            x.copy_(t)
+
+
+def allgather_multigpu(output_tensor_lists, input_tensor_list, group_name: str = "default"):
+    """``output_tensor_lists[i][r * L + j]`` = local input ``j`` of rank ``r`` (L local tensors)."""
+    g = _group(group_name)
+    L = len(input_tensor_list)
+    for j, inp in enumerate(input_tensor_list):
+        parts = [inp.new_empty(inp.shape) for _ in range(g.world_size)]
+        g.allgather([parts], [inp])
+        for outs in output_tensor_lists:
+            for r in range(g.world_size):
+                outs[r * L + j].copy_(parts[r])
+
+
+def reducescatter_multigpu(output_tensor_list, input_tensor_lists, group_name: str = "default",
+                           op=ReduceOp.SUM):
+    """``input_tensor_lists[i]`` holds ``world_size * L`` tensors; rank ``r`` receives the reductions
+    of entries ``r * L .. r * L + L - 1`` into its ``output_tensor_list``."""
+    g = _group(group_name)
+    L = len(output_tensor_list)
+    sums = [_local_sum([lst[k] for lst in input_tensor_lists], op) for k in range(g.world_size * L)]
+    for j, out in enumerate(output_tensor_list):
+        g.reducescatter([out], [[sums[r * L + j] for r in range(g.world_size)]], op)
+
+
+def send_multigpu(tensor, dst_rank: int, dst_gpu_index: int = 0, group_name: str = "default", n_elements: int = 0):
+    send(tensor if not n_elements else tensor.view(-1)[:n_elements], dst_rank, group_name)
+
+
+def recv_multigpu(tensor, src_rank: int, src_gpu_index: int = 0, group_name: str = "default", n_elements: int = 0):
+    recv(tensor if not n_elements else tensor.view(-1)[:n_elements], src_rank, group_name)
 
 
 def barrier(group_name: str = "default"):

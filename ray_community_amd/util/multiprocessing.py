@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import itertools
 import threading
+from multiprocessing import JoinableQueue, TimeoutError  # noqa: A004  (same names as the stdlib module)
 from typing import Any, Callable, Iterable, List, Optional
 
 
@@ -54,6 +55,10 @@ class AsyncResult:
                 self._done = True
                 self._fire(self._callback, self._result)
             except Exception as e:
+                from ..exceptions import GetTimeoutError
+
+                if isinstance(e, GetTimeoutError):
+                    raise TimeoutError(str(e)) from e  # multiprocessing's contract
                 self._fire(self._error_callback, e)
                 raise
         return self._result

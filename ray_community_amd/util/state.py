@@ -218,3 +218,29 @@ def summarize_objects(**kw):
 
 def object_store_stats():
     return _call("store_stats")
+
+
+class StateApiClient:
+    """Object form of the state API (reference ``util/state/api.py::StateApiClient``): ``list(resource)``,
+    ``get(resource, id)``, ``summary(resource)`` over the module functions."""
+
+    _LIST = {"actors": "list_actors", "tasks": "list_tasks", "objects": "list_objects", "nodes": "list_nodes",
+             "workers": "list_workers", "placement_groups": "list_placement_groups", "jobs": "list_jobs",
+             "runtime_envs": "list_runtime_envs", "cluster_events": "list_cluster_events"}
+    _GET = {"actors": "get_actor", "tasks": "get_task", "nodes": "get_node", "workers": "get_worker",
+            "placement_groups": "get_placement_group", "jobs": "get_job", "objects": "get_objects"}
+
+    def __init__(self, address: Optional[str] = None, cookies=None, headers=None):
+        self.address = address
+
+    def list(self, resource, options=None, raise_on_missing_output: bool = True, _explain: bool = False):
+        r = getattr(resource, "value", resource)
+        filters = getattr(options, "filters", None) if options is not None else None
+        limit = getattr(options, "limit", 10000) if options is not None else 10000
+        return globals()[self._LIST[r]](filters=filters, limit=limit)
+
+    def get(self, resource, id: str, options=None, _explain: bool = False):
+        return globals()[self._GET[getattr(resource, "value", resource)]](id)
+
+    def summary(self, resource, *, options=None, raise_on_missing_output: bool = True, _explain: bool = False):
+        return globals()[f"summarize_{getattr(resource, 'value', resource)}"]()

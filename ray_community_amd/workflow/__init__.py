@@ -479,7 +479,68 @@ class options:
         return f
 
 
+# ------------------------------------------------------------------------------ timers and events
+def _sleep_until(end_time: float):
+    time.sleep(max(0.0, end_time - time.time()))
+    return end_time
+
+
+def sleep(duration: float) -> DAGNode:
+    """A workflow task that finishes ``duration`` seconds after this DAG was BUILT (reference
+    ``workflow/api.py::sleep``): the wake-up time is stored with the DAG, so a resumed workflow
+    only waits for what is left."""
+    from ..remote_function import RemoteFunction
+
+    return RemoteFunction(_sleep_until, {"num_cpus": 0}).bind(time.time() + float(duration))
+
+
+class EventListener:
+    """Subclass and implement ``poll_for_event`` (async, returns the event); ``event_checkpointed``
+    is called once the event is part of the workflow's durable state (reference
+    ``workflow/event_listener.py``)."""
+
+    def __init__(self):
+        pass
+
+    async def poll_for_event(self, *args, **kwargs):
+        raise NotImplementedError
+
+    async def event_checkpointed(self, event) -> None:
+        pass
+
+
+class TimerListener(EventListener):
+    async def poll_for_event(self, timestamp):
+        import asyncio
+
+        await asyncio.sleep(max(0.0, timestamp - time.time()))
+        return timestamp
+
+
+def _wait_event(listener_type, args, kwargs):
+    import asyncio
+
+    listener = listener_type()
+
+    async def go():
+        ev = await listener.poll_for_event(*args, **kwargs)
+        await listener.event_checkpointed(ev)
+        return ev
+
+    return asyncio.run(go())
+
+
+def wait_for_event(event_listener_type, *args, **kwargs) -> DAGNode:
+    """A workflow task whose output is the first event ``event_listener_type().poll_for_event(*args)``
+    returns; once checkpointed, a resumed workflow does not wait for it again."""
+    from ..remote_function import RemoteFunction
+
+    if not (isinstance(event_listener_type, type) and issubclass(event_listener_type, EventListener)):
+        raise TypeError("wait_for_event needs an EventListener subclass")
+    return RemoteFunction(_wait_event, {"num_cpus": 0}).bind(event_listener_type, args, kwargs)
+
+
 __all__ = ["init", "run", "run_async", "resume", "resume_async", "resume_all", "cancel", "list_all", "delete",
            "get_output", "get_output_async", "get_status", "get_metadata", "continuation", "options",
            "WorkflowStatus", "WorkflowError", "WorkflowExecutionError", "WorkflowCancellationError",
-           "WorkflowNotFoundError"]
+           "WorkflowNotFoundError", "sleep", "wait_for_event", "EventListener", "TimerListener"]

@@ -167,6 +167,44 @@ def test_collective_gloo_actors(ray_start_regular):
     assert (r0[5], r1[5]) == (0, 1)
 
 
+def test_collective_multigpu_list_forms_gloo(ray_start_regular):
+    """*_multigpu with two local tensors per rank (one-GPU-per-process design: local combine, one
+    collective, copy back) match the reference's per-GPU semantics."""
+    @ray.remote
+    class W:
+        def __init__(self, rank):
+            self.rank = rank
+
+        def run(self, world):
+            import torch
+
+            col.init_collective_group(world, self.rank, backend="gloo", group_name="mg")
+            r = self.rank
+            ts = [torch.full((2,), float(r + 1)), torch.full((2,), float(10 * (r + 1)))]
+            col.allreduce_multigpu(ts, group_name="mg")
+            red = [torch.full((1,), float(r + 1)), torch.full((1,), 1.0)]
+            col.reduce_multigpu(red, dst_rank=1, dst_tensor=1, group_name="mg")
+            bc = [torch.full((1,), float(r)), torch.full((1,), float(100 + r))]
+            col.broadcast_multigpu(bc, src_rank=0, src_tensor=1, group_name="mg")
+            outs = [[torch.zeros(1) for _ in range(world * 2)] for _ in range(2)]
+            col.allgather_multigpu(outs, [torch.full((1,), float(10 * r)), torch.full((1,), float(10 * r + 1))],
+                                   group_name="mg")
+            ins = [[torch.full((1,), float(k)) for k in range(world * 2)] for _ in range(2)]
+            rs = [torch.zeros(1), torch.zeros(1)]
+            col.reducescatter_multigpu(rs, ins, group_name="mg")
+            return ([t.tolist() for t in ts], red[1].item(), [b.item() for b in bc],
+                    [o.item() for o in outs[1]], [x.item() for x in rs], col.gloo_available())
+
+    ws = [W.remote(i) for i in range(2)]
+    r0, r1 = ray.get([w.run.remote(2) for w in ws])
+    assert r0[0] == [[33.0, 33.0], [33.0, 33.0]] and r1[0] == r0[0]  # (1+10) + (2+20)
+    assert r1[1] == 1 + 1 + 2 + 1  # sum over both ranks' local lists, landed in tensor 1 of rank 1
+    assert r0[2] == [100.0, 100.0] and r1[2] == [100.0, 100.0]
+    assert r1[3] == [0.0, 1.0, 10.0, 11.0]
+    assert r0[4] == [0.0, 4.0] and r1[4] == [8.0, 12.0]  # 2 local lists x 2 ranks x k
+    assert r0[5] is True
+
+
 def test_collective_declarative(ray_start_regular):
     @ray.remote
     class W:
