@@ -36,5 +36,10 @@ class TorchTrainer(DataParallelTrainer):
             os.environ["RCA_TRAIN_DEVICE_INDEX"] = str(lr)
             kw["device_id"] = torch.device("cuda", lr)
         backend = self.backend_config.backend or ("nccl" if use_gpu else "gloo")
+        from .config import rccl_pg_options
+
+        opts = rccl_pg_options(backend)
+        if opts is not None:
+            kw["pg_options"] = opts
         if world > 1:
             dist.init_process_group(backend, timeout=timedelta(seconds=self.backend_config.timeout_s), **kw)
