@@ -460,8 +460,12 @@ class Worker:
                         async for x in value:
                             items.append(x)
                         value = iter(items)
-                loop = asyncio.get_running_loop()
-                results = await loop.run_in_executor(None, self._pack_returns, spec, value)
+                if _small_value(value):
+                    # small results serialise in microseconds: no thread-pool round trip
+                    results = self._pack_returns(spec, value)
+                else:
+                    loop = asyncio.get_running_loop()
+                    results = await loop.run_in_executor(None, self._pack_returns, spec, value)
             except _ActorExit:
                 info["actor_exit"] = True
                 results = []
@@ -487,6 +491,26 @@ class Worker:
             if spans:
                 info["spans"] = spans
             self._finish(spec, results, info, t_start)
+
+
+_SCALARS = (type(None), bool, int, float, complex)
+
+
+def _small_value(v, depth: int = 0) -> bool:
+    """True for results cheap enough to pickle on the event loop (no large buffers, no object refs
+    to register): scalars, short str/bytes, small arrays and shallow small containers."""
+    if isinstance(v, _SCALARS):
+        return True
+    if isinstance(v, (str, bytes, bytearray)):
+        return len(v) <= 65536
+    nb = getattr(v, "nbytes", None)
+    if nb is not None and type(v).__module__ == "numpy":
+        return nb <= 65536 and v.dtype != object
+    if depth < 2 and isinstance(v, (tuple, list)) and len(v) <= 64:
+        return all(_small_value(x, depth + 1) for x in v)
+    if depth < 2 and isinstance(v, dict) and len(v) <= 64:
+        return all(isinstance(k, (str, int)) and _small_value(x, depth + 1) for k, x in v.items())
+    return False
 
 
 class _DepError(Exception):
