@@ -31,6 +31,7 @@ sync 2.3k -> 2.75k/s (a 1 ms lease linger keeps one-at-a-time callers on their l
 """
 from __future__ import annotations
 
+import asyncio
 import collections
 import concurrent.futures
 import os
@@ -1041,6 +1042,12 @@ class DirectServer:
                 s, _ = self.sock.accept()
             except OSError:
                 return
+            loop = getattr(self.worker, "aloop", None)
+            if loop is not None:
+                # async actor: the connection is read on the actor's event loop itself, so a call
+                # becomes a task there without a reader-thread -> loop hand-off
+                asyncio.run_coroutine_threadsafe(self._conn_async(s), loop)
+                continue
             conn = P.Connection(s)
             threading.Thread(target=self._conn_loop, args=(conn,), name="rca-direct-conn", daemon=True).start()
 
@@ -1057,6 +1064,28 @@ class DirectServer:
                 self.worker._dispatch_spec(spec)
             elif t == P.DCANCEL:
                 self.worker._cancel(msg[1], msg[2])
+
+    async def _conn_async(self, s):
+        reader, _writer = await asyncio.open_unix_connection(sock=s)
+        conn = P.Connection(s)  # replies: one sendmsg each (GIL released only if the socket is full)
+        w = self.worker
+        hdr_len = P._LEN.size
+        while True:
+            try:
+                (n,) = P._LEN.unpack(await reader.readexactly(hdr_len))
+                msg = P.loads(await reader.readexactly(n))
+            except (asyncio.IncompleteReadError, ConnectionError, OSError):
+                return
+            t = msg[0]
+            if t == P.DEXEC:
+                spec = msg[1]
+                spec["_reply"] = conn
+                if spec["kind"] == "actor_task":
+                    asyncio.ensure_future(w._run_async(spec))
+                else:
+                    w._dispatch_spec(spec)
+            elif t == P.DCANCEL:
+                w._cancel(msg[1], msg[2])
 
     def record(self, spec, start, end, info):
         with self.rec_lock:

@@ -226,3 +226,37 @@ def test_pipelined_actor_calls_do_not_deadlock_on_full_sockets(shutdown_only):
     t.start()
     t.join(150)
     assert done, "pipelined actor calls stalled"
+
+
+def test_async_actor_calls_start_in_submission_order(shutdown_only):
+    """Async actors read their direct connections on the actor's event loop: calls from one caller
+    still start in submission order, and cancellation of a queued call works."""
+    import asyncio
+
+    ray.init(num_cpus=2, include_dashboard=False)
+
+    @ray.remote
+    class Rec:
+        def __init__(self):
+            self.seen = []
+
+        async def add(self, i):
+            self.seen.append(i)
+            await asyncio.sleep(0)
+            return i
+
+        async def slow(self):
+            await asyncio.sleep(30)
+
+        async def get(self):
+            return self.seen
+
+    r = Rec.remote()
+    refs = [r.add.remote(i) for i in range(2000)]
+    assert ray.get(refs)[-1] == 1999
+    assert ray.get(r.get.remote()) == list(range(2000))
+    s = r.slow.remote()
+    time.sleep(0.3)
+    ray.cancel(s)
+    with pytest.raises((exc.TaskCancelledError, exc.RayTaskError)):
+        ray.get(s, timeout=20)
