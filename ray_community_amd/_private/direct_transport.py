@@ -1033,6 +1033,7 @@ class DirectServer:
         self.sock.listen(256)
         self.records: List[tuple] = []
         self.rec_lock = threading.Lock()
+        self._tasks: set = set()  # live tasks on the actor loop (strong refs)
         threading.Thread(target=self._accept_loop, name="rca-direct-accept", daemon=True).start()
         threading.Thread(target=self._flush_loop, name="rca-direct-events", daemon=True).start()
 
@@ -1046,7 +1047,7 @@ class DirectServer:
             if loop is not None:
                 # async actor: the connection is read on the actor's event loop itself, so a call
                 # becomes a task there without a reader-thread -> loop hand-off
-                asyncio.run_coroutine_threadsafe(self._conn_async(s), loop)
+                loop.call_soon_threadsafe(self._spawn, self._conn_async(s))
                 continue
             conn = P.Connection(s)
             threading.Thread(target=self._conn_loop, args=(conn,), name="rca-direct-conn", daemon=True).start()
@@ -1065,6 +1066,15 @@ class DirectServer:
             elif t == P.DCANCEL:
                 self.worker._cancel(msg[1], msg[2])
 
+    def _spawn(self, coro):
+        """Start a task on the actor loop and keep it referenced until it finishes: the loop only
+        holds tasks weakly, and a reader task parked on a paused transport (or a call parked on
+        the concurrency semaphore) is otherwise reachable from nothing but a reference cycle."""
+        t = asyncio.ensure_future(coro)
+        self._tasks.add(t)
+        t.add_done_callback(self._tasks.discard)
+        return t
+
     async def _conn_async(self, s):
         reader, _writer = await asyncio.open_unix_connection(sock=s)
         conn = P.Connection(s)  # replies: one sendmsg each (GIL released only if the socket is full)
@@ -1081,7 +1091,7 @@ class DirectServer:
                 spec = msg[1]
                 spec["_reply"] = conn
                 if spec["kind"] == "actor_task":
-                    asyncio.ensure_future(w._run_async(spec))
+                    self._spawn(w._run_async(spec))
                 else:
                     w._dispatch_spec(spec)
             elif t == P.DCANCEL:

@@ -128,7 +128,7 @@ class Worker:
     def _dispatch_spec(self, spec):
         """Route a task (from the head, or a direct actor call) to its executor."""
         if self.aloop is not None and spec["kind"] == "actor_task":
-            asyncio.run_coroutine_threadsafe(self._run_async(spec), self.aloop)
+            self.aloop.call_soon_threadsafe(self.direct._spawn, self._run_async(spec))
         elif self.pool is not None and spec["kind"] == "actor_task":
             self.pool.submit(self._execute, spec)
         else:
