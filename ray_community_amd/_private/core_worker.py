@@ -12,6 +12,7 @@ import asyncio
 import concurrent.futures
 import hashlib
 import itertools
+import operator
 import os
 import socket
 import threading
@@ -41,6 +42,8 @@ def set_global_core(c):
     global _core
     _core = c
 
+
+_REF_ID = operator.attrgetter("_id")
 
 # ====================================================================== ObjectRef
 class ObjectRef:
@@ -611,7 +614,7 @@ class CoreWorker:
         if isinstance(refs, ObjectRef):
             raise TypeError("wait() expected a list of ObjectRefs")
         refs = list(refs)
-        ids = [r._id for r in refs]
+        ids = list(map(_REF_ID, refs))  # C-level pass (wait() is called once per completion when polling)
         sids = set(ids)
         if len(sids) != len(ids):
             raise ValueError("Wait requires a list of unique object refs.")
