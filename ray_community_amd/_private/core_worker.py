@@ -356,6 +356,9 @@ class TaskContext(threading.local):
         self.actor_id = None
         self.task_name = None
         self.put_index = 0
+        self.pg_id = None        # placement group the running task / actor belongs to
+        self.capture_pg = None   # strategy children inherit (placement_group_capture_child_tasks)
+        self.runtime_env = None
 
 
 class CoreWorker:

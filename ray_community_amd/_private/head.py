@@ -1817,6 +1817,14 @@ class Head:
         self._actor_handles(a).add(caller)
         return {"actor_id": a.aid, "meta": a.spec.get("class_meta")}
 
+    def rpc_actor_handle(self, caller, aid):
+        """Handle metadata of an actor by id (``get_runtime_context().current_actor``)."""
+        a = self.actors.get(aid)
+        if a is None or a.state == A_DEAD:
+            return None
+        self._actor_handles(a).add(caller)
+        return {"actor_id": a.aid, "meta": a.spec.get("class_meta")}
+
     def rpc_actor_ready(self, caller, aid):
         a = self.actors.get(aid)
         d = Deferred()

@@ -371,6 +371,15 @@ def get_actor(name: str, namespace: Optional[str] = None):
     return ActorHandle._from_meta(info["actor_id"], info["meta"])
 
 
+def _actor_handle_by_id(aid: bytes):
+    from ..actor import ActorHandle
+
+    info = _core().client.call("actor_handle", aid)
+    if info is None:
+        raise ValueError(f"actor {aid.hex()} is not alive")
+    return ActorHandle._from_meta(info["actor_id"], info["meta"])
+
+
 def get_runtime_context():
     from ..runtime_context import RuntimeContext
 

@@ -239,6 +239,16 @@ class Worker:
         if spec.get("gpu_ids") is not None and spec["kind"] != "actor_task":
             self.core.gpu_ids = tuple(spec.get("gpu_ids") or ())
         self.core.assigned_resources = spec.get("resources") or {}
+        # placement group membership: an actor's calls run in the group its creation was placed in
+        st = (self.actor_spec if spec["kind"] == "actor_task" and getattr(self, "actor_spec", None) else spec).get(
+            "strategy")
+        if st and st.get("kind") == "pg":
+            c.pg_id = st["pg_id"]
+            c.capture_pg = dict(st, bundle_index=-1) if st.get("capture") else None
+        else:
+            c.pg_id = c.capture_pg = None
+        c.runtime_env = spec.get("runtime_env") if spec["kind"] != "actor_task" else \
+            (getattr(self, "actor_spec", None) or {}).get("runtime_env")
 
     def _execute(self, spec):
         tid = spec["tid"]

@@ -68,18 +68,50 @@ class RuntimeContext:
         return {"GPU": [str(g) for g in self._core.gpu_ids]}
 
     def get_runtime_env_string(self):
-        return "{}"
+        import json
+
+        return json.dumps(self.runtime_env or {}, default=str)
+
+    @property
+    def runtime_env(self):
+        """The runtime environment of the running task / actor (the job's in the driver)."""
+        env = getattr(self._core.ctx, "runtime_env", None)
+        if env is None and self._core.mode != "worker":
+            from ._private import worker as w
+
+            env = w._state.get("runtime_env")
+        return dict(env or {})
+
+    @property
+    def current_actor(self):
+        """Handle of the actor this code runs in (reference: ``get_runtime_context().current_actor``)."""
+        from ._private import worker as w
+
+        aid = self._core.actor_id
+        if aid is None:
+            raise RuntimeError("This method is only available in an actor.")
+        return w._actor_handle_by_id(aid)
+
+    def get_resource_ids(self):
+        return {"GPU": [(int(g) if str(g).isdigit() else g, 1.0) for g in self._core.gpu_ids]}
+
+    def should_capture_child_tasks_in_placement_group(self) -> bool:
+        return getattr(self._core.ctx, "capture_pg", None) is not None
 
     @property
     def gcs_address(self):
         return self._core.session_dir
 
     def get_placement_group_id(self):
-        return None
+        pg = getattr(self._core.ctx, "pg_id", None)
+        return pg.hex() if pg is not None else None
 
     @property
     def current_placement_group_id(self):
-        return None
+        from ._private.ids import PlacementGroupID
+
+        pg = getattr(self._core.ctx, "pg_id", None)
+        return PlacementGroupID(pg) if pg is not None else None
 
     def get(self):
         return {"job_id": self.job_id, "node_id": self.node_id, "namespace": self.namespace,

@@ -117,10 +117,10 @@ def get_current_placement_group() -> Optional[PlacementGroup]:
 
     if _core is None:
         return None
-    cur = getattr(_core.ctx, "capture_pg", None)
-    if cur is None:
+    pg_id = getattr(_core.ctx, "pg_id", None)
+    if pg_id is None:
         return None
-    return PlacementGroup(PlacementGroupID(cur["pg_id"]))
+    return PlacementGroup(PlacementGroupID(pg_id))
 
 
 def check_placement_group_index(placement_group, bundle_index):
