@@ -38,12 +38,21 @@ def _spec_of(x):
     return ("const", x)
 
 
+def _on_device(node) -> bool:
+    h = getattr(node, "type_hint", None)
+    return bool(h is not None and getattr(h, "on_device", False))
+
+
 def _actor_loop_main(actor, plan):
     """Runs inside the actor process (thread). ``plan``: channels + this actor's ordered tasks."""
     in_ch: Optional[Channel] = plan["input"]
     in_reader = plan["input_reader"]
     reads: Dict[int, Tuple[Channel, int]] = plan["reads"]  # node id -> (channel, reader index)
     tasks = plan["tasks"]
+    from .torch_tensor import DeviceSender, receiver
+
+    senders = {t["nid"]: DeviceSender() for t in tasks if t.get("device")}
+    recv = receiver() if plan.get("device_reads") else None
     while True:
         local: Dict[int, Any] = {}
         fetched: Dict[int, Any] = {}
@@ -59,7 +68,7 @@ def _actor_loop_main(actor, plan):
             if isinstance(v, _Closed):
                 closed = True
                 break
-            fetched[nid] = v
+            fetched[nid] = recv.unpack(v) if recv is not None else v
         if closed:
             for t in tasks:
                 if t["out"] is not None:
@@ -98,6 +107,12 @@ def _actor_loop_main(actor, plan):
                     out = _DAGTaskError(e, traceback.format_exc())
             local[t["nid"]] = out
             if t["out"] is not None:
+                snd = senders.get(t["nid"])
+                if snd is not None and not isinstance(out, _DAGTaskError):
+                    try:
+                        out = snd.pack(out)
+                    except Exception as e:  # noqa
+                        out = _DAGTaskError(e, traceback.format_exc())
                 t["out"].write(out)
         if in_ch is not None:
             in_ch.end_read(in_reader)
@@ -125,6 +140,10 @@ class CompiledDAGRef:
         for ch, r in self._dag._outputs:
             vals.append(ch.begin_read(r, timeout))
         self._read = True
+        if self._dag._device_outputs:
+            from .torch_tensor import receiver
+
+            vals = [receiver().unpack(v) for v in vals]  # copied out before the channel is released
         for v in vals:
             if isinstance(v, _DAGTaskError):
                 self.end_read()
@@ -227,13 +246,15 @@ class CompiledDAG:
                 args = [_spec_of(a) for a in m.get_args()]
                 kwargs = {k: _spec_of(v) for k, v in m.get_kwargs().items()}
                 tasks.append({"nid": id(m), "method": m.get_method_name(), "args": args, "kwargs": kwargs,
-                              "out": out_chan.get(id(m))})
+                              "out": out_chan.get(id(m)), "device": _on_device(m)})
             plan = {"input": self._input if ak in input_consumers else None,
                     "input_reader": in_readers.index(ak) if ak in input_consumers else 0,
-                    "reads": reads, "tasks": tasks}
+                    "reads": reads, "tasks": tasks,
+                    "device_reads": any(_on_device(d) for d in methods if id(d) in reads)}
             loops.append(handle_of[ak].__ray_call__.remote(_start_loop, plan))
         get(loops)
         self._outputs = [(out_chan[i], reader_idx[(i, "driver")]) for i in out_ids]
+        self._device_outputs = any(_on_device(o) for o in out_nodes)
         self._handles = handle_of
         self._seq = 0
         self._torn_down = False

@@ -56,6 +56,16 @@ class DAGNode:
     def get_stable_uuid(self) -> str:
         return self._stable_uuid
 
+    def with_type_hint(self, typ) -> "DAGNode":
+        """Mark this node's output type for compiled DAGs, e.g. ``TorchTensorType()``: tensors
+        then travel device-to-device (``dag/torch_tensor.py``) instead of through host memory."""
+        self._type_hint = typ
+        return self
+
+    @property
+    def type_hint(self):
+        return getattr(self, "_type_hint", None)
+
     def _children(self) -> List["DAGNode"]:
         out: List[DAGNode] = []
         _scan_nodes(list(self._bound_args), out)

@@ -122,3 +122,11 @@ class Channel:
 
 def _attach(name, capacity, num_readers):
     return Channel(capacity, num_readers, _name=name)
+
+
+def __getattr__(name):  # reference import path: ray.experimental.channel.torch_tensor_type.TorchTensorType
+    if name in ("TorchTensorType", "torch_tensor_type"):
+        from ..dag import torch_tensor
+
+        return torch_tensor.TorchTensorType if name == "TorchTensorType" else torch_tensor
+    raise AttributeError(name)
