@@ -246,7 +246,50 @@ class PopulationBasedTrainingReplay(TrialScheduler):  # pragma: no cover
     pass
 
 
-__all__ = ["TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
+class HyperBandForBOHB(HyperBandScheduler):
+    """HyperBand variant paired with a BOHB searcher in the reference (``hb_bohb.py``); the
+    successive-halving rungs are the same as HyperBand's here."""
+
+
+class ResourceChangingScheduler(TrialScheduler):
+    """Wraps a base scheduler and, on each result, asks ``resources_allocation_function(controller,
+    trial, result, scheduler)`` for new trial resources (reference ``resource_changing_scheduler.py``).
+    The new request is recorded on the trial (``trial.resources``) and applies from its next start."""
+
+    def __init__(self, base_scheduler: Optional[TrialScheduler] = None, resources_allocation_function=None):
+        super().__init__()
+        self.base = base_scheduler or FIFOScheduler()
+        self.fn = resources_allocation_function
+        self.changes: List[tuple] = []
+
+    def set_search_properties(self, metric, mode, **spec):
+        self.metric, self.mode = metric, mode
+        return self.base.set_search_properties(metric, mode, **spec)
+
+    def on_trial_add(self, controller, trial):
+        return self.base.on_trial_add(controller, trial)
+
+    def on_trial_result(self, controller, trial, result):
+        if self.fn is not None:
+            new = self.fn(controller, trial, result, self)
+            if new is not None:
+                res = getattr(new, "required_resources", new)
+                if dict(res) != dict(getattr(trial, "resources", {}) or {}):
+                    trial.resources = dict(res)
+                    self.changes.append((getattr(trial, "trial_id", None), dict(res)))
+        return self.base.on_trial_result(controller, trial, result)
+
+    def on_trial_complete(self, controller, trial, result):
+        return self.base.on_trial_complete(controller, trial, result)
+
+    def on_trial_error(self, controller, trial):
+        return self.base.on_trial_error(controller, trial)
+
+    def choose_trial_to_run(self, controller):
+        return self.base.choose_trial_to_run(controller)
+
+
+__all__ = ["HyperBandForBOHB", "ResourceChangingScheduler", "TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
            "MedianStoppingRule", "PopulationBasedTraining"]
 
 

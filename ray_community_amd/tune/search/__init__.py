@@ -196,7 +196,68 @@ class Repeater(Searcher):
         return copy.deepcopy(self._current)
 
 
+UNDEFINED_SEARCH_SPACE = "Trying to sample a configuration from {cls}, but no search space has been defined."
+UNDEFINED_METRIC_MODE = "Trying to sample a configuration from {cls}, but the `metric` ({metric}) or `mode` ({mode})" \
+                        " parameters have not been set."
+
+
+class SearchAlgorithm:
+    """Trial-producing interface (reference ``tune/search/search_algorithm.py``); every Searcher
+    is driven through it by ``SearchGenerator``."""
+
+    def set_search_properties(self, metric, mode, config, **spec) -> bool:
+        return True
+
+    def next_trial(self):
+        raise NotImplementedError
+
+    def on_trial_result(self, trial_id, result):
+        pass
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        pass
+
+    def is_finished(self) -> bool:
+        return False
+
+
+class SearchGenerator(SearchAlgorithm):
+    """Adapts a ``Searcher`` (suggest-style) to the SearchAlgorithm interface."""
+
+    def __init__(self, searcher: Searcher):
+        self.searcher = searcher
+        self._finished = False
+        self._n = 0
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        ok = self.searcher.set_search_properties(metric, mode, config, **spec)
+        if hasattr(self.searcher, "set_space") and config:
+            self.searcher.set_space(config, int(spec.get("num_samples", 1)))
+        return ok
+
+    def next_trial(self):
+        self._n += 1
+        cfg = self.searcher.suggest(f"trial_{self._n:05d}")
+        if cfg == Searcher.FINISHED:
+            self._finished = True
+            return None
+        return cfg
+
+    def on_trial_result(self, trial_id, result):
+        self.searcher.on_trial_result(trial_id, result)
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        self.searcher.on_trial_complete(trial_id, result, error)
+
+    def is_finished(self):
+        return self._finished
+
+
 def __getattr__(name):
+    if name == "grid_search":
+        from .sample import grid_search
+
+        return grid_search
     if name in ("TPESearch", "OptunaSearch", "HyperOptSearch"):
         from . import tpe
 
@@ -205,4 +266,5 @@ def __getattr__(name):
 
 
 __all__ = ["Searcher", "BasicVariantGenerator", "ConcurrencyLimiter", "RandomSearch", "Repeater",
-           "generate_variants", "TPESearch", "OptunaSearch", "HyperOptSearch"]
+           "generate_variants", "TPESearch", "OptunaSearch", "HyperOptSearch", "SearchAlgorithm", "SearchGenerator",
+           "grid_search", "UNDEFINED_SEARCH_SPACE", "UNDEFINED_METRIC_MODE"]
