@@ -80,6 +80,9 @@ class _ActorExit(BaseException):
 class Worker:
     def __init__(self):
         self._log_label = None  # last task / actor label announced to the log monitor
+        self.group_pools = {}   # concurrency group -> thread pool (threaded actors)
+        self.group_limits = {}  # concurrency group -> limit (async actors)
+        self.group_sems = {}
         env = os.environ
         self.wid = bytes.fromhex(env["RCA_WORKER_ID"])
         self.inbox: "queue.Queue" = queue.Queue()
@@ -127,8 +130,11 @@ class Worker:
 
     def _dispatch_spec(self, spec):
         """Route a task (from the head, or a direct actor call) to its executor."""
+        gp = self.group_pools.get(spec.get("concurrency_group")) if spec["kind"] == "actor_task" else None
         if self.aloop is not None and spec["kind"] == "actor_task":
             self.aloop.call_soon_threadsafe(self.direct._spawn, self._run_async(spec))
+        elif gp is not None:  # the method's concurrency group: its own thread pool
+            gp.submit(self._execute, spec)
         elif self.pool is not None and spec["kind"] == "actor_task":
             self.pool.submit(self._execute, spec)
         else:
@@ -417,12 +423,23 @@ class Worker:
         elif mc and mc > 1:
             self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=mc, thread_name_prefix="rca-actor")
         groups = spec.get("concurrency_groups") or {}
-        self.group_pools = {g: concurrent.futures.ThreadPoolExecutor(max_workers=n) for g, n in groups.items()}
+        if is_async:  # async actors: a semaphore per group bounds its concurrent coroutines
+            self.group_limits = dict(groups)
+            self.group_sems = {}
+        else:
+            self.group_pools = {g: concurrent.futures.ThreadPoolExecutor(max_workers=n, thread_name_prefix=f"rca-{g}")
+                                for g, n in groups.items()}
 
     async def _run_async(self, spec):
         if self.asem is None:
             self.asem = asyncio.Semaphore(self._amc)
-        async with self.asem:
+        sem = self.asem
+        g = spec.get("concurrency_group")
+        if g is not None and g in self.group_limits:
+            sem = self.group_sems.get(g)
+            if sem is None:
+                sem = self.group_sems[g] = asyncio.Semaphore(self.group_limits[g])
+        async with sem:
             tid = spec["tid"]
             self._set_ctx(spec)
             t_start = time.time()

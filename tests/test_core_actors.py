@@ -329,3 +329,53 @@ def test_direct_calls_visible_in_state_api_and_timeline(ray_start_regular):
         time.sleep(0.2)
     assert names.count("Counter.inc") >= 5
     assert any(e["name"] == "Counter.inc" for e in ray.timeline())
+
+
+def test_concurrency_groups_threaded_and_async(ray_start_regular):
+    """Methods in a concurrency group run on that group's own concurrency budget (reference
+    test_concurrency_group.py): two 'io' calls overlap (group of 2) while 'compute' calls
+    serialise (group of 1); async actors bound each group's coroutines the same way."""
+    import time as _t
+
+    @ray.remote(concurrency_groups={"io": 2, "compute": 1})
+    class T:
+        @ray.method(concurrency_group="io")
+        def io(self):
+            _t.sleep(0.6)
+            return _t.time()
+
+        @ray.method(concurrency_group="compute")
+        def compute(self):
+            _t.sleep(0.4)
+            return _t.time()
+
+    a = T.remote()
+    ray.get(a.__ray_ready__.remote()) if hasattr(a, "__ray_ready__") else None
+    t0 = _t.time()
+    ray.get([a.io.remote(), a.io.remote()])
+    assert _t.time() - t0 < 1.1  # overlapped
+    t0 = _t.time()
+    ray.get([a.compute.remote(), a.compute.remote()])
+    assert _t.time() - t0 >= 0.75  # serialised
+
+    import asyncio
+
+    @ray.remote(concurrency_groups={"one": 1})
+    class A:
+        @ray.method(concurrency_group="one")
+        async def solo(self):
+            await asyncio.sleep(0.3)
+            return 1
+
+        async def free(self):
+            await asyncio.sleep(0.3)
+            return 2
+
+    b = A.remote()
+    ray.get(b.free.remote())
+    t0 = _t.time()
+    ray.get([b.solo.remote() for _ in range(3)])
+    assert _t.time() - t0 >= 0.85  # one at a time
+    t0 = _t.time()
+    ray.get([b.free.remote() for _ in range(3)])
+    assert _t.time() - t0 < 0.8  # default group: concurrent
