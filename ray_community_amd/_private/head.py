@@ -1278,8 +1278,8 @@ class Head:
         return w
 
     def _worker_available(self, w: WorkerState):
-        if w.dead or w.actor is not None:
-            return
+        if w.dead or w.actor is not None or getattr(w, "retiring", False):
+            return  # (retiring: the worker hit a function's max_calls and is exiting)
         node = self.nodes.get(w.node_id)
         if node is None or not node.alive:
             self._kill_worker(w)
@@ -1400,6 +1400,8 @@ class Head:
         self._send(w, (P.EXECUTE, msg))
 
     def _on_task_done(self, w: WorkerState, tid, results, info):
+        if info.get("retire") and w is not None:
+            w.retiring = True
         sp = info.get("spans")
         if sp:
             self.spans.extend(sp)

@@ -80,6 +80,7 @@ class _ActorExit(BaseException):
 class Worker:
     def __init__(self):
         self._log_label = None  # last task / actor label announced to the log monitor
+        self._calls_by_fn = {}  # function id -> executions (max_calls)
         self.group_pools = {}   # concurrency group -> thread pool (threaded actors)
         self.group_limits = {}  # concurrency group -> limit (async actors)
         self.group_sems = {}
@@ -282,9 +283,21 @@ class Worker:
         spans = tracing.drain()
         if spans:
             info["spans"] = spans
+        mcalls = spec.get("max_calls") or 0
+        retire = False
+        if kind == "task" and mcalls > 0:
+            # ``max_calls``: this worker retires after running the function that many times
+            # (reference semantics, e.g. to hand leaked GPU memory back). The head learns it with
+            # the completion, so it never hands the retiring worker another task.
+            n = self._calls_by_fn[spec["fid"]] = self._calls_by_fn.get(spec["fid"], 0) + 1
+            retire = n >= mcalls
+            if retire:
+                info["retire"] = True
         self._finish(spec, results, info, t_start)
         self._keepalive = None
         self._value_keepalive.pop(tid, None)
+        if retire:
+            self.inbox.put(None)
 
     def _execute_body(self, spec, tid, kind, info):
         results = None

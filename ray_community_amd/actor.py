@@ -55,7 +55,7 @@ def _class_meta(cls, opts):
         mo["is_async"] = inspect.iscoroutinefunction(m) or inspect.isasyncgenfunction(m)
         methods[name] = mo
     return {"class_name": cls.__name__, "methods": methods, "max_task_retries": opts.get("max_task_retries", 0),
-            "module": cls.__module__}
+            "module": cls.__module__, "max_pending_calls": int(opts.get("max_pending_calls", -1) or -1)}
 
 
 class ActorClass:
@@ -246,6 +246,17 @@ class ActorHandle:
             generator, nret = "dynamic", 1
         else:
             nret = int(num_returns)
+        limit = self._meta.get("max_pending_calls", -1)
+        if limit is not None and limit > 0:
+            ch = core.channels.get(self._actor_id) if hasattr(core, "channels") else None
+            pending = (len(ch.queue) + len(ch.inflight)) if ch is not None else 0
+            if pending >= limit:
+                from .exceptions import PendingCallsLimitExceeded
+
+                raise PendingCallsLimitExceeded(
+                    f"The task {self._meta.get('class_name', 'Actor')}.{name} could not be submitted because more "
+                    f"than {limit} tasks are queued on the actor. This limit can be adjusted with the "
+                    "`max_pending_calls` actor option.")
         enc, kw_names, contained, deps = core.encode_args(args, kwargs)
         tid = new_id()
         rids = return_ids(tid, nret)

@@ -162,6 +162,7 @@ class RemoteFunction:
             "tid": tid, "kind": "task", "fid": fid, "name": opts.get("name") or self._name, "args": enc,
             "kw_names": kw_names, "return_ids": rids, "resources": build_resources(opts, 1),
             "strategy": build_strategy(opts), "max_retries": opts.get("max_retries", 3),
+            "max_calls": int(opts.get("max_calls") or 0),
             "retry_exceptions": opts.get("retry_exceptions", False), "runtime_env": _merge_runtime_env(opts),
             "contained": contained, "generator": generator,
         }

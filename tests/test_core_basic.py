@@ -332,3 +332,33 @@ def test_concurrent_sessions_get_distinct_store_segments(tmp_path):
         assert r.returncode == 0, r.stderr
         names += [ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("STORE")]
     assert len(names) == 2 and names[0] != names[1]
+
+
+def test_max_calls_retires_worker_and_max_pending_calls(shutdown_only):
+    """``max_calls``: a worker runs the function at most N times, then a new worker takes over;
+    ``max_pending_calls``: a handle refuses calls beyond the limit (PendingCallsLimitExceeded)."""
+    import time as _t
+
+    from ray_community_amd import exceptions as exc
+
+    ray.init(num_cpus=1, include_dashboard=False, log_to_driver=False)
+
+    @ray.remote(max_calls=2)
+    def pid():
+        return os.getpid()
+
+    pids = [ray.get(pid.remote()) for _ in range(6)]
+    assert all(pids.count(p) <= 2 for p in set(pids)) and len(set(pids)) >= 3
+
+    @ray.remote(max_pending_calls=3)
+    class Slow:
+        def f(self):
+            _t.sleep(0.5)
+            return 1
+
+    s = Slow.remote()
+    refs = [s.f.remote() for _ in range(3)]
+    with pytest.raises(exc.PendingCallsLimitExceeded):
+        s.f.remote()
+    assert ray.get(refs) == [1, 1, 1]
+    assert ray.get(s.f.remote()) == 1  # room again once the queue drained
