@@ -346,9 +346,17 @@ class TuneController:
                                metadata={"_ckpt_start": _next_ckpt_index(trial.local_path)})
             fn = self.trainable
             takes = len(inspect.signature(fn).parameters) >= 1
+            if not takes:
+                fn = (lambda c, f=fn: f())
+                takes = True
+            ltf = getattr(self.rc, "log_to_file", False)
+            if ltf:  # RunConfig(log_to_file=True | "file" | ("out", "err")): trial output into the trial dir
+                names = ("stdout", "stderr") if ltf is True else ((ltf, ltf) if isinstance(ltf, str) else tuple(ltf))
+                fn = _with_log_files(fn, os.path.join(trial.local_path, names[0]),
+                                     os.path.join(trial.local_path, names[1]))
             cfg = copy.deepcopy(trial.config)
             # non-blocking: the actor may wait for resources; the first poll queues behind start()
-            trial.runner.start.remote(fn if takes else (lambda c, f=fn: f()), cfg, ctx, ckpt, {})
+            trial.runner.start.remote(fn, cfg, ctx, ckpt, {})
             trial.pending = trial.runner.poll.remote(0.05)
         elif self.kind == "class":
             cls = ActorClass(_ClassTrainableRunner, {k: v for k, v in opts.items() if k != "max_concurrency"})
@@ -698,6 +706,28 @@ class Tuner:
             trials.append(t)
         return cls(trainable, param_space=param_space, tune_config=tune_config, run_config=run_config,
                    _restored_trials=trials, _exp_dir=path)
+
+
+def _with_log_files(fn, out_path, err_path):
+    """Run ``fn(config)`` with this process's stdout / stderr appended to the trial's log files."""
+
+    def run(config):
+        import contextlib
+        import sys
+
+        os.makedirs(os.path.dirname(out_path), exist_ok=True)
+        with open(out_path, "a", buffering=1) as fo:
+            fe = fo if err_path == out_path else open(err_path, "a", buffering=1)
+            try:
+                with contextlib.redirect_stdout(fo), contextlib.redirect_stderr(fe):
+                    return fn(config)
+            finally:
+                if fe is not fo:
+                    fe.close()
+                sys.stdout.flush()
+
+    run.__name__ = getattr(fn, "__name__", "trainable")
+    return run
 
 
 def _tname(t):

@@ -101,3 +101,26 @@ def test_search_generator_and_resource_changing_scheduler(ray4, tmp_path):
                       run_config=ray.train.RunConfig(storage_path=str(tmp_path))).fit()
     assert grid.get_best_result().config["x"] == 5
     assert sched.changes and all(r == {"CPU": 2} for _, r in sched.changes)
+
+
+def _noisy(config):
+    import sys
+
+    print("trial-stdout", config["x"])
+    print("trial-stderr", config["x"], file=sys.stderr)
+    tune.report({"score": config["x"]})
+
+
+def test_run_config_log_to_file(ray4, tmp_path):
+    import glob
+    import os
+
+    grid = tune.Tuner(_noisy, param_space={"x": tune.grid_search([1, 2])},
+                      run_config=ray.train.RunConfig(storage_path=str(tmp_path), name="ltf", log_to_file=True)).fit()
+    assert len(grid) == 2
+    outs = sorted(glob.glob(os.path.join(str(tmp_path), "ltf", "*", "stdout")))
+    errs = sorted(glob.glob(os.path.join(str(tmp_path), "ltf", "*", "stderr")))
+    assert len(outs) == 2 and len(errs) == 2
+    text = "".join(open(p).read() for p in outs)
+    assert "trial-stdout 1" in text and "trial-stdout 2" in text
+    assert "trial-stderr" in "".join(open(p).read() for p in errs)
