@@ -316,6 +316,8 @@ class TuneController:
         if self.tc.trial_dirname_creator:
             name = self.tc.trial_dirname_creator(_TrialView(tid, cfg))
         t = Trial(tid, cfg, os.path.join(self.exp_dir, name), self.resources)
+        # TuneConfig.trial_name_creator: the trial's display name (train.get_context().get_trial_name())
+        t.trial_name = str(self.tc.trial_name_creator(_TrialView(tid, cfg))) if self.tc.trial_name_creator else name
         os.makedirs(t.local_path, exist_ok=True)
         self.trials.append(t)
         self.scheduler.on_trial_add(self, t)
@@ -341,7 +343,7 @@ class TuneController:
             cls = ActorClass(_TrainWorker, opts)
             trial.runner = cls.remote()
             ctx = TrainContext(trial_dir=trial.local_path, trial_id=trial.trial_id,
-                               trial_name=os.path.basename(trial.local_path),
+                               trial_name=getattr(trial, "trial_name", None) or os.path.basename(trial.local_path),
                                experiment_name=os.path.basename(self.exp_dir),
                                metadata={"_ckpt_start": _next_ckpt_index(trial.local_path)})
             fn = self.trainable

@@ -124,3 +124,14 @@ def test_run_config_log_to_file(ray4, tmp_path):
     text = "".join(open(p).read() for p in outs)
     assert "trial-stdout 1" in text and "trial-stdout 2" in text
     assert "trial-stderr" in "".join(open(p).read() for p in errs)
+
+
+def _named(config):
+    tune.report({"name": tune.get_context().get_trial_name(), "score": config["x"]})
+
+
+def test_trial_name_creator(ray4, tmp_path):
+    grid = tune.Tuner(_named, param_space={"x": tune.grid_search([3, 4])},
+                      tune_config=tune.TuneConfig(trial_name_creator=lambda t: f"xval_{t.config['x']}"),
+                      run_config=ray.train.RunConfig(storage_path=str(tmp_path))).fit()
+    assert sorted(r.metrics["name"] for r in grid) == ["xval_3", "xval_4"]
