@@ -195,16 +195,33 @@ class OwnedTable:
 
         for o in oids:
             self.objs[o].callbacks.append(cb)
-        return ev
+        return ev, cb
+
+    def _disarm(self, oids, cb):
+        """Detach a timed-out getter's callback (a get-with-timeout polling loop on a pending
+        object would otherwise pile up one closure per call, and keep dropped entries alive)."""
+        with self.cond:
+            for o in oids:
+                e = self.objs.get(o)
+                if e is None:
+                    continue
+                try:
+                    e.callbacks.remove(cb)
+                except ValueError:
+                    continue
+                if e.dropped and e.desc is None and not e.callbacks and not e.published:
+                    del self.objs[o]
 
     def wait_descs(self, oids, deadline):
         """Block until every oid has a result (or the deadline passes). Returns the descs."""
         with self.cond:
             missing = [o for o in dict.fromkeys(oids) if o in self.objs and self.objs[o].desc is None]
-            ev = self._arm(missing, len(missing)) if missing else None
-        if ev is not None:
+            armed = self._arm(missing, len(missing)) if missing else None
+        if armed is not None:
+            ev, cb = armed
             rem = None if deadline is None else max(0.0, deadline - time.monotonic())
             if not ev.wait(rem):
+                self._disarm(missing, cb)
                 raise exc.GetTimeoutError("Get timed out: some object(s) not ready after the timeout.")
         out = []
         for o in oids:

@@ -2008,9 +2008,19 @@ class Head:
         self._end_lease(ts, make_available=False)
 
     def _return_leases_of(self, owner):
+        """The lease owner is gone (disconnected or dead). A granted lease's worker may still be
+        running a task the owner pushed to it directly -- the head cannot tell -- so, as the
+        reference does for leased workers of a dead owner, the worker is killed: returning it to
+        the idle pool would over-commit its resources and queue new tasks behind the orphan."""
         for lid in list(self.leases_by_owner.get(owner, ())):
             ts = self.leases.get(lid)
-            if ts is not None:
+            if ts is None:
+                continue
+            w = self.workers.get(ts.worker) if ts.state == T_RUNNING else None
+            if w is not None and not w.dead and w.task is ts:
+                self._end_lease(ts, make_available=False)
+                self._kill_worker(w)
+            else:
                 self._end_lease(ts)
 
     def rpc_get_function(self, caller, fid):

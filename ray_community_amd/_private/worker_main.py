@@ -297,7 +297,40 @@ class Worker:
         self._keepalive = None
         self._value_keepalive.pop(tid, None)
         if retire:
+            self._retire_when_unowned()
+
+    def _owns_live_objects(self) -> bool:
+        """Objects whose value lives only in this process: device tensors in its GPU object store
+        (the head maps readers to them over HIP IPC) and results of calls it made that it still has
+        to forward (pending owned entries)."""
+        from . import gpu_store
+
+        st = gpu_store._STORE
+        if st is not None and st.entries:
+            return True
+        owned = getattr(self.core, "owned", None)
+        if owned is None:
+            return False
+        with owned.cond:
+            return any(e.desc is None for e in owned.objs.values())
+
+    def _retire_when_unowned(self):
+        """``max_calls`` retirement. The head no longer hands this worker work; the process exits
+        once nothing it owns is alive -- a CUDA tensor returned by the task stays in this process's
+        GPU store until every reader has dropped it (exiting earlier would turn it into an
+        OwnerDiedError for the caller)."""
+        if not self._owns_live_objects():
             self.inbox.put(None)
+            return
+
+        def drain():
+            while not self.exiting:
+                time.sleep(0.05)
+                if not self._owns_live_objects():
+                    self.inbox.put(None)
+                    return
+
+        threading.Thread(target=drain, name="rca-retire-drain", daemon=True).start()
 
     def _execute_body(self, spec, tid, kind, info):
         results = None

@@ -2,7 +2,8 @@
 from __future__ import annotations
 
 import inspect
-from typing import Any, Dict, Optional
+import threading
+from typing import Any, Dict, List, Optional
 
 from . import exceptions as exc
 from ._private import serialization as ser
@@ -198,6 +199,43 @@ class ActorMethod:
         return ClassMethodNode(self._handle, self._name, args, kwargs, self._opts)
 
 
+# ``max_pending_calls`` bookkeeping, independent of the transport a call takes (direct actor
+# channel, head-routed generator methods, ray:// clients, calls parked across a restart): the first
+# return id of every call this process submitted to a limited actor, pruned lazily when counted.
+_PENDING: Dict[bytes, List[bytes]] = {}
+_PENDING_LOCK = threading.Lock()
+
+
+def _pending_calls(core, actor_id) -> int:
+    with _PENDING_LOCK:
+        ids = list(_PENDING.get(actor_id, ()))
+    if not ids:
+        return 0
+    owned = getattr(core, "owned", None)
+    still, remote = [], []
+    for o in ids:
+        e = owned.objs.get(o) if owned is not None else None
+        if e is not None:
+            if e.desc is None:
+                still.append(o)
+        elif core._refs.get(o, 0) > 0:  # head-managed result the caller still references
+            remote.append(o)
+    if remote:
+        try:
+            ready = set(core.client.call("wait", remote, len(remote), 0, False, True))
+        except Exception:
+            ready = set()
+        still.extend(o for o in remote if o not in ready)
+    keep = set(still)
+    with _PENDING_LOCK:
+        cur = _PENDING.get(actor_id, [])
+        # ids appended meanwhile (other threads) were not looked at: keep them
+        _PENDING[actor_id] = [o for o in cur if o in keep or o not in ids]
+        if not _PENDING[actor_id]:
+            _PENDING.pop(actor_id, None)
+    return len(still)
+
+
 class ActorHandle:
     def __init__(self, actor_id: bytes, meta: dict, _owner=False, _register=True):
         self._actor_id = actor_id
@@ -248,9 +286,7 @@ class ActorHandle:
             nret = int(num_returns)
         limit = self._meta.get("max_pending_calls", -1)
         if limit is not None and limit > 0:
-            ch = core.channels.get(self._actor_id) if hasattr(core, "channels") else None
-            pending = (len(ch.queue) + len(ch.inflight)) if ch is not None else 0
-            if pending >= limit:
+            if _pending_calls(core, self._actor_id) >= limit:
                 from .exceptions import PendingCallsLimitExceeded
 
                 raise PendingCallsLimitExceeded(
@@ -272,6 +308,9 @@ class ActorHandle:
             for r in rids:
                 core._refs[r] = core._refs.get(r, 0) + 1
         core.submit_actor_task(spec, deps)
+        if limit is not None and limit > 0 and rids:
+            with _PENDING_LOCK:
+                _PENDING.setdefault(self._actor_id, []).append(rids[0])
         if generator == "streaming":
             return ObjectRefGenerator(tid, refs[0])
         if nret == 0:

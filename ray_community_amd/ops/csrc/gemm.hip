@@ -195,19 +195,223 @@ int launch(const void* A, const void* B, void* C, int M, int N, int K, long lda,
   return (int)hipGetLastError();
 }
 
-// Measured on MI355X (scripts/gemm_bench.py, 8B training shapes, random operands; round 2):
-//   BK=64, 2 stages, 8 waves of 128x64 (kept)   fwd 1.03-1.18 PF, dgrad 0.90-0.96, wgrad 0.71-0.91
-//   BK=32 x 3/4 stages                           fwd 0.82-1.04,    dgrad 0.66-0.73, wgrad 0.60-0.74
-//   8 waves, next-k fragments prefetched         256 VGPRs + 12-60 B/lane scratch (register-bound)
-//   4 waves (1/SIMD) of 128x128, prefetched      fwd 0.81-1.01,    dgrad 0.75-0.80, wgrad 0.62-0.77
-// hipBLASLt on the same shapes: 1.41-1.61 PF (fwd), 1.21-1.50 incl. transposed copies (bwd), so
-// the model keeps hipBLASLt; this kernel is the natural-layout path (no transposed copies,
-// deterministic, no stream-K atomics) for the next round's 8-phase schedule.
+// ------------------------------------------------------------------------------------------------
+// Ping-pong schedule (variant 1, the default). Same 256x256x64 block tile and 8 waves, but:
+//   * the wave's 128x64 output is split into 4 quadrants (A half h, B half g) of 64x32 =
+//     4 x 2 accumulators x 2 k-slices = 16 MFMAs; a wave alternates an L segment (ds_read the
+//     fragments of its next quadrant + issue 2 LDS-DMA pieces of a future K-tile) and a C segment
+//     (the 16 MFMAs), each closed by a workgroup barrier;
+//   * waves 4-7 run one segment behind waves 0-3 (one extra barrier up front), so on every SIMD
+//     one wave of the pair is in its MFMA segment while its partner reads LDS / issues DMA
+//     (MI355X_MICROARCH.md "Two waves per SIMD"): the matrix pipe never waits on LDS latency;
+//   * each LDS stage holds the K-tile as four 16 KB half-tiles [A0 | A1 | B0 | B1]; a half-tile
+//     is staged as two 8 KB pieces by the 4 loading waves of two consecutive segments, on a
+//     fixed rota, with counted vmcnt and raw barriers, so DMA stays in flight across barriers.
+// Quadrant order per K-tile: (A0,B0) (A0,B1) (A1,B1) (A1,B0) -> L reads 12, 4, 8, 4 fragments.
+// Hazard schedule (segment I: waves 0-3 run L(t,q) at I = 8t+2q, waves 4-7 at I = 8t+2q+1):
+//   half-tile X of K-tile u is staged at I0 = 8(u-2)+3+2x, I0+1 for X = A0,B1,A1,B0 (x = 0..3);
+//   an issuing wave waits at the end of L(I) for every piece it issued at <= I-4, so a piece
+//   issued at I is visible after the barrier ending I+4 -> (u, X) readable from I0+6, which is
+//   before its first read (A0,B0: 8u; B1: 8u+2; A1: 8u+4). Its previous contents (K-tile u-2)
+//   were last read at I0-2 and retired by that reader's lgkmcnt in its C segment at I0-1.
+// ------------------------------------------------------------------------------------------------
+constexpr int HALF_BYTES = 128 * 64 * 2;     // 16 KB half-tile
+constexpr int PP_STAGE = 4 * HALF_BYTES;     // [A0 | A1 | B0 | B1]
+
+// Half-tile image fill. k-contiguous half [128 outer][8 chunks]: chunk' = chunk ^ ((row>>1)&7).
+// k-outer half [64 k][16 chunks] (256-B k-rows): chunk' = chunk ^ kswz(k) -- the 8 k-rows one
+// 32-lane half of a ds_read_b64_tr_b16 touches land on 8 distinct 32-B slots of the bank row.
+// Blocks [b0, b0 + NB) of the 16 one-KB blocks; lane-linear destination, swizzle on the source.
+template <bool KMAJ, int NB>
+__device__ __forceinline__ void pp_stage(const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* half,
+                                         int b0, int lane) {
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int blk = b0 + i;
+    const int p = blk * 64 + lane;
+    const bf16_t* src;
+    if constexpr (!KMAJ) {
+      const int row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+      src = g + (long)(o0 + row) * ld + k0 + c * 8;
+    } else {
+      const int kr = p >> 4, c = (p & 15) ^ kswz(kr);
+      src = g + (long)(k0 + kr) * ld + o0 + c * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(half + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// Fragment of a half-tile image: outer indices ob*16 + (lane&15), k = kk*32 + 8*(lane>>4) + 0..7.
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8_t pp_frag(const lds_char* h, int ob, int kk, int lane) {
+  if constexpr (!KMAJ) {
+    const int row = ob * 16 + (lane & 15);
+    const int c = (kk * 4 + (lane >> 4)) ^ ((row >> 1) & 7);
+    s16x8 v = *(const lds_s16x8*)(h + row * 128 + c * 16);
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int k1 = kk * 32 + 8 * g + q, k2 = k1 + 4;
+    const int c = ob * 2 + (p >> 1), hb = (p & 1) * 8;
+    s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(h + k1 * 256 + ((c ^ kswz(k1)) << 4) + hb));
+    s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(h + k2 * 256 + ((c ^ kswz(k2)) << 4) + hb));
+    s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool AK, bool BKM, bool ACC>
+__global__ __launch_bounds__(NTHR) void gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                       bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                       long ldb, long ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = wid >> 2, wc = wid & 3;  // grp: A-row group (and schedule half); wc: B-column group
+  const int grp_u = __builtin_amdgcn_readfirstlane(grp);
+
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int lin = xcd_remap(blockIdx.x, nwg);
+  const int gsz = GROUP_M * ntn, gi = lin / gsz, fm = gi * GROUP_M;
+  const int gm = min(ntm - fm, GROUP_M), r = lin % gsz;
+  const int m0 = (fm + r % gm) * BM, n0 = (r / gm) * BN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / 64;
+  // prologue: K-tiles 0 and 1 in full (every wave: 2 blocks of each half-tile), then drain
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (s < nt) {
+      lds_char* st = smem + s * PP_STAGE;
+      pp_stage<AK, 2>(A, lda, m0, s * 64, st, wid * 2, lane);
+      pp_stage<AK, 2>(A, lda, m0 + 128, s * 64, st + HALF_BYTES, wid * 2, lane);
+      pp_stage<BKM, 2>(B, ldb, n0, s * 64, st + 2 * HALF_BYTES, wid * 2, lane);
+      pp_stage<BKM, 2>(B, ldb, n0 + 128, s * 64, st + 3 * HALF_BYTES, wid * 2, lane);
+    }
+  }
+  wait_vmcnt<0>();
+  pp_barrier();
+  if (grp_u == 1) pp_barrier();  // stagger: waves 4-7 one segment behind
+
+  bf16x8_t af[4][2], bfr[2][2];
+  bool issued_prev = false;  // this wave issued DMA in its previous L segment
+  for (int t = 0; t < nt; ++t) {
+    const lds_char* st = smem + (t & 1) * PP_STAGE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = (q == 2 || q == 3) ? 1 : 0;  // A half
+      const int g = (q == 1 || q == 2) ? 1 : 0;  // B half
+      // ---- L segment: fragments of quadrant q
+      if (q == 0 || q == 2) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) af[mi][kk] = pp_frag<AK>(st + h * HALF_BYTES, grp * 4 + mi, kk, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) bfr[nj][kk] = pp_frag<BKM>(st + (2 + g) * HALF_BYTES, wc * 2 + nj, kk, lane);
+      // ---- DMA rota (see the hazard schedule above): target K-tile u, half-tile X, piece pc
+      int u, X;
+      if (grp_u == 0) {
+        u = q < 2 ? t + 1 : t + 2;
+        X = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 0 : 3;  // A1, B0, A0, B1 (image slots A0=0 A1=1 B0=2 B1=3)
+      } else {
+        u = q == 0 ? t + 1 : t + 2;
+        X = q == 0 ? 2 : q == 1 ? 0 : q == 2 ? 3 : 1;  // B0, A0, B1, A1
+      }
+      const int pc = 1 - grp_u;                      // waves 4-7 stage piece 0, waves 0-3 piece 1
+      const bool issue = u >= 2 && u < nt;           // K-tiles 0 and 1 come from the prologue
+      if (issue) {
+        lds_char* dst = smem + (u & 1) * PP_STAGE + X * HALF_BYTES;
+        const int b0 = pc * 8 + wc * 2;
+        if (X < 2) pp_stage<AK, 2>(A, lda, m0 + X * 128, u * 64, dst, b0, lane);
+        else pp_stage<BKM, 2>(B, ldb, n0 + (X - 2) * 128, u * 64, dst, b0, lane);
+      }
+      // retire every piece this wave issued two or more L segments ago
+      if (issue && issued_prev) wait_vmcnt<4>();
+      else if (issue || issued_prev) wait_vmcnt<2>();
+      else wait_vmcnt<0>();
+      issued_prev = issue;
+      pp_barrier();
+      // ---- C segment: 16 MFMAs of quadrant (h, g)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int nj = 0; nj < 2; ++nj)
+            acc[h * 4 + mi][g * 2 + nj] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nj][kk], af[mi][kk], acc[h * 4 + mi][g * 2 + nj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+  }
+  if (grp_u == 0) pp_barrier();  // match the stagger barrier of waves 4-7
+
+  // epilogue: acc[h*4+mi][g*2+nj] reg r = C[m0 + h*128 + grp*64 + mi*16 + (lane&15)]
+  //                                         [n0 + g*128 + wc*32 + nj*16 + 4*(lane>>4) + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + (i >> 2) * 128 + grp * 64 + (i & 3) * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4);
+      unsigned long long* dst = (unsigned long long*)(C + m * ldc + n);
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if constexpr (ACC) {
+        const unsigned long long old = *dst;
+        v0 += bf2f((bf16_t)(old & 0xffff));
+        v1 += bf2f((bf16_t)((old >> 16) & 0xffff));
+        v2 += bf2f((bf16_t)((old >> 32) & 0xffff));
+        v3 += bf2f((bf16_t)((old >> 48) & 0xffff));
+      }
+      const unsigned long long o = (unsigned long long)f2bf(v0) | ((unsigned long long)f2bf(v1) << 16) |
+                                   ((unsigned long long)f2bf(v2) << 32) | ((unsigned long long)f2bf(v3) << 48);
+      *dst = o;
+    }
+  }
+}
+
+template <bool AK, bool BKM, bool ACC>
+int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+              hipStream_t st) {
+  auto kern = gemm_pp_kernel<AK, BKM, ACC>;
+  constexpr int smem = 2 * PP_STAGE;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  if (K % 64) return -1;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NTHR), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+// Variants (RCA_GEMM_VARIANT, read once per process):
+//   0: two-stage ring, all 8 waves in lockstep (round 2; measured fwd 1.03-1.18 PF, dgrad
+//      0.90-0.96, wgrad 0.71-0.91 on the 8B shapes, random operands)
+//   1: ping-pong quadrant schedule above (default)
 template <bool AK, bool BKM, bool ACC>
 int launch_variant(int variant, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
                    long ldc, hipStream_t st) {
-  (void)variant;
-  return launch<AK, BKM, ACC, 64, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
+  if (variant == 0) return launch<AK, BKM, ACC, 64, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
+  return launch_pp<AK, BKM, ACC>(A, B, C, M, N, K, lda, ldb, ldc, st);
 }
 
 }  // namespace
@@ -215,12 +419,17 @@ int launch_variant(int variant, const void* A, const void* B, void* C, int M, in
 // Shape contract (checked here and by the Python wrapper): M % 256 == 0, N % 256 == 0,
 // K % 64 == 0; leading dimensions multiples of 8 elements and 16-B aligned base pointers.
 // a_kmaj / b_kmaj select the k-outer layouts; accumulate adds into C (bf16 read-modify-write).
-static int gemm_variant() {
-  static const int v = [] {
-    const char* e = getenv("RCA_GEMM_VARIANT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+static int g_gemm_variant = [] {
+  const char* e = getenv("RCA_GEMM_VARIANT");
+  return e ? atoi(e) : 1;
+}();
+static int gemm_variant() { return g_gemm_variant; }
+
+// A/B switch for benchmarks (same process, interleaved rounds); returns the previous variant.
+RCA_API int rca_gemm_set_variant(int v) {
+  const int old = g_gemm_variant;
+  g_gemm_variant = v;
+  return old;
 }
 
 RCA_API int rca_gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, long long lda, long long ldb,

@@ -56,7 +56,24 @@ class Trainable:
     def __init__(self, config: Optional[Dict] = None, **kw):
         self.config = config or {}
         self._iteration = 0
+        # trial identity (set by the trial runner before construction, so setup() can see it)
+        self._trial_info = dict(kw.get("trial_info") or _CURRENT_TRIAL_INFO)
         self.setup(copy.deepcopy(self.config))
+
+    @property
+    def trial_id(self) -> str:
+        return self._info().get("trial_id", "default")
+
+    @property
+    def trial_name(self) -> str:
+        return self._info().get("trial_name", "default")
+
+    @property
+    def logdir(self) -> Optional[str]:
+        return self._info().get("logdir")
+
+    def _info(self):
+        return getattr(self, "_trial_info", None) or _CURRENT_TRIAL_INFO
 
     def setup(self, config):
         pass
@@ -93,8 +110,15 @@ class Stopper:
         return False
 
 
+_CURRENT_TRIAL_INFO: Dict = {}
+
+
 class _ClassTrainableRunner:
-    def __init__(self, cls, config, checkpoint_path=None):
+    def __init__(self, cls, config, checkpoint_path=None, trial_info=None, log_paths=None):
+        global _CURRENT_TRIAL_INFO
+        if log_paths:  # RunConfig(log_to_file=...): this actor process is the trial's for its lifetime
+            _redirect_fds(*log_paths)
+        _CURRENT_TRIAL_INFO = dict(trial_info or {})
         self.t = cls(config)
         if checkpoint_path:
             st = None
@@ -323,6 +347,14 @@ class TuneController:
         self.scheduler.on_trial_add(self, t)
         return t
 
+    def _log_paths(self, trial):
+        """RunConfig(log_to_file=True | "file" | ("out", "err")): the trial's stdout / stderr files."""
+        ltf = getattr(self.rc, "log_to_file", False)
+        if not ltf:
+            return None
+        names = ("stdout", "stderr") if ltf is True else ((ltf, ltf) if isinstance(ltf, str) else tuple(ltf))
+        return os.path.join(trial.local_path, names[0]), os.path.join(trial.local_path, names[1])
+
     # ----------------------------------------------------------------------- lifecycle
     def _start(self, trial: Trial):
         from .._private.worker import get
@@ -351,18 +383,19 @@ class TuneController:
             if not takes:
                 fn = (lambda c, f=fn: f())
                 takes = True
-            ltf = getattr(self.rc, "log_to_file", False)
-            if ltf:  # RunConfig(log_to_file=True | "file" | ("out", "err")): trial output into the trial dir
-                names = ("stdout", "stderr") if ltf is True else ((ltf, ltf) if isinstance(ltf, str) else tuple(ltf))
-                fn = _with_log_files(fn, os.path.join(trial.local_path, names[0]),
-                                     os.path.join(trial.local_path, names[1]))
+            logs = self._log_paths(trial)
+            if logs:
+                fn = _with_log_files(fn, *logs)
             cfg = copy.deepcopy(trial.config)
             # non-blocking: the actor may wait for resources; the first poll queues behind start()
             trial.runner.start.remote(fn, cfg, ctx, ckpt, {})
             trial.pending = trial.runner.poll.remote(0.05)
         elif self.kind == "class":
             cls = ActorClass(_ClassTrainableRunner, {k: v for k, v in opts.items() if k != "max_concurrency"})
-            trial.runner = cls.remote(self.trainable, copy.deepcopy(trial.config), ckpt.path if ckpt else None)
+            info = {"trial_id": trial.trial_id, "logdir": trial.local_path,
+                    "trial_name": getattr(trial, "trial_name", None) or os.path.basename(trial.local_path)}
+            trial.runner = cls.remote(self.trainable, copy.deepcopy(trial.config), ckpt.path if ckpt else None, info,
+                                      self._log_paths(trial))
             trial.pending = trial.runner.step.remote()
         else:
             trial.thread_q = queue.Queue()
@@ -710,23 +743,47 @@ class Tuner:
                    _restored_trials=trials, _exp_dir=path)
 
 
+def _redirect_fds(out_path, err_path):
+    """Point this process's file descriptors 1 and 2 at the trial's log files (appending), so
+    output from C extensions and child processes lands there too, not only Python-level writes.
+    Returns the saved descriptors for ``_restore_fds``."""
+    import sys
+
+    os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    saved = (os.dup(1), os.dup(2))
+    fo = os.open(out_path, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+    fe = fo if err_path == out_path else os.open(err_path, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+    os.dup2(fo, 1)
+    os.dup2(fe, 2)
+    os.close(fo)
+    if fe != fo:
+        os.close(fe)
+    return saved
+
+
+def _restore_fds(saved):
+    import sys
+
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os.dup2(saved[0], 1)
+    os.dup2(saved[1], 2)
+    os.close(saved[0])
+    os.close(saved[1])
+
+
 def _with_log_files(fn, out_path, err_path):
-    """Run ``fn(config)`` with this process's stdout / stderr appended to the trial's log files."""
+    """Run ``fn(config)`` with this process's stdout / stderr (descriptors 1 and 2) appended to
+    the trial's log files; the worker's own descriptors come back afterwards."""
 
     def run(config):
-        import contextlib
-        import sys
-
-        os.makedirs(os.path.dirname(out_path), exist_ok=True)
-        with open(out_path, "a", buffering=1) as fo:
-            fe = fo if err_path == out_path else open(err_path, "a", buffering=1)
-            try:
-                with contextlib.redirect_stdout(fo), contextlib.redirect_stderr(fe):
-                    return fn(config)
-            finally:
-                if fe is not fo:
-                    fe.close()
-                sys.stdout.flush()
+        saved = _redirect_fds(out_path, err_path)
+        try:
+            return fn(config)
+        finally:
+            _restore_fds(saved)
 
     run.__name__ = getattr(fn, "__name__", "trainable")
     return run

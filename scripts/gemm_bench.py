@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--variants", default="1,0", help="hand-GEMM variants to time (gemm.hip launch_variant)")
     args = ap.parse_args()
     dev = "cuda"
     rows = []
@@ -64,31 +65,46 @@ def main():
         if args.only and args.only not in name:
             continue
         a, b, ak, bk, f_torch, f_tr = operands(kind, M, N, K, dev)
-        out = ops.gemm(a, b, ak, bk)
+        variants = [int(v) for v in args.variants.split(",") if v]
+        lib = ops._lib.lib()
         ref = f_torch().float()
-        err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
-        acc_out = out.clone()
-        ops.gemm(a, b, ak, bk, out=acc_out, accumulate=True)
-        acc_err = ((acc_out.float() - 2 * ref).abs().max() / (2 * ref.abs().max())).item()
-        f_ours = lambda: ops.gemm(a, b, ak, bk, out=out)
-        for f in (f_ours, f_torch, f_tr):
+        row_err = {}
+        for v in variants:
+            lib.rca_gemm_set_variant(v)
+            o = ops.gemm(a, b, ak, bk)
+            row_err[f"v{v}_err"] = ((o.float() - ref).abs().max() / ref.abs().max()).item()
+            o2 = o.clone()
+            ops.gemm(a, b, ak, bk, out=o2, accumulate=True)
+            row_err[f"v{v}_acc_err"] = ((o2.float() - 2 * ref).abs().max() / (2 * ref.abs().max())).item()
+            del o, o2
+        lib.rca_gemm_set_variant(variants[0])
+        out = ops.gemm(a, b, ak, bk)
+        def mk(v):
+            def f():
+                lib.rca_gemm_set_variant(v)
+                ops.gemm(a, b, ak, bk, out=out)
+            return f
+        fns = {f"v{v}": mk(v) for v in variants}
+        fns["torch"] = f_torch
+        fns["torch+tr"] = f_tr
+        for f in fns.values():
             f()
-        res = {"ours": [], "torch": [], "torch+tr": []}
+        res = {k: [] for k in fns}
         for _ in range(args.rounds):
-            res["ours"].append(timeit(f_ours, args.reps))
-            res["torch"].append(timeit(f_torch, args.reps))
-            res["torch+tr"].append(timeit(f_tr, args.reps))
+            for k, f in fns.items():
+                res[k].append(timeit(f, args.reps))
+        lib.rca_gemm_set_variant(variants[0])
         fl = 2.0 * M * N * K
-        row = {"name": name, "M": M, "N": N, "K": K, "max_rel_err": err, "acc_rel_err": acc_err}
+        row = {"name": name, "M": M, "N": N, "K": K, **row_err}
         for k, v in res.items():
             ms = min(v)
             row[k + "_ms"] = round(ms, 4)
             row[k + "_tf"] = round(fl / ms / 1e9, 1)
         rows.append(row)
         print(json.dumps(row), flush=True)
-        del a, b, out, ref, acc_out
+        del a, b, out, ref
         torch.cuda.empty_cache()
-    tot = {k: sum(r[k + "_ms"] for r in rows) for k in ("ours", "torch", "torch+tr")}
+    tot = {k: round(sum(r[k + "_ms"] for r in rows), 4) for k in list(res)}
     print(json.dumps({"total_ms": tot}), flush=True)
     if args.json:
         with open(args.json, "w") as f:

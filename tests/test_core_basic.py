@@ -362,3 +362,63 @@ def test_max_calls_retires_worker_and_max_pending_calls(shutdown_only):
         s.f.remote()
     assert ray.get(refs) == [1, 1, 1]
     assert ray.get(s.f.remote()) == 1  # room again once the queue drained
+
+
+def test_max_pending_calls_counts_head_routed_generator_calls(shutdown_only):
+    """Generator methods take the head-routed path (not the direct actor channel); the per-handle
+    pending count still applies to them, and frees up once they finish."""
+    import time as _t
+
+    from ray_community_amd import exceptions as exc
+
+    ray.init(num_cpus=2, include_dashboard=False, log_to_driver=False)
+
+    @ray.remote(max_pending_calls=2)
+    class G:
+        def gen(self, n):
+            for i in range(n):
+                _t.sleep(0.2)
+                yield i
+
+    g = G.remote()
+    gens = [g.gen.options(num_returns="streaming").remote(3) for _ in range(2)]
+    with pytest.raises(exc.PendingCallsLimitExceeded):
+        g.gen.options(num_returns="streaming").remote(1)
+    assert [[ray.get(r) for r in x] for x in gens] == [[0, 1, 2], [0, 1, 2]]
+    deadline = _t.time() + 10
+    while True:
+        try:
+            last = g.gen.options(num_returns="streaming").remote(1)
+            break
+        except exc.PendingCallsLimitExceeded:
+            assert _t.time() < deadline
+            _t.sleep(0.05)
+    assert [ray.get(r) for r in last] == [0]
+
+
+def test_get_timeout_polling_does_not_pile_callbacks(shutdown_only):
+    """ray.get(ref, timeout=small) in a loop on a pending caller-owned result must not leave one
+    callback per call on the object (unbounded growth)."""
+    import time as _t
+
+    from ray_community_amd import exceptions as exc
+    from ray_community_amd._private import worker
+
+    ray.init(num_cpus=2, include_dashboard=False, log_to_driver=False)
+
+    @ray.remote
+    class A:
+        def slow(self):
+            _t.sleep(1.0)
+            return 7
+
+    a = A.remote()
+    ray.get(a.slow.remote())
+    ref = a.slow.remote()
+    for _ in range(50):
+        with pytest.raises(exc.GetTimeoutError):
+            ray.get(ref, timeout=0.001)
+    core = worker._core()
+    e = core.owned.objs.get(ref._id)
+    assert e is None or len(e.callbacks) <= 1
+    assert ray.get(ref) == 7

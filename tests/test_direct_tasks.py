@@ -260,3 +260,63 @@ def test_async_actor_calls_start_in_submission_order(shutdown_only):
     ray.cancel(s)
     with pytest.raises((exc.TaskCancelledError, exc.RayTaskError)):
         ray.get(s, timeout=20)
+
+
+def test_leased_worker_of_a_dead_driver_is_killed(tmp_path):
+    """A second driver leases a worker, starts a long task on it and dies. The head cannot know
+    whether the worker is still running that orphan task, so it kills the worker instead of
+    returning it (busy) to the idle pool; the cluster keeps serving the remaining driver."""
+    import subprocess
+    import sys
+
+    import psutil
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("RCA_ADDRESS", None)
+    env.pop("RAY_ADDRESS", None)
+    env["RCA_TEMP_DIR"] = str(tmp_path)
+    head = subprocess.Popen([sys.executable, "-m", "ray_community_amd", "start", "--head", "--block", "--num-cpus",
+                             "1", "--temp-dir", str(tmp_path)], cwd=root, env=env, stdout=subprocess.DEVNULL,
+                            stderr=subprocess.STDOUT)
+    pidfile = tmp_path / "orphan.pid"
+    try:
+        drv = ("import os, sys, time; sys.path.insert(0, %r)\n"
+               "import ray_community_amd as ray\n"
+               "for _ in range(600):\n"
+               "    try:\n"
+               "        ray.init(address='auto'); break\n"
+               "    except Exception:\n"
+               "        time.sleep(0.2)\n"
+               "@ray.remote\n"
+               "def orphan(path):\n"
+               "    open(path + '.tmp', 'w').write(str(os.getpid())); os.replace(path + '.tmp', path)\n"
+               "    time.sleep(300)\n"
+               "orphan.remote(%r)\n"
+               "while not os.path.exists(%r): time.sleep(0.05)\n"
+               "os._exit(0)\n") % (root, str(pidfile), str(pidfile))
+        r = subprocess.run([sys.executable, "-c", drv], cwd=root, env=env, capture_output=True, text=True,
+                           timeout=180)
+        assert r.returncode == 0, r.stderr
+        pid = int(pidfile.read_text())
+        deadline = time.time() + 20
+        while time.time() < deadline and psutil.pid_exists(pid) and psutil.Process(pid).status() != "zombie":
+            time.sleep(0.1)
+        assert not psutil.pid_exists(pid) or psutil.Process(pid).status() == "zombie", "orphan worker still running"
+        drv2 = ("import sys; sys.path.insert(0, %r)\n"
+                "import ray_community_amd as ray\n"
+                "ray.init(address='auto')\n"
+                "@ray.remote\n"
+                "def one():\n"
+                "    return 1\n"
+                "assert ray.get(one.remote(), timeout=60) == 1\n"
+                "ray.shutdown()\n") % root
+        r = subprocess.run([sys.executable, "-c", drv2], cwd=root, env=env, capture_output=True, text=True,
+                           timeout=180)
+        assert r.returncode == 0, r.stderr
+    finally:
+        head.terminate()
+        try:
+            head.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            head.kill()

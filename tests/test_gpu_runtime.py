@@ -171,3 +171,23 @@ def test_gpu_object_keeps_channels_last_layout():
         assert ray.get(r.check.remote(ref))[1] == tuple(x.stride())
     finally:
         ray.shutdown()
+
+
+def test_max_calls_task_returns_cuda_tensor(ray_gpu):
+    """A ``max_calls=1`` GPU task's worker retires after the call, but the CUDA tensor it
+    returned lives in that worker's GPU object store: the process must stay until the reader is
+    done with it (exiting at once would turn the result into OwnerDiedError)."""
+    @ray.remote(num_gpus=1, max_calls=1)
+    def make(n):
+        import torch
+
+        return torch.full((n,), 3.0, device="cuda")
+
+    refs = [make.remote(1 << 16) for _ in range(2)]
+    import time
+
+    time.sleep(1.0)  # the retiring workers have long sent their completions
+    for r in refs:
+        t = ray.get(r)
+        assert t.is_cuda and float(t.sum().item()) == 3.0 * (1 << 16)
+    del t, refs

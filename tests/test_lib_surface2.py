@@ -135,3 +135,31 @@ def test_trial_name_creator(ray4, tmp_path):
                       tune_config=tune.TuneConfig(trial_name_creator=lambda t: f"xval_{t.config['x']}"),
                       run_config=ray.train.RunConfig(storage_path=str(tmp_path))).fit()
     assert sorted(r.metrics["name"] for r in grid) == ["xval_3", "xval_4"]
+
+
+class _NoisyTrainable(tune.Trainable):
+    def setup(self, config):
+        import os as _os
+
+        _os.write(1, f"fd-level {self.trial_name}\n".encode())  # bypasses sys.stdout
+        self.x = config["x"]
+
+    def step(self):
+        print("class-trial", self.x, flush=True)
+        return {"score": self.x, "name": self.trial_name, "done": True}
+
+
+def test_class_trainable_log_to_file_and_trial_name(ray4, tmp_path):
+    """RunConfig(log_to_file) and TuneConfig.trial_name_creator apply to class trainables too;
+    the redirect is at the descriptor level, so raw fd writes land in the file."""
+    import glob
+    import os
+
+    grid = tune.Tuner(_NoisyTrainable, param_space={"x": tune.grid_search([5, 6])},
+                      tune_config=tune.TuneConfig(trial_name_creator=lambda t: f"cls_{t.config['x']}"),
+                      run_config=ray.train.RunConfig(storage_path=str(tmp_path), name="cltf",
+                                                     log_to_file=True)).fit()
+    assert sorted(r.metrics["name"] for r in grid) == ["cls_5", "cls_6"]
+    text = "".join(open(p).read() for p in glob.glob(os.path.join(str(tmp_path), "cltf", "*", "stdout")))
+    assert "class-trial 5" in text and "class-trial 6" in text
+    assert "fd-level cls_5" in text and "fd-level cls_6" in text

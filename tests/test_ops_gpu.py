@@ -437,9 +437,11 @@ def test_flat_adamw_overlapped_with_forward_matches_serial():
     assert fl.grad[fl.zero_start:].abs().max().item() == 0  # zeroed behind the update
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (512, 768, 320),
+                                   (1024, 512, 1024)])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(False, False), (False, True), (True, True), (True, False)])
-def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj):
+@pytest.mark.parametrize("variant", [1, 0])
+def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj, variant):
     """ops.gemm (hand-written gfx950 MFMA GEMM, LDS-DMA staging, swizzled row / transposed-read
     operand images, XCD-grouped tile order) vs an fp32 torch reference, all four operand
     layouts, plain and accumulating epilogues; asymmetric operands (integer-valued rows/cols
@@ -452,11 +454,16 @@ def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj):
     af = a.float().t() if a_kmaj else a.float()
     bf = b.float() if b_kmaj else b.float().t()
     ref = af @ bf
-    out = ops.gemm(a, b, a_kmaj, b_kmaj)
+    lib = ops._lib.lib()
+    prev = lib.rca_gemm_set_variant(variant)
+    try:
+        out = ops.gemm(a, b, a_kmaj, b_kmaj)
+        base = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        acc = base.clone()
+        ops.gemm(a, b, a_kmaj, b_kmaj, out=acc, accumulate=True)
+    finally:
+        lib.rca_gemm_set_variant(prev)
     torch.cuda.synchronize()
     tol = 2e-2 * ref.abs().max().item()
     assert (out.float() - ref).abs().max().item() < tol
-    base = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    acc = base.clone()
-    ops.gemm(a, b, a_kmaj, b_kmaj, out=acc, accumulate=True)
     assert (acc.float() - (ref + base.float())).abs().max().item() < tol
