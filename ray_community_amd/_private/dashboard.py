@@ -17,6 +17,7 @@ class Dashboard:
 
         self.client = DirectClient(head)
         self.client.key = "dashboard"
+        self._serve_lock = threading.Lock()
         dash = self
 
         class Handler(BaseHTTPRequestHandler):
@@ -54,17 +55,34 @@ class Dashboard:
                     self._json(500, {"error": f"{type(e).__name__}: {e}"})
                 return True
 
+            def _serve(self, method):
+                """Serve applications REST API: returns True if the path was a serve route."""
+                u = urlparse(self.path)
+                parts = [p for p in u.path.split("/") if p]
+                if parts[:3] != ["api", "serve", "applications"]:
+                    return False
+                try:
+                    body = self._body() if method == "PUT" else None
+                    self._json(*dash._serve_route(method, body))
+                except Exception as e:  # noqa
+                    self._json(500, {"error": f"{type(e).__name__}: {e}"})
+                return True
+
+            def do_PUT(self):
+                if not self._serve("PUT"):
+                    self._send(404, "not found", "text/plain")
+
             def do_POST(self):
                 if not self._jobs("POST"):
                     self._send(404, "not found", "text/plain")
 
             def do_DELETE(self):
-                if not self._jobs("DELETE"):
+                if not self._jobs("DELETE") and not self._serve("DELETE"):
                     self._send(404, "not found", "text/plain")
 
             def do_GET(self):
                 try:
-                    if self._jobs("GET"):
+                    if self._jobs("GET") or self._serve("GET"):
                         return
                     path = self.path.split("?")[0].rstrip("/")
                     query = parse_qs(urlparse(self.path).query)
@@ -140,6 +158,47 @@ class Dashboard:
             except Exception as e:  # noqa
                 return 400, {"error": str(getattr(e, "cause", None) or e)}
         return 404, {"error": "unknown job route"}
+
+    def _serve_route(self, method, body):
+        """(status, json) for ``/api/serve/applications/`` (reference:
+        ``dashboard/modules/serve/serve_rest_api_impl.py``): GET the instance details, PUT a
+        ``ServeDeploySchema`` (declarative: apps missing from it are deleted), DELETE = shutdown."""
+        from ..serve import api as sapi
+        from ..serve._private.controller import CONTROLLER_NAME, NAMESPACE
+        from .worker import get, get_actor
+
+        with self._serve_lock:
+            sapi._STATE["controller"] = None  # another driver (the CLI) may have restarted Serve
+            sapi._STATE["proxy"] = None
+            try:
+                ctrl = get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+            except ValueError:
+                ctrl = None
+            if method == "GET":
+                if ctrl is None:
+                    return 200, {"controller_info": None, "proxy_location": None, "http_options": None,
+                                 "grpc_options": None, "proxies": {}, "deploy_mode": "UNSET", "applications": {},
+                                 "target_capacity": None}
+                return 200, get(ctrl.get_serve_instance_details.remote())
+            if method == "DELETE":
+                if ctrl is not None:
+                    sapi.shutdown()
+                return 200, {}
+            if method == "PUT":
+                from pydantic import ValidationError
+
+                from ..serve._private.config_deploy import deploy_config
+                from ..serve.schema import ServeDeploySchema
+
+                try:
+                    cfg = ServeDeploySchema.model_validate(body or {})
+                except ValidationError as e:
+                    return 400, {"error": str(e)}
+                try:
+                    return 200, {"applications": deploy_config(cfg)}
+                except Exception as e:  # noqa  (build / deploy errors are the caller's config)
+                    return 400, {"error": f"{type(e).__name__}: {getattr(e, 'cause', None) or e}"}
+            return 405, {"error": "method not allowed"}
 
     @property
     def url(self):

@@ -9,6 +9,7 @@
     python -m ray_community_amd job submit [--submission-id ID] [--no-wait] -- <entrypoint ...>
     python -m ray_community_amd job status|logs|stop|delete <id> | job list
     python -m ray_community_amd microbenchmark | healthcheck
+    python -m ray_community_amd serve start|deploy CONFIG|run CONFIG_OR_IMPORT_PATH|status|config|build|shutdown
 
 Single-node design: ``start --head`` runs the session's head (scheduler, object store, worker
 pool) in a detached process that owns it until ``stop``; every other command and every
@@ -540,7 +541,162 @@ def build_parser() -> argparse.ArgumentParser:
     jl = jsub.add_parser("list")
     conn_opts(jl)
     sp.set_defaults(fn=cmd_job)
+
+    sp = sub.add_parser("serve", help="Serve: deploy / run / status / config / build / shutdown")
+    ssub = sp.add_subparsers(dest="serve_cmd", required=True)
+    ss = ssub.add_parser("start", help="start Serve (controller + proxies) on the cluster")
+    ss.add_argument("--http-host", default="127.0.0.1")
+    ss.add_argument("--http-port", type=int, default=8000)
+    ss.add_argument("--grpc-port", type=int, default=9000)
+    ss.add_argument("--grpc-servicer-functions", action="append", default=[])
+    conn_opts(ss)
+    ss = ssub.add_parser("deploy", help="declaratively deploy a config file (apps not in it are deleted)")
+    ss.add_argument("config_file_name")
+    conn_opts(ss)
+    ss = ssub.add_parser("run", help="deploy a config file or an import path and wait until it runs")
+    ss.add_argument("config_or_import_path")
+    ss.add_argument("arguments", nargs="*", help="key=value application builder args")
+    ss.add_argument("--name", default=None)
+    ss.add_argument("--route-prefix", default=None)
+    ss.add_argument("--working-dir", default=None)
+    ss.add_argument("--app-dir", default=None)
+    ss.add_argument("--runtime-env-json", default=None)
+    ss.add_argument("--non-blocking", action="store_true")
+    conn_opts(ss)
+    ss = ssub.add_parser("status", help="application and deployment status (YAML)")
+    ss.add_argument("--name", default=None)
+    conn_opts(ss)
+    ss = ssub.add_parser("config", help="the configs the running applications were deployed from")
+    ss.add_argument("--name", default=None)
+    conn_opts(ss)
+    ss = ssub.add_parser("build", help="write a deployable config for import paths")
+    ss.add_argument("import_paths", nargs="+")
+    ss.add_argument("--app-dir", default=None)
+    ss.add_argument("--output-path", "-o", default=None)
+    ss = ssub.add_parser("shutdown", help="delete every application and stop Serve")
+    ss.add_argument("--yes", "-y", action="store_true")
+    conn_opts(ss)
+    sp.set_defaults(fn=cmd_serve)
     return p
+
+
+# ------------------------------------------------------------------------------------- serve
+def _serve_config_from_target(args):
+    """A ServeDeploySchema from ``serve run``'s target: a config file, or an import path plus
+    --name / --route-prefix / --working-dir / --app-dir / --runtime-env-json / key=value args."""
+    from ..serve.schema import parse_config
+
+    target = args.config_or_import_path
+    if os.path.exists(target) and target.endswith((".yaml", ".yml", ".json")):
+        return parse_config(target)
+    env = json.loads(args.runtime_env_json) if getattr(args, "runtime_env_json", None) else {}
+    wd = getattr(args, "working_dir", None) or getattr(args, "app_dir", None)
+    if wd:
+        env["working_dir"] = os.path.abspath(wd)
+    app_args = dict(a.split("=", 1) for a in (getattr(args, "arguments", None) or []))
+    app = {"name": args.name or "default", "import_path": target, "runtime_env": env, "args": app_args}
+    if args.route_prefix is not None:
+        app["route_prefix"] = args.route_prefix
+    return parse_config({"applications": [app]})
+
+
+def _yaml(obj) -> str:
+    import yaml
+
+    return yaml.safe_dump(json.loads(json.dumps(obj, default=str)), sort_keys=False)
+
+
+def cmd_serve(args) -> int:
+    """``serve start|deploy|run|status|config|build|shutdown`` (reference: ``serve/scripts.py``)."""
+    sc = args.serve_cmd
+    if sc == "build":
+        from ..serve._private.config_deploy import build_config
+
+        text = _yaml(build_config(args.import_paths, args.app_dir))
+        if args.output_path:
+            with open(args.output_path, "w") as f:
+                f.write(text)
+        else:
+            print(text, end="")
+        return 0
+    ray = _connect(args)
+    from .. import serve
+    from ..serve import api as sapi
+    from ..serve._private.controller import CONTROLLER_NAME, NAMESPACE
+
+    def controller():
+        try:
+            return ray.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+        except ValueError:
+            return None
+
+    if sc == "start":
+        grpc = None
+        if args.grpc_servicer_functions:
+            grpc = {"port": args.grpc_port, "grpc_servicer_functions": list(args.grpc_servicer_functions)}
+        serve.start(http_options={"host": args.http_host, "port": args.http_port}, grpc_options=grpc)
+        print(f"Serve started (HTTP {args.http_host}:{args.http_port}).")
+        return 0
+    if sc in ("deploy", "run"):
+        from pydantic import ValidationError
+
+        from ..serve._private.config_deploy import deploy_config
+        from ..serve.schema import parse_config
+
+        try:
+            cfg = parse_config(args.config_file_name) if sc == "deploy" else _serve_config_from_target(args)
+        except (ValidationError, ValueError, OSError) as e:
+            print(f"invalid Serve config: {e}", file=sys.stderr)
+            return 1
+        st = deploy_config(cfg, wait_running=(sc == "run"))
+        if sc == "deploy":
+            print(f"Sent deploy request for {len(cfg.applications)} application(s): {', '.join(st)}.")
+            return 0
+        bad = {k: v for k, v in st.items() if v != "RUNNING"}
+        if bad:
+            print(f"deploy failed: {bad}", file=sys.stderr)
+            return 1
+        print(f"Deployed {', '.join(st)}: RUNNING.", flush=True)
+        if args.non_blocking:
+            return 0
+        stop = {"v": False}
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            signal.signal(sig, lambda *_: stop.update(v=True))
+        while not stop["v"]:
+            time.sleep(0.5)
+        serve.shutdown()
+        return 0
+    if sc == "status":
+        c = controller()
+        if c is None:
+            print(_yaml({"proxies": {}, "applications": {}, "target_capacity": None}), end="")
+            return 0
+        d = ray.get(c.get_serve_instance_details.remote())
+        apps = {n: {"status": a["status"], "message": a["message"], "last_deployed_time_s": a["last_deployed_time_s"],
+                    "deployments": {dn: {"status": dd["status"], "replica_states": {"RUNNING": len(dd["replicas"])},
+                                         "target_num_replicas": dd["target_num_replicas"], "message": dd["message"]}
+                                    for dn, dd in a["deployments"].items()}}
+                for n, a in d["applications"].items() if not args.name or n == args.name}
+        print(_yaml({"proxies": {k: v.get("status") for k, v in d["proxies"].items()}, "applications": apps,
+                     "target_capacity": d.get("target_capacity")}), end="")
+        return 0
+    if sc == "config":
+        c = controller()
+        cfgs = ray.get(c.get_app_configs.remote()) if c is not None else {}
+        sel = [v for n, v in cfgs.items() if v is not None and (not args.name or n == args.name)]
+        print("\n---\n\n".join(_yaml(v) for v in sel) if sel else "No config has been deployed.", end="\n")
+        return 0
+    if sc == "shutdown":
+        if not args.yes:
+            ans = input("This will shut down Serve on the cluster. Continue? [y/N] ")
+            if ans.strip().lower() not in ("y", "yes"):
+                return 1
+        if controller() is not None:
+            serve.shutdown()
+        sapi._STATE["controller"] = None
+        print("Sent shutdown request; applications will be deleted asynchronously.")
+        return 0
+    raise SystemExit(f"unknown serve command {sc}")
 
 
 def main(argv: Optional[List[str]] = None) -> int:

@@ -42,8 +42,14 @@ class ServeController:
             self._loop_task = asyncio.ensure_future(self._control_loop())
 
     # ------------------------------------------------------------------ deploy
-    async def deploy_application(self, app_name: str, deployments: List[Dict], ingress: str, route_prefix: Optional[str]):
+    async def deploy_application(self, app_name: str, deployments: List[Dict], ingress: str, route_prefix: Optional[str],
+                                 app_config: Optional[Dict] = None):
+        """Create or update one application. ``app_config``: the declarative config it came from
+        (``ServeApplicationSchema`` dict; ``serve config`` / the REST API report it back)."""
         await self._ensure_loop()
+        for meta_app, meta in self.app_meta.items():
+            if meta_app != app_name and route_prefix is not None and meta.get("route_prefix") == route_prefix:
+                raise ValueError(f"route_prefix {route_prefix!r} is already used by application {meta_app!r}")
         old = self.apps.get(app_name, {})
         new = {}
         for spec in deployments:
@@ -51,8 +57,12 @@ class ServeController:
             if st is None:
                 st = _DeploymentState(app_name, spec["name"], spec)
             else:
-                code_changed = st.spec["body_hash"] != spec["body_hash"] or st.spec["init_args_blob"] != \
-                    spec["init_args_blob"] or st.spec["actor_options"] != spec["actor_options"]
+                if st.spec.get("code_version") and spec.get("code_version"):  # both from a config
+                    code_changed = st.spec["code_version"] != spec["code_version"]
+                else:
+                    code_changed = st.spec["body_hash"] != spec["body_hash"] or \
+                        st.spec["init_args_blob"] != spec["init_args_blob"]
+                code_changed = code_changed or st.spec["actor_options"] != spec["actor_options"]
                 if code_changed:
                     await self._stop_replicas(st, list(st.replicas))
                 elif spec.get("user_config") != st.spec.get("user_config"):
@@ -70,7 +80,7 @@ class ServeController:
                 await self._stop_replicas(st, list(st.replicas))
         self.apps[app_name] = new
         self.app_meta[app_name] = {"ingress": ingress, "route_prefix": route_prefix, "status": "DEPLOYING",
-                                   "deployed_at": time.time()}
+                                   "deployed_at": time.time(), "config": app_config}
         await self._reconcile_all()
         return True
 
@@ -238,6 +248,41 @@ class ServeController:
                                             "target": st.target, "message": st.message}
                                         for n, st in deps.items()}}
         return out
+
+    async def set_deploy_config(self, config: Dict):
+        self.deploy_config = config
+        return True
+
+    async def get_app_configs(self):
+        """{app: the declarative config it was deployed from} (apps deployed from code: None)."""
+        return {app: m.get("config") for app, m in self.app_meta.items()}
+
+    async def get_serve_instance_details(self):
+        """The ``GET /api/serve/applications/`` body (reference ``ServeInstanceDetails``):
+        instance options, and per application its status, route, deployed config and, per
+        deployment, status, target and live replicas."""
+        apps = {}
+        for app, deps in self.apps.items():
+            meta = self.app_meta.get(app, {})
+            dd = {}
+            for n, st in deps.items():
+                cfg = {k: st.spec.get(k) for k in ("num_replicas", "max_ongoing_requests", "user_config",
+                                                    "autoscaling_config")}
+                cfg["name"] = n
+                cfg["ray_actor_options"] = st.spec.get("actor_options") or {}
+                dd[n] = {"name": n, "status": st.status, "message": st.message, "target_num_replicas": st.target,
+                         "deployment_config": cfg,
+                         "replicas": [{"replica_id": tag, "state": "RUNNING"} for tag in st.replicas]}
+            apps[app] = {"name": app, "route_prefix": meta.get("route_prefix"), "status": meta.get("status"),
+                         "message": "", "last_deployed_time_s": meta.get("deployed_at"),
+                         "deployed_app_config": meta.get("config"), "docs_path": None, "deployments": dd}
+        dc = getattr(self, "deploy_config", None) or {}
+        return {"controller_info": {"actor_name": CONTROLLER_NAME}, "proxy_location": dc.get("proxy_location",
+                                                                                             "EveryNode"),
+                "http_options": dc.get("http_options") or self.http_options or None,
+                "grpc_options": dc.get("grpc_options"),
+                "proxies": {"head": {"status": "HEALTHY", **(self.proxy or {})}} if self.proxy else {},
+                "deploy_mode": "MULTI_APP", "applications": apps, "target_capacity": dc.get("target_capacity")}
 
     async def set_proxy(self, info):
         self.proxy = info
