@@ -22,8 +22,9 @@ ARCH = os.environ.get("RCA_OFFLOAD_ARCH", "gfx950")
 # AGPR-resident accumulator to VGPRs and back around each loop iteration once a kernel's live set
 # exceeds 256 VGPRs (the one-wave-per-SIMD attention dK/dV kernel: 574 v_accvgpr moves -> 26).
 EXTRA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
-# per-file overrides: the one-wave-per-SIMD dK/dV kernel keeps its accumulators in AGPRs
-FILE_FLAGS = {"attention_dkdv.hip": []}
+# per-file overrides: the one-wave-per-SIMD kernels (dK/dV, the 4-wave GEMM) keep their
+# accumulators in AGPRs
+FILE_FLAGS = {"attention_dkdv.hip": [], "gemm4.hip": []}
 
 
 def _hipcc() -> str:

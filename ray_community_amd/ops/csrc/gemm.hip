@@ -24,70 +24,10 @@
 // Workgroup order: XCD remap (each XCD gets a contiguous range) then GROUP_M=8 grouped tiles, so
 // the ~32 blocks co-resident on one XCD share A and B panels through that XCD's L2.
 #include "common.h"
+#include "gemm_common.h"
 
 namespace {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) char lds_char;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
-
-constexpr int BM = 256, BN = 256, NTHR = 512;
-constexpr int GROUP_M = 8;
-
-__device__ __forceinline__ int kswz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
-
-// Stage one 256 x BK operand tile into a lane-linear LDS image: 256*BK*2/1024 one-KB blocks, one
-// global_load_lds (64 lanes x 16 B) each, dealt round-robin over the NW waves.
-template <bool KMAJ, int BK, int NW = 8>
-__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* dst,
-                                           int wid, int lane) {
-  constexpr int CPR = BK / 8;  // 16-B chunks per k-contiguous row
-  constexpr int RSH = CPR == 8 ? 1 : 2;  // rows sharing a 256-B bank row differ in (row >> RSH)
-#pragma unroll
-  for (int i = 0; i < (BK / 2) / NW; ++i) {
-    const int blk = i * NW + wid;         // 1 KB block of the image this wave instruction fills
-    const int p = blk * 64 + lane;        // 16-B chunk index in the image
-    const bf16_t* src;
-    if constexpr (!KMAJ) {                // [256 outer][CPR chunks]
-      const int row = p / CPR, c = (p % CPR) ^ ((row >> RSH) & (CPR - 1));
-      src = g + (long)(o0 + row) * ld + k0 + c * 8;
-    } else {                              // [BK k][32 chunks]
-      const int kr = p >> 5, c = (p & 31) ^ kswz(kr);
-      src = g + (long)(k0 + kr) * ld + o0 + c * 8;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(dst + blk * 1024),
-                                     16, 0, 0);
-  }
-}
-
-// MFMA operand fragment: 16 outer indices (ob*16 + lane&15) x 8 k (kk*32 + 8*(lane>>4) + 0..7).
-template <bool KMAJ, int BK>
-__device__ __forceinline__ bf16x8_t load_frag(const lds_char* t, int ob, int kk, int lane) {
-  constexpr int CPR = BK / 8;
-  constexpr int RSH = CPR == 8 ? 1 : 2;
-  if constexpr (!KMAJ) {
-    const int row = ob * 16 + (lane & 15);
-    const int c = (kk * 4 + (lane >> 4)) ^ ((row >> RSH) & (CPR - 1));
-    s16x8 v = *(const lds_s16x8*)(t + row * (BK * 2) + c * 16);
-    return __builtin_bit_cast(bf16x8_t, v);
-  } else {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int k1 = kk * 32 + 8 * g + q, k2 = k1 + 4;
-    const int c = ob * 2 + (p >> 1), h = (p & 1) * 8;
-    s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + k1 * 512 + ((c ^ kswz(k1)) << 4) + h));
-    s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + k2 * 512 + ((c ^ kswz(k2)) << 4) + h));
-    s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+using namespace rca_gemm;
 
 // NS-stage ring of BK-deep stages; NS-1 stages in flight. One raw s_barrier per stage: the
 // counted vmcnt retires exactly the stage about to be read (the later stages stay in flight
@@ -195,223 +135,15 @@ int launch(const void* A, const void* B, void* C, int M, int N, int K, long lda,
   return (int)hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------------
-// Ping-pong schedule (variant 1, the default). Same 256x256x64 block tile and 8 waves, but:
-//   * the wave's 128x64 output is split into 4 quadrants (A half h, B half g) of 64x32 =
-//     4 x 2 accumulators x 2 k-slices = 16 MFMAs; a wave alternates an L segment (ds_read the
-//     fragments of its next quadrant + issue 2 LDS-DMA pieces of a future K-tile) and a C segment
-//     (the 16 MFMAs), each closed by a workgroup barrier;
-//   * waves 4-7 run one segment behind waves 0-3 (one extra barrier up front), so on every SIMD
-//     one wave of the pair is in its MFMA segment while its partner reads LDS / issues DMA
-//     (MI355X_MICROARCH.md "Two waves per SIMD"): the matrix pipe never waits on LDS latency;
-//   * each LDS stage holds the K-tile as four 16 KB half-tiles [A0 | A1 | B0 | B1]; a half-tile
-//     is staged as two 8 KB pieces by the 4 loading waves of two consecutive segments, on a
-//     fixed rota, with counted vmcnt and raw barriers, so DMA stays in flight across barriers.
-// Quadrant order per K-tile: (A0,B0) (A0,B1) (A1,B1) (A1,B0) -> L reads 12, 4, 8, 4 fragments.
-// Hazard schedule (segment I: waves 0-3 run L(t,q) at I = 8t+2q, waves 4-7 at I = 8t+2q+1):
-//   half-tile X of K-tile u is staged at I0 = 8(u-2)+3+2x, I0+1 for X = A0,B1,A1,B0 (x = 0..3);
-//   an issuing wave waits at the end of L(I) for every piece it issued at <= I-4, so a piece
-//   issued at I is visible after the barrier ending I+4 -> (u, X) readable from I0+6, which is
-//   before its first read (A0,B0: 8u; B1: 8u+2; A1: 8u+4). Its previous contents (K-tile u-2)
-//   were last read at I0-2 and retired by that reader's lgkmcnt in its C segment at I0-1.
-// ------------------------------------------------------------------------------------------------
-constexpr int HALF_BYTES = 128 * 64 * 2;     // 16 KB half-tile
-constexpr int PP_STAGE = 4 * HALF_BYTES;     // [A0 | A1 | B0 | B1]
-
-// Half-tile image fill. k-contiguous half [128 outer][8 chunks]: chunk' = chunk ^ ((row>>1)&7).
-// k-outer half [64 k][16 chunks] (256-B k-rows): chunk' = chunk ^ kswz(k) -- the 8 k-rows one
-// 32-lane half of a ds_read_b64_tr_b16 touches land on 8 distinct 32-B slots of the bank row.
-// Blocks [b0, b0 + NB) of the 16 one-KB blocks; lane-linear destination, swizzle on the source.
-template <bool KMAJ, int NB>
-__device__ __forceinline__ void pp_stage(const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* half,
-                                         int b0, int lane) {
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int blk = b0 + i;
-    const int p = blk * 64 + lane;
-    const bf16_t* src;
-    if constexpr (!KMAJ) {
-      const int row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
-      src = g + (long)(o0 + row) * ld + k0 + c * 8;
-    } else {
-      const int kr = p >> 4, c = (p & 15) ^ kswz(kr);
-      src = g + (long)(k0 + kr) * ld + o0 + c * 8;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(half + blk * 1024),
-                                     16, 0, 0);
-  }
-}
-
-// Fragment of a half-tile image: outer indices ob*16 + (lane&15), k = kk*32 + 8*(lane>>4) + 0..7.
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8_t pp_frag(const lds_char* h, int ob, int kk, int lane) {
-  if constexpr (!KMAJ) {
-    const int row = ob * 16 + (lane & 15);
-    const int c = (kk * 4 + (lane >> 4)) ^ ((row >> 1) & 7);
-    s16x8 v = *(const lds_s16x8*)(h + row * 128 + c * 16);
-    return __builtin_bit_cast(bf16x8_t, v);
-  } else {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int k1 = kk * 32 + 8 * g + q, k2 = k1 + 4;
-    const int c = ob * 2 + (p >> 1), hb = (p & 1) * 8;
-    s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(h + k1 * 256 + ((c ^ kswz(k1)) << 4) + hb));
-    s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(h + k2 * 256 + ((c ^ kswz(k2)) << 4) + hb));
-    s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  }
-}
-
-__device__ __forceinline__ void pp_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <bool AK, bool BKM, bool ACC>
-__global__ __launch_bounds__(NTHR) void gemm_pp_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                       bf16_t* __restrict__ C, int M, int N, int K, long lda,
-                                                       long ldb, long ldc) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char* smem = (lds_char*)smem_raw;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int grp = wid >> 2, wc = wid & 3;  // grp: A-row group (and schedule half); wc: B-column group
-  const int grp_u = __builtin_amdgcn_readfirstlane(grp);
-
-  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
-  const int lin = xcd_remap(blockIdx.x, nwg);
-  const int gsz = GROUP_M * ntn, gi = lin / gsz, fm = gi * GROUP_M;
-  const int gm = min(ntm - fm, GROUP_M), r = lin % gsz;
-  const int m0 = (fm + r % gm) * BM, n0 = (r / gm) * BN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nt = K / 64;
-  // prologue: K-tiles 0 and 1 in full (every wave: 2 blocks of each half-tile), then drain
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (s < nt) {
-      lds_char* st = smem + s * PP_STAGE;
-      pp_stage<AK, 2>(A, lda, m0, s * 64, st, wid * 2, lane);
-      pp_stage<AK, 2>(A, lda, m0 + 128, s * 64, st + HALF_BYTES, wid * 2, lane);
-      pp_stage<BKM, 2>(B, ldb, n0, s * 64, st + 2 * HALF_BYTES, wid * 2, lane);
-      pp_stage<BKM, 2>(B, ldb, n0 + 128, s * 64, st + 3 * HALF_BYTES, wid * 2, lane);
-    }
-  }
-  wait_vmcnt<0>();
-  pp_barrier();
-  if (grp_u == 1) pp_barrier();  // stagger: waves 4-7 one segment behind
-
-  bf16x8_t af[4][2], bfr[2][2];
-  bool issued_prev = false;  // this wave issued DMA in its previous L segment
-  for (int t = 0; t < nt; ++t) {
-    const lds_char* st = smem + (t & 1) * PP_STAGE;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int h = (q == 2 || q == 3) ? 1 : 0;  // A half
-      const int g = (q == 1 || q == 2) ? 1 : 0;  // B half
-      // ---- L segment: fragments of quadrant q
-      if (q == 0 || q == 2) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) af[mi][kk] = pp_frag<AK>(st + h * HALF_BYTES, grp * 4 + mi, kk, lane);
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int nj = 0; nj < 2; ++nj) bfr[nj][kk] = pp_frag<BKM>(st + (2 + g) * HALF_BYTES, wc * 2 + nj, kk, lane);
-      // ---- DMA rota (see the hazard schedule above): target K-tile u, half-tile X, piece pc
-      int u, X;
-      if (grp_u == 0) {
-        u = q < 2 ? t + 1 : t + 2;
-        X = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 0 : 3;  // A1, B0, A0, B1 (image slots A0=0 A1=1 B0=2 B1=3)
-      } else {
-        u = q == 0 ? t + 1 : t + 2;
-        X = q == 0 ? 2 : q == 1 ? 0 : q == 2 ? 3 : 1;  // B0, A0, B1, A1
-      }
-      const int pc = 1 - grp_u;                      // waves 4-7 stage piece 0, waves 0-3 piece 1
-      const bool issue = u >= 2 && u < nt;           // K-tiles 0 and 1 come from the prologue
-      if (issue) {
-        lds_char* dst = smem + (u & 1) * PP_STAGE + X * HALF_BYTES;
-        const int b0 = pc * 8 + wc * 2;
-        if (X < 2) pp_stage<AK, 2>(A, lda, m0 + X * 128, u * 64, dst, b0, lane);
-        else pp_stage<BKM, 2>(B, ldb, n0 + (X - 2) * 128, u * 64, dst, b0, lane);
-      }
-      // retire every piece this wave issued two or more L segments ago
-      if (issue && issued_prev) wait_vmcnt<4>();
-      else if (issue || issued_prev) wait_vmcnt<2>();
-      else wait_vmcnt<0>();
-      issued_prev = issue;
-      pp_barrier();
-      // ---- C segment: 16 MFMAs of quadrant (h, g)
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int nj = 0; nj < 2; ++nj)
-            acc[h * 4 + mi][g * 2 + nj] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nj][kk], af[mi][kk], acc[h * 4 + mi][g * 2 + nj], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      pp_barrier();
-    }
-  }
-  if (grp_u == 0) pp_barrier();  // match the stagger barrier of waves 4-7
-
-  // epilogue: acc[h*4+mi][g*2+nj] reg r = C[m0 + h*128 + grp*64 + mi*16 + (lane&15)]
-  //                                         [n0 + g*128 + wc*32 + nj*16 + 4*(lane>>4) + r]
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const long m = m0 + (i >> 2) * 128 + grp * 64 + (i & 3) * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4);
-      unsigned long long* dst = (unsigned long long*)(C + m * ldc + n);
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      if constexpr (ACC) {
-        const unsigned long long old = *dst;
-        v0 += bf2f((bf16_t)(old & 0xffff));
-        v1 += bf2f((bf16_t)((old >> 16) & 0xffff));
-        v2 += bf2f((bf16_t)((old >> 32) & 0xffff));
-        v3 += bf2f((bf16_t)((old >> 48) & 0xffff));
-      }
-      const unsigned long long o = (unsigned long long)f2bf(v0) | ((unsigned long long)f2bf(v1) << 16) |
-                                   ((unsigned long long)f2bf(v2) << 32) | ((unsigned long long)f2bf(v3) << 48);
-      *dst = o;
-    }
-  }
-}
-
-template <bool AK, bool BKM, bool ACC>
-int launch_pp(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
-              hipStream_t st) {
-  auto kern = gemm_pp_kernel<AK, BKM, ACC>;
-  constexpr int smem = 2 * PP_STAGE;
-  static bool attr = [&] {
-    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
-  }();
-  if (!attr) return -3;
-  if (K % 64) return -1;
-  const int nwg = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NTHR), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
-                     lda, ldb, ldc);
-  return (int)hipGetLastError();
-}
-
-// Variants (RCA_GEMM_VARIANT, read once per process):
-//   0: two-stage ring, all 8 waves in lockstep (round 2; measured fwd 1.03-1.18 PF, dgrad
-//      0.90-0.96, wgrad 0.71-0.91 on the 8B shapes, random operands)
-//   1: ping-pong quadrant schedule above (default)
+// Variants (RCA_GEMM_VARIANT, or rca_gemm_set_variant for same-process A/B):
+//   0: this file's 8-wave two-stage ring (round 2; fwd 1.15-1.24 PF, dgrad 0.97-1.04, wgrad
+//      0.82-0.98 on the 8B shapes, random operands, round-3 remeasure)
+//   2: gemm4.hip, one wave per SIMD with 128x128 wave tiles (default)
 template <bool AK, bool BKM, bool ACC>
 int launch_variant(int variant, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
                    long ldc, hipStream_t st) {
-  if (variant == 0) return launch<AK, BKM, ACC, 64, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
-  return launch_pp<AK, BKM, ACC>(A, B, C, M, N, K, lda, ldb, ldc, st);
+  (void)variant;
+  return launch<AK, BKM, ACC, 64, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
 }
 
 }  // namespace
@@ -419,9 +151,13 @@ int launch_variant(int variant, const void* A, const void* B, void* C, int M, in
 // Shape contract (checked here and by the Python wrapper): M % 256 == 0, N % 256 == 0,
 // K % 64 == 0; leading dimensions multiples of 8 elements and 16-B aligned base pointers.
 // a_kmaj / b_kmaj select the k-outer layouts; accumulate adds into C (bf16 read-modify-write).
+extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, int M, int N, int K, long long lda,
+                                       long long ldb, long long ldc, int a_kmaj, int b_kmaj, int accumulate,
+                                       hipStream_t st, int diag);
+
 static int g_gemm_variant = [] {
   const char* e = getenv("RCA_GEMM_VARIANT");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 2;
 }();
 static int gemm_variant() { return g_gemm_variant; }
 
@@ -438,6 +174,9 @@ RCA_API int rca_gemm_bf16(const void* A, const void* B, void* C, int M, int N, i
   if ((lda | ldb | ldc) & 7) return -2;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -2;
   const int v = gemm_variant();
+  if (v >= 90) return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, 0, st, v - 90);
+  if (v == 3) return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, accumulate, st, 3);
+  if (v != 0) return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, accumulate, st, 0);
 #define RCA_G(a, b, c) return launch_variant<a, b, c>(v, A, B, C, M, N, K, lda, ldb, ldc, st)
   if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G(false, false, true); RCA_G(false, false, false); }
   if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G(false, true, true); RCA_G(false, true, false); }

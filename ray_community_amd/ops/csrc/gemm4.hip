@@ -1,0 +1,423 @@
+// bf16 GEMM for gfx950, one wave per SIMD: 256x256x64 block tile, 4 waves of 128x128 each.
+//
+//   C[M][N] (+)= sum_k A(m, k) * B(n, k)     (layouts as gemm.hip: row = k-contiguous, kmaj = k-outer)
+//
+// Why this shape (MI355X_MICROARCH.md "Register files", "Two waves per SIMD"): a 128x128 wave
+// tile is 8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 = 256 accumulator registers, which fit
+// the AGPR half of a one-wave-per-SIMD register file (512 per lane) and leave the VGPR half for
+// TWO full fragment sets (k-slices kk = 0 and 1 of a 64-deep K-tile: 2 x 16 fragments x 4 VGPRs).
+// Each fragment feeds 8 MFMAs (vs 4 or 2 in the 8-wave 128x64 tiling), halving LDS read traffic
+// per MFMA, and the next k-slice's fragments are read while the current one's 64 MFMAs run, so
+// the matrix pipe never waits on LDS latency and there is no partner wave to share it with.
+// (This file is built WITHOUT -amdgpu-mfma-vgpr-form: the accumulators must live in AGPRs.)
+//
+// Per K-tile t (stage s = t & 1 of a two-stage, 2 x 64 KB LDS ring; images as gemm.hip):
+//   phase A: ds_read the kk=1 fragments (F1); 64 MFMAs on the kk=0 fragments (F0);
+//   phase B: 32 MFMAs on F1; lgkmcnt(0) + vmcnt(0) + barrier (K-tile t+1 landed for every wave,
+//            and every wave is done reading stage s); LDS-DMA of K-tile t+2 into stage s;
+//            ds_read F0 of K-tile t+1; 32 more MFMAs on F1.
+// One workgroup barrier per K-tile.
+#include "common.h"
+#include "gemm_common.h"
+
+namespace {
+using namespace rca_gemm;
+
+constexpr int NT4 = 256;            // 4 waves
+constexpr int TB = 256 * 64 * 2;    // one 256 x 64 bf16 operand tile (32 KB)
+constexpr int STG = 2 * TB;         // A tile | B tile
+
+// Stage one 256 x 64 operand tile (32 one-KB LDS-DMA blocks, 8 per wave) into the image layout of
+// gemm_common.h's stage_tile, with the addressing split into a wave-uniform base (SGPRs) plus one
+// per-lane 32-bit byte offset (k-outer: two, by block parity), so 16 in-flight DMAs cost two or
+// three VGPRs instead of a 64-bit address each.
+//   k-contiguous: block b = 4i + wid holds rows 8b .. 8b+7; the swizzle (row>>1)&7 of lane l is
+//                 (4*wid + (l>>4)) & 7 for every i  ->  src = g + (o0 + 8*wid)*ld + k0 + 32*i*ld + off
+//   k-outer:      block b holds k-rows 2b, 2b+1; kswz(k) depends on i only through i & 1.
+template <bool KMAJ>
+struct Stage4 {
+  unsigned off[2];
+  __device__ __forceinline__ Stage4(long ld, int wid, int lane) {
+    if constexpr (!KMAJ) {
+      const int c = (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7);
+      off[0] = off[1] = (unsigned)(((lane >> 3) * ld + c * 8) * 2);
+    } else {
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        const int kr = 8 * par + 2 * wid + (lane >> 5);
+        const int c = (lane & 31) ^ kswz(kr);
+        off[par] = (unsigned)(((lane >> 5) * ld + c * 8) * 2);
+      }
+    }
+  }
+  __device__ __forceinline__ void issue_one(int i, const bf16_t* __restrict__ g, long ld, int o0, int k0,
+                                            lds_char* dst, int wid) const {
+    const char* base;
+    if constexpr (!KMAJ) base = (const char*)(g + (long)(o0 + 8 * wid + 32 * i) * ld + k0);
+    else base = (const char*)(g + (long)(k0 + 2 * wid + 8 * i) * ld + o0);
+    __builtin_amdgcn_global_load_lds((const void*)(base + off[i & 1]),
+                                     (__attribute__((address_space(3))) void*)(dst + (4 * i + wid) * 1024), 16, 0, 0);
+  }
+  __device__ __forceinline__ void issue(const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* dst,
+                                        int wid) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) issue_one(i, g, ld, o0, k0, dst, wid);
+  }
+};
+
+// Fragment reads and MFMAs are inline asm. hipcc's own handling of this loop was the limit:
+// with the builtins it (a) drained every in-flight LDS-DMA (vmcnt(0)) before ds_read_b64_tr_b16
+// reads it could not prove disjoint from the DMA target, and (b) shuffled the 256 loop-carried
+// accumulators through spare AGPRs. Here the compiler only allocates registers: each MFMA is a
+// non-volatile asm tying its accumulator ("+a"), each LDS read a volatile asm, and the kernel
+// counts lgkmcnt itself at phase boundaries (the reads of a phase are consumed one phase later).
+__device__ __forceinline__ unsigned lds_off(const lds_char* p) { return (unsigned)(__UINTPTR_TYPE__)p; }
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8_t frag_asm(const lds_char* t, int ob, int kk, int lane) {
+  if constexpr (!KMAJ) {
+    const int row = ob * 16 + (lane & 15);
+    const int c = (kk * 4 + (lane >> 4)) ^ ((row >> 1) & 7);
+    s16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_off(t + row * 128 + c * 16)));
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int k1 = kk * 32 + 8 * g + q;
+    const int c = ob * 2 + (p >> 1), h = (p & 1) * 8;
+    // k2 = k1 + 4 has the same kswz (its bit 3 is k1's): the second read is 4 k-rows (2 KB) on
+    s16x4 a, b;
+    const unsigned addr = lds_off(t + k1 * 512 + ((c ^ kswz(k1)) << 4) + h);
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:2048"
+                 : "=&v"(a), "=&v"(b) : "v"(addr));
+    s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ void read_frags(const lds_char* st, int kk, int wr, int wc, int lane, bf16x8_t (&af)[8],
+                                           bf16x8_t (&bf)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) af[i] = frag_asm<AK>(st, wr * 8 + i, kk, lane);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bf[j] = frag_asm<BKM>(st + TB, wc * 8 + j, kk, lane);
+}
+
+template <int I0, int I1>
+__device__ __forceinline__ void mfma_rows(f32x4 (&acc)[8][8], const bf16x8_t (&af)[8], const bf16x8_t (&bf)[8]) {
+#pragma unroll
+  for (int i = I0; i < I1; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(bf[j]), "v"(af[i]));
+}
+
+template <int N>
+__device__ __forceinline__ void mfma_n(f32x4 (&acc)[8][8], const bf16x8_t (&af)[8], const bf16x8_t (&bf)[8], int i,
+                                       int j0) {
+#pragma unroll
+  for (int j = j0; j < j0 + N; ++j)
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(bf[j]), "v"(af[i]));
+}
+
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void fence_sched() { __builtin_amdgcn_sched_barrier(0); }
+
+template <bool AK, bool BKM, bool ACC, int DIAG = 0>
+__global__ __launch_bounds__(NT4, 1) void gemm4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                       bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                       long ldb, long ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  tile_origin(blockIdx.x, M, N, m0, n0);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / 64;
+  const Stage4<AK> sa(lda, wid, lane);
+  const Stage4<BKM> sb(ldb, wid, lane);
+  sa.issue(A, lda, m0, 0, smem, wid);
+  sb.issue(B, ldb, n0, 0, smem + TB, wid);
+  wait_vmcnt<0>();
+  fence_sched();
+  __builtin_amdgcn_s_barrier();
+  fence_sched();
+  {
+    const int k1 = min(1, nt - 1) * 64;
+    sa.issue(A, lda, m0, k1, smem + STG, wid);
+    sb.issue(B, ldb, n0, k1, smem + STG + TB, wid);
+  }
+
+  bf16x8_t f0a[8], f0b[8], f1a[8], f1b[8];
+  read_frags<AK, BKM>(smem, 0, wr, wc, lane, f0a, f0b);
+  wait_lgkm0();
+
+  // The loop body is ONE basic block (no branches): past the end the DMA re-reads K-tile nt-1
+  // and F0 reads the idle stage (harmless: nothing reads either afterwards). Scheduling fences
+  // between every small group pin the interleave of LDS reads, LDS-DMA issue and MFMAs.
+  // The DMA of K-tile t+2 goes out right after iteration t's barrier, into the stage K-tile t
+  // just vacated (every wave's F0(t) and F1(t) reads were retired before that barrier), so each
+  // tile is in flight for a whole iteration (~2,000 MFMA cycles) before it is waited for.
+  for (int t = 0; t < nt; ++t) {
+    const lds_char* st = smem + (t & 1) * STG;
+    const lds_char* nx = smem + ((t + 1) & 1) * STG;
+    const int k2 = min(t + 2, nt - 1) * 64;
+    // ---- phase A: the 16 F1 fragment reads spread over the first 64 MFMAs (on F0), one per 4
+    fence_sched();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (u < 8) f1a[u] = frag_asm<AK>(st, wr * 8 + u, 1, lane);
+      else f1b[u - 8] = frag_asm<BKM>(st + TB, wc * 8 + u - 8, 1, lane);
+      mfma_n<4>(acc, f0a, f0b, u >> 1, (u & 1) * 4);
+      fence_sched();
+    }
+    wait_lgkm0();  // F1 resident
+    fence_sched();
+    // ---- phase B: 32 MFMAs on F1 rows 0-3; K-tile t+1 landed everywhere and stage t&1 vacated;
+    //      then, beside the 32 MFMAs on rows 4-7, one F0 fragment read of K-tile t+1 and one
+    //      LDS-DMA block of K-tile t+2 (into stage t&1) per 2 MFMAs
+    mfma_rows<0, 4>(acc, f1a, f1b);
+    fence_sched();
+    if constexpr (DIAG != 2) wait_vmcnt<0>();
+    fence_sched();
+    __builtin_amdgcn_s_barrier();
+    fence_sched();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (u < 8) {
+        f0a[u] = frag_asm<AK>(nx, wr * 8 + u, 0, lane);
+        if constexpr (DIAG != 1) sa.issue_one(u, A, lda, m0, k2, (lds_char*)st, wid);
+      } else {
+        f0b[u - 8] = frag_asm<BKM>(nx + TB, wc * 8 + u - 8, 0, lane);
+        if constexpr (DIAG != 1) sb.issue_one(u - 8, B, ldb, n0, k2, (lds_char*)st + TB, wid);
+      }
+      mfma_n<2>(acc, f1a, f1b, 4 + (u >> 2), (u & 3) * 2);
+      fence_sched();
+    }
+    wait_lgkm0();  // F0 of K-tile t+1 resident
+    fence_sched();
+  }
+  wait_vmcnt<0>();
+  // the asm MFMAs are invisible to the hazard recognizer: cover the last ones' write latency
+  // before the epilogue reads the accumulators
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  fence_sched();
+
+  // epilogue: acc[i][j] reg r = C[m0 + wr*128 + i*16 + (lane&15)][n0 + wc*128 + j*16 + 4*(lane>>4) + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4<ACC>(C, m * ldc + n0 + wc * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Slice-ring variant (RCA_GEMM_VARIANT=3): same 4 waves x 128x128, but K advances in 32-deep
+// SLICES through a 4-stage LDS ring (4 x 32 KB). Measured on the 64-deep two-stage loop above:
+// without its LDS-DMA it runs 1.39-1.82 PF, with it 1.15-1.31 -- issuing 16 DMAs per wave in
+// the half-iteration between the barrier and the next tile's first read stalls the only wave
+// that feeds the SIMD's matrix pipe (a DMA costs the issuing wave far more than the 2 x 16-cycle
+// MFMA gap it was given). In the ring a stage frees up one slice after it was read, so the
+// DMA of slice s+3 can be spread over the WHOLE of slice s: 8 DMAs beside 64 MFMAs (one per 8
+// MFMAs), each in flight ~2 slices before it is waited for.
+//   iteration s (stage s & 3):  vmcnt(8) [own DMA of slice s+1 landed; slice s+2 in flight]
+//     + barrier [everyone's slice s+1 landed; everyone's reads of slice s-1 retired]
+//     -> 16 groups of { 1 F(s+1) fragment read, [1 DMA of slice s+3 -> stage (s+3)&3], 4 MFMA on F(s) }
+//     -> lgkmcnt(0) [F(s+1) resident]
+// 64-B k-contiguous rows: chunk' = chunk ^ ((-(row >> 2)) & 3) makes every ds_read_b128 lane
+// group of the 16x16x32 fragment read (16 rows, 2 chunks) hit 16 distinct 16-B bank slots.
+constexpr int SLB = 256 * 32 * 2;  // one operand slice (16 KB)
+constexpr int SST = 2 * SLB;       // stage: A slice | B slice
+
+__device__ __forceinline__ int swz32(int row) { return (-(row >> 2)) & 3; }
+
+template <bool KMAJ>
+struct SliceStage {
+  unsigned off;  // per-lane global byte offset from the step's wave-uniform base
+  __device__ __forceinline__ SliceStage(long ld, int wid, int lane) {
+    if constexpr (!KMAJ) {  // block b = 4i + wid: rows 16b .. 16b+15 (64-B rows, 4 chunks)
+      const int row = (lane >> 2), c = (lane & 3) ^ swz32(16 * wid + row);
+      off = (unsigned)((row * ld + c * 8) * 2);
+    } else {  // block b: k-rows 2b, 2b+1 (512-B rows, 32 chunks); kswz(2b + (l>>5)) indep. of i
+      const int kr = 2 * wid + (lane >> 5), c = (lane & 31) ^ kswz(kr);
+      off = (unsigned)(((lane >> 5) * ld + c * 8) * 2);
+    }
+  }
+  // step i (0..3) of a 16-KB slice: LDS block 4i + wid
+  __device__ __forceinline__ void issue(int i, const bf16_t* __restrict__ g, long ld, int o0, int k0, lds_char* dst,
+                                        int wid) const {
+    const char* base;
+    if constexpr (!KMAJ) base = (const char*)(g + (long)(o0 + 16 * wid + 64 * i) * ld + k0);
+    else base = (const char*)(g + (long)(k0 + 2 * wid + 8 * i) * ld + o0);
+    __builtin_amdgcn_global_load_lds((const void*)(base + off),
+                                     (__attribute__((address_space(3))) void*)(dst + (4 * i + wid) * 1024), 16, 0, 0);
+  }
+};
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8_t sfrag(const lds_char* t, int ob, int lane) {
+  if constexpr (!KMAJ) {
+    const int row = ob * 16 + (lane & 15);
+    const int c = (lane >> 4) ^ swz32(row);
+    s16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_off(t + row * 64 + c * 16)));
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    return frag_asm<true>(t, ob, 0, lane);  // [32 k][256] with 512-B rows: the kk = 0 read
+  }
+}
+
+template <bool AK, bool BKM, bool ACC>
+__global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                        long ldb, long ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  tile_origin(blockIdx.x, M, N, m0, n0);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / 32;  // even (K % 64 == 0)
+  const SliceStage<AK> sa(lda, wid, lane);
+  const SliceStage<BKM> sb(ldb, wid, lane);
+  auto dma = [&](int sl, int i) {  // step i of slice sl (clamped: past the end re-reads the last)
+    const int k0 = min(sl, ns - 1) * 32;
+    lds_char* st = smem + (sl & 3) * SST;
+    if (i < 4) sa.issue(i, A, lda, m0, k0, st, wid);
+    else sb.issue(i - 4, B, ldb, n0, k0, st + SLB, wid);
+  };
+#pragma unroll
+  for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma(sl, i);
+  wait_vmcnt<16>();  // slice 0 (own part) landed
+  fence_sched();
+  __builtin_amdgcn_s_barrier();
+  fence_sched();
+  bf16x8_t xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    xa[u] = sfrag<AK>(smem, wr * 8 + u, lane);
+    xb[u] = sfrag<BKM>(smem + SLB, wc * 8 + u, lane);
+  }
+  wait_lgkm0();
+
+  // one slice: cur = F(s) (in registers), nxt <- F(s+1)
+#define RCA_SLICE(S, CA, CB, NA, NB)                                                   \
+  {                                                                                    \
+    fence_sched();                                                                     \
+    wait_vmcnt<8>();                                                                   \
+    fence_sched();                                                                     \
+    __builtin_amdgcn_s_barrier();                                                      \
+    fence_sched();                                                                     \
+    const lds_char* ns_ = smem + (((S) + 1) & 3) * SST;                                \
+    _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                   \
+      if (u < 8) NA[u] = sfrag<AK>(ns_, wr * 8 + u, lane);                             \
+      else NB[u - 8] = sfrag<BKM>(ns_ + SLB, wc * 8 + u - 8, lane);                    \
+      if ((u & 1) == 0) dma((S) + 3, u >> 1);                                          \
+      mfma_n<4>(acc, CA, CB, u >> 1, (u & 1) * 4);                                     \
+      fence_sched();                                                                   \
+    }                                                                                  \
+    wait_lgkm0();                                                                      \
+    fence_sched();                                                                     \
+  }
+  for (int s = 0; s < ns; s += 2) {
+    RCA_SLICE(s, xa, xb, ya, yb)
+    RCA_SLICE(s + 1, ya, yb, xa, xb)
+  }
+#undef RCA_SLICE
+  wait_vmcnt<0>();
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  fence_sched();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4<ACC>(C, m * ldc + n0 + wc * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+template <bool AK, bool BKM, bool ACC>
+int launch4s(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+             hipStream_t st) {
+  auto kern = gemm4s_kernel<AK, BKM, ACC>;
+  constexpr int smem = 4 * SST;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+template <bool AK, bool BKM, bool ACC, int DIAG = 0>
+int launch4(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc, hipStream_t st) {
+  auto kern = gemm4_kernel<AK, BKM, ACC, DIAG>;
+  constexpr int smem = 2 * STG;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Internal entry (dispatched from rca_gemm_bf16 in gemm.hip; shapes already checked there).
+extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, int M, int N, int K, long long lda,
+                                       long long ldb, long long ldc, int a_kmaj, int b_kmaj, int accumulate,
+                                       hipStream_t st, int diag) {
+  // timing diagnostics (WRONG results): 1 = no LDS-DMA inside the K loop, 2 = DMA issued but
+  // never waited for
+  if (diag == 1 || diag == 2) {
+#define RCA_G4D(D)                                                                         \
+  {                                                                                        \
+    if (!a_kmaj && !b_kmaj) return launch4<false, false, false, D>(A, B, C, M, N, K, lda, ldb, ldc, st); \
+    if (!a_kmaj && b_kmaj) return launch4<false, true, false, D>(A, B, C, M, N, K, lda, ldb, ldc, st);   \
+    return launch4<true, true, false, D>(A, B, C, M, N, K, lda, ldb, ldc, st);                           \
+  }
+    if (diag == 1) RCA_G4D(1)
+    RCA_G4D(2)
+#undef RCA_G4D
+  }
+  if (diag == 3) {
+#define RCA_G4S(a, b, c) return launch4s<a, b, c>(A, B, C, M, N, K, lda, ldb, ldc, st)
+    if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G4S(false, false, true); RCA_G4S(false, false, false); }
+    if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G4S(false, true, true); RCA_G4S(false, true, false); }
+    if (a_kmaj && b_kmaj) { if (accumulate) RCA_G4S(true, true, true); RCA_G4S(true, true, false); }
+    if (accumulate) RCA_G4S(true, false, true);
+    RCA_G4S(true, false, false);
+#undef RCA_G4S
+  }
+#define RCA_G4(a, b, c) return launch4<a, b, c>(A, B, C, M, N, K, lda, ldb, ldc, st)
+  if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G4(false, false, true); RCA_G4(false, false, false); }
+  if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G4(false, true, true); RCA_G4(false, true, false); }
+  if (a_kmaj && b_kmaj) { if (accumulate) RCA_G4(true, true, true); RCA_G4(true, true, false); }
+  if (accumulate) RCA_G4(true, false, true);
+  RCA_G4(true, false, false);
+#undef RCA_G4
+}

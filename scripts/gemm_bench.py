@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
-    ap.add_argument("--variants", default="1,0", help="hand-GEMM variants to time (gemm.hip launch_variant)")
+    ap.add_argument("--variants", default="2,0", help="hand-GEMM variants to time (gemm.hip launch_variant)")
     args = ap.parse_args()
     dev = "cuda"
     rows = []
