@@ -1,11 +1,10 @@
-"""Streaming execution of a Dataset plan (reference: ``data/_internal/execution/streaming_executor.py``,
-``operators/{map_operator,actor_pool_map_operator}.py``, ``planner/exchange``).
+"""Task bodies of Dataset execution (reference: ``data/_internal/execution/operators/
+{map_operator,actor_pool_map_operator}.py``, ``planner/exchange``); the scheduling loop that runs
+them is ``streaming_executor.py``.
 
-* consecutive task-compute map operators are FUSED into one remote task per block;
-* actor-pool operators (callable-class UDFs, ``concurrency=``, ``num_gpus=``) keep a fixed pool of
-  actors, each fed up to ``max_tasks_in_flight_per_actor`` blocks (GPU preprocessing runs here);
-* every stage keeps a bounded window of in-flight tasks (backpressure) and yields block refs in
-  order, so a consumer iterating batches streams through the whole pipeline;
+* consecutive task-compute map operators are FUSED into one remote task per block (``_run_chain``);
+* actor-pool operators (callable-class UDFs, ``concurrency=``, ``num_gpus=``) run ``_MapActor``
+  (GPU preprocessing runs here);
 * all-to-all operators (repartition, shuffle, sort, groupby) are two-phase map/reduce exchanges.
 Each task returns ``(block, metadata)`` as two objects so counts/limits need no block fetches.
 """
@@ -135,135 +134,6 @@ def _remote_fn(f, opts):
     from ...remote_function import RemoteFunction
 
     return RemoteFunction(f, {"num_returns": 2, **opts})
-
-
-def _admit(rm, op, q) -> bool:
-    """May ``op`` launch another task now? With nothing queued for downstream it waits for
-    capacity instead of stalling the pipeline (resource_manager.py)."""
-    if rm is None or rm.can_submit(op):
-        return True
-    if q:
-        return False
-    rm.wait_for_capacity(op)
-    return True
-
-
-def source_stage(inputs, window: int, rm=None, op=None) -> Iterator[Tuple[Any, Any]]:
-    """inputs: list of ("ref", block_ref, meta_ref_or_None) or ("read", fn)."""
-    rf = None
-    q = collections.deque()
-    it = iter(inputs)
-    exhausted = False
-    while True:
-        while not exhausted and len(q) < window:
-            try:
-                x = next(it)
-            except StopIteration:
-                exhausted = True
-                break
-            if x[0] == "ref":
-                q.append((x[1], x[2]))
-            else:
-                if not _admit(rm, op, q):
-                    it = itertools.chain([x], it)
-                    break
-                if rf is None:
-                    rf = _remote_fn(_read_task, {"num_cpus": 1})
-                b, m = rf.remote(x[1])
-                if rm is not None:
-                    rm.on_submit(op, m)
-                q.append((b, m))
-        if not q:
-            return
-        yield q.popleft()
-
-
-def task_map_stage(upstream, ops, window: int, remote_opts: Dict, rm=None, op=None) -> Iterator:
-    rf = _remote_fn(_run_chain, remote_opts)
-    q = collections.deque()
-    exhausted = False
-    held = None  # upstream output pulled but not yet admitted (pulling may launch upstream work)
-    while True:
-        while not exhausted and len(q) < window:
-            if held is None:
-                try:
-                    held = next(upstream)
-                except StopIteration:
-                    exhausted = True
-                    break
-            if not _admit(rm, op, q):
-                break
-            b, held = held[0], None
-            refs = rf.remote(b, ops)
-            if rm is not None:
-                rm.on_submit(op, refs[1])
-            q.append(refs)
-        if not q:
-            return
-        yield tuple(q.popleft())
-
-
-def actor_map_stage(upstream, op, ops_before, ops_after, pool_size: int, actor_opts: Dict,
-                    max_in_flight: int = 4, rm=None, rm_op=None) -> Iterator:
-    from ..._private.worker import kill, wait
-    from ...actor import ActorClass
-
-    cls = ActorClass(_MapActor, actor_opts)
-    actors = [cls.remote(op["fn"], op.get("fn_constructor_args", ()), op.get("fn_constructor_kwargs", {}),
-                         ops_before, ops_after, {k: v for k, v in op.items() if k != "fn"}) for _ in range(pool_size)]
-    load = [0] * pool_size
-    q = collections.deque()  # (actor_idx, (block_ref, meta_ref))
-    exhausted = False
-    try:
-        while True:
-            while not exhausted and len(q) < pool_size * max_in_flight:
-                i = int(np.argmin(load))
-                if load[i] >= max_in_flight:
-                    break
-                try:
-                    b, _ = next(upstream)
-                except StopIteration:
-                    exhausted = True
-                    break
-                refs = actors[i].process.options(num_returns=2).remote(b)
-                if rm is not None:
-                    rm.on_submit(rm_op, refs[1])
-                load[i] += 1
-                q.append((i, refs))
-            if not q:
-                return
-            i, refs = q.popleft()
-            wait([refs[1]], num_returns=1)
-            load[i] -= 1
-            yield tuple(refs)
-    finally:
-        for a in actors:
-            try:
-                kill(a)
-            except Exception:
-                pass
-
-
-def limit_stage(upstream, n: int) -> Iterator:
-    from ..._private.worker import get
-    from ...remote_function import RemoteFunction
-
-    seen = 0
-    if n <= 0:
-        return
-    trunc = None
-    for b, m in upstream:
-        rows = get(m)["num_rows"]
-        if seen + rows <= n:
-            seen += rows
-            yield b, m
-        else:
-            if trunc is None:
-                trunc = _remote_fn(_truncate, {"num_cpus": 0.5})
-            yield tuple(trunc.remote(b, n - seen))
-            seen = n
-        if seen >= n:
-            return
 
 
 def _truncate(block, k):

@@ -2,8 +2,8 @@
 
 Reference behaviour: ``python/ray/data/_internal/execution/resource_manager.py:32`` (global
 limits from the cluster, a reserved share of them per operator plus a shared pool) and
-``execution/backpressure_policy/`` (per-operator concurrency caps). Redesigned for the
-pull-based stage chain of ``execution.py``:
+``execution/backpressure_policy/`` (per-operator concurrency caps). Consulted by the streaming
+executor's scheduling loop (``streaming_executor.py``) before every dispatch:
 
   * every stage registers an :class:`OpState`; a stage asks :meth:`ResourceManager.can_submit`
     before launching a task and, when it has nothing to hand downstream and may not launch,
@@ -139,6 +139,22 @@ class ResourceManager:
         self.peak_cpu = max(self.peak_cpu, u.cpu or 0.0)
         self.peak_gpu = max(self.peak_gpu, u.gpu or 0.0)
 
+    def on_finish(self, op: OpState, meta_ref):
+        """The streaming executor saw ``meta_ref`` complete: retire it without another wait."""
+        from ..._private.worker import get
+
+        try:
+            op.outstanding.remove(meta_ref)
+        except ValueError:
+            return
+        try:
+            m = get(meta_ref)
+            op.out_bytes += int(m.get("size_bytes", 0))
+            op.out_rows += int(m.get("num_rows", 0))
+        except Exception:  # a failed task: its error surfaces where the block is consumed
+            pass
+        op.finished += 1
+
     # ------------------------------------------------------------------ accounting
     def poll(self):
         """Retire finished tasks (non-blocking) and fold their output sizes into the estimates."""
@@ -181,8 +197,10 @@ class ResourceManager:
             return False
         return True
 
-    def can_submit(self, op: OpState) -> bool:
-        self.poll()
+    def can_submit(self, op: OpState, poll: bool = True) -> bool:
+        """``poll=False``: the caller (the streaming executor) retires finished tasks itself."""
+        if poll:
+            self.poll()
         if op.running == 0:
             # liveness: an idle operator may always run one task when the CPUs/GPUs allow it (or
             # when nothing at all is running); memory budgets and caps never block it

@@ -17,7 +17,7 @@ class ExecutionOptions:
     object_store_memory=)``; None = the cluster's CPUs/GPUs and
     ``object_store_memory_limit_fraction`` of its object store)."""
     resource_limits: object = field(default_factory=_no_limits)
-    preserve_order: bool = True
+    preserve_order: bool = True  # False: operators release blocks as they complete (no head-of-line blocking)
     locality_with_output: bool = False
     verbose_progress: bool = False
 
@@ -31,6 +31,7 @@ class DataContext:
     use_push_based_shuffle: bool = False
     object_store_memory_limit_fraction: float = 0.5
     op_resource_reservation_ratio: float = 0.5
+    actor_pool_idle_timeout_s: float = 1.0  # an autoscaling pool drops an actor idle this long
     last_execution_stats: object = None  # ResourceManager.stats() of the most recent execution
 
     _current = None

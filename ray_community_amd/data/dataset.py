@@ -36,9 +36,22 @@ def _ensure_init():
 
 
 class ActorPoolStrategy:
+    """Actor-pool compute: ``size`` (fixed) or ``min_size`` / ``max_size`` (the streaming executor
+    scales the pool between them on queue depth and idleness). Reference:
+    ``python/ray/data/_internal/compute.py`` ``ActorPoolStrategy``."""
+
     def __init__(self, size: Optional[int] = None, min_size: Optional[int] = None, max_size: Optional[int] = None,
                  max_tasks_in_flight_per_actor: int = 4):
-        self.size = size or max_size or min_size or 1
+        if size is not None and (min_size is not None or max_size is not None):
+            raise ValueError("min_size and max_size cannot be set at the same time as `size`")
+        if size is not None:
+            min_size = max_size = size
+        self.min_size = int(min_size or 1)
+        self.max_size = int(max_size) if max_size is not None else (self.min_size if min_size is not None else
+                                                                     self.min_size)
+        if self.max_size < self.min_size:
+            raise ValueError("min_size must be <= max_size")
+        self.size = self.max_size
         self.max_tasks_in_flight_per_actor = max_tasks_in_flight_per_actor
 
 
@@ -82,15 +95,19 @@ class Dataset:
         ctx.last_execution_stats = rm
         self._exec_rm = rm
         window = max(2, 2 * _cpus())
-        it = X.source_stage(self._inputs, window, rm, rm.register("Read", cpu=1))
+        from ._internal import streaming_executor as SE
 
-        def task_stage(it, ops):
-            opts = _task_opts(ops)
-            caps = [o.get("concurrency") for o in ops if isinstance(o.get("concurrency"), int)]
-            name = "->".join(_op_name(o) for o in ops)
+        ordered = bool(ctx.execution_options.preserve_order)
+        ex = SE.StreamingExecutor([], rm, window)
+        ops: List = [SE.InputOp(self._inputs, ordered, rm, rm.register("Read", cpu=1))]
+
+        def task_op(chain):
+            opts = _task_opts(chain)
+            caps = [o.get("concurrency") for o in chain if isinstance(o.get("concurrency"), int)]
+            name = "->".join(_op_name(o) for o in chain)
             st = rm.register(name, cpu=opts.get("num_cpus", 1) or 0, gpu=opts.get("num_gpus", 0) or 0,
                              concurrency_cap=min(caps) if caps else None)
-            return X.task_map_stage(it, ops, window, opts, rm, st)
+            return SE.TaskMapOp(name, chain, opts, ordered, rm, st)
 
         pending_tasks: List[Dict] = []
         for op in self._ops:
@@ -98,23 +115,25 @@ class Dataset:
                 pending_tasks.append(op)
                 continue
             if pending_tasks:
-                it = task_stage(it, pending_tasks)
+                ops.append(task_op(pending_tasks))
                 pending_tasks = []
-            if op["kind"] in _MAP_KINDS:  # actor pool stage
-                st = rm.register(_op_name(op) + "(actors)", concurrency_cap=op["pool_size"] *
-                                 op.get("max_tasks_in_flight_per_actor", 4))
-                it = X.actor_map_stage(it, op, [], [], op["pool_size"], op["actor_opts"],
-                                       op.get("max_tasks_in_flight_per_actor", 4), rm, st)
+            if op["kind"] in _MAP_KINDS:  # actor pool operator (autoscaling between min and max)
+                mif = op.get("max_tasks_in_flight_per_actor", 4)
+                name = _op_name(op) + "(actors)"
+                st = rm.register(name, concurrency_cap=op["max_size"] * mif)
+                ops.append(SE.ActorPoolMapOp(name, op, op["actor_opts"], op["min_size"], op["max_size"], mif,
+                                             ctx.actor_pool_idle_timeout_s, ordered, rm, st))
             elif op["kind"] == "limit":
-                it = X.limit_stage(it, op["n"])
+                ops.append(SE.LimitOp(op["n"], ordered, ex))
             elif op["kind"] == "alltoall":
-                mats = list(it)
-                it = iter(op["fn"](mats))
+                ops.append(SE.AllToAllOp(op.get("name", "AllToAll"), op["fn"], ordered))
             else:
                 raise ValueError(op["kind"])
         if pending_tasks:
-            it = task_stage(it, pending_tasks)
-        return it
+            ops.append(task_op(pending_tasks))
+        ex.__init__(ops, rm, window)
+        self._executor = ex
+        return ex.start().iter_outputs()
 
     def _refs(self) -> List[Tuple[Any, Any]]:
         if self._materialized is None:
@@ -515,6 +534,12 @@ class Dataset:
             for o in st["ops"]:
                 out += (f"\n  Operator {o['name']}: {o['tasks']} tasks, peak {o['peak_running']} concurrent, "
                         f"backpressured {o['backpressured']}x, {o['output_bytes'] / 2**20:.2f} MiB out")
+        ex = getattr(self, "_executor", None)
+        if ex is not None:
+            for name, o in ex.stats.items():
+                if "peak_pool_size" in o:
+                    out += (f"\n  Actor pool {name}: peak {o['peak_pool_size']} actors, {o['scale_ups']} scale-ups, "
+                            f"{o['scale_downs']} scale-downs")
         return out
 
     def _execution_stats(self) -> Optional[Dict]:
@@ -560,13 +585,19 @@ def _compute(op, fn, compute, concurrency, ctor_args, ctor_kwargs, num_cpus, num
     use_actors = is_class or isinstance(compute, ActorPoolStrategy) or compute == "actors"
     if use_actors:
         size = 1
+        lo = hi = None
         if isinstance(compute, ActorPoolStrategy):
-            size = compute.size
+            lo, hi = compute.min_size, compute.max_size
             op["max_tasks_in_flight_per_actor"] = compute.max_tasks_in_flight_per_actor
         elif concurrency is not None:
-            size = concurrency[-1] if isinstance(concurrency, tuple) else int(concurrency)
+            if isinstance(concurrency, tuple):
+                lo, hi = int(concurrency[0]), int(concurrency[-1])
+            else:
+                lo = hi = int(concurrency)
         op["compute"] = "actors"
-        op["pool_size"] = max(1, size)
+        op["min_size"] = max(1, lo or size)
+        op["max_size"] = max(op["min_size"], hi or op["min_size"])
+        op["pool_size"] = op["max_size"]
         opts = {"num_cpus": 1 if num_cpus is None else num_cpus}
         if num_gpus:
             opts["num_gpus"] = num_gpus

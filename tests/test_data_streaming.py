@@ -1,0 +1,127 @@
+"""Streaming executor behaviour (reference: data/tests/test_streaming_executor.py,
+test_actor_pool_map_operator.py): out-of-order release with preserve_order=False (no
+head-of-line blocking behind a slow actor), autoscaling actor pools between min_size and
+max_size, ordered mode, limits that stop upstream work."""
+import time
+
+import numpy as np
+import pytest
+
+import ray_community_amd as ray
+from ray_community_amd import data as rd
+from ray_community_amd.data import ActorPoolStrategy, DataContext
+
+
+@pytest.fixture(scope="module")
+def ray8():
+    ray.init(num_cpus=8, include_dashboard=False, log_to_driver=False)
+    yield
+    ray.shutdown()
+
+
+@pytest.fixture
+def unordered():
+    ctx = DataContext.get_current()
+    old = ctx.execution_options.preserve_order
+    ctx.execution_options.preserve_order = False
+    yield ctx
+    ctx.execution_options.preserve_order = old
+
+
+class _SlowFirstActor:
+    """The actor that handles block 0 sleeps long on it; everything else is fast."""
+
+    def __call__(self, batch):
+        if int(batch["id"][0]) == 0:
+            time.sleep(3.0)
+        return {"id": batch["id"], "t": np.full(len(batch["id"]), time.time())}
+
+
+def test_slow_actor_does_not_block_others_when_unordered(ray8, unordered):
+    ds = rd.range(40, parallelism=40).map_batches(_SlowFirstActor, batch_size=None,
+                                                 compute=ActorPoolStrategy(size=4), num_cpus=1)
+    firsts = []
+    t0 = time.time()
+    for b in ds.iter_batches(batch_size=None, batch_format="numpy"):
+        firsts.append((int(b["id"][0]), time.time() - t0))
+    order = [i for i, _ in firsts]
+    assert sorted(order) == list(range(40))
+    # block 0 (3 s on one actor) arrives after others have flowed through the remaining actors
+    pos0 = order.index(0)
+    assert pos0 >= 20, order
+    assert firsts[0][1] < 2.5, firsts[:3]
+
+
+def test_ordered_mode_returns_input_order(ray8):
+    assert DataContext.get_current().execution_options.preserve_order
+    ds = rd.range(24, parallelism=24).map_batches(_SlowFirstActor, batch_size=None,
+                                                 compute=ActorPoolStrategy(size=3), num_cpus=1)
+    ids = [int(r["id"]) for r in ds.iter_rows()]
+    assert ids == list(range(24))
+
+
+class _Sleepy:
+    def __call__(self, batch):
+        time.sleep(0.15)
+        return batch
+
+
+def _gate(batch):
+    # the first 24 blocks come at once, the rest after a pause long enough for the pool to idle
+    if int(batch["id"][0]) >= 24:
+        time.sleep(2.5)
+    return batch
+
+
+def test_actor_pool_autoscales_up_and_down(ray8, unordered):
+    ctx = unordered
+    old = ctx.actor_pool_idle_timeout_s
+    ctx.actor_pool_idle_timeout_s = 0.3
+    try:
+        ds = (rd.range(28, parallelism=28)
+              .map_batches(_gate, batch_size=None)
+              .map_batches(_Sleepy, batch_size=None, compute=ActorPoolStrategy(min_size=1, max_size=4,
+                                                                               max_tasks_in_flight_per_actor=1),
+                           num_cpus=1))
+        n = sum(len(b["id"]) for b in ds.iter_batches(batch_size=None, batch_format="numpy"))
+        assert n == 28
+        st = [o for name, o in ds._executor.stats.items() if "peak_pool_size" in o][0]
+        sizes = [s for _, s in st["pool_size_history"]]
+        assert st["peak_pool_size"] == 4, sizes
+        assert st["scale_ups"] >= 3 and st["scale_downs"] >= 1, st
+        peak_at = sizes.index(4)
+        assert min(sizes[peak_at:-1] or [4]) < 4, sizes  # shrank while the pipeline was still running
+        assert "Actor pool" in ds.stats()
+    finally:
+        ctx.actor_pool_idle_timeout_s = old
+
+
+def test_concurrency_tuple_means_min_max(ray8):
+    ds = rd.range(8, parallelism=8).map_batches(_Sleepy, batch_size=None, concurrency=(1, 3), num_cpus=1)
+    assert ds._ops[-1]["min_size"] == 1 and ds._ops[-1]["max_size"] == 3
+    assert ds.count() == 8
+    with pytest.raises(ValueError):
+        ActorPoolStrategy(size=2, min_size=1)
+    with pytest.raises(ValueError):
+        ActorPoolStrategy(min_size=3, max_size=2)
+
+
+def test_limit_stops_upstream(ray8):
+    calls = rd.range(1000, parallelism=100).map_batches(lambda b: {"id": b["id"] * 2}, batch_size=None).limit(15)
+    assert [int(r["id"]) for r in calls.take_all()] == [2 * i for i in range(15)]
+    st = calls._executor.stats
+    mapped = [o for name, o in st.items() if name.startswith("MapBatches")][0]
+    assert mapped["tasks"] < 100
+
+
+def test_unordered_results_complete_and_errors_surface(ray8, unordered):
+    ds = rd.range(30, parallelism=10).map(lambda r: {"id": r["id"] + 1})
+    assert sorted(int(r["id"]) for r in ds.iter_rows()) == list(range(1, 31))
+
+    def boom(b):
+        if int(b["id"][0]) == 5:
+            raise ValueError("bad block")
+        return b
+
+    with pytest.raises(Exception, match="bad block"):
+        rd.range(10, parallelism=10).map_batches(boom, batch_size=None).take_all()
