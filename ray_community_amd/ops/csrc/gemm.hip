@@ -157,7 +157,7 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
 
 static int g_gemm_variant = [] {
   const char* e = getenv("RCA_GEMM_VARIANT");
-  return e ? atoi(e) : 2;
+  return e ? atoi(e) : 3;
 }();
 static int gemm_variant() { return g_gemm_variant; }
 

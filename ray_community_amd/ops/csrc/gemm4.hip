@@ -121,6 +121,17 @@ __device__ __forceinline__ void mfma_n(f32x4 (&acc)[8][8], const bf16x8_t (&af)[
     asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(bf[j]), "v"(af[i]));
 }
 
+// The asm MFMAs are invisible to the hazard recognizer: before the epilogue reads the
+// accumulators, cover the last MFMAs' write latency with s_nops, then pass every accumulator
+// through an empty asm that redefines it, so no AGPR read can be scheduled ahead of the nops.
+__device__ __forceinline__ void drain_acc(f32x4 (&acc)[8][8]) {
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+}
+
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ void fence_sched() { __builtin_amdgcn_sched_barrier(0); }
@@ -210,8 +221,7 @@ __global__ __launch_bounds__(NT4, 1) void gemm4_kernel(const bf16_t* __restrict_
   wait_vmcnt<0>();
   // the asm MFMAs are invisible to the hazard recognizer: cover the last ones' write latency
   // before the epilogue reads the accumulators
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  fence_sched();
+  drain_acc(acc);
 
   // epilogue: acc[i][j] reg r = C[m0 + wr*128 + i*16 + (lane&15)][n0 + wc*128 + j*16 + 4*(lane>>4) + r]
 #pragma unroll
@@ -244,14 +254,17 @@ __device__ __forceinline__ int swz32(int row) { return (-(row >> 2)) & 3; }
 
 template <bool KMAJ>
 struct SliceStage {
-  unsigned off;  // per-lane global byte offset from the step's wave-uniform base
+  unsigned off[2];  // per-lane global byte offset from the step's wave-uniform base (by step parity)
   __device__ __forceinline__ SliceStage(long ld, int wid, int lane) {
     if constexpr (!KMAJ) {  // block b = 4i + wid: rows 16b .. 16b+15 (64-B rows, 4 chunks)
       const int row = (lane >> 2), c = (lane & 3) ^ swz32(16 * wid + row);
-      off = (unsigned)((row * ld + c * 8) * 2);
-    } else {  // block b: k-rows 2b, 2b+1 (512-B rows, 32 chunks); kswz(2b + (l>>5)) indep. of i
-      const int kr = 2 * wid + (lane >> 5), c = (lane & 31) ^ kswz(kr);
-      off = (unsigned)(((lane >> 5) * ld + c * 8) * 2);
+      off[0] = off[1] = (unsigned)((row * ld + c * 8) * 2);
+    } else {  // block b = 4i + wid: k-rows 8i + 2w + (l>>5); kswz sees i only through bit 3 (i & 1)
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        const int kr = 8 * par + 2 * wid + (lane >> 5), c = (lane & 31) ^ kswz(kr);
+        off[par] = (unsigned)(((lane >> 5) * ld + c * 8) * 2);
+      }
     }
   }
   // step i (0..3) of a 16-KB slice: LDS block 4i + wid
@@ -260,7 +273,7 @@ struct SliceStage {
     const char* base;
     if constexpr (!KMAJ) base = (const char*)(g + (long)(o0 + 16 * wid + 64 * i) * ld + k0);
     else base = (const char*)(g + (long)(k0 + 2 * wid + 8 * i) * ld + o0);
-    __builtin_amdgcn_global_load_lds((const void*)(base + off),
+    __builtin_amdgcn_global_load_lds((const void*)(base + off[i & 1]),
                                      (__attribute__((address_space(3))) void*)(dst + (4 * i + wid) * 1024), 16, 0, 0);
   }
 };
@@ -346,8 +359,7 @@ __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict
   }
 #undef RCA_SLICE
   wait_vmcnt<0>();
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  fence_sched();
+  drain_acc(acc);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const long m = m0 + wr * 128 + i * 16 + (lane & 15);
