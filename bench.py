@@ -102,6 +102,7 @@ def main():
                 "parallel_mode": m.get("parallel"),
                 "grad_reduce_dtype": m.get("grad_reduce_dtype"),
                 "launch": "torchrun" if external else "TorchTrainer worker actors",
+                "process_group": m.get("process_group"),
                 "tokens_per_step": args.micro_batch * world * args.seq_len,
                 "optimizer": "AdamW fp32 master (fused HIP)",
                 "data_parallel": {

@@ -131,5 +131,9 @@ def llama_train_loop_per_worker(config: dict):
         "parallel": net.parallel_mode,
         "grad_reduce_dtype": config.get("grad_reduce_dtype", "bf16"),
     }
+    if dev_kind == "cuda":
+        from .torch.config import group_info
+
+        metrics["process_group"] = group_info(torch.cuda.current_device())
     report(metrics)
     return metrics

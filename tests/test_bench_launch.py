@@ -57,3 +57,40 @@ def test_bench_data_serve_pipeline_cpu(tmp_path):
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec["value"] > 0 and rec["steps"] == 4 and rec["extra"]["images"] == 6 * 16
+
+
+def test_eight_virtual_gpu_workers_get_distinct_devices():
+    """8 GPU worker actors on a node with 8 (virtual) GPUs: each sees its own GPU id, the plan
+    gives every worker the union 0..7 in HIP_VISIBLE_DEVICES and a distinct device index that
+    points back at its own GPU (what _setup_torch_process_group then asserts on real hardware)."""
+    import ray_community_amd as ray
+    from ray_community_amd.train._internal.worker_group import WorkerGroup
+    from ray_community_amd.train.backend import _assign_ranks, _node_info_fn
+    from ray_community_amd.train.torch.config import plan_devices
+
+    ray.init(num_cpus=8, num_gpus=8, include_dashboard=False, log_to_driver=False)
+    try:
+        wg = WorkerGroup(8, {"CPU": 0.5, "GPU": 1})
+        infos = _assign_ranks(wg.execute(_node_info_fn))
+        plan = plan_devices(infos, use_gpu=True)
+        own = [inf["visible"][0] for inf in infos]
+        assert sorted(own, key=int) == [str(i) for i in range(8)]
+        for inf, (dev, vis) in zip(infos, plan):
+            assert vis == [str(i) for i in range(8)]
+            assert vis[dev] == inf["visible"][0]
+        assert sorted(d for d, _ in plan) == list(range(8))
+        assert [inf["local_rank"] for inf in infos] == list(range(8)) and {inf["local_world_size"] for inf in infos} == {8}
+        wg.shutdown()
+    finally:
+        ray.shutdown()
+
+
+def test_plan_devices_rejects_two_workers_on_one_gpu():
+    import pytest as _pt
+
+    from ray_community_amd.train.torch.config import plan_devices
+
+    infos = [{"node_id": "n", "visible": ["3"]}, {"node_id": "n", "visible": ["3"]}]
+    with _pt.raises(RuntimeError, match="both use GPU 3"):
+        plan_devices(infos, use_gpu=True)
+    assert plan_devices(infos, use_gpu=False) == [(None, None), (None, None)]

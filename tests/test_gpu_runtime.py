@@ -191,3 +191,38 @@ def test_max_calls_task_returns_cuda_tensor(ray_gpu):
         t = ray.get(r)
         assert t.is_cuda and float(t.sum().item()) == 3.0 * (1 << 16)
     del t, refs
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (peer import over xGMI)")
+def test_gpu_object_peer_import_between_gpus():
+    """Actor on GPU a produces a CUDA tensor; an actor on GPU b maps it through the GPU object
+    store's HIP IPC import (peer access over xGMI) and reads it bit-exactly."""
+    ray.init(num_cpus=4, num_gpus=2)
+    try:
+        @ray.remote(num_gpus=1)
+        class P:
+            def make(self, n):
+                import torch
+
+                return torch.arange(n, device="cuda", dtype=torch.float32) * 3
+
+            def dev(self):
+                return ray.get_gpu_ids()
+
+        @ray.remote(num_gpus=1)
+        class C:
+            def check(self, t, n):
+                import torch
+
+                return t.is_cuda, float(t[-1].item()), bool(torch.equal(t.cpu(), torch.arange(n).float() * 3))
+
+            def dev(self):
+                return ray.get_gpu_ids()
+
+        p, c = P.remote(), C.remote()
+        assert ray.get(p.dev.remote()) != ray.get(c.dev.remote())
+        n = 1 << 20
+        is_cuda, last, same = ray.get(c.check.remote(p.make.remote(n), n))
+        assert is_cuda and last == 3.0 * (n - 1) and same
+    finally:
+        ray.shutdown()
