@@ -789,8 +789,8 @@ def _leasable(spec) -> bool:
     which the head pins while a head-scheduled task runs)."""
     if spec["kind"] != "task" or spec.get("generator") is not None or spec.get("strategy") is not None:
         return False
-    if spec.get("runtime_env") or spec.get("contained") or spec.get("max_calls"):
-        return False  # (max_calls: the worker retires after N calls -- head-scheduled)
+    if spec.get("runtime_env") or spec.get("contained") or spec.get("max_calls") or spec.get("label_selector"):
+        return False  # (max_calls: the worker retires after N calls; label selectors: node choice -- head-scheduled)
     for k in (spec.get("resources") or {}):
         if k == "GPU" or k.startswith("GPU_group") or k.startswith("accelerator_type"):
             return False

@@ -99,6 +99,7 @@ class ObjEntry:
 class TaskState:
     __slots__ = ("tid", "spec", "state", "deps", "retries_left", "worker", "node", "demand", "owner", "key", "gpus",
                  "times", "children", "parent", "cancelled", "blocked", "gen_items", "gen_done", "gen_waiters",
+                 "gen_consumed", "gen_bp_waiters",
                  "error_type", "attempt", "reply")
 
     def __init__(self, tid, spec, owner):
@@ -119,6 +120,8 @@ class TaskState:
         self.cancelled = False
         self.blocked = False
         self.gen_items: List[bytes] = []
+        self.gen_consumed = 0          # items handed to the consumer (streaming backpressure)
+        self.gen_bp_waiters: List = []  # (needed count, Deferred) of a paused producer
         self.gen_done = False
         self.gen_waiters: Dict[int, List[Deferred]] = {}
         self.error_type = None
@@ -205,6 +208,7 @@ class Head:
         self.namespace = namespace
         self.job_id = job_id or new_id()
         self.sched = native().Scheduler(float(self.config.get("scheduler_spread_threshold", 0.5)))
+        self.label_selectors: Dict[str, list] = {}  # synthetic resource name -> selector clauses
         cap = object_store_memory or default_store_capacity()
         # random, not derived from new_id(): its last bytes are a per-process counter, so two
         # sessions on one machine would pick the same segment name and unlink each other's store
@@ -298,10 +302,46 @@ class Head:
         res[f"node:{node_id}"] = 1.0
         if is_head:
             res["node:__internal_head__"] = 1.0
+        for name, clauses in getattr(self, "label_selectors", {}).items():
+            if self._selector_matches(labels, clauses):
+                res[name] = 1e6
         self.sched.add_node(node_id, res)
-        self.nodes[node_id] = NodeState(node_id, res, labels, is_head)
+        self.nodes[node_id] = NodeState(node_id, {k: v for k, v in res.items() if not k.startswith("__labelsel:")},
+                                        labels, is_head)
         self._cluster_event("INFO", "NODE", f"node {node_id[:8]} added", node_id=node_id)
         return node_id
+
+    # ------------------------------------------------------------ label selectors
+    # ``label_selector`` / ``NodeLabelSchedulingStrategy`` hard constraints become a synthetic
+    # resource per distinct selector, present (with a capacity no task exhausts) exactly on the
+    # nodes whose labels match; the native scheduler then only places the task on those nodes.
+    @staticmethod
+    def _label_clause_ok(labels, key, op, values):
+        have = labels.get(key)
+        if op == "in":
+            return have is not None and have in values
+        if op == "not_in":
+            return have is None or have not in values
+        if op == "exists":
+            return have is not None
+        if op == "not_exists":
+            return have is None
+        raise ValueError(f"unknown label operator {op}")
+
+    def _selector_matches(self, labels, clauses):
+        return all(self._label_clause_ok(labels or {}, k, op, vals) for k, op, vals in clauses)
+
+    def _selector_resource(self, clauses) -> str:
+        import hashlib
+
+        canon = json.dumps(sorted([k, op, sorted(vals)] for k, op, vals in clauses))
+        name = "__labelsel:" + hashlib.sha1(canon.encode()).hexdigest()[:16]
+        if name not in self.label_selectors:
+            self.label_selectors[name] = clauses
+            for nid, n in self.nodes.items():
+                if n.alive and self._selector_matches(n.labels, clauses):
+                    self.sched.adjust(nid, {name: 1e6})
+        return name
 
     def add_node(self, resources: dict, labels=None) -> str:
         with self.lock:
@@ -1086,6 +1126,11 @@ class Head:
     def _demand_of(self, spec):
         res = dict(spec.get("resources") or {})
         strat = spec.get("strategy") or {}
+        clauses = list(spec.get("label_selector") or ())
+        if strat.get("kind") == "labels":
+            clauses += list(strat.get("hard") or ())
+        if clauses:
+            res[self._selector_resource(clauses)] = 0.001
         if strat.get("kind") == "pg":
             pgid = strat["pg_id"].hex()
             idx = strat.get("bundle_index", -1)
@@ -1622,11 +1667,36 @@ class Head:
         if ts is not None:
             self._flush_gen_waiters(ts)
 
+    def _gen_consumed(self, ts, index):
+        """The consumer was handed item ``index``: wake a producer paused on backpressure."""
+        if index + 1 > ts.gen_consumed:
+            ts.gen_consumed = index + 1
+            if ts.gen_bp_waiters:
+                keep = []
+                for need, d in ts.gen_bp_waiters:
+                    if ts.gen_consumed >= need:
+                        d.resolve(ts.gen_consumed)
+                    else:
+                        keep.append((need, d))
+                ts.gen_bp_waiters = keep
+
+    def rpc_gen_wait_consumed(self, caller, tid, need):
+        """``_generator_backpressure_num_objects``: the producer blocks until the consumer has
+        taken ``need`` items (reference: ``src/ray/core_worker/generator_waiter.h``)."""
+        ts = self.tasks.get(tid)
+        d = Deferred()
+        if ts is None or ts.gen_consumed >= need or ts.cancelled:
+            d.resolve(ts.gen_consumed if ts is not None else need)
+        else:
+            ts.gen_bp_waiters.append((need, d))
+        return d
+
     def _flush_gen_waiters(self, ts):
         for idx in list(ts.gen_waiters):
             if idx < len(ts.gen_items) and ts.gen_items[idx] is not None:
                 for d in ts.gen_waiters.pop(idx):
                     d.resolve(ts.gen_items[idx])
+                self._gen_consumed(ts, idx)
             elif ts.gen_done:
                 for d in ts.gen_waiters.pop(idx):
                     d.resolve(None)
@@ -1643,6 +1713,7 @@ class Head:
             if e is not None:
                 e.holders.add(caller)
             d.resolve(oid)
+            self._gen_consumed(ts, index)
             return d
         if ts.gen_done:
             # error of the generator task is surfaced through its return object
@@ -2192,7 +2263,7 @@ class Head:
         tot = collections.Counter()
         for nid, res in self.sched.totals().items():
             for k, v in res.items():
-                if "_group_" in k:
+                if "_group_" in k or k.startswith("__labelsel:"):
                     continue
                 tot[k] += v
         return dict(tot)
@@ -2201,7 +2272,7 @@ class Head:
         tot = collections.Counter()
         for nid, res in self.sched.available().items():
             for k, v in res.items():
-                if "_group_" in k:
+                if "_group_" in k or k.startswith("__labelsel:"):
                     continue
                 if v > 0:
                     tot[k] += v

@@ -421,12 +421,17 @@ class Worker:
         if gen == "streaming":
             n = spec.get("_streamed", 0)  # items already streamed by an async generator
             it = value
+            bp = int(spec.get("gen_backpressure") or 0)
+            consumed = 0
             if inspect.isgenerator(it) or hasattr(it, "__next__") or hasattr(it, "__iter__"):
                 for item in it:
                     oid = new_id()
                     r = self._pack_one(oid, item)
                     self.client.send((P.GEN_ITEM, spec["tid"], n, r + (oid,)))
                     n += 1
+                    if bp and n - consumed >= bp:
+                        # backpressure: do not run ahead of the consumer by more than bp items
+                        consumed = self.client.call("gen_wait_consumed", spec["tid"], n - bp + 1)
             return [self._pack_one(rids[0], n)] if rids else []
         if gen == "dynamic":
             refs = []
@@ -521,11 +526,16 @@ class Worker:
                         # stream each item to the caller as the coroutine produces it
                         loop = asyncio.get_running_loop()
                         n = 0
+                        bp = int(spec.get("gen_backpressure") or 0)
+                        consumed = 0
                         async for x in value:
                             oid = new_id()
                             r = await loop.run_in_executor(None, self._pack_one, oid, x)
                             self.client.send((P.GEN_ITEM, spec["tid"], n, r + (oid,)))
                             n += 1
+                            if bp and n - consumed >= bp:
+                                consumed = await loop.run_in_executor(None, self.client.call, "gen_wait_consumed",
+                                                                      spec["tid"], n - bp + 1)
                         value = iter(())
                         spec = dict(spec, _streamed=n)
                     else:

@@ -159,6 +159,10 @@ class ActorClass:
             "class_meta": meta, "max_retries": 0,
         }
         spec["actor_name"] = name
+        if opts.get("label_selector"):
+            from .util.scheduling_strategies import normalize_label_selector
+
+            spec["label_selector"] = normalize_label_selector(opts["label_selector"])
         if fid not in core.registered_functions:
             spec["fblob"] = self._blob
             core.registered_functions.add(fid)
@@ -303,6 +307,9 @@ class ActorHandle:
             "max_task_retries": mo.get("max_task_retries", self._meta.get("max_task_retries", 0)),
             "concurrency_group": mo.get("concurrency_group"),
         }
+        bp = int(mo.get("_generator_backpressure_num_objects") or 0)
+        if generator == "streaming" and bp > 0:
+            spec["gen_backpressure"] = bp
         refs = [ObjectRef(r, _register=False) for r in rids]
         with core._ref_lock:
             for r in rids:

@@ -63,7 +63,10 @@ def build_strategy(opts: dict):
         return {"kind": "pg", "pg_id": s.placement_group.id.binary(), "bundle_index": -1 if idx is None else idx,
                 "capture": bool(s.placement_group_capture_child_tasks)}
     if isinstance(s, NodeLabelSchedulingStrategy):
-        return {"kind": "default"}
+        from .util.scheduling_strategies import normalize_label_selector
+
+        # hard constraints are enforced; soft preferences are not ranked (placement as DEFAULT)
+        return {"kind": "labels", "hard": normalize_label_selector(s.hard)}
     if isinstance(s, PlacementGroup):
         return {"kind": "pg", "pg_id": s.id.binary(), "bundle_index": -1}
     raise ValueError(f"unsupported scheduling_strategy {s!r}")
@@ -166,6 +169,13 @@ class RemoteFunction:
             "retry_exceptions": opts.get("retry_exceptions", False), "runtime_env": _merge_runtime_env(opts),
             "contained": contained, "generator": generator,
         }
+        bp = int(opts.get("_generator_backpressure_num_objects") or 0)
+        if generator == "streaming" and bp > 0:
+            spec["gen_backpressure"] = bp  # producer pauses with this many items unconsumed
+        if opts.get("label_selector"):
+            from .util.scheduling_strategies import normalize_label_selector
+
+            spec["label_selector"] = normalize_label_selector(opts["label_selector"])
         if fid not in core.registered_functions:
             spec["fblob"] = self._blob
             core.registered_functions.add(fid)

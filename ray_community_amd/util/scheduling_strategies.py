@@ -44,5 +44,33 @@ class NodeLabelSchedulingStrategy:
         self.soft = soft
 
 
+def normalize_label_selector(sel) -> list:
+    """``label_selector`` / ``NodeLabelSchedulingStrategy(hard=...)`` as (key, op, values) clauses
+    the head's scheduler understands. Values: ``"v"`` (equals), ``"!v"`` (not equals),
+    ``"in(a,b)"`` / ``"!in(a,b)"``, or the ``In`` / ``NotIn`` / ``Exists`` / ``DoesNotExist``
+    objects (reference: ``python/ray/util/scheduling_strategies.py``, label selectors)."""
+    out = []
+    for key, v in (sel or {}).items():
+        if isinstance(v, In):
+            out.append((key, "in", [str(x) for x in v.values]))
+        elif isinstance(v, NotIn):
+            out.append((key, "not_in", [str(x) for x in v.values]))
+        elif isinstance(v, Exists) or v is Exists:
+            out.append((key, "exists", []))
+        elif isinstance(v, DoesNotExist) or v is DoesNotExist:
+            out.append((key, "not_exists", []))
+        elif isinstance(v, str):
+            neg = v.startswith("!")
+            body = v[1:] if neg else v
+            if body.startswith("in(") and body.endswith(")"):
+                vals = [x.strip() for x in body[3:-1].split(",") if x.strip()]
+            else:
+                vals = [body]
+            out.append((key, "not_in" if neg else "in", vals))
+        else:
+            raise TypeError(f"label selector value for {key!r} must be a string or In/NotIn/Exists/DoesNotExist")
+    return out
+
+
 SchedulingStrategyT = Union[None, str, PlacementGroupSchedulingStrategy, NodeAffinitySchedulingStrategy,
                             NodeLabelSchedulingStrategy]

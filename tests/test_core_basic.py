@@ -422,3 +422,41 @@ def test_get_timeout_polling_does_not_pile_callbacks(shutdown_only):
     e = core.owned.objs.get(ref._id)
     assert e is None or len(e.callbacks) <= 1
     assert ray.get(ref) == 7
+
+
+def test_streaming_generator_backpressure(shutdown_only, tmp_path):
+    """``_generator_backpressure_num_objects=N``: the producer runs at most N items ahead of the
+    consumer (reference: ``core_worker/generator_waiter.h``); without it, it runs to the end."""
+    import time as _t
+
+    ray.init(num_cpus=2, include_dashboard=False, log_to_driver=False)
+    mark = str(tmp_path / "produced")
+
+    @ray.remote
+    def gen(n, path):
+        for i in range(n):
+            with open(path, "w") as f:
+                f.write(str(i + 1))
+            yield i
+
+    def produced(p):
+        try:
+            return int(open(p).read() or 0)
+        except (OSError, ValueError):
+            return 0
+
+    g = gen.options(_generator_backpressure_num_objects=3).remote(20, mark)
+    got = [ray.get(next(g)) for _ in range(2)]
+    _t.sleep(1.5)
+    assert got == [0, 1]
+    assert produced(mark) <= 2 + 3 + 1, produced(mark)
+    assert [ray.get(r) for r in g] == list(range(2, 20))
+
+    mark2 = str(tmp_path / "produced2")
+    g2 = gen.remote(20, mark2)
+    ray.get(next(g2))
+    deadline = _t.time() + 10
+    while produced(mark2) < 20 and _t.time() < deadline:
+        _t.sleep(0.05)
+    assert produced(mark2) == 20
+    assert [ray.get(r) for r in g2] == list(range(1, 20))

@@ -130,3 +130,39 @@ def test_remove_node_fails_tasks(ray_start_cluster):
     c.remove_node(n)
     with pytest.raises((exc.WorkerCrashedError, exc.RayError)):
         ray.get(r, timeout=20)
+
+
+def test_label_selector_places_tasks_and_actors_on_matching_nodes(ray_start_cluster):
+    """``label_selector`` and ``NodeLabelSchedulingStrategy`` hard constraints: work lands only on
+    nodes whose labels match (equality, negation, in(...), Exists); an unmatched selector keeps
+    the task pending instead of running it anywhere."""
+    from ray_community_amd.util.scheduling_strategies import Exists, In, NodeLabelSchedulingStrategy
+
+    c = ray_start_cluster
+    if True:
+        n_a = c.add_node(num_cpus=2, labels={"accel": "mi355x", "zone": "a"})
+        n_b = c.add_node(num_cpus=2, labels={"accel": "cpu", "zone": "b"})
+
+        @ray.remote(num_cpus=0.5)
+        def where():
+            return ray.get_runtime_context().get_node_id()
+
+        ids_a = {ray.get(where.options(label_selector={"accel": "mi355x"}).remote()) for _ in range(6)}
+        assert ids_a == {n_a.node_id}
+        ids_b = {ray.get(where.options(label_selector={"accel": "!mi355x", "zone": "in(b,c)"}).remote())
+                 for _ in range(6)}
+        assert ids_b == {n_b.node_id}
+        ids_s = {ray.get(where.options(scheduling_strategy=NodeLabelSchedulingStrategy(
+            hard={"zone": In("a"), "accel": Exists()})).remote()) for _ in range(4)}
+        assert ids_s == {n_a.node_id}
+
+        @ray.remote(num_cpus=0.5, label_selector={"zone": "b"})
+        class A:
+            def node(self):
+                return ray.get_runtime_context().get_node_id()
+
+        assert ray.get(A.remote().node.remote()) == n_b.node_id
+        assert "__labelsel" not in str(ray.cluster_resources())
+        pending = where.options(label_selector={"accel": "tpu"}).remote()
+        ready, _ = ray.wait([pending], timeout=1.0)
+        assert not ready
