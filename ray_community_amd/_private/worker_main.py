@@ -245,7 +245,9 @@ class Worker:
         c.put_index = 0
         if spec.get("gpu_ids") is not None and spec["kind"] != "actor_task":
             self.core.gpu_ids = tuple(spec.get("gpu_ids") or ())
-        self.core.assigned_resources = spec.get("resources") or {}
+        # an actor's methods hold the actor's resources (get_runtime_context().get_assigned_resources())
+        rs = spec if spec["kind"] != "actor_task" else (getattr(self, "actor_spec", None) or spec)
+        self.core.assigned_resources = rs.get("resources") or {}
         # placement group membership: an actor's calls run in the group its creation was placed in
         st = (self.actor_spec if spec["kind"] == "actor_task" and getattr(self, "actor_spec", None) else spec).get(
             "strategy")

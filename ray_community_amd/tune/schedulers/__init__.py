@@ -1,5 +1,6 @@
-"""Trial schedulers (reference: ``python/ray/tune/schedulers``): FIFO, ASHA, HyperBand (async
-successive-halving brackets), MedianStoppingRule, PopulationBasedTraining."""
+"""Trial schedulers (reference: ``python/ray/tune/schedulers``): FIFO, ASHA (asynchronous
+successive halving), synchronous HyperBand (+ the BOHB variant), MedianStoppingRule,
+PopulationBasedTraining (+ replay of its policy log), ResourceChangingScheduler."""
 from __future__ import annotations
 
 import copy
@@ -114,13 +115,114 @@ class AsyncHyperBandScheduler(TrialScheduler):
 ASHAScheduler = AsyncHyperBandScheduler
 
 
-class HyperBandScheduler(AsyncHyperBandScheduler):
-    """HyperBand as multiple asynchronous successive-halving brackets (no synchronous pausing)."""
+class HyperBandScheduler(TrialScheduler):
+    """Synchronous HyperBand (Li et al. 2017; reference ``python/ray/tune/schedulers/hyperband.py``).
+
+    Trials are dealt into brackets s = s_max .. 0 (s_max = floor(log_eta(max_t))); bracket s
+    takes n_s = ceil((s_max + 1) / (s + 1) * eta^s) trials starting at budget r_s = max_t * eta^-s.
+    Each bracket runs successive halving SYNCHRONOUSLY: a trial that reaches the bracket's current
+    milestone is PAUSED (checkpointed, actor released); once every live trial of the (filled)
+    bracket has reached it, the top 1/eta continue to milestone * eta and the rest are stopped.
+    A bracket counts as filled when it holds n_s trials or the searcher has no more trials.
+    """
+
+    manages_paused_trials = True
 
     def __init__(self, time_attr="training_iteration", metric=None, mode=None, max_t=81, reduction_factor=3,
                  stop_last_trials=True):
-        nb = max(1, int(math.log(max_t) / math.log(reduction_factor)) + 1)
-        super().__init__(time_attr, metric, mode, max_t, 1, reduction_factor, brackets=nb)
+        super().__init__(metric, mode)
+        if max_t <= 0 or reduction_factor <= 1:
+            raise ValueError("invalid HyperBand parameters")
+        self.time_attr = time_attr
+        self.max_t = max_t
+        self.eta = reduction_factor
+        self.stop_last_trials = stop_last_trials
+        self.s_max = int(math.floor(math.log(max_t) / math.log(reduction_factor) + 1e-9))
+        self.brackets: List[Dict] = []
+        self._trial_bracket: Dict[str, Dict] = {}
+        self._next_s = self.s_max
+        self.decisions: List[tuple] = []  # (bracket index, milestone, kept ids, stopped ids)
+
+    def _new_bracket(self):
+        s = self._next_s
+        self._next_s = self._next_s - 1 if self._next_s > 0 else self.s_max
+        n = int(math.ceil((self.s_max + 1) / (s + 1) * self.eta ** s))
+        r = self.max_t * self.eta ** (-s)
+        b = {"index": len(self.brackets), "s": s, "n": n, "milestone": max(1.0, r), "trials": [], "live": set(),
+             "reached": {}}
+        self.brackets.append(b)
+        return b
+
+    def on_trial_add(self, controller, trial):
+        b = self.brackets[-1] if self.brackets and len(self.brackets[-1]["trials"]) < self.brackets[-1]["n"] else \
+            self._new_bracket()
+        b["trials"].append(trial.trial_id)
+        b["live"].add(trial.trial_id)
+        self._trial_bracket[trial.trial_id] = b
+
+    def _filled(self, controller, b) -> bool:
+        return len(b["trials"]) >= b["n"] or getattr(controller, "searcher_done", False)
+
+    def on_trial_result(self, controller, trial, result):
+        t = result.get(self.time_attr)
+        b = self._trial_bracket.get(trial.trial_id)
+        if t is None or b is None:
+            return self.CONTINUE
+        if t >= self.max_t:
+            b["live"].discard(trial.trial_id)
+            return self.STOP if self.stop_last_trials else self.CONTINUE
+        if t < b["milestone"]:
+            return self.CONTINUE
+        s = self._score(result)
+        b["reached"][trial.trial_id] = -math.inf if s is None else s
+        decision = self._maybe_halve(controller, b, current=trial.trial_id)
+        return decision if decision is not None else self.PAUSE
+
+    def on_trial_complete(self, controller, trial, result):
+        b = self._trial_bracket.get(trial.trial_id)
+        if b is not None:
+            b["live"].discard(trial.trial_id)
+            b["reached"].pop(trial.trial_id, None)
+            self._maybe_halve(controller, b)
+
+    def on_trial_error(self, controller, trial):
+        self.on_trial_complete(controller, trial, None)
+
+    def _maybe_halve(self, controller, b, current=None):
+        """Run successive halving on bracket ``b`` if every live trial reached its milestone.
+        Returns the decision for ``current`` (the trial whose result triggered it), if any."""
+        if not b["live"] or not self._filled(controller, b) or not set(b["live"]) <= set(b["reached"]):
+            return None
+        ranked = sorted(b["live"], key=lambda tid: b["reached"][tid], reverse=True)
+        k = max(1, int(len(ranked) // self.eta))
+        keep, cut = ranked[:k], ranked[k:]
+        self.decisions.append((b["index"], b["milestone"], list(keep), list(cut)))
+        b["milestone"] = min(self.max_t, b["milestone"] * self.eta)
+        b["reached"] = {}
+        b["live"] = set(keep)
+        out = None
+        for tid in keep:
+            if tid == current:
+                out = self.CONTINUE
+            else:
+                tr = controller.get_trial(tid)
+                if tr is not None:
+                    controller.unpause(tr)
+        for tid in cut:
+            if tid == current:
+                out = self.STOP
+            else:
+                tr = controller.get_trial(tid)
+                if tr is not None:
+                    controller.stop_paused(tr)
+        return out
+
+    def choose_trial_to_run(self, controller):
+        # the searcher ran dry: brackets that will never fill are halved with what they have
+        if getattr(controller, "searcher_done", False):
+            for b in self.brackets:
+                self._maybe_halve(controller, b)
+        return None
 
 
 class MedianStoppingRule(TrialScheduler):
@@ -177,6 +279,7 @@ class PopulationBasedTraining(TrialScheduler):
         self.factors = perturbation_factors
         self.custom_explore_fn = custom_explore_fn
         self.last_perturb: Dict[str, float] = {}
+        self.log_config = log_config
         self.scores: Dict[str, float] = {}
         self.num_perturbations = 0
         self._rng = random.Random(seed)
@@ -212,6 +315,23 @@ class PopulationBasedTraining(TrialScheduler):
         finally:
             self.mutations = saved
 
+    def _log_policy(self, controller, trial, donor, new_cfg):
+        """One JSON line per exploit in ``pbt_policy_<trial_id>.txt`` (what
+        PopulationBasedTrainingReplay reads back)."""
+        import json
+        import os
+
+        d = getattr(controller, "exp_dir", None)
+        if not d or not self.log_config:
+            return
+        row = [donor.trial_id, trial.trial_id, donor.last_result.get(self.time_attr, 0),
+               trial.last_result.get(self.time_attr, 0), donor.config, new_cfg]
+        try:
+            with open(os.path.join(d, f"pbt_policy_{trial.trial_id}.txt"), "a") as f:
+                f.write(json.dumps(row, default=str) + "\n")
+        except OSError:
+            pass
+
     def on_trial_result(self, controller, trial, result):
         t = result.get(self.time_attr)
         s = self._score(result)
@@ -237,30 +357,71 @@ class PopulationBasedTraining(TrialScheduler):
             if donor is not None and donor.checkpoint is not None:
                 new_cfg = self._explore(donor.config)
                 self.num_perturbations += 1
+                self._log_policy(controller, trial, donor, new_cfg)
                 controller.exploit(trial, donor, new_cfg)
                 return self.NOOP
         return self.CONTINUE
 
 
-class PopulationBasedTrainingReplay(TrialScheduler):  # pragma: no cover
-    pass
+class PopulationBasedTrainingReplay(TrialScheduler):
+    """Replays the hyperparameter schedule one trial followed in a PBT run (reference
+    ``pbt.py`` ``PopulationBasedTrainingReplay``): the policy log PBT writes for every exploit
+    (``pbt_policy_<trial_id>.txt`` in the experiment directory, one JSON line per change:
+    ``[old_trial, new_trial, old_step, new_step, old_config, new_config]``) becomes a list of
+    (step, config) changes. The replayed trial starts from the first logged config and, when its
+    ``time_attr`` reaches a change point, is checkpointed and restarted with that config."""
+
+    def __init__(self, policy_file: str, time_attr: str = "training_iteration"):
+        super().__init__()
+        import json
+
+        self.time_attr = time_attr
+        with open(policy_file) as f:
+            rows = [json.loads(l) for l in f if l.strip()]
+        if not rows:
+            raise ValueError(f"policy file {policy_file} holds no PBT changes")
+        self.config = dict(rows[0][4])
+        self._changes = [(int(r[3]), dict(r[5])) for r in rows]
+        self._i = 0
+        self.applied: List[tuple] = []
+
+    def on_trial_add(self, controller, trial):
+        trial.config = dict(self.config)
+
+    def on_trial_result(self, controller, trial, result):
+        t = result.get(self.time_attr)
+        if t is None or self._i >= len(self._changes):
+            return self.CONTINUE
+        step, cfg = self._changes[self._i]
+        if t < step:
+            return self.CONTINUE
+        self._i += 1
+        self.applied.append((t, cfg))
+        controller.restart(trial, new_config=cfg)
+        return self.NOOP
 
 
 class HyperBandForBOHB(HyperBandScheduler):
-    """HyperBand variant paired with a BOHB searcher in the reference (``hb_bohb.py``); the
-    successive-halving rungs are the same as HyperBand's here."""
+    """Synchronous HyperBand paired with the ``TuneBOHB`` searcher (reference ``hb_bohb.py``): the
+    searcher sees every milestone result with its budget (``time_attr``), so its model is fitted
+    on the largest budget that has enough observations."""
 
 
 class ResourceChangingScheduler(TrialScheduler):
-    """Wraps a base scheduler and, on each result, asks ``resources_allocation_function(controller,
-    trial, result, scheduler)`` for new trial resources (reference ``resource_changing_scheduler.py``).
-    The new request is recorded on the trial (``trial.resources``) and applies from its next start."""
+    """Wraps a base scheduler; on each result ``resources_allocation_function(controller, trial,
+    result, scheduler)`` may return new trial resources (a dict or a ``PlacementGroupFactory``;
+    reference ``resource_changing_scheduler.py``). A change checkpoints the trial and restarts it
+    from that checkpoint in a trial actor of the new size."""
 
     def __init__(self, base_scheduler: Optional[TrialScheduler] = None, resources_allocation_function=None):
         super().__init__()
         self.base = base_scheduler or FIFOScheduler()
         self.fn = resources_allocation_function
         self.changes: List[tuple] = []
+
+    @property
+    def manages_paused_trials(self):
+        return getattr(self.base, "manages_paused_trials", False)
 
     def set_search_properties(self, metric, mode, **spec):
         self.metric, self.mode = metric, mode
@@ -270,14 +431,19 @@ class ResourceChangingScheduler(TrialScheduler):
         return self.base.on_trial_add(controller, trial)
 
     def on_trial_result(self, controller, trial, result):
-        if self.fn is not None:
-            new = self.fn(controller, trial, result, self)
-            if new is not None:
-                res = getattr(new, "required_resources", new)
-                if dict(res) != dict(getattr(trial, "resources", {}) or {}):
-                    trial.resources = dict(res)
-                    self.changes.append((getattr(trial, "trial_id", None), dict(res)))
-        return self.base.on_trial_result(controller, trial, result)
+        decision = self.base.on_trial_result(controller, trial, result)
+        if decision != self.CONTINUE or self.fn is None:
+            return decision
+        new = self.fn(controller, trial, result, self)
+        if new is None:
+            return decision
+        res = getattr(new, "required_resources", new)
+        res = {k: v for k, v in dict(res).items() if v}
+        if res != {k: v for k, v in dict(getattr(trial, "resources", {}) or {}).items() if v}:
+            self.changes.append((getattr(trial, "trial_id", None), dict(res)))
+            controller.restart(trial, new_resources=res)
+            return self.NOOP
+        return decision
 
     def on_trial_complete(self, controller, trial, result):
         return self.base.on_trial_complete(controller, trial, result)
@@ -289,7 +455,7 @@ class ResourceChangingScheduler(TrialScheduler):
         return self.base.choose_trial_to_run(controller)
 
 
-__all__ = ["HyperBandForBOHB", "ResourceChangingScheduler", "TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
+__all__ = ["HyperBandForBOHB", "ResourceChangingScheduler", "PopulationBasedTrainingReplay", "TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler", "HyperBandScheduler",
            "MedianStoppingRule", "PopulationBasedTraining"]
 
 

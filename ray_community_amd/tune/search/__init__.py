@@ -262,9 +262,13 @@ def __getattr__(name):
         from . import tpe
 
         return getattr(tpe, name)
+    if name == "TuneBOHB":
+        from .bohb import TuneBOHB
+
+        return TuneBOHB
     raise AttributeError(name)
 
 
 __all__ = ["Searcher", "BasicVariantGenerator", "ConcurrencyLimiter", "RandomSearch", "Repeater",
-           "generate_variants", "TPESearch", "OptunaSearch", "HyperOptSearch", "SearchAlgorithm", "SearchGenerator",
+           "generate_variants", "TPESearch", "OptunaSearch", "HyperOptSearch", "TuneBOHB", "SearchAlgorithm", "SearchGenerator",
            "grid_search", "UNDEFINED_SEARCH_SPACE", "UNDEFINED_METRIC_MODE"]

@@ -367,7 +367,7 @@ class TuneController:
         trial.stop_flag = False
         ckpt = trial.checkpoint if trial.restore_path is None else _ckpt(trial.restore_path)
         trial.restore_path = None
-        res = dict(self.resources)
+        res = dict(getattr(trial, "resources", None) or self.resources)
         opts = {"num_cpus": res.pop("CPU", 0), "num_gpus": res.pop("GPU", 0), "resources": res or None,
                 "max_concurrency": 4}
         opts = {k: v for k, v in opts.items() if v is not None}
@@ -500,6 +500,37 @@ class TuneController:
         trial.iteration_offset = trial.last_result.get("training_iteration", 0)
         trial.status = PENDING
 
+    # ------------------------------------------------------------ scheduler hooks
+    def unpause(self, trial: Trial):
+        """A PAUSED trial goes back to PENDING and resumes from its last checkpoint."""
+        if trial.status != PAUSED:
+            return
+        trial.status = PENDING
+        trial.restore_path = trial.checkpoint.path if trial.checkpoint else None
+        trial.iteration_offset = trial.last_result.get("training_iteration", 0) if trial.checkpoint else 0
+
+    def stop_paused(self, trial: Trial):
+        """Terminate a PAUSED trial (e.g. cut by synchronous successive halving)."""
+        if trial.status == PAUSED:
+            self._complete(trial)
+
+    def restart(self, trial: Trial, new_config: Optional[Dict] = None, new_resources: Optional[Dict] = None):
+        """Checkpoint a RUNNING trial, stop it and queue it again with a new config and/or
+        resources (ResourceChangingScheduler, PopulationBasedTrainingReplay); it resumes from that
+        checkpoint in a fresh trial actor sized by ``new_resources``."""
+        self._stop_runner(trial, save=True)
+        if new_config is not None:
+            trial.config = new_config
+        if new_resources is not None:
+            trial.resources = dict(new_resources)
+        trial.status = PENDING
+        trial.restore_path = trial.checkpoint.path if trial.checkpoint else None
+        trial.iteration_offset = trial.last_result.get("training_iteration", 0) if trial.checkpoint else 0
+
+    @property
+    def searcher_done(self) -> bool:
+        return bool(self._searcher_done)
+
     def _should_stop(self, trial, result) -> bool:
         stop = self.rc.stop
         if stop is None:
@@ -587,6 +618,9 @@ class TuneController:
                 self._start(t)
                 running.append(t)
             if not running:
+                # everything left may be PAUSED: let the scheduler (or the generic rule) resume some
+                if self._resume_paused() and any(x.status == PENDING for x in self.trials):
+                    continue
                 if self._searcher_done or all(t.status in (TERMINATED, ERROR) for t in self.trials) and \
                         self._new_trial_blocked():
                     break
@@ -615,15 +649,23 @@ class TuneController:
                         self._complete(t, ev[1])
                         break
             self._save_state()
-            # resume paused trials when nothing else is pending
-            if not any(x.status in (PENDING,) for x in self.trials) and self._searcher_done:
-                for x in self.trials:
-                    if x.status == PAUSED and len([y for y in self.trials if y.status == RUNNING]) < self.max_conc:
-                        x.status = PENDING
-                        x.restore_path = x.checkpoint.path if x.checkpoint else None
-                        x.iteration_offset = x.last_result.get("training_iteration", 0)
+            self._resume_paused()
         self._save_state()
         return self._results()
+
+    def _resume_paused(self) -> bool:
+        """Schedulers that pace trials themselves (synchronous HyperBand) get a hook every pass;
+        for the others, PAUSED trials resume when nothing else is pending. True if any trial
+        is PAUSED."""
+        self.scheduler.choose_trial_to_run(self)
+        if (not getattr(self.scheduler, "manages_paused_trials", False)
+                and not any(x.status in (PENDING,) for x in self.trials) and self._searcher_done):
+            for x in self.trials:
+                if x.status == PAUSED and len([y for y in self.trials if y.status == RUNNING]) < self.max_conc:
+                    x.status = PENDING
+                    x.restore_path = x.checkpoint.path if x.checkpoint else None
+                    x.iteration_offset = x.last_result.get("training_iteration", 0)
+        return any(x.status in (PAUSED, PENDING) for x in self.trials)
 
     def _new_trial_blocked(self):
         return self._searcher_done
