@@ -40,6 +40,8 @@ _SIGS = {
     "rca_sumsq": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "rca_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float, c_float,
                           c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
+    "rca_adamw_split": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float,
+                                c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
     "rca_gae": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                         c_float, c_float, c_int, c_void_p, c_void_p, c_float, c_void_p]),
     "rca_vtrace": (c_int, [c_void_p] * 8 + [c_int, c_int, c_float, c_float, c_float, c_float, c_void_p]),

@@ -52,6 +52,25 @@ def adamw_ref(p, g, m, v, lr, b1, b2, eps, wd, step, grad_mul=1.0, clip=1.0):
     return p
 
 
+def split_master(master):
+    """fp32 master -> (hi, lo): hi = the bit pattern rounded half-up in magnitude to 16 bits (a bf16
+    tensor: the model weight; equal to RNE except at exact ties), lo = the low 16 bits (int16
+    storage). ``join_master(hi, lo)`` reconstructs ``master`` bit-exactly (loss_optim.hip)."""
+    M = master.float().contiguous().view(torch.int32)
+    hi = ((M + 0x8000) >> 16) & 0xFFFF
+    lo = M & 0xFFFF
+    to16 = lambda x: (x - ((x >> 15) << 16)).to(torch.int16)  # 0..65535 -> same 16 bits as int16
+    return to16(hi).view(torch.bfloat16), to16(lo)
+
+
+def join_master(hi, lo):
+    """Inverse of ``split_master``: the fp32 master from the bf16 weight and its low halves."""
+    h = hi.contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
+    l_ = lo.contiguous().to(torch.int32) & 0xFFFF
+    up = h - (l_ >> 15)
+    return ((up << 16) | l_).view(torch.float32)
+
+
 def gae_ref(rewards, values, terminateds, dones, gamma, lam, last_values=None, next_values=None):
     """rewards/values/...: [B, T] -> (advantages, value_targets) in fp64-accurate float32."""
     B, T = rewards.shape

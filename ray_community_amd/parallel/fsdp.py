@@ -34,6 +34,7 @@ import torch.nn as nn
 
 from .. import ops
 from .flat import ALIGN, FlatParameters, register_grad_ready
+from .optim import _use_split
 
 
 class ShardedDataParallel(nn.Module):
@@ -173,7 +174,8 @@ class ShardedAdamW:
     for owned elements only); same update rule as ``FlatAdamW`` / ``torch.optim.AdamW``."""
 
     def __init__(self, sdp: ShardedDataParallel, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
-                 weight_decay: float = 0.1, max_grad_norm: Optional[float] = 1.0, lr_schedule=None):
+                 weight_decay: float = 0.1, max_grad_norm: Optional[float] = 1.0, lr_schedule=None,
+                 master_format: str = "auto"):
         self.sdp = sdp
         flat = sdp.flat
         self.lr, (self.b1, self.b2), self.eps, self.wd = lr, betas, eps, weight_decay
@@ -189,9 +191,19 @@ class ShardedAdamW:
             lo += e - s
         self.local_numel = lo
         dev = flat.device
-        self.master = torch.empty(lo, dtype=torch.float32, device=dev)
-        for _, s, e, o, _ in self.chunks:
-            self.master[o: o + e - s].copy_(flat.data[s:e])
+        # split master (optim.py): the owned chunks' bf16 weights hold the high halves, ``lo`` the
+        # low 16 bits; needs 8-element-aligned chunks for the vector kernel
+        aligned = all(s % 8 == 0 and o % 8 == 0 for _, s, _, o, _ in self.chunks)
+        fmt = master_format if aligned or master_format == "fp32" else ("fp32" if master_format == "auto" else "unaligned")
+        if fmt == "unaligned":
+            raise ValueError("split master format needs 8-element-aligned shard chunks")
+        self.split_master = _use_split(fmt, self.master_weights, flat.data)
+        self.lo = torch.zeros(lo, dtype=torch.int16, device=dev) if self.split_master else None
+        self._master = None
+        if not self.split_master:
+            self._master = torch.empty(lo, dtype=torch.float32, device=dev)
+            for _, s, e, o, _ in self.chunks:
+                self._master[o: o + e - s].copy_(flat.data[s:e])
         self.m = torch.zeros(lo, dtype=torch.float32, device=dev)
         self.v = torch.zeros(lo, dtype=torch.float32, device=dev)
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -203,6 +215,17 @@ class ShardedAdamW:
 
     def current_lr(self) -> float:
         return self.lr_schedule(self.step_count) if self.lr_schedule else self.lr
+
+    def _hi_local(self) -> torch.Tensor:
+        flat = self.sdp.flat
+        return torch.cat([flat.data[s:e] for _, s, e, _, _ in self.chunks]) if self.chunks else flat.data[:0]
+
+    @property
+    def master(self) -> torch.Tensor:
+        """fp32 master of the owned elements (split format: reconstructed, a fresh tensor)."""
+        if self.split_master:
+            return ops.reference.join_master(self._hi_local(), self.lo)
+        return self._master
 
     @torch.no_grad()
     def step(self, grad_scale: Optional[float] = None):
@@ -231,8 +254,17 @@ class ShardedAdamW:
                     if g.dtype not in (torch.bfloat16, torch.float32):
                         raise TypeError(f"unsupported grad dtype {g.dtype}")
                     gdt = 0 if g.dtype == torch.bfloat16 else 1
+                    if self.split_master:
+                        check(lib().rca_adamw_split(flat.data.data_ptr() + s * 2, self.lo.data_ptr() + o * 2,
+                                                    g.data_ptr() + s * g.element_size(), gdt,
+                                                    self.m.data_ptr() + o * 4, self.v.data_ptr() + o * 4, n, lr,
+                                                    self.b1, self.b2, self.eps, wd, bc1, bc2, grad_scale,
+                                                    self._sumsq.data_ptr() if clip else 0, float(clip),
+                                                    stream_ptr(g.device)), "adamw_split")
+                        sdp.launch_all_gather(bi)
+                        continue
                     p16 = flat.data.data_ptr() + s * flat.data.element_size() if self.master_weights else 0
-                    mp = self.master.data_ptr() + o * 4
+                    mp = self._master.data_ptr() + o * 4 if self.master_weights else 0
                     if not self.master_weights:  # fp32 model: update the flat data in place
                         mp = flat.data.data_ptr() + s * 4
                     check(lib().rca_adamw(mp, p16, g.data_ptr() + s * g.element_size(), gdt,
@@ -245,10 +277,17 @@ class ShardedAdamW:
                     if clip:
                         nrm = math.sqrt(float(self._sumsq)) * abs(grad_scale)
                         coef = min(1.0, clip / (nrm + 1e-6))
-                    master = self.master[o: o + n] if self.master_weights else flat.data[s:e]
+                    if self.split_master:
+                        master = ops.reference.join_master(flat.data[s:e], self.lo[o: o + n])
+                    else:
+                        master = self._master[o: o + n] if self.master_weights else flat.data[s:e]
                     ops.reference.adamw_ref(master, g[s:e], self.m[o: o + n], self.v[o: o + n], lr, self.b1, self.b2,
                                             self.eps, wd, t, grad_mul=grad_scale, clip=coef)
-                    if self.master_weights:
+                    if self.split_master:
+                        hi, lo_ = ops.reference.split_master(master)
+                        flat.data[s:e].copy_(hi)
+                        self.lo[o: o + n].copy_(lo_)
+                    elif self.master_weights:
                         flat.data[s:e].copy_(master.to(flat.dtype))
             sdp.launch_all_gather(bi)
 
@@ -269,10 +308,17 @@ class ShardedAdamW:
         self.step_count = sd["step"]
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
-        self.master.copy_(sd["master"])
         flat = self.sdp.flat
+        master = sd["master"].to(flat.device)
         with torch.no_grad():
+            if self.split_master:
+                hi, lo = ops.reference.split_master(master)
+                self.lo.copy_(lo)
+            elif self._master is not None:
+                self._master.copy_(master)
             for bi, s, e, o, _ in self.chunks:
-                if self.master_weights:
-                    flat.data[s:e].copy_(self.master[o: o + e - s].to(flat.dtype))
+                if self.split_master:
+                    flat.data[s:e].copy_(hi[o: o + e - s])
+                elif self.master_weights:
+                    flat.data[s:e].copy_(master[o: o + e - s].to(flat.dtype))
                 self.sdp.launch_all_gather(bi)

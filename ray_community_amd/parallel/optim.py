@@ -5,10 +5,16 @@ One HIP kernel launch per weight-decay group streams (fp32 master, bf16/f32 grad
 global-norm clipping (norm read from device memory) are folded into the same pass, so the
 step needs no host synchronisation and no extra elementwise passes.
 Works on any ``FlatParameters`` (CPU tensors use the PyTorch reference math).
+
+Master format (``master_format``): "split" (the GPU bf16 default) keeps only the LOW 16 bits of
+each fp32 master beside the bf16 model weight, which holds the high half rounded (the pair
+reconstructs the master bit-exactly; ``ops.reference.split_master``): 26 instead of 28 B of HBM
+traffic per parameter per step and 2 B/param less memory. "fp32" keeps a separate fp32 master.
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -21,7 +27,7 @@ from .flat import FlatParameters
 class FlatAdamW:
     def __init__(self, flat: FlatParameters, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, max_grad_norm: Optional[float] = 1.0, master_weights: bool = True,
-                 lr_schedule=None):
+                 lr_schedule=None, master_format: str = "auto"):
         self.flat = flat
         self.lr = lr
         self.b1, self.b2 = betas
@@ -32,7 +38,9 @@ class FlatAdamW:
         self.step_count = 0
         dev = flat.device
         self.master_weights = master_weights and flat.dtype != torch.float32
-        self.master = flat.data.float() if self.master_weights else flat.data
+        self.split_master = _use_split(master_format, self.master_weights, flat.data)
+        self.lo = torch.zeros(flat.numel, dtype=torch.int16, device=dev) if self.split_master else None
+        self._master = None if self.split_master else (flat.data.float() if self.master_weights else flat.data)
         self.m = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
         self.v = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -104,10 +112,19 @@ class FlatAdamW:
     def current_lr(self) -> float:
         return self.lr_schedule(self.step_count) if self.lr_schedule else self.lr
 
+    @property
+    def master(self) -> torch.Tensor:
+        """The fp32 master weights (with the split format: reconstructed, a fresh tensor)."""
+        if self.split_master:
+            return ops.reference.join_master(self.flat.data, self.lo)
+        return self._master
+
     def sync_master(self):
         """Re-read model weights into the fp32 master copy (after load_state_dict)."""
-        if self.master_weights:
-            self.master.copy_(self.flat.data.float())
+        if self.split_master:
+            self.lo.zero_()
+        elif self.master_weights:
+            self._master.copy_(self.flat.data.float())
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0):
@@ -158,13 +175,18 @@ class FlatAdamW:
             if clip:
                 nrm = math.sqrt(float(self._sumsq)) * abs(grad_scale)
                 coef = min(1.0, clip / (nrm + 1e-6))
+            master = self.master
             for s, e, wd in segs:
                 if e <= s:
                     continue
-                ops.reference.adamw_ref(self.master[s:e], g[s:e], self.m[s:e], self.v[s:e], lr, self.b1, self.b2,
+                ops.reference.adamw_ref(master[s:e], g[s:e], self.m[s:e], self.v[s:e], lr, self.b1, self.b2,
                                         self.eps, wd, t, grad_mul=grad_scale, clip=coef)
-            if self.master_weights:
-                flat.data.copy_(self.master.to(flat.dtype))
+            if self.split_master:
+                hi, lo = ops.reference.split_master(master)
+                flat.data.copy_(hi)
+                self.lo.copy_(lo)
+            elif self.master_weights:
+                flat.data.copy_(master.to(flat.dtype))
 
     def _launch(self, g, s, e, wd, lr, bc1, bc2, grad_scale, clip, st):
         n = e - s
@@ -172,8 +194,15 @@ class FlatAdamW:
             return
         flat = self.flat
         gdt = 0 if g.dtype == torch.bfloat16 else 1
+        if self.split_master:
+            check(lib().rca_adamw_split(flat.data.data_ptr() + s * 2, self.lo.data_ptr() + s * 2,
+                                        g.data_ptr() + s * g.element_size(), gdt, self.m.data_ptr() + s * 4,
+                                        self.v.data_ptr() + s * 4, n, lr, self.b1, self.b2, self.eps, wd, bc1, bc2,
+                                        grad_scale, self._sumsq.data_ptr() if clip else 0, float(clip), st),
+                  "adamw_split")
+            return
         p16 = flat.data.data_ptr() + s * flat.data.element_size() if self.master_weights else 0
-        check(lib().rca_adamw(self.master.data_ptr() + s * self.master.element_size(), p16,
+        check(lib().rca_adamw(self._master.data_ptr() + s * self._master.element_size(), p16,
                               g.data_ptr() + s * g.element_size(), gdt, self.m.data_ptr() + s * 4,
                               self.v.data_ptr() + s * 4, n, lr, self.b1, self.b2, self.eps, wd, bc1, bc2, grad_scale,
                               self._sumsq.data_ptr() if clip else 0, float(clip), st), "adamw")
@@ -206,8 +235,25 @@ class FlatAdamW:
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         if self.master_weights and sd.get("master") is not None:
-            self.master.copy_(sd["master"])
-            self.flat.data.copy_(self.master.to(self.flat.dtype))
+            if self.split_master:
+                hi, lo = ops.reference.split_master(sd["master"].to(self.flat.device))
+                self.flat.data.copy_(hi)
+                self.lo.copy_(lo)
+            else:
+                self._master.copy_(sd["master"])
+                self.flat.data.copy_(self._master.to(self.flat.dtype))
+
+
+def _use_split(master_format: str, master_weights: bool, data: torch.Tensor) -> bool:
+    """"auto": the split master on GPU bf16 models; "split" / "fp32" force the choice."""
+    if master_format not in ("auto", "split", "fp32"):
+        raise ValueError(f"master_format must be auto|split|fp32, got {master_format!r}")
+    ok = master_weights and data.dtype == torch.bfloat16
+    if master_format == "split" and not ok:
+        raise ValueError("the split master format needs bf16 model weights with master_weights=True")
+    if master_format == "auto":
+        return ok and data.is_cuda and os.environ.get("RCA_ADAMW_SPLIT", "1") != "0"
+    return master_format == "split"
 
 
 class FlatSGD:

@@ -22,6 +22,7 @@ class Algorithm(Trainable):
     _default_config_cls = AlgorithmConfig
     multi_agent = False      # set in setup() from the config
     learner_groups = None
+    _supports_lstm = False   # recurrent RLModules (model.use_lstm): PPO
 
     def __init__(self, config: Optional[AlgorithmConfig] = None, env=None, **kw):
         if isinstance(config, dict):
@@ -47,7 +48,10 @@ class Algorithm(Trainable):
         cfg = self.config
         rd = cfg.runner_dict()
         rd.update(self._runner_extra())
+        rd["_algo"] = "PPO" if self._supports_lstm else type(self).__name__
         self.multi_agent = cfg.is_multi_agent
+        if self.multi_agent and (cfg.model or {}).get("use_lstm"):
+            raise ValueError("use_lstm is supported for single-agent PPO only")
         runner_cls = EnvRunner
         if self.multi_agent:
             from ..env.multi_agent_env_runner import MultiAgentEnvRunner
@@ -67,7 +71,9 @@ class Algorithm(Trainable):
         from ..core.learner import LearnerGroup
 
         ld = cfg.to_dict()
+        ld.update(cfg._connector_dict())
         ld.update(self._runner_extra())
+        ld["_algo"] = rd["_algo"]
         if self.multi_agent:
             # one learner group (RLModule + optimizer, possibly several GPU learners) per policy
             sp = self.local_runner.spaces()
@@ -102,6 +108,22 @@ class Algorithm(Trainable):
         if self.remote_runners:
             ref = put(st)
             get([r.set_weights.remote(ref, self._weights_version) for r in self.remote_runners])
+        self._sync_connector_states()
+
+    def _sync_connector_states(self):
+        """Merge every env runner's env-to-module connector state (e.g. MeanStdFilter statistics)
+        and broadcast the merged state back (reference: ``EnvRunnerGroup.sync_env_runner_states``)."""
+        from ..._private.worker import get
+
+        if self.multi_agent or not getattr(self.local_runner, "has_stateful_connectors", False):
+            return
+        states = [self.local_runner.get_connector_state()]
+        if self.remote_runners:
+            states += get([r.get_connector_state.remote() for r in self.remote_runners])
+        merged = self.local_runner.env_to_module.merge_states(states)
+        self.local_runner.set_connector_state(merged)
+        if self.remote_runners:
+            get([r.set_connector_state.remote(merged) for r in self.remote_runners])
 
     def _sample_fragments(self, steps_total: int) -> List[SampleBatch]:
         from ..._private.worker import get
@@ -214,8 +236,20 @@ class Algorithm(Trainable):
                 "env_runners": {"episode_return_mean": float(np.mean(rets)) if rets else float("nan")},
                 "num_episodes": len(eps)}
 
-    def compute_single_action(self, observation, explore: bool = False, policy_id=None, **kw):
+    def compute_single_action(self, observation, state=None, explore: bool = False, policy_id=None, **kw):
+        """One action for one observation. Recurrent modules: pass ``state`` (None = initial) and
+        get ``(action, state_out, {})`` back, as in the reference API."""
         obs = torch.as_tensor(np.asarray(observation)[None])
+        m0 = self.local_runner.module if not self.multi_agent else None
+        if m0 is not None and getattr(m0, "is_stateful", False):
+            m0.set_state(self.learner_group.get_weights())
+            st = m0.get_initial_state(1) if state is None else torch.as_tensor(np.asarray(state))[None].float()
+            if explore:
+                a, _, _, _, st2 = m0.forward_exploration_step(obs, st)
+            else:
+                a, _, st2 = m0.forward_inference_step(obs, st)
+            a = a[0].numpy()
+            return (int(a) if a.ndim == 0 else a), st2[0].numpy(), {}
         if self.multi_agent:
             pid = policy_id or next(iter(self.learner_groups))
             m = self.local_runner.modules[pid]

@@ -26,6 +26,13 @@ class AlgorithmConfig:
         self.num_cpus_per_env_runner = 1
         self.num_gpus_per_env_runner = 0  # > 0: the runner's RLModule runs its inference on that GPU share
         self.explore = True
+        self.normalize_actions = False       # module acts in [-1, 1]; unsquashed to the Box bounds
+        self.clip_actions = False
+        self.add_default_connectors_to_env_to_module_pipeline = True
+        # ConnectorV2 factories (callables; kept out of to_dict / checkpoints)
+        self._env_to_module_connector = None  # (env) -> connector | [connectors]
+        self._module_to_env_connector = None  # (env) -> connector | [connectors]
+        self._learner_connector = None        # (obs_space, act_space) -> connector | [connectors]
         # training
         self.gamma = 0.99
         self.lr = 0.001
@@ -64,13 +71,31 @@ class AlgorithmConfig:
         return self
 
     def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None, rollout_fragment_length=None,
-                    batch_mode=None, num_cpus_per_env_runner=None, num_gpus_per_env_runner=None, explore=None, **kw):
+                    batch_mode=None, num_cpus_per_env_runner=None, num_gpus_per_env_runner=None, explore=None,
+                    env_to_module_connector=None, module_to_env_connector=None,
+                    add_default_connectors_to_env_to_module_pipeline=None, normalize_actions=None,
+                    clip_actions=None, **kw):
+        """``env_to_module_connector(env)`` / ``module_to_env_connector(env)``: return a ConnectorV2,
+        a list of them or a pipeline (rllib/connectors)."""
         for k, v in dict(num_env_runners=num_env_runners, num_envs_per_env_runner=num_envs_per_env_runner,
                          rollout_fragment_length=rollout_fragment_length, batch_mode=batch_mode,
                          num_cpus_per_env_runner=num_cpus_per_env_runner,
-                         num_gpus_per_env_runner=num_gpus_per_env_runner, explore=explore).items():
+                         num_gpus_per_env_runner=num_gpus_per_env_runner, explore=explore,
+                         add_default_connectors_to_env_to_module_pipeline=add_default_connectors_to_env_to_module_pipeline,
+                         normalize_actions=normalize_actions, clip_actions=clip_actions).items():
             if v is not None:
                 setattr(self, k, v)
+        if env_to_module_connector is not None:
+            self._env_to_module_connector = env_to_module_connector
+        if module_to_env_connector is not None:
+            self._module_to_env_connector = module_to_env_connector
+        unknown = set(kw) - {"sample_timeout_s", "num_gpus_per_env_runner", "create_env_on_local_worker",
+                             "observation_filter", "compress_observations", "remote_worker_envs",
+                             "remote_env_batch_wait_ms", "validate_env_runners_after_construction",
+                             "episode_lookback_horizon", "use_worker_filter_stats", "update_worker_filter_stats",
+                             "gym_env_vectorize_mode"}
+        if unknown:
+            raise TypeError(f"env_runners() got unsupported argument(s) {sorted(unknown)}")
         return self
 
     def rollouts(self, *, num_rollout_workers=None, num_envs_per_worker=None, rollout_fragment_length=None,
@@ -79,7 +104,12 @@ class AlgorithmConfig:
                                 rollout_fragment_length=rollout_fragment_length, batch_mode=batch_mode)
 
     def training(self, **kw):
+        """Algorithm hyperparameters; ``learner_connector(obs_space, act_space)`` returns learner
+        ConnectorV2 piece(s) run on the train batch before the loss."""
         aliases = {"sgd_minibatch_size": "minibatch_size", "num_sgd_iter": "num_epochs", "lambda": "lambda_"}
+        if kw.get("learner_connector") is not None:
+            self._learner_connector = kw.pop("learner_connector")
+        kw.pop("learner_connector", None)
         for k, v in kw.items():
             k = aliases.get(k, k)
             if k == "model" and v is not None:
@@ -229,4 +259,10 @@ class AlgorithmConfig:
         d = self.to_dict()
         d["rollout_fragment_length"] = self.get_rollout_fragment_length()
         d["callbacks_class"] = getattr(self, "_callbacks", None)
+        d.update(self._connector_dict())
         return d
+
+    def _connector_dict(self) -> Dict:
+        return {"env_to_module_connector": self._env_to_module_connector,
+                "module_to_env_connector": self._module_to_env_connector,
+                "learner_connector": self._learner_connector}

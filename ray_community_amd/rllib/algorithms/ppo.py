@@ -37,6 +37,7 @@ class PPOConfig(AlgorithmConfig):
 
 class PPO(Algorithm):
     _default_config_cls = PPOConfig
+    _supports_lstm = True
 
     @classmethod
     def get_default_config(cls):

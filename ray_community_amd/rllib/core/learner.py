@@ -49,9 +49,12 @@ class Learner:
         self.kl_coeff = config.get("kl_coeff", 0.2)
         self.target = None
         self.num_updates = 0
+        from ..connectors import build_learner_connector
 
-    def forward(self, obs):
-        return (self.ddp or self.module)(obs)
+        self.learner_connector = build_learner_connector(config, obs_space, act_space)
+
+    def forward(self, obs, *args):
+        return (self.ddp or self.module)(obs, *args)
 
     def get_weights(self):
         return self.module.get_state()
@@ -120,11 +123,15 @@ class Learner:
         t0 = time.perf_counter()
         b = _to_device_batch(batch, self.device)
         N, T = b.fragment_shape
+        if len(self.learner_connector):
+            b = self.learner_connector(rl_module=self.module, batch=b, episodes=None, shared_data={})
         rew, vf, nvf = b["rewards"], b["vf_preds"], b["next_vf_preds"]
         term, trunc = b["terminateds"], b["truncateds"]
         done = term | trunc
         gamma, lam = cfg.get("gamma", 0.99), cfg.get("lambda_", 1.0)
-        if cfg.get("use_gae", True):
+        if "advantages" in b and "value_targets" in b:  # a learner connector (GeneralAdvantageEstimation) made them
+            adv, vt = b["advantages"].float(), b["value_targets"].float()
+        elif cfg.get("use_gae", True):
             adv, vt = ops.compute_gae(rew, vf, term, done, gamma, lam, next_values=nvf, standardize=False)
         else:
             adv, vt = ops.compute_gae(rew, torch.zeros_like(vf), term, done, gamma, 1.0,
@@ -162,35 +169,43 @@ class Learner:
         def mean(x, w):
             return x.mean() if w is None else (x * w).sum() / w.sum().clamp(min=1.0)
 
-        for _ in range(epochs):
-            perm = torch.randperm(n, device=self.device, generator=gen)
-            for i in range(0, n - mb + 1, mb):
-                idx = perm[i: i + mb]
-                w = mask[idx] if mask is not None else None
-                logits, v = self.forward(obs[idx])
-                d = self.module.dist(logits)
-                lp = d.logp(act[idx])
-                ratio = torch.exp(lp - old_logp[idx])
-                a_mb = adv[idx]
-                surr = torch.min(ratio * a_mb, ratio.clamp(1 - clip, 1 + clip) * a_mb)
-                vf_err = (v - vt[idx]) ** 2
-                vf_loss = vf_err.clamp(0, vclip) if vclip else vf_err
-                ent = d.entropy()
-                pi_term, vf_term, ent_term = mean(surr, w), mean(vf_loss, w), mean(ent, w)
-                loss = -pi_term + vf_coeff * vf_term - ent_coeff * ent_term
-                if use_kl:
-                    kl = mean(self.module.dist(old_logits[idx]).kl(d), w)
-                    if self.kl_coeff > 0:
-                        loss = loss + self.kl_coeff * kl
-                else:
-                    kl = torch.zeros((), device=self.device)
-                self._step(loss)
-                stats["policy_loss"] += -pi_term.detach()
-                stats["vf_loss"] += vf_term.detach()
-                stats["entropy"] += ent_term.detach()
-                stats["mean_kl"] += kl.detach()
-                stats["total_loss"] += loss.detach()
-                count += 1
+        if getattr(self.module, "is_stateful", False):
+            minibatches = self._recurrent_minibatches(b, N, T, obs, act, old_logp, adv, vt, old_logits, mask, mb,
+                                                      epochs, gen)
+        else:
+            def minibatches():
+                for _ in range(epochs):
+                    perm = torch.randperm(n, device=self.device, generator=gen)
+                    for i in range(0, n - mb + 1, mb):
+                        idx = perm[i: i + mb]
+                        logits, v = self.forward(obs[idx])
+                        yield (logits, v, act[idx], old_logp[idx], adv[idx], vt[idx],
+                               old_logits[idx] if old_logits is not None else None,
+                               mask[idx] if mask is not None else None)
+
+        for logits, v, act_mb, olp_mb, a_mb, vt_mb, olg_mb, w in minibatches():
+            d = self.module.dist(logits)
+            lp = d.logp(act_mb)
+            ratio = torch.exp(lp - olp_mb)
+            surr = torch.min(ratio * a_mb, ratio.clamp(1 - clip, 1 + clip) * a_mb)
+            vf_err = (v - vt_mb) ** 2
+            vf_loss = vf_err.clamp(0, vclip) if vclip else vf_err
+            ent = d.entropy()
+            pi_term, vf_term, ent_term = mean(surr, w), mean(vf_loss, w), mean(ent, w)
+            loss = -pi_term + vf_coeff * vf_term - ent_coeff * ent_term
+            if use_kl:
+                kl = mean(self.module.dist(olg_mb).kl(d), w)
+                if self.kl_coeff > 0:
+                    loss = loss + self.kl_coeff * kl
+            else:
+                kl = torch.zeros((), device=self.device)
+            self._step(loss)
+            stats["policy_loss"] += -pi_term.detach()
+            stats["vf_loss"] += vf_term.detach()
+            stats["entropy"] += ent_term.detach()
+            stats["mean_kl"] += kl.detach()
+            stats["total_loss"] += loss.detach()
+            count += 1
         keys = list(stats)
         vec = torch.stack([torch.as_tensor(stats[k], device=self.device, dtype=torch.float64) for k in keys])
         vec = vec / max(count, 1)
@@ -211,6 +226,45 @@ class Learner:
         out.update({"kl_coeff": self.kl_coeff, "vf_explained_var": float(ev), "num_minibatches": count,
                     "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr()})
         return out
+
+    def _recurrent_minibatches(self, b, N, T, obs, act, old_logp, adv, vt, old_logits, mask, mb, epochs, gen):
+        """Recurrent PPO: the ``[N, T]`` fragments are cut into ``max_seq_len`` chunks (the tail
+        padded and masked out), each replayed from the state its first step entered with
+        (``state_in``) and reset where ``is_first`` marks a new episode inside the chunk.
+        Minibatches are ``minibatch_size // max_seq_len`` whole chunks."""
+        L = int(self.module.max_seq_len)
+        nch = -(-T // L)
+        Tp = nch * L
+        S = N * nch
+
+        def chunk(x):  # [N * T, ...] -> [S, L, ...] (tail zero-padded)
+            x = x.reshape((N, T) + tuple(x.shape[1:]))
+            if Tp != T:
+                pad = torch.zeros((N, Tp - T) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device)
+                x = torch.cat([x, pad], 1)
+            return x.reshape((S, L) + tuple(x.shape[2:]))
+
+        valid = torch.ones(N * T, device=self.device) if mask is None else mask.reshape(-1)
+        valid_c = chunk(valid)
+        obs_c, act_c, olp_c, adv_c, vt_c = (chunk(x) for x in (obs, act, old_logp, adv, vt))
+        olg_c = chunk(old_logits) if old_logits is not None else None
+        resets = chunk(b["is_first"].bool().reshape(-1))
+        state0 = b["state_in"][:, ::L].reshape(S, -1).float()
+        mbs = max(1, mb // L)
+
+        def flat(x):
+            return x.reshape((-1,) + tuple(x.shape[2:]))
+
+        def gen_mb():
+            for _ in range(epochs):
+                perm = torch.randperm(S, device=self.device, generator=gen)
+                for i in range(0, S - mbs + 1, mbs):
+                    idx = perm[i: i + mbs]
+                    logits, v = self.forward(obs_c[idx], state0[idx], resets[idx])
+                    yield (flat(logits), flat(v), flat(act_c[idx]), flat(olp_c[idx]), flat(adv_c[idx]),
+                           flat(vt_c[idx]), flat(olg_c[idx]) if olg_c is not None else None, flat(valid_c[idx]))
+
+        return gen_mb
 
     # ------------------------------------------------------------------ IMPALA / APPO
     def _vtrace_targets(self, b, N, T, logits, values):

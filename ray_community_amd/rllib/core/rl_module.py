@@ -171,11 +171,114 @@ class RLModule(nn.Module):
         self.load_state_dict(state)
 
 
+class RecurrentRLModule(nn.Module):
+    """LSTM actor-critic (reference: the new-stack default ``use_lstm`` encoder,
+    ``rllib/core/models/torch/encoder.py`` TorchLSTMEncoder): MLP encoder -> LSTM cell -> policy and
+    value heads. Stateful: the env runner carries one ``(h, c)`` row per sub-env (zeroed at episode
+    starts) and records the state each step entered with; the learner replays ``max_seq_len``
+    chunks from the recorded chunk-start states, zeroing the state inside a chunk where a new
+    episode begins (``resets``), so training sees exactly the recurrence the rollout used."""
+
+    is_stateful = True
+
+    def __init__(self, observation_space, action_space, model_config: Optional[Dict] = None):
+        super().__init__()
+        cfg = dict(model_config or {})
+        self.obs_space, self.act_space = observation_space, action_space
+        if len(observation_space.shape) == 3:
+            raise ValueError("use_lstm over image observations is not supported; stack frames with "
+                             "FrameStackingEnvToModule instead")
+        if isinstance(action_space, Discrete):
+            self.n_out, self.dist_cls = action_space.n, Categorical
+        else:
+            self.n_out, self.dist_cls = 2 * int(np.prod(action_space.shape)), DiagGaussian
+        self.cell_size = int(cfg.get("lstm_cell_size", 256))
+        self.max_seq_len = int(cfg.get("max_seq_len", 20))
+        hiddens = cfg.get("fcnet_hiddens", [256, 256])
+        inp = int(np.prod(observation_space.shape))
+        self.encoder, feat = _mlp(inp, hiddens, cfg.get("fcnet_activation", "tanh"))
+        self.lstm = nn.LSTMCell(feat, self.cell_size)
+        self.pi = nn.Linear(self.cell_size, self.n_out)
+        self.vf = nn.Linear(self.cell_size, 1)
+        nn.init.orthogonal_(self.pi.weight, 0.01)
+        nn.init.zeros_(self.pi.bias)
+
+    # ------------------------------------------------------------------ state
+    def get_initial_state(self, batch_size: int = 1, device=None):
+        z = torch.zeros(batch_size, 2 * self.cell_size, device=device)
+        return z
+
+    def _cell(self, x, state):
+        h, c = state[:, : self.cell_size], state[:, self.cell_size:]
+        h, c = self.lstm(x, (h, c))
+        return h, torch.cat([h, c], 1)
+
+    # ------------------------------------------------------------------ rollout (one step)
+    def forward_step(self, obs, state):
+        x = preprocess_obs(obs).reshape(obs.shape[0], -1)
+        h, new_state = self._cell(self.encoder(x), state.to(x.dtype))
+        return self.pi(h), self.vf(h).squeeze(-1), new_state
+
+    @torch.no_grad()
+    def forward_exploration_step(self, obs, state):
+        logits, v, st = self.forward_step(obs, state)
+        d = self.dist(logits)
+        a = d.sample()
+        return a, d.logp(a), v, logits, st
+
+    @torch.no_grad()
+    def forward_inference_step(self, obs, state):
+        logits, v, st = self.forward_step(obs, state)
+        return self.dist(logits).deterministic_sample(), v, st
+
+    # ------------------------------------------------------------------ training (sequences)
+    def forward_seq(self, obs, state0, resets):
+        """obs [B, L, ...], state0 [B, 2H], resets [B, L] (state zeroed BEFORE step t where set)
+        -> logits [B, L, A], values [B, L]."""
+        B, L = obs.shape[:2]
+        x = self.encoder(preprocess_obs(obs).reshape(B, L, -1))
+        st = state0.to(x.dtype)
+        keep = (~resets.bool()).to(x.dtype).unsqueeze(-1)
+        hs = []
+        for t in range(L):
+            st = st * keep[:, t]
+            h, st = self._cell(x[:, t], st)
+            hs.append(h)
+        h = torch.stack(hs, 1)
+        return self.pi(h), self.vf(h).squeeze(-1)
+
+    def forward(self, obs, state=None, resets=None):
+        """``resets`` given: the sequence form (``forward_seq``; what the learner calls, so a DDP
+        wrapper sees it). Otherwise one step per row from ``state`` (default: a fresh state)."""
+        if resets is not None:
+            return self.forward_seq(obs, state, resets)
+        st = self.get_initial_state(obs.shape[0], obs.device) if state is None else state
+        logits, v, _ = self.forward_step(obs, st)
+        return logits, v
+
+    def dist(self, logits):
+        return self.dist_cls(logits)
+
+    def get_state(self):
+        return {k: v.detach().cpu() for k, v in self.state_dict().items()}
+
+    def set_state(self, state):
+        self.load_state_dict(state)
+
+
 def make_module(config: Dict, observation_space, action_space):
-    """Module factory keyed by ``config['module_class']`` (``"actor_critic"`` default, ``"sac"``)."""
+    """Module factory keyed by ``config['module_class']`` (``"actor_critic"`` default, ``"sac"``);
+    ``model.use_lstm`` selects the recurrent actor-critic (PPO)."""
     kind = config.get("module_class", "actor_critic")
+    model = config.get("model") or {}
     if kind == "sac":
+        if model.get("use_lstm"):
+            raise ValueError("use_lstm is supported for PPO (actor-critic modules) only")
         from .sac_module import SACModule
 
         return SACModule(observation_space, action_space, config.get("model"))
+    if model.get("use_lstm"):
+        if config.get("q_head") or config.get("_algo") not in (None, "PPO"):
+            raise ValueError("use_lstm is supported for PPO only")
+        return RecurrentRLModule(observation_space, action_space, model)
     return RLModule(observation_space, action_space, config.get("model"), q_head=config.get("q_head", False))

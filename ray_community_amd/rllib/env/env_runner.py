@@ -3,6 +3,11 @@
 Each runner owns a natively vectorised env (N sub-envs stepped as one numpy batch) and a CPU
 copy of the RLModule; it returns rollout fragments as env-major ``[N, T]`` column blocks with
 the value bootstraps needed for exact GAE under auto-reset and truncation (``next_vf_preds``).
+Observations pass through the env-to-module ConnectorV2 pipeline and actions through the
+module-to-env pipeline (``rllib/connectors``); the fragment stores what the module saw.
+Recurrent modules (``model.use_lstm``): one ``(h, c)`` row per sub-env, zeroed at episode
+starts; the state each step entered with is stored (``state_in``) with the episode-start flags
+(``is_first``) so the learner can replay the recurrence.
 """
 from __future__ import annotations
 
@@ -30,8 +35,16 @@ class EnvRunner:
         self.env = make_vector_env(config["env"], config.get("num_envs_per_env_runner", 1), config.get("env_config"),
                                    seed=self.seed)
         self.N = self.env.num_envs
-        self.module = make_module(config, self.env.observation_space, self.env.action_space)
+        from ..connectors import VectorEnvContext, build_env_to_module, build_module_to_env
+
+        self.env_to_module = build_env_to_module(config, self.env)
+        self.module_to_env = build_module_to_env(config, self.env)
+        self.has_stateful_connectors = len(self.env_to_module) > 0
+        self._ctx = VectorEnvContext(self.N)
+        self._pending_mobs = None  # connector output for self.obs computed at the previous fragment's end
+        self.module = make_module(config, self.env_to_module.observation_space, self.env.action_space)
         self.module.eval()
+        self.stateful = bool(getattr(self.module, "is_stateful", False))
         # GPU inference (num_gpus_per_env_runner > 0): the module lives on the runner's GPU share,
         # observations go up once per step and ONE packed [N, 3 + A] tensor comes back
         self.device = torch.device("cpu")
@@ -39,6 +52,7 @@ class EnvRunner:
             self.device = torch.device("cuda", torch.cuda.current_device())
             self.module.to(self.device)
         self.obs, _ = self.env.reset(seed=self.seed)
+        self._rstate = self.module.get_initial_state(self.N, self.device) if self.stateful else None
         self.ep_ret = np.zeros(self.N)
         self.ep_len = np.zeros(self.N, dtype=np.int64)
         self.completed = collections.deque(maxlen=int(config.get("metrics_num_episodes_for_smoothing", 100)))
@@ -59,7 +73,38 @@ class EnvRunner:
                 self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i)
 
     def spaces(self):
-        return self.env.observation_space, self.env.action_space
+        """(module observation space = the env-to-module pipeline's output, action space)."""
+        return self.env_to_module.observation_space, self.env.action_space
+
+    # ------------------------------------------------------------------ connectors
+    def get_connector_state(self):
+        return self.env_to_module.get_state()
+
+    def set_connector_state(self, state):
+        self.env_to_module.set_state(state)
+        return True
+
+    def _module_obs(self, obs, explore):
+        """env obs [N, ...] -> module input through the env-to-module pipeline (advances its state)."""
+        if not len(self.env_to_module):
+            return obs
+        return self.env_to_module(rl_module=self.module, batch={"obs": obs}, episodes=self._ctx, explore=explore,
+                                  shared_data={})["obs"]
+
+    def _peek_obs(self, obs, idx, actions, rewards):
+        """Module input for sub-envs ``idx`` observing ``obs`` after ``actions`` / ``rewards``,
+        without committing connector state (final observations of truncated episodes)."""
+        if not len(self.env_to_module):
+            return obs
+        ctx = self._ctx.subset(idx, actions, rewards)
+        return self.env_to_module(rl_module=self.module, batch={"obs": obs}, episodes=ctx, explore=False,
+                                  shared_data={"peek": True})["obs"]
+
+    def _env_actions(self, an, explore):
+        if not len(self.module_to_env):
+            return an
+        return self.module_to_env(rl_module=self.module, batch={"actions": an, "actions_for_env": an.copy()},
+                                  episodes=self._ctx, explore=explore, shared_data={})["actions_for_env"]
 
     def set_weights(self, state, version: int = 0):
         if version != self.weights_version:
@@ -105,10 +150,12 @@ class EnvRunner:
         h = torch.cat(cols, 1).cpu()
         return h[:, 0].long(), h[:, 1], h[:, 2], (h[:, 3:] if logits is not None else None)
 
-    def _value(self, obs):
-        o = torch.from_numpy(obs)
+    def _value(self, obs, state=None):
+        o = torch.from_numpy(np.ascontiguousarray(obs))
         if self.device.type == "cuda":
             o = o.to(self.device, non_blocking=True)
+        if self.stateful:
+            return self.module.forward_step(o, state)[1].float().cpu().numpy()
         return self.module.forward(o)[1].float().cpu().numpy()
 
     @torch.no_grad()
@@ -116,7 +163,6 @@ class EnvRunner:
         """On-policy fragment of T = num_steps // N steps per sub-env (PPO / IMPALA)."""
         T = max(1, int(num_steps or self.cfg.get("rollout_fragment_length", 64) * self.N) // self.N)
         N = self.N
-        obs_buf = np.empty((N, T) + self.obs.shape[1:], dtype=self.obs.dtype)
         dist = getattr(self.module, "dist_cls", None)  # None: SAC-style module with its own squashed policy
         act_shape = () if dist is not None and dist.__name__ == "Categorical" else self.env.action_space.shape
         acts = np.empty((N, T) + tuple(act_shape), dtype=np.int64 if act_shape == () else np.float32)
@@ -125,14 +171,34 @@ class EnvRunner:
         rew = np.empty((N, T), dtype=np.float32)
         term = np.empty((N, T), dtype=bool)
         trunc = np.empty((N, T), dtype=bool)
-        logits_buf = None
-        trunc_fix = []  # (t, env indices, final obs)
+        first_buf = np.empty((N, T), dtype=bool)
+        obs_buf = logits_buf = state_buf = None
+        trunc_fix = []  # (t, env indices, module-input final obs, state after the step)
         gpu = self.device.type == "cuda"
+        ctx = self._ctx
         for t in range(T):
-            o = torch.from_numpy(self.obs)
+            if self._pending_mobs is not None:
+                mobs, self._pending_mobs = self._pending_mobs, None
+            else:
+                mobs = self._module_obs(self.obs, explore)
+            if obs_buf is None:
+                obs_buf = np.empty((N, T) + mobs.shape[1:], dtype=mobs.dtype)
+            first_buf[:, t] = ctx.is_first
+            o = torch.from_numpy(np.ascontiguousarray(mobs))
             if gpu:
                 o = o.to(self.device, non_blocking=True)
-            if explore:
+            if self.stateful:
+                if ctx.is_first.any():
+                    self._rstate[torch.from_numpy(ctx.is_first).to(self._rstate.device)] = 0.0
+                if state_buf is None:
+                    state_buf = np.empty((N, T, self._rstate.shape[1]), dtype=np.float32)
+                state_buf[:, t] = self._rstate.float().cpu().numpy()
+                if explore:
+                    a, lp, v, logits, self._rstate = self.module.forward_exploration_step(o, self._rstate)
+                else:
+                    a, v, self._rstate = self.module.forward_inference_step(o, self._rstate)
+                    lp, logits = torch.zeros(N, device=o.device), None
+            elif explore:
                 a, lp, v, logits = self.module.forward_exploration(o)
             else:
                 a, v = self.module.forward_inference(o)
@@ -144,37 +210,46 @@ class EnvRunner:
                 if logits_buf is None:
                     logits_buf = np.empty((N, T, logits.shape[-1]), dtype=np.float32)
                 logits_buf[:, t] = logits.numpy()
-            obs_buf[:, t] = self.obs
+            obs_buf[:, t] = mobs
             an = a.numpy()
             acts[:, t] = an
             logp[:, t] = lp.numpy()
             vf[:, t] = v.numpy()
-            nobs, r, te, tr, info = self.env.step(an)
+            nobs, r, te, tr, info = self.env.step(self._env_actions(an, explore))
             rew[:, t] = r
             term[:, t] = te
             trunc[:, t] = tr
             if tr.any():
                 idx = np.nonzero(tr)[0]
-                trunc_fix.append((t, idx, info["final_obs"][idx]))
+                fo = self._peek_obs(info["final_obs"][idx], idx, an, r)
+                trunc_fix.append((t, idx, fo, self._rstate[torch.from_numpy(idx)] if self.stateful else None))
             self._track(r, te, tr, info)
             self.obs = nobs
-        last_v = self._value(self.obs)
+            ctx.is_first = te | tr
+            ctx.last_actions, ctx.last_rewards = an, r
+        # bootstrap V(s_T): the next fragment starts from these module inputs (connector state
+        # advances exactly once per env step)
+        self._pending_mobs = self._module_obs(self.obs, explore)
+        st_next = None
+        if self.stateful:
+            st_next = self._rstate.clone()
+            if ctx.is_first.any():
+                st_next[torch.from_numpy(ctx.is_first).to(st_next.device)] = 0.0
+        last_v = self._value(self._pending_mobs, st_next)
         next_vf = np.empty_like(vf)
         next_vf[:, :-1] = vf[:, 1:]
         next_vf[:, -1] = last_v
-        if trunc_fix:
-            fo = np.concatenate([x[2] for x in trunc_fix], axis=0)
-            fv = self._value(fo)
-            k = 0
-            for t, idx, _ in trunc_fix:
-                next_vf[idx, t] = fv[k: k + len(idx)]
-                k += len(idx)
+        for t, idx, fo, st in trunc_fix:
+            next_vf[idx, t] = self._value(fo, st)
         self.steps_sampled += N * T
         b = SampleBatch({SampleBatch.OBS: obs_buf, SampleBatch.ACTIONS: acts, SampleBatch.ACTION_LOGP: logp,
                          SampleBatch.VF_PREDS: vf, SampleBatch.REWARDS: rew, SampleBatch.TERMINATEDS: term,
                          SampleBatch.TRUNCATEDS: trunc, SampleBatch.NEXT_VF_PREDS: next_vf})
         if logits_buf is not None:
             b[SampleBatch.ACTION_DIST_INPUTS] = logits_buf
+        if self.stateful:
+            b["state_in"] = state_buf
+            b["is_first"] = first_buf
         b.fragment_shape = (N, T)
         if self.cfg.get("output"):
             if getattr(self, "_writer", None) is None:
@@ -189,6 +264,9 @@ class EnvRunner:
     @torch.no_grad()
     def sample_transitions(self, num_steps: int, epsilon: float = 0.0) -> SampleBatch:
         """Off-policy transitions (DQN): epsilon-greedy on the Q head."""
+        if len(self.env_to_module) or len(self.module_to_env):
+            raise NotImplementedError("ConnectorV2 pipelines are supported on the on-policy sampling path "
+                                      "(PPO / IMPALA / APPO); off-policy transitions take raw observations")
         N = self.N
         T = max(1, int(num_steps) // N)
         out = {k: [] for k in ("obs", "actions", "rewards", "new_obs", "terminateds")}

@@ -2,6 +2,7 @@
 
 gymnasium / ALE are not installed in this environment, so the framework ships:
   * ``CartPole-v1`` and ``Pendulum-v1`` (classic-control dynamics, vectorised over N envs);
+  * ``StatelessCartPole-v1`` (CartPole without the velocities: needs a memory-based policy);
   * ``SyntheticAtari-v0`` — an Atari-shaped task (84x84x4 uint8 frame stacks, Discrete(6)
     actions, +/-1 rewards): a falling-ball "catch" game rendered into 84x84 frames, used as the
     shape-faithful stand-in for ALE games (``ALE/*`` ids resolve to it, flagged in ``info``).
@@ -107,6 +108,25 @@ class CartPoleVec(VectorEnv):
             self.t[done] = 0
             obs = self.state.astype(np.float32)
         return obs, rew, term, trunc, {"final_obs": final}
+
+
+class StatelessCartPoleVec(CartPoleVec):
+    """CartPole with the velocities masked out (observation = [x, theta]): only a policy with
+    memory (LSTM, frame stacking or previous-action inputs) can infer the dynamics. Reference:
+    ``rllib/examples/envs/classes/stateless_cartpole.py``."""
+
+    def __init__(self, num_envs=1, max_episode_steps=500, seed=None):
+        super().__init__(num_envs, max_episode_steps, seed)
+        high = np.array([self.x_th * 2, self.theta_th * 2], dtype=np.float32)
+        self.observation_space = Box(-high, high, dtype=np.float32)
+
+    def reset(self, seed=None):
+        obs, info = super().reset(seed)
+        return obs[:, [0, 2]], info
+
+    def step(self, actions):
+        obs, rew, term, trunc, info = super().step(actions)
+        return obs[:, [0, 2]], rew, term, trunc, {"final_obs": info["final_obs"][:, [0, 2]]}
 
 
 class PendulumVec(VectorEnv):
@@ -292,6 +312,8 @@ def make_vector_env(env, num_envs: int, env_config: Optional[dict] = None, seed=
             return SingleToVector(lambda: _REGISTRY[env](cfg), num_envs, seed)
         if env == "CartPole-v1" or env == "CartPole-v0":
             return CartPoleVec(num_envs, max_episode_steps=500 if env.endswith("1") else 200, seed=seed)
+        if env in ("StatelessCartPole-v1", "StatelessCartPole"):
+            return StatelessCartPoleVec(num_envs, max_episode_steps=int(cfg.get("max_episode_steps", 500)), seed=seed)
         if env == "Pendulum-v1":
             return PendulumVec(num_envs, seed=seed)
         if env.startswith("ALE/") or env == "SyntheticAtari-v0" or "NoFrameskip" in env:

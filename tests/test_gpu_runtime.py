@@ -91,6 +91,26 @@ def test_ppo_gpu_learner_synthetic_atari(ray_gpu):
     algo.stop()
 
 
+def test_ppo_lstm_gpu_learner(ray_gpu):
+    """Recurrent PPO with the learner on the GPU: chunked sequence replay + LSTM backward on HIP."""
+    from ray_community_amd.rllib import PPOConfig
+
+    cfg = (PPOConfig().environment("StatelessCartPole-v1").env_runners(num_envs_per_env_runner=8)
+           .training(train_batch_size=512, minibatch_size=128, num_epochs=2,
+                     model={"use_lstm": True, "lstm_cell_size": 32, "max_seq_len": 16, "fcnet_hiddens": [32]})
+           .resources(num_gpus=1))
+    algo = cfg.build()
+    try:
+        assert algo.learner_group.local.device.type == "cuda"
+        for _ in range(2):
+            r = algo.train()
+        info = r["info"]["learner"]["default_policy"]
+        assert r["num_env_steps_sampled_this_iter"] == 512 and info["num_minibatches"] > 0
+        assert all(v == v for v in (info["total_loss"], info["vf_loss"]))  # finite, not NaN
+    finally:
+        algo.stop()
+
+
 def test_gpu_object_store_spill_and_restore_bit_exact():
     """HBM budget 48 MB: putting 4 x 16 MB GPU objects pushes the least recently used ones to
     pinned host memory (hipMemcpyAsync on a side stream); get() restores them into HBM bit-exact."""

@@ -146,3 +146,47 @@ def test_flat_sgd_matches_torch_sgd():
         topt.zero_grad()
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         assert torch.allclose(pa, pb, atol=1e-5, rtol=1e-4), n
+
+
+def test_split_master_roundtrip_is_exact():
+    """fp32 master <-> (bf16 high half, low 16 bits): bit-exact, including exact rounding ties,
+    negatives, zeros and subnormals; the high half is the RNE bf16 except at ties (<= 1 ulp)."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1 << 16, generator=g) * torch.logspace(-30, 30, 1 << 16)
+    bits = x.view(torch.int32)
+    ties = (bits & ~0xFFFF) | 0x8000  # exact half-way cases
+    specials = torch.tensor([0.0, -0.0, 1e-40, -1e-40, 1.0, -1.0, 3.0e38, -3.0e38])
+    for t in (x, ties.view(torch.float32), specials):
+        hi, lo = ref.split_master(t)
+        assert hi.dtype == torch.bfloat16 and lo.dtype == torch.int16
+        back = ref.join_master(hi, lo)
+        assert torch.equal(back.view(torch.int32), t.contiguous().view(torch.int32))
+        d = (hi.view(torch.int16).to(torch.int32) - t.to(torch.bfloat16).view(torch.int16).to(torch.int32)).abs()
+        assert int(d.max()) <= 1
+
+
+def test_flat_adamw_split_master_matches_fp32_master():
+    """The split master format (GPU default for bf16 models) follows the fp32-master trajectory
+    bit-exactly (reference math on CPU; the HIP kernel is checked on the GPU)."""
+    from ray_community_amd.parallel import FlatAdamW
+    from ray_community_amd.parallel.flat import FlatParameters
+
+    outs = []
+    for fmt in ("fp32", "split"):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.Linear(17, 5)).to(torch.bfloat16)
+        flat = FlatParameters(net)
+        opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5, master_format=fmt)
+        assert opt.split_master == (fmt == "split")
+        g = torch.Generator().manual_seed(1)
+        for _ in range(4):
+            flat.grad.copy_(torch.randn(flat.numel, generator=g).to(torch.bfloat16))
+            opt.step(0.5)
+        outs.append((opt.master.clone(), opt.m.clone(), flat.data.clone()))
+        sd = opt.state_dict()
+        opt.load_state_dict(sd)
+        assert torch.equal(opt.master, outs[-1][0])
+    (m32, mm32, w32), (ms, mms, ws) = outs
+    assert torch.equal(m32, ms) and torch.equal(mm32, mms)
+    dw = (w32.view(torch.int16).to(torch.int32) - ws.view(torch.int16).to(torch.int32)).abs()
+    assert int(dw.max()) <= 1  # model weights: RNE vs half-up only at exact ties
