@@ -2550,6 +2550,26 @@ class Head:
         ac = Counter(a.state for a in self.actors.values())
         gauge("rca_actors", "Actors by state", [({"state": k}, v) for k, v in ac.items()])
         gauge("rca_workers", "Worker processes", [({"node_id": "all"}, len(self.workers))])
+        # GPU object store (HBM-resident objects, per physical GPU) and its host spill traffic
+        gauge("rca_gpu_object_store_hbm_bytes", "HBM bytes held by GPU objects",
+              [({"gpu": str(k)}, v) for k, v in self.gpu_usage.items()])
+        gauge("rca_gpu_object_store_budget_bytes", "GPU object store budget per GPU (0 = unlimited)",
+              [({}, self.gpu_budget)])
+        gauge("rca_gpu_object_store_objects", "GPU objects by residence",
+              [({"state": st}, sum(1 for e in self.gpu_objects.values() if e.gpu["state"] == st))
+               for st in ("hbm", "host")])
+        gauge("rca_gpu_object_store_spilled_bytes_total", "Bytes of GPU objects spilled HBM -> host",
+              [({}, self.gpu_spilled_bytes)])
+        gauge("rca_gpu_object_store_spills_total", "GPU objects spilled to host", [({}, self.gpu_num_spilled)])
+        gauge("rca_gpu_object_store_restores_total", "GPU objects restored to HBM", [({}, self.gpu_num_restored)])
+        # node + MI355X telemetry (sysfs / amd-smi / psutil; reference METRICS_GAUGES names)
+        from . import node_telemetry
+
+        if not hasattr(self, "_telemetry"):
+            self._telemetry = node_telemetry.TelemetryCache()
+        node, gpus = self._telemetry.get()
+        lines.extend(node_telemetry.prometheus_lines(node, gpus, ip="127.0.0.1",
+                                                     session=os.path.basename(self.session_dir or "")))
         seen = set()
         now = time.time()
         for src, (t, text) in list(getattr(self, "_metrics_text", {}).items()):
