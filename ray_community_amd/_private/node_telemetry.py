@@ -70,7 +70,12 @@ def read_gpus_sysfs(root: str = _SYSFS_ROOT) -> List[Dict]:
     out = []
     for i, (_, p) in enumerate(sorted(cards)):
         d = os.path.join(p, "device")
-        rec = {"index": i, "name": _read(os.path.join(d, "product_name")) or "AMD Instinct GPU",
+        try:
+            pci = os.path.basename(os.path.realpath(d))
+        except OSError:
+            pci = ""
+        rec = {"index": i, "pci": pci, "unique_id": (_read(os.path.join(d, "unique_id")) or "").lower(),
+               "name": _read(os.path.join(d, "product_name")) or "AMD Instinct GPU",
                "vram_total": _read_int(os.path.join(d, "mem_info_vram_total")),
                "vram_used": _read_int(os.path.join(d, "mem_info_vram_used")),
                "busy_percent": _read_int(os.path.join(d, "gpu_busy_percent")),
@@ -176,8 +181,45 @@ def read_gpus_amd_smi(timeout: float = 10.0) -> List[Dict]:
         return []
 
 
-def read_gpus(allow_amd_smi: bool = True) -> List[Dict]:
+def visible_gpu_serials(timeout: float = 20.0) -> Optional[List[str]]:
+    """ASIC serials of the GPUs this process may use, in device order (``amd-smi static --asic``
+    honours the visibility the container / HIP_VISIBLE_DEVICES imposes; sysfs lists every GPU of
+    the host, other tenants' included). None when amd-smi is unavailable."""
+    exe = shutil.which("amd-smi") or ("/opt/rocm/bin/amd-smi" if os.path.exists("/opt/rocm/bin/amd-smi") else None)
+    if exe is None:
+        return None
+    try:
+        r = subprocess.run([exe, "static", "--asic", "--json"], capture_output=True, text=True, timeout=timeout)
+        data = json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip() else None
+    except (OSError, subprocess.TimeoutExpired, ValueError):
+        return None
+    if data is None:
+        return None
+    return parse_amd_smi_serials(data)
+
+
+def parse_amd_smi_serials(data) -> List[str]:
+    if isinstance(data, str):
+        data = json.loads(data)
+    if isinstance(data, dict):
+        data = data.get("gpu_data") or [data]
+    out = []
+    for g in sorted((g for g in data if isinstance(g, dict)), key=lambda g: int(g.get("gpu", 0))):
+        ser = str((g.get("asic") or {}).get("asic_serial", "")).lower()
+        out.append(ser[2:] if ser.startswith("0x") else ser)
+    return out
+
+
+def read_gpus(allow_amd_smi: bool = True, serials: Optional[List[str]] = None) -> List[Dict]:
+    """GPU records; with ``serials`` (visible_gpu_serials) only those GPUs, indexed in that order."""
     g = read_gpus_sysfs()
+    if g and serials:
+        by = {r.get("unique_id"): r for r in g}
+        sel = [by[s] for s in serials if s in by]
+        if sel:
+            for i, r in enumerate(sel):
+                r["index"] = i
+            g = sel
     if not g and allow_amd_smi:
         g = read_gpus_amd_smi()
     return g
@@ -216,7 +258,9 @@ class TelemetryCache:
         self._thread = None
 
     def _refresh(self, allow_amd_smi):
-        node, gpus = read_node(), read_gpus(allow_amd_smi)
+        if not hasattr(self, "_serials"):
+            self._serials = None if os.environ.get("RCA_TELEMETRY_ALL_GPUS") == "1" else visible_gpu_serials()
+        node, gpus = read_node(), read_gpus(allow_amd_smi, self._serials)
         if allow_amd_smi and not gpus:
             self._smi_misses = getattr(self, "_smi_misses", 0) + 1
             if self._smi_misses >= 2:  # no AMD GPU visible to either source: stop forking amd-smi
@@ -226,17 +270,19 @@ class TelemetryCache:
 
     def _loop(self):
         while True:
-            time.sleep(self.period_s)
             try:
                 self._refresh(self.allow_amd_smi)
             except Exception:  # noqa - telemetry must never take the head down
                 pass
+            time.sleep(self.period_s)
 
     def get(self):
         if self._thread is None:
             import threading
 
-            self._refresh(False)
+            with self._lock:
+                self._node = read_node()
+            # the first GPU read (which resolves the visible GPUs through amd-smi) runs on the thread
             self._thread = threading.Thread(target=self._loop, daemon=True, name="rca-telemetry")
             self._thread.start()
         with self._lock:

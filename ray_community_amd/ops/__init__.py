@@ -411,7 +411,7 @@ def compute_gae(rewards, values, terminateds, dones=None, gamma=0.99, lam=0.95, 
     if rewards.is_cuda:
         dev = rewards.device
         f = lambda x: x.to(device=dev, dtype=torch.float32).contiguous() if x is not None else None  # noqa: E731
-        u8 = lambda x: x.to(device=dev, dtype=torch.uint8).contiguous()  # noqa: E731
+        u8 = lambda x: _as_u8(x, dev)  # noqa: E731
         r, v, nv, lv = f(rewards), f(values), f(next_values), f(last_values)
         te, do = u8(terminateds), u8(dones)
         adv = torch.empty(B, T, device=dev, dtype=torch.float32)
@@ -443,7 +443,7 @@ def vtrace(log_rhos, rewards, values, next_values, terminateds, dones=None, gamm
     if rewards.is_cuda:
         dev = rewards.device
         f = lambda x: x.to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
-        u8 = lambda x: x.to(device=dev, dtype=torch.uint8).contiguous()  # noqa: E731
+        u8 = lambda x: _as_u8(x, dev)  # noqa: E731
         lr, r, v, nv, te, do = f(log_rhos), f(rewards), f(values), f(next_values), u8(terminateds), u8(dones)
         vs = torch.empty(B, T, device=dev, dtype=torch.float32)
         pg = torch.empty_like(vs)
@@ -453,6 +453,15 @@ def vtrace(log_rhos, rewards, values, next_values, terminateds, dones=None, gamm
         return vs, pg
     return ref.vtrace_ref(log_rhos, rewards, values, next_values, terminateds, dones, gamma, clip_rho_threshold,
                           clip_c_threshold, clip_pg_rho_threshold)
+
+
+def _as_u8(x, dev):
+    """Flags as uint8 for the RL kernels: a contiguous bool tensor on the device is reinterpreted
+    in place (same 1-byte storage) instead of converted by an extra elementwise kernel."""
+    x = torch.as_tensor(x)
+    if x.dtype == torch.bool and x.device == torch.device(dev) and x.is_contiguous():
+        return x.view(torch.uint8)
+    return x.to(device=dev, dtype=torch.uint8).contiguous()
 
 
 def _gae_cpu(rewards, values, terminateds, dones, gamma, lam, last_values, next_values):

@@ -40,6 +40,7 @@ _SIGS = {
     "rca_sumsq": (c_int, [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "rca_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float, c_float,
                           c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
+    "rca_adamw_split_set_blocks": (None, [c_ll]),
     "rca_adamw_split": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float,
                                 c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
     "rca_gae": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

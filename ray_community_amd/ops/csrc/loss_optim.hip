@@ -414,9 +414,11 @@ __global__ __launch_bounds__(256) void adamw_split_kernel(bf16_t* __restrict__ h
     u32x4* lp4 = reinterpret_cast<u32x4*>(lo16) + i;
     f32x4* mp = reinterpret_cast<f32x4*>(m) + 2 * i;
     f32x4* vp = reinterpret_cast<f32x4*>(v) + 2 * i;
-    const u32x4 H = __builtin_nontemporal_load(hp4), L = __builtin_nontemporal_load(lp4);
-    const f32x4 M0 = __builtin_nontemporal_load(mp), M1 = __builtin_nontemporal_load(mp + 1);
-    const f32x4 V0 = __builtin_nontemporal_load(vp), V1 = __builtin_nontemporal_load(vp + 1);
+    // state streams use the default cache policy (measured: non-temporal loads/stores of the
+    // read-modify-write state ran the 8B step at 3.7 TB/s vs 5.7 TB/s)
+    const u32x4 H = hp4[0], L = lp4[0];
+    const f32x4 M0 = mp[0], M1 = mp[1];
+    const f32x4 V0 = vp[0], V1 = vp[1];
     float P[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -436,12 +438,12 @@ __global__ __launch_bounds__(256) void adamw_split_kernel(bf16_t* __restrict__ h
       Ho[k] = h0 | (h1 << 16);
       Lo[k] = l0 | (l1 << 16);
     }
-    __builtin_nontemporal_store(Ho, hp4);
-    __builtin_nontemporal_store(Lo, lp4);
-    __builtin_nontemporal_store(f32x4{Mv[0], Mv[1], Mv[2], Mv[3]}, mp);
-    __builtin_nontemporal_store(f32x4{Mv[4], Mv[5], Mv[6], Mv[7]}, mp + 1);
-    __builtin_nontemporal_store(f32x4{Vv[0], Vv[1], Vv[2], Vv[3]}, vp);
-    __builtin_nontemporal_store(f32x4{Vv[4], Vv[5], Vv[6], Vv[7]}, vp + 1);
+    hp4[0] = Ho;
+    lp4[0] = Lo;
+    mp[0] = f32x4{Mv[0], Mv[1], Mv[2], Mv[3]};
+    mp[1] = f32x4{Mv[4], Mv[5], Mv[6], Mv[7]};
+    vp[0] = f32x4{Vv[0], Vv[1], Vv[2], Vv[3]};
+    vp[1] = f32x4{Vv[4], Vv[5], Vv[6], Vv[7]};
   }
   for (long long i = (nv << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float g = (GDT == 0 ? bf2f(((const bf16_t*)grad)[i]) : ((const float*)grad)[i]) * gm;
@@ -456,6 +458,9 @@ __global__ __launch_bounds__(256) void adamw_split_kernel(bf16_t* __restrict__ h
   }
 }
 
+static long long g_adamw_split_blocks = 4096;
+RCA_API void rca_adamw_split_set_blocks(long long nb) { g_adamw_split_blocks = nb > 0 ? nb : 4096; }
+
 // hi16: the bf16 model weights (in/out), lo16: low halves of the fp32 master bit patterns (in/out).
 // Contract: hi16, lo16, grad, m, v 16-B aligned when n >= 8.
 RCA_API int rca_adamw_split(void* hi16, void* lo16, const void* grad, int grad_dtype, float* m, float* v, long long n,
@@ -465,7 +470,7 @@ RCA_API int rca_adamw_split(void* hi16, void* lo16, const void* grad, int grad_d
   if ((((uintptr_t)hi16 | (uintptr_t)lo16 | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15) && n >= 8) return -1;
   AdamHP hp{lr, b1, b2, eps, wd, bc1, bc2, grad_mul, max_norm};
   long long nb = ((n >> 3) + 255) / 256;
-  if (nb > 8192) nb = 8192;
+  if (nb > g_adamw_split_blocks) nb = g_adamw_split_blocks;
   if (nb < 1) nb = 1;
   if (grad_dtype == 0)
     hipLaunchKernelGGL(adamw_split_kernel<0>, dim3((int)nb), dim3(256), 0, stream, (bf16_t*)hi16,

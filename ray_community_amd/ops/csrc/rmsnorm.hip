@@ -402,7 +402,8 @@ RCA_API int rca_rmsnorm_fwd(const void* x, const void* res, const void* w, void*
   return (int)hipGetLastError();
 }
 
-// returns the number of blocks used for dw partials; dw_part must hold nb*H floats (nb <= 512)
+// H = 2048 / 4096 take the column-split backward kernel (rmsnorm_bwd_split); the others the
+// LDS-slice kernels. dw_part must hold rca_rmsnorm_bwd_blocks(rows, H) * H floats (<= 1024 rows).
 static inline bool rmsnorm_bwd_split(int H) { return H == 2048 || H == 4096; }
 
 // Number of workgroups (= rows of the fp32 dw partials buffer) rca_rmsnorm_bwd launches for

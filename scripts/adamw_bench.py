@@ -19,8 +19,15 @@ hi = torch.zeros(N, dtype=torch.bfloat16, device=dev)
 sumsq = torch.ones(1, device=dev)
 st = stream_ptr(dev)
 out = {}
-for kind in ("split", "fp32"):
-    if kind == "fp32":
+kinds = ["split", "fp32"] + [f"split@{nb}" for nb in (2048, 8192, 16384)]
+for kind in kinds:
+    if kind.startswith("split@"):
+        lib().rca_adamw_split_set_blocks(int(kind.split("@")[1]))
+        kind_base = "split"
+    else:
+        lib().rca_adamw_split_set_blocks(4096)
+        kind_base = kind
+    if kind_base == "fp32":
         master = torch.zeros(N, dtype=torch.float32, device=dev)
         fn = lambda: check(lib().rca_adamw(master.data_ptr(), hi.data_ptr(), g.data_ptr(), 0, m.data_ptr(),
                                            v.data_ptr(), N, 1e-4, 0.9, 0.95, 1e-8, 0.1, 0.1, 0.05, 1.0,
@@ -43,7 +50,7 @@ for kind in ("split", "fp32"):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
     out[kind] = {"ms": round(ms, 3), "TB/s": round(N * bpp / ms / 1e9, 3), "bytes_per_param": bpp}
-    if kind == "split":
+    if kind_base == "split":
         del lo
     else:
         del master

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_ops_gpu.py -k "adamw" \
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_ops_gpu.py -k "adamw" tests/test_telemetry.py tests/test_gpu_runtime.py::test_ppo_lstm_gpu_learner \
   > gpurun_out/r3g_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r3g_tests.log; exit 1; }
 tail -3 gpurun_out/r3g_tests.log
 timeout -k 10 200 python -u scripts/adamw_bench.py > gpurun_out/r3g_adamw.json 2> gpurun_out/r3g_adamw.err || { echo adamw bench failed; tail gpurun_out/r3g_adamw.err; exit 1; }

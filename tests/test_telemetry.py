@@ -122,25 +122,58 @@ def test_hbm_gauge_tracks_allocation_gpu(shutdown_only):
     url = url if url.startswith("http") else "http://" + url
 
     def used():
+        # node telemetry covers every GPU of the node (sysfs / amd-smi see all of them, the
+        # process only its own): {GpuIndex: bytes}
         text = urllib.request.urlopen(url + "/metrics", timeout=10).read().decode()
-        vals = [float(m.group(1)) for m in re.finditer(r'^ray_node_gram_used\{[^}]*GpuIndex="0"[^}]*\} (\S+)$', text,
-                                                        re.M)]
+        vals = {m.group(1): float(m.group(2)) for m in
+                re.finditer(r'^ray_node_gram_used\{[^}]*GpuIndex="(\d+)"[^}]*\} (\S+)$', text, re.M)}
         assert vals, "no HBM gauge in /metrics: " + text[:500]
-        return vals[0]
+        return vals
 
     torch.cuda.init()
     torch.cuda.synchronize()
-    time.sleep(2.5)
-    before = used()
+    t0 = time.time()
+    while True:  # the first GPU read (visible-GPU resolution through amd-smi) runs in the background
+        try:
+            before = used()
+            break
+        except AssertionError:
+            if time.time() - t0 > 30:
+                raise
+            time.sleep(1.0)
+    assert len(before) == torch.cuda.device_count(), before  # only this process's GPUs
     x = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
     x.fill_(1)
     torch.cuda.synchronize()
     deadline = time.time() + 15
-    after = before
+    grew = 0.0
     while time.time() < deadline:
         time.sleep(1.0)
         after = used()
-        if after - before >= 7.5 * (1 << 30):
+        grew = max(after[k] - before.get(k, after[k]) for k in after)
+        if grew >= 7.5 * (1 << 30):
             break
     del x
-    assert after - before >= 7.5 * (1 << 30), (before, after)
+    assert grew >= 7.5 * (1 << 30), (before, after)
+
+
+def test_visible_gpu_filter_by_asic_serial(tmp_path):
+    """sysfs lists every GPU of the host; only the ones amd-smi reports visible are exported,
+    matched by ASIC serial (sysfs unique_id)."""
+    for i, uid in enumerate(["aaaa000000000001", "bbbb000000000002", "cccc000000000003"]):
+        d = tmp_path / f"card{i * 8}" / "device"
+        _w(str(d / "mem_info_vram_total"), str(288 << 30))
+        _w(str(d / "mem_info_vram_used"), str((i + 1) << 30))
+        _w(str(d / "unique_id"), uid)
+    static = {"gpu_data": [{"gpu": 0, "asic": {"asic_serial": "0xCCCC000000000003"}}]}
+    serials = nt.parse_amd_smi_serials(static)
+    assert serials == ["cccc000000000003"]
+    orig = nt._SYSFS_ROOT
+    try:
+        nt.read_gpus_sysfs.__defaults__ = (str(tmp_path),)
+        g = nt.read_gpus(allow_amd_smi=False, serials=serials)
+    finally:
+        nt.read_gpus_sysfs.__defaults__ = (orig,)
+    assert len(g) == 1 and g[0]["index"] == 0 and g[0]["vram_used"] == 3 << 30
+    with open(os.path.join(FIX, "amd_smi_static_mi355x.json")) as f:
+        assert len(nt.parse_amd_smi_serials(f.read())[0]) == 16  # real capture: 64-bit serial
