@@ -26,8 +26,6 @@
 // examples (python/ray/train/examples, release/train_tests) — the reference itself has no kernel.
 #include "attention_common.h"
 
-#include <cstdlib>
-
 // dK/dV lives in attention_dkdv.hip (its own register-form flags)
 void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                           const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
@@ -205,63 +203,17 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// delta = rowsum(dO * O) (fp32), [B, Hq, S]. One wave per RPW consecutive OUTPUT rows
-// ((b, hq, s) order, so the stores are one contiguous burst): LPR = D/8 lanes per row, RPS rows
-// per load step, 4 steps unrolled with all 8 loads issued before the first use (memory-level
-// parallelism: the one-row-per-16-lanes version ran at ~2.5 TB/s), 32-bit index math.
-template <int D>
-__global__ __launch_bounds__(kThreads) void attn_bwd_delta_kernel(const bf16_t* __restrict__ O,
-                                                                  const bf16_t* __restrict__ dO,
-                                                                  float* __restrict__ delta, int B, int S, int Hq,
-                                                                  long so, long sdo) {
-  constexpr int LPR = D / 8, RPS = 64 / LPR, U = 4, RPW = RPS * U;
-  const int lane = threadIdx.x & 63;
-  const int total = B * S * Hq;
-  const int base = (blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * RPW;
-  const int c = lane % LPR, r = lane / LPR;
-  u32x4 va[U], vg[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int row = base + u * RPS + r;  // = (b * Hq + hq) * S + s
-    if (row < total) {
-      const int s_ = row % S, bh = row / S;
-      const long tok = (long)(bh / Hq) * S + s_;
-      const int hq = bh % Hq;
-      va[u] = *reinterpret_cast<const u32x4*>(O + tok * so + hq * D + c * 8);
-      vg[u] = *reinterpret_cast<const u32x4*>(dO + tok * sdo + hq * D + c * 8);
-    } else {
-      va[u] = vg[u] = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  float out = 0.f;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    float a[8], g[8];
-    unpack8(va[u], a);
-    unpack8(vg[u], g);
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc += a[i] * g[i];
-#pragma unroll
-    for (int off = LPR / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    // lane L < RPW collects row L = u * RPS + (L % RPS) from lane (L % RPS) * LPR
-    const float v = __shfl(acc, (lane % RPS) * LPR, 64);
-    if (lane / RPS == u) out = v;
-  }
-  if (lane < RPW && base + lane < total) delta[base + lane] = out;
-}
-
-// ---------------------------------------------------------------------------------------------
 // dQ (query-major twin of the forward: recomputes P from LSE and dP = dO.V^T, accumulates
-// dQ^T = K^T.dS^T in registers). 32-key tiles, 2-deep LDS ring (loop unrolled over it); per
+// dQ^T = K^T.dS^T in registers; also writes delta = rowsum(dO * O) for the dK/dV kernel).
+// 32-key tiles, 2-deep LDS ring (loop unrolled over it); per
 // tile: K-row burst -> S^T MFMAs, V-row burst -> dP^T MFMAs, dS on the VALU, K^T transposed
 // burst -> dQ^T MFMAs.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    bf16_t* __restrict__ dQ, int B, int S, int Hq, int Hk, long sq, long sk, long sv, long sdo, long sdq,
-    float scale2, float scale) {
+    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
+    float* __restrict__ Delta, bf16_t* __restrict__ dQ, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
+    long so, long sdo, long sdq, float scale2, float scale) {
   constexpr int BQ = 128, BK = 32, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2, G8 = Img<D>::G8;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
@@ -293,13 +245,24 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
     settle(gf[kk]);
   }
   const float nlse = -LSE[(long)bh * S + qrow];
-  // -delta as the dP chain's initial accumulator (one query per lane: a constant vector built
-  // once), so dS = P * dP' needs no per-tile subtraction
+  // delta = rowsum(dO * O) for this lane's query row, fused here: the lane already holds its half
+  // of the dO row (gf), so only the matching O half is loaded; the two halves meet across lanes
+  // l / l^32. Written out for the dK/dV kernel, which runs after this one. -delta is the dP
+  // chain's initial accumulator (a constant vector), so dS = P * dP' needs no per-tile subtraction.
   f32x16 ndlt;
   {
-    const float d = -Delta[(long)bh * S + qrow];
+    const bf16_t* Orow = O + ((long)b * S + qrow) * so + (long)hq * D;
+    float acc = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ndlt[i] = d;
+    for (int kk = 0; kk < NKS; ++kk) {
+      const bf16x8_t of = gload8(Orow + 16 * kk + 8 * h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf((float)of[j], (float)gf[kk][j], acc);
+    }
+    const float d = xhalf_sum(acc);
+    if (h == 0) Delta[(long)bh * S + qrow] = d;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ndlt[i] = -d;
   }
 
   f32x16 dq[NDB];
@@ -398,70 +361,16 @@ void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, fl
                      sk, sv, so, scale2);
 }
 
-// dQ and dK/dV are independent once delta exists. RCA_ATTN_BWD_OVERLAP=1 (2: dQ first) forks dQ
-// onto a per-device side stream (event fork/join, capture-safe) so its workgroups can fill CUs the
-// dK/dV grid's causal tail leaves idle; 0 (default) runs them back to back on the caller's stream.
-struct BwdSide {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
-int bwd_overlap_mode() {
-  // default off: measured neutral-to-worse at the 8B shape (bwd 1.176-1.185 ms serial vs
-  // 1.196-1.218 ms forked; 353.6 vs 354.2 ms/step) -- the LPT-ordered dK/dV grid leaves no tail
-  // worth filling, and its 462-register waves cannot share a SIMD with dQ waves
-  static const int mode = [] {
-    const char* e = getenv("RCA_ATTN_BWD_OVERLAP");
-    return e ? atoi(e) : 0;
-  }();
-  return mode;
-}
-
-BwdSide* bwd_side() {
-  static BwdSide sides[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  BwdSide& sd = sides[dev];
-  if (!sd.s) {
-    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) {
-      sd.s = nullptr;
-      return nullptr;
-    }
-  }
-  return &sd;
-}
-
 template <int D, bool C>
 void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                 const float* lse, float* delta, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
                 long sq, long sk, long sv, long so, long sdo, long sdq, long sdk, long sdv, float scale2, float scale,
                 hipStream_t st) {
-  const long rows = (long)B * S * Hq;  // < 2^31 (shapes_ok)
-  const long rows_per_block = (kThreads / 64) * 4 * (64 / (D / 8));
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((rows + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
-                     st, o, dout, delta, B, S, Hq, so, sdo);
-  auto dq_on = [&](hipStream_t s) {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3(B * Hq * (S / 128)), dim3(kThreads), 0, s, q, k, v, dout, lse,
-                       delta, dq, B, S, Hq, Hk, sq, sk, sv, sdo, sdq, scale2, scale);
-  };
-  const int mode = bwd_overlap_mode();
-  BwdSide* sd = mode ? bwd_side() : nullptr;
-  if (sd) {
-    hipEventRecord(sd->fork, st);
-    hipStreamWaitEvent(sd->s, sd->fork, 0);
-    if (mode == 2) dq_on(sd->s);
-    rca_attn_launch_dkdv(D, C, q, k, v, dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2,
-                         scale, st);
-    if (mode != 2) dq_on(sd->s);
-    hipEventRecord(sd->join, sd->s);
-    hipStreamWaitEvent(st, sd->join, 0);
-    return;
-  }
+  // dQ first: it also produces delta = rowsum(dO * O), which dK/dV reads
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3(B * Hq * (S / 128)), dim3(kThreads), 0, st, q, k, v, o, dout, lse,
+                     delta, dq, B, S, Hq, Hk, sq, sk, sv, so, sdo, sdq, scale2, scale);
   rca_attn_launch_dkdv(D, C, q, k, v, dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale,
                        st);
-  dq_on(st);
 }
 
 bool shapes_ok(int B, int S, int Hq, int Hk, int D) {
