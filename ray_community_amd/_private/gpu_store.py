@@ -177,11 +177,12 @@ def import_tensor(rec):
 
 # ====================================================================== owner side
 class _Entry:
-    __slots__ = ("tensors", "host", "nbytes", "gpus", "tensor_gpus", "last", "state", "serialized")
+    __slots__ = ("tensors", "host", "host_bufs", "nbytes", "gpus", "tensor_gpus", "last", "state", "serialized")
 
     def __init__(self, tensors, serialized):
         self.tensors = tensors            # store-owned device tensors (None while spilled)
         self.host = None                  # pinned host copies while spilled
+        self.host_bufs = None             # the pool buffers under them (returned on restore)
         self.nbytes = sum(t.numel() * t.element_size() for t in tensors)
         self.tensor_gpus = [physical_gpu(t.device.index) for t in tensors]
         self.gpus = sorted(set(self.tensor_gpus))
@@ -190,13 +191,70 @@ class _Entry:
         self.serialized = serialized      # the value with its CUDA tensors as slots (host parts)
 
 
+class _PinnedPool:
+    """Reusable pinned (page-locked) host buffers for spills, by size class. ``hipHostMalloc`` is
+    slow (it maps and pins every page) and used to run once per spilled tensor under the store
+    lock; buffers now come from this pool and go back to it on restore. Cached bytes are bounded
+    by ``RCA_GPU_SPILL_POOL_BYTES`` (default 8 GiB)."""
+
+    def __init__(self, cap_bytes: Optional[int] = None):
+        import os
+
+        self.cap = int(cap_bytes if cap_bytes is not None else os.environ.get("RCA_GPU_SPILL_POOL_BYTES", 8 << 30))
+        self.free_lists: Dict[int, list] = {}
+        self.cached = 0
+        self.hits = 0
+        self.misses = 0
+        self.lock = threading.Lock()
+
+    @staticmethod
+    def size_class(n: int) -> int:
+        if n <= (1 << 20):
+            return 1 << 20
+        return 1 << (int(n - 1).bit_length())  # next power of two: <= 2x slack, few classes
+
+    def take(self, nbytes: int):
+        import torch
+
+        c = self.size_class(max(1, nbytes))
+        with self.lock:
+            fl = self.free_lists.get(c)
+            if fl:
+                self.cached -= c
+                self.hits += 1
+                return fl.pop()
+            self.misses += 1
+        return torch.empty(c, dtype=torch.uint8, pin_memory=True)
+
+    def give(self, buf):
+        c = buf.numel()
+        with self.lock:
+            if self.cached + c <= self.cap:
+                self.free_lists.setdefault(c, []).append(buf)
+                self.cached += c
+
+
+def _host_view(buf, t):
+    """A host tensor shaped / strided like device tensor ``t`` over pinned byte buffer ``buf``."""
+    span = 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride())) if t.numel() else 0
+    flat = buf[: max(span, 1) * t.element_size()].view(t.dtype)
+    return flat.as_strided(t.shape, t.stride())
+
+
 class GpuObjectStore:
-    """Device-resident objects owned by this process."""
+    """Device-resident objects owned by this process.
+
+    Spill / restore copy outside the store lock: an entry moves hbm -> spilling -> host (and
+    host -> restoring -> hbm) under the lock, the copies run on a per-device side stream with ONE
+    event per object, and pinned host buffers come from ``_PinnedPool``. Readers of other objects
+    never wait behind a copy; a restore of an object that is being spilled waits for that spill."""
 
     def __init__(self):
         self.entries: Dict[bytes, _Entry] = {}
         self.lock = threading.RLock()
+        self.cond = threading.Condition(self.lock)
         self._stream = None
+        self.pool = _PinnedPool()
         self.num_spilled = 0
         self.num_restored = 0
         self.spilled_bytes = 0
@@ -253,74 +311,122 @@ class GpuObjectStore:
 
     # -------------------------------------------------------------- spill / restore
     def spill(self, oid) -> int:
-        """Copy the object's tensors into pinned host memory (hipMemcpyAsync on a side stream)
-        and release its HBM. Returns the bytes released."""
+        """Copy the object's tensors into pinned host memory (async copies on a side stream, one
+        event) and release its HBM. Returns the bytes released."""
         import torch
 
         with self.lock:
             e = self.entries.get(oid)
             if e is None or e.state != "hbm":
                 return 0
-            host = []
-            events = []
-            for t in e.tensors:
+            e.state = "spilling"
+            tensors = list(e.tensors)
+        try:
+            host, bufs, last = [], [], {}
+            for t in tensors:
                 s = self._side_stream(t.device)
-                s.wait_stream(torch.cuda.current_stream(t.device))
-                h = torch.empty_strided(t.shape, t.stride(), dtype=t.dtype, pin_memory=True)
+                if t.device not in last:
+                    s.wait_stream(torch.cuda.current_stream(t.device))
+                buf = self.pool.take(t.numel() * t.element_size())
+                h = _host_view(buf, t)
                 with torch.cuda.stream(s):
                     h.copy_(t, non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(s)
-                events.append(ev)
+                last[t.device] = s
                 host.append(h)
-            for ev in events:
+                bufs.append(buf)
+            for s in last.values():  # one wait per device, not per tensor
+                ev = torch.cuda.Event()
+                ev.record(s)
                 ev.synchronize()
-            e.host = host
+        except BaseException:
+            with self.lock:
+                e.state = "hbm"
+                self.cond.notify_all()
+            raise
+        with self.lock:
+            e.host, e.host_bufs = host, bufs
             e.tensors = None
             e.state = "host"
             self.num_spilled += 1
             self.spilled_bytes += e.nbytes
-            return e.nbytes
+            self.cond.notify_all()
+        return e.nbytes
 
     def restore(self, oid) -> Optional[bytes]:
-        """Bring a spilled object back into HBM (pinned H2D copies on a side stream); returns the
-        object's fresh wire bytes."""
+        """Bring a spilled object back into HBM (pinned H2D copies on a side stream, one event);
+        returns the object's fresh wire bytes."""
         import torch
 
         with self.lock:
             e = self.entries.get(oid)
             if e is None:
                 return None
-            if e.state == "host":
-                out = []
-                for h, g in zip(e.host, e.tensor_gpus):
+            while e.state in ("spilling", "restoring"):
+                self.cond.wait(timeout=1.0)
+                if self.entries.get(oid) is not e:
+                    return None
+            mine = e.state == "host"
+            if mine:
+                e.state = "restoring"
+                host, bufs = e.host, e.host_bufs
+        if mine:
+            try:
+                out, last = [], {}
+                for h, g in zip(host, e.tensor_gpus):
                     dev = _local_index(g)
                     dev = torch.cuda.current_device() if dev is None else dev
-                    s = self._side_stream(torch.device("cuda", dev))
+                    d = torch.device("cuda", dev)
+                    s = self._side_stream(d)
                     with torch.cuda.stream(s):
-                        d = torch.empty_strided(h.shape, h.stride(), dtype=h.dtype, device=f"cuda:{dev}")
-                        d.copy_(h, non_blocking=True)
-                    s.synchronize()
-                    out.append(d)
+                        t = torch.empty_strided(h.shape, h.stride(), dtype=h.dtype, device=d)
+                        t.copy_(h, non_blocking=True)
+                    last[d] = s
+                    out.append(t)
+                for d, s in last.items():
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                    ev.synchronize()
+                    # tensors allocated on the side stream are used on the default stream next
+                    for t in out:
+                        if t.device == d:
+                            t.record_stream(torch.cuda.current_stream(d))
+            except BaseException:
+                with self.lock:
+                    e.state = "host"
+                    self.cond.notify_all()
+                raise
+            for b in bufs or ():
+                self.pool.give(b)
+            with self.lock:
                 e.tensors = out
-                e.host = None
+                e.host = e.host_bufs = None
                 e.state = "hbm"
                 self.num_restored += 1
+                self.cond.notify_all()
+        with self.lock:
+            if e.tensors is None:
+                return None
             e.last = time.time()
             table = encode_table([export_tensor(t, oid, i) for i, t in enumerate(e.tensors)])
             return e.serialized.to_bytes_with_table(table)
 
     def free(self, oids):
+        bufs = []
         with self.lock:
             for o in oids:
-                self.entries.pop(o, None)
+                e = self.entries.pop(o, None)
+                if e is not None and e.state == "host" and e.host_bufs:
+                    bufs += e.host_bufs
+        for b in bufs:
+            self.pool.give(b)
 
     def stats(self):
         with self.lock:
             hbm = sum(e.nbytes for e in self.entries.values() if e.state == "hbm")
             host = sum(e.nbytes for e in self.entries.values() if e.state == "host")
         return {"objects": len(self.entries), "hbm_bytes": hbm, "host_bytes": host, "num_spilled": self.num_spilled,
-                "num_restored": self.num_restored}
+                "num_restored": self.num_restored, "pinned_pool_cached_bytes": self.pool.cached,
+                "pinned_pool_hits": self.pool.hits, "pinned_pool_misses": self.pool.misses}
 
 
 _STORE: Optional[GpuObjectStore] = None

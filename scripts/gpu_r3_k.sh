@@ -3,6 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_runtime.py -k "spill or pinned or owner_death" > gpurun_out/r3k_tests.log 2>&1 || { tail -30 gpurun_out/r3k_tests.log; exit 1; }
+tail -2 gpurun_out/r3k_tests.log
 OLD=$GRAFT_REPO_ROOT/scripts/ab_lib/libraca_kernels_delta_kernel.so
 for i in 1 2; do
   timeout -k 10 120 python scripts/attn_bench.py > gpurun_out/r3k_new_$i.log 2>&1 || exit 1; echo "fused  : $(grep rca-hip gpurun_out/r3k_new_$i.log)"

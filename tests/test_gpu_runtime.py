@@ -139,6 +139,50 @@ def test_gpu_object_store_spill_and_restore_bit_exact():
         ray.shutdown()
 
 
+def test_gpu_store_pinned_pool_and_concurrent_spill_restore():
+    """Spill / restore run outside the store lock on pooled pinned buffers: a second spill cycle
+    reuses the pool (no new hipHostMalloc), objects spill and restore concurrently from threads,
+    and every restore is bit-exact (incl. a channels-last tensor's strides)."""
+    import threading
+
+    from ray_community_amd._private.gpu_store import GpuObjectStore
+    from ray_community_amd._private.serialization import serialize
+
+    st = GpuObjectStore()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    vals = [torch.randn(1 << 20, device="cuda", generator=g) for _ in range(6)]
+    vals.append(torch.randn(4, 8, 5, 7, device="cuda", generator=g).contiguous(memory_format=torch.channels_last))
+    keep = [v.cpu() for v in vals]
+    oids = [bytes([i]) * 20 for i in range(len(vals))]
+    for o, v in zip(oids, vals):
+        st.add(o, serialize(v), copy=True)
+    for cycle in range(2):
+        errs = []
+
+        def worker(idx):
+            try:
+                for i in idx:
+                    assert st.spill(oids[i]) > 0
+                for i in idx:
+                    assert st.restore(oids[i]) is not None
+            except Exception as e:  # noqa
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(list(range(k, len(oids), 3)),)) for k in range(3)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not errs, errs
+        for o, k in zip(oids, keep):
+            t = st.local_tensor({"oid": o, "slot": 0})
+            assert t is not None and torch.equal(t.cpu(), k) and t.stride() == k.stride()
+    s = st.stats()
+    assert s["num_spilled"] == 2 * len(oids) and s["num_restored"] == 2 * len(oids)
+    assert s["pinned_pool_hits"] >= len(oids)  # cycle 2 took every buffer from the pool
+    st.free(oids)
+
+
 def test_gpu_object_owner_death_is_object_lost(ray_gpu):
     """A GPU object lives in its owner's HBM: once the owner dies, readers get ObjectLostError."""
     from ray_community_amd import exceptions as exc
