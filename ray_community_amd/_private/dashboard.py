@@ -175,11 +175,17 @@ class Dashboard:
             except ValueError:
                 ctrl = None
             if method == "GET":
+                empty = {"controller_info": None, "proxy_location": None, "http_options": None,
+                         "grpc_options": None, "proxies": {}, "deploy_mode": "UNSET", "applications": {},
+                         "target_capacity": None}
                 if ctrl is None:
-                    return 200, {"controller_info": None, "proxy_location": None, "http_options": None,
-                                 "grpc_options": None, "proxies": {}, "deploy_mode": "UNSET", "applications": {},
-                                 "target_capacity": None}
-                return 200, get(ctrl.get_serve_instance_details.remote())
+                    return 200, empty
+                from .. import exceptions as rexc
+
+                try:
+                    return 200, get(ctrl.get_serve_instance_details.remote())
+                except rexc.RayActorError:  # the controller is being shut down (DELETE just ran)
+                    return 200, empty
             if method == "DELETE":
                 if ctrl is not None:
                     sapi.shutdown()

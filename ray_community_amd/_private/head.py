@@ -76,15 +76,14 @@ class Deferred:
 
 
 class ObjEntry:
-    __slots__ = ("oid", "state", "desc", "holders", "pins", "waiters", "contained", "task", "gpu_owner", "size",
+    # holders / pins live in the native reference table (Head.refs, _native/ref_table.cpp)
+    __slots__ = ("oid", "state", "desc", "waiters", "contained", "task", "gpu_owner", "size",
                  "flags", "created", "gpu", "node")
 
     def __init__(self, oid, task=None):
         self.oid = oid
         self.state = PENDING
         self.desc = None
-        self.holders: Set[str] = set()
-        self.pins = 0
         self.waiters: List[Callable] = []
         self.contained: List[bytes] = []
         self.task = task
@@ -216,6 +215,10 @@ class Head:
         self.store = ObjectStore(self.store_name, cap, create=True)
         self.store_capacity = cap
         self.objects: Dict[bytes, ObjEntry] = {}
+        # who keeps each object alive (holder keys + anonymous pins) and where its value lives:
+        # C++ (_native/ref_table.cpp), with a holder -> objects index so a process death frees
+        # what it held without scanning every object
+        self.refs = native().RefTable()
         self.tasks: Dict[bytes, TaskState] = {}
         self.task_keys: Dict[int, TaskState] = {}
         self._key = 0
@@ -362,7 +365,8 @@ class Head:
                 if w.node_id == node_id and not w.dead:
                     self._kill_worker(w)
             # objects in the node's store are gone with it: reconstruct from lineage or fail
-            for e in [e for e in self.objects.values() if e.node == node_id and e.state == READY and e.desc
+            on_node = (self.objects.get(o) for o in self.refs.objects_on_node(node_id))
+            for e in [e for e in on_node if e is not None and e.node == node_id and e.state == READY and e.desc
                       and e.desc[0] in ("shm", "spill")]:
                 self._lose_object(e)
             self._schedule()
@@ -523,6 +527,7 @@ class Head:
         if e is None and create:
             e = ObjEntry(oid, task)
             self.objects[oid] = e
+            self.refs.add(oid)
         return e
 
     def _add_holder(self, oid, key):
@@ -534,7 +539,7 @@ class Head:
                     self._actor_handles(a).add(key)
             return
         if e.state != FREED:
-            e.holders.add(key)
+            self.refs.add_holder(oid, key)
 
     def _remove_holder(self, oid, key):
         if oid[:1] == b"A" and len(oid) == 21:
@@ -546,8 +551,8 @@ class Head:
         e = self.objects.get(oid)
         if e is None:
             return
-        e.holders.discard(key)
-        self._maybe_free(e)
+        if self.refs.remove_holder(oid, key):
+            self._maybe_free(e)
 
     def _actor_handles(self, a):
         hs = getattr(a, "handles", None)
@@ -559,7 +564,7 @@ class Head:
     def _pin(self, oid, n=1):
         e = self.objects.get(oid)
         if e is not None:
-            e.pins += n
+            self.refs.pin(oid, n)
         elif oid[:1] == b"A" and len(oid) == 21:
             a = self.actors.get(oid[1:])
             if a is not None:
@@ -568,8 +573,8 @@ class Head:
     def _unpin(self, oid, n=1):
         e = self.objects.get(oid)
         if e is not None:
-            e.pins -= n
-            self._maybe_free(e)
+            if self.refs.pin(oid, -n):
+                self._maybe_free(e)
         elif oid[:1] == b"A" and len(oid) == 21:
             a = self.actors.get(oid[1:])
             if a is not None:
@@ -584,7 +589,7 @@ class Head:
         self._kill_actor(a, no_restart=True, reason="all handles to the actor went out of scope")
 
     def _maybe_free(self, e: ObjEntry):
-        if e.holders or e.pins > 0 or e.state == FREED:
+        if e.state == FREED or self.refs.referenced(e.oid):
             return
         if e.state == PENDING:
             return  # freed when the producing task completes (result discarded)
@@ -609,6 +614,7 @@ class Head:
             self._unpin(c)
         e.contained = []
         self.objects.pop(e.oid, None)
+        self.refs.erase(e.oid)
 
     def _free_gpu_object(self, owner, oid):
         if owner == DRIVER:
@@ -620,11 +626,12 @@ class Head:
             self._send(w, (P.FREE_GPU, [oid]))
 
     def _drop_holder_everywhere(self, key):
-        for e in list(self.objects.values()):
+        for e in list(self.gpu_objects.values()):
             if e.gpu is not None:
                 e.gpu["maps"].pop(key, None)
-            if key in e.holders:
-                e.holders.discard(key)
+        for oid in self.refs.drop_holder(key):  # only the objects this holder kept alive
+            e = self.objects.get(oid)
+            if e is not None:
                 self._maybe_free(e)
         for a in list(self.actors.values()):
             hs = getattr(a, "handles", None)
@@ -648,7 +655,7 @@ class Head:
         ws, e.waiters = e.waiters, []
         for cb in ws:
             cb(e)
-        if not e.holders and e.pins <= 0:
+        if not self.refs.referenced(e.oid):
             self._free(e)
 
     def _set_error(self, e: ObjEntry, err: BaseException):
@@ -673,7 +680,7 @@ class Head:
         for c in e.contained:
             ce = self.objects.get(c)
             if ce is not None:
-                ce.holders.add(caller)
+                self.refs.add_holder(c, caller)
         d = e.desc
         if d[0] == "spill" and self.config.get("restore_spilled", True):
             self._restore(e)
@@ -688,7 +695,7 @@ class Head:
     # -------------------------------------------------------------- put
     def rpc_put(self, caller, oid, desc, contained, is_gpu=False, flags=0):
         e = self._obj(oid)
-        e.holders.add(caller)
+        self.refs.add_holder(oid, caller)
         owner = None
         if is_gpu:
             if caller == DRIVER:
@@ -1053,8 +1060,7 @@ class Head:
         for oid in oids:
             e = self.objects.get(oid)
             if e is not None:
-                e.holders.clear()
-                e.pins = 0
+                self.refs.clear_refs(oid)
                 if e.state == READY:
                     self._free(e)
 
@@ -1083,8 +1089,8 @@ class Head:
         if parent is not None and parent in self.tasks:
             self.tasks[parent].children.append(tid)
         for rid in spec["return_ids"]:
-            e = self._obj(rid, task=tid)
-            e.holders.add(owner)
+            self._obj(rid, task=tid)
+            self.refs.add_holder(rid, owner)
         if spec.get("generator") == "streaming":
             pass
         for c in spec.get("contained", ()):
@@ -1488,6 +1494,8 @@ class Head:
             if owner is not None:
                 w.gpu_objects.add(rid)
             e.node = ts.node
+            if ts.node is not None:
+                self.refs.set_node(rid, ts.node)
             self._set_ready(e, tuple(desc), contained, owner, flags, gpu_info=is_gpu)
         if spec.get("generator") == "streaming":
             ts.gen_done = True
@@ -1658,7 +1666,7 @@ class Head:
         oid = res[6]
         e = self._obj(oid, task=tid)
         if ts is not None:
-            e.holders.add(ts.owner)
+            self.refs.add_holder(oid, ts.owner)
             while len(ts.gen_items) <= index:
                 ts.gen_items.append(None)
             ts.gen_items[index] = oid
@@ -1709,9 +1717,8 @@ class Head:
             return d
         if index < len(ts.gen_items) and ts.gen_items[index] is not None:
             oid = ts.gen_items[index]
-            e = self.objects.get(oid)
-            if e is not None:
-                e.holders.add(caller)
+            if oid in self.objects:
+                self.refs.add_holder(oid, caller)
             d.resolve(oid)
             self._gen_consumed(ts, index)
             return d
@@ -1949,8 +1956,8 @@ class Head:
 
     def rpc_declare_object(self, caller, oid):
         """A caller-owned (direct-call) result whose ref escaped before its value arrived."""
-        e = self._obj(oid)
-        e.holders.add(caller)
+        self._obj(oid)
+        self.refs.add_holder(oid, caller)
         return True
 
     def rpc_put_owned(self, caller, items, owner_key, lineage=None):
@@ -1968,11 +1975,12 @@ class Head:
                 self.lineage.popitem(last=False)
         for oid, desc, contained, is_gpu, flags in items:
             e = self._obj(oid)
-            e.holders.add(owner_key)
+            self.refs.add_holder(oid, owner_key)
             if tid is not None:
                 e.task = tid
             if w is not None:
                 e.node = w.node_id
+                self.refs.set_node(oid, w.node_id)
             owner = None
             if is_gpu and w is not None:
                 owner = gpu_owner
@@ -2407,8 +2415,8 @@ class Head:
         for e in self.objects.values():
             out.append({"object_id": e.oid.hex(), "object_size": e.size,
                         "task_status": "FINISHED" if e.state == READY else "PENDING",
-                        "reference_type": "LOCAL_REFERENCE" if e.holders else "PINNED_IN_MEMORY",
-                        "num_holders": len(e.holders), "pins": e.pins,
+                        "reference_type": "LOCAL_REFERENCE" if self.refs.num_holders(e.oid) else "PINNED_IN_MEMORY",
+                        "num_holders": self.refs.num_holders(e.oid), "pins": self.refs.pins(e.oid),
                         "storage": e.desc[0] if e.desc else None, "gpu": e.gpu_owner is not None})
         return out
 

@@ -43,6 +43,9 @@ _SIGS = {
     "rca_adamw_split_set_blocks": (None, [c_ll]),
     "rca_adamw_split": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_float, c_float,
                                 c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_float, c_void_p]),
+    "rca_adamw_split_seg": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_ll,
+                                    c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
+                                    c_float, c_void_p]),
     "rca_gae": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                         c_float, c_float, c_int, c_void_p, c_void_p, c_float, c_void_p]),
     "rca_vtrace": (c_int, [c_void_p] * 8 + [c_int, c_int, c_float, c_float, c_float, c_float, c_void_p]),

@@ -4,6 +4,7 @@
 // All accesses are 16 B per lane (8 x bf16). Grids are capped at 256 CUs x 8 blocks and
 // grid-stride the remainder (cdna_hip_programming.md Guideline 11).
 #include "common.h"
+#include <stdlib.h>
 
 static inline int grid_for(long long nvec, int block) {
   long long g = (nvec + block - 1) / block;
@@ -282,9 +283,68 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
   }
 }
 
+// 128 x 128 tiles (R, C multiples of 128): 256-B row segments on both the read and the write side
+// (the 64 x 64 kernel's 128-B pieces, 8 KB apart, cost DRAM page locality) and no 16-bit LDS
+// traffic. Each lane loads two input rows (2q, 2q+1) x 8 columns and pairs them in registers
+// (v_perm) into 8 dwords = (out[j][2q], out[j][2q+1]) for its 8 output rows j; the dwords go to an
+// LDS image W[j][q] (128 x 64 dwords, XOR-swizzled q' = q ^ 2*(j/8): the 32 lanes of a
+// ds_write_b32 group -- 16 column chunks x 2 row pairs -- hit 32 distinct banks), and each output
+// 16-B chunk is one ds_read_b128 of 4 consecutive q (the swizzle only swaps dword pairs inside the
+// aligned quad when j/8 is odd). Per lane: 8 x 16-B loads in flight, 64 ds_write_b32, 8
+// ds_read_b128, 8 x 16-B stores.
+__global__ __launch_bounds__(256) void transpose128_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                                int R, int C, long ldi) {
+  __shared__ u32x4 W4[128 * 64 / 4];
+  unsigned* W = reinterpret_cast<unsigned*>(W4);
+  const int tilesC = C >> 7;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = (bid / tilesC) << 7, c0 = (bid % tilesC) << 7;
+  const int t = threadIdx.x, ch = t & 15, rp = t >> 4;
+  u32x4 va[4], vb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bf16_t* p = in + (long)(r0 + 2 * rp + 32 * k) * ldi + c0 + ch * 8;
+    va[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    vb[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + ldi));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int q = (rp + 16 * k) ^ (2 * ch);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      // lo halves of both rows -> column 2m, hi halves -> column 2m+1 (v_perm_b32 byte selects)
+      W[(ch * 8 + 2 * m) * 64 + q] = __builtin_amdgcn_perm(vb[k][m], va[k][m], 0x05040100u);
+      W[(ch * 8 + 2 * m + 1) * 64 + q] = __builtin_amdgcn_perm(vb[k][m], va[k][m], 0x07060302u);
+    }
+  }
+  __syncthreads();
+  const int q4 = (t & 15) * 4;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int j = (t >> 4) + 16 * p;
+    const int sw = 2 * (j >> 3);
+    u32x4 o = W4[(j * 64 + (q4 ^ (sw & ~3))) >> 2];
+    if (sw & 2) o = u32x4{o[2], o[3], o[0], o[1]};
+    *reinterpret_cast<u32x4*>(out + (long)(c0 + j) * R + r0 + q4 * 2) = o;
+  }
+}
+
 RCA_API int rca_transpose_bf16(const void* in, void* out, int R, int C, long long ldi, hipStream_t stream) {
   if (R <= 0 || C <= 0 || (R & 63) || (C & 63) || (ldi & 7) || ldi < C) return -1;
   if (((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return -3;
+  // 128 x 128 tiles measured faster only on the ~117 M-element 8B operands (gate_up / down weights,
+  // 8192 x 14336 activations: 73 vs 93-95 us); below ~64 M elements the 64 x 64 kernel's 4x more
+  // workgroups fill the chip better, and on the 1 G-element dlogits it is ~4 % ahead
+  // (scripts/transpose_bench.py). RCA_TRANSPOSE_TILE64=1 forces the 64 x 64 kernel.
+  static const bool tile64 = getenv("RCA_TRANSPOSE_TILE64") != nullptr;
+  const long long nel = (long long)R * C;
+  if (!tile64 && !(R & 127) && !(C & 127) && nel >= (96LL << 20) && nel <= (256LL << 20)) {
+    const long long tiles = (long long)(R >> 7) * (C >> 7);
+    if (tiles >= (1LL << 31)) return -2;
+    hipLaunchKernelGGL(transpose128_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, (const bf16_t*)in,
+                       (bf16_t*)out, R, C, (long)ldi);
+    return (int)hipGetLastError();
+  }
   const long long tiles = (long long)(R >> 6) * (C >> 6);
   if (tiles >= (1LL << 31)) return -2;
   hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, (const bf16_t*)in,

@@ -310,12 +310,18 @@ __device__ __forceinline__ float clip_coef(const float* sumsq, float max_norm, f
   return fminf(1.f, max_norm / (nrm + 1e-6f));
 }
 
+// Explicit fmas and no compiler contraction: every kernel that inlines this (flat fp32-master,
+// split-master, segmented) rounds identically whatever the surrounding code lets the backend fuse
+// (with contraction on, the segmented kernel's larger body fused a different subset of the
+// mul/add pairs than the flat kernels and the results differed in the last bit).
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamHP& hp) {
-  m = hp.b1 * m + (1.f - hp.b1) * g;
-  v = hp.b2 * v + (1.f - hp.b2) * g * g;
+#pragma clang fp contract(off)
+  m = __builtin_fmaf(hp.b1, m, (1.f - hp.b1) * g);
+  v = __builtin_fmaf(hp.b2, v, ((1.f - hp.b2) * g) * g);
   const float mh = m / hp.bc1;
   const float vh = v / hp.bc2;
-  p = p - hp.lr * (mh / (sqrtf(vh) + hp.eps) + hp.wd * p);
+  const float u = __builtin_fmaf(hp.wd, p, mh / (sqrtf(vh) + hp.eps));
+  p = __builtin_fmaf(-hp.lr, u, p);
 }
 
 // GDT: 0 = bf16 grads, 1 = f32 grads. p16 (optional) receives the bf16 copy of the master weights.
@@ -394,6 +400,72 @@ __device__ __forceinline__ void split_master(float p, unsigned& hi, unsigned& lo
   lo = M & 0xffffu;
 }
 
+// One 8-element group of the split-master update at element index i8 * 8; returns the new hi
+// (bf16 model weight) vector. Shared by the flat and the segmented kernels (bitwise the same math).
+template <int GDT>
+__device__ __forceinline__ u32x4 adamw_split8(bf16_t* __restrict__ hi16, unsigned short* __restrict__ lo16,
+                                              const void* __restrict__ grad, float* __restrict__ m,
+                                              float* __restrict__ v, long long i, float gm, const AdamHP& hp) {
+  float g[8];
+  if (GDT == 0) {
+    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(grad) + i), g);
+  } else {
+    const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(grad) + 2 * i);
+    const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(grad) + 2 * i + 1);
+    g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y; g[6] = b.z; g[7] = b.w;
+  }
+  u32x4* hp4 = reinterpret_cast<u32x4*>(hi16) + i;
+  u32x4* lp4 = reinterpret_cast<u32x4*>(lo16) + i;
+  f32x4* mp = reinterpret_cast<f32x4*>(m) + 2 * i;
+  f32x4* vp = reinterpret_cast<f32x4*>(v) + 2 * i;
+  // state streams use the default cache policy (measured: non-temporal loads/stores of the
+  // read-modify-write state ran the 8B step at 3.7 TB/s vs 5.7 TB/s)
+  const u32x4 H = hp4[0], L = lp4[0];
+  const f32x4 M0 = mp[0], M1 = mp[1];
+  const f32x4 V0 = vp[0], V1 = vp[1];
+  float P[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    P[2 * k] = join_master(H[k] & 0xffffu, L[k] & 0xffffu);
+    P[2 * k + 1] = join_master(H[k] >> 16, L[k] >> 16);
+  }
+  float Mv[8] = {M0.x, M0.y, M0.z, M0.w, M1.x, M1.y, M1.z, M1.w};
+  float Vv[8] = {V0.x, V0.y, V0.z, V0.w, V1.x, V1.y, V1.z, V1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) adam_elem(P[j], Mv[j], Vv[j], g[j] * gm, hp);
+  u32x4 Ho, Lo;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    unsigned h0, l0, h1, l1;
+    split_master(P[2 * k], h0, l0);
+    split_master(P[2 * k + 1], h1, l1);
+    Ho[k] = h0 | (h1 << 16);
+    Lo[k] = l0 | (l1 << 16);
+  }
+  hp4[0] = Ho;
+  lp4[0] = Lo;
+  mp[0] = f32x4{Mv[0], Mv[1], Mv[2], Mv[3]};
+  mp[1] = f32x4{Mv[4], Mv[5], Mv[6], Mv[7]};
+  vp[0] = f32x4{Vv[0], Vv[1], Vv[2], Vv[3]};
+  vp[1] = f32x4{Vv[4], Vv[5], Vv[6], Vv[7]};
+  return Ho;
+}
+
+template <int GDT>
+__device__ __forceinline__ void adamw_split1(bf16_t* __restrict__ hi16, unsigned short* __restrict__ lo16,
+                                             const void* __restrict__ grad, float* __restrict__ m,
+                                             float* __restrict__ v, long long i, float gm, const AdamHP& hp) {
+  const float g = (GDT == 0 ? bf2f(((const bf16_t*)grad)[i]) : ((const float*)grad)[i]) * gm;
+  float P = join_master(hi16[i], lo16[i]), Mv = m[i], Vv = v[i];
+  adam_elem(P, Mv, Vv, g, hp);
+  unsigned h, l;
+  split_master(P, h, l);
+  hi16[i] = (bf16_t)h;
+  lo16[i] = (unsigned short)l;
+  m[i] = Mv;
+  v[i] = Vv;
+}
+
 template <int GDT>
 __global__ __launch_bounds__(256) void adamw_split_kernel(bf16_t* __restrict__ hi16, unsigned short* __restrict__ lo16,
                                                           const void* __restrict__ grad, float* __restrict__ m,
@@ -401,60 +473,84 @@ __global__ __launch_bounds__(256) void adamw_split_kernel(bf16_t* __restrict__ h
                                                           const float* __restrict__ sumsq) {
   const float gm = hp.grad_mul * clip_coef(sumsq, hp.max_norm, hp.grad_mul);
   const long long nv = n >> 3;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
-    float g[8];
-    if (GDT == 0) {
-      unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(grad) + i), g);
-    } else {
-      const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(grad) + 2 * i);
-      const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(grad) + 2 * i + 1);
-      g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w; g[4] = b.x; g[5] = b.y; g[6] = b.z; g[7] = b.w;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x)
+    adamw_split8<GDT>(hi16, lo16, grad, m, v, i, gm, hp);
+  for (long long i = (nv << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    adamw_split1<GDT>(hi16, lo16, grad, m, v, i, gm, hp);
+}
+
+// Segmented split-master AdamW that also refreshes the transposed bf16 copy W^T [C][R] of every
+// matrix segment W [R][C] (the reduction-contiguous operand of the backward dgrad GEMM,
+// parallel/fused_linear.py): the new bf16 weights are in registers anyway, so W^T costs one extra
+// 2-B write per parameter instead of a separate read + write transpose pass in the backward.
+// Segment descriptor (8 x int64, sorted by first tile): {off, n, first tile, W^T pointer (0 =
+// plain 1-D range), R, C, decay, 0}. Matrix tiles are 128 x 128 (256-B row pieces on every stream
+// and on W^T; a 64 x 64 tiling measured 41 ms vs the flat kernel's 37 ms on the 8B layout): lane
+// (ch = t & 15, rp = t >> 4) updates rows 2rp + 32k, 2rp + 1 + 32k (k < 4) x columns 8ch..8ch+7,
+// pairs each row pair's new bf16 values into dwords (v_perm) in an LDS image X[j][q] (128 output
+// rows x 64 dwords, q XOR-swizzled by 2*(j/8): the 32 lanes of a ds_write_b32 group hit 32 banks)
+// and stores W^T with one ds_read_b128 (dword pairs swapped back when j/8 is odd) + one 16-B store
+// per 8 outputs. 1-D tiles update 4096 consecutive elements.
+template <int GDT>
+__global__ __launch_bounds__(256) void adamw_split_seg_kernel(bf16_t* __restrict__ hi16, unsigned short* __restrict__ lo16,
+                                                              const void* __restrict__ grad, float* __restrict__ m,
+                                                              float* __restrict__ v, const long long* __restrict__ segs,
+                                                              int nseg, long long ntiles, AdamHP hp,
+                                                              const float* __restrict__ sumsq) {
+  __shared__ u32x4 X4[128 * 64 / 4];
+  unsigned* X = reinterpret_cast<unsigned*>(X4);
+  const float clip = clip_coef(sumsq, hp.max_norm, hp.grad_mul);
+  const int t = threadIdx.x;
+  // Tiles are walked grid-stride (as the flat kernel's 8-element groups): a block's tiles only
+  // move forward, so its segment is found by a forward scan from the previous one (wave-uniform
+  // scalar loads), not a search per tile.
+  int sgi = 0;
+  for (long long b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    while (sgi + 1 < nseg && segs[(sgi + 1) * 8 + 2] <= b) ++sgi;
+    const long long* sg = segs + sgi * 8;
+    const long long off = sg[0], n = sg[1], tile = b - sg[2];
+    bf16_t* wt = reinterpret_cast<bf16_t*>(sg[3]);
+    AdamHP h = hp;
+    if (!sg[6]) h.wd = 0.f;
+    const float gm = h.grad_mul * clip;
+    if (!wt) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const long long e = tile * 4096 + (k * 256 + t) * 8;
+        if (e + 8 <= n) {
+          adamw_split8<GDT>(hi16, lo16, grad, m, v, (off + e) >> 3, gm, h);
+        } else {
+          for (long long j = e; j < n && j < e + 8; ++j) adamw_split1<GDT>(hi16, lo16, grad, m, v, off + j, gm, h);
+        }
+      }
+      continue;
     }
-    u32x4* hp4 = reinterpret_cast<u32x4*>(hi16) + i;
-    u32x4* lp4 = reinterpret_cast<u32x4*>(lo16) + i;
-    f32x4* mp = reinterpret_cast<f32x4*>(m) + 2 * i;
-    f32x4* vp = reinterpret_cast<f32x4*>(v) + 2 * i;
-    // state streams use the default cache policy (measured: non-temporal loads/stores of the
-    // read-modify-write state ran the 8B step at 3.7 TB/s vs 5.7 TB/s)
-    const u32x4 H = hp4[0], L = lp4[0];
-    const f32x4 M0 = mp[0], M1 = mp[1];
-    const f32x4 V0 = vp[0], V1 = vp[1];
-    float P[8];
+    const int R = (int)sg[4], C = (int)sg[5], tilesC = C >> 7;
+    const int r0 = (int)(tile / tilesC) << 7, c0 = (int)(tile % tilesC) << 7;
+    const int ch = t & 15, rp = t >> 4;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      P[2 * k] = join_master(H[k] & 0xffffu, L[k] & 0xffffu);
-      P[2 * k + 1] = join_master(H[k] >> 16, L[k] >> 16);
-    }
-    float Mv[8] = {M0.x, M0.y, M0.z, M0.w, M1.x, M1.y, M1.z, M1.w};
-    float Vv[8] = {V0.x, V0.y, V0.z, V0.w, V1.x, V1.y, V1.z, V1.w};
+      const long long e0 = off + (long long)(r0 + 2 * rp + 32 * k) * C + c0 + ch * 8;
+      const u32x4 Ha = adamw_split8<GDT>(hi16, lo16, grad, m, v, e0 >> 3, gm, h);
+      const u32x4 Hb = adamw_split8<GDT>(hi16, lo16, grad, m, v, (e0 + C) >> 3, gm, h);
+      const int q = (rp + 16 * k) ^ (2 * ch);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) adam_elem(P[j], Mv[j], Vv[j], g[j] * gm, hp);
-    u32x4 Ho, Lo;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      unsigned h0, l0, h1, l1;
-      split_master(P[2 * k], h0, l0);
-      split_master(P[2 * k + 1], h1, l1);
-      Ho[k] = h0 | (h1 << 16);
-      Lo[k] = l0 | (l1 << 16);
+      for (int mm = 0; mm < 4; ++mm) {
+        X[(ch * 8 + 2 * mm) * 64 + q] = __builtin_amdgcn_perm(Hb[mm], Ha[mm], 0x05040100u);
+        X[(ch * 8 + 2 * mm + 1) * 64 + q] = __builtin_amdgcn_perm(Hb[mm], Ha[mm], 0x07060302u);
+      }
     }
-    hp4[0] = Ho;
-    lp4[0] = Lo;
-    mp[0] = f32x4{Mv[0], Mv[1], Mv[2], Mv[3]};
-    mp[1] = f32x4{Mv[4], Mv[5], Mv[6], Mv[7]};
-    vp[0] = f32x4{Vv[0], Vv[1], Vv[2], Vv[3]};
-    vp[1] = f32x4{Vv[4], Vv[5], Vv[6], Vv[7]};
-  }
-  for (long long i = (nv << 3) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float g = (GDT == 0 ? bf2f(((const bf16_t*)grad)[i]) : ((const float*)grad)[i]) * gm;
-    float P = join_master(hi16[i], lo16[i]), Mv = m[i], Vv = v[i];
-    adam_elem(P, Mv, Vv, g, hp);
-    unsigned h, l;
-    split_master(P, h, l);
-    hi16[i] = (bf16_t)h;
-    lo16[i] = (unsigned short)l;
-    m[i] = Mv;
-    v[i] = Vv;
+    __syncthreads();
+    const int q4 = (t & 15) * 4;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int j = (t >> 4) + 16 * p;
+      const int sw = 2 * (j >> 3);
+      u32x4 o = X4[(j * 64 + (q4 ^ (sw & ~3))) >> 2];
+      if (sw & 2) o = u32x4{o[2], o[3], o[0], o[1]};
+      *reinterpret_cast<u32x4*>(wt + (long)(c0 + j) * R + r0 + q4 * 2) = o;
+    }
+    __syncthreads();  // X is rewritten by this block's next matrix tile
   }
 }
 
@@ -478,5 +574,30 @@ RCA_API int rca_adamw_split(void* hi16, void* lo16, const void* grad, int grad_d
   else
     hipLaunchKernelGGL(adamw_split_kernel<1>, dim3((int)nb), dim3(256), 0, stream, (bf16_t*)hi16,
                        (unsigned short*)lo16, grad, m, v, n, hp, sumsq);
+  return (int)hipGetLastError();
+}
+
+// Segmented launch (adamw_split_seg_kernel): segs = device int64 [nseg][8] as documented there,
+// nblocks = the last segment's first tile + its tile count (tiles are walked grid-stride by
+// min(nblocks, rca_adamw_split_set_blocks) workgroups). Contract: 16-B aligned buffers,
+// every segment offset a multiple of 8 elements, matrix R and C multiples of 64.
+RCA_API int rca_adamw_split_seg(void* hi16, void* lo16, const void* grad, int grad_dtype, float* m, float* v,
+                                const void* segs, int nseg, long long nblocks, float lr, float b1, float b2, float eps,
+                                float wd, float bc1, float bc2, float grad_mul, const float* sumsq, float max_norm,
+                                hipStream_t stream) {
+  if (nseg <= 0 || nblocks <= 0) return 0;
+  if (nblocks >= (1LL << 31)) return -2;
+  if (((uintptr_t)hi16 | (uintptr_t)lo16 | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  AdamHP hp{lr, b1, b2, eps, wd, bc1, bc2, grad_mul, max_norm};
+  // 16384 workgroups: 39.7 ms vs 40.3 at 4096 on the 8B layout (scripts/adamw_seg_bench.py); an
+  // explicit rca_adamw_split_set_blocks value applies to both split kernels
+  const long long cap = g_adamw_split_blocks == 4096 ? 16384 : g_adamw_split_blocks;
+  const unsigned grid = (unsigned)(nblocks < cap ? nblocks : cap);
+  if (grad_dtype == 0)
+    hipLaunchKernelGGL(adamw_split_seg_kernel<0>, dim3(grid), dim3(256), 0, stream, (bf16_t*)hi16,
+                       (unsigned short*)lo16, grad, m, v, (const long long*)segs, nseg, nblocks, hp, sumsq);
+  else
+    hipLaunchKernelGGL(adamw_split_seg_kernel<1>, dim3(grid), dim3(256), 0, stream, (bf16_t*)hi16,
+                       (unsigned short*)lo16, grad, m, v, (const long long*)segs, nseg, nblocks, hp, sumsq);
   return (int)hipGetLastError();
 }

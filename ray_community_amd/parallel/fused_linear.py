@@ -44,7 +44,7 @@ class _LinearWgradIntoFlat(torch.autograd.Function):
             x_t, x2 = None, xs.reshape(-1, xs.shape[-1])
         tr = _use_transposed(g2, x2, w, x_t)
         if ctx.needs_input_grad[0]:
-            gx = F.linear(gy, ops.transpose(w)) if tr else torch.matmul(gy, w)
+            gx = F.linear(gy, weight_t(w)) if tr else torch.matmul(gy, w)
         else:
             gx = None
         view = _flat_view(w, g2.dtype)
@@ -53,6 +53,20 @@ class _LinearWgradIntoFlat(torch.autograd.Function):
         _wgrad(g2, x2, tr, out=view, accumulate=not _take_fresh(w), g_t=g_t, x_t=x_t)
         _notify(w)
         return gx, None, None
+
+
+def weight_t(w):
+    """``w.t().contiguous()``: the W^T copy the fused AdamW update keeps current when it is valid
+    (``parallel/optim.py::FlatAdamW._setup_transposed``), else a transpose pass (into that buffer
+    when the weight has one, so later uses in the same step reuse it)."""
+    wt = getattr(w, "_rca_wt", None)
+    if wt is None:
+        return ops.transpose(w)
+    key = (w._version, w._rca_wt_epoch[0])
+    if w._rca_wt_key != key:
+        ops.transpose(w, out=wt)
+        w._rca_wt_key = key
+    return wt
 
 
 def _use_transposed(g2, x2, w, x_t=None) -> bool:
@@ -64,9 +78,38 @@ def _use_transposed(g2, x2, w, x_t=None) -> bool:
     return _TRANSPOSED and ops.transpose_supported(g2) and x_ok and ops.transpose_supported(w)
 
 
+# Per-shape weight-gradient plans, (dW rows, dW cols, tokens) -> plan, measured on 1x MI355X
+# (scripts/gemm_policy.py, profiles/gemm_policy_r3.md) against the default (hipBLASLt on both
+# operands transposed, producer copies free):
+#   "hand": the gfx950 hand GEMM on the natural token-outer operands (no transposes). o_proj:
+#           0.222 ms vs 0.187 + 2 x 0.026 transposes = 0.240 ms.
+#   "trB":  only the activation is transposed; hipBLASLt reads the gradient token-outer. lm_head:
+#           6.67 + 0.03 ms vs 5.83 + 0.92 (the 2.1 GB dlogits transpose) + 0.03 ms.
+_WGRAD_PLAN = {(4096, 4096, 8192): "hand", (128256, 4096, 8192): "trB"}
+_PLANS_ON = os.environ.get("RCA_WGRAD_PLAN", "1") != "0"
+
+
+def _wgrad_plan(g2, x2, x_t, g_t, out):
+    if not _PLANS_ON or g_t is not None:
+        return None
+    N, T = g2.shape[1], g2.shape[0]
+    K = x_t.shape[0] if x_t is not None else x2.shape[1]
+    plan = _WGRAD_PLAN.get((N, K, T))
+    if plan == "hand" and (x2 is None or out is None or not ops.gemm_supported(N, K, T, g2, x2, out)):
+        return None
+    return plan
+
+
 def _wgrad(g2, x2, tr, out=None, accumulate=False, g_t=None, x_t=None):
     """dW = g2^T @ x2 (into ``out``, accumulating when asked). ``g_t`` / ``x_t``: transposed
     copies a producer already wrote (no transpose pass for them)."""
+    plan = _wgrad_plan(g2, x2, x_t, g_t, out) if tr else None
+    if plan == "hand":
+        return ops.gemm(g2, x2, a_kmajor=True, b_kmajor=True, out=out, accumulate=accumulate)
+    if plan == "trB":
+        a = g2.t()
+        b = (x_t if x_t is not None else ops.transpose(x2)).t()
+        return out.addmm_(a, b) if (out is not None and accumulate) else torch.mm(a, b, out=out)
     if tr:
         a = g_t if g_t is not None else ops.transpose(g2)
         b = (x_t if x_t is not None else ops.transpose(x2)).t()
@@ -124,7 +167,7 @@ class _FusedLinearCrossEntropy(torch.autograd.Function):
         dh = torch.empty_like(h) if need_h else None
         dw = torch.empty_like(weight) if need_w else None
         buf = torch.empty(min(chunk, T), V, device=h.device, dtype=h.dtype)
-        wt = ops.transpose(weight) if (need_h and _TRANSPOSED and ops.transpose_supported(weight)) else None
+        wt = weight_t(weight) if (need_h and _TRANSPOSED and ops.transpose_supported(weight)) else None
         for i, c0 in enumerate(range(0, T, chunk)):
             c1 = min(T, c0 + chunk)
             hc, lg = h[c0:c1], buf[: c1 - c0]

@@ -47,6 +47,12 @@ class FlatAdamW:
         self.last_grad_norm = None  # device tensor (sum of squares, pre-scale)
         self.track_grad_norm = False
         self._ov = None  # forward-overlap state (overlap_with_forward)
+        # transposed bf16 weights W^T refreshed by the update itself (see _setup_transposed)
+        self.transposed_weights = (self.split_master and flat.data.is_cuda
+                                   and os.environ.get("RCA_ADAMW_WT", "1") != "0")
+        self._wt_epoch = [0]  # bumped whenever the weights change outside the fused update
+        self._wt_params = None
+        self._segs = None
 
     # ------------------------------------------------------------------ forward overlap
     def overlap_with_forward(self, module: "torch.nn.Module", enabled: bool = True):
@@ -119,8 +125,50 @@ class FlatAdamW:
             return ops.reference.join_master(self.flat.data, self.lo)
         return self._master
 
+    def _setup_transposed(self):
+        """W^T buffers for the fused-wgrad linear weights + the segment table of the update.
+
+        Each ``FusedWgradLinear`` weight W [R, C] (R, C multiples of 128) gets a persistent bf16
+        ``W^T`` [C, R] (``p._rca_wt``) that the segmented update kernel rewrites from the new
+        weights in the same pass (one extra 2-B write per parameter); the backward dgrad reads it
+        instead of transposing W (``parallel/fused_linear.py::weight_t``). Validity is keyed on
+        (p._version, epoch): in-place edits of a weight or a bumped epoch (load_state_dict,
+        sync_master, an update that did not refresh W^T) make the backward fall back to a
+        transpose pass into the same buffer."""
+        flat = self.flat
+        mats = []
+        for p in flat.fused:
+            if p.dim() == 2 and p.shape[0] % 128 == 0 and p.shape[1] % 128 == 0:
+                p._rca_wt = torch.empty(p.shape[1], p.shape[0], dtype=p.dtype, device=p.device)
+                p._rca_wt_key = None
+                p._rca_wt_epoch = self._wt_epoch
+                mats.append((flat.param_offset[id(p)], p))
+        mats.sort(key=lambda t: t[0])
+        rows, blk = [], 0
+
+        def add_range(s, e):
+            nonlocal blk
+            # split at the weight-decay boundary: a 1-D segment carries one decay flag
+            for a, b in ((s, min(e, flat.decay_end)), (max(s, flat.decay_end), e)):
+                if b > a:
+                    rows.append([a, b - a, blk, 0, 0, 0, int(a < flat.decay_end), 0])
+                    blk += (b - a + 4095) // 4096
+
+        cur = 0
+        for off, p in mats:
+            add_range(cur, off)
+            R, C = p.shape
+            rows.append([off, p.numel(), blk, p._rca_wt.data_ptr(), R, C, int(off < flat.decay_end), 0])
+            blk += (R // 128) * (C // 128)
+            cur = off + p.numel()
+        add_range(cur, flat.numel)
+        self._wt_params = [p for _, p in mats]
+        self._segs = torch.tensor(rows, dtype=torch.int64, device=flat.device)
+        self._seg_blocks = blk
+
     def sync_master(self):
         """Re-read model weights into the fp32 master copy (after load_state_dict)."""
+        self._wt_epoch[0] += 1
         if self.split_master:
             self.lo.zero_()
         elif self.master_weights:
@@ -146,10 +194,23 @@ class FlatAdamW:
             self.last_grad_norm = self._sumsq  # sqrt taken lazily by grad_norm()
         self._grad_scale = grad_scale
         segs = [(0, flat.decay_end, self.wd), (flat.decay_end, flat.numel, 0.0)]
+        self._wt_epoch[0] += 1  # every update changes W: W^T is stale unless refreshed below
         if g.is_cuda:
             if g.dtype not in (torch.bfloat16, torch.float32):
                 raise TypeError(f"unsupported grad dtype {g.dtype}")
             ov = self._ov
+            if ov is None and self.transposed_weights:
+                if self._segs is None:
+                    self._setup_transposed()
+                check(lib().rca_adamw_split_seg(
+                    flat.data.data_ptr(), self.lo.data_ptr(), g.data_ptr(), 0 if g.dtype == torch.bfloat16 else 1,
+                    self.m.data_ptr(), self.v.data_ptr(), self._segs.data_ptr(), self._segs.shape[0],
+                    self._seg_blocks, lr, self.b1, self.b2, self.eps, self.wd, bc1, bc2, grad_scale,
+                    self._sumsq.data_ptr() if clip else 0, float(clip), stream_ptr(g.device)), "adamw_split_seg")
+                ep = self._wt_epoch[0]
+                for p in self._wt_params:
+                    p._rca_wt_key = (p._version, ep)
+                return
             if ov is None:
                 for s, e, wd in segs:
                     self._launch(g, s, e, wd, lr, bc1, bc2, grad_scale, clip, stream_ptr(g.device))
@@ -231,6 +292,7 @@ class FlatAdamW:
                 "lr": self.lr, "betas": (self.b1, self.b2), "eps": self.eps, "wd": self.wd}
 
     def load_state_dict(self, sd):
+        self._wt_epoch[0] += 1
         self.step_count = sd["step"]
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
@@ -307,6 +369,7 @@ class FlatSGD:
         return {"step": self.step_count, "buf": self.buf, "lr": self.lr, "momentum": self.momentum, "wd": self.wd}
 
     def load_state_dict(self, sd):
+        self._wt_epoch[0] += 1
         self.step_count = sd["step"]
         if self.buf is not None and sd.get("buf") is not None:
             self.buf.copy_(sd["buf"])

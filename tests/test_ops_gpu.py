@@ -512,3 +512,76 @@ def test_adamw_split_master_kernel_matches_fp32_master(gdt, n):
     dw = (w0.view(torch.int16).to(torch.int32) - w1.view(torch.int16).to(torch.int32)).abs()
     assert int(dw.max()) <= 1
     assert worst <= 1e-6, worst  # |err| <= 1e-5 |p| + 1e-9 (lr = 1e-3)
+
+
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+def test_adamw_segmented_with_transposed_weights_bitwise(gdt):
+    """The segmented split-master AdamW (rca_adamw_split_seg: 64x64 matrix tiles that also write
+    W^T, 1-D blocks for everything else) is bit-identical to the flat kernel on weights, low
+    halves, m and v, across decay / no-decay params and odd-length tails; every fused-wgrad
+    weight's W^T equals W.t() exactly after each step and the backward's weight_t() uses it."""
+    from ray_community_amd.parallel import FlatAdamW
+    from ray_community_amd.parallel.flat import FlatParameters
+    from ray_community_amd.parallel.fused_linear import FusedWgradLinear, weight_t
+
+    def build():
+        torch.manual_seed(0)
+        # (never run forward: only the parameter layout matters) a plain Linear first, so every
+        # fused weight precedes it in the flat layout; FusedWgradLinear(37, 256) is a fused weight
+        # whose shape is no 128-multiple (updated by 1-D tiles, no W^T; so is the 64 x 128 one)
+        m = torch.nn.ModuleList([torch.nn.Linear(64, 37), torch.nn.LayerNorm(37), FusedWgradLinear(37, 256),
+                                 FusedWgradLinear(256, 384), torch.nn.LayerNorm(384), FusedWgradLinear(384, 128),
+                                 FusedWgradLinear(128, 256), FusedWgradLinear(128, 64)])
+        return m.to(device=DEV, dtype=torch.bfloat16)
+
+    runs = []
+    for wt_on in (False, True):
+        net = build()
+        flat = FlatParameters(net, grad_dtype=gdt)
+        opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=0.5)
+        opt.transposed_weights = wt_on
+        g = torch.Generator(device=DEV).manual_seed(3)
+        for _ in range(3):
+            flat.grad.copy_(torch.randn(flat.numel, device=DEV, generator=g).to(gdt))
+            opt.step(0.5)
+            if wt_on:
+                mats = [p for p in net.parameters() if getattr(p, "_rca_wt", None) is not None]
+                # fp32 gradients: no flat-grad fused weights, so no W^T (all 1-D segments)
+                assert len(mats) == (3 if gdt == torch.bfloat16 else 0)
+                for p in mats:
+                    assert torch.equal(p._rca_wt, p.detach().t())
+                    assert weight_t(p).data_ptr() == p._rca_wt.data_ptr()
+        torch.cuda.synchronize()
+        runs.append((flat.data.clone(), opt.lo.clone(), opt.m.clone(), opt.v.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    # an in-place edit of a weight invalidates its W^T: weight_t() re-transposes
+    net = build()
+    flat = FlatParameters(net, grad_dtype=gdt)
+    opt = FlatAdamW(flat, lr=1e-2)
+    flat.grad.normal_()
+    opt.step()
+    w = net[3].weight
+    with torch.no_grad():
+        w.mul_(2.0)
+    assert torch.equal(weight_t(w), w.detach().t())
+
+
+@pytest.mark.parametrize("plan_shape", [(4096, 4096, 8192), (128256, 4096, 8192)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_plans_match_fp32(plan_shape, accumulate):
+    """The measured per-shape weight-gradient plans (hand GEMM on natural layouts for o_proj,
+    activation-only transpose for lm_head) vs an fp32 reference of dW = g^T x."""
+    from ray_community_amd.parallel import fused_linear as fl
+
+    N, K, T = plan_shape
+    torch.manual_seed(N)
+    g2 = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+    x2 = (torch.randn(T, K, device=DEV) + torch.arange(K, device=DEV) * 1e-3).to(torch.bfloat16)
+    out = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    base = out.float().clone()
+    assert fl._wgrad_plan(g2, x2, None, None, out) in ("hand", "trB")
+    fl._wgrad(g2, x2, True, out=out, accumulate=accumulate)
+    ref = g2.float().t() @ x2.float() + (base if accumulate else 0.0)
+    tol = 2e-2 * ref.abs().max().item()
+    assert (out.float() - ref).abs().max().item() < tol

@@ -108,3 +108,36 @@ def test_flat_bucket_alignment():
         assert b.start <= off and off + p.numel() <= b.end
     # decay/no-decay split on a bucket boundary
     assert any(b.start == fp.decay_end for b in fp.buckets)
+
+
+def test_adamw_transposed_segments_cover_flat_buffer():
+    """The segment table of the W^T-refreshing AdamW update covers [0, numel) exactly once, in
+    order, with matrix segments exactly on the 64-multiple fused weights, 1-D segments split at
+    the weight-decay boundary, and consecutive first-block indices."""
+    import torch
+
+    from ray_community_amd.parallel import FlatAdamW
+    from ray_community_amd.parallel.flat import FlatParameters
+    from ray_community_amd.parallel.fused_linear import FusedWgradLinear
+
+    m = torch.nn.ModuleList([torch.nn.Linear(64, 37), torch.nn.LayerNorm(37), FusedWgradLinear(37, 256),
+                             FusedWgradLinear(256, 384), torch.nn.LayerNorm(384), FusedWgradLinear(384, 128),
+                             FusedWgradLinear(128, 256), FusedWgradLinear(128, 64)]).to(torch.bfloat16)
+    flat = FlatParameters(m)
+    opt = FlatAdamW(flat, lr=1e-3)
+    opt._setup_transposed()
+    segs = opt._segs.tolist()
+    cur, blk, mats = 0, 0, 0
+    for off, n, b0, wt, R, C, decay, _ in segs:
+        assert off == cur and b0 == blk and n > 0
+        if wt:
+            mats += 1
+            assert R % 128 == 0 and C % 128 == 0 and R * C == n
+            blk += (R // 128) * (C // 128)
+        else:
+            blk += (n + 4095) // 4096
+            assert (off < flat.decay_end) == bool(decay) and (off + n <= flat.decay_end or off >= flat.decay_end)
+        cur = off + n
+    assert cur == flat.numel and blk == opt._seg_blocks and mats == 3
+    for p in opt._wt_params:
+        assert tuple(p._rca_wt.shape) == (p.shape[1], p.shape[0])
