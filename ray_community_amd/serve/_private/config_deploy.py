@@ -110,6 +110,9 @@ def build_specs(app_cfg: Dict[str, Any]) -> Tuple[List[Dict[str, Any]], str]:
             s["max_ongoing_requests"] = int(mo)
         if "user_config" in o:
             s["user_config"] = o["user_config"]
+        from ..api import _LIFECYCLE_DEFAULTS, _lifecycle_options
+
+        s.update(_lifecycle_options({k: o.get(k, s.get(k)) for k in _LIFECYCLE_DEFAULTS}))
         s["actor_options"] = _merge_actor_options(s.get("actor_options") or {}, o.get("ray_actor_options") or {}, env)
         s["code_version"] = code_version
     return list(specs.values()), ingress

@@ -26,6 +26,7 @@ class _DeploymentState:
         self.last_scale = 0.0
         self.counter = 0
         self.unhealthy_since = {}
+        self.health: Dict[str, float] = {}  # tag -> time of the last passed health check
 
 
 class ServeController:
@@ -129,20 +130,28 @@ class ServeController:
         return tag, r
 
     async def _stop_replicas(self, st, tags):
+        await asyncio.gather(*[self._stop_replica(st, t) for t in tags])
+
+    async def _stop_replica(self, st, t):
         from ..._private.worker import kill
 
-        for t in tags:
-            r = st.replicas.pop(t, None)
-            if r is None:
-                continue
-            try:
-                await asyncio.wait_for(r.prepare_for_shutdown.remote(), 5)
-            except Exception:
-                pass
-            try:
-                kill(r)
-            except Exception:
-                pass
+        r = st.replicas.pop(t, None)
+        if r is None:
+            return
+        st.health.pop(t, None)
+        # graceful shutdown (reference replica.py perform_graceful_shutdown): the replica is
+        # already out of the routing table; it drains its ongoing requests, polling every
+        # graceful_shutdown_wait_loop_s, and is killed after graceful_shutdown_timeout_s
+        loop_s = float(st.spec.get("graceful_shutdown_wait_loop_s", 2.0))
+        timeout_s = float(st.spec.get("graceful_shutdown_timeout_s", 20.0))
+        try:
+            await asyncio.wait_for(r.prepare_for_shutdown.remote(loop_s, timeout_s), timeout_s + 5)
+        except Exception:
+            pass
+        try:
+            kill(r)
+        except Exception:
+            pass
 
     async def _reconcile_all(self):
         for app, deps in list(self.apps.items()):
@@ -155,18 +164,34 @@ class ServeController:
                         await self._start_replica(st)
                 elif cur > st.target:
                     await self._stop_replicas(st, list(st.replicas)[st.target:])
-                # readiness
-                ready = 0
-                for tag, r in list(st.replicas.items()):
+                # readiness + periodic health checks: a replica is checked until it first passes
+                # (constructor still running: a timeout is "not ready yet"), then every
+                # health_check_period_s; after that a failed or timed-out check (> health_check_
+                # timeout_s) replaces it (reference deployment_state.py check_health)
+                period = float(st.spec.get("health_check_period_s", 10.0))
+                hto = float(st.spec.get("health_check_timeout_s", 30.0))
+                now = time.time()
+                due = [(tag, r) for tag, r in list(st.replicas.items())
+                       if tag not in st.health or now - st.health[tag] >= period]
+                results = await asyncio.gather(*[asyncio.wait_for(r.check_health.remote(), hto) for _, r in due],
+                                               return_exceptions=True)
+                for (tag, r), res in zip(due, results):
+                    if not isinstance(res, BaseException):
+                        st.health[tag] = time.time()
+                        continue
+                    if isinstance(res, asyncio.TimeoutError) and tag not in st.health:
+                        continue  # never ready yet
+                    st.message = f"replica {tag} failed its health check: {type(res).__name__}: {res}"
+                    st.replicas.pop(tag, None)
+                    st.health.pop(tag, None)
+                    failed = True
                     try:
-                        await asyncio.wait_for(r.check_health.remote(), 30)
-                        ready += 1
-                    except asyncio.TimeoutError:
+                        from ..._private.worker import kill
+
+                        kill(r)
+                    except Exception:  # noqa
                         pass
-                    except Exception as e:  # noqa
-                        st.message = f"replica {tag} failed: {e}"
-                        st.replicas.pop(tag, None)
-                        failed = True
+                ready = sum(1 for tag in st.replicas if tag in st.health)
                 if ready >= st.target and st.target > 0:
                     st.status = "HEALTHY"
                 elif failed:
@@ -226,7 +251,7 @@ class ServeController:
         if st is None:
             return None
         return {"replicas": list(st.replicas.items()), "max_ongoing_requests": st.spec.get("max_ongoing_requests", 5),
-                "version": st.version}
+                "max_queued_requests": st.spec.get("max_queued_requests", -1), "version": st.version}
 
     async def get_ingress(self, app_name: str):
         meta = self.app_meta.get(app_name)

@@ -18,6 +18,8 @@ import importlib
 import json
 import threading
 import time
+
+from ..exceptions import BackPressureError
 from concurrent import futures
 from typing import Dict, List, Optional
 
@@ -148,6 +150,8 @@ class _Router:
                 try:
                     for item in h.remote(req):
                         yield item
+                except BackPressureError as e:
+                    ctx.abort(grpc.StatusCode.UNAVAILABLE, e.message)
                 except Exception as e:  # noqa
                     ctx.abort(grpc.StatusCode.INTERNAL, f"{type(e).__name__}: {e}")
 
@@ -157,6 +161,8 @@ class _Router:
             h = self.proxy.handle_for(ctx, method)
             try:
                 return h.remote(req).result()
+            except BackPressureError as e:
+                ctx.abort(grpc.StatusCode.UNAVAILABLE, e.message)
             except Exception as e:  # noqa
                 ctx.abort(grpc.StatusCode.INTERNAL, f"{type(e).__name__}: {e}")
 

@@ -10,9 +10,11 @@ from typing import Dict, Optional
 
 
 class HTTPProxy:
-    def __init__(self, host: str = "127.0.0.1", port: int = 8000):
+    def __init__(self, host: str = "127.0.0.1", port: int = 8000, request_timeout_s: Optional[float] = None):
         self.host = host
         self.port = port
+        # end-to-end request timeout (HTTPOptions.request_timeout_s): 408 if no response started
+        self.request_timeout_s = request_timeout_s if request_timeout_s and request_timeout_s > 0 else None
         self.routes: Dict[str, tuple] = {}
         self.last_routes = 0.0
         self._server = None
@@ -77,22 +79,42 @@ class HTTPProxy:
                "root_path": root}
         from ..handle import _Router
 
+        from ..exceptions import BackPressureError
+
         started = False
+        deadline = None if self.request_timeout_s is None else time.monotonic() + self.request_timeout_s
+
+        def left():
+            return None if deadline is None else max(0.0, deadline - time.monotonic())
+
         try:
             router = _Router.get(app_name, ingress)
             loop = asyncio.get_running_loop()
             fut = await loop.run_in_executor(None, router.submit, None, (req,), {}, {}, "handle_http_stream")
-            gen, _ = await asyncio.wrap_future(fut)
+            gen, _ = await asyncio.wait_for(asyncio.wrap_future(fut), left())
             # streamed response: each message is forwarded the moment the replica produces it
-            async for ref in gen:
-                msg = await ref
+            it = gen.__aiter__()
+            while True:
+                try:
+                    ref = await asyncio.wait_for(it.__anext__(), left())
+                except StopAsyncIteration:
+                    break
+                msg = await asyncio.wait_for(ref, left())
                 if msg[0] == "start":
                     await send({"type": "http.response.start", "status": msg[1],
                                 "headers": [(k.encode(), v.encode()) for k, v in msg[2]]})
                     started = True
                 else:
                     await send({"type": "http.response.body", "body": msg[1], "more_body": True})
-            await gen.completed()  # surfaces a replica-side failure
+            await asyncio.wait_for(gen.completed(), left())  # surfaces a replica-side failure
+        except asyncio.TimeoutError:
+            if not started:
+                await _respond(send, 408, f"Request timed out after {self.request_timeout_s}s.".encode())
+                return
+        except BackPressureError as e:
+            if not started:
+                await _respond(send, 503, e.message.encode())
+                return
         except Exception as e:  # noqa
             if not started:
                 await _respond(send, 500, f"Internal Server Error: {e}".encode())

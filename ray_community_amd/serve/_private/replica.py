@@ -197,9 +197,21 @@ class ServeReplica:
     async def stats(self):
         return {"ongoing": self.ongoing, "total": self.total, "pid": os.getpid(), "tag": self.tag}
 
-    async def prepare_for_shutdown(self):
-        deadline = time.time() + 5
+    async def prepare_for_shutdown(self, wait_loop_s: float = 2.0, timeout_s: float = 20.0):
+        """Graceful shutdown (reference replica.py perform_graceful_shutdown): the controller has
+        already removed this replica from routing; sleep one wait-loop period so callers' routers
+        see that, then poll until the ongoing requests drain (or ``timeout_s``), then run the
+        user's destructor."""
+        deadline = time.time() + max(0.0, timeout_s)
+        await asyncio.sleep(max(0.0, min(wait_loop_s, timeout_s)))
         while self.ongoing > 0 and time.time() < deadline:
-            await asyncio.sleep(0.05)
+            await asyncio.sleep(min(max(wait_loop_s, 0.01), max(0.0, deadline - time.time())) or 0.01)
         d = getattr(self.obj, "__del__", None)
-        return True
+        if d is not None:
+            try:
+                r = d()
+                if inspect.isawaitable(r):
+                    await r
+            except Exception:  # noqa  (a failing destructor must not block the shutdown)
+                pass
+        return self.ongoing

@@ -96,8 +96,22 @@ class Application:
                      "autoscaling_config": ac if ac else ({"min_replicas": 1, "max_replicas": 100,
                                                            "target_ongoing_requests": 2}
                                                           if cfg.get("num_replicas") == "auto" else None),
-                     "user_config": cfg.get("user_config"), "_app": self}
+                     "user_config": cfg.get("user_config"), "_app": self,
+                     **_lifecycle_options(cfg)}
         return name
+
+
+# replica lifecycle options and their reference defaults (serve/config.py DeploymentConfig)
+_LIFECYCLE_DEFAULTS = {"max_queued_requests": -1, "health_check_period_s": 10.0, "health_check_timeout_s": 30.0,
+                       "graceful_shutdown_wait_loop_s": 2.0, "graceful_shutdown_timeout_s": 20.0}
+
+
+def _lifecycle_options(cfg: Dict) -> Dict:
+    out = {}
+    for k, d in _LIFECYCLE_DEFAULTS.items():
+        v = cfg.get(k)
+        out[k] = d if v is None else (int(v) if k == "max_queued_requests" else float(v))
+    return out
 
 
 def deployment(_func_or_class=None, *, name: Optional[str] = None, num_replicas: Union[int, str, None] = None,
@@ -108,7 +122,12 @@ def deployment(_func_or_class=None, *, name: Optional[str] = None, num_replicas:
                placement_group_bundles=None, placement_group_strategy=None, logging_config=None):
     cfg = {k: v for k, v in dict(num_replicas=num_replicas, ray_actor_options=ray_actor_options,
                                  max_ongoing_requests=max_ongoing_requests or max_concurrent_queries,
-                                 autoscaling_config=autoscaling_config, user_config=user_config).items()
+                                 autoscaling_config=autoscaling_config, user_config=user_config,
+                                 max_queued_requests=max_queued_requests,
+                                 health_check_period_s=health_check_period_s,
+                                 health_check_timeout_s=health_check_timeout_s,
+                                 graceful_shutdown_wait_loop_s=graceful_shutdown_wait_loop_s,
+                                 graceful_shutdown_timeout_s=graceful_shutdown_timeout_s).items()
            if v is not None}
     if num_replicas is not None and autoscaling_config is not None and num_replicas != "auto":
         raise ValueError("Manually setting num_replicas is not allowed when autoscaling_config is provided.")
@@ -143,8 +162,10 @@ def start(http_options: Optional[Dict] = None, detached: bool = True, proxy_loca
     ``grpc_servicer_functions`` (``add_<Service>Servicer_to_server`` callables or import paths)."""
     if http_options:
         if not isinstance(http_options, dict):
-            http_options = {"host": getattr(http_options, "host", None), "port": getattr(http_options, "port", None)}
-        _STATE["http"].update({k: v for k, v in http_options.items() if k in ("host", "port") and v is not None})
+            http_options = {"host": getattr(http_options, "host", None), "port": getattr(http_options, "port", None),
+                            "request_timeout_s": getattr(http_options, "request_timeout_s", None)}
+        _STATE["http"].update({k: v for k, v in http_options.items()
+                               if k in ("host", "port", "request_timeout_s") and v is not None})
     if grpc_options is not None:
         if not isinstance(grpc_options, dict):
             grpc_options = {"host": getattr(grpc_options, "host", "127.0.0.1"), "port": grpc_options.port,
@@ -186,7 +207,8 @@ def _ensure_proxy():
         p = w.get_actor("SERVE_PROXY_ACTOR", namespace=NAMESPACE)
     except ValueError:
         p = ActorClass(HTTPProxy, {"name": "SERVE_PROXY_ACTOR", "namespace": NAMESPACE, "lifetime": "detached",
-                                   "num_cpus": 0, "max_concurrency": 100}).remote(h["host"], h["port"])
+                                   "num_cpus": 0, "max_concurrency": 100}).remote(h["host"], h["port"],
+                                                                                 h.get("request_timeout_s"))
     w.get(p.ready.remote())
     _STATE["proxy"] = p
 

@@ -54,6 +54,7 @@ class _Router:
         self.replicas: List[Tuple[str, Any]] = []
         self.inflight: Dict[str, int] = {}
         self.max_ongoing = 5
+        self.max_queued = -1  # max_queued_requests (-1: unbounded)
         self.last_refresh = 0.0
         self.cv = threading.Condition()
         self.queue: "collections.deque" = collections.deque()
@@ -83,6 +84,7 @@ class _Router:
         with self.cv:
             self.replicas = info["replicas"]
             self.max_ongoing = info["max_ongoing_requests"]
+            self.max_queued = int(info.get("max_queued_requests", -1))
             live = {t for t, _ in self.replicas}
             for tag in live:
                 self.inflight.setdefault(tag, 0)
@@ -118,8 +120,17 @@ class _Router:
         fut: concurrent.futures.Future = concurrent.futures.Future()
         self._refresh()
         with self.cv:
-            self.queue.append((actor_method, method, args, kwargs, meta, fut))
+            item = (actor_method, method, args, kwargs, meta, fut)
+            self.queue.append(item)
             self._drain_locked()
+            # backpressure (reference router.py wrap_request_assignment): a request no replica
+            # can take right now is dropped once max_queued_requests others are already waiting
+            if self.max_queued >= 0 and self.queue and self.queue[-1] is item and len(self.queue) > self.max_queued:
+                self.queue.pop()
+                from .exceptions import BackPressureError
+
+                fut.set_exception(BackPressureError(num_queued_requests=len(self.queue),
+                                                    max_queued_requests=self.max_queued))
             pending = bool(self.queue)
         if pending:
             self._ensure_drainer()

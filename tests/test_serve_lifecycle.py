@@ -1,0 +1,166 @@
+"""Serve request/replica lifecycle options (reference: serve/config.py DeploymentConfig, HTTPOptions;
+_private/router.py backpressure, _private/proxy.py request timeouts, _private/replica.py graceful
+shutdown, _private/deployment_state.py health checks)."""
+import concurrent.futures
+import os
+import threading
+import time
+
+import pytest
+import requests
+
+import ray_community_amd as ray
+from ray_community_amd import serve
+from ray_community_amd.serve.exceptions import BackPressureError, RayServeException
+
+PORT = 18131
+
+
+@pytest.fixture
+def serve_instance():
+    ray.init(num_cpus=8, log_to_driver=False)
+    serve.start(http_options={"port": PORT, "request_timeout_s": 1.5})
+    yield
+    serve.shutdown()
+    ray.shutdown()
+
+
+def test_max_queued_requests_rejects_with_backpressure(serve_instance):
+    @serve.deployment(max_ongoing_requests=1, max_queued_requests=1)
+    class Slow:
+        def __call__(self, s):
+            time.sleep(s)
+            return "done"
+
+    h = serve.run(Slow.bind(), name="bp", route_prefix="/bp")
+    assert h.remote(0).result() == "done"
+    first = h.remote(2.0)   # occupies the only replica slot
+    time.sleep(0.3)
+    second = h.remote(0)    # waits in the caller's queue (1 allowed)
+    third = h.remote(0)     # over max_queued_requests
+    with pytest.raises(BackPressureError) as ei:
+        third.result(timeout_s=10)
+    assert isinstance(ei.value, RayServeException) and "max_queued_requests=1" in ei.value.message
+    assert first.result(timeout_s=30) == "done" and second.result(timeout_s=30) == "done"
+    # once the queue drained, requests are accepted again
+    assert h.remote(0).result(timeout_s=30) == "done"
+
+
+def test_http_backpressure_is_503_and_timeout_is_408(serve_instance):
+    @serve.deployment(max_ongoing_requests=1, max_queued_requests=0)
+    class Web:
+        async def __call__(self, request):
+            s = float(request.query_params.get("s", "0"))
+            import asyncio
+
+            await asyncio.sleep(s)
+            return {"slept": s}
+
+    serve.run(Web.bind(), name="web", route_prefix="/web")
+    url = f"http://127.0.0.1:{PORT}/web"
+    assert requests.get(url, params={"s": 0}, timeout=30).json() == {"slept": 0.0}
+    with concurrent.futures.ThreadPoolExecutor(2) as pool:
+        slow = pool.submit(requests.get, url, params={"s": 1.0}, timeout=30)
+        time.sleep(0.4)
+        rejected = requests.get(url, params={"s": 0}, timeout=30)
+        assert rejected.status_code == 503 and "backpressure" in rejected.text
+        assert slow.result().status_code == 200
+    # HTTPOptions.request_timeout_s = 1.5: a 4 s request gets 408 before it finishes
+    t0 = time.time()
+    r = requests.get(url, params={"s": 4}, timeout=30)
+    assert r.status_code == 408 and "timed out" in r.text
+    assert time.time() - t0 < 3.5
+
+
+def test_graceful_shutdown_drains_ongoing_requests(serve_instance):
+    @serve.deployment(graceful_shutdown_wait_loop_s=0.2, graceful_shutdown_timeout_s=10)
+    class Drain:
+        def __call__(self, s):
+            time.sleep(s)
+            return os.getpid()
+
+    h = serve.run(Drain.bind(), name="drain", route_prefix=None)
+    h.remote(0).result()
+    inflight = h.remote(2.0)
+    time.sleep(0.3)
+    done = threading.Event()
+
+    def delete():
+        serve.delete("drain")
+        done.set()
+
+    t = threading.Thread(target=delete)
+    t.start()
+    # the in-flight request completes although the app is being deleted
+    assert isinstance(inflight.result(timeout_s=30), int)
+    t.join(30)
+    assert done.is_set()
+
+
+def test_graceful_shutdown_timeout_bounds_the_wait(serve_instance):
+    @serve.deployment(graceful_shutdown_wait_loop_s=0.1, graceful_shutdown_timeout_s=0.5)
+    class Stuck:
+        def __call__(self):
+            time.sleep(30)
+
+    h = serve.run(Stuck.bind(), name="stuck", route_prefix=None)
+    h.remote()
+    time.sleep(0.5)
+    t0 = time.time()
+    serve.delete("stuck")
+    assert time.time() - t0 < 10
+
+
+def test_health_check_period_and_timeout(serve_instance):
+    """A health check that hangs longer than health_check_timeout_s marks the replica failed and
+    the controller replaces it; the check runs every health_check_period_s."""
+
+    @serve.deployment(health_check_period_s=0.2, health_check_timeout_s=1.0)
+    class Hang:
+        def __init__(self):
+            self.hang = False
+            self.checks = 0
+
+        def check_health(self):
+            self.checks += 1
+            if self.hang:
+                time.sleep(30)
+
+        def n_checks(self):
+            return self.checks
+
+        def start_hanging(self):
+            self.hang = True
+            return os.getpid()
+
+        def __call__(self):
+            return os.getpid()
+
+    h = serve.run(Hang.bind(), name="hang", route_prefix=None)
+    c0 = h.n_checks.remote().result()
+    time.sleep(1.5)
+    assert h.n_checks.remote().result() >= c0 + 3  # periodic
+    pid = h.start_hanging.remote().result()
+    deadline = time.time() + 60
+    while time.time() < deadline:
+        try:
+            if h.remote().result(timeout_s=5) != pid:
+                break
+        except Exception:  # noqa
+            pass
+        time.sleep(0.3)
+    assert h.remote().result(timeout_s=10) != pid
+
+
+def test_lifecycle_options_reach_the_spec():
+    from ray_community_amd.serve.api import _lifecycle_options
+
+    @serve.deployment(max_queued_requests=7, health_check_period_s=3, graceful_shutdown_timeout_s=9)
+    def f():
+        return 1
+
+    spec = _lifecycle_options(f._config)
+    assert spec == {"max_queued_requests": 7, "health_check_period_s": 3.0, "health_check_timeout_s": 30.0,
+                    "graceful_shutdown_wait_loop_s": 2.0, "graceful_shutdown_timeout_s": 9.0}
+    g = f.options(max_queued_requests=2)
+    assert _lifecycle_options(g._config)["max_queued_requests"] == 2
