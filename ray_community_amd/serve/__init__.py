@@ -19,7 +19,10 @@ class AutoscalingConfig:
 
 class HTTPOptions:
     """HTTP proxy options for ``serve.start(http_options=HTTPOptions(...))`` (reference
-    ``serve/config.py``): ``host``/``port`` are used by the proxy; the rest are accepted."""
+    ``serve/config.py``): ``host``/``port`` bind the proxy, ``request_timeout_s`` bounds each HTTP
+    request (408), ``keep_alive_timeout_s`` is the server's keep-alive and ``root_path`` the ASGI
+    root path (serving behind a path-prefixing reverse proxy). ``location`` is informational: one
+    proxy runs on the head."""
 
     def __init__(self, host: str = "127.0.0.1", port: int = 8000, root_path: str = "", location: str = "HeadOnly",
                  request_timeout_s=None, keep_alive_timeout_s: int = 5, **kw):

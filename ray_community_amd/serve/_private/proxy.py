@@ -10,9 +10,12 @@ from typing import Dict, Optional
 
 
 class HTTPProxy:
-    def __init__(self, host: str = "127.0.0.1", port: int = 8000, request_timeout_s: Optional[float] = None):
+    def __init__(self, host: str = "127.0.0.1", port: int = 8000, request_timeout_s: Optional[float] = None,
+                 keep_alive_timeout_s: int = 5, root_path: str = ""):
         self.host = host
         self.port = port
+        self.keep_alive_timeout_s = int(keep_alive_timeout_s)
+        self.root_path = root_path or ""
         # end-to-end request timeout (HTTPOptions.request_timeout_s): 408 if no response started
         self.request_timeout_s = request_timeout_s if request_timeout_s and request_timeout_s > 0 else None
         self.routes: Dict[str, tuple] = {}
@@ -30,7 +33,8 @@ class HTTPProxy:
         import uvicorn
 
         config = uvicorn.Config(self._app, host=self.host, port=self.port, log_level="warning", lifespan="off",
-                                interface="asgi3")
+                                interface="asgi3", timeout_keep_alive=self.keep_alive_timeout_s,
+                                root_path=self.root_path)
         self._server = uvicorn.Server(config)
         self._server.run()
 

@@ -162,10 +162,11 @@ def start(http_options: Optional[Dict] = None, detached: bool = True, proxy_loca
     ``grpc_servicer_functions`` (``add_<Service>Servicer_to_server`` callables or import paths)."""
     if http_options:
         if not isinstance(http_options, dict):
-            http_options = {"host": getattr(http_options, "host", None), "port": getattr(http_options, "port", None),
-                            "request_timeout_s": getattr(http_options, "request_timeout_s", None)}
+            http_options = {k: getattr(http_options, k, None)
+                            for k in ("host", "port", "request_timeout_s", "keep_alive_timeout_s", "root_path")}
         _STATE["http"].update({k: v for k, v in http_options.items()
-                               if k in ("host", "port", "request_timeout_s") and v is not None})
+                               if k in ("host", "port", "request_timeout_s", "keep_alive_timeout_s", "root_path")
+                               and v is not None})
     if grpc_options is not None:
         if not isinstance(grpc_options, dict):
             grpc_options = {"host": getattr(grpc_options, "host", "127.0.0.1"), "port": grpc_options.port,
@@ -207,8 +208,8 @@ def _ensure_proxy():
         p = w.get_actor("SERVE_PROXY_ACTOR", namespace=NAMESPACE)
     except ValueError:
         p = ActorClass(HTTPProxy, {"name": "SERVE_PROXY_ACTOR", "namespace": NAMESPACE, "lifetime": "detached",
-                                   "num_cpus": 0, "max_concurrency": 100}).remote(h["host"], h["port"],
-                                                                                 h.get("request_timeout_s"))
+                                   "num_cpus": 0, "max_concurrency": 100}).remote(
+            h["host"], h["port"], h.get("request_timeout_s"), h.get("keep_alive_timeout_s", 5), h.get("root_path", ""))
     w.get(p.ready.remote())
     _STATE["proxy"] = p
 
