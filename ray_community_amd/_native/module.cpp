@@ -1,5 +1,5 @@
 // _rca_native: C++ runtime core (shared-memory object store, cluster resource scheduler, I/O reactor,
-// object reference table).
+// object reference table, internal KV).
 #include <pybind11/pybind11.h>
 
 namespace py = pybind11;
@@ -8,6 +8,7 @@ void register_store(py::module_& m);
 void register_scheduler(py::module_& m);
 void register_reactor(py::module_& m);
 void register_ref_table(py::module_& m);
+void register_kv_table(py::module_& m);
 
 PYBIND11_MODULE(_rca_native, m) {
   m.doc() = "ray_community_amd native runtime core";
@@ -15,4 +16,5 @@ PYBIND11_MODULE(_rca_native, m) {
   register_scheduler(m);
   register_reactor(m);
   register_ref_table(m);
+  register_kv_table(m);
 }

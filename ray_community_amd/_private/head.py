@@ -228,7 +228,7 @@ class Head:
         self.nodes: Dict[str, NodeState] = {}
         self.pgs: Dict[bytes, dict] = {}
         self.pending_pgs: List[bytes] = []
-        self.kv: Dict[tuple, bytes] = {}
+        self.kv = native().KvTable()  # internal KV (GCS InternalKV)
         self.functions: Dict[bytes, bytes] = {}
         self.events: collections.deque = collections.deque(maxlen=int(self.config.get("task_events_max", 100000)))
         self.finished_tasks: collections.deque = collections.deque(maxlen=10000)
@@ -2334,30 +2334,22 @@ class Head:
         return out
 
     # ================================================================== KV
+    # byte keys/values in namespaces, in C++ (_native/kv_table.cpp: ordered per namespace, so
+    # prefix listing / deletion touch only the matching range); str keys are stored as UTF-8
     def rpc_kv_put(self, caller, key, value, overwrite=True, namespace=None):
-        k = (namespace, key)
-        if not overwrite and k in self.kv:
-            return False
-        existed = k in self.kv
-        self.kv[k] = value
-        return not existed
+        return self.kv.put(key, value, overwrite, namespace)
 
     def rpc_kv_get(self, caller, key, namespace=None):
-        return self.kv.get((namespace, key))
+        return self.kv.get(key, namespace)
 
     def rpc_kv_del(self, caller, key, namespace=None, del_by_prefix=False):
-        if del_by_prefix:
-            ks = [k for k in self.kv if k[0] == namespace and k[1].startswith(key)]
-            for k in ks:
-                del self.kv[k]
-            return len(ks)
-        return 1 if self.kv.pop((namespace, key), None) is not None else 0
+        return self.kv.delete(key, namespace, del_by_prefix)
 
     def rpc_kv_keys(self, caller, prefix, namespace=None):
-        return [k[1] for k in self.kv if k[0] == namespace and k[1].startswith(prefix)]
+        return self.kv.keys(prefix, namespace)
 
     def rpc_kv_exists(self, caller, key, namespace=None):
-        return (namespace, key) in self.kv
+        return self.kv.exists(key, namespace)
 
     # ================================================================== state / observability
     def _event(self, ts, what, worker=None):

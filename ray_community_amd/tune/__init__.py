@@ -5,7 +5,7 @@ import functools
 import inspect
 from typing import Any, Callable, Dict, Optional
 
-from ..air.config import CheckpointConfig, FailureConfig, RunConfig
+from ..air.config import CheckpointConfig, FailureConfig, RunConfig, SyncConfig
 from ..air.result import Result
 from ..train._checkpoint import Checkpoint
 from .schedulers import (ASHAScheduler, AsyncHyperBandScheduler, FIFOScheduler, HyperBandScheduler,
@@ -155,7 +155,7 @@ class Callback:
         pass
 
 
-__all__ = ["Tuner", "TuneConfig", "ResultGrid", "Trainable", "Stopper", "report", "get_checkpoint", "get_context",
+__all__ = ["SyncConfig", "Tuner", "TuneConfig", "ResultGrid", "Trainable", "Stopper", "report", "get_checkpoint", "get_context",
            "run", "with_resources", "with_parameters", "choice", "uniform", "quniform", "loguniform", "qloguniform",
            "randn", "qrandn", "randint", "qrandint", "lograndint", "qlograndint", "sample_from", "grid_search",
            "ASHAScheduler", "AsyncHyperBandScheduler", "HyperBandScheduler", "MedianStoppingRule",

@@ -101,3 +101,36 @@ def test_head_table_tracks_driver_refs(ray_start_regular):
     while time.time() < deadline and any(head.refs.contains(o) for o in oids):
         time.sleep(0.05)
     assert not any(head.refs.contains(o) for o in oids)
+
+
+def test_kv_table_namespaces_prefixes_and_overwrite():
+    """Native internal KV (GCS InternalKV semantics): put reports whether the key was added,
+    overwrite=False keeps the old value, None and b"" namespaces are distinct, prefix listing and
+    prefix deletion see only matching keys of that namespace."""
+    kv = native().KvTable()
+    assert kv.put(b"job:1", b"a") and not kv.put(b"job:1", b"b", False)
+    assert kv.get(b"job:1") == b"a"
+    assert not kv.put("job:1", "c") and kv.get(b"job:1") == b"c"  # str keys are UTF-8 bytes
+    kv.put(b"job:2", b"x")
+    kv.put(b"jobx", b"y")
+    kv.put(b"job:1", b"other", True, b"ns")
+    kv.put(b"job:9", b"empty-ns", True, b"")
+    assert kv.keys(b"job:") == [b"job:1", b"job:2"]
+    assert kv.keys(b"job", b"ns") == [b"job:1"] and kv.keys(b"job", b"") == [b"job:9"]
+    assert kv.get(b"job:1", b"ns") == b"other" and kv.get(b"missing") is None
+    assert kv.delete(b"job:", None, True) == 2 and kv.keys(b"job") == [b"jobx"]
+    assert kv.exists(b"job:1", b"ns") and not kv.exists(b"job:1")
+    assert kv.delete(b"job:1", b"ns") == 1 and kv.delete(b"job:1", b"ns") == 0
+    assert len(kv) == 2 and kv.nbytes() == len(b"y") + len(b"empty-ns")
+
+
+def test_internal_kv_through_the_head(ray_start_regular):
+    from ray_community_amd.experimental import internal_kv as ikv
+
+    assert not ikv._internal_kv_put(b"k1", b"v1")
+    assert ikv._internal_kv_put(b"k1", b"v2")  # existed
+    assert ikv._internal_kv_get(b"k1") == b"v2"
+    ikv._internal_kv_put("k2", "v", namespace="n")
+    assert ikv._internal_kv_list(b"k", namespace="n") == [b"k2"]
+    assert ikv._internal_kv_del(b"k", del_by_prefix=True) == 1
+    assert not ikv._internal_kv_exists(b"k1")
