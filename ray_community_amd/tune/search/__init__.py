@@ -180,20 +180,62 @@ class RandomSearch(Searcher):
         return generate_variants(self.space, 1, self._rng)[0]
 
 
+TRIAL_INDEX = "__trial_index__"
+
+
 class Repeater(Searcher):
+    """Evaluates every configuration of the wrapped searcher ``repeat`` times (reference
+    ``tune/search/repeater.py``): the copies carry ``config[TRIAL_INDEX]`` = 0..repeat-1 when
+    ``set_index``, and once all copies of a configuration completed the wrapped searcher is told
+    ONE completion with the mean of their ``metric`` (so model-based searchers see averaged,
+    less noisy scores)."""
+
     def __init__(self, searcher: Searcher, repeat: int = 1, set_index: bool = True):
         super().__init__(searcher.metric, searcher.mode)
         self.searcher = searcher
-        self.repeat = repeat
+        self.repeat = max(1, int(repeat))
+        self.set_index = set_index
         self._current = None
         self._left = 0
+        self._group = -1
+        self._group_of: Dict[str, int] = {}
+        self._groups: Dict[int, Dict] = {}  # group -> {"first": trial id, "scores": [...], "done": n}
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        super().set_search_properties(metric, mode, config)
+        return self.searcher.set_search_properties(metric, mode, config, **spec)
 
     def suggest(self, trial_id):
         if self._left == 0:
-            self._current = self.searcher.suggest(trial_id)
+            cfg = self.searcher.suggest(trial_id)
+            if cfg is None or cfg == Searcher.FINISHED:
+                return cfg
+            self._current = cfg
             self._left = self.repeat
+            self._group += 1
+            self._groups[self._group] = {"first": trial_id, "scores": [], "done": 0}
+        idx = self.repeat - self._left
         self._left -= 1
-        return copy.deepcopy(self._current)
+        self._group_of[trial_id] = self._group
+        cfg = copy.deepcopy(self._current)
+        if self.set_index and isinstance(cfg, dict):
+            cfg[TRIAL_INDEX] = idx
+        return cfg
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        g = self._group_of.pop(trial_id, None)
+        if g is None:
+            return
+        st = self._groups[g]
+        st["done"] += 1
+        metric = self.searcher.metric or self.metric
+        if result and metric in result and not error:
+            st["scores"].append(float(result[metric]))
+        if st["done"] == self.repeat:
+            self._groups.pop(g)
+            mean = float(np.nanmean(st["scores"])) if st["scores"] else float("nan")
+            self.searcher.on_trial_complete(st["first"], {metric: mean} if metric else None,
+                                            error=not st["scores"])
 
 
 UNDEFINED_SEARCH_SPACE = "Trying to sample a configuration from {cls}, but no search space has been defined."

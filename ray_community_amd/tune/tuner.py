@@ -276,7 +276,9 @@ class TuneController:
         self.scheduler = tune_config.scheduler or FIFOScheduler()
         self.scheduler.set_search_properties(tune_config.metric, tune_config.mode)
         self.searcher = tune_config.search_alg or BasicVariantGenerator()
-        inner = self.searcher.searcher if isinstance(self.searcher, ConcurrencyLimiter) else self.searcher
+        inner = self.searcher
+        while isinstance(getattr(inner, "searcher", None), Searcher):  # ConcurrencyLimiter / Repeater
+            inner = inner.searcher
         if isinstance(inner, BasicVariantGenerator):
             inner.set_space(self.param_space, tune_config.num_samples)
             self._budget = None  # until exhausted

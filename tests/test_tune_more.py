@@ -1,0 +1,143 @@
+"""More Tune behaviour (reference test models: python/ray/tune/tests/test_trial_scheduler.py
+MedianStoppingRule, test_searchers.py ConcurrencyLimiter/Repeater, test_tuner.py
+max_concurrent_trials / errors / result grid dataframe, test_api.py with_resources)."""
+import os
+import time
+
+import pytest
+
+import ray_community_amd as ray
+from ray_community_amd import train, tune
+from ray_community_amd.tune.schedulers import MedianStoppingRule
+from ray_community_amd.tune.search import ConcurrencyLimiter, Repeater
+
+
+@pytest.fixture
+def ray6():
+    ray.init(num_cpus=6, log_to_driver=False)
+    yield
+    ray.shutdown()
+
+
+def _run_cfg(tmp_path, name):
+    return train.RunConfig(name=name, storage_path=str(tmp_path))
+
+
+def test_median_stopping_rule_stops_below_median_trials(ray6, tmp_path):
+    def trainable(config):
+        for i in range(20):
+            train.report({"score": config["q"] * (i + 1)})
+            time.sleep(0.05)
+
+    sched = MedianStoppingRule(time_attr="training_iteration", metric="score", mode="max", grace_period=3,
+                               min_samples_required=2)
+    grid = tune.Tuner(trainable, param_space={"q": tune.grid_search([1.0, 2.0, 3.0, 4.0, 0.1])},
+                      tune_config=tune.TuneConfig(scheduler=sched, max_concurrent_trials=5),
+                      run_config=_run_cfg(tmp_path, "median")).fit()
+    iters = {r.config["q"]: r.metrics["training_iteration"] for r in grid}
+    assert iters[4.0] == 20  # the best trial runs to completion
+    assert iters[0.1] < 20   # the worst is stopped early
+
+
+def test_max_concurrent_trials_and_concurrency_limiter(ray6, tmp_path):
+    marks = os.path.join(str(tmp_path), "marks")
+    os.makedirs(marks)
+
+    def trainable(config):
+        p = os.path.join(marks, f"{config['i']}")
+        open(p + ".start", "w").write(str(time.time()))
+        time.sleep(0.4)
+        open(p + ".end", "w").write(str(time.time()))
+        train.report({"v": config["i"]})
+
+    def max_overlap():
+        iv = []
+        for f in os.listdir(marks):
+            if f.endswith(".start"):
+                k = f[:-6]
+                iv.append((float(open(os.path.join(marks, f)).read()),
+                           float(open(os.path.join(marks, k + ".end")).read())))
+        return max(sum(1 for s2, e2 in iv if s2 < e and s < e2) for s, e in iv)
+
+    tune.Tuner(trainable, param_space={"i": tune.grid_search(list(range(6)))},
+               tune_config=tune.TuneConfig(max_concurrent_trials=2), run_config=_run_cfg(tmp_path, "mct")).fit()
+    assert max_overlap() <= 2
+    for f in os.listdir(marks):
+        os.unlink(os.path.join(marks, f))
+    searcher = ConcurrencyLimiter(tune.search.BasicVariantGenerator(), max_concurrent=1)
+    grid = tune.Tuner(trainable, param_space={"i": tune.choice(list(range(100, 200)))},
+                      tune_config=tune.TuneConfig(search_alg=searcher, num_samples=3, metric="v", mode="max"),
+                      run_config=_run_cfg(tmp_path, "limiter")).fit()
+    assert len(grid) == 3 and max_overlap() == 1
+
+
+def test_repeater_averages_repeated_configs(ray6, tmp_path):
+    def trainable(config):
+        train.report({"loss": config["x"] + (0.1 if tune.get_context().get_trial_id()[-1] in "02468" else -0.1)})
+
+    rep = Repeater(tune.search.BasicVariantGenerator(), repeat=2)
+    grid = tune.Tuner(trainable, param_space={"x": tune.grid_search([1.0, 5.0])},
+                      tune_config=tune.TuneConfig(search_alg=rep, metric="loss", mode="min"),
+                      run_config=_run_cfg(tmp_path, "repeat")).fit()
+    assert len(grid) == 4
+    xs = sorted(r.config["x"] for r in grid)
+    assert xs == [1.0, 1.0, 5.0, 5.0]
+
+
+def test_trial_errors_and_dataframe(ray6, tmp_path):
+    def trainable(config):
+        train.report({"acc": config["a"]})
+        if config["a"] == 2:
+            raise ValueError("bad trial")
+        train.report({"acc": config["a"] + 10})
+
+    grid = tune.Tuner(trainable, param_space={"a": tune.grid_search([1, 2, 3])},
+                      tune_config=tune.TuneConfig(metric="acc", mode="max"),
+                      run_config=_run_cfg(tmp_path, "errs")).fit()
+    assert grid.num_errors == 1 and grid.num_terminated == 2
+    bad = [r for r in grid if r.error is not None]
+    assert len(bad) == 1 and "bad trial" in str(bad[0].error)
+    assert grid.get_best_result().config["a"] == 3
+    df = grid.get_dataframe()
+    assert len(df) == 3 and "acc" in df.columns and "config/a" in df.columns
+
+
+def test_with_resources_reserves_cpus(ray6, tmp_path):
+    def trainable(config):
+        train.report({"cpus": ray.get_runtime_context().get_assigned_resources().get("CPU", 0)})
+
+    grid = tune.Tuner(tune.with_resources(trainable, {"cpu": 3}), param_space={"i": tune.grid_search([0, 1])},
+                      run_config=_run_cfg(tmp_path, "res")).fit()
+    assert all(r.metrics["cpus"] == 3 for r in grid)
+
+
+def test_repeater_reports_group_means_to_the_wrapped_searcher():
+    from ray_community_amd.tune.search import Searcher
+    from ray_community_amd.tune.search import TRIAL_INDEX
+
+    class Rec(Searcher):
+        def __init__(self):
+            super().__init__(metric="loss", mode="min")
+            self.n = 0
+            self.done = []
+
+        def suggest(self, trial_id):
+            self.n += 1
+            return {"x": self.n} if self.n <= 2 else Searcher.FINISHED
+
+        def on_trial_complete(self, trial_id, result=None, error=False):
+            self.done.append((trial_id, result, error))
+
+    inner = Rec()
+    rep = Repeater(inner, repeat=3)
+    cfgs = [rep.suggest(f"t{i}") for i in range(7)]
+    assert [c["x"] for c in cfgs[:6]] == [1, 1, 1, 2, 2, 2] and cfgs[6] == Searcher.FINISHED
+    assert [c[TRIAL_INDEX] for c in cfgs[:6]] == [0, 1, 2, 0, 1, 2]
+    for i, loss in enumerate([1.0, 2.0, 3.0]):
+        rep.on_trial_complete(f"t{i}", {"loss": loss})
+    assert inner.done == [("t0", {"loss": 2.0}, False)]
+    rep.on_trial_complete("t3", {"loss": 5.0})
+    rep.on_trial_complete("t4", None, error=True)
+    assert len(inner.done) == 1  # the group of t3..t5 is not complete yet
+    rep.on_trial_complete("t5", {"loss": 7.0})
+    assert inner.done[-1] == ("t3", {"loss": 6.0}, False)
