@@ -72,6 +72,7 @@ class DistributedDataParallel(nn.Module):
     def _on_grad(self, p):
         if not self._sync:
             return
+        self.flat.adopt_grad(p)
         if self.auto_finalize and not self._finalize_queued:
             self._finalize_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize_cb)

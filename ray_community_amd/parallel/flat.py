@@ -157,6 +157,22 @@ class FlatParameters:
             self.fused = []
             self.zero_start = 0
 
+    def adopt_grad(self, p):
+        """Make ``p.grad`` the flat-buffer view again if something replaced it (a torch optimizer's
+        ``zero_grad(set_to_none=True)`` drops the view, and the next backward then accumulates into
+        a fresh tensor that the bucket collectives would never see): copy the fresh gradient into
+        the parameter's slot and re-point ``p.grad`` at it. No-op in the normal case."""
+        if not self.grad_is_view:
+            return
+        g = p.grad
+        if g is None:
+            return
+        off = self.param_offset[id(p)]
+        if g.data_ptr() != self.grad.data_ptr() + off * self.grad.element_size():
+            view = self.grad[off: off + p.numel()]
+            view.copy_(g.reshape(-1))
+            p.grad = view.view_as(p)
+
     def finalize_fresh_range(self, bucket):
         """``finalize_fresh`` restricted to one bucket's parameters."""
         for p in bucket.params:

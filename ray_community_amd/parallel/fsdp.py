@@ -83,6 +83,7 @@ class ShardedDataParallel(nn.Module):
     def _on_grad(self, p):
         if not self._sync:
             return
+        self.flat.adopt_grad(p)
         bi = self.flat.param_bucket[id(p)]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
