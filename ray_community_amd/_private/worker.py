@@ -272,16 +272,32 @@ def put(value, *, _owner=None) -> ObjectRef:
     return _core().put(value)
 
 
+_CDR = []
+
+
+def _compiled_dag_ref_type():
+    if not _CDR:
+        from ..dag.compiled_dag_node import CompiledDAGRef
+
+        _CDR.append(CompiledDAGRef)
+    return _CDR[0]
+
+
 def get(object_refs, *, timeout: Optional[float] = None):
     core = _core()
     from .core_worker import ObjectRefGenerator
 
     if isinstance(object_refs, ObjectRefGenerator):
         object_refs = list(object_refs)
+    cdr = _compiled_dag_ref_type()
+    if isinstance(object_refs, cdr):  # compiled-DAG result (reference: ray.get dispatches these too)
+        return object_refs.get(timeout=timeout)
     if isinstance(object_refs, (list, tuple)):
         refs = list(object_refs)
         if not refs:
             return []
+        if all(isinstance(r, cdr) for r in refs):
+            return [r.get(timeout=timeout) for r in refs]
         for r in refs:
             if not isinstance(r, ObjectRef):
                 raise ValueError(f"'object_refs' must either be an ObjectRef or a list of ObjectRefs; got {type(r)}")

@@ -98,3 +98,27 @@ def test_compiled_dag_pipeline(ray_start_regular):
         cdag.teardown()
     # the actors are still usable normally afterwards
     assert ray.get(s1.fwd.remote(4)) == 8
+
+
+def test_ray_get_accepts_compiled_dag_refs(ray_start_regular):
+    """ray.get(CompiledDAGRef) / ray.get([CompiledDAGRef, ...]) as in the reference."""
+    from ray_community_amd.dag import InputNode
+
+    @ray.remote
+    class Acc:
+        def __init__(self):
+            self.t = 0
+
+        def add(self, x):
+            self.t += x
+            return self.t
+
+    a = Acc.remote()
+    with InputNode() as inp:
+        dag = a.add.bind(inp)
+    cd = dag.experimental_compile()
+    try:
+        assert ray.get(cd.execute(1)) == 1
+        assert ray.get([cd.execute(2)]) == [3]
+    finally:
+        cd.teardown()
