@@ -264,10 +264,49 @@ class Algorithm(Trainable):
         a = a[0].numpy()
         return int(a) if a.ndim == 0 else a
 
-    def get_module(self):
+    def get_module(self, module_id=None):
+        """The (weight-synced) RLModule; multi-agent: the one of ``module_id`` (default: first)."""
+        if self.multi_agent:
+            pid = module_id or next(iter(self.learner_groups))
+            m = self.local_runner.modules[pid]
+            m.set_state(self.learner_groups[pid].get_weights())
+            return m
         m = self.local_runner.module
         m.set_state(self.learner_group.get_weights())
         return m
+
+    def get_policy(self, policy_id=None):
+        """Old-API-stack view (reference ``Algorithm.get_policy``): a ``TorchPolicy`` over the
+        current module (``compute_actions`` / ``get_weights`` / ``set_weights``)."""
+        from ..policy.policy import TorchPolicy
+
+        m = self.get_module(policy_id)
+        if self.multi_agent:
+            pid = policy_id or next(iter(self.learner_groups))
+            obs_sp, act_sp = self.local_runner.spaces_[pid]
+        else:
+            obs_sp = self.local_runner.env_to_module.observation_space
+            act_sp = self.local_runner.env.action_space
+        return TorchPolicy(obs_sp, act_sp, self.config.to_dict(), model=m)
+
+    def compute_actions(self, observations, state=None, explore: bool = False, policy_id=None, **kw):
+        """Batched ``compute_single_action``: a dict {agent/env key: obs} gives a dict of actions,
+        an array batch gives an array (reference ``Algorithm.compute_actions``)."""
+        if isinstance(observations, dict):
+            return {k: self.compute_single_action(o, explore=explore, policy_id=policy_id)
+                    for k, o in observations.items()}
+        acts, _, _ = self.get_policy(policy_id).compute_actions(np.asarray(observations), explore=explore)
+        return acts
+
+    def export_policy_model(self, export_dir: str, policy_id=None):
+        """Save the policy network's ``state_dict`` (``model.pt``, loadable with
+        ``torch.load(..., weights_only=True)``) plus its class name."""
+        os.makedirs(export_dir, exist_ok=True)
+        m = self.get_module(policy_id)
+        torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, os.path.join(export_dir, "model.pt"))
+        with open(os.path.join(export_dir, "model_info.json"), "w") as f:
+            json.dump({"module_class": type(m).__name__, "policy_id": policy_id}, f)
+        return export_dir
 
     def get_weights(self, policies=None):
         if self.multi_agent:

@@ -440,3 +440,34 @@ def test_two_learners_take_the_single_learner_step(shutdown_only):
         assert torch.allclose(wa[k], wb[k], atol=2e-6, rtol=1e-4), k
     assert abs(s1["policy_loss"] - s2["policy_loss"]) < 1e-5
     two.shutdown()
+
+
+def test_algorithm_policy_views_and_export(tmp_path):
+    """Old-API-stack accessors on a built algorithm: get_policy().compute_actions matches
+    compute_single_action (greedy), compute_actions over a dict and a batch, and
+    export_policy_model writes a weights-only-loadable state dict."""
+    import numpy as np
+    import torch
+
+    import ray_community_amd as ray
+    from ray_community_amd.rllib.algorithms.ppo import PPOConfig
+
+    ray.init(num_cpus=2, log_to_driver=False)
+    try:
+        algo = (PPOConfig().environment("CartPole-v1").env_runners(num_env_runners=0)
+                .training(train_batch_size=256)).build()
+        algo.train()
+        obs = np.random.RandomState(0).randn(5, 4).astype(np.float32)
+        pol = algo.get_policy()
+        acts, _, info = pol.compute_actions(obs, explore=False)
+        assert [int(a) for a in acts] == [algo.compute_single_action(o) for o in obs]
+        assert "vf_preds" in info
+        assert list(algo.compute_actions(obs)) == [int(a) for a in acts]
+        d = algo.compute_actions({"a": obs[0], "b": obs[1]})
+        assert d == {"a": int(acts[0]), "b": int(acts[1])}
+        out = algo.export_policy_model(str(tmp_path / "export"))
+        sd = torch.load(str(tmp_path / "export" / "model.pt"), weights_only=True)
+        assert out and sd and all(torch.equal(sd[k], v.cpu()) for k, v in algo.get_module().state_dict().items())
+        algo.stop()
+    finally:
+        ray.shutdown()
