@@ -117,12 +117,12 @@ class RefTable {
     return false;
   }
 
-  // pin(+n) / unpin(-n); returns true when the object is now unreferenced. Unknown objects: false.
+  // pin(+n) / unpin(-n); returns true when the object is now unreferenced. Creates the record
+  // (the head only pins objects it tracks, so no separate add() is needed on the hot path).
   bool pin(const py::bytes& oid, int64_t n) {
-    auto it = objs_.find(std::string(oid));
-    if (it == objs_.end()) return false;
-    it->second.pins += n;
-    return it->second.holders.empty() && it->second.pins <= 0;
+    Rec& r = objs_[std::string(oid)];
+    r.pins += n;
+    return r.holders.empty() && r.pins <= 0;
   }
 
   int64_t pins(const py::bytes& oid) const {

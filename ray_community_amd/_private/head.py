@@ -526,8 +526,7 @@ class Head:
         e = self.objects.get(oid)
         if e is None and create:
             e = ObjEntry(oid, task)
-            self.objects[oid] = e
-            self.refs.add(oid)
+            self.objects[oid] = e  # its reference record is created by the first holder or pin
         return e
 
     def _add_holder(self, oid, key):

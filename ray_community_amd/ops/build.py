@@ -23,8 +23,12 @@ ARCH = os.environ.get("RCA_OFFLOAD_ARCH", "gfx950")
 # exceeds 256 VGPRs (the one-wave-per-SIMD attention dK/dV kernel: 574 v_accvgpr moves -> 26).
 EXTRA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
 # per-file overrides: the one-wave-per-SIMD kernels (dK/dV, the 4-wave GEMM) keep their
-# accumulators in AGPRs
-FILE_FLAGS = {"attention_dkdv.hip": [], "gemm4.hip": []}
+# accumulators in AGPRs. The attention kernels use LLVM's iterative-ILP machine-scheduling
+# strategy: fwd+bwd 1.489 vs 1.512 ms at the 8B shape over three interleaved rounds (max-ilp,
+# max-memory-clause and iterative-minreg were 2-8 % slower; scripts/ab_sched_build.sh,
+# scripts/gpu_r3_q.sh, profiles/attn_sched_r3.log).
+_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+FILE_FLAGS = {"attention_dkdv.hip": _ILP, "gemm4.hip": [], "attention.hip": EXTRA_FLAGS + _ILP}
 
 
 def _hipcc() -> str:

@@ -382,6 +382,39 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   }
 }
 
+// Wide-grid variant for H % 16 == 0 (the Llama widths): one block per 16 columns (4 quads) x
+// 64 row groups, so H = 4096 launches 256 blocks instead of colsum_kernel's 64 (which left 3 of 4
+// CUs idle on a latency-bound 16 MB read). Fixed summation order: bitwise reproducible.
+__global__ __launch_bounds__(256) void colsum16_kernel(const float* __restrict__ part, int nb, int H,
+                                                       bf16_t* __restrict__ dw_bf16, float* __restrict__ dw_f32,
+                                                       int accumulate) {
+  __shared__ f32x4 red[64][4];
+  __shared__ f32x4 red2[4][4];
+  const int cq = threadIdx.x & 3;   // column quad within the block's 16 columns
+  const int rg = threadIdx.x >> 2;  // row group (64)
+  const int c = blockIdx.x * 16 + cq * 4;
+  f32x4 t = {0.f, 0.f, 0.f, 0.f};
+  for (int b = rg; b < nb; b += 64) t += *reinterpret_cast<const f32x4*>(part + (size_t)b * H + c);
+  red[rg][cq] = t;
+  __syncthreads();
+  if (rg < 4) {  // 4 x 4 threads: quad cq, partial over row groups rg, rg+4, ..
+    f32x4 u = red[rg][cq];
+#pragma unroll
+    for (int k = rg + 4; k < 64; k += 4) u += red[k][cq];
+    red2[rg][cq] = u;
+  }
+  __syncthreads();
+  if (rg == 0) {
+    f32x4 v = red2[0][cq] + red2[1][cq] + red2[2][cq] + red2[3][cq];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = v[j];
+      if (dw_f32) dw_f32[c + j] = accumulate ? dw_f32[c + j] + x : x;
+      if (dw_bf16) dw_bf16[c + j] = f2bf(accumulate ? bf2f(dw_bf16[c + j]) + x : x);
+    }
+  }
+}
+
 RCA_API int rca_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd,
                             int rows, int H, float eps, hipStream_t stream) {
   if (H % 8 != 0) return -1;
@@ -443,7 +476,11 @@ RCA_API int rca_rmsnorm_bwd(const void* s, const void* dy, const void* w, const 
     // kernel (second pass served from L2) keeps 7 waves/SIMD
     default: hipLaunchKernelGGL(rmsnorm_bwd_generic, grid, block, lds, stream, S, G, W, rstd, DR, DX, dw_part, rows, H);
   }
-  hipLaunchKernelGGL(colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, stream, dw_part, nb, H, (bf16_t*)dw_bf16, dw_f32,
-                     accumulate);
+  if (H % 16 == 0)
+    hipLaunchKernelGGL(colsum16_kernel, dim3(H / 16), dim3(256), 0, stream, dw_part, nb, H, (bf16_t*)dw_bf16, dw_f32,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, stream, dw_part, nb, H, (bf16_t*)dw_bf16,
+                       dw_f32, accumulate);
   return (int)hipGetLastError();
 }

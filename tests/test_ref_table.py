@@ -31,7 +31,7 @@ def test_holders_pins_and_unreferenced_transitions():
     assert not t.remove_holder(o, "never-seen") or t.unreferenced(o)
     t.erase(o)
     assert not t.contains(o) and len(t) == 0
-    assert not t.pin(o, 1)  # unknown objects are not created by pins
+    assert not t.pin(o, 1) and t.pins(o) == 1  # a pin creates the record
 
 
 def test_drop_holder_returns_exactly_the_objects_it_kept_alive():
