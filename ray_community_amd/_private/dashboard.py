@@ -94,6 +94,9 @@ class Dashboard:
                         return self._send(200, "\n".join(lines), "text/plain; charset=utf-8")
                     if path == "/metrics":
                         return self._send(200, dash._call("metrics_text"), "text/plain; version=0.0.4")
+                    if path.startswith("/api/v0/"):
+                        code, body = dash._state_route(path[len("/api/v0/"):].split("/"), query)
+                        return self._send(code, json.dumps(body, default=str), "application/json")
                     routes = {"/api/version": lambda: {"version": _version(), "ray_compatible": "3.0.0.dev0"},
                               "/api/cluster_status": lambda: {"total": dash._call("cluster_resources"),
                                                               "available": dash._call("available_resources")},
@@ -120,6 +123,40 @@ class Dashboard:
 
     def _call(self, method, *args):
         return self.client.call(method, *args)
+
+    def _state_route(self, parts, query):
+        """Reference state-API HTTP protocol (``dashboard/modules/state/state_head.py``):
+        ``GET /api/v0/<resource>?limit=&detail=&filter_keys=&filter_predicates=&filter_values=`` and
+        ``GET /api/v0/<tasks|actors|objects>/summarize``, answered in the reference envelope."""
+        from ..util import state as st
+
+        def env(ok, msg, data):
+            return (200 if ok else 400), {"result": ok, "msg": msg, "data": data}
+
+        res = parts[0] if parts else ""
+        try:
+            with st._using_client(self.client):
+                if len(parts) == 2 and parts[1] == "summarize" and res in ("tasks", "actors", "objects"):
+                    summary = getattr(st, f"summarize_{res}")()
+                    return env(True, "", {"result": {"node_id_to_summary": summary}})
+                if len(parts) != 1 or res not in st._RESOURCES:
+                    return 404, {"result": False, "msg": f"unknown state resource {'/'.join(parts)!r}", "data": {}}
+                keys = query.get("filter_keys", [])
+                preds = query.get("filter_predicates", [])
+                vals = query.get("filter_values", [])
+                if not (len(keys) == len(preds) == len(vals)):
+                    return env(False, "filter_keys, filter_predicates and filter_values must have equal lengths", {})
+                filters = list(zip(keys, preds, vals))
+                limit = int((query.get("limit") or ["100"])[0])
+                rows = getattr(st, f"list_{res}")(filters=None)
+                total = len(rows)
+                rows = st._filter(rows, filters)
+                out = rows[:limit]
+                return env(True, "", {"result": {"total": total, "num_after_truncation": len(out),
+                                                 "num_filtered": len(rows), "result": out,
+                                                 "partial_failure_warning": "", "warnings": None}})
+        except ValueError as e:
+            return env(False, str(e), {})
 
     def _job_route(self, method, rest, body, query):
         """(status, json) for one job REST call."""

@@ -2,14 +2,56 @@
 from __future__ import annotations
 
 from collections import Counter
+import contextlib
 import os
+import threading
 from typing import Any, Dict, Iterator, List, Optional, Tuple
+
+_LOCAL = threading.local()
 
 
 def _call(method, *args):
+    c = getattr(_LOCAL, "client", None)  # the dashboard answering /api/v0 with its own head link
+    if c is not None:
+        return c.call(method, *args)
     from .._private.worker import _core
 
     return _core().client.call(method, *args)
+
+
+@contextlib.contextmanager
+def _using_client(client):
+    prev = getattr(_LOCAL, "client", None)
+    _LOCAL.client = client
+    try:
+        yield
+    finally:
+        _LOCAL.client = prev
+
+
+_RESOURCES = ("actors", "tasks", "objects", "nodes", "workers", "placement_groups", "jobs", "runtime_envs",
+              "cluster_events")
+
+
+def _http_list(address: str, resource: str, filters, limit: int, detail: bool):
+    """List through a dashboard's ``/api/v0/<resource>`` (reference state-API HTTP protocol)."""
+    import requests
+
+    params = [("limit", str(limit)), ("detail", str(bool(detail)))]
+    for k, op, v in filters or []:
+        params += [("filter_keys", k), ("filter_predicates", op), ("filter_values", str(v))]
+    base = address if address.startswith("http") else "http://" + address
+    r = requests.get(f"{base.rstrip('/')}/api/v0/{resource}", params=params, timeout=30)
+    r.raise_for_status()
+    body = r.json()
+    if not body.get("result", False):
+        raise RuntimeError(body.get("msg") or f"state API request for {resource} failed")
+    return body["data"]["result"]["result"]
+
+
+def _remote(kw) -> Optional[str]:
+    a = kw.get("address")
+    return a if isinstance(a, str) and (a.startswith("http") or ":" in a and not a.startswith("ray://")) else None
 
 
 _PREDICATES = ("=", "==", "!=")
@@ -44,11 +86,16 @@ def _filter(rows, filters):
 
 
 def list_actors(filters: Optional[List[Tuple[str, str, Any]]] = None, limit: int = 10000, detail=False, **kw):
+    if _remote(kw):
+        return _http_list(_remote(kw), "actors", filters, limit, detail)
     return _filter(_call("list_actors"), filters)[:limit]
 
 
 def list_tasks(filters=None, limit: int = 10000, detail=False, **kw):
-    _flush_own_task_records()
+    if _remote(kw):
+        return _http_list(_remote(kw), "tasks", filters, limit, detail)
+    if getattr(_LOCAL, "client", None) is None:
+        _flush_own_task_records()
     return _filter(_call("list_tasks", limit), filters)[:limit]
 
 
@@ -67,26 +114,36 @@ def _flush_own_task_records():
 
 
 def list_objects(filters=None, limit: int = 10000, detail=False, **kw):
+    if _remote(kw):
+        return _http_list(_remote(kw), "objects", filters, limit, detail)
     return _filter(_call("list_objects"), filters)[:limit]
 
 
 def list_nodes(filters=None, limit: int = 10000, detail=False, **kw):
+    if _remote(kw):
+        return _http_list(_remote(kw), "nodes", filters, limit, detail)
     rows = [{"node_id": n["NodeID"], "state": "ALIVE" if n["Alive"] else "DEAD", "is_head_node": n["IsHead"],
              "resources_total": n["Resources"], "labels": n.get("Labels", {})} for n in _call("nodes")]
     return _filter(rows, filters)[:limit]
 
 
 def list_workers(filters=None, limit: int = 10000, detail=False, **kw):
+    if _remote(kw):
+        return _http_list(_remote(kw), "workers", filters, limit, detail)
     return _filter(_call("list_workers"), filters)[:limit]
 
 
 def list_placement_groups(filters=None, limit: int = 10000, detail=False, **kw):
+    if _remote(kw):
+        return _http_list(_remote(kw), "placement_groups", filters, limit, detail)
     return _filter(list(_call("pg_table", None).values()), filters)[:limit]
 
 
 def list_jobs(filters=None, limit: int = 10000, detail=False, **kw):
     """The driver job of this session plus submitted jobs (job submission manager), reference
     ``list_jobs`` fields: ``job_id``/``submission_id``, ``type``, ``status``, ``entrypoint``."""
+    if _remote(kw):
+        return _http_list(_remote(kw), "jobs", filters, limit, detail)
     from .._private.worker import _core
 
     core = _core()
@@ -112,6 +169,8 @@ def list_jobs(filters=None, limit: int = 10000, detail=False, **kw):
 
 def list_runtime_envs(filters=None, limit: int = 10000, detail=False, **kw):
     """Distinct runtime environments of the live workers (one row per env, with its worker count)."""
+    if _remote(kw):
+        return _http_list(_remote(kw), "runtime_envs", filters, limit, detail)
     rows = {}
     for w in _call("list_workers"):
         key = str(w.get("runtime_env") or {})
@@ -122,6 +181,8 @@ def list_runtime_envs(filters=None, limit: int = 10000, detail=False, **kw):
 
 def list_cluster_events(filters=None, limit: int = 10000, detail=False, **kw):
     """Node / worker / OOM-kill events recorded by the head (reference: ``list_cluster_events``)."""
+    if _remote(kw):
+        return _http_list(_remote(kw), "cluster_events", filters, limit, detail)
     return _filter(_call("cluster_events"), filters)[:limit]
 
 

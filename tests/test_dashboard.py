@@ -69,3 +69,50 @@ def test_dashboard_overview_page_logs_and_events(shutdown_only):
     ev = json.loads(_get(url + "/api/cluster_events"))
     assert any(e["source_type"] == "NODE" for e in ev)
     assert json.loads(_get(url + "/api/placement_groups")) == []
+
+
+def test_state_api_over_http(shutdown_only):
+    """The reference state-API HTTP protocol on the dashboard (/api/v0/<resource> with limit and
+    filter_keys/predicates/values, /api/v0/<resource>/summarize, the result envelope) and the
+    Python state API pointed at it with ``address=`` (what a remote ``ray list actors`` does)."""
+    import requests
+
+    from ray_community_amd.util import state
+
+    ctx = ray.init(num_cpus=2, include_dashboard=True, dashboard_port=0)
+    url = ctx.dashboard_url
+
+    @ray.remote
+    class Named:
+        def ping(self):
+            return 1
+
+    a = Named.options(name="alpha").remote()
+    b = Named.options(name="beta").remote()
+    ray.get([a.ping.remote(), b.ping.remote()])
+
+    @ray.remote
+    def t():
+        return 1
+
+    ray.get([t.remote() for _ in range(3)])
+    body = requests.get(url + "/api/v0/actors", params={"limit": 10}, timeout=10).json()
+    assert body["result"] is True
+    res = body["data"]["result"]
+    assert res["total"] >= 2 and {r["name"] for r in res["result"]} >= {"alpha", "beta"}
+    body = requests.get(url + "/api/v0/actors", params={"filter_keys": "name", "filter_predicates": "=",
+                                                        "filter_values": "beta"}, timeout=10).json()
+    assert [r["name"] for r in body["data"]["result"]["result"]] == ["beta"]
+    assert body["data"]["result"]["num_filtered"] == 1
+    lim = requests.get(url + "/api/v0/actors", params={"limit": 1}, timeout=10).json()["data"]["result"]
+    assert lim["num_after_truncation"] == 1 and lim["total"] >= 2
+    bad = requests.get(url + "/api/v0/actors", params={"filter_keys": "name", "filter_predicates": "~",
+                                                       "filter_values": "x"}, timeout=10)
+    assert bad.status_code == 400 and bad.json()["result"] is False
+    summ = requests.get(url + "/api/v0/tasks/summarize", timeout=10).json()
+    assert summ["result"] and "cluster" in summ["data"]["result"]["node_id_to_summary"]
+    assert requests.get(url + "/api/v0/nope", timeout=10).status_code == 404
+    # the Python state API against the HTTP endpoint
+    names = [r["name"] for r in state.list_actors(address=url, filters=[("name", "=", "alpha")])]
+    assert names == ["alpha"]
+    assert len(state.list_nodes(address=url)) == 1
