@@ -458,8 +458,10 @@ class Dataset:
         return list(r.values())[0]
 
     # ------------------------------------------------------------------ writes
-    def write_parquet(self, path: str, **kw):
-        self._write(path, "parquet")
+    def write_parquet(self, path: str, *, partition_cols: Optional[List[str]] = None, **kw):
+        """``partition_cols``: hive layout ``path/col=value/...`` with those columns moved into
+        the directory names (reference ``Dataset.write_parquet``); ``read_parquet`` restores them."""
+        self._write(path, "parquet", partition_cols=list(partition_cols or []))
 
     def write_csv(self, path: str, **kw):
         self._write(path, "csv")
@@ -515,12 +517,12 @@ class Dataset:
 
         return _copy.copy(self)
 
-    def _write(self, path, fmt, column=None):
+    def _write(self, path, fmt, column=None, partition_cols=None):
         from .._private.worker import get
 
         os.makedirs(path, exist_ok=True)
         w = X._remote_fn(_write_block, {"num_cpus": 1})
-        refs = [w.remote(b, path, i, fmt, column)[0] for i, (b, _) in enumerate(self._refs())]
+        refs = [w.remote(b, path, i, fmt, column, partition_cols)[0] for i, (b, _) in enumerate(self._refs())]
         get(refs)
 
     # ------------------------------------------------------------------ misc
@@ -711,11 +713,33 @@ def _zip_blocks(a, b):
     return out, X._meta(out)
 
 
-def _write_block(block, path, i, fmt, column):
+def _pa_table(df):
+    import pyarrow as pa
+
+    return pa.Table.from_pandas(df, preserve_index=False)
+
+
+def _write_block(block, path, i, fmt, column, partition_cols=None):
     acc = BlockAccessor(block)
     if acc.num_rows() == 0:
         return None, {}
     fn = os.path.join(path, f"{i:06d}.{fmt}")
+    if fmt == "parquet" and partition_cols:
+        import pyarrow.parquet as pq
+
+        df = acc.to_pandas()
+        missing = [c for c in partition_cols if c not in df.columns]
+        if missing:
+            raise ValueError(f"partition_cols {missing} are not columns of the dataset")
+        out = []
+        for key, part in df.groupby(partition_cols, sort=True, dropna=False):
+            key = key if isinstance(key, tuple) else (key,)
+            d = os.path.join(path, *[f"{c}={v}" for c, v in zip(partition_cols, key)])
+            os.makedirs(d, exist_ok=True)
+            f = os.path.join(d, f"{i:06d}.parquet")
+            pq.write_table(_pa_table(part.drop(columns=partition_cols).reset_index(drop=True)), f)
+            out.append(f)
+        return out, {}
     if fmt == "parquet":
         import pyarrow.parquet as pq
 

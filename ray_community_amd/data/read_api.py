@@ -117,7 +117,9 @@ def from_huggingface(dataset) -> Dataset:
     return from_arrow(dataset.data.table if hasattr(dataset, "data") else dataset.with_format("arrow")[:])
 
 
-def _expand_paths(paths, exts=None):
+def _expand_paths(paths, exts=None, bases=None):
+    """Input files under ``paths``; ``bases`` (optional dict) receives file -> the directory it
+    was found under (the root for hive partition discovery)."""
     if isinstance(paths, str):
         paths = [paths]
     out = []
@@ -129,6 +131,8 @@ def _expand_paths(paths, exts=None):
                         continue
                     if exts is None or any(f.endswith(e) for e in exts):
                         out.append(os.path.join(root, f))
+                        if bases is not None:
+                            bases[out[-1]] = p
         elif any(c in p for c in "*?["):
             out.extend(sorted(glob.glob(p)))
         else:
@@ -136,24 +140,43 @@ def _expand_paths(paths, exts=None):
     return sorted(out)
 
 
+def _hive_fields(path, base):
+    """``col=value`` directory components between ``base`` and the file (hive partitioning)."""
+    if not base:
+        return []
+    rel = os.path.relpath(os.path.dirname(path), base)
+    out = []
+    for part in ([] if rel in (".", "") else rel.split(os.sep)):
+        if "=" in part:
+            k, v = part.split("=", 1)
+            out.append((k, v))
+    return out
+
+
 class _FileRead:
-    def __init__(self, path, fmt, kwargs, include_paths=False):
+    def __init__(self, path, fmt, kwargs, include_paths=False, base=None):
         self.path, self.fmt, self.kwargs, self.include_paths = path, fmt, kwargs, include_paths
+        self.base = base
 
     def __call__(self):
         p, fmt, kw = self.path, self.fmt, self.kwargs
         if fmt == "parquet":
             import pyarrow.parquet as pq
 
-            t = pq.read_table(p, columns=kw.get("columns"))
+            cols = kw.get("columns")
+            if cols is not None and kw.get("partitioning", "hive") == "hive":
+                have = set(pq.read_schema(p).names)  # partition columns live in the path, not the file
+                cols = [c for c in cols if c in have]
+            t = pq.read_table(p, columns=cols, filters=kw.get("filter"))
         elif fmt == "csv":
             import pyarrow.csv as pcsv
 
-            t = pcsv.read_csv(p)
+            t = pcsv.read_csv(p, **{k: kw[k] for k in ("read_options", "parse_options", "convert_options")
+                                    if kw.get(k) is not None})
         elif fmt == "json":
             import pyarrow.json as pj
 
-            t = pj.read_json(p)
+            t = pj.read_json(p, **{k: kw[k] for k in ("read_options", "parse_options") if kw.get(k) is not None})
         elif fmt == "text":
             with open(p, "r", encoding=kw.get("encoding", "utf-8")) as f:
                 lines = f.read().splitlines()
@@ -186,6 +209,15 @@ class _FileRead:
             return b
         else:
             raise ValueError(fmt)
+        if kw.get("partitioning", "hive") == "hive":
+            import pyarrow as pa
+
+            cols = kw.get("columns")
+            for k, v in _hive_fields(p, self.base):
+                if k not in t.column_names and (cols is None or k in cols):
+                    t = t.append_column(k, pa.array([v] * t.num_rows, type=pa.string()))
+            if cols is not None and fmt == "parquet":
+                t = t.select([c for c in cols if c in t.column_names])
         if self.include_paths:
             import pyarrow as pa
 
@@ -194,22 +226,43 @@ class _FileRead:
 
 
 def _read(paths, fmt, exts, include_paths=False, **kw) -> Dataset:
-    files = _expand_paths(paths, exts)
+    bases = {}
+    files = _expand_paths(paths, exts, bases)
     if not files:
         raise ValueError(f"No input files found to read from paths {paths}")
-    return Dataset([("read", _FileRead(f, fmt, kw, include_paths)) for f in files])
+    return Dataset([("read", _FileRead(f, fmt, kw, include_paths, bases.get(f))) for f in files])
 
 
-def read_parquet(paths, *, columns=None, include_paths=False, **kw) -> Dataset:
-    return _read(paths, "parquet", [".parquet"], include_paths, columns=columns)
+def _partitioning(p):
+    """``partitioning``: "hive" / a reference ``Partitioning("hive")`` object (default) or None."""
+    if p is None:
+        return None
+    style = getattr(p, "style", p)
+    style = getattr(style, "value", style)
+    if str(style).lower() != "hive":
+        raise NotImplementedError(f"only hive partitioning is supported, got {p!r}")
+    return "hive"
 
 
-def read_csv(paths, *, include_paths=False, **kw) -> Dataset:
-    return _read(paths, "csv", [".csv"], include_paths)
+def read_parquet(paths, *, columns=None, include_paths=False, partitioning="hive", filter=None, **kw) -> Dataset:
+    """Parquet files; hive ``col=value`` directories become string columns (reference default
+    ``Partitioning("hive")``); ``filter``: a pyarrow filter expression / DNF list."""
+    return _read(paths, "parquet", [".parquet"], include_paths, columns=columns, filter=filter,
+                 partitioning=_partitioning(partitioning))
 
 
-def read_json(paths, *, include_paths=False, **kw) -> Dataset:
-    return _read(paths, "json", [".json", ".jsonl"], include_paths)
+def read_csv(paths, *, include_paths=False, partitioning="hive", parse_options=None, read_options=None,
+             convert_options=None, **kw) -> Dataset:
+    """CSV files through ``pyarrow.csv`` (``parse_options`` / ``read_options`` / ``convert_options``
+    forwarded, e.g. ``ParseOptions(delimiter="\t")``)."""
+    return _read(paths, "csv", [".csv"], include_paths, partitioning=_partitioning(partitioning),
+                 parse_options=parse_options, read_options=read_options, convert_options=convert_options)
+
+
+def read_json(paths, *, include_paths=False, partitioning="hive", parse_options=None, read_options=None,
+              **kw) -> Dataset:
+    return _read(paths, "json", [".json", ".jsonl"], include_paths, partitioning=_partitioning(partitioning),
+                 parse_options=parse_options, read_options=read_options)
 
 
 def read_text(paths, *, encoding="utf-8", drop_empty_lines=True, include_paths=False, **kw) -> Dataset:

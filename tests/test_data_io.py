@@ -133,3 +133,30 @@ def test_random_access_dataset(ray2):
     got = rad.multiget([5, 199, 0, 300, 42])
     assert [g["v"] if g else None for g in got] == ["val5", "val199", "val0", None, "val42"]
     assert "worker 0" in rad.stats()
+
+
+def test_hive_partitioned_parquet_and_csv_options(ray_start_regular, tmp_path):
+    """write_parquet(partition_cols=...) writes hive directories without the partition columns;
+    read_parquet restores them as string columns (reference default Partitioning("hive")) and
+    honours columns= / filter=; read_csv forwards pyarrow ParseOptions."""
+    import pyarrow.csv as pcsv
+    import pyarrow.dataset as pads
+
+    from ray_community_amd import data
+
+    ds = data.from_items([{"k": i % 3, "g": "ab"[i % 2], "v": i} for i in range(30)])
+    out = str(tmp_path / "pq")
+    ds.write_parquet(out, partition_cols=["k", "g"])
+    dirs = sorted(os.listdir(out))
+    assert dirs == ["k=0", "k=1", "k=2"] and sorted(os.listdir(os.path.join(out, "k=0"))) == ["g=a", "g=b"]
+    back = data.read_parquet(out)
+    rows = sorted((r["k"], r["g"], r["v"]) for r in back.take_all())
+    assert rows == sorted((str(i % 3), "ab"[i % 2], i) for i in range(30))
+    assert data.read_parquet(out, columns=["v", "k"]).columns() == ["v", "k"]
+    assert data.read_parquet(out, partitioning=None).columns() == ["v"]
+    small = data.read_parquet(out, filter=pads.field("v") < 5)
+    assert sorted(r["v"] for r in small.take_all()) == [0, 1, 2, 3, 4]
+    tsv = tmp_path / "t.csv"
+    tsv.write_text("a\tb\n1\t2\n3\t4\n")
+    t = data.read_csv(str(tsv), parse_options=pcsv.ParseOptions(delimiter="\t"))
+    assert t.take_all() == [{"a": 1, "b": 2}, {"a": 3, "b": 4}]
