@@ -461,16 +461,25 @@ class Dataset:
     def write_parquet(self, path: str, *, partition_cols: Optional[List[str]] = None, **kw):
         """``partition_cols``: hive layout ``path/col=value/...`` with those columns moved into
         the directory names (reference ``Dataset.write_parquet``); ``read_parquet`` restores them."""
-        self._write(path, "parquet", partition_cols=list(partition_cols or []))
+        self._sized(kw)._write(path, "parquet", partition_cols=list(partition_cols or []))
 
     def write_csv(self, path: str, **kw):
-        self._write(path, "csv")
+        self._sized(kw)._write(path, "csv")
 
     def write_json(self, path: str, **kw):
-        self._write(path, "json")
+        self._sized(kw)._write(path, "json")
 
     def write_numpy(self, path: str, *, column: str = "data", **kw):
-        self._write(path, "npy", column=column)
+        self._sized(kw)._write(path, "npy", column=column)
+
+    def _sized(self, kw) -> "Dataset":
+        """``min_rows_per_file`` / ``num_rows_per_file`` (reference writers): coalesce blocks so
+        every written file holds at least that many rows (one file per block otherwise)."""
+        n = kw.get("min_rows_per_file") or kw.get("num_rows_per_file")
+        if not n:
+            return self
+        total = self.count()
+        return self.repartition(max(1, total // int(n)))
 
     def write_datasink(self, datasink, *, ray_remote_args=None, concurrency=None):
         from .datasource import write_datasink

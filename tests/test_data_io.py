@@ -160,3 +160,14 @@ def test_hive_partitioned_parquet_and_csv_options(ray_start_regular, tmp_path):
     tsv.write_text("a\tb\n1\t2\n3\t4\n")
     t = data.read_csv(str(tsv), parse_options=pcsv.ParseOptions(delimiter="\t"))
     assert t.take_all() == [{"a": 1, "b": 2}, {"a": 3, "b": 4}]
+
+
+def test_min_rows_per_file(ray_start_regular, tmp_path):
+    from ray_community_amd import data
+
+    ds = data.range(100, override_num_blocks=10)
+    out = str(tmp_path / "csv")
+    ds.write_csv(out, min_rows_per_file=30)
+    files = os.listdir(out)
+    assert len(files) == 3
+    assert data.read_csv(out).count() == 100
