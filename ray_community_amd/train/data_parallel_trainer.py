@@ -103,10 +103,45 @@ class DataParallelTrainer(BaseTrainer):
             w.init()
         name, exp_dir = self._experiment_dir()
         trial_dir = exp_dir
-        result = self._run(trial_dir, name)
+        result = self._run(trial_dir, name, self._standalone_reporter(trial_dir))
+        cbs = list(getattr(self.run_config, "callbacks", None) or [])
+        if cbs:
+            trial = self._cb_trial
+            trial.status = "ERROR" if result.error is not None else "TERMINATED"
+            for cb in cbs:
+                if hasattr(cb, "on_trial_complete"):
+                    cb.on_trial_complete(iteration=0, trials=[trial], trial=trial)
         if result.error is not None and not getattr(self, "_in_tune", False):
             raise result.error
         return result
+
+    def _standalone_reporter(self, trial_dir):
+        """``fit()`` outside Tune still honours ``RunConfig.stop`` and ``RunConfig.callbacks`` (the
+        reference runs every trainer through a one-trial Tune experiment)."""
+        from ..tune.tuner import Trial, evaluate_stop
+
+        stop = getattr(self.run_config, "stop", None)
+        cbs = list(getattr(self.run_config, "callbacks", None) or [])
+        trial = Trial(os.path.basename(trial_dir), dict(self.train_loop_config or {}), trial_dir, {})
+        trial.status = "RUNNING"
+        trial.start_time = time.time()
+        self._cb_trial = trial
+        if stop is None and not cbs:
+            return None
+
+        def on_report(metrics, checkpoint):
+            trial.last_result = metrics
+            trial.metrics_history.append(metrics)
+            if checkpoint is not None:
+                trial.checkpoint = checkpoint
+            for cb in cbs:
+                if hasattr(cb, "on_trial_result"):
+                    cb.on_trial_result(iteration=len(trial.metrics_history), trials=[trial], trial=trial,
+                                       result=metrics)
+            s, s_all = evaluate_stop(stop, trial.trial_id, metrics)
+            return s or s_all
+
+        return on_report
 
     def _fit_in_trial(self, trial_dir=None, report_callback=None):
         name, exp_dir = self._experiment_dir()

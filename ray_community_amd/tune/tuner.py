@@ -167,6 +167,25 @@ class _ClassTrainableRunner:
         return True
 
 
+def evaluate_stop(stop, trial_id, result):
+    """``RunConfig.stop`` semantics (reference ``tune/stopper``): a dict stops once any listed
+    metric reaches its value, a ``Stopper`` / callable decides per result (a Stopper's
+    ``stop_all()`` ends the whole experiment), ``result["done"]`` always stops.
+    Returns ``(stop_this_trial, stop_all)``."""
+    if stop is None:
+        return bool(result.get("done")), False
+    if isinstance(stop, dict):
+        for k, v in stop.items():
+            if k in result and result[k] >= v:
+                return True, False
+        return bool(result.get("done")), False
+    if isinstance(stop, Stopper):
+        return bool(stop(trial_id, result)), bool(stop.stop_all())
+    if callable(stop):
+        return bool(stop(trial_id, result)), False
+    return False, False
+
+
 class Trial:
     def __init__(self, trial_id: str, config: Dict, local_path: str, resources: Dict):
         self.trial_id = trial_id
@@ -534,21 +553,10 @@ class TuneController:
         return bool(self._searcher_done)
 
     def _should_stop(self, trial, result) -> bool:
-        stop = self.rc.stop
-        if stop is None:
-            return bool(result.get("done"))
-        if isinstance(stop, dict):
-            for k, v in stop.items():
-                if k in result and result[k] >= v:
-                    return True
-            return bool(result.get("done"))
-        if isinstance(stop, Stopper):
-            if stop.stop_all():
-                self._stop_all = True
-            return bool(stop(trial.trial_id, result))
-        if callable(stop):
-            return bool(stop(trial.trial_id, result))
-        return False
+        stop_trial, stop_all = evaluate_stop(self.rc.stop, trial.trial_id, result)
+        if stop_all:
+            self._stop_all = True
+        return stop_trial
 
     def _on_result(self, trial: Trial, metrics: Dict, ckpt_path: Optional[str]):
         m = dict(metrics)

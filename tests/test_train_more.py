@@ -104,3 +104,36 @@ def test_ddp_flat_grads_survive_set_to_none_zero_grad():
             slot = ddp.flat.grad[off: off + p.numel()].view_as(p)
             assert p.grad.data_ptr() == slot.data_ptr() and torch.equal(p.grad, slot)
         opt.step()
+
+
+def test_trainer_fit_honours_stop_and_callbacks(ray4, tmp_path):
+    """Standalone ``fit()`` applies RunConfig.stop (dict / callable) and calls RunConfig.callbacks
+    (on_trial_result per report, on_trial_complete once), as the reference's one-trial Tune run."""
+    import time as _t
+
+    from ray_community_amd import tune
+
+    def loop(config):
+        for i in range(20):
+            train.report({"i": i, "loss": 1.0 / (i + 1)})
+            _t.sleep(0.02)
+
+    class CB(tune.Callback):
+        def __init__(self):
+            self.results, self.completed = [], 0
+
+        def on_trial_result(self, iteration, trials, trial, result, **info):
+            self.results.append(result["i"])
+
+        def on_trial_complete(self, iteration, trials, trial, **info):
+            self.completed += 1
+
+    cb = CB()
+    r = DataParallelTrainer(loop, scaling_config=ScalingConfig(num_workers=1),
+                            run_config=RunConfig(name="stop1", storage_path=str(tmp_path),
+                                                 stop={"training_iteration": 4}, callbacks=[cb])).fit()
+    assert r.metrics["i"] == 3 and cb.results == [0, 1, 2, 3] and cb.completed == 1
+    r2 = DataParallelTrainer(loop, scaling_config=ScalingConfig(num_workers=2),
+                             run_config=RunConfig(name="stop2", storage_path=str(tmp_path),
+                                                  stop=lambda tid, res: res["loss"] < 0.2)).fit()
+    assert r2.metrics["i"] == 5  # first report with loss = 1/6 < 0.2
