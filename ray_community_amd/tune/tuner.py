@@ -167,6 +167,22 @@ class _ClassTrainableRunner:
         return True
 
 
+def _add_flat_keys(m: Dict, prefix: str = "", out: Optional[Dict] = None):
+    """Nested result dicts also get ``"outer/inner"`` keys (reference: metrics such as
+    ``"env_runners/episode_return_mean"`` work in TuneConfig(metric=), stoppers, schedulers,
+    searchers and ``get_best_result``); the nested values stay as they are."""
+    out = m if out is None else out
+    for k, v in list(m.items()):
+        if isinstance(v, dict) and k != "config" and v:
+            for k2, v2 in v.items():
+                key = f"{prefix}{k}/{k2}"
+                if isinstance(v2, dict):
+                    _add_flat_keys({k2: v2}, prefix=f"{prefix}{k}/", out=out)
+                else:
+                    out.setdefault(key, v2)
+    return out
+
+
 def evaluate_stop(stop, trial_id, result):
     """``RunConfig.stop`` semantics (reference ``tune/stopper``): a dict stops once any listed
     metric reaches its value, a ``Stopper`` / callable decides per result (a Stopper's
@@ -560,6 +576,7 @@ class TuneController:
 
     def _on_result(self, trial: Trial, metrics: Dict, ckpt_path: Optional[str]):
         m = dict(metrics)
+        _add_flat_keys(m)
         if trial.iteration_offset:
             m["training_iteration"] = m.get("training_iteration", 0) + trial.iteration_offset
         m.setdefault("training_iteration", len(trial.metrics_history) + 1)
@@ -734,6 +751,8 @@ class Tuner:
         from .registry import resolve_trainable
 
         self.trainable = resolve_trainable(trainable)  # a name from tune.register_trainable works too
+        if param_space is not None and not isinstance(param_space, dict) and hasattr(param_space, "to_dict"):
+            param_space = param_space.to_dict()  # an RLlib AlgorithmConfig (its search-space leaves kept)
         self.param_space = param_space or {}
         self.tune_config = tune_config or TuneConfig()
         from ..train.data_parallel_trainer import BaseTrainer

@@ -141,3 +141,25 @@ def test_repeater_reports_group_means_to_the_wrapped_searcher():
     assert len(inner.done) == 1  # the group of t3..t5 is not complete yet
     rep.on_trial_complete("t5", {"loss": 7.0})
     assert inner.done[-1] == ("t3", {"loss": 6.0}, False)
+
+
+def test_nested_metrics_and_algorithm_config_param_space(ray6, tmp_path):
+    """Nested result dicts are addressable as "outer/inner" (TuneConfig metric, stop, get_best_result,
+    dataframe), and an object with to_dict() (an RLlib AlgorithmConfig) is accepted as param_space."""
+
+    def trainable(config):
+        for i in range(10):
+            train.report({"env_runners": {"episode_return_mean": config["lr"] * (i + 1), "inner": {"x": i}}})
+
+    class Cfg:
+        def to_dict(self):
+            return {"lr": tune.grid_search([1.0, 2.0])}
+
+    grid = tune.Tuner(trainable, param_space=Cfg(),
+                      tune_config=tune.TuneConfig(metric="env_runners/episode_return_mean", mode="max"),
+                      run_config=train.RunConfig(name="nested", storage_path=str(tmp_path),
+                                                 stop={"env_runners/inner/x": 4})).fit()
+    assert sorted(r.metrics["env_runners/inner/x"] for r in grid) == [4, 4]
+    best = grid.get_best_result()
+    assert best.config["lr"] == 2.0 and best.metrics["env_runners"]["episode_return_mean"] == 10.0
+    assert "env_runners/episode_return_mean" in grid.get_dataframe().columns
