@@ -80,6 +80,10 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
         if _state["core"] is not None:
             if ignore_reinit_error:
                 return RayContext(_state)
+            if address is not None and address == _state.get("address") and _state.get("head") is not None:
+                # ``ray.init(address=cluster.address)`` after an in-process ``cluster_utils.Cluster``
+                # started this very session: connecting to it is what the caller asked for
+                return RayContext(_state)
             raise RuntimeError("Maybe you called init() twice by accident? Use ignore_reinit_error=True.")
         if job_config is not None:
             if namespace is None and job_config.ray_namespace is not None:

@@ -166,3 +166,26 @@ def test_label_selector_places_tasks_and_actors_on_matching_nodes(ray_start_clus
         pending = where.options(label_selector={"accel": "tpu"}).remote()
         ready, _ = ray.wait([pending], timeout=1.0)
         assert not ready
+
+
+def test_init_with_cluster_address_connects_to_the_in_process_cluster():
+    """The reference's ``cluster = Cluster(initialize_head=True); ray.init(address=cluster.address)``
+    pattern: connecting to the session the cluster already started is not a double init."""
+    from ray_community_amd.cluster_utils import Cluster
+
+    c = Cluster(initialize_head=True, head_node_args={"num_cpus": 1})
+    try:
+        c.add_node(num_cpus=1, resources={"side": 1})
+        ctx = ray.init(address=c.address)
+        assert ctx is not None and ray.cluster_resources().get("side") == 1
+
+        @ray.remote(resources={"side": 1})
+        def f():
+            return "side"
+
+        assert ray.get(f.remote()) == "side"
+        with pytest.raises(RuntimeError):
+            ray.init()  # a different (new local) session is still a double init
+    finally:
+        ray.shutdown()
+        c.shutdown()
