@@ -23,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..parallel.fused_linear import FusedWgradLinear
+from ..parallel.fused_linear import FusedEmbedding, FusedWgradLinear
 
 
 @dataclass
@@ -138,7 +138,9 @@ class Llama(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.cfg = cfg
-        self.embed = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        # untied: the lookup's gradient goes straight into the flat buffer; tied, the weight also
+        # gets the lm-head gradient, so both must meet in autograd's single accumulation
+        self.embed = (nn.Embedding if cfg.tie_embeddings else FusedEmbedding)(cfg.vocab_size, cfg.hidden_size)
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.num_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.norm_eps)
         self.lm_head = None if cfg.tie_embeddings else FusedWgradLinear(cfg.hidden_size, cfg.vocab_size)

@@ -71,6 +71,7 @@ class _RMSNorm(torch.autograd.Function):
                                 float(eps), stream_ptr(x.device)), "rmsnorm_fwd")
         saved = s if s is not None else x2
         ctx.save_for_backward(saved, w, rstd)
+        ctx.weight = w
         ctx.has_res = residual is not None
         ctx.shape = x.shape
         if s is None:
@@ -88,10 +89,20 @@ class _RMSNorm(torch.autograd.Function):
         L = lib()
         nb = L.rca_rmsnorm_bwd_blocks(rows, H)
         part = torch.empty(nb, H, device=s.device, dtype=torch.float32)
-        dw = torch.empty_like(w)
+        # flat-buffer gradients (parallel/flat.py, DDP grad-ready hooks registered): the column sum
+        # accumulates dw straight into the weight's bf16 grad view -- no dw tensor, no separate
+        # AccumulateGrad add kernel (two per layer in the 8B step)
+        wp = ctx.weight
+        view = wp.grad
+        into = (ctx.needs_input_grad[1] and view is not None and view.dtype == torch.bfloat16 and view.is_cuda
+                and view.is_contiguous() and getattr(wp, "_rca_grad_ready", None) is not None)
+        dw = None if into else torch.empty_like(w)
         check(L.rca_rmsnorm_bwd(s.data_ptr(), dy2.data_ptr(), w.data_ptr(), rstd.data_ptr(), _p(ds2), dx.data_ptr(),
-                                part.data_ptr(), dw.data_ptr(), 0, 0, rows, H, stream_ptr(s.device)), "rmsnorm_bwd")
+                                part.data_ptr(), (view if into else dw).data_ptr(), 0, 1 if into else 0, rows, H,
+                                stream_ptr(s.device)), "rmsnorm_bwd")
         dx = dx.view(ctx.shape)
+        if into:
+            wp._rca_grad_ready(wp)
         return dx, dw, None, (dx if ctx.has_res else None)
 
 

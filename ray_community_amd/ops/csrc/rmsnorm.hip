@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_split(const bf16_t* __restric
   int parity = 0;
   for (int r0 = blockIdx.x * 2; r0 < rows; r0 += gridDim.x * 2, parity ^= 1) {
     const bool two = r0 + 1 < rows;
-    u32x4 ps[2][CPW], pg[2][CPW];
+    u32x4 ps[2][CPW], pg[2][CPW], pd[2][CPW];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int row = two ? r0 + k : r0;
@@ -231,6 +231,13 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_split(const bf16_t* __restric
       for (int i = 0; i < CPW; ++i) {
         ps[k][i] = __builtin_nontemporal_load(sr + cbase + i * 64);
         pg[k][i] = __builtin_nontemporal_load(gr + cbase + i * 64);
+      }
+      // the residual gradient is only added after the row-dot barrier: issue its loads now so
+      // they are in flight across the reduction instead of starting after it
+      if (dres) {
+        const u32x4* drr = reinterpret_cast<const u32x4*>(dres + (size_t)row * H);
+#pragma unroll
+        for (int i = 0; i < CPW; ++i) pd[k][i] = __builtin_nontemporal_load(drr + cbase + i * 64);
       }
     }
     float rr[2], dot[2] = {0.f, 0.f};
@@ -261,7 +268,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_split(const bf16_t* __restric
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int i = 0; i < CPW; ++i) asm volatile("" : "+v"(ps[k][i]), "+v"(pg[k][i]));
+      for (int i = 0; i < CPW; ++i) asm volatile("" : "+v"(ps[k][i]), "+v"(pg[k][i]), "+v"(pd[k][i]));
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (k == 1 && !two) break;
@@ -270,7 +277,6 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_split(const bf16_t* __restric
       const float r = rr[k];
       const float c = d * r * r * r * invH;
       u32x4* xr = reinterpret_cast<u32x4*>(dx + (size_t)row * H);
-      const u32x4* drr = dres ? reinterpret_cast<const u32x4*>(dres + (size_t)row * H) : nullptr;
 #pragma unroll
       for (int i = 0; i < CPW; ++i) {
         float sv[8], gv[8], o[8];
@@ -278,9 +284,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_split(const bf16_t* __restric
         unpack8(pg[k][i], gv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = r * wf[i][j] * gv[j] - c * sv[j];
-        if (drr) {
+        if (dres) {
           float t[8];
-          unpack8(__builtin_nontemporal_load(drr + cbase + i * 64), t);
+          unpack8(pd[k][i], t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += t[j];
         }

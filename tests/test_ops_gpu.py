@@ -585,3 +585,48 @@ def test_wgrad_plans_match_fp32(plan_shape, accumulate):
     ref = g2.float().t() @ x2.float() + (base if accumulate else 0.0)
     tol = 2e-2 * ref.abs().max().item()
     assert (out.float() - ref).abs().max().item() < tol
+
+
+def test_rmsnorm_weight_grads_accumulated_into_flat_buffer_match_plain_autograd():
+    """With flat gradient buffers + DDP grad-ready hooks the RMSNorm backward accumulates dw
+    straight into the bf16 grad view (no dw tensor, no AccumulateGrad add); the result equals the
+    plain-autograd gradient bit for bit and the bucket bookkeeping still counts the weight once."""
+    from ray_community_amd.models import build_llama
+    from ray_community_amd.parallel import DistributedDataParallel
+
+    def run(use_ddp):
+        torch.manual_seed(0)
+        net = build_llama("llama3-tiny", device=DEV)
+        mod = DistributedDataParallel(net, precompute_grad_norm=True) if use_ddp else net
+        toks = torch.randint(0, net.cfg.vocab_size, (2, 129), device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+        loss = mod(toks[:, :-1], toks[:, 1:])
+        loss.backward()
+        if use_ddp:
+            mod.finish_gradient_sync()
+            assert mod.flat.precomputed_sumsq is not None  # every bucket was counted
+        return {n: p.grad.detach().clone() for n, p in net.named_parameters() if "norm" in n}
+
+    plain, flat = run(False), run(True)
+    assert plain.keys() == flat.keys() and len(plain) >= 3
+    for k in plain:
+        assert torch.equal(plain[k], flat[k]), k
+
+
+def test_fused_embedding_grad_into_flat_buffer_matches_dense():
+    """FusedEmbedding scatter-adds into the flat bf16 grad view (DDP hooks registered) and equals
+    torch's dense embedding gradient; repeated token ids accumulate."""
+    from ray_community_amd.parallel import DistributedDataParallel
+    from ray_community_amd.parallel.fused_linear import FusedEmbedding
+
+    torch.manual_seed(0)
+    emb = FusedEmbedding(1000, 256).to(device=DEV, dtype=torch.bfloat16)
+    ref = torch.nn.Embedding(1000, 256).to(device=DEV, dtype=torch.bfloat16)
+    ref.weight.data.copy_(emb.weight.data)
+    ddp = DistributedDataParallel(torch.nn.ModuleDict({"e": emb}), precompute_grad_norm=True)
+    idx = torch.randint(0, 50, (4, 300), device=DEV)  # many repeats
+    g = torch.randn(4, 300, 256, device=DEV, dtype=torch.bfloat16)
+    emb(idx).backward(g)
+    ddp.finish_gradient_sync()
+    ref(idx).backward(g)
+    assert emb.weight.grad.data_ptr() == ddp.flat.grad.data_ptr() + ddp.flat.param_offset[id(emb.weight)] * 2
+    assert torch.equal(emb.weight.grad, ref.weight.grad)  # same fp32-accumulating kernel, one rounding
