@@ -26,7 +26,7 @@ __all__ = [
     "grad_sumsq",
     "compute_gae",
     "vtrace",
-    "standardize_",
+    "standardize_", "gbdt_histogram",
     "batched_concat",
     "image_normalize",
     "crop_resize_normalize",
@@ -507,6 +507,39 @@ def standardize_(x, eps=1e-4):
         return x
     m, s = x.mean(), x.std(unbiased=False)
     return x.sub_(m).div_(s + eps)
+
+
+# ----------------------------------------------------------------------------------- GBDT
+def gbdt_histogram(bins, node, gh, num_nodes, out=None):
+    """Per-node gradient histograms for histogram GBDT (``train/gbdt``).
+
+    bins: uint8 [F, ld] feature-major quantised matrix (bin 255 = missing), node: int32 [ld] node
+    slot of every row (-1 = skip), gh: float32 [ld, C] (grad, hess[, count]).
+    Returns float32 [num_nodes, F, 256, C]. GPU: ``gbdt_hist_kernel`` (LDS-private histograms,
+    ld % 4 == 0); CPU: one ``index_add_``."""
+    F, ld = bins.shape
+    C = gh.shape[1]
+    if out is None:
+        out = torch.zeros(num_nodes, F, 256, C, dtype=torch.float32, device=bins.device)
+    else:
+        out.zero_()
+    if bins.is_cuda:
+        assert bins.dtype == torch.uint8 and node.dtype == torch.int32 and gh.dtype == torch.float32
+        assert bins.is_contiguous() and node.is_contiguous() and gh.is_contiguous()
+        assert ld % 4 == 0 and node.numel() == ld and gh.shape[0] == ld and C in (2, 3)
+        assert out.shape == (num_nodes, F, 256, C) and out.is_contiguous()
+        check(lib().rca_gbdt_hist(bins.data_ptr(), node.data_ptr(), gh.data_ptr(), out.data_ptr(), F, ld,
+                                  int(num_nodes), C, stream_ptr(bins.device)), "gbdt_hist")
+        return out
+    keep = (node >= 0) & (node < num_nodes)
+    rows = keep.nonzero().squeeze(1)
+    if rows.numel() == 0:
+        return out
+    nd = node[rows].long()
+    idx = (nd[None, :] * F + torch.arange(F, device=bins.device)[:, None]) * 256 + bins[:, rows].long()
+    vals = gh[rows].unsqueeze(0).expand(F, -1, -1)
+    out.view(-1, C).index_add_(0, idx.reshape(-1), vals.reshape(-1, C))
+    return out
 
 
 # ----------------------------------------------------------------------------------- data ops
