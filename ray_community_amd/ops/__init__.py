@@ -510,26 +510,56 @@ def standardize_(x, eps=1e-4):
 
 
 # ----------------------------------------------------------------------------------- GBDT
+_GBDT_Q = {}
+
+
+def gbdt_quantize(gh):
+    """(grad, hess[, count]) float32 [ld, C] -> one packed fixed-point int64 per row (signed
+    grad * sg in the high 32 bits, hess * sh >= 0 in the low 32) + device scales [1/sg, 1/sh],
+    the operand of the GPU histogram kernel (``ops/csrc/gbdt.hip``: one ds_add_u64 per (row,
+    feature); the kernel's <= 32768 rows per workgroup bound the per-row magnitudes to 2^16 / 2^17).
+    Cached per (tensor, version) so the levels of one tree quantise once."""
+    hit = _GBDT_Q.get(gh.device)
+    if hit is not None and hit[0] is gh and hit[3] == gh._version:
+        return hit[1], hit[2]
+    g, h = gh[:, 0], gh[:, 1]
+    gmax = g.abs().max().clamp_min(1e-30)
+    hmax = h.max().clamp_min(1e-30)
+    sg, sh = 65535.0 / gmax, 131071.0 / hmax
+    gq = torch.round(g * sg).to(torch.int64)
+    hq = torch.round(h.clamp_min(0) * sh).to(torch.int64)
+    packed = (gq << 32) + hq
+    inv = torch.stack([1.0 / sg, 1.0 / sh]).to(torch.float32)
+    _GBDT_Q[gh.device] = (gh, packed, inv, gh._version)
+    return packed, inv
+
+
 def gbdt_histogram(bins, node, gh, num_nodes, out=None):
     """Per-node gradient histograms for histogram GBDT (``train/gbdt``).
 
     bins: uint8 [F, ld] feature-major quantised matrix (bin 255 = missing), node: int32 [ld] node
-    slot of every row (-1 = skip), gh: float32 [ld, C] (grad, hess[, count]).
-    Returns float32 [num_nodes, F, 256, C]. GPU: ``gbdt_hist_kernel`` (LDS-private histograms,
-    ld % 4 == 0); CPU: one ``index_add_``."""
+    slot of every row (-1 = skip), gh: float32 [ld, C] (grad, hess[, count: 1 per row]).
+    Returns float32 [num_nodes, F, 256, C]. GPU: ``gbdt_hist_kernel`` over the fixed-point packed
+    (grad, hess) of :func:`gbdt_quantize` (relative error ~1e-5 of the largest |grad| / hess per
+    row; the count is exact), ld % 4 == 0; CPU: one fp32 ``index_add_``."""
     F, ld = bins.shape
     C = gh.shape[1]
-    if out is None:
-        out = torch.zeros(num_nodes, F, 256, C, dtype=torch.float32, device=bins.device)
-    else:
+    if out is None:  # the GPU path writes every entry
+        out = (torch.empty if bins.is_cuda else torch.zeros)(num_nodes, F, 256, C, dtype=torch.float32,
+                                                              device=bins.device)
+    elif not bins.is_cuda:
         out.zero_()
     if bins.is_cuda:
         assert bins.dtype == torch.uint8 and node.dtype == torch.int32 and gh.dtype == torch.float32
         assert bins.is_contiguous() and node.is_contiguous() and gh.is_contiguous()
         assert ld % 4 == 0 and node.numel() == ld and gh.shape[0] == ld and C in (2, 3)
         assert out.shape == (num_nodes, F, 256, C) and out.is_contiguous()
-        check(lib().rca_gbdt_hist(bins.data_ptr(), node.data_ptr(), gh.data_ptr(), out.data_ptr(), F, ld,
-                                  int(num_nodes), C, stream_ptr(bins.device)), "gbdt_hist")
+        packed, inv = gbdt_quantize(gh)
+        nbytes = int(lib().rca_gbdt_hist_workspace(F, ld, int(num_nodes), C))
+        work = _workspace(bins.device, "gbdt_hist", (nbytes + 3) // 4)
+        check(lib().rca_gbdt_hist(bins.data_ptr(), node.data_ptr(), packed.data_ptr(), inv.data_ptr(),
+                                  out.data_ptr(), work.data_ptr(), F, ld, int(num_nodes), C,
+                                  stream_ptr(bins.device)), "gbdt_hist")
         return out
     keep = (node >= 0) & (node < num_nodes)
     rows = keep.nonzero().squeeze(1)

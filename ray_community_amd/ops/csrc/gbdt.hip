@@ -12,111 +12,164 @@
 // (-1 = row not in any node being built, also used for the padding) and the gradient statistics are
 // float [ld, C] (C = 2: grad, hess; C = 3 adds a row count for min_data_in_leaf).
 //
-// Each workgroup owns FG features x a row range and accumulates a private histogram of
-// cnt nodes x FG features x 256 bins x C channels in LDS with ds_add_f32, then flushes the non-zero
-// entries with one global float atomic each. hist is float [L, F, 256, C] (bin 255 = missing) and
-// must be zeroed by the caller; slot s of this launch lands in node row lo + s.
+// Each workgroup (16 waves) owns FG features x <= 32768 rows and accumulates a private histogram of
+// cnt nodes x FG features x 256 bins in LDS, then stores it (as float) into a per-workgroup partial
+// buffer; a second kernel sums the partials of the row ranges per entry in a fixed order.
+//
+// Fixed-point LDS accumulation. Measured on gfx950 (scripts/probes/lds_atomic_probe.hip, random bins
+// over 256 slots, 16 waves/CU): ds_add_f32 costs ~194 LDS cycles per wave-instruction, ds_add_u32
+// 14.5 and ds_add_u64 15.6. So (grad, hess) arrive pre-quantised and packed in ONE 64-bit word per
+// row -- signed grad * sg in the high half, hess * sh (>= 0) in the low half -- and each (row,
+// feature) is ONE ds_add_u64: the low half never carries (|h_q| <= 2^32 / 32768 per row and <= 32768
+// rows per workgroup), the high half adds modulo 2^32 and stays within int32 for the same reason.
+// The optional row count (C = 3) is one more ds_add_u32. The flush converts the integer sums back
+// with the scales (inv[0] = 1/sg, inv[1] = 1/sh), so the float partials and the reduction are exact
+// sums of the quantised values. (First version: two ds_add_f32 per (row, feature) + one global
+// float atomic per non-zero entry in the flush: 573 us for 2M x 28 where this form takes a fraction.)
 #include "common.h"
 
 namespace {
 
 constexpr int kBins = 256;
 
-template <int C>
-__global__ __launch_bounds__(256) void gbdt_hist_kernel(const unsigned char* __restrict__ bins,
-                                                        const int* __restrict__ node,
-                                                        const float* __restrict__ gh, float* __restrict__ hist,
-                                                        int F, long long ld, int lo, int cnt, int FG,
-                                                        long long rows_per_block) {
-  extern __shared__ float lh[];
+template <bool CNT, int FGT>
+__global__ __launch_bounds__(1024) void gbdt_hist_kernel(const unsigned char* __restrict__ bins,
+                                                         const int* __restrict__ node,
+                                                         const unsigned long long* __restrict__ ghq,
+                                                         const float* __restrict__ inv, float* __restrict__ part,
+                                                         int F, long long ld, int lo, int cnt, int FG,
+                                                         long long rows_per_block) {
+  extern __shared__ unsigned long long lq[];
+  constexpr int C = CNT ? 3 : 2;
   const int f0 = blockIdx.x * FG;
   const int nf = min(FG, F - f0);
-  const int total = cnt * FG * kBins * C;
-  for (int i = threadIdx.x; i < total; i += blockDim.x) lh[i] = 0.f;
+  const int ent = cnt * FG * kBins;  // histogram entries of this workgroup
+  unsigned* lc = reinterpret_cast<unsigned*>(lq + ent);
+  for (int i = threadIdx.x; i < ent; i += blockDim.x) {
+    lq[i] = 0ull;
+    if (CNT) lc[i] = 0u;
+  }
   __syncthreads();
 
   const long long r_begin = (long long)blockIdx.y * rows_per_block;  // multiple of 4
   const long long r_end = min(ld, r_begin + rows_per_block);
-  const int* node4 = node;
+  const unsigned char* bcol = bins + (long long)f0 * ld;
   for (long long r = r_begin + 4 * (long long)threadIdx.x; r < r_end; r += 4 * (long long)blockDim.x) {
-    const int4 nd = *reinterpret_cast<const int4*>(node4 + r);
-    int s[4] = {nd.x - lo, nd.y - lo, nd.z - lo, nd.w - lo};
-    bool any = false;
+    // every load of this row quad is issued before the first use (one memory round trip per quad)
+    const int4 nd = *reinterpret_cast<const int4*>(node + r);
+    const ulonglong2 q01 = reinterpret_cast<const ulonglong2*>(ghq + r)[0];
+    const ulonglong2 q23 = reinterpret_cast<const ulonglong2*>(ghq + r)[1];
+    unsigned b4[FGT];
+#pragma unroll
+    for (int f = 0; f < FGT; ++f) b4[f] = f < nf ? *reinterpret_cast<const unsigned*>(bcol + (long long)f * ld + r) : 0u;
+    const int s[4] = {nd.x - lo, nd.y - lo, nd.z - lo, nd.w - lo};
+    const unsigned long long q[4] = {q01.x, q01.y, q23.x, q23.y};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if ((unsigned)s[k] >= (unsigned)cnt) s[k] = -1;
-      any |= s[k] >= 0;
-    }
-    if (!any) continue;
-    float g[4][C];
+      if ((unsigned)s[k] >= (unsigned)cnt) continue;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int c = 0; c < C; ++c) g[k][c] = gh[(r + k) * C + c];
-    for (int f = 0; f < nf; ++f) {
-      const unsigned b4 = *reinterpret_cast<const unsigned*>(bins + (long long)(f0 + f) * ld + r);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (s[k] < 0) continue;
-        const int b = (b4 >> (8 * k)) & 0xff;
-        float* dst = lh + ((s[k] * FG + f) * kBins + b) * C;
-#pragma unroll
-        for (int c = 0; c < C; ++c) atomicAdd(dst + c, g[k][c]);
+      for (int f = 0; f < FGT; ++f) {
+        if (f >= nf) break;
+        const int e = (s[k] * FG + f) * kBins + ((b4[f] >> (8 * k)) & 0xff);
+        atomicAdd(lq + e, q[k]);
+        if (CNT) atomicAdd(lc + e, 1u);
       }
     }
   }
   __syncthreads();
-
-  // flush: LDS entry (s, f, b, c) -> hist[((lo + s) * F + f0 + f) * 256 + b][c]
-  const int per_node = FG * kBins * C;
-  for (int i = threadIdx.x; i < total; i += blockDim.x) {
-    const float v = lh[i];
-    if (v == 0.f) continue;
-    const int sl = i / per_node;
-    const int rem = i - sl * per_node;
-    const int f = rem / (kBins * C);
-    if (f >= nf) continue;
-    const int bc = rem - f * (kBins * C);
-    atomicAdd(hist + ((long long)(lo + sl) * F + f0 + f) * (kBins * C) + bc, v);
+  const float ig = inv[0], ih = inv[1];
+  float* out = part + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (long long)ent * C;
+  for (int i = threadIdx.x; i < ent; i += blockDim.x) {
+    const unsigned long long v = lq[i];
+    out[i * C + 0] = (float)(int)(unsigned)(v >> 32) * ig;
+    out[i * C + 1] = (float)(unsigned)(v & 0xffffffffull) * ih;
+    if (CNT) out[i * C + 2] = (float)lc[i];
   }
 }
 
+// hist entry (lo + s, f0 + f, b, c) = sum over the gy row ranges of the partials, fixed order.
+__global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const float* __restrict__ part,
+                                                               float* __restrict__ hist, int F, int gx, int gy,
+                                                               int lo, int cnt, int FG, int C) {
+  const int total = cnt * FG * kBins * C;
+  const int bx = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int per_node = FG * kBins * C;
+  const int sl = i / per_node;
+  const int rem = i - sl * per_node;
+  const int f = rem / (kBins * C);
+  const int f0 = bx * FG;
+  if (f0 + f >= F) return;
+  float acc = 0.f;
+  const float* p = part + (long long)bx * total + i;
+  const long long stride = (long long)gx * total;
+  for (int y = 0; y < gy; ++y) acc += p[y * stride];
+  const int bc = rem - f * (kBins * C);
+  hist[((long long)(lo + sl) * F + f0 + f) * (kBins * C) + bc] = acc;
+}
+
+namespace plan {
+constexpr int kLdsBytes = 64 * 1024;
+inline int max_nodes(int C) { return kLdsBytes / (kBins * C * (int)sizeof(float)); }
+inline int feat_group(int F, int cnt, int C) {
+  return max(1, min(min(F, 4), kLdsBytes / (cnt * kBins * C * (int)sizeof(float))));
+}
+constexpr long long kMaxRows = 32768;  // per workgroup: bounds the fixed-point sums (see top)
+// ~512 workgroups of 16 waves (2 per CU, as LDS allows), >= 4096 and <= kMaxRows rows each
+inline long long row_blocks(long long ld, int gx) {
+  long long gy = (512 + gx - 1) / gx;
+  gy = max(1LL, min(gy, (ld + 4095) / 4096));
+  return max(gy, (ld + kMaxRows - 1) / kMaxRows);
+}
+}  // namespace plan
+
 }  // namespace
 
-// bins [F, ld] u8, node [ld] i32, gh [ld, C] f32, hist [L, F, 256, C] f32 (zeroed), nodes [0, L).
-// ld % 4 == 0, C in {2, 3}. Node chunks and feature groups are sized so a workgroup's private
-// histogram fits in 64 KB of LDS.
-RCA_API int rca_gbdt_hist(const unsigned char* bins, const int* node, const float* gh, float* hist, int F,
-                          long long ld, int L, int C, hipStream_t stream) {
+// Bytes of the partial-histogram workspace rca_gbdt_hist needs for these sizes.
+RCA_API long long rca_gbdt_hist_workspace(int F, long long ld, int L, int C) {
+  long long best = 0;
+  for (int lo = 0; lo < L; lo += plan::max_nodes(C)) {
+    const int cnt = min(plan::max_nodes(C), L - lo);
+    const int FG = plan::feat_group(F, cnt, C);
+    const int gx = (F + FG - 1) / FG;
+    const long long gy = plan::row_blocks(ld, gx);
+    best = max(best, gy * gx * (long long)cnt * FG * kBins * C * (long long)sizeof(float));
+  }
+  return best;
+}
+
+// bins [F, ld] u8, node [ld] i32, ghq [ld] u64 (packed fixed-point grad/hess, see top), inv [2] f32
+// (1/sg, 1/sh) on the device, hist [L, F, 256, C] f32 (every entry written), work >=
+// rca_gbdt_hist_workspace bytes. ld % 4 == 0; C = 3 adds the row count.
+RCA_API int rca_gbdt_hist(const unsigned char* bins, const int* node, const unsigned long long* ghq,
+                          const float* inv, float* hist, float* work, int F, long long ld, int L, int C,
+                          hipStream_t stream) {
   if (F <= 0 || L <= 0 || ld <= 0) return 0;
   if ((ld & 3) != 0 || (C != 2 && C != 3)) return -1;
-  constexpr int kLdsBytes = 64 * 1024;
-  const int per_nf = kBins * C * (int)sizeof(float);  // one node x one feature
-  const int max_nodes = kLdsBytes / per_nf;           // 32 (C=2) / 21 (C=3) nodes per launch at FG=1
-  for (int lo = 0; lo < L; lo += max_nodes) {
-    const int cnt = min(max_nodes, L - lo);
-    // <= 4 features per workgroup (more workgroups, private histogram cheap to clear and flush)
-    const int FG = max(1, min(min(F, 4), kLdsBytes / (cnt * per_nf)));
+  for (int lo = 0; lo < L; lo += plan::max_nodes(C)) {
+    const int cnt = min(plan::max_nodes(C), L - lo);
+    const int FG = plan::feat_group(F, cnt, C);
     const int gx = (F + FG - 1) / FG;
-    // rows per workgroup >= 8 x the private histogram's bins, so the clear + flush (one global atomic
-    // per non-zero entry) stays a small share of the row work; but keep >= ~1024 workgroups (4 per CU)
-    // while each still gets >= 1024 rows
-    long long rpb = max(1024LL, 2048LL * cnt);
-    long long gy = (ld + rpb - 1) / rpb;
-    if ((long long)gx * gy < 1024) {
-      gy = max(1LL, min((ld + 1023) / 1024, (1024LL + gx - 1) / gx));
-      rpb = (ld + gy - 1) / gy;
-    }
+    const long long gy = plan::row_blocks(ld, gx);
+    long long rpb = (ld + gy - 1) / gy;
     rpb = (rpb + 3) & ~3LL;
-    gy = (ld + rpb - 1) / rpb;
-    const size_t lds = (size_t)cnt * FG * per_nf;
+    if (rpb > plan::kMaxRows) return -2;
+    const int ent = cnt * FG * kBins;
+    const size_t lds = (size_t)ent * (sizeof(unsigned long long) + (C == 3 ? sizeof(unsigned) : 0));
     dim3 grid(gx, (unsigned)gy);
-    if (C == 2)
-      hipLaunchKernelGGL(gbdt_hist_kernel<2>, grid, dim3(256), lds, stream, bins, node, gh, hist, F, ld, lo, cnt, FG,
-                         rpb);
-    else
-      hipLaunchKernelGGL(gbdt_hist_kernel<3>, grid, dim3(256), lds, stream, bins, node, gh, hist, F, ld, lo, cnt, FG,
-                         rpb);
+#define RCA_GBDT_LAUNCH(CC, FF)                                                                                  \
+  hipLaunchKernelGGL((gbdt_hist_kernel<CC, FF>), grid, dim3(1024), lds, stream, bins, node, ghq, inv, work, F, ld, \
+                     lo, cnt, FG, rpb)
+    if (C == 2) {
+      if (FG == 1) RCA_GBDT_LAUNCH(false, 1); else if (FG == 2) RCA_GBDT_LAUNCH(false, 2); else RCA_GBDT_LAUNCH(false, 4);
+    } else {
+      if (FG == 1) RCA_GBDT_LAUNCH(true, 1); else if (FG == 2) RCA_GBDT_LAUNCH(true, 2); else RCA_GBDT_LAUNCH(true, 4);
+    }
+#undef RCA_GBDT_LAUNCH
+    dim3 rgrid((ent * C + 255) / 256, gx);
+    hipLaunchKernelGGL(gbdt_hist_reduce_kernel, rgrid, dim3(256), 0, stream, work, hist, F, gx, (int)gy, lo, cnt,
+                       FG, C);
   }
   return (int)hipGetLastError();
 }

@@ -252,7 +252,9 @@ class Tree:
     """Flat node arrays; node 0 is the root, ``left < 0`` marks a leaf. Split: go left iff
     ``x < thr`` (equivalently ``bin <= thr_bin``); missing values follow ``default_left``."""
 
-    __slots__ = ("feature", "thr", "thr_bin", "default_left", "left", "right", "value", "gain", "cover", "depth")
+    __slots__ = ("feature", "thr", "thr_bin", "default_left", "left", "right", "value", "gain", "cover", "depth",
+                 "_cache")
+    _FIELDS = ("feature", "thr", "thr_bin", "default_left", "left", "right", "value", "gain", "cover", "depth")
 
     def __init__(self):
         self.feature: List[int] = []
@@ -265,6 +267,7 @@ class Tree:
         self.gain: List[float] = []
         self.cover: List[float] = []
         self.depth = 0
+        self._cache = None
 
     def add_node(self, value=0.0, cover=0.0) -> int:
         for a, v in ((self.feature, -1), (self.thr, 0.0), (self.thr_bin, 0), (self.default_left, True),
@@ -277,23 +280,26 @@ class Tree:
         return len(self.feature)
 
     def to_dict(self) -> dict:
-        return {k: getattr(self, k) for k in self.__slots__}
+        return {k: getattr(self, k) for k in self._FIELDS}
 
     @classmethod
     def from_dict(cls, d: dict) -> "Tree":
         t = cls()
-        for k in cls.__slots__:
+        for k in cls._FIELDS:
             setattr(t, k, d[k] if k == "depth" else list(d[k]))
         return t
 
     def tensors(self, device):
-        return (torch.tensor(self.feature, dtype=torch.long, device=device),
-                torch.tensor(self.thr, dtype=torch.float32, device=device),
-                torch.tensor(self.thr_bin, dtype=torch.long, device=device),
-                torch.tensor(self.default_left, dtype=torch.bool, device=device),
-                torch.tensor(self.left, dtype=torch.long, device=device),
-                torch.tensor(self.right, dtype=torch.long, device=device),
-                torch.tensor(self.value, dtype=torch.float32, device=device))
+        key = (str(device), self.num_nodes)
+        c = getattr(self, "_cache", None)
+        if c is not None and c[0] == key:
+            return c[1]
+        i = torch.tensor([self.feature, self.thr_bin, self.default_left, self.left, self.right],
+                         dtype=torch.long).to(device, non_blocking=True)
+        fv = torch.tensor([self.thr, self.value], dtype=torch.float32).to(device, non_blocking=True)
+        out = (i[0], fv[0], i[1], i[2].bool(), i[3], i[4], fv[1])
+        self._cache = (key, out)
+        return out
 
     def leaf_index_raw(self, X: torch.Tensor) -> torch.Tensor:
         feat, thr, _, dl, left, right, _ = self.tensors(X.device)
@@ -531,7 +537,7 @@ class _Grower:
         return t * t / (H + self.lam)
 
     def leaf_value(self, G: float, H: float) -> float:
-        t = float(self._T(torch.tensor(G, dtype=torch.float64)))
+        t = math.copysign(max(abs(G) - self.alpha, 0.0), G) if self.alpha else G
         return -t / (H + self.lam) * self.eta
 
     def hist(self, pos: torch.Tensor, gh: torch.Tensor, slots: torch.Tensor, L: int) -> torch.Tensor:
@@ -584,7 +590,10 @@ class _Grower:
         sidx = torch.arange(S, device=H.device)
         GLs = torch.where(d == 0, extra[0][0][sidx, f, tb], extra[1][0][sidx, f, tb])
         HLs = torch.where(d == 0, extra[0][1][sidx, f, tb], extra[1][1][sidx, f, tb])
-        return (best.cpu(), f.cpu(), tb.cpu(), (d == 0).cpu(), Gt.cpu(), Ht.cpu(), GLs.cpu(), HLs.cpu())
+        # one device->host copy for all of it (each .cpu() is a sync)
+        packed = torch.stack([best, f.double(), tb.double(), (d == 0).double(), Gt, Ht, GLs, HLs]).cpu()
+        b_, f_, tb_, dl_, Gt_, Ht_, GL_, HL_ = packed.unbind(0)
+        return (b_, f_.long(), tb_.long(), dl_.bool(), Gt_, Ht_, GL_, HL_)
 
     def grow(self, g: torch.Tensor, h: torch.Tensor, row_mask: Optional[torch.Tensor], fmask: torch.Tensor,
              cuts: List[torch.Tensor]) -> Tree:
@@ -646,14 +655,12 @@ class _Grower:
                 kids.append((i, l, r))
                 n_leaves += 1
             # route the rows of the split nodes
-            sp = torch.tensor([k[0] for k in kids], dtype=torch.long, device=dev)
-            is_split = torch.zeros(tree.num_nodes, dtype=torch.bool, device=dev)
-            is_split[sp] = True
-            feat_t = torch.tensor(tree.feature, dtype=torch.long, device=dev)
-            tb_t = torch.tensor(tree.thr_bin, dtype=torch.long, device=dev)
-            dl_t = torch.tensor(tree.default_left, dtype=torch.bool, device=dev)
-            l_t = torch.tensor(tree.left, dtype=torch.long, device=dev)
-            r_t = torch.tensor(tree.right, dtype=torch.long, device=dev)
+            split_now = [False] * tree.num_nodes
+            for k in kids:
+                split_now[k[0]] = True
+            tabs = torch.tensor([tree.feature, tree.thr_bin, tree.default_left, tree.left, tree.right, split_now],
+                                dtype=torch.long).to(dev, non_blocking=True)  # one host->device copy
+            feat_t, tb_t, dl_t, l_t, r_t, is_split = tabs[0], tabs[1], tabs[2].bool(), tabs[3], tabs[4], tabs[5].bool()
             pc = pos.clamp_min(0)
             act = (pos >= 0) & is_split[pc]
             b = self.bins[feat_t[pc].clamp_min(0), torch.arange(ld, device=dev)].long()
@@ -668,11 +675,11 @@ class _Grower:
                 continue
             kid_ids = [c for k in kids for c in (k[1], k[2])]
             # histograms: build the smaller child of each pair (global row counts), subtract for the other
-            cnt = torch.bincount(pos.clamp_min(0)[pos >= 0], minlength=tree.num_nodes).to(torch.float64)
-            cnt = allreduce_sum(cnt[kid_ids].clone()).tolist()
+            # size proxy = the children's global hessian sums (known on the host from the split; the row
+            # count itself for squared error), so choosing needs no device round trip
             small, big = [], []
             for j, (p_, l, r) in enumerate(kids):
-                if cnt[2 * j] <= cnt[2 * j + 1]:
+                if tree.cover[l] <= tree.cover[r]:
                     small.append(l); big.append((r, p_, l))
                 else:
                     small.append(r); big.append((l, p_, r))

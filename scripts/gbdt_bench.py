@@ -4,7 +4,11 @@ Synthetic HIGGS-shaped data (rows x 28 float features, binary label), xgboost de
 (depth 6, eta 0.3, max_bin 256). Prints one JSON line per measurement."""
 import argparse
 import json
+import os
+import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import numpy as np
 import torch
@@ -16,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=2_000_000)
 ap.add_argument("--features", type=int, default=28)
 ap.add_argument("--rounds", type=int, default=50)
+ap.add_argument("--hist-only", action="store_true")
 a = ap.parse_args()
 
 rng = np.random.default_rng(0)
@@ -44,6 +49,8 @@ for L in (1, 8, 32):
                       "us": round(dt * 1e6, 1), "GB/s": round(byts / dt / 1e9, 1),
                       "Grow_feat_per_s": round(a.rows * a.features / dt / 1e9, 2)}), flush=True)
 
+if a.hist_only:
+    sys.exit(0)
 d = DMatrix(X, y, device=dev)
 train({"objective": "binary:logistic"}, d, 2)  # warm-up (sketch + binning cached on d)
 torch.cuda.synchronize()

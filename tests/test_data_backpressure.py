@@ -38,7 +38,7 @@ def test_memory_budget_bounds_in_flight_tasks(ray_start_regular, ctx_reset):
     mp = [o for o in lim["ops"] if o["name"].startswith("MapBatches")][0]
     # ~128 KiB outputs, per-op budget = reserved half / 2 ops + shared remainder -> a handful in flight
     assert mp["peak_running"] <= 6 < peak_free or peak_free <= 6, (mp, peak_free)
-    assert mp["backpressured"] > 0
+    assert mp["backpressured"] > 0 or peak_free <= 6  # a loaded machine may never get ahead of the budget
 
 
 def test_cpu_limit_caps_global_concurrency(ray_start_regular, ctx_reset):
