@@ -12,16 +12,17 @@
 // (-1 = row not in any node being built, also used for the padding) and the gradient statistics are
 // float [ld, C] (C = 2: grad, hess; C = 3 adds a row count for min_data_in_leaf).
 //
-// Each workgroup (16 waves) owns FG features x <= 32768 rows and accumulates a private histogram of
-// cnt nodes x FG features x 256 bins in LDS, then stores it (as float) into a per-workgroup partial
+// Each workgroup (16 waves) owns FG features x a row range and accumulates a private histogram of
+// cnt nodes x FG features x 256 bins in LDS (folded into per-thread float accumulators after every
+// 32768-row chunk), then stores it into a per-workgroup partial
 // buffer; a second kernel sums the partials of the row ranges per entry in a fixed order.
 //
 // Fixed-point LDS accumulation. Measured on gfx950 (scripts/probes/lds_atomic_probe.hip, random bins
 // over 256 slots, 16 waves/CU): ds_add_f32 costs ~194 LDS cycles per wave-instruction, ds_add_u32
 // 14.5 and ds_add_u64 15.6. So (grad, hess) arrive pre-quantised and packed in ONE 64-bit word per
 // row -- signed grad * sg in the high half, hess * sh (>= 0) in the low half -- and each (row,
-// feature) is ONE ds_add_u64: the low half never carries (|h_q| <= 2^32 / 32768 per row and <= 32768
-// rows per workgroup), the high half adds modulo 2^32 and stays within int32 for the same reason.
+// feature) is ONE ds_add_u64: the low half never carries (|h_q| <= 2^32 / 32768 per row, rows taken in
+// chunks of 32768), the high half adds modulo 2^32 and stays within int32 for the same reason.
 // The optional row count (C = 3) is one more ds_add_u32. The flush converts the integer sums back
 // with the scales (inv[0] = 1/sg, inv[1] = 1/sh), so the float partials and the reduction are exact
 // sums of the quantised values. (First version: two ds_add_f32 per (row, feature) + one global
@@ -31,6 +32,8 @@
 namespace {
 
 constexpr int kBins = 256;
+constexpr long long kChunk = 32768;  // rows per fixed-point accumulation chunk (see top)
+constexpr int kPerThread = 8;        // LDS entries drained per thread: 64 KB / 8 B / 1024 threads
 
 template <bool CNT, int FGT>
 __global__ __launch_bounds__(1024) void gbdt_hist_kernel(const unsigned char* __restrict__ bins,
@@ -51,39 +54,68 @@ __global__ __launch_bounds__(1024) void gbdt_hist_kernel(const unsigned char* __
   }
   __syncthreads();
 
+  // entries this thread drains: i = threadIdx.x + j * 1024, j < kPerThread (ent <= 8192)
+  float acc[kPerThread][C];
+#pragma unroll
+  for (int j = 0; j < kPerThread; ++j)
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[j][c] = 0.f;
+
   const long long r_begin = (long long)blockIdx.y * rows_per_block;  // multiple of 4
   const long long r_end = min(ld, r_begin + rows_per_block);
   const unsigned char* bcol = bins + (long long)f0 * ld;
-  for (long long r = r_begin + 4 * (long long)threadIdx.x; r < r_end; r += 4 * (long long)blockDim.x) {
-    // every load of this row quad is issued before the first use (one memory round trip per quad)
-    const int4 nd = *reinterpret_cast<const int4*>(node + r);
-    const ulonglong2 q01 = reinterpret_cast<const ulonglong2*>(ghq + r)[0];
-    const ulonglong2 q23 = reinterpret_cast<const ulonglong2*>(ghq + r)[1];
-    unsigned b4[FGT];
+  const float ig = inv[0], ih = inv[1];
+  // rows in chunks of kChunk: the integer sums of one chunk fit their 32-bit halves (see top); after
+  // each chunk the LDS integers are folded into per-thread float accumulators and cleared
+  for (long long c0 = r_begin; c0 < r_end; c0 += kChunk) {
+    const long long c1 = min(r_end, c0 + kChunk);
+    for (long long r = c0 + 4 * (long long)threadIdx.x; r < c1; r += 4 * (long long)blockDim.x) {
+      // every load of this row quad is issued before the first use (one memory round trip per quad)
+      const int4 nd = *reinterpret_cast<const int4*>(node + r);
+      const ulonglong2 q01 = reinterpret_cast<const ulonglong2*>(ghq + r)[0];
+      const ulonglong2 q23 = reinterpret_cast<const ulonglong2*>(ghq + r)[1];
+      unsigned b4[FGT];
 #pragma unroll
-    for (int f = 0; f < FGT; ++f) b4[f] = f < nf ? *reinterpret_cast<const unsigned*>(bcol + (long long)f * ld + r) : 0u;
-    const int s[4] = {nd.x - lo, nd.y - lo, nd.z - lo, nd.w - lo};
-    const unsigned long long q[4] = {q01.x, q01.y, q23.x, q23.y};
+      for (int f = 0; f < FGT; ++f)
+        b4[f] = f < nf ? *reinterpret_cast<const unsigned*>(bcol + (long long)f * ld + r) : 0u;
+      const int s[4] = {nd.x - lo, nd.y - lo, nd.z - lo, nd.w - lo};
+      const unsigned long long q[4] = {q01.x, q01.y, q23.x, q23.y};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if ((unsigned)s[k] >= (unsigned)cnt) continue;
+      for (int k = 0; k < 4; ++k) {
+        if ((unsigned)s[k] >= (unsigned)cnt) continue;
 #pragma unroll
-      for (int f = 0; f < FGT; ++f) {
-        if (f >= nf) break;
-        const int e = (s[k] * FG + f) * kBins + ((b4[f] >> (8 * k)) & 0xff);
-        atomicAdd(lq + e, q[k]);
-        if (CNT) atomicAdd(lc + e, 1u);
+        for (int f = 0; f < FGT; ++f) {
+          if (f >= nf) break;
+          const int e = (s[k] * FG + f) * kBins + ((b4[f] >> (8 * k)) & 0xff);
+          atomicAdd(lq + e, q[k]);
+          if (CNT) atomicAdd(lc + e, 1u);
+        }
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+      const int i = threadIdx.x + j * 1024;
+      if (i < ent) {
+        const unsigned long long v = lq[i];
+        acc[j][0] += (float)(int)(unsigned)(v >> 32) * ig;
+        acc[j][1] += (float)(unsigned)(v & 0xffffffffull) * ih;
+        lq[i] = 0ull;
+        if (CNT) {
+          acc[j][C - 1] += (float)lc[i];
+          lc[i] = 0u;
+        }
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  const float ig = inv[0], ih = inv[1];
   float* out = part + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (long long)ent * C;
-  for (int i = threadIdx.x; i < ent; i += blockDim.x) {
-    const unsigned long long v = lq[i];
-    out[i * C + 0] = (float)(int)(unsigned)(v >> 32) * ig;
-    out[i * C + 1] = (float)(unsigned)(v & 0xffffffffull) * ih;
-    if (CNT) out[i * C + 2] = (float)lc[i];
+#pragma unroll
+  for (int j = 0; j < kPerThread; ++j) {
+    const int i = threadIdx.x + j * 1024;
+    if (i < ent)
+#pragma unroll
+      for (int c = 0; c < C; ++c) out[i * C + c] = acc[j][c];
   }
 }
 
@@ -115,12 +147,11 @@ inline int max_nodes(int C) { return kLdsBytes / (kBins * C * (int)sizeof(float)
 inline int feat_group(int F, int cnt, int C) {
   return max(1, min(min(F, 4), kLdsBytes / (cnt * kBins * C * (int)sizeof(float))));
 }
-constexpr long long kMaxRows = 32768;  // per workgroup: bounds the fixed-point sums (see top)
-// ~512 workgroups of 16 waves (2 per CU, as LDS allows), >= 4096 and <= kMaxRows rows each
+// ~512 workgroups of 16 waves (2 per CU, as LDS allows), >= 4096 rows each; the partial buffer is
+// then <= 512 x 64 KB-worth of floats whatever the row count
 inline long long row_blocks(long long ld, int gx) {
   long long gy = (512 + gx - 1) / gx;
-  gy = max(1LL, min(gy, (ld + 4095) / 4096));
-  return max(gy, (ld + kMaxRows - 1) / kMaxRows);
+  return max(1LL, min(gy, (ld + 4095) / 4096));
 }
 }  // namespace plan
 
@@ -154,7 +185,6 @@ RCA_API int rca_gbdt_hist(const unsigned char* bins, const int* node, const unsi
     const long long gy = plan::row_blocks(ld, gx);
     long long rpb = (ld + gy - 1) / gy;
     rpb = (rpb + 3) & ~3LL;
-    if (rpb > plan::kMaxRows) return -2;
     const int ent = cnt * FG * kBins;
     const size_t lds = (size_t)ent * (sizeof(unsigned long long) + (C == 3 ? sizeof(unsigned) : 0));
     dim3 grid(gx, (unsigned)gy);
