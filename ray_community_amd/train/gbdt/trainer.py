@@ -179,9 +179,10 @@ class _GBDTTrainer(DataParallelTrainer):
         self.label_column = label_column
         self.params = dict(params or {})
         self.num_boost_round = num_boost_round
-        fn = partial(_gbdt_train_fn_per_worker, label_column=label_column, num_boost_round=num_boost_round,
-                     dataset_keys=set(datasets), train_kwargs=train_kwargs, flavor=self._flavor,
-                     use_gpu=bool(getattr(scaling_config, "use_gpu", False)))
+        self._fn_args = dict(label_column=label_column, num_boost_round=num_boost_round,
+                             dataset_keys=set(datasets), train_kwargs=train_kwargs, flavor=self._flavor,
+                             use_gpu=bool(getattr(scaling_config, "use_gpu", False)))
+        fn = partial(_gbdt_train_fn_per_worker, **self._fn_args)
         super().__init__(_as_one_arg(fn), train_loop_config=self.params, backend_config=TorchConfig(),
                          scaling_config=scaling_config, run_config=run_config, datasets=datasets,
                          dataset_config=dataset_config, resume_from_checkpoint=resume_from_checkpoint,
@@ -194,6 +195,25 @@ class _GBDTTrainer(DataParallelTrainer):
     @classmethod
     def get_model(cls, checkpoint: Checkpoint) -> Booster:
         return RayTrainReportCallback.get_model(checkpoint)
+
+    def _with_config(self, config):
+        """A Tune trial's config: ``{"params": {...}}`` overrides booster parameters (the reference's
+        ``Tuner(XGBoostTrainer(...), param_space={"params": {...}})``), ``num_boost_round`` too."""
+        import copy
+
+        t = copy.copy(self)
+        cfg = dict(self.train_loop_config or {})
+        if isinstance(config, dict):
+            cfg.update(config.get("params", {}) or {})
+            cfg.update(config.get("train_loop_config", {}) or {})
+        t.train_loop_config = cfg
+        t.params = cfg
+        if isinstance(config, dict) and "num_boost_round" in config:
+            t.num_boost_round = int(config["num_boost_round"])
+            fn = self._fn_args
+            t.train_loop_per_worker = _as_one_arg(partial(_gbdt_train_fn_per_worker, **dict(
+                fn, num_boost_round=t.num_boost_round)))
+        return t
 
 
 def _as_one_arg(fn):

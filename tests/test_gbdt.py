@@ -298,3 +298,28 @@ def test_gbdt_training_on_gpu_matches_cpu_quality():
     p = bg.predict(torch.as_tensor(X, device="cuda"))
     assert p.is_cuda and abs(float(torch.sqrt(torch.mean((p.cpu() - torch.as_tensor(y)) ** 2)))
                              - res_g["train"]["rmse"][-1]) < 1e-3
+
+
+def test_tuner_searches_xgboost_params(ray4, tmp_path):
+    """``Tuner(XGBoostTrainer(...), param_space={"params": {...}})`` as in the reference's GBDT
+    tuning examples: each trial trains with its own booster parameters."""
+    from ray_community_amd import data, tune
+    from ray_community_amd.train import RunConfig, ScalingConfig
+    from ray_community_amd.train.xgboost import XGBoostTrainer
+
+    X, y = _reg(1500, f=4)
+    df = pd.DataFrame(X, columns=["a", "b", "c", "d"])
+    df["y"] = y
+    trainer = XGBoostTrainer(label_column="y", params={"objective": "reg:squarederror"}, num_boost_round=6,
+                             scaling_config=ScalingConfig(num_workers=1),
+                             datasets={"train": data.from_pandas(df.iloc[:1200]),
+                                       "valid": data.from_pandas(df.iloc[1200:])})
+    grid = tune.Tuner(trainer, param_space={"params": {"max_depth": tune.grid_search([1, 5])}},
+                      tune_config=tune.TuneConfig(metric="valid-rmse", mode="min"),
+                      run_config=RunConfig(name="tune_xgb", storage_path=str(tmp_path))).fit()
+    assert len(grid) == 2 and not grid.errors
+    best = grid.get_best_result()
+    assert best.config["params"]["max_depth"] == 5
+    scores = sorted(r.metrics["valid-rmse"] for r in grid)
+    assert scores[0] < scores[1]
+    assert XGBoostTrainer.get_model(best.checkpoint).trees[0][0].depth == 5
