@@ -136,7 +136,17 @@ __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const float* __re
   float acc = 0.f;
   const float* p = part + (long long)bx * total + i;
   const long long stride = (long long)gx * total;
-  for (int y = 0; y < gy; ++y) acc += p[y * stride];
+  // 8 independent loads in flight per step (the partials are one HBM round trip each); the sum
+  // order is fixed: bitwise-reproducible histograms for a given launch geometry
+  float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int y = 0;
+  for (; y + 8 <= gy; y += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a8[u] += p[(long long)(y + u) * stride];
+  }
+  for (; y < gy; ++y) a8[0] += p[(long long)y * stride];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc += a8[u];
   const int bc = rem - f * (kBins * C);
   hist[((long long)(lo + sl) * F + f0 + f) * (kBins * C) + bc] = acc;
 }
