@@ -359,6 +359,27 @@ def transform(obj: str, margin: torch.Tensor) -> torch.Tensor:
 _EPS = 1e-15
 
 
+_AUC_BINS = 1 << 16
+
+
+def _auc(margin: torch.Tensor, y: torch.Tensor) -> float:
+    """Distributed ROC AUC from score histograms: every worker bins its predicted probabilities
+    (65536 bins) separately for positives and negatives, the histograms are all-reduced, and the
+    AUC is the probability a random positive outscores a random negative (ties within a bin count
+    1/2) -- exact up to the bin width, with no gather of the predictions."""
+    p = torch.sigmoid(margin[:, 0]).clamp(0, 1)
+    b = (p * (_AUC_BINS - 1)).round().long()
+    pos = torch.bincount(b[y > 0.5], minlength=_AUC_BINS).double()
+    neg = torch.bincount(b[y <= 0.5], minlength=_AUC_BINS).double()
+    h = allreduce_sum(torch.stack([pos, neg]).cpu())
+    pos, neg = h[0], h[1]
+    P, N = float(pos.sum()), float(neg.sum())
+    if P == 0 or N == 0:
+        return float("nan")
+    neg_below = torch.cumsum(neg, 0) - neg
+    return float((pos * (neg_below + 0.5 * neg)).sum()) / (P * N)
+
+
 def _metric_sums(name: str, obj: str, margin: torch.Tensor, y: torch.Tensor) -> Tuple[float, float]:
     """(sum of per-row loss, row count) for one metric; summed over workers by the caller."""
     n = float(y.numel())
@@ -779,6 +800,9 @@ def train(params: Dict[str, Any], dtrain: DMatrix, num_boost_round: int = 10,
         for j, (d, name, _, _) in enumerate(eval_sets):
             m = margin if d is dtrain else eval_margins[j]
             for met in p["eval_metric"]:
+                if met == "auc":
+                    evals_log.setdefault(name, {}).setdefault(met, []).append(_auc(m, d.y))
+                    continue
                 s, n = _metric_sums(met, obj, m, d.y)
                 tot = allreduce_sum(torch.tensor([s, n], dtype=torch.float64))
                 evals_log.setdefault(name, {}).setdefault(met, []).append(_metric_finish(met, float(tot[0]), float(tot[1])))

@@ -323,3 +323,18 @@ def test_tuner_searches_xgboost_params(ray4, tmp_path):
     scores = sorted(r.metrics["valid-rmse"] for r in grid)
     assert scores[0] < scores[1]
     assert XGBoostTrainer.get_model(best.checkpoint).trees[0][0].depth == 5
+
+
+def test_auc_metric_matches_sklearn_and_drives_early_stopping():
+    from sklearn.metrics import roc_auc_score
+
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(4000, 4)).astype(np.float32)
+    y = ((X[:, 0] + rng.normal(size=4000)) > 0).astype(np.float32)
+    res = {}
+    dv = DMatrix(X[3000:], y[3000:])
+    b = train({"objective": "binary:logistic", "eval_metric": ["logloss", "auc"]}, DMatrix(X[:3000], y[:3000]), 60,
+              evals=[(dv, "valid")], evals_result=res, early_stopping_rounds=5)
+    assert abs(res["valid"]["auc"][-1] - roc_auc_score(y[3000:], b.predict(X[3000:]))) < 1e-4
+    # auc is the last metric -> early stopping maximises it
+    assert b.best_score == max(res["valid"]["auc"]) and b.num_boosted_rounds() < 60
