@@ -338,3 +338,35 @@ def test_auc_metric_matches_sklearn_and_drives_early_stopping():
     assert abs(res["valid"]["auc"][-1] - roc_auc_score(y[3000:], b.predict(X[3000:]))) < 1e-4
     # auc is the last metric -> early stopping maximises it
     assert b.best_score == max(res["valid"]["auc"]) and b.num_boosted_rounds() < 60
+
+
+@pytest.mark.gpu
+def test_xgboost_trainer_on_gpu_worker(tmp_path):
+    """The trainer path end to end on a GPU worker: shard -> HBM DMatrix -> HIP histograms."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ray_community_amd as ray
+    from ray_community_amd import data
+    from ray_community_amd.train import RunConfig, ScalingConfig
+    from ray_community_amd.train.xgboost import XGBoostTrainer
+
+    ray.init(num_cpus=4, num_gpus=1, log_to_driver=False)
+    try:
+        rng = np.random.default_rng(6)
+        X = rng.normal(size=(20_000, 6))
+        df = pd.DataFrame(X, columns=[f"f{i}" for i in range(6)])
+        df["label"] = ((X[:, 0] + 0.5 * X[:, 1] ** 2) > 0.5).astype(float)
+
+        def dev_probe(batch):
+            return batch
+
+        res = XGBoostTrainer(label_column="label",
+                             params={"objective": "binary:logistic", "eval_metric": ["error", "auc"]},
+                             num_boost_round=10, scaling_config=ScalingConfig(num_workers=1, use_gpu=True),
+                             datasets={"train": data.from_pandas(df.iloc[:16000]).map_batches(dev_probe),
+                                       "valid": data.from_pandas(df.iloc[16000:])},
+                             run_config=RunConfig(name="xgb_gpu", storage_path=str(tmp_path))).fit()
+        assert res.metrics["valid-error"] < 0.1 and res.metrics["valid-auc"] > 0.95
+        assert XGBoostTrainer.get_model(res.checkpoint).num_boosted_rounds() == 10
+    finally:
+        ray.shutdown()
