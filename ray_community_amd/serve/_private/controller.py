@@ -19,6 +19,7 @@ class _DeploymentState:
         self.name = name
         self.spec = spec
         self.replicas: Dict[str, Any] = {}  # tag -> actor handle
+        self.members = 0  # bumped on every change of ``replicas`` (routers long-poll it)
         self.version = 0
         self.target = spec["num_replicas"]
         self.status = "UPDATING"
@@ -127,7 +128,40 @@ class ServeController:
         r = cls.remote(st.app, st.name, tag, spec["body"], spec["init_args"], spec["init_kwargs"],
                        spec.get("user_config"), spec["is_function"])
         st.replicas[tag] = r
+        self._bump(st)
         return tag, r
+
+    def _bump(self, st):
+        """The replica set of ``st`` changed: wake every router long-polling it."""
+        st.members += 1
+        ev = getattr(self, "_members_ev", None)
+        if ev is not None:
+            ev.set()
+        self._members_ev = asyncio.Event()
+
+    async def listen_replicas(self, app_name: str, deployment: str, known: int, timeout_s: float = 10.0):
+        """Long poll (reference: serve/_private/long_poll.py LongPollHost): returns the replica set
+        as soon as its membership counter differs from ``known``, or ``{"unchanged": True}`` after
+        ``timeout_s``; None once the deployment is gone."""
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout_s
+        while True:
+            st = self.apps.get(app_name, {}).get(deployment)
+            if st is None:
+                return None
+            if st.members != known:
+                info = await self.get_replicas(app_name, deployment)
+                info["members"] = st.members
+                return info
+            rem = deadline - loop.time()
+            if rem <= 0:
+                return {"unchanged": True, "members": known}
+            if getattr(self, "_members_ev", None) is None:
+                self._members_ev = asyncio.Event()
+            try:
+                await asyncio.wait_for(self._members_ev.wait(), rem)
+            except asyncio.TimeoutError:
+                pass
 
     async def _stop_replicas(self, st, tags):
         await asyncio.gather(*[self._stop_replica(st, t) for t in tags])
@@ -138,6 +172,7 @@ class ServeController:
         r = st.replicas.pop(t, None)
         if r is None:
             return
+        self._bump(st)
         st.health.pop(t, None)
         # graceful shutdown (reference replica.py perform_graceful_shutdown): the replica is
         # already out of the routing table; it drains its ongoing requests, polling every
@@ -182,7 +217,8 @@ class ServeController:
                     if isinstance(res, asyncio.TimeoutError) and tag not in st.health:
                         continue  # never ready yet
                     st.message = f"replica {tag} failed its health check: {type(res).__name__}: {res}"
-                    st.replicas.pop(tag, None)
+                    if st.replicas.pop(tag, None) is not None:
+                        self._bump(st)
                     st.health.pop(tag, None)
                     failed = True
                     try:
@@ -251,7 +287,8 @@ class ServeController:
         if st is None:
             return None
         return {"replicas": list(st.replicas.items()), "max_ongoing_requests": st.spec.get("max_ongoing_requests", 5),
-                "max_queued_requests": st.spec.get("max_queued_requests", -1), "version": st.version}
+                "max_queued_requests": st.spec.get("max_queued_requests", -1), "version": st.version,
+                "members": st.members}
 
     async def get_ingress(self, app_name: str):
         meta = self.app_meta.get(app_name)

@@ -81,6 +81,42 @@ class _Router:
         self.last_refresh = now
         if info is None:
             raise RuntimeError(f"Deployment {self.dep} of app {self.app} does not exist")
+        self._apply(info)
+        self._ensure_listener()
+
+    def _ensure_listener(self):
+        """One daemon thread per router long-polls the controller for replica-set changes, so
+        scale-ups, replacements and removals reach routing right away instead of at the next
+        periodic refresh (reference: the router's LongPollClient on the deployment's targets)."""
+        if getattr(self, "_listener", None) is not None and self._listener.is_alive():
+            return
+        self._listener = threading.Thread(target=self._listen_loop, name=f"serve-router-{self.dep}", daemon=True)
+        self._listener.start()
+
+    def _listen_loop(self):
+        from .._private import worker as w
+        from .api import _get_controller
+
+        known = getattr(self, "_members", -1)
+        while w.is_initialized():
+            try:
+                info = w.get(_get_controller().listen_replicas.remote(self.app, self.dep, known, 10.0),
+                             timeout=30)
+            except Exception:  # controller restarting / shutting down
+                if not w.is_initialized():
+                    return
+                time.sleep(1.0)
+                continue
+            if info is None:  # deployment deleted
+                return
+            if info.get("unchanged"):
+                continue
+            known = info.get("members", known)
+            self._apply(info)
+            self.last_refresh = time.time()
+
+    def _apply(self, info):
+        self._members = info.get("members", -1)
         with self.cv:
             self.replicas = info["replicas"]
             self.max_ongoing = info["max_ongoing_requests"]
