@@ -306,6 +306,10 @@ class TuneController:
         self.param_space = param_space or {}
         self.tc = tune_config
         self.rc = run_config
+        from .logger import default_logger_callbacks
+
+        # user callbacks + the default CSV / JSON result loggers (progress.csv, params.json)
+        self.callbacks = list(run_config.callbacks or []) + default_logger_callbacks(run_config.callbacks)
         self.exp_dir = exp_dir
         os.makedirs(exp_dir, exist_ok=True)
         self.scheduler = tune_config.scheduler or FIFOScheduler()
@@ -401,6 +405,10 @@ class TuneController:
 
         trial.status = RUNNING
         trial.start_time = time.time()
+        os.makedirs(trial.local_path, exist_ok=True)
+        for cb in self.callbacks:
+            if hasattr(cb, "on_trial_start"):
+                cb.on_trial_start(iteration=0, trials=self.trials, trial=trial)
         trial.stop_flag = False
         ckpt = trial.checkpoint if trial.restore_path is None else _ckpt(trial.restore_path)
         trial.restore_path = None
@@ -591,7 +599,7 @@ class TuneController:
         with open(os.path.join(trial.local_path, "result.json"), "a") as f:
             f.write(json.dumps(_jsonable(m)) + "\n")
         self.searcher.on_trial_result(trial.trial_id, m)
-        for cb in (self.rc.callbacks or []):
+        for cb in self.callbacks:
             if hasattr(cb, "on_trial_result"):
                 cb.on_trial_result(iteration=0, trials=self.trials, trial=trial, result=m)
         if self._should_stop(trial, m):
@@ -617,7 +625,7 @@ class TuneController:
             trial.status = TERMINATED
             self.scheduler.on_trial_complete(self, trial, trial.last_result)
             self.searcher.on_trial_complete(trial.trial_id, trial.last_result)
-        for cb in (self.rc.callbacks or []):
+        for cb in self.callbacks:
             if hasattr(cb, "on_trial_complete"):
                 cb.on_trial_complete(iteration=0, trials=self.trials, trial=trial)
 
