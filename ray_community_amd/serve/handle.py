@@ -98,7 +98,8 @@ class _Router:
         from .api import _get_controller
 
         known = getattr(self, "_members", -1)
-        while w.is_initialized():
+        # exits with the session, with the deployment, or when serve.shutdown() dropped this router
+        while w.is_initialized() and _Router._routers.get((self.app, self.dep)) is self:
             try:
                 info = w.get(_get_controller().listen_replicas.remote(self.app, self.dep, known, 10.0),
                              timeout=30)
