@@ -156,14 +156,44 @@ def _gbdt_train_fn_per_worker(config: dict, label_column: str, num_boost_round: 
           flavor=flavor, **kw)
 
 
+class GBDTConfig(TorchConfig):
+    """Backend of the GBDT trainers: the workers' collective group for histogram all-reduces
+    (RCCL on GPU workers, gloo on CPU). Stands in for the reference's ``XGBoostConfig``
+    (``xgboost_communicator="rabit"``) / lightgbm network setup; ``"rabit"`` is accepted as an
+    alias of the default."""
+
+    def __init__(self, xgboost_communicator: str = "rabit", backend=None, timeout_s: int = 1800):
+        if xgboost_communicator not in ("rabit", "rccl", "nccl", "gloo"):
+            raise NotImplementedError(f"Unsupported backend: {xgboost_communicator}")
+        super().__init__()
+        self.xgboost_communicator = xgboost_communicator
+        self.backend = backend or ({"rccl": "nccl", "nccl": "nccl", "gloo": "gloo"}.get(xgboost_communicator))
+        self.timeout_s = timeout_s
+
+
 class _GBDTTrainer(DataParallelTrainer):
     _flavor = "xgboost"
 
-    def __init__(self, *, datasets: Dict[str, Any], label_column: str, params: Dict[str, Any],
+    def __init__(self, train_loop_per_worker=None, *, datasets: Optional[Dict[str, Any]] = None,
+                 label_column: Optional[str] = None, params: Optional[Dict[str, Any]] = None,
                  num_boost_round: int = 10, scaling_config=None, run_config=None, dataset_config=None,
-                 resume_from_checkpoint=None, metadata=None, **train_kwargs):
+                 resume_from_checkpoint=None, metadata=None, train_loop_config=None, xgboost_config=None,
+                 lightgbm_config=None, **train_kwargs):
         from ...air.config import RunConfig, ScalingConfig
 
+        if train_loop_per_worker is not None:
+            # the reference's v2 form: the user's loop calls ``train(...)`` with a report callback
+            self._v2 = True
+            self.label_column, self.params, self.num_boost_round = label_column, dict(params or {}), num_boost_round
+            DataParallelTrainer.__init__(self, train_loop_per_worker, train_loop_config=train_loop_config,
+                                         backend_config=xgboost_config or lightgbm_config or GBDTConfig(),
+                                         scaling_config=scaling_config, run_config=run_config, datasets=datasets,
+                                         dataset_config=dataset_config, resume_from_checkpoint=resume_from_checkpoint,
+                                         metadata=metadata)
+            return
+        self._v2 = False
+        if label_column is None:
+            raise TypeError("label_column is required (or pass a train_loop_per_worker)")
         if TRAIN_DATASET_KEY not in (datasets or {}):
             raise KeyError(f"'{TRAIN_DATASET_KEY}' key must be preset in `datasets`. Got {list((datasets or {}))}")
         run_config = run_config or RunConfig()
@@ -197,6 +227,11 @@ class _GBDTTrainer(DataParallelTrainer):
         return RayTrainReportCallback.get_model(checkpoint)
 
     def _with_config(self, config):
+        if getattr(self, "_v2", False):
+            return DataParallelTrainer._with_config(self, config)
+        return self._with_params(config)
+
+    def _with_params(self, config):
         """A Tune trial's config: ``{"params": {...}}`` overrides booster parameters (the reference's
         ``Tuner(XGBoostTrainer(...), param_space={"params": {...}})``), ``num_boost_round`` too."""
         import copy

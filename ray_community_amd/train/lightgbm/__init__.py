@@ -10,7 +10,7 @@ with ``num_leaves`` 31, ``learning_rate`` 0.1, ``min_data_in_leaf`` 20,
 """
 from ..gbdt.core import Booster, DMatrix
 from ..gbdt.core import train as _train
-from ..gbdt.trainer import GBDTCheckpoint, GBDTPredictor, _GBDTTrainer
+from ..gbdt.trainer import GBDTCheckpoint, GBDTConfig, GBDTPredictor, _GBDTTrainer
 from ..gbdt.trainer import RayTrainReportCallback as _Report
 
 
@@ -33,6 +33,10 @@ class LightGBMCheckpoint(GBDTCheckpoint):
     pass
 
 
+class LightGBMConfig(GBDTConfig):
+    """Worker-group backend for ``LightGBMTrainer(train_loop_per_worker, ...)``."""
+
+
 class LightGBMPredictor(GBDTPredictor):
     pass
 
@@ -47,5 +51,5 @@ class LightGBMTrainer(_GBDTTrainer):
         return RayTrainReportCallback
 
 
-__all__ = ["LightGBMTrainer", "RayTrainReportCallback", "LightGBMCheckpoint", "LightGBMPredictor", "Booster",
+__all__ = ["LightGBMTrainer", "RayTrainReportCallback", "LightGBMCheckpoint", "LightGBMConfig", "LightGBMPredictor", "Booster",
            "Dataset", "train"]

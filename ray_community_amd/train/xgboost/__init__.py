@@ -9,7 +9,7 @@ depthwise growth) and accepts xgboost's parameter names and defaults (``eta`` 0.
 mae, logloss, error, mlogloss, merror). Models are this framework's JSON format, not xgboost's.
 """
 from ..gbdt.core import Booster, DMatrix, train
-from ..gbdt.trainer import GBDTCheckpoint, GBDTPredictor, _GBDTTrainer
+from ..gbdt.trainer import GBDTCheckpoint, GBDTConfig, GBDTPredictor, _GBDTTrainer
 from ..gbdt.trainer import RayTrainReportCallback as _Report
 
 
@@ -21,6 +21,10 @@ class XGBoostCheckpoint(GBDTCheckpoint):
     pass
 
 
+class XGBoostConfig(GBDTConfig):
+    """Worker-group backend for the v2 form ``XGBoostTrainer(train_loop_per_worker, ...)``."""
+
+
 class XGBoostPredictor(GBDTPredictor):
     pass
 
@@ -28,7 +32,9 @@ class XGBoostPredictor(GBDTPredictor):
 class XGBoostTrainer(_GBDTTrainer):
     """Data-parallel boosting over the ``"train"`` dataset's shards; every other dataset is an eval
     set reported as ``{name}-{metric}``. ``num_boost_round`` is the TARGET number of trees (a
-    resumed model trains only the remaining rounds)."""
+    resumed model trains only the remaining rounds). The reference's v2 form also works: pass a
+    ``train_loop_per_worker`` (it calls ``ray.train.xgboost.train(..., callbacks=[
+    RayTrainReportCallback()])`` on its ``get_dataset_shard`` data) plus ``xgboost_config``."""
 
     _flavor = "xgboost"
 
@@ -37,5 +43,5 @@ class XGBoostTrainer(_GBDTTrainer):
         return RayTrainReportCallback
 
 
-__all__ = ["XGBoostTrainer", "RayTrainReportCallback", "XGBoostCheckpoint", "XGBoostPredictor", "Booster",
+__all__ = ["XGBoostTrainer", "RayTrainReportCallback", "XGBoostCheckpoint", "XGBoostConfig", "XGBoostPredictor", "Booster",
            "DMatrix", "train"]

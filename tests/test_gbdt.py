@@ -370,3 +370,29 @@ def test_xgboost_trainer_on_gpu_worker(tmp_path):
         assert XGBoostTrainer.get_model(res.checkpoint).num_boosted_rounds() == 10
     finally:
         ray.shutdown()
+
+
+def test_xgboost_trainer_v2_form_with_user_loop(ray4, tmp_path):
+    """Reference v2 form: ``XGBoostTrainer(train_loop_per_worker, xgboost_config=...)``, the loop
+    trains on its shard with ``train(...)`` and ``RayTrainReportCallback``."""
+    from ray_community_amd import data, train as rtrain
+    from ray_community_amd.train import RunConfig, ScalingConfig
+    from ray_community_amd.train.xgboost import RayTrainReportCallback, XGBoostConfig, XGBoostTrainer
+    from ray_community_amd.train.xgboost import train as xtrain
+
+    X, y = _reg(1600, f=4)
+    df = pd.DataFrame(X, columns=["a", "b", "c", "d"])
+    df["y"] = y
+
+    def loop(config):
+        shard = rtrain.get_dataset_shard("train").materialize().to_pandas()
+        d = DMatrix(shard.drop(columns=["y"]), label=shard["y"])
+        xtrain(config, d, num_boost_round=config["rounds"], evals=[(d, "train")],
+               callbacks=[RayTrainReportCallback(metrics={"loss": "train-rmse"}, frequency=2)])
+
+    res = XGBoostTrainer(loop, train_loop_config={"max_depth": 3, "rounds": 4},
+                         xgboost_config=XGBoostConfig(), scaling_config=ScalingConfig(num_workers=2),
+                         datasets={"train": data.from_pandas(df)},
+                         run_config=RunConfig(name="v2", storage_path=str(tmp_path))).fit()
+    assert set(res.metrics) >= {"loss"} and res.metrics["loss"] < np.std(y)
+    assert RayTrainReportCallback.get_model(res.checkpoint).num_boosted_rounds() == 4
