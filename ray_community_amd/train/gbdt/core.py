@@ -32,8 +32,7 @@ from __future__ import annotations
 
 import json
 import math
-import os
-from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch

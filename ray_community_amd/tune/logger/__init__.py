@@ -15,7 +15,7 @@ from __future__ import annotations
 import csv
 import json
 import os
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List
 
 from .. import Callback
 

@@ -9,4 +9,4 @@ tail -3 gpurun_out/r3v_tests.log
 timeout -k 10 300 python -u scripts/gbdt_bench.py > gpurun_out/r3v_bench.log 2>&1 || { tail -30 gpurun_out/r3v_bench.log; exit 1; }
 cat gpurun_out/r3v_bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3v_prof -o gb -- python -u scripts/gbdt_bench.py --rounds 10 > gpurun_out/r3v_prof.log 2>&1 || { tail -30 gpurun_out/r3v_prof.log; exit 1; }
-find gpurun_out/r3v_prof -name "*kernel_stats.csv" | head -3
+f=$(find gpurun_out/r3v_prof -name "*.db" | head -1); python scripts/rocpd_summary.py "$f" 12 > gpurun_out/r3v_prof_summary.md; cat gpurun_out/r3v_prof_summary.md; find gpurun_out/r3v_prof -name "*.db" -delete
