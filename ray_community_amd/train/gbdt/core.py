@@ -597,7 +597,8 @@ class _Grower:
                 CR = Ct[:, None, None] - CL
                 ok &= (CL >= max(self.mdl, 1)) & (CR >= max(self.mdl, 1))
             g = self._score(GL, HL) + self._score(GR, HR) - parent
-            g = torch.where(ok & fmask[None, :, None], g, torch.full_like(g, -math.inf))
+            fm = fmask[None, :, None] if fmask.dim() == 1 else fmask[:, :, None]
+            g = torch.where(ok & fm, g, torch.full_like(g, -math.inf))
             gains.append(g)
             extra.append((GL, HL))
         both = torch.stack(gains, -1)  # [S, F, 255, 2]
@@ -614,6 +615,21 @@ class _Grower:
         packed = torch.stack([best, f.double(), tb.double(), (d == 0).double(), Gt, Ht, GLs, HLs]).cpu()
         b_, f_, tb_, dl_, Gt_, Ht_, GL_, HL_ = packed.unbind(0)
         return (b_, f_.long(), tb_.long(), dl_.bool(), Gt_, Ht_, GL_, HL_)
+
+    def _node_masks(self, nodes: List[int], tree_mask: torch.Tensor) -> torch.Tensor:
+        """xgboost's nested column sampling: ``colsample_bylevel`` draws from the tree's columns
+        once per depth, ``colsample_bynode`` from the level's columns at every split."""
+        byl = float(self.p.get("colsample_bylevel", 1.0) or 1.0)
+        byn = float(self.p.get("colsample_bynode", 1.0) or 1.0)
+        if byl >= 1.0 and byn >= 1.0:
+            return tree_mask
+        seed, F = int(self.p["seed"]), tree_mask.numel()
+        out = []
+        for i in nodes:
+            d = self._depth_of[i]
+            lvl = _feature_mask(F, byl, self._round * 4099 + 7 * d + 1, seed + 17, tree_mask.device, tree_mask)
+            out.append(_feature_mask(F, byn, self._round * 4099 * 131 + 2 * i + 3, seed + 29, tree_mask.device, lvl))
+        return torch.stack(out)
 
     def grow(self, g: torch.Tensor, h: torch.Tensor, row_mask: Optional[torch.Tensor], fmask: torch.Tensor,
              cuts: List[torch.Tensor]) -> Tree:
@@ -632,6 +648,8 @@ class _Grower:
         max_leaves = int(self.p["max_leaves"]) if lossguide else 0
         max_depth = self.max_depth if self.max_depth > 0 else (10 ** 6)
         depth_of = {0: 0}
+        self._depth_of = depth_of
+        self._round = getattr(self, "_round_no", 0)
         slots = torch.full((1,), 0, dtype=torch.long, device=dev)
         root_h = self.hist(pos, gh, slots, 1)
         hists = {0: root_h[0]}
@@ -641,7 +659,7 @@ class _Grower:
             if not nodes:
                 return
             Hs = torch.stack([hists[i] for i in nodes])
-            res = self.best_splits(Hs, fmask)
+            res = self.best_splits(Hs, self._node_masks(nodes, fmask))
             for j, i in enumerate(nodes):
                 gain, f, tb, dl, Gt, Ht, GL, HL = (r[j] for r in res)
                 tree.cover[i] = float(Ht)
@@ -716,13 +734,17 @@ class _Grower:
         return tree
 
 
-def _feature_mask(F: int, frac: float, rnd: int, seed: int, device) -> torch.Tensor:
+def _feature_mask(F: int, frac: float, rnd: int, seed: int, device, parent: Optional[torch.Tensor] = None
+                  ) -> torch.Tensor:
+    """``frac`` of the features (of ``parent``'s when given), seeded identically on every worker."""
+    base = torch.ones(F, dtype=torch.bool) if parent is None else parent.cpu()
     if frac >= 1.0:
-        return torch.ones(F, dtype=torch.bool, device=device)
+        return base.to(device)
     g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + rnd)  # same on every worker
-    k = max(1, int(round(frac * F)))
+    idx = base.nonzero().squeeze(1)
+    k = max(1, int(round(frac * idx.numel())))
     m = torch.zeros(F, dtype=torch.bool)
-    m[torch.randperm(F, generator=g)[:k]] = True
+    m[idx[torch.randperm(idx.numel(), generator=g)[:k]]] = True
     return m.to(device)
 
 
@@ -777,13 +799,21 @@ def train(params: Dict[str, Any], dtrain: DMatrix, num_boost_round: int = 10,
     gen = torch.Generator(device="cpu").manual_seed(int(p["seed"]) * 7 + 13 + 7919 * (dist.get_rank() if _world() > 1 else 0))
     start = bst.num_boosted_rounds()
     best = (math.inf, -1)
+    row_mask_keep = None
     for it in range(start, start + num_boost_round):
         if any(cb.before_iteration(bst, it, evals_log) for cb in cbs):
             break
         g, h = _grad_hess(obj, margin, dtrain.y, dtrain.w)
         sub = float(p["subsample"])
-        row_mask = (torch.rand(N, generator=gen) < sub).to(dev) if sub < 1.0 else None
+        freq = int(p.get("bagging_freq", p.get("subsample_freq", 0)) or 0)
+        if p["_flavor"] == "lightgbm":  # lightgbm bags only with bagging_freq > 0, re-drawn every freq rounds
+            if sub < 1.0 and freq > 0 and (it % freq == 0 or row_mask_keep is None):
+                row_mask_keep = (torch.rand(N, generator=gen) < sub).to(dev)
+            row_mask = row_mask_keep if sub < 1.0 and freq > 0 else None
+        else:
+            row_mask = (torch.rand(N, generator=gen) < sub).to(dev) if sub < 1.0 else None
         fmask = _feature_mask(F, float(p["colsample_bytree"]), it, int(p["seed"]), dev)
+        grower._round_no = it
         rnd = []
         for k in range(K):
             t = grower.grow(g[:, k].contiguous(), h[:, k].contiguous(), row_mask, fmask, cuts)

@@ -396,3 +396,24 @@ def test_xgboost_trainer_v2_form_with_user_loop(ray4, tmp_path):
                          run_config=RunConfig(name="v2", storage_path=str(tmp_path))).fit()
     assert set(res.metrics) >= {"loss"} and res.metrics["loss"] < np.std(y)
     assert RayTrainReportCallback.get_model(res.checkpoint).num_boosted_rounds() == 4
+
+
+def test_column_sampling_levels_and_lightgbm_bagging_freq():
+    X, y = _reg(1500, f=6)
+    # colsample_bynode: every split draws its own columns -> the strong feature 0 cannot win every split
+    b = train({"max_depth": 3, "colsample_bynode": 0.34, "seed": 3}, DMatrix(X, y), 6)
+    full = train({"max_depth": 3}, DMatrix(X, y), 6)
+    roots_full = {r[0].feature[0] for r in full.trees}
+    roots = {r[0].feature[0] for r in b.trees}
+    assert roots_full == {0} and len(roots) > 1
+    again = train({"max_depth": 3, "colsample_bynode": 0.34, "seed": 3}, DMatrix(X, y), 6)
+    assert again.to_dict()["trees"] == b.to_dict()["trees"]  # seeded, reproducible
+    lv = train({"max_depth": 3, "colsample_bylevel": 0.5, "seed": 1}, DMatrix(X, y), 4)
+    assert lv.num_boosted_rounds() == 4
+    # lightgbm: bagging_fraction alone does nothing (bagging_freq defaults to 0)
+    a = train({"objective": "regression", "bagging_fraction": 0.5}, DMatrix(X, y), 3, flavor="lightgbm")
+    c = train({"objective": "regression"}, DMatrix(X, y), 3, flavor="lightgbm")
+    assert a.to_dict()["trees"] == c.to_dict()["trees"]
+    d = train({"objective": "regression", "bagging_fraction": 0.5, "bagging_freq": 1}, DMatrix(X, y), 3,
+              flavor="lightgbm")
+    assert d.to_dict()["trees"] != c.to_dict()["trees"]
