@@ -124,3 +124,25 @@ def test_parse_address():
 
     assert parse_address("ray://10.0.0.1:12345") == ("10.0.0.1", 12345)
     assert parse_address("ray://headnode") == ("headnode", 10001)
+
+
+def test_util_client_connect_and_disconnect(client_head):
+    """ray.util.client_connect.connect / disconnect (reference util/client_connect.py)."""
+    from ray_community_amd.util.client_connect import connect, disconnect
+
+    info = connect(client_head[len("ray://"):], namespace="cc")
+    try:
+        assert info["address"] == client_head
+
+        @ray.remote
+        def f(x):
+            return x + 1
+
+        assert ray.get(f.remote(1)) == 2
+        with pytest.raises(RuntimeError):
+            connect(client_head)
+        assert connect(client_head, ray_init_kwargs={"ignore_reinit_error": True})["reused"]
+    finally:
+        disconnect()
+    assert not ray.is_initialized()
+    disconnect()  # idempotent
