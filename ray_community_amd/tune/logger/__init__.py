@@ -7,8 +7,8 @@ reported result, flattened ``a/b`` keys, header fixed by the first result as in 
 ``result.json`` (one JSON line per result; the experiment controller writes it for every trial since
 ``Result.from_path`` / ``Tuner.restore`` read it). The CSV and JSON callbacks are added by default
 unless ``TUNE_DISABLE_AUTO_CALLBACK_LOGGERS=1`` or the run config already holds one of that class;
-``TBXLoggerCallback`` writes TensorBoard scalars through ``torch.utils.tensorboard`` when that
-import works (the tensorboard package is optional) and otherwise raises at construction.
+``TBXLoggerCallback`` writes TensorBoard scalars as tfevents files with a built-in protobuf /
+TFRecord encoder (tensorboard itself is not installed here).
 """
 from __future__ import annotations
 
@@ -172,26 +172,86 @@ class CSVLoggerCallback(LoggerCallback):
             ent[0].close()
 
 
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    n &= (1 << 64) - 1
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _field(num: int, wire: int, payload: bytes) -> bytes:
+    return _varint((num << 3) | wire) + payload
+
+
+def _scalar_event(wall_time: float, step: int, tag: str, value: float) -> bytes:
+    """tensorboard ``Event{wall_time, step, summary{value{tag, simple_value}}}`` in protobuf wire
+    format (event.proto / summary.proto field numbers), encoded by hand: no tensorboard needed."""
+    import struct
+
+    t = tag.encode()
+    val = _field(1, 2, _varint(len(t)) + t) + _field(2, 5, struct.pack("<f", float(value)))
+    summ = _field(1, 2, _varint(len(val)) + val)
+    return (_field(1, 1, struct.pack("<d", wall_time)) + _field(2, 0, _varint(int(step)))
+            + _field(5, 2, _varint(len(summ)) + summ))
+
+
+class _EventFile:
+    """Append-only ``events.out.tfevents.*`` writer: TFRecord framing (length, masked CRC32C of the
+    length, payload, masked CRC32C of the payload) around Event protos."""
+
+    def __init__(self, logdir: str):
+        import socket
+        import struct
+        import time
+
+        os.makedirs(logdir, exist_ok=True)
+        self.path = os.path.join(logdir, f"events.out.tfevents.{int(time.time())}.{socket.gethostname()}")
+        self._f = open(self.path, "ab")
+        ver = b"brain.Event:2"
+        self._write(_field(1, 1, struct.pack("<d", time.time())) + _field(3, 2, _varint(len(ver)) + ver))
+
+    def _write(self, payload: bytes):
+        import struct
+
+        from ...data.datasource import _masked_crc
+
+        hdr = struct.pack("<Q", len(payload))
+        self._f.write(hdr + struct.pack("<I", _masked_crc(hdr)) + payload + struct.pack("<I", _masked_crc(payload)))
+
+    def add_scalar(self, tag: str, value: float, step: int):
+        import time
+
+        self._write(_scalar_event(time.time(), step, tag, value))
+
+    def flush(self):
+        self._f.flush()
+
+    def close(self):
+        self._f.close()
+
+
 class TBXLoggerCallback(LoggerCallback):
-    """TensorBoard scalars of every numeric result key, step = ``training_iteration``."""
+    """TensorBoard scalars (``ray/tune/<key>``) of every numeric result key, step =
+    ``training_iteration``, written as tfevents files in each trial directory by a built-in
+    encoder (the tensorboard / tensorboardX packages are not needed)."""
 
     def __init__(self):
-        try:
-            from torch.utils.tensorboard import SummaryWriter  # noqa: F401
-        except Exception as e:  # tensorboard is not installed on this platform
-            raise ImportError("TBXLoggerCallback needs torch.utils.tensorboard (the tensorboard package)") from e
-        self._writers: Dict[str, Any] = {}
+        self._writers: Dict[str, _EventFile] = {}
 
     def log_trial_result(self, iteration, trial, result):
-        from torch.utils.tensorboard import SummaryWriter
-
         w = self._writers.get(trial.trial_id)
         if w is None:
-            w = self._writers[trial.trial_id] = SummaryWriter(trial.local_path)
+            w = self._writers[trial.trial_id] = _EventFile(trial.local_path)
         step = int(result.get("training_iteration", iteration))
         for k, v in _flatten(result).items():
             if isinstance(v, (int, float)) and not isinstance(v, bool) and not k.startswith("config/"):
-                w.add_scalar(f"ray/tune/{k}", v, global_step=step)
+                w.add_scalar(f"ray/tune/{k}", v, step)
         w.flush()
 
     def log_trial_end(self, trial, failed=False):

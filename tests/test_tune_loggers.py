@@ -74,3 +74,66 @@ def test_explicit_default_loggers_are_not_duplicated(ray4, tmp_path):
     d = next(iter(grid)).path
     rows = list(csv.DictReader(open(os.path.join(d, "progress.csv"))))
     assert len(rows) == 3  # one writer, not two
+
+
+def _read_tfevents(path):
+    """Minimal tfevents reader: TFRecord frames -> (step, tag, value) of scalar Events."""
+    import struct
+
+    from ray_community_amd.data.datasource import _masked_crc
+
+    def varint(b, i):
+        n = s = 0
+        while True:
+            c = b[i]
+            i += 1
+            n |= (c & 0x7F) << s
+            s += 7
+            if c < 0x80:
+                return n, i
+
+    def fields(b):
+        i, out = 0, []
+        while i < len(b):
+            key, i = varint(b, i)
+            num, wire = key >> 3, key & 7
+            if wire == 0:
+                v, i = varint(b, i)
+            elif wire == 1:
+                v, i = b[i:i + 8], i + 8
+            elif wire == 5:
+                v, i = b[i:i + 4], i + 4
+            else:
+                n, i = varint(b, i)
+                v, i = b[i:i + n], i + n
+            out.append((num, v))
+        return out
+
+    out, data = [], open(path, "rb").read()
+    i = 0
+    while i < len(data):
+        (n,) = struct.unpack("<Q", data[i:i + 8])
+        assert struct.unpack("<I", data[i + 8:i + 12])[0] == _masked_crc(data[i:i + 8])
+        payload = data[i + 12:i + 12 + n]
+        assert struct.unpack("<I", data[i + 12 + n:i + 16 + n])[0] == _masked_crc(payload)
+        i += 16 + n
+        ev = dict(fields(payload))
+        if 5 in ev:
+            val = dict(fields(dict(fields(ev[5]))[1]))
+            out.append((ev.get(2, 0), val[1].decode(), struct.unpack("<f", val[2])[0]))
+    return out
+
+
+def test_tbx_logger_writes_tfevents_scalars(ray4, tmp_path):
+    from ray_community_amd.tune.logger import TBXLoggerCallback
+
+    grid = tune.Tuner(_train, param_space={"x": 2},
+                      run_config=RunConfig(name="tb", storage_path=str(tmp_path),
+                                           callbacks=[TBXLoggerCallback()])).fit()
+    d = next(iter(grid)).path
+    files = [f for f in os.listdir(d) if f.startswith("events.out.tfevents.")]
+    assert len(files) == 1
+    ev = _read_tfevents(os.path.join(d, files[0]))
+    score = [(s, v) for s, t, v in ev if t == "ray/tune/score"]
+    assert score == [(1, 2.0), (2, 4.0), (3, 6.0)]
+    assert any(t == "ray/tune/nested/a" for _, t, _ in ev)
