@@ -369,7 +369,6 @@ class FlatSGD:
         return {"step": self.step_count, "buf": self.buf, "lr": self.lr, "momentum": self.momentum, "wd": self.wd}
 
     def load_state_dict(self, sd):
-        self._wt_epoch[0] += 1
         self.step_count = sd["step"]
         if self.buf is not None and sd.get("buf") is not None:
             self.buf.copy_(sd["buf"])

@@ -148,6 +148,40 @@ def test_flat_sgd_matches_torch_sgd():
         assert torch.allclose(pa, pb, atol=1e-5, rtol=1e-4), n
 
 
+def test_flat_sgd_state_dict_roundtrip():
+    """Resume: a fresh FlatSGD restored from a state_dict continues exactly like the original."""
+    import copy
+
+    import torch.nn.functional as F
+
+    from ray_community_amd.models.resnet import ResNet
+    from ray_community_amd.parallel import DistributedDataParallel, FlatSGD
+
+    torch.manual_seed(0)
+    a = ResNet((1, 1, 1, 1), num_classes=5)
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 3, 32, 32)
+    y = torch.randint(0, 5, (4,))
+    da = DistributedDataParallel(a)
+    oa = FlatSGD(da.flat, lr=0.05, momentum=0.9, nesterov=True)
+    for _ in range(2):
+        F.cross_entropy(da(x), y).backward()
+        oa.step(da.grad_scale)
+        oa.zero_grad()
+    sd = copy.deepcopy(oa.state_dict())
+    b.load_state_dict(a.state_dict())
+    db = DistributedDataParallel(b)
+    ob = FlatSGD(db.flat, lr=0.05, momentum=0.9, nesterov=True)
+    ob.load_state_dict(sd)
+    assert ob.step_count == 2 and torch.equal(ob.buf, oa.buf)
+    for d, o in ((da, oa), (db, ob)):
+        F.cross_entropy(d(x), y).backward()
+        o.step(d.grad_scale)
+        o.zero_grad()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(pa, pb), n
+
+
 def test_split_master_roundtrip_is_exact():
     """fp32 master <-> (bf16 high half, low 16 bits): bit-exact, including exact rounding ties,
     negatives, zeros and subnormals; the high half is the RNE bf16 except at ties (<= 1 ulp)."""
