@@ -164,6 +164,18 @@ class ObjectRefGenerator:
     def is_finished(self):
         return self._done
 
+    def __del__(self):
+        # dropped before the end of the stream: a producer paused on backpressure would otherwise
+        # hold its worker forever (reference: DelObjectRefStream)
+        if self._done:
+            return
+        try:
+            core = global_core()
+            if core is not None and not core._shutdown:
+                core.client.call_async("gen_drop", self._tid)
+        except Exception:
+            pass
+
 
 class DynamicObjectRefGenerator:
     """Return value of a ``num_returns="dynamic"`` task: an iterable of ObjectRefs."""

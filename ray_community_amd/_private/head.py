@@ -98,7 +98,7 @@ class ObjEntry:
 class TaskState:
     __slots__ = ("tid", "spec", "state", "deps", "retries_left", "worker", "node", "demand", "owner", "key", "gpus",
                  "times", "children", "parent", "cancelled", "blocked", "gen_items", "gen_done", "gen_waiters",
-                 "gen_consumed", "gen_bp_waiters",
+                 "gen_consumed", "gen_bp_waiters", "gen_dropped",
                  "error_type", "attempt", "reply")
 
     def __init__(self, tid, spec, owner):
@@ -121,6 +121,7 @@ class TaskState:
         self.gen_items: List[bytes] = []
         self.gen_consumed = 0          # items handed to the consumer (streaming backpressure)
         self.gen_bp_waiters: List = []  # (needed count, Deferred) of a paused producer
+        self.gen_dropped = False  # the consumer dropped its ObjectRefGenerator (or its owner died)
         self.gen_done = False
         self.gen_waiters: Dict[int, List[Deferred]] = {}
         self.error_type = None
@@ -447,6 +448,7 @@ class Head:
                 if getattr(cc, "log_sink", None) is not None:
                     self.log_monitor.remove_sink(cc.log_sink)
                 self._return_leases_of(cc.client_key)
+                self._drop_streams_of(cc.client_key)
                 self._drop_holder_everywhere(cc.client_key)
                 self._schedule()
 
@@ -1499,6 +1501,7 @@ class Head:
         if spec.get("generator") == "streaming":
             ts.gen_done = True
             self._flush_gen_waiters(ts)
+            self._release_gen_producer(ts, self.GEN_STOP_DROPPED)
         self._finish_task_bookkeeping(ts)
         if kind == "actor_creation":
             a = self.actors.get(spec["actor_id"])
@@ -1563,6 +1566,7 @@ class Head:
         if ts.spec.get("generator") == "streaming":
             ts.gen_done = True
             self._flush_gen_waiters(ts)
+            self._release_gen_producer(ts, self.GEN_STOP_DROPPED)
         self._event(ts, "failed")
         self._finish_task_bookkeeping(ts)
 
@@ -1610,6 +1614,7 @@ class Head:
             if lst and w in lst:
                 lst.remove(w)
         self.workers.pop(w.wid, None)
+        self._drop_streams_of("w:" + w.wid.hex())
         # GPU objects owned by the worker are lost
         for oid in list(w.gpu_objects):
             e = self.objects.get(oid)
@@ -1687,16 +1692,49 @@ class Head:
                         keep.append((need, d))
                 ts.gen_bp_waiters = keep
 
+    # what a paused producer is told when it must stop instead of producing more
+    GEN_STOP_DROPPED, GEN_STOP_CANCELLED = -1, -2
+
     def rpc_gen_wait_consumed(self, caller, tid, need):
         """``_generator_backpressure_num_objects``: the producer blocks until the consumer has
-        taken ``need`` items (reference: ``src/ray/core_worker/generator_waiter.h``)."""
+        taken ``need`` items (reference: ``src/ray/core_worker/generator_waiter.h``). Answers a
+        negative code instead when the stream is gone: the task was cancelled, or its consumer
+        dropped the generator / died (reference: ``HandleDelObjectRefStream`` releasing the waiter)."""
         ts = self.tasks.get(tid)
         d = Deferred()
-        if ts is None or ts.gen_consumed >= need or ts.cancelled:
-            d.resolve(ts.gen_consumed if ts is not None else need)
+        if ts is None:
+            d.resolve(self.GEN_STOP_DROPPED)
+        elif ts.cancelled:
+            d.resolve(self.GEN_STOP_CANCELLED)
+        elif ts.gen_dropped:
+            d.resolve(self.GEN_STOP_DROPPED)
+        elif ts.gen_consumed >= need:
+            d.resolve(ts.gen_consumed)
         else:
             ts.gen_bp_waiters.append((need, d))
         return d
+
+    def _release_gen_producer(self, ts, code):
+        """Wake a producer paused on backpressure with a stop ``code``: nothing will ever consume
+        what it is waiting to produce, and a blocked producer would hold its worker forever."""
+        waiters, ts.gen_bp_waiters = ts.gen_bp_waiters, []
+        for _need, d in waiters:
+            d.resolve(code)
+
+    def rpc_gen_drop(self, caller, tid):
+        """The consumer's ObjectRefGenerator was garbage-collected before the stream ended."""
+        ts = self.tasks.get(tid)
+        if ts is not None and not ts.gen_done:
+            ts.gen_dropped = True
+            self._release_gen_producer(ts, self.GEN_STOP_DROPPED)
+        return True
+
+    def _drop_streams_of(self, owner_key):
+        """An owner process is gone: release the paused producers of the streams it consumed."""
+        for ts in list(self.tasks.values()):
+            if ts.gen_bp_waiters and ts.owner == owner_key and not ts.gen_done:
+                ts.gen_dropped = True
+                self._release_gen_producer(ts, self.GEN_STOP_DROPPED)
 
     def _flush_gen_waiters(self, ts):
         for idx in list(ts.gen_waiters):
@@ -2146,6 +2184,8 @@ class Head:
         if ts.state in (T_FINISHED, T_FAILED, T_CANCELLED):
             return
         ts.cancelled = True
+        if ts.gen_bp_waiters:
+            self._release_gen_producer(ts, self.GEN_STOP_CANCELLED)
         if recursive:
             for c in ts.children:
                 cts = self.tasks.get(c)

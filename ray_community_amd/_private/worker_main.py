@@ -434,6 +434,11 @@ class Worker:
                     if bp and n - consumed >= bp:
                         # backpressure: do not run ahead of the consumer by more than bp items
                         consumed = self.client.call("gen_wait_consumed", spec["tid"], n - bp + 1)
+                        if consumed < 0:  # the stream is gone: stop producing
+                            _close_gen(it)
+                            if consumed == -2:
+                                raise exc.TaskCancelledError(spec["tid"].hex())
+                            break
             return [self._pack_one(rids[0], n)] if rids else []
         if gen == "dynamic":
             refs = []
@@ -538,6 +543,11 @@ class Worker:
                             if bp and n - consumed >= bp:
                                 consumed = await loop.run_in_executor(None, self.client.call, "gen_wait_consumed",
                                                                       spec["tid"], n - bp + 1)
+                                if consumed < 0:  # the stream is gone: stop producing
+                                    await value.aclose()
+                                    if consumed == -2:
+                                        raise exc.TaskCancelledError(spec["tid"].hex())
+                                    break
                         value = iter(())
                         spec = dict(spec, _streamed=n)
                     else:
@@ -579,6 +589,16 @@ class Worker:
 
 
 _SCALARS = (type(None), bool, int, float, complex)
+
+
+def _close_gen(it):
+    """Run a generator's ``finally`` blocks now that nobody will consume its items."""
+    close = getattr(it, "close", None)
+    if close is not None:
+        try:
+            close()
+        except Exception:
+            pass
 
 
 def _small_value(v, depth: int = 0) -> bool:

@@ -460,3 +460,53 @@ def test_streaming_generator_backpressure(shutdown_only, tmp_path):
         _t.sleep(0.05)
     assert produced(mark2) == 20
     assert [ray.get(r) for r in g2] == list(range(1, 20))
+
+
+def test_paused_producer_released_on_cancel_and_drop(shutdown_only, tmp_path):
+    """A producer paused on generator backpressure gives its worker back when the task is
+    cancelled (non-force) and when the consumer drops the ObjectRefGenerator; its ``finally``
+    blocks run."""
+    import gc
+    import time as _t
+
+    ray.init(num_cpus=1, include_dashboard=False, log_to_driver=False)
+
+    @ray.remote
+    def gen(n, path):
+        try:
+            for i in range(n):
+                yield i
+        finally:
+            with open(path, "w") as f:
+                f.write("closed")
+
+    @ray.remote
+    def probe():
+        return "free"
+
+    def wait_closed(p, timeout=15):
+        deadline = _t.time() + timeout
+        while _t.time() < deadline:
+            if os.path.exists(p):
+                return open(p).read()
+            _t.sleep(0.05)
+        return None
+
+    # cancel: the consumer stops reading, the producer is parked, then cancelled
+    p1 = str(tmp_path / "c1")
+    g = gen.options(_generator_backpressure_num_objects=2).remote(1000, p1)
+    assert ray.get(next(g)) == 0
+    _t.sleep(0.5)
+    ray.cancel(g)
+    assert wait_closed(p1) == "closed"
+    assert ray.get(probe.remote(), timeout=20) == "free"  # the only CPU is free again
+
+    # drop: the generator object goes away mid-stream
+    p2 = str(tmp_path / "c2")
+    g = gen.options(_generator_backpressure_num_objects=2).remote(1000, p2)
+    assert ray.get(next(g)) == 0
+    _t.sleep(0.5)
+    del g
+    gc.collect()
+    assert wait_closed(p2) == "closed"
+    assert ray.get(probe.remote(), timeout=20) == "free"
