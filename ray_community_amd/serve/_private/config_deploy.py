@@ -114,6 +114,14 @@ def build_specs(app_cfg: Dict[str, Any]) -> Tuple[List[Dict[str, Any]], str]:
 
         s.update(_lifecycle_options({k: o.get(k, s.get(k)) for k in _LIFECYCLE_DEFAULTS}))
         s["actor_options"] = _merge_actor_options(s.get("actor_options") or {}, o.get("ray_actor_options") or {}, env)
+        from ..api import _placement_options
+
+        placement = {k: (o[k] if o.get(k) is not None else s.get(k))
+                     for k in ("placement_group_bundles", "placement_group_strategy", "max_replicas_per_node",
+                               "logging_config")}
+        if o.get("logging_config") is None and app_cfg.get("logging_config") is not None:
+            placement["logging_config"] = app_cfg["logging_config"]  # application-level default
+        s.update(_placement_options(dict(placement, ray_actor_options=s["actor_options"])))
         s["code_version"] = code_version
     return list(specs.values()), ingress
 

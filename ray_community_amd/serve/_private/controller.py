@@ -28,6 +28,8 @@ class _DeploymentState:
         self.counter = 0
         self.unhealthy_since = {}
         self.health: Dict[str, float] = {}  # tag -> time of the last passed health check
+        self.pgs: Dict[str, Any] = {}  # tag -> the replica's placement group (placement_group_bundles)
+        self.nodes: Dict[str, str] = {}  # tag -> node id it was pinned to (max_replicas_per_node)
 
 
 class ServeController:
@@ -38,6 +40,7 @@ class ServeController:
         self._loop_task = None
         self.proxy = None
         self.handle_queues: Dict[tuple, Dict[str, tuple]] = {}  # (app, dep) -> router id -> (n, ts)
+        self._draining: Dict[str, asyncio.Future] = {}  # tag -> background drain-and-kill of a stopped replica
 
     async def _ensure_loop(self):
         if self._loop_task is None:
@@ -65,7 +68,7 @@ class ServeController:
                     code_changed = st.spec["body_hash"] != spec["body_hash"] or \
                         st.spec["init_args_blob"] != spec["init_args_blob"]
                 code_changed = code_changed or st.spec["actor_options"] != spec["actor_options"]
-                if code_changed:
+                if code_changed:  # old replicas drain in the background while new ones start
                     await self._stop_replicas(st, list(st.replicas))
                 elif spec.get("user_config") != st.spec.get("user_config"):
                     from ..._private.worker import _core
@@ -100,9 +103,9 @@ class ServeController:
 
     async def delete_application(self, app_name: str):
         deps = self.apps.pop(app_name, {})
-        for st in deps.values():
-            await self._stop_replicas(st, list(st.replicas))
         self.app_meta.pop(app_name, None)
+        # this call (not the control loop) waits for the replicas to drain
+        await asyncio.gather(*[self._stop_replicas(st, list(st.replicas), wait=True) for st in deps.values()])
         return True
 
     async def shutdown(self):
@@ -118,18 +121,68 @@ class ServeController:
         from .replica import ServeReplica
 
         spec = st.spec
-        st.counter += 1
-        tag = f"{st.app}#{st.name}#{st.counter}"
         opts = dict(spec["actor_options"])
         mc = spec.get("max_ongoing_requests", 5)
         opts["max_concurrency"] = max(mc, 1) + 4
         opts.setdefault("num_cpus", 0)
+        node = None
+        if spec.get("max_replicas_per_node"):
+            node = self._pick_node(st)
+            if node is None:
+                st.message = (f"replicas pending: no node can take another replica under "
+                              f"max_replicas_per_node={spec['max_replicas_per_node']}")
+                return None
+        st.counter += 1
+        tag = f"{st.app}#{st.name}#{st.counter}"
+        pg = None
+        if spec.get("placement_group_bundles"):
+            # reference deployment_scheduler.py: one placement group per replica, actor in bundle 0,
+            # the replica's child tasks/actors captured into the other bundles
+            from ...util.placement_group import placement_group
+            from ...util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+            pg = placement_group(spec["placement_group_bundles"], strategy=spec.get("placement_group_strategy") or "PACK")
+            opts["scheduling_strategy"] = PlacementGroupSchedulingStrategy(
+                pg, placement_group_bundle_index=0, placement_group_capture_child_tasks=True)
+            st.pgs[tag] = pg
+        elif node is not None:
+            from ...util.scheduling_strategies import NodeAffinitySchedulingStrategy
+
+            opts["scheduling_strategy"] = NodeAffinitySchedulingStrategy(node, soft=False)
+            st.nodes[tag] = node
         cls = ActorClass(ServeReplica, opts)
         r = cls.remote(st.app, st.name, tag, spec["body"], spec["init_args"], spec["init_kwargs"],
-                       spec.get("user_config"), spec["is_function"])
+                       spec.get("user_config"), spec["is_function"], logging_config=spec.get("logging_config"))
         st.replicas[tag] = r
         self._bump(st)
         return tag, r
+
+    def _pick_node(self, st: _DeploymentState) -> Optional[str]:
+        """A node for one more replica under ``max_replicas_per_node``: alive, big enough for the
+        replica's resources, below the cap; the one holding the fewest replicas (spread)."""
+        from ..._private.worker import nodes
+
+        cap = int(st.spec["max_replicas_per_node"])
+        opts = st.spec.get("actor_options") or {}
+        need = {"CPU": float(opts.get("num_cpus", 0) or 0), "GPU": float(opts.get("num_gpus", 0) or 0)}
+        need.update({k: float(v) for k, v in (opts.get("resources") or {}).items()})
+        counts: Dict[str, int] = {}
+        for t in st.replicas:
+            n = st.nodes.get(t)
+            if n is not None:
+                counts[n] = counts.get(n, 0) + 1
+        best = None
+        for n in nodes():
+            if not n.get("Alive", True):
+                continue
+            nid = n["NodeID"]
+            c = counts.get(nid, 0)
+            res = n.get("Resources") or {}
+            if c >= cap or any(v > 0 and res.get(k, 0.0) < v for k, v in need.items()):
+                continue
+            if best is None or (c, nid) < best[0]:
+                best = ((c, nid), nid)
+        return None if best is None else best[1]
 
     def _bump(self, st):
         """The replica set of ``st`` changed: wake every router long-polling it."""
@@ -163,30 +216,66 @@ class ServeController:
             except asyncio.TimeoutError:
                 pass
 
-    async def _stop_replicas(self, st, tags):
-        await asyncio.gather(*[self._stop_replica(st, t) for t in tags])
+    async def _stop_replicas(self, st, tags, wait: bool = False):
+        """Take replicas out of routing NOW; each drains and is killed by a background task
+        (reference deployment_state.py: STOPPING replicas are polled by the state machine, so one
+        slow drain never stalls reconciliation of other deployments). ``wait``: also await them."""
+        tasks = [self._stop_replica(st, t) for t in tags]
+        tasks = [x for x in tasks if x is not None]
+        if wait and tasks:
+            await asyncio.gather(*tasks, return_exceptions=True)
 
-    async def _stop_replica(self, st, t):
-        from ..._private.worker import kill
-
+    def _stop_replica(self, st, t):
         r = st.replicas.pop(t, None)
         if r is None:
-            return
+            return None
         self._bump(st)
         st.health.pop(t, None)
+        st.nodes.pop(t, None)
+        pg = st.pgs.pop(t, None)
+        loop_s = float(st.spec.get("graceful_shutdown_wait_loop_s", 2.0))
+        timeout_s = float(st.spec.get("graceful_shutdown_timeout_s", 20.0))
+        task = asyncio.ensure_future(self._drain_and_kill(r, pg, loop_s, timeout_s))
+        self._draining[t] = task
+        task.add_done_callback(lambda _f, t=t: self._draining.pop(t, None))
+        return task
+
+    async def _drain_and_kill(self, r, pg, loop_s: float, timeout_s: float):
         # graceful shutdown (reference replica.py perform_graceful_shutdown): the replica is
         # already out of the routing table; it drains its ongoing requests, polling every
         # graceful_shutdown_wait_loop_s, and is killed after graceful_shutdown_timeout_s
-        loop_s = float(st.spec.get("graceful_shutdown_wait_loop_s", 2.0))
-        timeout_s = float(st.spec.get("graceful_shutdown_timeout_s", 20.0))
         try:
             await asyncio.wait_for(r.prepare_for_shutdown.remote(loop_s, timeout_s), timeout_s + 5)
         except Exception:
             pass
+        self._kill_replica(r, pg)
+
+    @staticmethod
+    def _kill_replica(r, pg):
+        from ..._private.worker import kill
+
         try:
             kill(r)
         except Exception:
             pass
+        if pg is not None:
+            from ...util.placement_group import remove_placement_group
+
+            try:
+                remove_placement_group(pg)
+            except Exception:
+                pass
+
+    async def num_draining(self):
+        return len(self._draining)
+
+    async def get_replica_placement(self, app_name: str, deployment: str):
+        """{replica tag: {"node_id", "placement_group_id"}} (placement tests / the dashboard)."""
+        st = self.apps.get(app_name, {}).get(deployment)
+        if st is None:
+            return None
+        return {t: {"node_id": st.nodes.get(t),
+                    "placement_group_id": st.pgs[t].id.hex() if t in st.pgs else None} for t in st.replicas}
 
     async def _reconcile_all(self):
         for app, deps in list(self.apps.items()):
@@ -196,7 +285,8 @@ class ServeController:
                 cur = len(st.replicas)
                 if cur < st.target:
                     for _ in range(st.target - cur):
-                        await self._start_replica(st)
+                        if await self._start_replica(st) is None:
+                            break  # no node can take it now (max_replicas_per_node): retried next round
                 elif cur > st.target:
                     await self._stop_replicas(st, list(st.replicas)[st.target:])
                 # readiness + periodic health checks: a replica is checked until it first passes
@@ -220,13 +310,9 @@ class ServeController:
                     if st.replicas.pop(tag, None) is not None:
                         self._bump(st)
                     st.health.pop(tag, None)
+                    st.nodes.pop(tag, None)
                     failed = True
-                    try:
-                        from ..._private.worker import kill
-
-                        kill(r)
-                    except Exception:  # noqa
-                        pass
+                    self._kill_replica(r, st.pgs.pop(tag, None))
                 ready = sum(1 for tag in st.replicas if tag in st.health)
                 if ready >= st.target and st.target > 0:
                     st.status = "HEALTHY"

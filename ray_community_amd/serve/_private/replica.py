@@ -42,15 +42,80 @@ class ReplicaContext:
         self.servable_object = servable_object
 
 
+class _JsonFormatter:
+    """``LoggingConfig(encoding="JSON")``: one JSON object per record (reference
+    ``serve/_private/logging_utils.py`` ServeJSONFormatter fields)."""
+
+    def __init__(self, deployment, replica, app):
+        import logging
+
+        self._base = logging.Formatter()
+        self.fields = {"deployment": deployment, "replica": replica, "application": app}
+
+    def format(self, record):
+        import json
+
+        out = {"levelname": record.levelname, "asctime": self._base.formatTime(record), **self.fields,
+               "message": record.getMessage()}
+        for k in ("request_id", "route", "method", "status", "latency_ms"):
+            if hasattr(record, k):
+                out[k] = getattr(record, k)
+        if record.exc_info:
+            out["exc_text"] = self._base.formatException(record.exc_info)
+        return json.dumps(out)
+
+
+def configure_replica_logging(logging_config: Optional[Dict], app_name: str, deployment: str, tag: str):
+    """Apply a deployment's ``LoggingConfig`` to the ``ray.serve`` logger of this replica process:
+    level, TEXT/JSON encoding, a per-replica log file under ``logs_dir`` (default: the session's
+    ``logs/serve``). Returns (logger, log file path)."""
+    import logging
+
+    lc = dict(logging_config or {})
+    level = lc.get("log_level", "INFO")
+    if isinstance(level, str):
+        level = logging.getLevelName(level.upper())
+        if not isinstance(level, int):
+            raise ValueError(f"invalid log_level {lc.get('log_level')!r}")
+    logs_dir = lc.get("logs_dir")
+    if not logs_dir:
+        from ..._private.worker import _core
+
+        try:
+            sess = _core().session_dir
+        except Exception:
+            sess = ""
+        logs_dir = os.path.join(sess or "/tmp/rca_serve", "logs", "serve")
+    os.makedirs(logs_dir, exist_ok=True)
+    safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in tag)
+    path = os.path.join(logs_dir, f"replica_{safe}_{os.getpid()}.log")
+    logger = logging.getLogger("ray.serve")
+    logger.setLevel(level)
+    for h in [h for h in logger.handlers if getattr(h, "_rca_serve", False)]:
+        logger.removeHandler(h)
+        h.close()
+    h = logging.FileHandler(path)
+    h._rca_serve = True
+    if str(lc.get("encoding", "TEXT")).upper() == "JSON":
+        h.setFormatter(_JsonFormatter(deployment, tag, app_name))
+    else:
+        h.setFormatter(logging.Formatter(f"%(levelname)s %(asctime)s {deployment} {tag} -- %(message)s"))
+    logger.addHandler(h)
+    return logger, path
+
+
 class ServeReplica:
     def __init__(self, app_name: str, deployment_name: str, replica_tag: str, body_blob: bytes, init_args, init_kwargs,
-                 user_config=None, is_function: bool = False):
+                 user_config=None, is_function: bool = False, logging_config: Optional[Dict] = None):
         from ..._private import serialization as ser
         from ..handle import _resolve_handle_args
 
         self.app_name = app_name
         self.deployment_name = deployment_name
         self.tag = replica_tag
+        self.logging_config = dict(logging_config or {})
+        self.logger, self.log_path = configure_replica_logging(logging_config, app_name, deployment_name, replica_tag)
+        self.access_log = bool(self.logging_config.get("enable_access_log", True))
         body = ser.loads_function(body_blob)
         init_args, init_kwargs = _resolve_handle_args(init_args, init_kwargs)
         self.is_function = is_function
@@ -123,12 +188,20 @@ class ServeReplica:
         finally:
             multiplex._reset_model_id(tok)
 
+    def _access(self, route, status, t0):
+        """One access-log line per request (``LoggingConfig.enable_access_log``)."""
+        if self.access_log:
+            ms = 1000.0 * (time.time() - t0)
+            self.logger.info(f"{route} {status} {ms:.1f}ms",
+                             extra={"route": route, "status": status, "latency_ms": round(ms, 3)})
+
     async def handle_request(self, method_name, args, kwargs, meta=None):
         from ..handle import _resolve_handle_args
 
         meta = meta or {}
         self.ongoing += 1
         self.total += 1
+        t0, status = time.time(), "OK"
         try:
             args, kwargs = _resolve_handle_args(args, kwargs)
             from ..._private.core_worker import ObjectRef
@@ -137,8 +210,12 @@ class ServeReplica:
             args = tuple([(await a) if isinstance(a, ObjectRef) else a for a in args])
             kwargs = {k: ((await v) if isinstance(v, ObjectRef) else v) for k, v in kwargs.items()}
             return await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
+        except BaseException:
+            status = "ERROR"
+            raise
         finally:
             self.ongoing -= 1
+            self._access(f"CALL {method_name or '__call__'}", status, t0)
 
     async def handle_request_stream(self, method_name, args, kwargs, meta=None):
         """Generator counterpart of ``handle_request`` for ``handle.options(stream=True)``:
@@ -176,12 +253,16 @@ class ServeReplica:
         """req: {method, path, query_string, headers, body, root_path}. Returns (status, headers, body)."""
         self.ongoing += 1
         self.total += 1
+        t0, status = time.time(), 500
         try:
             from .http_util import run_asgi_or_call
 
-            return await run_asgi_or_call(self, req)
+            out = await run_asgi_or_call(self, req)
+            status = out[0] if isinstance(out, tuple) and out else 200
+            return out
         finally:
             self.ongoing -= 1
+            self._access(f"{req.get('method', 'GET')} {req.get('path', '/')}", status, t0)
 
     async def get_num_ongoing(self):
         return self.ongoing
@@ -195,7 +276,8 @@ class ServeReplica:
         return True
 
     async def stats(self):
-        return {"ongoing": self.ongoing, "total": self.total, "pid": os.getpid(), "tag": self.tag}
+        return {"ongoing": self.ongoing, "total": self.total, "pid": os.getpid(), "tag": self.tag,
+                "log_path": self.log_path}
 
     async def prepare_for_shutdown(self, wait_loop_s: float = 2.0, timeout_s: float = 20.0):
         """Graceful shutdown (reference replica.py perform_graceful_shutdown): the controller has

@@ -17,7 +17,8 @@ _STATE = {"controller": None, "proxy": None, "http": {"host": "127.0.0.1", "port
 _DEP_OPTS = {"name", "num_replicas", "ray_actor_options", "max_ongoing_requests", "max_concurrent_queries",
              "autoscaling_config", "user_config", "health_check_period_s", "health_check_timeout_s",
              "graceful_shutdown_wait_loop_s", "graceful_shutdown_timeout_s", "route_prefix", "version",
-             "max_queued_requests", "placement_group_bundles", "placement_group_strategy", "logging_config"}
+             "max_queued_requests", "placement_group_bundles", "placement_group_strategy", "logging_config",
+             "max_replicas_per_node"}
 
 
 class Deployment:
@@ -97,8 +98,52 @@ class Application:
                                                            "target_ongoing_requests": 2}
                                                           if cfg.get("num_replicas") == "auto" else None),
                      "user_config": cfg.get("user_config"), "_app": self,
-                     **_lifecycle_options(cfg)}
+                     **_lifecycle_options(cfg), **_placement_options(cfg)}
         return name
+
+
+def _logging_dict(lc) -> Optional[Dict]:
+    """``LoggingConfig`` (model or dict) -> plain dict with the reference defaults filled in."""
+    if lc is None:
+        return None
+    if not isinstance(lc, dict):
+        lc = lc.model_dump() if hasattr(lc, "model_dump") else dict(lc.__dict__)
+    from .schema import LoggingConfig
+
+    return LoggingConfig(**lc).model_dump()
+
+
+def _placement_options(cfg: Dict) -> Dict:
+    """Replica placement (reference: serve/_private/deployment_scheduler.py): every replica gets a
+    placement group of ``placement_group_bundles`` (the replica actor in bundle 0) with
+    ``placement_group_strategy``; ``max_replicas_per_node`` caps replicas per node."""
+    bundles = cfg.get("placement_group_bundles")
+    strategy = cfg.get("placement_group_strategy")
+    mrpn = cfg.get("max_replicas_per_node")
+    if strategy is not None and bundles is None:
+        raise ValueError("placement_group_strategy is set but placement_group_bundles is not")
+    if bundles is not None:
+        if not isinstance(bundles, (list, tuple)) or not bundles or not all(isinstance(b, dict) for b in bundles):
+            raise ValueError("placement_group_bundles must be a non-empty list of resource dicts")
+        bundles = [{k: float(v) for k, v in b.items()} for b in bundles]
+        strategy = strategy or "PACK"
+        if strategy not in ("PACK", "SPREAD", "STRICT_PACK", "STRICT_SPREAD"):
+            raise ValueError(f"invalid placement_group_strategy {strategy!r}")
+        opts = cfg.get("ray_actor_options") or {}
+        need = {"CPU": float(opts.get("num_cpus", 0) or 0), "GPU": float(opts.get("num_gpus", 0) or 0)}
+        need.update({k: float(v) for k, v in (opts.get("resources") or {}).items()})
+        for k, v in need.items():
+            if v > 0 and bundles[0].get(k, 0.0) < v:
+                raise ValueError(f"the replica actor needs {k}={v} but placement_group_bundles[0] has "
+                                 f"{bundles[0].get(k, 0.0)}: the actor runs in the first bundle")
+    if mrpn is not None:
+        mrpn = int(mrpn)
+        if mrpn < 1:
+            raise ValueError("max_replicas_per_node must be >= 1")
+        if bundles is not None:
+            raise ValueError("max_replicas_per_node cannot be combined with placement_group_bundles")
+    return {"placement_group_bundles": bundles, "placement_group_strategy": strategy,
+            "max_replicas_per_node": mrpn, "logging_config": _logging_dict(cfg.get("logging_config"))}
 
 
 # replica lifecycle options and their reference defaults (serve/config.py DeploymentConfig)
@@ -119,7 +164,8 @@ def deployment(_func_or_class=None, *, name: Optional[str] = None, num_replicas:
                max_concurrent_queries: Optional[int] = None, autoscaling_config=None, user_config=None,
                health_check_period_s=None, health_check_timeout_s=None, graceful_shutdown_wait_loop_s=None,
                graceful_shutdown_timeout_s=None, route_prefix=None, version=None, max_queued_requests=None,
-               placement_group_bundles=None, placement_group_strategy=None, logging_config=None):
+               placement_group_bundles=None, placement_group_strategy=None, logging_config=None,
+               max_replicas_per_node=None):
     cfg = {k: v for k, v in dict(num_replicas=num_replicas, ray_actor_options=ray_actor_options,
                                  max_ongoing_requests=max_ongoing_requests or max_concurrent_queries,
                                  autoscaling_config=autoscaling_config, user_config=user_config,
@@ -127,8 +173,13 @@ def deployment(_func_or_class=None, *, name: Optional[str] = None, num_replicas:
                                  health_check_period_s=health_check_period_s,
                                  health_check_timeout_s=health_check_timeout_s,
                                  graceful_shutdown_wait_loop_s=graceful_shutdown_wait_loop_s,
-                                 graceful_shutdown_timeout_s=graceful_shutdown_timeout_s).items()
+                                 graceful_shutdown_timeout_s=graceful_shutdown_timeout_s,
+                                 placement_group_bundles=placement_group_bundles,
+                                 placement_group_strategy=placement_group_strategy,
+                                 max_replicas_per_node=max_replicas_per_node,
+                                 logging_config=logging_config).items()
            if v is not None}
+    _placement_options(cfg)  # validate at decoration time, as the reference does
     if num_replicas is not None and autoscaling_config is not None and num_replicas != "auto":
         raise ValueError("Manually setting num_replicas is not allowed when autoscaling_config is provided.")
 
@@ -225,8 +276,11 @@ def run(target: Union[Application, Deployment], *, name: str = "default", route_
         raise TypeError("serve.run expects an Application (deployment.bind(...))")
     specs: Dict[str, Dict] = {}
     ingress = target._collect(name, specs)
+    app_logging = _logging_dict(logging_config)
     for s in specs.values():
         s.pop("_app", None)
+        if s.get("logging_config") is None:
+            s["logging_config"] = app_logging  # the application-level default
     ctrl = _get_controller()
     w.get(ctrl.deploy_application.remote(name, list(specs.values()), ingress, route_prefix))
     status = w.get(ctrl.wait_app_running.remote(name, 300.0))
