@@ -9,6 +9,7 @@ import time
 from collections import deque
 from typing import Any, Dict, List, Optional
 
+import cloudpickle
 import numpy as np
 import torch
 
@@ -59,25 +60,25 @@ class Algorithm(Trainable):
             runner_cls = MultiAgentEnvRunner
         # the local runner (index 0) never takes the runners' GPU share
         self.local_runner = runner_cls(dict(rd, num_gpus_per_env_runner=0), 0)
-        self.remote_runners = []
-        if cfg.num_env_runners > 0:
-            from ...actor import ActorClass
+        from ..env.env_runner_group import EnvRunnerGroup
 
-            opts = {"num_cpus": cfg.num_cpus_per_env_runner}
-            if getattr(cfg, "num_gpus_per_env_runner", 0):
-                opts["num_gpus"] = cfg.num_gpus_per_env_runner
-            cls = ActorClass(runner_cls, opts)
-            self.remote_runners = [cls.remote(rd, i + 1) for i in range(cfg.num_env_runners)]
+        opts = {"num_cpus": cfg.num_cpus_per_env_runner, "max_restarts": 0}
+        if getattr(cfg, "num_gpus_per_env_runner", 0):
+            opts["num_gpus"] = cfg.num_gpus_per_env_runner
+        self._runner_cls = runner_cls
+        self.env_runner_group = EnvRunnerGroup(runner_cls, rd, cfg, self.local_runner, int(cfg.num_env_runners), opts)
+        self._counters = {"total_num_restored_workers": 0}
         from ..core.learner import LearnerGroup
 
         ld = cfg.to_dict()
         ld.update(cfg._connector_dict())
         ld.update(self._runner_extra())
         ld["_algo"] = rd["_algo"]
+        self._learner_dict = ld
         if self.multi_agent:
             # one learner group (RLModule + optimizer, possibly several GPU learners) per policy
             sp = self.local_runner.spaces()
-            self.learner_groups = {p: LearnerGroup(ld, *sp[p]) for p in self.local_runner.modules}
+            self.learner_groups = {p: LearnerGroup(dict(ld, _module_id=p), *sp[p]) for p in self.local_runner.modules}
             self.policies_to_train = list(cfg.policies_to_train or self.learner_groups)
             first = next(iter(self.learner_groups))
             self.obs_space, self.act_space = sp[first]
@@ -97,6 +98,74 @@ class Algorithm(Trainable):
     def _runner_extra(self):
         return {}
 
+    # ------------------------------------------------------------------ env runners
+    @property
+    def workers(self):
+        """The env runner group (reference name ``Algorithm.workers`` / ``env_runner_group``)."""
+        return getattr(self, "env_runner_group", None)
+
+    @property
+    def remote_runners(self) -> List:
+        """The HEALTHY remote env runner actors."""
+        g = getattr(self, "env_runner_group", None)
+        if g is None:
+            return list(self.__dict__.get("_remote_runners_override", []))
+        return g.healthy_env_runners()
+
+    @remote_runners.setter
+    def remote_runners(self, value):
+        if getattr(self, "env_runner_group", None) is not None and not value:
+            self.env_runner_group.stop()
+        else:
+            self.__dict__["_remote_runners_override"] = list(value or [])
+
+    def _foreach_runner(self, method: str, *args, local_fallback: bool = True) -> List:
+        """``method(*args)`` on every healthy remote runner (failures handled by the group's
+        fault-tolerance policy); with no remote runner left, on the local one."""
+        g = getattr(self, "env_runner_group", None)
+        out = g.foreach_env_runner(method, *args) if g is not None and g.num_remote_env_runners() else []
+        if not out and local_fallback:
+            out = [getattr(self.local_runner, method)(*args)]
+        return out
+
+    def restore_workers(self, workers=None) -> List[int]:
+        """Bring recreated / recovered env runners up to date (reference ``algorithm.py:1429``):
+        probe the unhealthy ones, push the current weights and connector state to those that
+        answer, mark them healthy and fire ``on_workers_recreated``."""
+        from ..._private.worker import get, put
+
+        workers = workers or getattr(self, "env_runner_group", None)
+        if workers is None:
+            return []
+        restored = workers.probe_unhealthy_env_runners()
+        if not restored:
+            return []
+        st = ({p: g.get_weights() for p, g in self.learner_groups.items()} if self.multi_agent
+              else self.learner_group.get_weights())
+        ref = put(st)
+        actors = workers.manager.actors()
+        calls = [actors[i].set_weights.remote(ref, self._weights_version) for i in restored]
+        if not self.multi_agent and getattr(self.local_runner, "has_stateful_connectors", False):
+            cs = self.local_runner.get_connector_state()
+            calls += [actors[i].set_connector_state.remote(cs) for i in restored]
+        ok = []
+        try:
+            get(calls, timeout=workers.restore_timeout)
+            ok = restored
+        except Exception:  # noqa  (a runner that dies while being restored stays unhealthy)
+            for i in restored:
+                try:
+                    get(actors[i].ping.remote(), timeout=workers.probe_timeout)
+                    ok.append(i)
+                except Exception:  # noqa
+                    pass
+        workers.mark_healthy(ok)
+        self._counters["total_num_restored_workers"] += len(ok)
+        if ok and getattr(self, "callbacks", None) is not None:
+            self.callbacks.on_workers_recreated(algorithm=self, worker_set=workers, worker_ids=ok,
+                                                is_evaluation=False)
+        return ok
+
     # ------------------------------------------------------------------ rollouts
     def _sync_weights(self):
         from ..._private.worker import get, put
@@ -106,8 +175,7 @@ class Algorithm(Trainable):
         self._weights_version += 1
         self.local_runner.set_weights(st, self._weights_version)
         if self.remote_runners:
-            ref = put(st)
-            get([r.set_weights.remote(ref, self._weights_version) for r in self.remote_runners])
+            self._foreach_runner("set_weights", put(st), self._weights_version, local_fallback=False)
         self._sync_connector_states()
 
     def _sync_connector_states(self):
@@ -119,18 +187,16 @@ class Algorithm(Trainable):
             return
         states = [self.local_runner.get_connector_state()]
         if self.remote_runners:
-            states += get([r.get_connector_state.remote() for r in self.remote_runners])
+            states += self._foreach_runner("get_connector_state", local_fallback=False)
         merged = self.local_runner.env_to_module.merge_states(states)
         self.local_runner.set_connector_state(merged)
         if self.remote_runners:
-            get([r.set_connector_state.remote(merged) for r in self.remote_runners])
+            self._foreach_runner("set_connector_state", merged, local_fallback=False)
 
     def _sample_fragments(self, steps_total: int) -> List[SampleBatch]:
-        from ..._private.worker import get
-
-        if self.remote_runners:
-            per = max(1, steps_total // len(self.remote_runners))
-            return get([r.sample.remote(per) for r in self.remote_runners])
+        n = len(self.remote_runners)
+        if n:
+            return self._foreach_runner("sample", max(1, steps_total // n))
         return [self.local_runner.sample(steps_total)]
 
     def _sample(self, steps_total: int) -> SampleBatch:
@@ -141,7 +207,7 @@ class Algorithm(Trainable):
 
         ms = [self.local_runner.get_metrics()]
         if self.remote_runners:
-            ms += get([r.get_metrics.remote() for r in self.remote_runners])
+            ms += self._foreach_runner("get_metrics", local_fallback=False)
         eps = [e for m in ms for e in m["episodes"]]
         self._custom_metrics = [c for m in ms for c in m.get("custom_metrics", ())]
         if self.multi_agent:
@@ -165,6 +231,7 @@ class Algorithm(Trainable):
 
     def train(self) -> Dict:
         t0 = time.perf_counter()
+        self.restore_workers()
         info = self.training_step()
         eps = self._collect_metrics()
         self._iteration += 1
@@ -189,6 +256,12 @@ class Algorithm(Trainable):
             res["policy_reward_mean"] = {p: float(np.mean(d)) for p, d in getattr(self, "_policy_recent", {}).items()
                                          if d}
         res["env_steps_per_sec"] = res["num_env_steps_sampled_this_iter"] / dt if dt > 0 else 0.0
+        g = getattr(self, "env_runner_group", None)
+        if g is not None:
+            res["num_healthy_workers"] = g.num_healthy_remote_env_runners()
+            res["num_remote_worker_restarts"] = g.num_remote_env_runner_restarts()
+            res["num_env_runner_failures"] = len(g.failures)
+            res["counters"] = dict(getattr(self, "_counters", {}))
         res["env_runners"] = {"episode_return_mean": res["episode_reward_mean"],
                               "episode_return_max": res["episode_reward_max"],
                               "episode_return_min": res["episode_reward_min"],
@@ -308,6 +381,113 @@ class Algorithm(Trainable):
             json.dump({"module_class": type(m).__name__, "policy_id": policy_id}, f)
         return export_dir
 
+    # ------------------------------------------------------------------ runtime policy mutation
+    def add_policy(self, policy_id, policy_cls=None, policy=None, *, observation_space=None, action_space=None,
+                   config=None, policy_state=None, policy_mapping_fn=None, policies_to_train=None,
+                   module_spec=None, evaluation_workers=True, **kw):
+        """Add a policy (its RLModule + learner group) to a running multi-agent algorithm and to
+        every env runner (reference ``algorithm.py:1929``; league / self-play training).
+        ``policy_state``: initial weights (e.g. a frozen copy of another policy's
+        ``get_weights()``); ``policy_mapping_fn``: the new agent -> policy mapping;
+        ``policies_to_train``: the new trainable set. Returns the new policy's ``TorchPolicy``."""
+        if not self.multi_agent:
+            raise ValueError("add_policy needs a multi-agent algorithm (config.multi_agent(policies=...))")
+        if policy_id in self.learner_groups:
+            raise KeyError(f"policy {policy_id!r} already exists")
+        from ..core.learner import LearnerGroup
+
+        sp = self.local_runner.spaces()
+        if observation_space is None or action_space is None:
+            if module_spec is not None and module_spec.observation_space is not None:
+                observation_space = observation_space or module_spec.observation_space
+                action_space = action_space or module_spec.action_space
+            else:
+                fn = policy_mapping_fn or self.config.policy_mapping_fn
+                env0 = self.local_runner.envs[0]
+                agents = [a for a in self.local_runner.agent_ids if fn is not None and fn(a, None, worker=None) ==
+                          policy_id]
+                if agents:
+                    observation_space = observation_space or env0.get_observation_space(agents[0])
+                    action_space = action_space or env0.get_action_space(agents[0])
+                else:
+                    first = next(iter(sp.values()))
+                    observation_space, action_space = observation_space or first[0], action_space or first[1]
+        if module_spec is not None:
+            from ..core.rl_module import MultiRLModuleSpec
+
+            spec = self._learner_dict.get("rl_module_spec")
+            if isinstance(spec, MultiRLModuleSpec):
+                specs = dict(spec.module_specs)
+            elif isinstance(spec, dict):
+                specs = dict(spec)
+            else:
+                specs = {} if spec is None else {"default_policy": spec}
+            specs[policy_id] = module_spec
+            self._learner_dict["rl_module_spec"] = specs
+            self.env_runner_group._runner_config["rl_module_spec"] = specs
+            self.local_runner.cfg["rl_module_spec"] = specs
+        ld = dict(self._learner_dict, **(config or {}), _module_id=policy_id)
+        g = LearnerGroup(ld, observation_space, action_space)
+        if policy_state is not None:
+            g.call("set_weights", policy_state)
+        self.learner_groups[policy_id] = g
+        w = g.get_weights()
+        self.local_runner.add_policy(policy_id, observation_space, action_space, w, policy_mapping_fn)
+        if self.remote_runners:
+            self._foreach_runner("add_policy", policy_id, observation_space, action_space, w, policy_mapping_fn,
+                                 local_fallback=False)
+        self.env_runner_group._runner_config["policies"] = dict.fromkeys(self.learner_groups)
+        if policy_mapping_fn is not None:
+            self.config.policy_mapping_fn = policy_mapping_fn
+            self.env_runner_group._runner_config["policy_mapping_fn"] = policy_mapping_fn
+        pols = dict(self.config.policies or {})
+        pols[policy_id] = None
+        self.config.policies = pols
+        if policies_to_train is not None:
+            self.policies_to_train = [p for p in policies_to_train if p in self.learner_groups]
+        else:
+            self.policies_to_train = list(self.policies_to_train) + [policy_id]
+        self.config.policies_to_train = list(self.policies_to_train)
+        self._sync_weights()
+        return self.get_policy(policy_id)
+
+    def remove_policy(self, policy_id, *, policy_mapping_fn=None, policies_to_train=None, evaluation_workers=True,
+                      **kw):
+        """Remove a policy from the learners and every env runner (reference ``algorithm.py:2126``)."""
+        if not self.multi_agent or policy_id not in self.learner_groups:
+            raise KeyError(f"unknown policy {policy_id!r}")
+        if len(self.learner_groups) == 1:
+            raise ValueError("cannot remove the last policy")
+        self.local_runner.remove_policy(policy_id, policy_mapping_fn)
+        if self.remote_runners:
+            self._foreach_runner("remove_policy", policy_id, policy_mapping_fn, local_fallback=False)
+        self.learner_groups.pop(policy_id).shutdown()
+        if self.learner_group is None or policy_id not in self.learner_groups:
+            first = next(iter(self.learner_groups))
+            self.learner_group = self.learner_groups[first]
+            self.obs_space, self.act_space = self.local_runner.spaces()[first]
+        pols = dict(self.config.policies or {})
+        pols.pop(policy_id, None)
+        self.config.policies = pols
+        self.env_runner_group._runner_config["policies"] = dict.fromkeys(self.learner_groups)
+        if policy_mapping_fn is not None:
+            self.config.policy_mapping_fn = policy_mapping_fn
+            self.env_runner_group._runner_config["policy_mapping_fn"] = policy_mapping_fn
+        self.policies_to_train = [p for p in (policies_to_train or self.policies_to_train) if p != policy_id]
+        self.config.policies_to_train = list(self.policies_to_train)
+
+    def add_module(self, module_id, module_spec=None, *, config_overrides=None, new_agent_to_module_mapping_fn=None,
+                   new_should_module_be_updated=None, add_to_learners=True, add_to_env_runners=True, **kw):
+        """New-API-stack name of ``add_policy`` (reference ``algorithm.py:2054``)."""
+        return self.add_policy(module_id, module_spec=module_spec, config=config_overrides,
+                               policy_mapping_fn=new_agent_to_module_mapping_fn,
+                               policies_to_train=new_should_module_be_updated)
+
+    def remove_module(self, module_id, *, new_agent_to_module_mapping_fn=None, new_should_module_be_updated=None,
+                      **kw):
+        return self.remove_policy(module_id, policy_mapping_fn=new_agent_to_module_mapping_fn,
+                                  policies_to_train=new_should_module_be_updated)
+
     def get_weights(self, policies=None):
         if self.multi_agent:
             return {p: g.get_weights() for p, g in self.learner_groups.items() if policies is None or p in policies}
@@ -323,13 +503,20 @@ class Algorithm(Trainable):
 
     def save_checkpoint(self, checkpoint_dir: str):
         os.makedirs(checkpoint_dir, exist_ok=True)
-        learner = ({p: g.call("get_state") for p, g in self.learner_groups.items()} if self.multi_agent
-                   else self.learner_group.call("get_state"))
+        if self.multi_agent:
+            keep = (set(self.policies_to_train) if self.config.checkpoint_trainable_policies_only
+                    else set(self.learner_groups))
+            learner = {p: g.call("get_state") for p, g in self.learner_groups.items() if p in keep}
+        else:
+            learner = self.learner_group.call("get_state")
+        if self.config.export_native_model_files:
+            for p in (list(learner) if self.multi_agent else [None]):
+                self.export_policy_model(os.path.join(checkpoint_dir, "native_models", str(p or "default_policy")), p)
         st = {"learner": learner, "iteration": self._iteration, "multi_agent": self.multi_agent,
               "timesteps_total": self._timesteps_total, "config": self.config.to_dict(),
               "extra": self._extra_state()}
         with open(os.path.join(checkpoint_dir, "algorithm_state.pkl"), "wb") as f:
-            pickle.dump(st, f)
+            cloudpickle.dump(st, f)  # configs hold user callables (policy_mapping_fn, ...)
         with open(os.path.join(checkpoint_dir, "rllib_checkpoint.json"), "w") as f:
             json.dump({"type": "Algorithm", "algo": type(self).__name__, "format": "rca-1"}, f)
         return checkpoint_dir
@@ -340,7 +527,8 @@ class Algorithm(Trainable):
             st = pickle.load(f)
         if st.get("multi_agent"):
             for p, ls in st["learner"].items():
-                self.learner_groups[p].call("set_state", ls)
+                if p in self.learner_groups:
+                    self.learner_groups[p].call("set_state", ls)
         else:
             self.learner_group.call("set_state", st["learner"])
         self._iteration = st["iteration"]
@@ -377,14 +565,9 @@ class Algorithm(Trainable):
         return algo
 
     def stop(self):
-        from ..._private.worker import kill
-
-        for r in self.remote_runners:
-            try:
-                kill(r)
-            except Exception:
-                pass
-        self.remote_runners = []
+        g = getattr(self, "env_runner_group", None)
+        if g is not None:
+            g.stop()
         for g in (self.learner_groups.values() if self.multi_agent else [self.learner_group]):
             g.shutdown()
 

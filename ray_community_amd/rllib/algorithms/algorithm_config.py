@@ -59,6 +59,20 @@ class AlgorithmConfig:
         self.policy_mapping_fn = None        # (agent_id, episode, worker, **kw) -> policy_id
         self.policies_to_train = None
         self.min_sample_timesteps_per_iteration = 0
+        # fault tolerance (reference algorithm_config.py:486-499, fault_tolerance():2673)
+        self.ignore_env_runner_failures = False
+        self.recreate_failed_env_runners = False
+        self.max_num_env_runner_restarts = 1000
+        self.delay_between_env_runner_restarts_s = 60.0
+        self.restart_failed_sub_environments = False
+        self.num_consecutive_env_runner_failures_tolerance = 100
+        self.env_runner_health_probe_timeout_s = 30.0
+        self.env_runner_restore_timeout_s = 1800.0
+        # checkpointing (reference checkpointing():2596)
+        self.export_native_model_files = False
+        self.checkpoint_trainable_policies_only = False
+        # custom RLModule (reference rl_module():2737)
+        self._rl_module_spec = None
 
     # ------------------------------------------------------------------ builder methods
     def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None, **kw):
@@ -160,11 +174,117 @@ class AlgorithmConfig:
             self.min_sample_timesteps_per_iteration = min_sample_timesteps_per_iteration
         return self
 
-    def rl_module(self, *, model_config=None, model_config_dict=None, **kw):
+    def rl_module(self, *, model_config=None, model_config_dict=None, rl_module_spec=None, **kw):
+        """``model_config``: network settings merged into ``model``; ``rl_module_spec``: an
+        ``RLModuleSpec`` (custom ``module_class`` built with (obs_space, act_space, model_config))
+        or, multi-agent, a ``MultiRLModuleSpec`` / {module_id: RLModuleSpec}."""
         m = model_config or model_config_dict
         if m:
             self.model = {**self.model, **dict(m)}
+        if rl_module_spec is not None:
+            self._rl_module_spec = rl_module_spec
         return self
+
+    @property
+    def rl_module_spec(self):
+        return self._rl_module_spec
+
+    def fault_tolerance(self, *, recreate_failed_env_runners=None, ignore_env_runner_failures=None,
+                        max_num_env_runner_restarts=None, delay_between_env_runner_restarts_s=None,
+                        restart_failed_sub_environments=None, num_consecutive_env_runner_failures_tolerance=None,
+                        env_runner_health_probe_timeout_s=None, env_runner_restore_timeout_s=None,
+                        recreate_failed_workers=None, ignore_worker_failures=None, max_num_worker_restarts=None,
+                        delay_between_worker_restarts_s=None, num_consecutive_worker_failures_tolerance=None,
+                        worker_health_probe_timeout_s=None, worker_restore_timeout_s=None,
+                        restart_failed_env_runners=None, **kw):
+        """Env-runner fault tolerance (reference ``fault_tolerance``, old ``*_worker*`` names
+        accepted): ``recreate_failed_env_runners`` replaces a dead runner with a fresh actor of the
+        same index (restored with the current weights before it samples again);
+        ``ignore_env_runner_failures`` drops it and goes on with the healthy ones."""
+        def pick(*vals):
+            for v in vals:
+                if v is not None:
+                    return v
+            return None
+
+        vals = {
+            "recreate_failed_env_runners": pick(recreate_failed_env_runners, restart_failed_env_runners,
+                                                recreate_failed_workers),
+            "ignore_env_runner_failures": pick(ignore_env_runner_failures, ignore_worker_failures),
+            "max_num_env_runner_restarts": pick(max_num_env_runner_restarts, max_num_worker_restarts),
+            "delay_between_env_runner_restarts_s": pick(delay_between_env_runner_restarts_s,
+                                                        delay_between_worker_restarts_s),
+            "restart_failed_sub_environments": restart_failed_sub_environments,
+            "num_consecutive_env_runner_failures_tolerance": pick(num_consecutive_env_runner_failures_tolerance,
+                                                                  num_consecutive_worker_failures_tolerance),
+            "env_runner_health_probe_timeout_s": pick(env_runner_health_probe_timeout_s, worker_health_probe_timeout_s),
+            "env_runner_restore_timeout_s": pick(env_runner_restore_timeout_s, worker_restore_timeout_s),
+        }
+        for k, v in vals.items():
+            if v is not None:
+                setattr(self, k, v)
+        if kw:
+            raise TypeError(f"fault_tolerance() got unsupported argument(s) {sorted(kw)}")
+        return self
+
+    # old-stack attribute names
+    @property
+    def recreate_failed_workers(self):
+        return self.recreate_failed_env_runners
+
+    @property
+    def ignore_worker_failures(self):
+        return self.ignore_env_runner_failures
+
+    def checkpointing(self, *, export_native_model_files=None, checkpoint_trainable_policies_only=None, **kw):
+        """``checkpoint_trainable_policies_only``: multi-agent checkpoints hold only the policies
+        in ``policies_to_train``; ``export_native_model_files``: each checkpoint also gets every
+        policy's ``model.pt`` (a ``weights_only``-loadable ``state_dict``)."""
+        if export_native_model_files is not None:
+            self.export_native_model_files = bool(export_native_model_files)
+        if checkpoint_trainable_policies_only is not None:
+            self.checkpoint_trainable_policies_only = bool(checkpoint_trainable_policies_only)
+        return self
+
+    def validate(self) -> None:
+        """Reject inconsistent settings before anything is built (reference ``validate``,
+        ``algorithm_config.py:791``). Algorithm configs extend it with their own checks."""
+        def bad(msg):
+            raise ValueError(msg)
+
+        if self.framework_str != "torch":
+            bad("only the torch framework is supported")
+        if int(self.num_env_runners) < 0:
+            bad(f"num_env_runners must be >= 0, got {self.num_env_runners}")
+        if int(self.num_envs_per_env_runner) < 1:
+            bad(f"num_envs_per_env_runner must be >= 1, got {self.num_envs_per_env_runner}")
+        rfl = self.rollout_fragment_length
+        if rfl != "auto" and (not isinstance(rfl, int) or rfl <= 0):
+            bad(f"rollout_fragment_length must be 'auto' or a positive int, got {rfl!r}")
+        if self.batch_mode not in ("truncate_episodes", "complete_episodes"):
+            bad(f"batch_mode must be 'truncate_episodes' or 'complete_episodes', got {self.batch_mode!r}")
+        if not (0.0 <= float(self.gamma) <= 1.0):
+            bad(f"gamma must be in [0, 1], got {self.gamma}")
+        if self.lr is not None and self.lr_schedule is None and float(self.lr) <= 0:
+            bad(f"lr must be > 0, got {self.lr}")
+        if int(self.train_batch_size) <= 0:
+            bad(f"train_batch_size must be > 0, got {self.train_batch_size}")
+        if int(self.num_learners) < 0 or float(self.num_gpus_per_learner) < 0:
+            bad("num_learners and num_gpus_per_learner must be >= 0")
+        if self.evaluation_duration_unit not in ("episodes", "timesteps"):
+            bad(f"evaluation_duration_unit must be 'episodes' or 'timesteps', got {self.evaluation_duration_unit!r}")
+        if self.evaluation_interval is not None and int(self.evaluation_interval) < 0:
+            bad("evaluation_interval must be >= 0 or None")
+        if self.policies:
+            if self.policy_mapping_fn is not None and not callable(self.policy_mapping_fn):
+                bad("policy_mapping_fn must be callable")
+            unknown = set(self.policies_to_train or ()) - set(self.policies)
+            if unknown and not callable(self.policies_to_train):
+                bad(f"policies_to_train names unknown policies {sorted(unknown)}")
+        if int(self.max_num_env_runner_restarts) < 0 or float(self.delay_between_env_runner_restarts_s) < 0:
+            bad("max_num_env_runner_restarts and delay_between_env_runner_restarts_s must be >= 0")
+        if (self.model or {}).get("use_lstm") and int((self.model or {}).get("max_seq_len", 20)) <= 0:
+            bad("model.max_seq_len must be > 0 with use_lstm")
 
     def api_stack(self, **kw):
         return self
@@ -245,6 +365,7 @@ class AlgorithmConfig:
     def build(self, env=None, logger_creator=None, use_copy=True):
         if env is not None:
             self.env = env
+        self.validate()
         return self.algo_class(config=self.copy() if use_copy else self)
 
     build_algo = build
@@ -265,4 +386,5 @@ class AlgorithmConfig:
     def _connector_dict(self) -> Dict:
         return {"env_to_module_connector": self._env_to_module_connector,
                 "module_to_env_connector": self._module_to_env_connector,
-                "learner_connector": self._learner_connector}
+                "learner_connector": self._learner_connector,
+                "rl_module_spec": self._rl_module_spec}

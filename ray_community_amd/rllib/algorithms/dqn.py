@@ -53,15 +53,10 @@ class DQN(Algorithm):
         return sched[-1][1]
 
     def training_step(self) -> Dict:
-        from ..._private.worker import get
-
         cfg = self.config
         eps = self._epsilon()
         steps = max(1, cfg.get_rollout_fragment_length()) * self.local_runner.N
-        if self.remote_runners:
-            batches = get([r.sample_transitions.remote(steps, eps) for r in self.remote_runners])
-        else:
-            batches = [self.local_runner.sample_transitions(steps, eps)]
+        batches = self._foreach_runner("sample_transitions", steps, eps)
         b = concat_samples(batches)
         self.buffer.add(b)
         n = b.count

@@ -49,24 +49,38 @@ class IMPALA(Algorithm):
         from ..._private.worker import get, wait
 
         cfg = self.config
-        if not self.remote_runners:
-            return self.local_runner.sample(max(steps, self.local_runner.N))
+        g = self.env_runner_group
         frag = cfg.get_rollout_fragment_length() * max(1, cfg.num_envs_per_env_runner)
         if not hasattr(self, "_inflight"):
-            self._inflight = {}
-            for r in self.remote_runners:
-                for _ in range(max(1, cfg.max_requests_in_flight_per_env_runner)):
-                    self._inflight[r.sample.remote(frag)] = r
+            self._inflight = {}  # sample ref -> runner id
+        # top every healthy runner (new, or restored by restore_workers) up to its request budget
+        actors = g.manager.actors()
+        per = max(1, cfg.max_requests_in_flight_per_env_runner)
+        for i in g.healthy_env_runner_ids():
+            for _ in range(per - sum(1 for v in self._inflight.values() if v == i)):
+                self._inflight[actors[i].sample.remote(frag)] = i
         got: List = []
         n = 0
         while n < steps:
-            ready, _ = wait(list(self._inflight), num_returns=1)
-            for ref in ready:
-                r = self._inflight.pop(ref)
-                b = get(ref)
+            if not self._inflight:  # no healthy remote runner left: the local one samples
+                b = self.local_runner.sample(max(steps - n, self.local_runner.N))
                 got.append(b)
                 n += b.count
-                self._inflight[r.sample.remote(frag)] = r
+                break
+            ready, _ = wait(list(self._inflight), num_returns=1)
+            for ref in ready:
+                i = self._inflight.pop(ref)
+                try:
+                    b = get(ref)
+                except Exception as e:  # noqa  (the group's policy decides: raise, or drop the runner)
+                    g.mark_failed(i, e)
+                    for other in [r for r, j in self._inflight.items() if j == i]:
+                        self._inflight.pop(other, None)
+                    continue
+                got.append(b)
+                n += b.count
+                if g.manager.is_actor_healthy(i):
+                    self._inflight[g.manager.actors()[i].sample.remote(frag)] = i
         return concat_samples(got)
 
     def _broadcast_async(self):

@@ -26,6 +26,20 @@ class PPOConfig(AlgorithmConfig):
         self.num_epochs = 30
         self.grad_clip = None
 
+    def validate(self) -> None:
+        super().validate()
+        if self.minibatch_size is not None and int(self.minibatch_size) > int(self.train_batch_size):
+            raise ValueError(f"minibatch_size ({self.minibatch_size}) must be <= train_batch_size "
+                             f"({self.train_batch_size})")
+        if int(self.num_epochs) < 1:
+            raise ValueError(f"num_epochs must be >= 1, got {self.num_epochs}")
+        if float(self.entropy_coeff) < 0:
+            raise ValueError(f"entropy_coeff must be >= 0, got {self.entropy_coeff}")
+        if float(self.clip_param) <= 0 or float(self.vf_clip_param) <= 0:
+            raise ValueError("clip_param and vf_clip_param must be > 0")
+        if float(self.kl_coeff) < 0:
+            raise ValueError(f"kl_coeff must be >= 0, got {self.kl_coeff}")
+
     @property
     def sgd_minibatch_size(self):
         return self.minibatch_size

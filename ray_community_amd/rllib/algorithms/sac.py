@@ -54,10 +54,7 @@ class SAC(Algorithm):
         warm = self._timesteps_total < cfg.num_steps_sampled_before_learning_starts
         eps = 1.0 if warm else 0.0
         steps = max(1, cfg.get_rollout_fragment_length()) * self.local_runner.N
-        if self.remote_runners:
-            batches = get([r.sample_transitions.remote(steps, eps) for r in self.remote_runners])
-        else:
-            batches = [self.local_runner.sample_transitions(steps, eps)]
+        batches = self._foreach_runner("sample_transitions", steps, eps)
         b = concat_samples(batches)
         self.buffer.add(b)
         n = b.count

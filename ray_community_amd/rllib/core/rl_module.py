@@ -165,7 +165,7 @@ class RLModule(nn.Module):
         return a, d.logp(a), v, logits
 
     def get_state(self):
-        return {k: v.detach().cpu() for k, v in self.state_dict().items()}
+        return {k: v.detach().to("cpu", copy=True) for k, v in self.state_dict().items()}
 
     def set_state(self, state):
         self.load_state_dict(state)
@@ -260,15 +260,71 @@ class RecurrentRLModule(nn.Module):
         return self.dist_cls(logits)
 
     def get_state(self):
-        return {k: v.detach().cpu() for k, v in self.state_dict().items()}
+        return {k: v.detach().to("cpu", copy=True) for k, v in self.state_dict().items()}
 
     def set_state(self, state):
         self.load_state_dict(state)
 
 
-def make_module(config: Dict, observation_space, action_space):
-    """Module factory keyed by ``config['module_class']`` (``"actor_critic"`` default, ``"sac"``);
-    ``model.use_lstm`` selects the recurrent actor-critic (PPO)."""
+class RLModuleSpec:
+    """How to build one RLModule (reference ``rllib/core/rl_module/rl_module.py`` RLModuleSpec):
+    ``module_class(observation_space, action_space, model_config)``. A custom class subclasses
+    ``RLModule`` (or implements its forward_* / get_state / set_state API)."""
+
+    def __init__(self, module_class=None, observation_space=None, action_space=None, model_config=None,
+                 model_config_dict=None, catalog_class=None, load_state_path=None):
+        self.module_class = module_class
+        self.observation_space = observation_space
+        self.action_space = action_space
+        self.model_config = dict(model_config or model_config_dict or {})
+        self.catalog_class = catalog_class
+        self.load_state_path = load_state_path
+
+    def build(self, observation_space=None, action_space=None, base_model_config=None):
+        cls = self.module_class or RLModule
+        obs = self.observation_space or observation_space
+        act = self.action_space or action_space
+        if obs is None or act is None:
+            raise ValueError("RLModuleSpec.build needs observation_space and action_space")
+        m = cls(obs, act, {**dict(base_model_config or {}), **self.model_config})
+        if self.load_state_path:
+            m.load_state_dict(torch.load(self.load_state_path, weights_only=True))
+        return m
+
+
+SingleAgentRLModuleSpec = RLModuleSpec
+
+
+class MultiRLModuleSpec:
+    """{module_id: RLModuleSpec} for multi-agent algorithms (reference MultiRLModuleSpec)."""
+
+    def __init__(self, module_specs: Optional[Dict] = None, multi_rl_module_class=None, **kw):
+        self.module_specs = dict(module_specs or {})
+        self.multi_rl_module_class = multi_rl_module_class
+
+
+MultiAgentRLModuleSpec = MultiRLModuleSpec
+
+
+def _spec_for(config: Dict, module_id):
+    spec = config.get("rl_module_spec")
+    if spec is None:
+        return None
+    if isinstance(spec, MultiRLModuleSpec):
+        spec = spec.module_specs
+    if isinstance(spec, dict):
+        spec = spec.get(module_id if module_id is not None else config.get("_module_id"),
+                        spec.get("default_policy"))
+    return spec if isinstance(spec, RLModuleSpec) else None
+
+
+def make_module(config: Dict, observation_space, action_space, module_id=None):
+    """Module factory: an ``rl_module_spec`` with a custom ``module_class`` wins (per module id in
+    multi-agent configs); else keyed by ``config['module_class']`` (``"actor_critic"`` default,
+    ``"sac"``); ``model.use_lstm`` selects the recurrent actor-critic (PPO)."""
+    spec = _spec_for(config, module_id)
+    if spec is not None and spec.module_class is not None:
+        return spec.build(observation_space, action_space, config.get("model"))
     kind = config.get("module_class", "actor_critic")
     model = config.get("model") or {}
     if kind == "sac":

@@ -308,3 +308,7 @@ class EnvRunner:
 
     def ping(self):
         return "ok"
+
+    def apply(self, func, *args, **kwargs):
+        """``func(self, *args)`` (``EnvRunnerGroup.foreach_env_runner`` with a callable)."""
+        return func(self, *args, **kwargs)

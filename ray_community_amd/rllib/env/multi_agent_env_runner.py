@@ -60,7 +60,8 @@ class MultiAgentEnvRunner:
                 obs_sp = obs_sp or env0.get_observation_space(agents[0])
                 act_sp = act_sp or env0.get_action_space(agents[0])
             self.spaces_[p] = (obs_sp, act_sp)
-        self.modules = {p: make_module(config, *self.spaces_[p]) for p in self.policy_ids if self.spaces_[p][0]}
+        self.modules = {p: make_module(config, *self.spaces_[p], module_id=p) for p in self.policy_ids
+                        if self.spaces_[p][0]}
         for m in self.modules.values():
             m.eval()
         # fixed row layout per policy: (sub-env, agent)
@@ -80,6 +81,48 @@ class MultiAgentEnvRunner:
 
     def spaces(self):
         return {p: sp for p, sp in self.spaces_.items()}
+
+    def _remap(self, fn):
+        """Re-bind agents to policies (runtime policy mutation); takes effect for the next
+        ``sample`` call, whose per-policy row layout is rebuilt here."""
+        mapping = {a: fn(a, None, worker=self) for a in self.agent_ids}
+        for a, p in mapping.items():
+            if p not in self.modules:
+                raise ValueError(f"policy_mapping_fn maps agent {a!r} to unknown policy {p!r}")
+        self.agent_policy = mapping
+        self.cfg["policy_mapping_fn"] = fn
+        self.rows = {p: [(i, a) for i in range(self.N) for a in self.agent_ids if self.agent_policy[a] == p]
+                     for p in self.modules}
+
+    def add_policy(self, policy_id, observation_space, action_space, weights=None, policy_mapping_fn=None):
+        """Add a policy's RLModule (reference ``Algorithm.add_policy`` on every env runner)."""
+        if policy_id in self.modules:
+            raise KeyError(f"policy {policy_id!r} already exists")
+        self.spaces_[policy_id] = (observation_space, action_space)
+        self.policy_ids.append(policy_id)
+        m = make_module(self.cfg, observation_space, action_space, module_id=policy_id)
+        m.eval()
+        if weights is not None:
+            m.set_state(weights)
+        self.modules[policy_id] = m
+        self._remap(policy_mapping_fn or self.cfg.get("policy_mapping_fn") or default_policy_mapping_fn)
+        return True
+
+    def remove_policy(self, policy_id, policy_mapping_fn=None):
+        if policy_id not in self.modules:
+            raise KeyError(f"unknown policy {policy_id!r}")
+        fn = policy_mapping_fn or self.cfg.get("policy_mapping_fn") or default_policy_mapping_fn
+        keep = dict(self.modules)
+        keep.pop(policy_id)
+        for a in self.agent_ids:
+            if fn(a, None, worker=self) not in keep:
+                raise ValueError(f"after removing {policy_id!r}, agent {a!r} would map to no policy: "
+                                 f"pass a new policy_mapping_fn")
+        self.modules = keep
+        self.spaces_.pop(policy_id, None)
+        self.policy_ids = [p for p in self.policy_ids if p != policy_id]
+        self._remap(fn)
+        return True
 
     def set_weights(self, states: Dict, version: int = 0):
         if version != self.weights_version:
@@ -211,3 +254,7 @@ class MultiAgentEnvRunner:
 
     def ping(self):
         return "ok"
+
+    def apply(self, func, *args, **kwargs):
+        """``func(self, *args)`` (``EnvRunnerGroup.foreach_env_runner`` with a callable)."""
+        return func(self, *args, **kwargs)
