@@ -115,6 +115,8 @@ def main():
                 "loss": round(m["loss"], 4),
                 "peak_mem_gb": round(m["mem_gb"], 2),
                 "model_tflops_per_gpu": round(m["tokens_per_s"] / world * m["flops_per_token"] / 1e12, 1),
+                # per-step compute-stream stall on gradient/parameter collectives (max over ranks)
+                "exposed_comm_ms": round(float(m.get("exposed_comm_ms", 0.0)), 3),
             },
         }
         print(json.dumps(out), flush=True)

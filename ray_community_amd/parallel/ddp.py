@@ -33,6 +33,39 @@ import torch.nn as nn
 from .flat import FlatParameters, register_grad_ready
 
 
+class CommWaitTimer:
+    """Exposed communication time: every place a data-parallel wrapper makes the compute stream
+    wait for a collective is bracketed by two timing events on that stream, so the elapsed time
+    between them is exactly the compute-stream stall on communication (what overlap did NOT
+    hide). Off unless ``enabled``; ``take_ms()`` synchronises and returns the total since the
+    last call."""
+
+    def __init__(self):
+        self.enabled = False
+        self._pairs = []
+
+    @contextlib.contextmanager
+    def region(self):
+        if not self.enabled or not torch.cuda.is_available():
+            yield
+            return
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        try:
+            yield
+        finally:
+            b.record()
+            self._pairs.append((a, b))
+
+    def take_ms(self) -> float:
+        if not self._pairs:
+            return 0.0
+        self._pairs[-1][1].synchronize()
+        total = sum(a.elapsed_time(b) for a, b in self._pairs)
+        self._pairs = []
+        return float(total)
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0, broadcast_buffers=True,
                  flat: Optional[FlatParameters] = None, average_in_optimizer: bool = True,
@@ -54,6 +87,7 @@ class DistributedDataParallel(nn.Module):
         self.reduce_dtype = reduce_dtype or self.flat.grad.dtype
         if self.world > 1 and self.reduce_dtype != self.flat.grad.dtype:
             self.flat.reduced_grad = torch.zeros(self.flat.numel, dtype=self.reduce_dtype, device=self.flat.device)
+        self.comm_timer = CommWaitTimer()
         self._norm = None
         if precompute_grad_norm and self.flat.device.type == "cuda":
             dev = self.flat.device
@@ -147,10 +181,11 @@ class DistributedDataParallel(nn.Module):
         for bi, w in enumerate(self._works):
             if w is None:
                 self._launch(bi)
-        for bi, w in enumerate(self._works):
-            if w is not None:
-                w.wait()
-            self._works[bi] = None
+        with self.comm_timer.region():
+            for bi, w in enumerate(self._works):
+                if w is not None:
+                    w.wait()
+                self._works[bi] = None
         self._pending = [len(b.params) for b in self.flat.buckets]
         self._publish_norm()
 

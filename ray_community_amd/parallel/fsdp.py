@@ -33,6 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import ops
+from .ddp import CommWaitTimer
 from .flat import ALIGN, FlatParameters, register_grad_ready
 from .optim import _use_split
 
@@ -48,6 +49,7 @@ class ShardedDataParallel(nn.Module):
         self.flat = FlatParameters(module, bucket_cap_mb=bucket_cap_mb, bucket_align=ALIGN * self.world)
         # fp32 gradient reduction: see DistributedDataParallel(reduce_dtype=...)
         self.reduce_dtype = reduce_dtype or self.flat.grad.dtype
+        self.comm_timer = CommWaitTimer()
         if self.world > 1 and self.reduce_dtype != self.flat.grad.dtype:
             self.flat.reduced_grad = torch.zeros(self.flat.numel, dtype=self.reduce_dtype, device=self.flat.device)
         self._sync = True
@@ -107,10 +109,11 @@ class ShardedDataParallel(nn.Module):
         for bi, w in enumerate(self._rs):
             if w is None:
                 self._launch_rs(bi)
-        for bi, w in enumerate(self._rs):
-            if w is not None:
-                w.wait()
-            self._rs[bi] = None
+        with self.comm_timer.region():
+            for bi, w in enumerate(self._rs):
+                if w is not None:
+                    w.wait()
+                self._rs[bi] = None
         self._pending = [len(b.params) for b in self.flat.buckets]
 
     # ------------------------------------------------------------------ weights
@@ -128,11 +131,12 @@ class ShardedDataParallel(nn.Module):
                                                    group=self.pg, async_op=True)
 
     def wait_all_gathers(self, buckets=None):
-        for bi in (range(len(self._ag)) if buckets is None else buckets):
-            w = self._ag[bi]
-            if w is not None:
-                w.wait()
-                self._ag[bi] = None
+        with self.comm_timer.region():
+            for bi in (range(len(self._ag)) if buckets is None else buckets):
+                w = self._ag[bi]
+                if w is not None:
+                    w.wait()
+                    self._ag[bi] = None
 
     def _pre_forward(self, m, args):
         bis = self._module_buckets.get(id(m))

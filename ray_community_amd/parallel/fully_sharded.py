@@ -108,6 +108,9 @@ class FullyShardedDataParallel(nn.Module):
         self.device = torch.device(device) if device is not None else params0[0].device
         self.dtype = params0[0].dtype
         self.reduce_dtype = reduce_dtype or self.dtype
+        from .ddp import CommWaitTimer
+
+        self.comm_timer = CommWaitTimer()
         if unit_modules is None:
             layers = getattr(module, "layers", None)
             unit_modules = list(layers) if isinstance(layers, nn.ModuleList) else []
@@ -220,7 +223,8 @@ class FullyShardedDataParallel(nn.Module):
             u.state = _GATHERING
             u.stale = False
         if wait and u.state == _GATHERING:
-            u.work.wait()
+            with self.comm_timer.region():
+                u.work.wait()
             u.work = None
             u.state = _READY
 
@@ -362,7 +366,8 @@ class FullyShardedDataParallel(nn.Module):
 
     def _retire(self, item):
         u, work, src, tmp = item
-        work.wait()
+        with self.comm_timer.region():
+            work.wait()
         if tmp is not None:
             u.local_grad.add_(tmp)
         _storage_resize(u.full_grad, 0)

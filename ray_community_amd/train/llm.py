@@ -107,6 +107,10 @@ def llama_train_loop_per_worker(config: dict):
     if world > 1:
         dist.barrier()
     sync()
+    timer = getattr(ddp, "comm_timer", None)
+    if timer is not None:
+        timer.take_ms()
+        timer.enabled = dev_kind == "cuda" and world > 1
     t0 = time.perf_counter()
     for i in range(steps):
         loss = step(*data[i % 2])
@@ -115,6 +119,14 @@ def llama_train_loop_per_worker(config: dict):
         dist.barrier()
     sync()
     el = time.perf_counter() - t0
+    # compute-stream stall on collectives (events around every wait: what overlap did not hide)
+    exposed = timer.take_ms() / max(steps, 1) if timer is not None and timer.enabled else 0.0
+    if timer is not None:
+        timer.enabled = False
+    ex_t = torch.tensor([exposed], dtype=torch.float64, device="cuda" if dev_kind == "cuda" else "cpu")
+    if world > 1:
+        dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)
+    exposed = float(ex_t.item())
     el_t = torch.tensor([el], device="cuda" if dev_kind == "cuda" else "cpu", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -130,6 +142,7 @@ def llama_train_loop_per_worker(config: dict):
         "flops_per_token": net.cfg.flops_per_token(seq_len),
         "parallel": net.parallel_mode,
         "grad_reduce_dtype": config.get("grad_reduce_dtype", "bf16"),
+        "exposed_comm_ms": exposed,
     }
     if dev_kind == "cuda":
         from .torch.config import group_info

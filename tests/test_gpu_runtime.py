@@ -290,3 +290,52 @@ def test_gpu_object_peer_import_between_gpus():
         assert is_cuda and last == 3.0 * (n - 1) and same
     finally:
         ray.shutdown()
+
+
+def _rccl_rank(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    res = {}
+    for dt in (torch.bfloat16, torch.float32):
+        g = torch.Generator(device="cuda").manual_seed(1234)
+        full = [torch.randn(4096, 129, device="cuda", generator=g).to(dt) for _ in range(world)]  # every rank's input
+        mine = full[rank].clone()
+        dist.all_reduce(mine)
+        ref = torch.stack([f.float() for f in full]).sum(0)
+        tol = 2e-2 if dt == torch.bfloat16 else 1e-5
+        res[f"allreduce_{dt}"] = bool(torch.allclose(mine.float(), ref, atol=tol, rtol=tol))
+        rs = torch.empty(4096 // world, 129, device="cuda", dtype=dt)
+        dist.reduce_scatter_tensor(rs, full[rank].clone())
+        res[f"reduce_scatter_{dt}"] = bool(torch.allclose(rs.float(), ref.chunk(world)[rank], atol=tol, rtol=tol))
+        ag = torch.empty(world * 4096, 129, device="cuda", dtype=dt)
+        dist.all_gather_into_tensor(ag, full[rank])
+        res[f"all_gather_{dt}"] = bool(torch.equal(ag, torch.cat(full)))
+    torch.cuda.synchronize()
+    if rank == 0:
+        import json
+
+        with open(os.path.join(out_dir, "rccl.json"), "w") as f:
+            json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL over xGMI)")
+def test_rccl_two_ranks_collectives_match_torch(tmp_path):
+    """Two processes, one GPU each, RCCL: all-reduce / reduce-scatter / all-gather of bf16 and
+    fp32 tensors against sums computed on one device."""
+    import json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_rccl_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    res = json.load(open(os.path.join(tmp_path, "rccl.json")))
+    assert res and all(res.values()), res

@@ -31,6 +31,7 @@ def _worker(rank, world, port, mode, steps, out_dir, bucket_mb):
                                             FullyShardedDataParallel, ShardedAdamW, ShardedDataParallel)
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)  # world x default threads would oversubscribe the 8 CPUs
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(100)
     toks = torch.randint(0, 1024, (2 * world, 33))
@@ -61,6 +62,15 @@ def _worker(rank, world, port, mode, steps, out_dir, bucket_mb):
 
 
 def _single(steps, world):
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)  # the ranks' thread count: same CPU reduction orders
+    try:
+        return _single_run(steps, world)
+    finally:
+        torch.set_num_threads(nt)
+
+
+def _single_run(steps, world):
     from ray_community_amd.parallel import DistributedDataParallel, FlatAdamW
 
     torch.manual_seed(100)
@@ -141,3 +151,66 @@ def test_adamw_transposed_segments_cover_flat_buffer():
     assert cur == flat.numel and blk == opt._seg_blocks and mats == 3
     for p in opt._wt_params:
         assert tuple(p._rca_wt.shape) == (p.shape[1], p.shape[0])
+
+
+@pytest.mark.parametrize("mode", ["ddp", "zero", "fsdp"])
+def test_world8_data_parallel_matches_single_process(tmp_path, mode):
+    """The driver's N=8 launch shape, rehearsed on gloo: 8 ranks (2 sequences each) follow the
+    single-process trajectory on the 16-sequence batch for DDP, ZeRO-1/2 and ZeRO-3."""
+    world, steps = 8, 3
+    mp.spawn(_worker, args=(world, _port(), mode, steps, str(tmp_path), 0.05 if mode != "fsdp" else None),
+             nprocs=world, join=True)
+    got = torch.load(os.path.join(tmp_path, f"{mode}.pt"), weights_only=True)
+    ref = _single(steps, world)
+    for k in ref:
+        # 8-way sums in another order: AdamW (lr 1e-2) turns ~1e-7 gradient noise into <= 1e-4 steps
+        assert torch.allclose(got[k], ref[k], atol=1e-4, rtol=2e-4), (k, (got[k] - ref[k]).abs().max())
+
+
+def _bf16_worker(rank, world, port, steps, out_dir):
+    import torch.distributed as dist
+
+    from ray_community_amd.models import build_llama
+    from ray_community_amd.parallel import DistributedDataParallel, FlatAdamW
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)  # world x default threads would oversubscribe the 8 CPUs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(7)
+    toks = torch.randint(0, 1024, (2 * world, 65))
+    mine = toks[2 * rank: 2 * rank + 2]
+    for reduce in ("bf16", "fp32"):  # same init, same data: only the collective's dtype differs
+        torch.manual_seed(0)
+        net = build_llama("llama3-tiny", dtype=torch.bfloat16, num_layers=2)  # bf16 weights + grads
+        wrap = DistributedDataParallel(net, bucket_cap_mb=0.05,
+                                       reduce_dtype=torch.float32 if reduce == "fp32" else None)
+        opt = FlatAdamW(wrap.flat, lr=3e-3, weight_decay=0.1, max_grad_norm=1.0)
+        losses = []
+        for _ in range(steps):
+            loss = wrap(mine[:, :-1], mine[:, 1:])
+            loss.backward()
+            wrap.finish_gradient_sync()
+            opt.step(wrap.grad_scale)
+            opt.zero_grad()
+            lt = loss.detach().float().reshape(1)
+            dist.all_reduce(lt)
+            losses.append(float(lt) / world)
+        if rank == 0:
+            torch.save(torch.tensor(losses), os.path.join(out_dir, f"bf16_{reduce}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bf16_gradient_reduction_tracks_fp32_at_world8(tmp_path):
+    """The bench's N>1 default reduces bf16 gradients in bf16 (half the xGMI bytes of torch DDP's
+    fp32 reduction under AMP). At world 8 the global-batch loss curve over 12 AdamW steps tracks the
+    fp32-reduced run: every step's loss within 0.5 % of the initial loss (measured: 0.23 %, the
+    gap growing only as the tiny model memorises its batch), the total loss drop within 1 %."""
+    world, steps = 8, 12
+    mp.spawn(_bf16_worker, args=(world, _port(), steps, str(tmp_path)), nprocs=world, join=True)
+    a = torch.load(os.path.join(tmp_path, "bf16_bf16.pt"), weights_only=True)
+    b = torch.load(os.path.join(tmp_path, "bf16_fp32.pt"), weights_only=True)
+    gap = ((a - b).abs().max() / b[0]).item()
+    assert gap < 5e-3, (gap, a.tolist(), b.tolist())
+    drop_a, drop_b = (a[0] - a[-1]).item(), (b[0] - b[-1]).item()
+    assert drop_b > 3.0 and abs(drop_a - drop_b) / drop_b < 1e-2, (drop_a, drop_b)
