@@ -515,6 +515,8 @@ class Algorithm(Trainable):
         st = {"learner": learner, "iteration": self._iteration, "multi_agent": self.multi_agent,
               "timesteps_total": self._timesteps_total, "config": self.config.to_dict(),
               "extra": self._extra_state()}
+        if not self.multi_agent and getattr(self.local_runner, "has_stateful_connectors", False):
+            st["connector_state"] = self.local_runner.get_connector_state()  # e.g. MeanStd statistics
         with open(os.path.join(checkpoint_dir, "algorithm_state.pkl"), "wb") as f:
             cloudpickle.dump(st, f)  # configs hold user callables (policy_mapping_fn, ...)
         with open(os.path.join(checkpoint_dir, "rllib_checkpoint.json"), "w") as f:
@@ -534,6 +536,10 @@ class Algorithm(Trainable):
         self._iteration = st["iteration"]
         self._timesteps_total = st["timesteps_total"]
         self._load_extra_state(st.get("extra") or {})
+        if st.get("connector_state") is not None and getattr(self.local_runner, "has_stateful_connectors", False):
+            self.local_runner.set_connector_state(st["connector_state"])
+            if self.remote_runners:
+                self._foreach_runner("set_connector_state", st["connector_state"], local_fallback=False)
         self._sync_weights()
         if getattr(self, "callbacks", None) is not None:
             self.callbacks.on_checkpoint_loaded(algorithm=self)

@@ -263,31 +263,55 @@ class EnvRunner:
 
     @torch.no_grad()
     def sample_transitions(self, num_steps: int, epsilon: float = 0.0) -> SampleBatch:
-        """Off-policy transitions (DQN): epsilon-greedy on the Q head."""
-        if len(self.env_to_module) or len(self.module_to_env):
-            raise NotImplementedError("ConnectorV2 pipelines are supported on the on-policy sampling path "
-                                      "(PPO / IMPALA / APPO); off-policy transitions take raw observations")
+        """Off-policy transitions (DQN: epsilon-greedy on the Q head; SAC: the stochastic policy
+        with probability-epsilon uniform actions). Observations go through the env-to-module
+        pipeline exactly as on the on-policy path -- ``obs`` / ``new_obs`` are module inputs (e.g.
+        stacked frames, MeanStd-normalised) and connector state advances once per env step; the
+        final observation of an ended episode is the pipeline's view of it WITHOUT committing state
+        (``_peek_obs``). Actions are stored in module space and sent through module-to-env."""
         N = self.N
         T = max(1, int(num_steps) // N)
         out = {k: [] for k in ("obs", "actions", "rewards", "new_obs", "terminateds")}
         continuous = not hasattr(self.module, "q_values")
         space = self.env.action_space
+        conn = len(self.env_to_module) > 0
+        ctx = self._ctx
         for _ in range(T):
+            if self._pending_mobs is not None:
+                mobs, self._pending_mobs = self._pending_mobs, None
+            else:
+                mobs = self._module_obs(self.obs, True)
+            o = torch.from_numpy(np.ascontiguousarray(mobs))
             if continuous:  # SAC: stochastic policy; epsilon = probability of a uniform random action
-                a = self.module.forward_exploration(torch.from_numpy(self.obs))[0].numpy().astype(np.float32)
+                a = self.module.forward_exploration(o)[0].numpy().astype(np.float32)
                 rnd = self._rng.random(N) < epsilon
                 if rnd.any():
-                    a[rnd] = self._rng.uniform(space.low, space.high, size=(int(rnd.sum()),) + space.shape)
+                    lo, hi = ((-1.0, 1.0) if self.cfg.get("normalize_actions") else (space.low, space.high))
+                    a[rnd] = self._rng.uniform(lo, hi, size=(int(rnd.sum()),) + space.shape)
             else:
-                q = self.module.q_values(torch.from_numpy(self.obs))
+                q = self.module.q_values(o)
                 a = q.argmax(-1).numpy()
                 rnd = self._rng.random(N) < epsilon
                 if rnd.any():
                     a[rnd] = self._rng.integers(0, space.n, int(rnd.sum()))
-            nobs, r, te, tr, info = self.env.step(a)
+            nobs, r, te, tr, info = self.env.step(self._env_actions(a, True))
             done = te | tr
-            nxt = np.where(done.reshape((-1,) + (1,) * (nobs.ndim - 1)), info["final_obs"], nobs)
-            out["obs"].append(self.obs)
+            if conn:
+                nxt = None
+                if done.any():  # peek the ended episodes' final observations before state moves on
+                    idx = np.nonzero(done)[0]
+                    fin = self._peek_obs(info["final_obs"][idx], idx, a, r)
+                ctx.is_first = done
+                ctx.last_actions, ctx.last_rewards = a, r
+                self._pending_mobs = self._module_obs(nobs, True)  # the next step's module input
+                nxt = np.array(self._pending_mobs, copy=True)
+                if done.any():
+                    nxt[idx] = fin
+            else:
+                nxt = np.where(done.reshape((-1,) + (1,) * (nobs.ndim - 1)), info["final_obs"], nobs)
+                ctx.is_first = done
+                ctx.last_actions, ctx.last_rewards = a, r
+            out["obs"].append(mobs)
             out["actions"].append(a)
             out["rewards"].append(r)
             out["new_obs"].append(nxt)

@@ -183,8 +183,12 @@ class SyntheticAtariVec(VectorEnv):
     H = W = 84
     STACK = 4
 
-    def __init__(self, num_envs=1, balls_per_episode=5, max_episode_steps=10000, seed=None, frameskip=1):
+    def __init__(self, num_envs=1, balls_per_episode=5, max_episode_steps=10000, seed=None, frameskip=1,
+                 frame_stack=4):
+        """``frame_stack=1``: single frames, for a FrameStacking env-to-module connector to stack
+        (the reference's Atari setup); 4 (default): the env stacks them itself."""
         self.num_envs = num_envs
+        self.STACK = int(frame_stack)
         self.observation_space = Box(0, 255, shape=(self.H, self.W, self.STACK), dtype=np.uint8)
         self.action_space = Discrete(6)
         self.balls = balls_per_episode
@@ -318,7 +322,8 @@ def make_vector_env(env, num_envs: int, env_config: Optional[dict] = None, seed=
             return PendulumVec(num_envs, seed=seed)
         if env.startswith("ALE/") or env == "SyntheticAtari-v0" or "NoFrameskip" in env:
             return SyntheticAtariVec(num_envs, seed=seed, **{k: v for k, v in cfg.items()
-                                                             if k in ("balls_per_episode", "max_episode_steps")})
+                                                             if k in ("balls_per_episode", "max_episode_steps",
+                                                                      "frame_stack")})
         raise ValueError(f"unknown env {env!r}; register it with register_env()")
     if isinstance(env, type) and issubclass(env, VectorEnv):
         return env(num_envs=num_envs, **cfg)

@@ -339,3 +339,27 @@ def test_rccl_two_ranks_collectives_match_torch(tmp_path):
     mp.spawn(_rccl_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     res = json.load(open(os.path.join(tmp_path, "rccl.json")))
     assert res and all(res.values()), res
+
+
+def test_dqn_frame_stacking_connector_gpu_learner(ray_gpu):
+    """Atari-style DQN: single 84x84 frames from the env, stacked to 4 by the FrameStacking
+    env-to-module connector on the off-policy path; the CNN Q-learner trains on the GPU."""
+    import numpy as np
+
+    from ray_community_amd.rllib import DQNConfig
+    from ray_community_amd.rllib.connectors.env_to_module import FrameStackingEnvToModule
+
+    cfg = (DQNConfig().environment("ALE/Pong-v5", env_config={"frame_stack": 1})
+           .env_runners(num_env_runners=1, num_envs_per_env_runner=4,
+                        env_to_module_connector=lambda env: [FrameStackingEnvToModule(num_frames=4)])
+           .training(train_batch_size=32, num_steps_sampled_before_learning_starts=64, target_network_update_freq=100)
+           .resources(num_gpus=1))
+    algo = cfg.build()
+    try:
+        assert algo.obs_space.shape == (84, 84, 4)
+        assert algo.learner_group.local.device.type == "cuda"
+        for _ in range(6):
+            r = algo.train()
+        assert r["timesteps_total"] >= 64 and np.isfinite(r["info"]["learner"]["default_policy"]["loss"])
+    finally:
+        algo.stop()

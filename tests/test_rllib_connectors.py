@@ -168,3 +168,73 @@ def test_use_lstm_rejected_outside_ppo(shutdown_only):
     ray.init(num_cpus=2, include_dashboard=False)
     with pytest.raises(ValueError, match="use_lstm"):
         DQNConfig().environment("CartPole-v1").training(model={"use_lstm": True}).build()
+
+
+def test_dqn_frame_stacking_connector_learns(shutdown_only):
+    """Off-policy sampling through the env-to-module pipeline: DQN with a FrameStacking connector
+    learns CartPole; the replay buffer holds module inputs (stacked frames), consecutive
+    transitions share frames, and episode ends are peeked, not committed."""
+    from ray_community_amd.rllib import DQNConfig
+    from ray_community_amd.rllib.connectors.env_to_module import FrameStackingEnvToModule
+
+    ray.init(num_cpus=2, include_dashboard=False)
+    cfg = (DQNConfig().environment("CartPole-v1")
+           .env_runners(num_envs_per_env_runner=4,
+                        env_to_module_connector=lambda env: [FrameStackingEnvToModule(num_frames=4)])
+           .training(lr=1e-3, train_batch_size=64, training_intensity=8, num_steps_sampled_before_learning_starts=500,
+                     target_network_update_freq=400, model={"fcnet_hiddens": [64, 64]})
+           .debugging(seed=1))
+    cfg.epsilon = [(0, 1.0), (4000, 0.05)]
+    algo = cfg.build()
+    try:
+        assert algo.obs_space.shape == (16,)  # 4 features x 4 frames
+        b = algo.local_runner.sample_transitions(256, 1.0)
+        assert b["obs"].shape == (256, 16) and b["new_obs"].shape == (256, 16)
+        o, n = b["obs"].reshape(64, 4, 16), b["new_obs"].reshape(64, 4, 16)
+        term = b["terminateds"].reshape(64, 4)
+        live = ~term[:-1]
+        assert np.allclose(n[:-1][live], o[1:][live])          # new_obs(t) is obs(t+1) of the same sub-env
+        assert np.allclose(n[..., :12], o[..., 4:])             # and shares 3 of its 4 frames with obs(t)
+        if term.any():                                          # a fresh episode restarts its stack
+            t, e = np.argwhere(term[:-1])[0]
+            nxt = o[t + 1, e]
+            assert np.allclose(nxt[:4], nxt[12:])
+        best = 0.0
+        for _ in range(3000):
+            r = algo.train()
+            if r["episode_reward_mean"] == r["episode_reward_mean"]:
+                best = max(best, r["episode_reward_mean"])
+            if best > 100:
+                break
+        assert best > 100, best
+    finally:
+        algo.stop()
+
+
+def test_sac_meanstd_connector_and_checkpointed_state(shutdown_only, tmp_path):
+    """SAC samples through a MeanStdFilter on its remote runner; the merged filter statistics are
+    saved with the algorithm and restored."""
+    from ray_community_amd.rllib import SACConfig
+    from ray_community_amd.rllib.connectors.env_to_module import MeanStdFilter
+
+    ray.init(num_cpus=3, include_dashboard=False)
+    cfg = (SACConfig().environment("Pendulum-v1")
+           .env_runners(num_env_runners=1, num_envs_per_env_runner=2,
+                        env_to_module_connector=lambda env: [MeanStdFilter()])
+           .training(train_batch_size=64, num_steps_sampled_before_learning_starts=64)
+           .debugging(seed=0))
+    algo = cfg.build()
+    try:
+        while algo._timesteps_total < 96:  # past the 64 warm-up steps: updates + weight/filter syncs
+            r = algo.train()
+        assert r["num_env_steps_sampled_this_iter"] > 0
+        st = algo.local_runner.get_connector_state()["000_MeanStdFilter"]
+        assert st["base"]["n"] > 0
+        path = algo.save(str(tmp_path / "ck")).checkpoint.path
+        algo2 = cfg.build()
+        algo2.restore(path)
+        st2 = algo2.local_runner.get_connector_state()["000_MeanStdFilter"]
+        assert st2["base"]["n"] == st["base"]["n"] and np.allclose(st2["base"]["mean"], st["base"]["mean"])
+        algo2.stop()
+    finally:
+        algo.stop()
