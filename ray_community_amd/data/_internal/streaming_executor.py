@@ -155,8 +155,9 @@ class TaskMapOp(PhysicalOp):
 
 class ActorPoolMapOp(PhysicalOp):
     def __init__(self, name, op, actor_opts, min_size, max_size, max_in_flight, idle_timeout_s, ordered, rm,
-                 rm_op):
+                 rm_op, pre_ops=None):
         super().__init__(name, ordered, rm, rm_op)
+        self._pre = list(pre_ops or [])  # fused upstream task-compute maps, run in the actor first
         from ...actor import ActorClass
         from .execution import _MapActor
 
@@ -174,8 +175,8 @@ class ActorPoolMapOp(PhysicalOp):
 
     def _add_actor(self):
         op = self._op
-        h = self._cls.remote(op["fn"], op.get("fn_constructor_args", ()), op.get("fn_constructor_kwargs", {}), [], [],
-                             {k: v for k, v in op.items() if k != "fn"})
+        h = self._cls.remote(op["fn"], op.get("fn_constructor_args", ()), op.get("fn_constructor_kwargs", {}),
+                             self._pre, [], {k: v for k, v in op.items() if k != "fn"})
         self.actors[self._next_id] = {"h": h, "load": 0, "ready": h.ready.remote(), "is_ready": False,
                                       "idle_since": time.monotonic()}
         self._next_id += 1

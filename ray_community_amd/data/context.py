@@ -32,6 +32,9 @@ class DataContext:
     object_store_memory_limit_fraction: float = 0.5
     op_resource_reservation_ratio: float = 0.5
     actor_pool_idle_timeout_s: float = 1.0  # an autoscaling pool drops an actor idle this long
+    # logical optimizer rules (data/_internal/logical_optimizer.py)
+    enable_operator_fusion: bool = True
+    enable_limit_pushdown: bool = True
     last_execution_stats: object = None  # ResourceManager.stats() of the most recent execution
 
     _current = None

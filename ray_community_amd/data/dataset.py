@@ -109,28 +109,34 @@ class Dataset:
                              concurrency_cap=min(caps) if caps else None)
             return SE.TaskMapOp(name, chain, opts, ordered, rm, st)
 
-        pending_tasks: List[Dict] = []
-        for op in self._ops:
-            if op["kind"] in _MAP_KINDS and op.get("compute") != "actors":
-                pending_tasks.append(op)
-                continue
-            if pending_tasks:
-                ops.append(task_op(pending_tasks))
-                pending_tasks = []
-            if op["kind"] in _MAP_KINDS:  # actor pool operator (autoscaling between min and max)
+        from ._internal import logical_optimizer as LO
+
+        logical, rules = LO.push_down_limits(self._ops, getattr(ctx, "enable_limit_pushdown", True))
+        fuse = getattr(ctx, "enable_operator_fusion", True)
+        stages = LO.plan_stages(logical, fuse)
+        if fuse and any(st[0] == "actor" and st[2] or st[0] == "task" and len(st[1]) > 1 for st in stages):
+            rules = rules + ["OperatorFusion"]
+        self._plan_info = {"logical": LO.describe([("task", [o]) if o["kind"] in _MAP_KINDS and
+                                                    o.get("compute") != "actors" else
+                                                    (("actor", o, []) if o["kind"] in _MAP_KINDS else
+                                                     (("limit", o["n"]) if o["kind"] == "limit" else ("alltoall", o)))
+                                                    for o in self._ops], _op_name),
+                           "optimized": LO.describe(stages, _op_name), "rules": rules}
+        for st in stages:
+            if st[0] == "task":
+                ops.append(task_op(st[1]))
+            elif st[0] == "actor":  # actor pool operator (autoscaling between min and max)
+                op, pre = st[1], st[2]
                 mif = op.get("max_tasks_in_flight_per_actor", 4)
-                name = _op_name(op) + "(actors)"
-                st = rm.register(name, concurrency_cap=op["max_size"] * mif)
+                name = "->".join([_op_name(o) for o in pre] + [_op_name(op)]) + "(actors)"
+                caps = [o.get("concurrency") for o in pre if isinstance(o.get("concurrency"), int)]
+                st_rm = rm.register(name, concurrency_cap=min([op["max_size"] * mif] + caps))
                 ops.append(SE.ActorPoolMapOp(name, op, op["actor_opts"], op["min_size"], op["max_size"], mif,
-                                             ctx.actor_pool_idle_timeout_s, ordered, rm, st))
-            elif op["kind"] == "limit":
-                ops.append(SE.LimitOp(op["n"], ordered, ex))
-            elif op["kind"] == "alltoall":
-                ops.append(SE.AllToAllOp(op.get("name", "AllToAll"), op["fn"], ordered))
+                                             ctx.actor_pool_idle_timeout_s, ordered, rm, st_rm, pre_ops=pre))
+            elif st[0] == "limit":
+                ops.append(SE.LimitOp(st[1], ordered, ex))
             else:
-                raise ValueError(op["kind"])
-        if pending_tasks:
-            ops.append(task_op(pending_tasks))
+                ops.append(SE.AllToAllOp(st[1].get("name", "AllToAll"), st[1]["fn"], ordered))
         ex.__init__(ops, rm, window)
         self._executor = ex
         return ex.start().iter_outputs()
@@ -539,6 +545,12 @@ class Dataset:
         ms = self._metas()
         out = (f"Dataset: {len(ms)} blocks, {sum(m['num_rows'] for m in ms)} rows, "
                f"{sum(m['size_bytes'] for m in ms) / 2**20:.2f} MiB")
+        pi = getattr(self, "_plan_info", None)
+        if pi is not None:
+            out += f"\n  Logical plan: {pi['logical']}"
+            out += f"\n  Optimized plan: {pi['optimized']}"
+            if pi["rules"]:
+                out += f"\n  Optimizer rules applied: {', '.join(pi['rules'])}"
         rm = getattr(self, "_exec_rm", None)
         if rm is not None:
             st = rm.stats()

@@ -77,6 +77,7 @@ def test_actor_pool_autoscales_up_and_down(ray8, unordered):
     ctx = unordered
     old = ctx.actor_pool_idle_timeout_s
     ctx.actor_pool_idle_timeout_s = 0.3
+    ctx.enable_operator_fusion = False  # _gate must run as its own tasks to open an idle gap
     try:
         ds = (rd.range(28, parallelism=28)
               .map_batches(_gate, batch_size=None)
@@ -94,6 +95,7 @@ def test_actor_pool_autoscales_up_and_down(ray8, unordered):
         assert "Actor pool" in ds.stats()
     finally:
         ctx.actor_pool_idle_timeout_s = old
+        ctx.enable_operator_fusion = True
 
 
 def test_concurrency_tuple_means_min_max(ray8):
@@ -125,3 +127,73 @@ def test_unordered_results_complete_and_errors_surface(ray8, unordered):
 
     with pytest.raises(Exception, match="bad block"):
         rd.range(10, parallelism=10).map_batches(boom, batch_size=None).take_all()
+
+
+@ray.remote
+class _Seen:
+    def __init__(self):
+        self.n = 0
+
+    def add(self, k):
+        self.n += k
+
+    def get(self):
+        return self.n
+
+
+def test_limit_pushdown_runs_map_on_limited_rows(ray8):
+    """ds.map(f).limit(10): the limit moves below the 1:1 map, so f sees 10 rows (one block's
+    worth), not every block the read produced; the plan is reported by stats()."""
+    seen = _Seen.remote()
+
+    def f(row):
+        ray.get(seen.add.remote(1))
+        return {"id": row["id"] * 2}
+
+    ds = rd.range(1000, parallelism=20).map(f).limit(10)
+    assert [r["id"] for r in ds.take_all()] == [2 * i for i in range(10)]
+    assert ray.get(seen.get.remote()) == 10
+    st = ds.stats()
+    assert "Logical plan: Input -> TaskMap[Map(f)] -> Limit[10]" in st
+    assert "Optimized plan: Input -> Limit[10] -> TaskMap[Map(f)]" in st and "LimitPushdown" in st
+    # a row-count-changing op (filter) is a barrier for the pushdown; consecutive limits fuse
+    ds2 = rd.range(100, parallelism=4).filter(lambda r: r["id"] % 2 == 0).limit(20).limit(7)
+    assert [r["id"] for r in ds2.take_all()] == [0, 2, 4, 6, 8, 10, 12]
+    assert "Input -> TaskMap[Filter(<lambda>)] -> Limit[7]" in ds2.stats()
+    # disabled: f runs on more rows than the limit keeps
+    ctx = DataContext.get_current()
+    ctx.enable_limit_pushdown = False
+    try:
+        seen2 = _Seen.remote()
+
+        def g(row):
+            ray.get(seen2.add.remote(1))
+            return row
+
+        assert len(rd.range(1000, parallelism=20).map(g).limit(10).take_all()) == 10
+        assert ray.get(seen2.get.remote()) > 10
+    finally:
+        ctx.enable_limit_pushdown = True
+
+
+class _AddOne:
+    def __call__(self, b):
+        b["id"] = b["id"] + 1
+        return b
+
+
+def test_operator_fusion_rules(ray8):
+    """Compatible task maps fuse into one task; a differently placed one stays separate; a CPU
+    task chain fuses into the downstream actor pool."""
+    ds = (rd.range(64, parallelism=4).map_batches(lambda b: b, batch_size=None)
+          .map(lambda r: r)
+          .map_batches(lambda b: b, batch_size=None, scheduling_strategy="SPREAD")
+          .map_batches(_AddOne, batch_size=None, concurrency=2))
+    assert sorted(r["id"] for r in ds.take_all()) == list(range(1, 65))
+    st = ds.stats()
+    assert ("Optimized plan: Input -> TaskMap[MapBatches(<lambda>)->Map(<lambda>)] -> "
+            "TaskMap[MapBatches(<lambda>)] -> ActorPoolMap[MapBatches(_AddOne)]") in st, st
+    ds2 = rd.range(64, parallelism=4).map(lambda r: r).map_batches(_AddOne, batch_size=None, concurrency=2)
+    assert sorted(r["id"] for r in ds2.take_all()) == list(range(1, 65))
+    st2 = ds2.stats()
+    assert "Optimized plan: Input -> ActorPoolMap[Map(<lambda>)->MapBatches(_AddOne)]" in st2 and "OperatorFusion" in st2
