@@ -51,8 +51,14 @@ class _TrainWorker:
     def execute(self, fn, *args, **kwargs):
         return fn(*args, **kwargs)
 
+    def idle(self) -> bool:
+        """No training thread running (a finished trial's actor can take the next one)."""
+        return self._thread is None or not self._thread.is_alive()
+
     def start(self, fn, config, context, checkpoint, dataset_shards):
         from . import session as S
+
+        self._done, self._error, self._ret = False, None, None
 
         sess = S.init_session(context, checkpoint=checkpoint, dataset_shards=dataset_shards)
         self._sess = sess

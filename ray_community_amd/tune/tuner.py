@@ -141,6 +141,26 @@ class _ClassTrainableRunner:
                 return pickle.load(f)
         return None
 
+    def reset(self, config, checkpoint_path=None, trial_info=None, log_paths=None) -> bool:
+        """``reuse_actors``: take a new trial in this actor if the trainable's ``reset_config``
+        accepts its config (reference ``Trainable.reset``)."""
+        global _CURRENT_TRIAL_INFO
+        if not self.t.reset_config(config):
+            return False
+        if log_paths:
+            _redirect_fds(*log_paths)
+        _CURRENT_TRIAL_INFO = dict(trial_info or {})
+        self.t.config = config
+        self.t._iteration = 0
+        if checkpoint_path:
+            p = os.path.join(checkpoint_path, "_state.json")
+            if os.path.exists(p):
+                with open(p) as f:
+                    self.t._iteration = json.load(f).get("iteration", 0)
+            data = self._load_dict(checkpoint_path)
+            self.t.load_checkpoint(data if data is not None else checkpoint_path)
+        return True
+
     def step(self):
         before = self.t._iteration
         r = self.t.step() or {}
@@ -331,6 +351,9 @@ class TuneController:
         self.max_conc = tune_config.max_concurrent_trials or self._default_concurrency()
         self._t0 = time.time()
         self._stop_all = False
+        # TuneConfig.reuse_actors: finished trials' actors, by resource request, for the next trial
+        self._actor_cache: Dict[tuple, List] = {}
+        self.num_actor_reuses = 0
 
     # ----------------------------------------------------------------------- helpers
     def _kind(self, t):
@@ -416,9 +439,14 @@ class TuneController:
         opts = {"num_cpus": res.pop("CPU", 0), "num_gpus": res.pop("GPU", 0), "resources": res or None,
                 "max_concurrency": 4}
         opts = {k: v for k, v in opts.items() if v is not None}
+        key = self._resource_key(trial)
         if self.kind == "function":
-            cls = ActorClass(_TrainWorker, opts)
-            trial.runner = cls.remote()
+            cached = self._take_cached(key)
+            if cached is not None:  # reuse_actors: a finished trial's idle worker actor
+                trial.runner = cached
+                self.num_actor_reuses += 1
+            else:
+                trial.runner = ActorClass(_TrainWorker, opts).remote()
             ctx = TrainContext(trial_dir=trial.local_path, trial_id=trial.trial_id,
                                trial_name=getattr(trial, "trial_name", None) or os.path.basename(trial.local_path),
                                experiment_name=os.path.basename(self.exp_dir),
@@ -439,8 +467,23 @@ class TuneController:
             cls = ActorClass(_ClassTrainableRunner, {k: v for k, v in opts.items() if k != "max_concurrency"})
             info = {"trial_id": trial.trial_id, "logdir": trial.local_path,
                     "trial_name": getattr(trial, "trial_name", None) or os.path.basename(trial.local_path)}
-            trial.runner = cls.remote(self.trainable, copy.deepcopy(trial.config), ckpt.path if ckpt else None, info,
-                                      self._log_paths(trial))
+            cached = self._take_cached(key)
+            if cached is not None:
+                # reuse_actors: the trainable accepts the new config in place (reset_config -> True)
+                try:
+                    ok = get(cached.reset.remote(copy.deepcopy(trial.config), ckpt.path if ckpt else None, info,
+                                                 self._log_paths(trial)))
+                except Exception:  # noqa
+                    ok = False
+                if ok:
+                    trial.runner = cached
+                    self.num_actor_reuses += 1
+                else:
+                    self._kill_quietly(cached)
+                    cached = None
+            if cached is None:
+                trial.runner = cls.remote(self.trainable, copy.deepcopy(trial.config), ckpt.path if ckpt else None,
+                                          info, self._log_paths(trial))
             trial.pending = trial.runner.step.remote()
         else:
             trial.thread_q = queue.Queue()
@@ -514,7 +557,49 @@ class TuneController:
                 out.append(("done", ev[1]))
         return out
 
-    def _stop_runner(self, trial: Trial, save=False):
+    # ----------------------------------------------------------------------- actor reuse
+    def _resource_key(self, trial: Trial) -> tuple:
+        res = dict(getattr(trial, "resources", None) or self.resources)
+        return tuple(sorted((k, float(v)) for k, v in res.items()))
+
+    def _take_cached(self, key):
+        lst = self._actor_cache.get(key)
+        return lst.pop() if lst else None
+
+    @staticmethod
+    def _kill_quietly(actor):
+        from .._private.worker import kill
+
+        try:
+            kill(actor)
+        except Exception:
+            pass
+
+    def _try_cache(self, trial: Trial) -> bool:
+        """``reuse_actors``: keep the actor of a trial that ended cleanly (function trainables:
+        only once its training thread has returned) for the next trial with the same resources."""
+        from .._private.worker import get
+
+        if not self.tc.reuse_actors or self.kind not in ("function", "class") or trial.runner is None:
+            return False
+        if sum(len(v) for v in self._actor_cache.values()) >= max(1, self.max_conc):
+            return False
+        if self.kind == "function":
+            try:
+                if not get(trial.runner.idle.remote(), timeout=10):
+                    return False
+            except Exception:  # noqa
+                return False
+        self._actor_cache.setdefault(self._resource_key(trial), []).append(trial.runner)
+        return True
+
+    def _clear_actor_cache(self):
+        for lst in self._actor_cache.values():
+            for a in lst:
+                self._kill_quietly(a)
+        self._actor_cache = {}
+
+    def _stop_runner(self, trial: Trial, save=False, reuse=False):
         from .._private.worker import get, kill
 
         if self.kind in ("function", "class") and trial.runner is not None:
@@ -525,6 +610,9 @@ class TuneController:
                     trial.checkpoint = _ckpt(p)
                 except Exception:
                     pass
+            if reuse and self._try_cache(trial):
+                trial.runner = None
+                return
             try:
                 kill(trial.runner)
             except Exception:
@@ -668,11 +756,11 @@ class TuneController:
                     if ev[0] == "result":
                         decision = self._on_result(t, ev[1], ev[2])
                         if decision == TrialScheduler.STOP:
-                            self._stop_runner(t)
+                            self._stop_runner(t, reuse=True)
                             self._complete(t)
                             break
                         if decision == TrialScheduler.PAUSE:
-                            self._stop_runner(t, save=True)
+                            self._stop_runner(t, save=True, reuse=True)
                             t.status = PAUSED
                             break
                         if decision == TrialScheduler.NOOP:
@@ -680,11 +768,12 @@ class TuneController:
                         if self.kind == "class" and t.status == RUNNING and t.runner is not None:
                             t.pending = t.runner.step.remote()
                     else:
-                        self._stop_runner(t)
+                        self._stop_runner(t, reuse=ev[1] is None)
                         self._complete(t, ev[1])
                         break
             self._save_state()
             self._resume_paused()
+        self._clear_actor_cache()
         self._save_state()
         return self._results()
 
