@@ -368,6 +368,113 @@ __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict
   }
 }
 
+// Staggered slice ring (RCA_GEMM_VARIANT=4): variant 3's stream, but wave w issues each group's
+// memory instructions (fragment read, LDS-DMA) after w of the group's 4 MFMAs instead of before
+// them. Measured on a probe (scripts/probes/issue_probe.hip): at one wave per SIMD a memory
+// instruction costs the issuing wave roughly the time the CU's shared memory path (TA for
+// global/LDS-DMA loads, the LDS for reads) takes to accept it, and the 4 waves of a workgroup run
+// in lockstep after each barrier, so their identical streams present every memory instruction to
+// that path 4 at a time and each waits for the ones ahead of it (~35 cycles per LDS-DMA, ~15 per
+// ds_read_b128 at 16 cycles per MFMA). One MFMA (16 cycles) between the waves' issue points is
+// about one LDS-DMA's TA time, so the staggered waves do not queue behind each other.
+// The wave index is wave-uniform (SGPR): the choice is a scalar branch around each group's memory
+// instructions, the MFMAs are shared code.
+template <bool AK, bool BKM, bool ACC>
+__global__ __launch_bounds__(NT4, 1) void gemm4t_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                        long ldb, long ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  tile_origin(blockIdx.x, M, N, m0, n0);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / 32;
+  const SliceStage<AK> sa(lda, wid, lane);
+  const SliceStage<BKM> sb(ldb, wid, lane);
+  auto dma = [&](int sl, int i) {
+    const int k0 = min(sl, ns - 1) * 32;
+    lds_char* st = smem + (sl & 3) * SST;
+    if (i < 4) sa.issue(i, A, lda, m0, k0, st, wid);
+    else sb.issue(i - 4, B, ldb, n0, k0, st + SLB, wid);
+  };
+#pragma unroll
+  for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma(sl, i);
+  wait_vmcnt<16>();
+  fence_sched();
+  __builtin_amdgcn_s_barrier();
+  fence_sched();
+  bf16x8_t xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    xa[u] = sfrag<AK>(smem, wr * 8 + u, lane);
+    xb[u] = sfrag<BKM>(smem + SLB, wc * 8 + u, lane);
+  }
+  wait_lgkm0();
+
+#define RCA_TSLICE(S, CA, CB, NA, NB)                                                  \
+  {                                                                                    \
+    fence_sched();                                                                     \
+    wait_vmcnt<8>();                                                                   \
+    fence_sched();                                                                     \
+    __builtin_amdgcn_s_barrier();                                                      \
+    fence_sched();                                                                     \
+    const lds_char* ns_ = smem + (((S) + 1) & 3) * SST;                                \
+    _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                   \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                  \
+        if (wid == j) {                                                                \
+          if (u < 8) NA[u] = sfrag<AK>(ns_, wr * 8 + u, lane);                         \
+          else NB[u - 8] = sfrag<BKM>(ns_ + SLB, wc * 8 + u - 8, lane);                \
+          if ((u & 1) == 0) dma((S) + 3, u >> 1);                                      \
+        }                                                                              \
+        fence_sched();                                                                 \
+        mfma_n<1>(acc, CA, CB, u >> 1, (u & 1) * 4 + j);                               \
+        fence_sched();                                                                 \
+      }                                                                                \
+    }                                                                                  \
+    wait_lgkm0();                                                                      \
+    fence_sched();                                                                     \
+  }
+  for (int s = 0; s < ns; s += 2) {
+    RCA_TSLICE(s, xa, xb, ya, yb)
+    RCA_TSLICE(s + 1, ya, yb, xa, xb)
+  }
+#undef RCA_TSLICE
+  wait_vmcnt<0>();
+  drain_acc(acc);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4<ACC>(C, m * ldc + n0 + wc * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+template <bool AK, bool BKM, bool ACC>
+int launch4t(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+             hipStream_t st) {
+  auto kern = gemm4t_kernel<AK, BKM, ACC>;
+  constexpr int smem = 4 * SST;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
 template <bool AK, bool BKM, bool ACC>
 int launch4s(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
              hipStream_t st) {
@@ -415,6 +522,15 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
     if (diag == 1) RCA_G4D(1)
     RCA_G4D(2)
 #undef RCA_G4D
+  }
+  if (diag == 4) {
+#define RCA_G4T(a, b, c) return launch4t<a, b, c>(A, B, C, M, N, K, lda, ldb, ldc, st)
+    if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G4T(false, false, true); RCA_G4T(false, false, false); }
+    if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G4T(false, true, true); RCA_G4T(false, true, false); }
+    if (a_kmaj && b_kmaj) { if (accumulate) RCA_G4T(true, true, true); RCA_G4T(true, true, false); }
+    if (accumulate) RCA_G4T(true, false, true);
+    RCA_G4T(true, false, false);
+#undef RCA_G4T
   }
   if (diag == 3) {
 #define RCA_G4S(a, b, c) return launch4s<a, b, c>(A, B, C, M, N, K, lda, ldb, ldc, st)

@@ -43,7 +43,51 @@ enum {
   M_BUF = 16,      // 1 buffer_load_dwordx4 ... lds per slot (instead of the global form)
   M_SPLIT = 32,    // 8 waves: waves 0-3 compute (acc[8][4]... same 64 MFMA/iter), waves 4-7 issue the memory ops
   M_PRIO = 64,     // compute waves at s_setprio 1 (with M_SPLIT)
+  M_STAG = 128,    // wave w issues its memory ops 2*w MFMAs later than wave 0 (no two waves collide)
+  M_ONE = 256,     // only memory-wave 0 issues memory ops (no contention at all)
 };
+
+// One iteration (64 MFMAs, 8 memory slots) of a wave whose memory ops are shifted by SH MFMAs.
+template <int MODE, int SH, int NJ>
+__device__ __forceinline__ void iteration(f32x4 (&acc)[8][NJ], const s16x8& fa, const s16x8& fb, s16x8 (&rd)[2],
+                                          u32x4 (&ga)[8], u32x4 (&gb)[8], const char* src, long gbase,
+                                          lds_char* smem, lds_char* stg, int it, int half, int mw, bool computer,
+                                          bool memer, unsigned lane_off, __amdgpu_buffer_rsrc_t rsrc) {
+#pragma unroll
+  for (int u = 0; u < 64; ++u) {
+    // STAG: memory-wave w's ops sit 2*w MFMAs after wave 0's; a uniform branch per op
+    const bool at = (MODE & M_STAG) ? ((u & 7) % 2 == 0 && mw == (u & 7) / 2) : ((u & 7) == SH);
+    if (at && memer) {
+      const int s = u >> 3;
+      fence();
+      const char* gp = src + gbase + (long)(s * 4 + mw) * 1024;
+      if constexpr (MODE & M_DMA)
+        __builtin_amdgcn_global_load_lds((const void*)(gp + lane_off),
+                                         (__attribute__((address_space(3))) void*)(stg + (s * 4 + mw) * 1024), 16, 0, 0);
+      if constexpr (MODE & M_BUF)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(stg + (s * 4 + mw) * 1024),
+                                                 16, (int)(gbase + (s * 4 + mw) * 1024) + (int)lane_off, 0, 0, 0);
+      if constexpr (MODE & M_GLD) {
+        u32x4& r = half ? gb[s] : ga[s];
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(lane_off), "s"(gp) : "memory");
+      }
+      if constexpr (MODE & M_DSW) {
+        const u32x4& r = half ? ga[s] : gb[s];
+        asm volatile("ds_write_b128 %0, %1" ::"v"(lds_off(stg + (s * 4 + mw) * 1024) + lane_off), "v"(r) : "memory");
+      }
+      if constexpr (MODE & M_DSR) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          asm volatile("ds_read_b128 %0, %1" : "=v"(rd[q]) : "v"(lds_off(smem + (((it + half + 1) & 3) * 32768) + (s * 2 + q) * 1024) + lane_off) : "memory");
+      }
+      fence();
+    }
+    if (computer) {
+      const int idx = u % (8 * NJ);
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[idx / NJ][idx % NJ]) : "v"(fa), "v"(fb));
+    }
+  }
+}
 
 template <int MODE>
 __global__ __launch_bounds__((MODE & M_SPLIT) ? 512 : 256, 1) void probe(const char* __restrict__ src, long region,
@@ -80,38 +124,11 @@ __global__ __launch_bounds__((MODE & M_SPLIT) ? 512 : 256, 1) void probe(const c
     for (int half = 0; half < 2; ++half) {
       const long gbase = ((long)(it + half) * 32768L) % region;
       lds_char* stg = smem + ((it + half) & 3) * 32768;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        fence();
-        if (memer) {
-          const char* gp = src + gbase + (long)(s * 4 + mw) * 1024;
-          if constexpr (MODE & M_DMA)
-            __builtin_amdgcn_global_load_lds((const void*)(gp + lane_off),
-                                             (__attribute__((address_space(3))) void*)(stg + (s * 4 + mw) * 1024), 16, 0, 0);
-          if constexpr (MODE & M_BUF)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(stg + (s * 4 + mw) * 1024),
-                                                     16, (int)(gbase + (s * 4 + mw) * 1024) + (int)lane_off, 0, 0, 0);
-          if constexpr (MODE & M_GLD) {
-            u32x4& r = half ? gb[s] : ga[s];
-            asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(lane_off), "s"(gp) : "memory");
-          }
-          if constexpr (MODE & M_DSW) {
-            const u32x4& r = half ? ga[s] : gb[s];  // the other set: loaded one iteration ago
-            asm volatile("ds_write_b128 %0, %1" ::"v"(lds_off(stg + (s * 4 + mw) * 1024) + lane_off), "v"(r) : "memory");
-          }
-          if constexpr (MODE & M_DSR) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-              asm volatile("ds_read_b128 %0, %1" : "=v"(rd[q]) : "v"(lds_off(smem + (((it + half + 1) & 3) * 32768) + (s * 2 + q) * 1024) + lane_off) : "memory");
-          }
-        }
-        fence();
-        if (computer) {
-          if constexpr ((MODE & M_PRIO) != 0) __builtin_amdgcn_s_setprio(1);
-          mfma8(acc, fa, fb, s * 8);
-        }
-        fence();
-      }
+      fence();
+      if constexpr ((MODE & M_PRIO) != 0) { if (computer) __builtin_amdgcn_s_setprio(1); }
+      const bool mem_here = memer && (!(MODE & M_ONE) || mw == 0);
+      iteration<MODE, 0>(acc, fa, fb, rd, ga, gb, src, gbase, smem, stg, it, half, mw, computer, mem_here, lane_off, rsrc);
+      fence();
       // end of iteration: keep one iteration of loads in flight, drain LDS ops, one barrier
       if (memer) {
         if constexpr ((MODE & (M_DMA | M_GLD | M_BUF)) != 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -185,21 +202,26 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(src, 0x3c, big + (1 << 20)));
   CHECK(hipMalloc(&sink, nwg * 512 * 4));
   CHECK(hipMalloc(&cyc, nwg * 4 * 8));
-  for (long region : {2L << 20, 64L << 20}) {
+  for (long region : {64L << 20}) {
     run<0>("mfma only", src, region, sink, cyc, nwg, nit);
     run<M_DSR>("+16 ds_read_b128", src, region, sink, cyc, nwg, nit);
-    run<M_DMA>("+8 glds (global)", src, region, sink, cyc, nwg, nit);
-    run<M_BUF>("+8 glds (buffer)", src, region, sink, cyc, nwg, nit);
-    run<M_GLD>("+8 global_load_dwordx4", src, region, sink, cyc, nwg, nit);
-    run<M_DSW>("+8 ds_write_b128", src, region, sink, cyc, nwg, nit);
-    run<M_GLD | M_DSW>("+8 gld +8 ds_write", src, region, sink, cyc, nwg, nit);
-    run<M_DSR | M_DMA>("+16 ds_read +8 glds", src, region, sink, cyc, nwg, nit);
-    run<M_DSR | M_BUF>("+16 ds_read +8 glds(buf)", src, region, sink, cyc, nwg, nit);
-    run<M_DSR | M_GLD | M_DSW>("+16 ds_read +8 gld +8 ds_write", src, region, sink, cyc, nwg, nit);
-    run<M_SPLIT>("8w: mfma only (4 compute)", src, region, sink, cyc, nwg, nit);
+    run<M_DSR | M_STAG>("+16 ds_read_b128 STAG", src, region, sink, cyc, nwg, nit);
+    run<M_DSR | M_ONE>("+16 ds_read_b128 wave0 only", src, region, sink, cyc, nwg, nit);
+    run<M_DMA>("+8 glds", src, region, sink, cyc, nwg, nit);
+    run<M_DMA | M_STAG>("+8 glds STAG", src, region, sink, cyc, nwg, nit);
+    run<M_DMA | M_ONE>("+8 glds wave0 only", src, region, sink, cyc, nwg, nit);
+    run<M_GLD>("+8 gld", src, region, sink, cyc, nwg, nit);
+    run<M_GLD | M_STAG>("+8 gld STAG", src, region, sink, cyc, nwg, nit);
+    run<M_DSW>("+8 ds_write", src, region, sink, cyc, nwg, nit);
+    run<M_DSW | M_STAG>("+8 ds_write STAG", src, region, sink, cyc, nwg, nit);
+    run<M_DSR | M_DMA>("+16 dsr +8 glds", src, region, sink, cyc, nwg, nit);
+    run<M_DSR | M_DMA | M_STAG>("+16 dsr +8 glds STAG", src, region, sink, cyc, nwg, nit);
+    run<M_DSR | M_GLD | M_DSW>("+16 dsr +8 gld +8 dsw", src, region, sink, cyc, nwg, nit);
+    run<M_DSR | M_GLD | M_DSW | M_STAG>("+16 dsr +8 gld +8 dsw STAG", src, region, sink, cyc, nwg, nit);
+    run<M_SPLIT>("8w: mfma only", src, region, sink, cyc, nwg, nit);
     run<M_SPLIT | M_DMA>("8w: partner +8 glds", src, region, sink, cyc, nwg, nit);
-    run<M_SPLIT | M_DMA | M_DSR>("8w: partner +8 glds +16 dsr", src, region, sink, cyc, nwg, nit);
-    run<M_SPLIT | M_DMA | M_DSR | M_PRIO>("8w: partner glds+dsr, prio", src, region, sink, cyc, nwg, nit);
+    run<M_SPLIT | M_DMA | M_STAG>("8w: partner +8 glds STAG", src, region, sink, cyc, nwg, nit);
+    run<M_SPLIT | M_DMA | M_ONE>("8w: partner0 only +8 glds", src, region, sink, cyc, nwg, nit);
   }
   printf("done\n");
   return 0;

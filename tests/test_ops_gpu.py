@@ -439,6 +439,17 @@ def test_flat_adamw_overlapped_with_forward_matches_serial():
     assert fl.grad[fl.zero_start:].abs().max().item() == 0  # zeroed behind the update
 
 
+def _gemm_excess(out, ref, absprod, K, base=None):
+    """Largest ratio |out - ref| / bound over all elements (> 1 = outside the rounding model).
+    Per element: the bf16 rounding of the stored result (<= 2^-9 relative, bound taken as 2^-8)
+    plus fp32 accumulation over K (<= K * 2^-24 * sum_k |a||b|), plus the bf16 base it was added
+    to in an accumulating epilogue; a wrong or missing K-slice moves an element by a whole
+    slice's contribution, far above this."""
+    exact = ref if base is None else ref + base
+    bound = 2.0 ** -8 * exact.abs() + K * 2.0 ** -24 * absprod + 1e-6
+    return ((out.float() - exact).abs() / bound).max().item()
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (512, 768, 320),
                                    (1024, 512, 1024)])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(False, False), (False, True), (True, True), (True, False)])
@@ -466,9 +477,31 @@ def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj, variant):
     finally:
         lib.rca_gemm_set_variant(prev)
     torch.cuda.synchronize()
-    tol = 2e-2 * ref.abs().max().item()
-    assert (out.float() - ref).abs().max().item() < tol
-    assert (acc.float() - (ref + base.float())).abs().max().item() < tol
+    absprod = af.abs() @ bf.abs()
+    assert _gemm_excess(out, ref, absprod, K) <= 1.0
+    assert _gemm_excess(acc, ref, absprod, K, base.float()) <= 1.0
+
+
+def test_gemm_check_catches_a_corrupted_k_slice():
+    """The per-element bound above is tight enough to fail a kernel that drops K-tiles: variant 91
+    (timing diagnostic: no LDS-DMA inside the K loop, so every tile after the first two re-reads
+    stale LDS) is rejected on a shape where only a few of 16 K-tiles go wrong."""
+    M, N, K = 512, 512, 1024
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    b = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    ref = a.float() @ b.float().t()
+    absprod = a.float().abs() @ b.float().abs().t()
+    lib = ops._lib.lib()
+    prev = lib.rca_gemm_set_variant(3)
+    try:
+        assert _gemm_excess(ops.gemm(a, b), ref, absprod, K) <= 1.0
+        lib.rca_gemm_set_variant(91)
+        bad = ops.gemm(a, b)
+    finally:
+        lib.rca_gemm_set_variant(prev)
+    torch.cuda.synchronize()
+    assert _gemm_excess(bad, ref, absprod, K) > 10.0
 
 
 @pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
@@ -582,9 +615,9 @@ def test_wgrad_plans_match_fp32(plan_shape, accumulate):
     base = out.float().clone()
     assert fl._wgrad_plan(g2, x2, None, None, out) in ("hand", "trB")
     fl._wgrad(g2, x2, True, out=out, accumulate=accumulate)
-    ref = g2.float().t() @ x2.float() + (base if accumulate else 0.0)
-    tol = 2e-2 * ref.abs().max().item()
-    assert (out.float() - ref).abs().max().item() < tol
+    ref = g2.float().t() @ x2.float()
+    absprod = g2.float().abs().t() @ x2.float().abs()
+    assert _gemm_excess(out, ref, absprod, T, base if accumulate else None) <= 1.0
 
 
 def test_rmsnorm_weight_grads_accumulated_into_flat_buffer_match_plain_autograd():
