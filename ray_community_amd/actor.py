@@ -204,40 +204,44 @@ class ActorMethod:
 
 
 # ``max_pending_calls`` bookkeeping, independent of the transport a call takes (direct actor
-# channel, head-routed generator methods, ray:// clients, calls parked across a restart): the first
-# return id of every call this process submitted to a limited actor, pruned lazily when counted.
-_PENDING: Dict[bytes, List[bytes]] = {}
+# channel, head-routed generator methods, ray:// clients, calls parked across a restart): a
+# per-actor count of this process's submitted, unfinished calls, incremented at submit and
+# decremented by a completion callback on the call's first return object -- whether or not the
+# caller still holds its refs, and with no RPC on the submit path (reference: the submitter's
+# per-actor pending-task count in ``ActorTaskSubmitter``).
+_INFLIGHT: Dict[bytes, int] = {}
 _PENDING_LOCK = threading.Lock()
 
 
 def _pending_calls(core, actor_id) -> int:
     with _PENDING_LOCK:
-        ids = list(_PENDING.get(actor_id, ()))
-    if not ids:
-        return 0
-    owned = getattr(core, "owned", None)
-    still, remote = [], []
-    for o in ids:
-        e = owned.objs.get(o) if owned is not None else None
-        if e is not None:
-            if e.desc is None:
-                still.append(o)
-        elif core._refs.get(o, 0) > 0:  # head-managed result the caller still references
-            remote.append(o)
-    if remote:
-        try:
-            ready = set(core.client.call("wait", remote, len(remote), 0, False, True))
-        except Exception:
-            ready = set()
-        still.extend(o for o in remote if o not in ready)
-    keep = set(still)
+        return _INFLIGHT.get(actor_id, 0)
+
+
+def _track_call(core, actor_id, rid):
     with _PENDING_LOCK:
-        cur = _PENDING.get(actor_id, [])
-        # ids appended meanwhile (other threads) were not looked at: keep them
-        _PENDING[actor_id] = [o for o in cur if o in keep or o not in ids]
-        if not _PENDING[actor_id]:
-            _PENDING.pop(actor_id, None)
-    return len(still)
+        _INFLIGHT[actor_id] = _INFLIGHT.get(actor_id, 0) + 1
+    done = [False]
+
+    def finished(*_a):
+        with _PENDING_LOCK:
+            if done[0]:
+                return
+            done[0] = True
+            n = _INFLIGHT.get(actor_id, 0) - 1
+            if n > 0:
+                _INFLIGHT[actor_id] = n
+            else:
+                _INFLIGHT.pop(actor_id, None)
+
+    owned = getattr(core, "owned", None)
+    if owned is not None and owned.get_entry(rid) is not None:
+        owned.on_ready(rid, finished)  # the entry outlives dropped refs while it has callbacks
+        return
+    try:  # head-managed result: one async wait, off the submit path
+        core.client.call_async("wait", [rid], 1, None, False, True).add_done_callback(finished)
+    except Exception:  # noqa  (no head connection: nothing will ever complete it)
+        finished()
 
 
 class ActorHandle:
@@ -316,8 +320,7 @@ class ActorHandle:
                 core._refs[r] = core._refs.get(r, 0) + 1
         core.submit_actor_task(spec, deps)
         if limit is not None and limit > 0 and rids:
-            with _PENDING_LOCK:
-                _PENDING.setdefault(self._actor_id, []).append(rids[0])
+            _track_call(core, self._actor_id, rids[0])
         if generator == "streaming":
             return ObjectRefGenerator(tid, refs[0])
         if nret == 0:

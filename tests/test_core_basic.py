@@ -362,6 +362,19 @@ def test_max_calls_retires_worker_and_max_pending_calls(shutdown_only):
         s.f.remote()
     assert ray.get(refs) == [1, 1, 1]
     assert ray.get(s.f.remote()) == 1  # room again once the queue drained
+    # calls whose refs the caller dropped still count until they finish
+    for _ in range(3):
+        s.f.remote()
+    with pytest.raises(exc.PendingCallsLimitExceeded):
+        s.f.remote()
+    deadline = _t.time() + 10
+    while True:
+        try:
+            assert ray.get(s.f.remote()) == 1
+            break
+        except exc.PendingCallsLimitExceeded:
+            assert _t.time() < deadline
+            _t.sleep(0.05)
 
 
 def test_max_pending_calls_counts_head_routed_generator_calls(shutdown_only):
