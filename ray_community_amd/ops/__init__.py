@@ -534,14 +534,40 @@ def gbdt_quantize(gh):
     return packed, inv
 
 
-def gbdt_histogram(bins, node, gh, num_nodes, out=None):
+# Fixed-point histograms keep the hessian sums to ~1e-5 of the LARGEST per-row hessian; when the
+# hessians span more than this ratio (e.g. confident logistic rows next to uncertain ones) the
+# smallest would keep fewer than ~128 quantisation steps, biasing min_child_weight checks and
+# leaf values, so "auto" switches to the exact (fp64-accumulated) kernel.
+GBDT_EXACT_HESS_RATIO = 2.0 ** 10
+
+
+def _gbdt_needs_exact(gh) -> bool:
+    hit = _GBDT_Q.get(("exact", gh.device))
+    if hit is not None and hit[0] is gh and hit[2] == gh._version:
+        return hit[1]
+    h = gh[:, 1]
+    pos = h[h > 0]
+    need = bool(pos.numel() and (pos.max() / pos.min()).item() > GBDT_EXACT_HESS_RATIO)
+    _GBDT_Q[("exact", gh.device)] = (gh, need, gh._version)
+    return need
+
+
+def gbdt_histogram(bins, node, gh, num_nodes, out=None, precision: str = "auto"):
     """Per-node gradient histograms for histogram GBDT (``train/gbdt``).
 
     bins: uint8 [F, ld] feature-major quantised matrix (bin 255 = missing), node: int32 [ld] node
     slot of every row (-1 = skip), gh: float32 [ld, C] (grad, hess[, count: 1 per row]).
-    Returns float32 [num_nodes, F, 256, C]. GPU: ``gbdt_hist_kernel`` over the fixed-point packed
-    (grad, hess) of :func:`gbdt_quantize` (relative error ~1e-5 of the largest |grad| / hess per
-    row; the count is exact), ld % 4 == 0; CPU: one fp32 ``index_add_``."""
+    Returns float32 [num_nodes, F, 256, C].
+
+    ``precision``: "fixed" -- GPU ``gbdt_hist_kernel`` over the fixed-point packed (grad, hess) of
+    :func:`gbdt_quantize` (error ~1e-5 of the largest |grad| / hess per row; the count is exact;
+    CPU: one fp32 ``index_add_``); "exact" -- fp64 accumulation rounded to fp32 once, the SAME
+    numbers on GPU (``gbdt_hist_exact_kernel``, fp64 LDS atomics) and CPU (fp64 ``index_add_``)
+    up to the last bit of the fp64 sum, for parity checks; "auto" (default) -- "fixed" unless the
+    positive hessians span more than ``GBDT_EXACT_HESS_RATIO``. ld % 4 == 0 on GPU."""
+    if precision not in ("auto", "fixed", "exact"):
+        raise ValueError(f"precision must be auto|fixed|exact, got {precision!r}")
+    exact = precision == "exact" or (precision == "auto" and bins.is_cuda and _gbdt_needs_exact(gh))
     F, ld = bins.shape
     C = gh.shape[1]
     if out is None:  # the GPU path writes every entry
@@ -554,6 +580,13 @@ def gbdt_histogram(bins, node, gh, num_nodes, out=None):
         assert bins.is_contiguous() and node.is_contiguous() and gh.is_contiguous()
         assert ld % 4 == 0 and node.numel() == ld and gh.shape[0] == ld and C in (2, 3)
         assert out.shape == (num_nodes, F, 256, C) and out.is_contiguous()
+        if exact:
+            nbytes = int(lib().rca_gbdt_hist_exact_workspace(F, ld, int(num_nodes), C))
+            work = _workspace(bins.device, "gbdt_hist_exact", (nbytes + 3) // 4)
+            check(lib().rca_gbdt_hist_exact(bins.data_ptr(), node.data_ptr(), gh.data_ptr(), out.data_ptr(),
+                                            work.data_ptr(), F, ld, int(num_nodes), C, stream_ptr(bins.device)),
+                  "gbdt_hist_exact")
+            return out
         packed, inv = gbdt_quantize(gh)
         nbytes = int(lib().rca_gbdt_hist_workspace(F, ld, int(num_nodes), C))
         work = _workspace(bins.device, "gbdt_hist", (nbytes + 3) // 4)
@@ -567,6 +600,12 @@ def gbdt_histogram(bins, node, gh, num_nodes, out=None):
         return out
     nd = node[rows].long()
     idx = (nd[None, :] * F + torch.arange(F, device=bins.device)[:, None]) * 256 + bins[:, rows].long()
+    if exact:
+        vals = gh[rows].double().unsqueeze(0).expand(F, -1, -1)
+        acc = torch.zeros(out.numel() // C, C, dtype=torch.float64, device=bins.device)
+        acc.index_add_(0, idx.reshape(-1), vals.reshape(-1, C))
+        out.view(-1, C).copy_(acc)
+        return out
     vals = gh[rows].unsqueeze(0).expand(F, -1, -1)
     out.view(-1, C).index_add_(0, idx.reshape(-1), vals.reshape(-1, C))
     return out

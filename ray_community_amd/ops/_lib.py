@@ -59,6 +59,9 @@ _SIGS = {
     "rca_bn_apply": (c_int, [c_void_p] * 4 + [c_ll, c_int, c_int, c_void_p]),
     "rca_bn_bwd": (c_int, [c_void_p] * 11 + [c_ll, c_int, c_int, c_void_p]),
     "rca_gbdt_hist_workspace": (c_ll, [c_int, c_ll, c_int, c_int]),
+    "rca_gbdt_hist_exact_workspace": (c_ll, [c_int, c_ll, c_int, c_int]),
+    "rca_gbdt_hist_exact": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_int, c_int,
+                                    c_void_p]),
     "rca_gbdt_hist": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_int, c_int,
                               c_void_p]),
     "rca_image_normalize": (c_int, [c_void_p, c_void_p, c_ll, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,

@@ -151,8 +151,81 @@ __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const float* __re
   hist[((long long)(lo + sl) * F + f0 + f) * (kBins * C) + bc] = acc;
 }
 
+// Exact mode (parity checks; also chosen automatically when the hessians span too many binades
+// for the fixed-point scales -- ops.gbdt_histogram): the float (grad, hess) are added in fp64 LDS
+// atomics (ds_add_f64), partials and the fixed-order reduction stay fp64 and the result is rounded
+// to fp32 once, so it equals an fp64 accumulation on the CPU rounded to fp32 (the CPU exact path)
+// up to the last bit of the fp64 sum.
+template <bool CNT, int FGT>
+__global__ __launch_bounds__(1024) void gbdt_hist_exact_kernel(const unsigned char* __restrict__ bins,
+                                                               const int* __restrict__ node,
+                                                               const float* __restrict__ gh,
+                                                               double* __restrict__ part, int F, long long ld, int lo,
+                                                               int cnt, int FG, long long rows_per_block) {
+  extern __shared__ double ld64[];
+  constexpr int C = CNT ? 3 : 2;
+  const int f0 = blockIdx.x * FG;
+  const int nf = min(FG, F - f0);
+  const int ent = cnt * FG * kBins;
+  for (int i = threadIdx.x; i < ent * C; i += blockDim.x) ld64[i] = 0.0;
+  __syncthreads();
+  const long long r_begin = (long long)blockIdx.y * rows_per_block;
+  const long long r_end = min(ld, r_begin + rows_per_block);
+  const unsigned char* bcol = bins + (long long)f0 * ld;
+  for (long long r = r_begin + 4 * (long long)threadIdx.x; r < r_end; r += 4 * (long long)blockDim.x) {
+    const int4 nd = *reinterpret_cast<const int4*>(node + r);
+    unsigned b4[FGT];
+#pragma unroll
+    for (int f = 0; f < FGT; ++f) b4[f] = f < nf ? *reinterpret_cast<const unsigned*>(bcol + (long long)f * ld + r) : 0u;
+    const int s[4] = {nd.x - lo, nd.y - lo, nd.z - lo, nd.w - lo};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if ((unsigned)s[k] >= (unsigned)cnt) continue;
+      const float* row = gh + (r + k) * C;
+      const double g = row[0], h = row[1];
+#pragma unroll
+      for (int f = 0; f < FGT; ++f) {
+        if (f >= nf) break;
+        const int e = (s[k] * FG + f) * kBins + ((b4[f] >> (8 * k)) & 0xff);
+        atomicAdd(ld64 + e * C, g);
+        atomicAdd(ld64 + e * C + 1, h);
+        if (CNT) atomicAdd(ld64 + e * C + 2, (double)row[2]);
+      }
+    }
+  }
+  __syncthreads();
+  double* out = part + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (long long)ent * C;
+  for (int i = threadIdx.x; i < ent * C; i += blockDim.x) out[i] = ld64[i];
+}
+
+__global__ __launch_bounds__(256) void gbdt_hist_exact_reduce_kernel(const double* __restrict__ part,
+                                                                     float* __restrict__ hist, int F, int gx, int gy,
+                                                                     int lo, int cnt, int FG, int C) {
+  const int total = cnt * FG * kBins * C;
+  const int bx = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int per_node = FG * kBins * C;
+  const int sl = i / per_node;
+  const int rem = i - sl * per_node;
+  const int f = rem / (kBins * C);
+  const int f0 = bx * FG;
+  if (f0 + f >= F) return;
+  double acc = 0.0;
+  const double* p = part + (long long)bx * total + i;
+  const long long stride = (long long)gx * total;
+  for (int y = 0; y < gy; ++y) acc += p[(long long)y * stride];
+  const int bc = rem - f * (kBins * C);
+  hist[((long long)(lo + sl) * F + f0 + f) * (kBins * C) + bc] = (float)acc;
+}
+
 namespace plan {
 constexpr int kLdsBytes = 64 * 1024;
+// exact mode: one fp64 per (entry, channel)
+inline int max_nodes_exact(int C) { return kLdsBytes / (kBins * C * (int)sizeof(double)); }
+inline int feat_group_exact(int F, int cnt, int C) {
+  return max(1, min(min(F, 4), kLdsBytes / (cnt * kBins * C * (int)sizeof(double))));
+}
 inline int max_nodes(int C) { return kLdsBytes / (kBins * C * (int)sizeof(float)); }
 inline int feat_group(int F, int cnt, int C) {
   return max(1, min(min(F, 4), kLdsBytes / (cnt * kBins * C * (int)sizeof(float))));
@@ -210,6 +283,50 @@ RCA_API int rca_gbdt_hist(const unsigned char* bins, const int* node, const unsi
     dim3 rgrid((ent * C + 255) / 256, gx);
     hipLaunchKernelGGL(gbdt_hist_reduce_kernel, rgrid, dim3(256), 0, stream, work, hist, F, gx, (int)gy, lo, cnt,
                        FG, C);
+  }
+  return (int)hipGetLastError();
+}
+
+// Exact-mode workspace bytes and launch (fp64 LDS accumulation, see gbdt_hist_exact_kernel).
+RCA_API long long rca_gbdt_hist_exact_workspace(int F, long long ld, int L, int C) {
+  long long best = 0;
+  for (int lo = 0; lo < L; lo += plan::max_nodes_exact(C)) {
+    const int cnt = min(plan::max_nodes_exact(C), L - lo);
+    const int FG = plan::feat_group_exact(F, cnt, C);
+    const int gx = (F + FG - 1) / FG;
+    const long long gy = plan::row_blocks(ld, gx);
+    best = max(best, gy * gx * (long long)cnt * FG * kBins * C * (long long)sizeof(double));
+  }
+  return best;
+}
+
+// gh: float [ld, C] (grad, hess[, count]) as is (no quantisation); hist float [L, F, 256, C].
+RCA_API int rca_gbdt_hist_exact(const unsigned char* bins, const int* node, const float* gh, float* hist,
+                                double* work, int F, long long ld, int L, int C, hipStream_t stream) {
+  if (F <= 0 || L <= 0 || ld <= 0) return 0;
+  if ((ld & 3) != 0 || (C != 2 && C != 3)) return -1;
+  for (int lo = 0; lo < L; lo += plan::max_nodes_exact(C)) {
+    const int cnt = min(plan::max_nodes_exact(C), L - lo);
+    const int FG = plan::feat_group_exact(F, cnt, C);
+    const int gx = (F + FG - 1) / FG;
+    const long long gy = plan::row_blocks(ld, gx);
+    long long rpb = (ld + gy - 1) / gy;
+    rpb = (rpb + 3) & ~3LL;
+    const int ent = cnt * FG * kBins;
+    const size_t lds = (size_t)ent * C * sizeof(double);
+    dim3 grid(gx, (unsigned)gy);
+#define RCA_GBDT_EX(CC, FF)                                                                                      \
+  hipLaunchKernelGGL((gbdt_hist_exact_kernel<CC, FF>), grid, dim3(1024), lds, stream, bins, node, gh, work, F, ld, \
+                     lo, cnt, FG, rpb)
+    if (C == 2) {
+      if (FG == 1) RCA_GBDT_EX(false, 1); else if (FG == 2) RCA_GBDT_EX(false, 2); else RCA_GBDT_EX(false, 4);
+    } else {
+      if (FG == 1) RCA_GBDT_EX(true, 1); else if (FG == 2) RCA_GBDT_EX(true, 2); else RCA_GBDT_EX(true, 4);
+    }
+#undef RCA_GBDT_EX
+    dim3 rgrid((ent * C + 255) / 256, gx);
+    hipLaunchKernelGGL(gbdt_hist_exact_reduce_kernel, rgrid, dim3(256), 0, stream, work, hist, F, gx, (int)gy, lo,
+                       cnt, FG, C);
   }
   return (int)hipGetLastError();
 }

@@ -97,7 +97,7 @@ _ALIASES = {
 _XGB_DEFAULTS = dict(eta=0.3, max_depth=6, grow_policy="depthwise", max_leaves=0, **{"lambda": 1.0}, alpha=0.0,
                      gamma=0.0, min_child_weight=1.0, min_data_in_leaf=0, subsample=1.0, colsample_bytree=1.0,
                      max_bin=256, seed=0, objective="reg:squarederror", num_class=1, base_score=None,
-                     eval_metric=None)
+                     eval_metric=None, hist_precision="auto")
 _LGB_DEFAULTS = dict(_XGB_DEFAULTS, eta=0.1, max_depth=-1, grow_policy="lossguide", max_leaves=31,
                      **{"lambda": 0.0}, min_child_weight=1e-3, min_data_in_leaf=20, max_bin=255,
                      objective="regression")
@@ -565,7 +565,7 @@ class _Grower:
         from ...ops import gbdt_histogram
 
         node = torch.where(pos >= 0, slots[pos.clamp_min(0)], torch.full_like(pos, -1)).to(torch.int32)
-        h = gbdt_histogram(self.bins, node.contiguous(), gh, L)
+        h = gbdt_histogram(self.bins, node.contiguous(), gh, L, precision=str(self.p.get("hist_precision", "auto")))
         return allreduce_sum(h)
 
     def best_splits(self, H: torch.Tensor, fmask: torch.Tensor):

@@ -417,3 +417,74 @@ def test_column_sampling_levels_and_lightgbm_bagging_freq():
     d = train({"objective": "regression", "bagging_fraction": 0.5, "bagging_freq": 1}, DMatrix(X, y), 3,
               flavor="lightgbm")
     assert d.to_dict()["trees"] != c.to_dict()["trees"]
+
+
+def test_histogram_exact_precision_cpu():
+    """precision="exact" on the CPU: fp64 accumulation rounded once (the GPU exact kernel's
+    numbers); "auto" on the CPU keeps the plain fp32 path."""
+    rng = np.random.default_rng(2)
+    F, n, L = 4, 4001, 3
+    ld = (n + 3) // 4 * 4
+    bins = torch.as_tensor(rng.integers(0, 256, size=(F, ld)), dtype=torch.uint8)
+    node = torch.as_tensor(rng.integers(-1, L, size=ld), dtype=torch.int32)
+    gh = torch.as_tensor(rng.normal(size=(ld, 2)) * 10.0 ** rng.integers(-6, 3, size=(ld, 2)), dtype=torch.float32)
+    ex = ops.gbdt_histogram(bins, node, gh, L, precision="exact")
+    ref = torch.zeros(L * F * 256, 2, dtype=torch.float64)
+    keep = node >= 0
+    idx = ((node[keep].long()[None] * F + torch.arange(F)[:, None]) * 256 + bins[:, keep].long()).reshape(-1)
+    ref.index_add_(0, idx, gh[keep].double().unsqueeze(0).expand(F, -1, -1).reshape(-1, 2))
+    assert torch.equal(ex.view(-1, 2), ref.float())
+    with pytest.raises(ValueError):
+        ops.gbdt_histogram(bins, node, gh, L, precision="bf16")
+
+
+def _heavy_tailed_logistic(n, F, L, seed=7):
+    """Logistic-loss statistics with confident rows: hessians p(1-p) spanning ~6 binades."""
+    rng = np.random.default_rng(seed)
+    ld = (n + 3) // 4 * 4
+    bins = torch.full((F, ld), MISSING_BIN, dtype=torch.uint8)
+    bins[:, :n] = torch.as_tensor(rng.integers(0, 64, size=(F, n)), dtype=torch.uint8)
+    node = torch.full((ld,), -1, dtype=torch.int32)
+    node[:n] = torch.as_tensor(rng.integers(0, L, size=n), dtype=torch.int32)
+    margin = rng.normal(scale=6.0, size=n)
+    p = 1.0 / (1.0 + np.exp(-margin))
+    y = rng.random(n) < p
+    gh = torch.zeros(ld, 2)
+    gh[:n, 0] = torch.as_tensor(p - y, dtype=torch.float32)
+    gh[:n, 1] = torch.as_tensor(p * (1 - p), dtype=torch.float32)
+    return bins, node, gh
+
+
+@pytest.mark.gpu
+def test_gbdt_exact_histograms_gpu_match_cpu_on_heavy_tailed_hessians():
+    """Exact mode: GPU histograms equal the CPU fp64 ones (to the last fp32 ulp). With hessians
+    spanning ~1e-6..0.25 the fixed-point kernel misses the small hessian sums by far more, which
+    is why "auto" switches to the exact kernel on such data."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    bins, node, gh = _heavy_tailed_logistic(200_003, 5, 6)
+    ref = ops.gbdt_histogram(bins, node, gh, 6, precision="exact")
+    got = ops.gbdt_histogram(bins.cuda(), node.cuda(), gh.cuda(), 6, precision="exact").cpu()
+    torch.testing.assert_close(got, ref, rtol=2e-7, atol=1e-12)
+    fixed = ops.gbdt_histogram(bins.cuda(), node.cuda(), gh.cuda(), 6, precision="fixed").cpu()
+    small = ref[..., 1] > 0
+    rel_fixed = ((fixed[..., 1] - ref[..., 1]).abs() / ref[..., 1].clamp_min(1e-30))[small].max().item()
+    assert rel_fixed > 1e-3  # the bias the exact mode removes
+    assert ops._gbdt_needs_exact(gh.cuda())
+    auto = ops.gbdt_histogram(bins.cuda(), node.cuda(), gh.cuda(), 6).cpu()
+    torch.testing.assert_close(auto, ref, rtol=2e-7, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gbdt_exact_mode_grows_the_same_trees_on_gpu_and_cpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    X, y = _reg(20_000, f=8, nan=0.02)
+    params = {"max_depth": 5, "hist_precision": "exact"}
+    bc = train(params, DMatrix(X, y), 8)
+    bg = train(params, DMatrix(X, y, device="cuda"), 8)
+    for tc, tg in zip(bc.trees, bg.trees):
+        assert list(tc[0].feature) == list(tg[0].feature)
+    pc = bc.predict(torch.as_tensor(X))
+    pg = bg.predict(torch.as_tensor(X, device="cuda")).cpu()
+    torch.testing.assert_close(pg, pc, rtol=1e-5, atol=1e-5)
