@@ -36,9 +36,11 @@ def main():
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
-    ap.add_argument("--parallel", default="ddp", choices=["ddp", "zero", "fsdp", "auto"],
+    ap.add_argument("--parallel", default="auto", choices=["ddp", "zero", "fsdp", "auto"],
                     help="ddp (replicated AdamW after bucketed all-reduce) | zero (ZeRO-1/2 sharded AdamW) | "
-                         "fsdp (ZeRO-3: parameters sharded, per-block all-gather) | auto (zero for N>1)")
+                         "fsdp (ZeRO-3: parameters sharded, per-block all-gather) | auto (default: ddp at N=1, "
+                         "zero for N>1 -- data-parallel training with the AdamW pass, 10 %% of a 1-GPU step, "
+                         "sharded 1/N; world-2/world-8 parity with single-process training: tests/test_parallel.py)")
     ap.add_argument("--grad-reduce-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="dtype of the gradient collective (fp32 = torch DDP-under-AMP parity)")
     ap.add_argument("--overlap-optimizer", action="store_true",

@@ -41,7 +41,9 @@ def test_bench_self_launch_two_workers_cpu(tmp_path):
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
-    assert rec["config"]["parallel_mode"] == "ddp" and rec["config"]["launch"] == "TorchTrainer worker actors"
+    # the default --parallel auto: ZeRO-sharded AdamW for N > 1
+    assert rec["config"]["parallel_mode"] == "zero" and rec["config"]["launch"] == "TorchTrainer worker actors"
+    assert rec["extra"]["exposed_comm_ms"] == 0.0  # events are only recorded on GPUs
     assert rec["config"]["global_batch"] == 4
 
 
