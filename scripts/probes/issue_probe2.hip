@@ -73,10 +73,10 @@ __global__ __launch_bounds__(64 * NW, 1) void probe2(const char* __restrict__ sr
       }
       if constexpr (OP == OP_GLD_V) {
         const char* p = gp + lane_off;
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(g[s]) : "v"(p) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(g[s]) : "v"(p) : "memory");
       }
       if constexpr (OP == OP_GLD_S) {
-        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(g[s]) : "v"(lane_off), "s"(gp) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(g[s]) : "v"(lane_off), "s"(gp) : "memory");
       }
       if constexpr (OP == OP_DSW) {
         asm volatile("ds_write_b128 %0, %1" ::"v"(lds_off(lp) + lane_off), "v"(g[s]) : "memory");
@@ -108,7 +108,8 @@ __global__ __launch_bounds__(64 * NW, 1) void probe2(const char* __restrict__ sr
   if constexpr (OP == OP_DSR) sm += (float)rd0[1] + (float)rd1[2];
   if constexpr (OP >= OP_GLD_V) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sm += (float)g[e][0];
+    for (int e = 0; e < 8; ++e) sm += (float)(g[e][0] + g[e][1] + g[e][2] + g[e][3]);  // every dword live:
+    // an asm load's destination is written asynchronously, so no part of it may be reused early
   }
   sink[blockIdx.x * blockDim.x + tid] = sm;
   if (lane == 0) cyc[blockIdx.x * NW + wid] = t1 - t0;
