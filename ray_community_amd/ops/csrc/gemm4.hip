@@ -291,7 +291,24 @@ __device__ __forceinline__ bf16x8_t sfrag(const lds_char* t, int ob, int lane) {
   }
 }
 
-template <bool AK, bool BKM, bool ACC>
+// lgkmcnt(n) for a value that is a constant once the surrounding loop is unrolled (the switch
+// folds away); n >= 16 needs no wait (the counter holds at most 15 pending LDS reads here).
+__device__ __forceinline__ void wait_lgkm_upto(int n) {
+  switch (n) {
+#define RCA_W(k) case k: asm volatile("s_waitcnt lgkmcnt(" #k ")" ::: "memory"); break;
+    RCA_W(0) RCA_W(1) RCA_W(2) RCA_W(3) RCA_W(4) RCA_W(5) RCA_W(6) RCA_W(7)
+    RCA_W(8) RCA_W(9) RCA_W(10) RCA_W(11) RCA_W(12) RCA_W(13) RCA_W(14) RCA_W(15)
+#undef RCA_W
+    default: break;
+  }
+}
+
+// PW (variant 5): no lgkmcnt(0) drain at the end of a slice. The next slice's fragments are read
+// B first, then A, and before group u each wave waits only until the reads that group's MFMAs
+// consume have landed (counted: the reads of earlier groups of this slice are younger, so they may
+// stay in flight). Variant 3 drained every fragment read and then met the barrier with the matrix
+// pipe idle for the LDS latency once per slice.
+template <bool AK, bool BKM, bool ACC, bool PW = false>
 __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         bf16_t* __restrict__ C, int M, int N, int K, long lda,
                                                         long ldb, long ldc) {
@@ -334,6 +351,8 @@ __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict
   }
   wait_lgkm0();
 
+  // LDS reads per fragment (k-outer images take two ds_read_b64_tr_b16)
+  constexpr int RA = AK ? 2 : 1, RB = BKM ? 2 : 1, RTOT = 8 * RA + 8 * RB;
   // one slice: cur = F(s) (in registers), nxt <- F(s+1)
 #define RCA_SLICE(S, CA, CB, NA, NB)                                                   \
   {                                                                                    \
@@ -344,13 +363,24 @@ __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict
     fence_sched();                                                                     \
     const lds_char* ns_ = smem + (((S) + 1) & 3) * SST;                                \
     _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                   \
-      if (u < 8) NA[u] = sfrag<AK>(ns_, wr * 8 + u, lane);                             \
-      else NB[u - 8] = sfrag<BKM>(ns_ + SLB, wc * 8 + u - 8, lane);                    \
+      if constexpr (PW) {                                                              \
+        /* group u's MFMAs use all of B and A rows 0..u>>1 of the previous slice's */  \
+        /* reads (issued B0..B7, A0..A7); this slice's u earlier reads are younger */  \
+        const int need = 8 * RB + ((u >> 1) + 1) * RA;                                 \
+        const int younger = (u < 8 ? u : 8) * RB + (u > 8 ? u - 8 : 0) * RA;           \
+        wait_lgkm_upto(RTOT - need + younger);                                         \
+        fence_sched();                                                                 \
+        if (u < 8) NB[u] = sfrag<BKM>(ns_ + SLB, wc * 8 + u, lane);                    \
+        else NA[u - 8] = sfrag<AK>(ns_, wr * 8 + u - 8, lane);                         \
+      } else {                                                                         \
+        if (u < 8) NA[u] = sfrag<AK>(ns_, wr * 8 + u, lane);                           \
+        else NB[u - 8] = sfrag<BKM>(ns_ + SLB, wc * 8 + u - 8, lane);                  \
+      }                                                                                \
       if ((u & 1) == 0) dma((S) + 3, u >> 1);                                          \
       mfma_n<4>(acc, CA, CB, u >> 1, (u & 1) * 4);                                     \
       fence_sched();                                                                   \
     }                                                                                  \
-    wait_lgkm0();                                                                      \
+    if constexpr (!PW) wait_lgkm0();                                                   \
     fence_sched();                                                                     \
   }
   for (int s = 0; s < ns; s += 2) {
@@ -358,98 +388,7 @@ __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict
     RCA_SLICE(s + 1, ya, yb, xa, xb)
   }
 #undef RCA_SLICE
-  wait_vmcnt<0>();
-  drain_acc(acc);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const long m = m0 + wr * 128 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) store4<ACC>(C, m * ldc + n0 + wc * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
-  }
-}
-
-// Staggered slice ring (RCA_GEMM_VARIANT=4): variant 3's stream, but wave w issues each group's
-// memory instructions (fragment read, LDS-DMA) after w of the group's 4 MFMAs instead of before
-// them. Measured on a probe (scripts/probes/issue_probe.hip): at one wave per SIMD a memory
-// instruction costs the issuing wave roughly the time the CU's shared memory path (TA for
-// global/LDS-DMA loads, the LDS for reads) takes to accept it, and the 4 waves of a workgroup run
-// in lockstep after each barrier, so their identical streams present every memory instruction to
-// that path 4 at a time and each waits for the ones ahead of it (~35 cycles per LDS-DMA, ~15 per
-// ds_read_b128 at 16 cycles per MFMA). One MFMA (16 cycles) between the waves' issue points is
-// about one LDS-DMA's TA time, so the staggered waves do not queue behind each other.
-// The wave index is wave-uniform (SGPR): the choice is a scalar branch around each group's memory
-// instructions, the MFMAs are shared code.
-template <bool AK, bool BKM, bool ACC>
-__global__ __launch_bounds__(NT4, 1) void gemm4t_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                        bf16_t* __restrict__ C, int M, int N, int K, long lda,
-                                                        long ldb, long ldc) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char* smem = (lds_char*)smem_raw;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-  int m0, n0;
-  tile_origin(blockIdx.x, M, N, m0, n0);
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int ns = K / 32;
-  const SliceStage<AK> sa(lda, wid, lane);
-  const SliceStage<BKM> sb(ldb, wid, lane);
-  auto dma = [&](int sl, int i) {
-    const int k0 = min(sl, ns - 1) * 32;
-    lds_char* st = smem + (sl & 3) * SST;
-    if (i < 4) sa.issue(i, A, lda, m0, k0, st, wid);
-    else sb.issue(i - 4, B, ldb, n0, k0, st + SLB, wid);
-  };
-#pragma unroll
-  for (int sl = 0; sl < 3; ++sl)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dma(sl, i);
-  wait_vmcnt<16>();
-  fence_sched();
-  __builtin_amdgcn_s_barrier();
-  fence_sched();
-  bf16x8_t xa[8], xb[8], ya[8], yb[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    xa[u] = sfrag<AK>(smem, wr * 8 + u, lane);
-    xb[u] = sfrag<BKM>(smem + SLB, wc * 8 + u, lane);
-  }
   wait_lgkm0();
-
-#define RCA_TSLICE(S, CA, CB, NA, NB)                                                  \
-  {                                                                                    \
-    fence_sched();                                                                     \
-    wait_vmcnt<8>();                                                                   \
-    fence_sched();                                                                     \
-    __builtin_amdgcn_s_barrier();                                                      \
-    fence_sched();                                                                     \
-    const lds_char* ns_ = smem + (((S) + 1) & 3) * SST;                                \
-    _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                   \
-      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                  \
-        if (wid == j) {                                                                \
-          if (u < 8) NA[u] = sfrag<AK>(ns_, wr * 8 + u, lane);                         \
-          else NB[u - 8] = sfrag<BKM>(ns_ + SLB, wc * 8 + u - 8, lane);                \
-          if ((u & 1) == 0) dma((S) + 3, u >> 1);                                      \
-        }                                                                              \
-        fence_sched();                                                                 \
-        mfma_n<1>(acc, CA, CB, u >> 1, (u & 1) * 4 + j);                               \
-        fence_sched();                                                                 \
-      }                                                                                \
-    }                                                                                  \
-    wait_lgkm0();                                                                      \
-    fence_sched();                                                                     \
-  }
-  for (int s = 0; s < ns; s += 2) {
-    RCA_TSLICE(s, xa, xb, ya, yb)
-    RCA_TSLICE(s + 1, ya, yb, xa, xb)
-  }
-#undef RCA_TSLICE
   wait_vmcnt<0>();
   drain_acc(acc);
 #pragma unroll
@@ -460,25 +399,10 @@ __global__ __launch_bounds__(NT4, 1) void gemm4t_kernel(const bf16_t* __restrict
   }
 }
 
-template <bool AK, bool BKM, bool ACC>
-int launch4t(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
-             hipStream_t st) {
-  auto kern = gemm4t_kernel<AK, BKM, ACC>;
-  constexpr int smem = 4 * SST;
-  static bool attr = [&] {
-    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
-  }();
-  if (!attr) return -3;
-  const int nwg = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
-                     lda, ldb, ldc);
-  return (int)hipGetLastError();
-}
-
-template <bool AK, bool BKM, bool ACC>
+template <bool AK, bool BKM, bool ACC, bool PW = false>
 int launch4s(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
              hipStream_t st) {
-  auto kern = gemm4s_kernel<AK, BKM, ACC>;
+  auto kern = gemm4s_kernel<AK, BKM, ACC, PW>;
   constexpr int smem = 4 * SST;
   static bool attr = [&] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
@@ -523,14 +447,14 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
     RCA_G4D(2)
 #undef RCA_G4D
   }
-  if (diag == 4) {
-#define RCA_G4T(a, b, c) return launch4t<a, b, c>(A, B, C, M, N, K, lda, ldb, ldc, st)
-    if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G4T(false, false, true); RCA_G4T(false, false, false); }
-    if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G4T(false, true, true); RCA_G4T(false, true, false); }
-    if (a_kmaj && b_kmaj) { if (accumulate) RCA_G4T(true, true, true); RCA_G4T(true, true, false); }
-    if (accumulate) RCA_G4T(true, false, true);
-    RCA_G4T(true, false, false);
-#undef RCA_G4T
+  if (diag == 5) {
+#define RCA_G4P(a, b, c) return launch4s<a, b, c, true>(A, B, C, M, N, K, lda, ldb, ldc, st)
+    if (!a_kmaj && !b_kmaj) { if (accumulate) RCA_G4P(false, false, true); RCA_G4P(false, false, false); }
+    if (!a_kmaj && b_kmaj) { if (accumulate) RCA_G4P(false, true, true); RCA_G4P(false, true, false); }
+    if (a_kmaj && b_kmaj) { if (accumulate) RCA_G4P(true, true, true); RCA_G4P(true, true, false); }
+    if (accumulate) RCA_G4P(true, false, true);
+    RCA_G4P(true, false, false);
+#undef RCA_G4P
   }
   if (diag == 3) {
 #define RCA_G4S(a, b, c) return launch4s<a, b, c>(A, B, C, M, N, K, lda, ldb, ldc, st)

@@ -453,7 +453,7 @@ def _gemm_excess(out, ref, absprod, K, base=None):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (512, 768, 320),
                                    (1024, 512, 1024)])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(False, False), (False, True), (True, True), (True, False)])
-@pytest.mark.parametrize("variant", [3, 2, 0])
+@pytest.mark.parametrize("variant", [5, 3, 2, 0])
 def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj, variant):
     """ops.gemm (hand-written gfx950 MFMA GEMM, LDS-DMA staging, swizzled row / transposed-read
     operand images, XCD-grouped tile order) vs an fp32 torch reference, all four operand
