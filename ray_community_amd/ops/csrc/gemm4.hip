@@ -399,6 +399,337 @@ __global__ __launch_bounds__(NT4, 1) void gemm4s_kernel(const bf16_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Variant 6: variant 3's slice ring for the k-contiguous (TN) layout with no per-iteration vector
+// address arithmetic. Variant 3's loop body carried ~50 VALU ops per 64-deep K-tile beside its 128
+// MFMAs (a 64-bit v_lshl_add_u64 per LDS-DMA, a v_add_u32 per fragment read: the asm read took a
+// materialised address); hipBLASLt's 256x256x64 kernel carries two. Here:
+//   - LDS-DMA is a buffer load (`buffer_load_dwordx4 ... offen lds`): a per-wave resource
+//     descriptor (SGPRs) whose base is the wave's first row, a per-lane byte offset per DMA step
+//     that never changes (8 VGPRs), and the slice's k offset in the scalar soffset operand;
+//   - fragment reads are `ds_read_b128 base offset:IMM`: with the 64-B-row swizzle the chunk
+//     index depends on the lane only, so each of the 16 reads per slice is one of two constant
+//     base VGPRs (stages 0-1 / 2-3, the immediate field is 16 bits) plus a compile-time offset;
+//   - four slices per loop iteration, so every stage index is a template constant.
+// Placement per 64-MFMA slice: the 16 reads of the next slice's fragments one per MFMA gap right
+// after the barrier, the 8 DMAs of slice s+3 one every 6 MFMAs after that.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x8_t rd_imm(unsigned base) {
+  s16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(OFF));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(NT4, 1) void gemm4b_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                        long ldb, long ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  tile_origin(blockIdx.x, M, N, m0, n0);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / 32;  // multiple of 4 (host check)
+  // DMA block 4i + wid of a slice = rows 16(4i + wid) .. +15 of the 256-row panel, 64 B each.
+  // Wave base row 16 wid; lane row (l >> 2) + 64 i; chunk (l & 3) ^ swz32(row) = (l & 3) ^ swz32(l >> 2).
+  const bf16_t* wa = A + (long)(m0 + 16 * wid) * lda;
+  const bf16_t* wb = B + (long)(n0 + 16 * wid) * ldb;
+  const __amdgpu_buffer_rsrc_t ra = wave_rsrc(wa, (unsigned)((long)(M - m0 - 16 * wid) * lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = wave_rsrc(wb, (unsigned)((long)(N - n0 - 16 * wid) * ldb * 2));
+  const int lrow = lane >> 2, lch = (lane & 3) ^ swz32(lrow);
+  int va[4], vb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    va[i] = (int)(((long)(lrow + 64 * i) * lda + lch * 8) * 2);
+    vb[i] = (int)(((long)(lrow + 64 * i) * ldb + lch * 8) * 2);
+  }
+  // fragment read base: row ob*16 + (l & 15) of the stage image, chunk (l >> 4) ^ swz32(l & 15)
+  const unsigned rl = (unsigned)((lane & 15) * 64 + (((lane >> 4) ^ swz32(lane & 15)) << 4));
+  const unsigned sbase = lds_off(smem);
+  const unsigned ba_lo = sbase + rl + wr * 8 * 1024, bb_lo = sbase + rl + SLB + wc * 8 * 1024;
+  const unsigned ba_hi = ba_lo + 2 * SST, bb_hi = bb_lo + 2 * SST;
+
+  auto dma = [&](int sl, int stage, int step) {  // step 0..7: A steps 0..3, then B steps 0..3
+    const int soff = min(sl, ns - 1) * 64;
+    lds_char* st = smem + stage * SST;
+    if (step < 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(st + (4 * step + wid) * 1024),
+                                               16, va[step], soff, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(st + SLB + (4 * (step - 4) + wid) * 1024), 16, vb[step - 4],
+          soff, 0, 0);
+  };
+#pragma unroll
+  for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma(sl, sl, i);
+  wait_vmcnt<16>();
+  fence_sched();
+  __builtin_amdgcn_s_barrier();
+  fence_sched();
+  bf16x8_t xa[8], xb[8], ya[8], yb[8];
+#define RCA_RD0(u)                                    \
+  xa[u] = rd_imm<(u) * 1024>(ba_lo);                  \
+  xb[u] = rd_imm<(u) * 1024>(bb_lo);
+  RCA_RD0(0) RCA_RD0(1) RCA_RD0(2) RCA_RD0(3) RCA_RD0(4) RCA_RD0(5) RCA_RD0(6) RCA_RD0(7)
+#undef RCA_RD0
+  wait_lgkm0();
+
+  // one MFMA of slice position p (0..63): acc[p>>3][p&7]
+#define RCA_MF(CA, CB, p) \
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[(p) >> 3][(p)&7]) : "v"(CB[(p)&7]), "v"(CA[(p) >> 3]))
+  // read r (0..15) of the next slice (stage NST): A fragments 0..7, then B 0..7
+#define RCA_RDN(NST, NA, NB, r)                                                                    \
+  {                                                                                                \
+    constexpr int off_ = ((NST)&1) * SST + ((r)&7) * 1024;                                         \
+    if constexpr ((r) < 8) NA[(r)&7] = rd_imm<off_>((NST) < 2 ? ba_lo : ba_hi);                   \
+    else NB[(r)&7] = rd_imm<off_>((NST) < 2 ? bb_lo : bb_hi);                                      \
+  }
+#define RCA_P(ST, CA, CB, NA, NB, p)                                                               \
+  {                                                                                                \
+    fence_sched();                                                                                 \
+    if constexpr ((p) < 16) RCA_RDN(((ST) + 1) & 3, NA, NB, (p));                                  \
+    if constexpr ((p) >= 16 && ((p)-16) % 6 == 0 && ((p)-16) / 6 < 8)                              \
+      dma(s + (ST) + 3, ((ST) + 3) & 3, ((p)-16) / 6);                                             \
+    fence_sched();                                                                                 \
+    RCA_MF(CA, CB, p);                                                                             \
+  }
+#define RCA_P8(ST, CA, CB, NA, NB, b)                                                              \
+  RCA_P(ST, CA, CB, NA, NB, (b) + 0) RCA_P(ST, CA, CB, NA, NB, (b) + 1)                             \
+  RCA_P(ST, CA, CB, NA, NB, (b) + 2) RCA_P(ST, CA, CB, NA, NB, (b) + 3)                             \
+  RCA_P(ST, CA, CB, NA, NB, (b) + 4) RCA_P(ST, CA, CB, NA, NB, (b) + 5)                             \
+  RCA_P(ST, CA, CB, NA, NB, (b) + 6) RCA_P(ST, CA, CB, NA, NB, (b) + 7)
+#define RCA_SL(ST, CA, CB, NA, NB)                                                                 \
+  {                                                                                                \
+    fence_sched();                                                                                 \
+    wait_vmcnt<8>();                                                                               \
+    fence_sched();                                                                                 \
+    __builtin_amdgcn_s_barrier();                                                                  \
+    RCA_P8(ST, CA, CB, NA, NB, 0) RCA_P8(ST, CA, CB, NA, NB, 8)                                    \
+    RCA_P8(ST, CA, CB, NA, NB, 16) RCA_P8(ST, CA, CB, NA, NB, 24)                                  \
+    RCA_P8(ST, CA, CB, NA, NB, 32) RCA_P8(ST, CA, CB, NA, NB, 40)                                  \
+    RCA_P8(ST, CA, CB, NA, NB, 48) RCA_P8(ST, CA, CB, NA, NB, 56)                                  \
+    fence_sched();                                                                                 \
+    wait_lgkm0();                                                                                  \
+    fence_sched();                                                                                 \
+  }
+  for (int s = 0; s < ns; s += 4) {
+    RCA_SL(0, xa, xb, ya, yb)
+    RCA_SL(1, ya, yb, xa, xb)
+    RCA_SL(2, xa, xb, ya, yb)
+    RCA_SL(3, ya, yb, xa, xb)
+  }
+#undef RCA_SL
+#undef RCA_P8
+#undef RCA_P
+#undef RCA_RDN
+#undef RCA_MF
+  wait_lgkm0();
+  wait_vmcnt<0>();
+  drain_acc(acc);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4<ACC>(C, m * ldc + n0 + wc * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+template <bool ACC>
+int launch4b(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+             hipStream_t st) {
+  auto kern = gemm4b_kernel<ACC>;
+  constexpr int smem = 4 * SST;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Variant 7: full-cache-line LDS-DMA. A PMC pass on the o_proj forward product
+// (`profiles/gemm_r4.md`) showed variant 6's 32-deep slices costing twice hipBLASLt's L1->L2 read
+// requests (TCP_TCC_READ_REQ 34.1 M vs 16.8 M) and a texture-addresser unit busy 86 % of the
+// kernel (TA_TA_BUSY 86.8 M vs 40.0 M): each DMA instruction covered 16 rows x 64 B, i.e. 16 half
+// cache lines. Here K-tiles are 64 deep (128-B rows: 8 rows x 128 B per DMA instruction) in two
+// 64 KB LDS buffers, and a buffer is refilled while the tile it held is still being multiplied:
+// both 32-deep halves of a tile's fragments are in registers by the middle of its iteration
+// (F0 read during the previous iteration, F1 in the first 16 MFMAs), so after one barrier the
+// DMAs of tile t+2 go into tile t's buffer, two tiles (~250 MFMAs) ahead of their use.
+//   iteration t (buffer b = t & 1), 128 MFMAs: [0, 64) on F0(t), [64, 128) on F1(t)
+//     M0-15   read F1(t) from b                       M24   lgkmcnt(0) + barrier (b is free)
+//     M24-84  16 DMAs of tile t+2 into b               M96   vmcnt(16) + barrier (t+1 landed)
+//     M96-127 read F0(t+1) from b ^ 1, one per 2 MFMAs  end   lgkmcnt(0)
+// Image: row-major 256 x 128 B per operand; 16-B chunk c of row r at c ^ ((r >> 1) & 7) (the
+// variant-2 image: conflict-free ds_read_b128 fragment reads).
+template <bool ACC>
+__global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        bf16_t* __restrict__ C, int M, int N, int K, long lda,
+                                                        long ldb, long ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  tile_origin(blockIdx.x, M, N, m0, n0);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / 64;  // even (host check: K % 128 == 0)
+  // DMA step i (0..7) of an operand: LDS block 4i + wid = rows 8(4i + wid) .. +7 of the panel.
+  // Wave base row 8 wid, lane row (l >> 3) + 32 i; the lane's 16-B LDS slot l & 7 holds logical
+  // chunk (l & 7) ^ ((row >> 1) & 7) = (l & 7) ^ ((4 wid + (l >> 4)) & 7).
+  const bf16_t* wa = A + (long)(m0 + 8 * wid) * lda;
+  const bf16_t* wb = B + (long)(n0 + 8 * wid) * ldb;
+  const __amdgpu_buffer_rsrc_t ra = wave_rsrc(wa, (unsigned)((long)(M - m0 - 8 * wid) * lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = wave_rsrc(wb, (unsigned)((long)(N - n0 - 8 * wid) * ldb * 2));
+  const int lch = (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7);
+  int va[8], vb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    va[i] = (int)(((long)((lane >> 3) + 32 * i) * lda + lch * 8) * 2);
+    vb[i] = (int)(((long)((lane >> 3) + 32 * i) * ldb + lch * 8) * 2);
+  }
+  // fragment read of row block ob, half kk: row ob*16 + (l & 15), chunk (4 kk + (l >> 4)) ^ ((l & 15) >> 1)
+  constexpr int TBK = 256 * 128;  // one operand tile (32 KB); buffer = A | B = 64 KB
+  const unsigned sbase = lds_off(smem);
+  unsigned rbA[2][2], rbB[2][2];  // [buffer][kk]
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const unsigned lo = (unsigned)((lane & 15) * 128 + (((4 * kk + (lane >> 4)) ^ ((lane & 15) >> 1)) << 4));
+    rbA[0][kk] = sbase + lo + wr * 128 * 128;
+    rbB[0][kk] = sbase + lo + TBK + wc * 128 * 128;
+    rbA[1][kk] = rbA[0][kk] + 2 * TBK;
+    rbB[1][kk] = rbB[0][kk] + 2 * TBK;
+  }
+
+  auto dma = [&](int t, int buf, int step) {  // step 0..7: A, 8..15: B
+    const int soff = min(t, nt - 1) * 128;
+    lds_char* st = smem + buf * 2 * TBK;
+    if (step < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(st + (4 * step + wid) * 1024),
+                                               16, va[step], soff, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(st + TBK + (4 * (step - 8) + wid) * 1024), 16, vb[step - 8],
+          soff, 0, 0);
+  };
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dma(t, t, i);
+  wait_vmcnt<16>();
+  fence_sched();
+  __builtin_amdgcn_s_barrier();
+  fence_sched();
+  bf16x8_t xa[8], xb[8], ya[8], yb[8];
+#define RCA_RD0(u)                                      \
+  xa[u] = rd_imm<(u) * 2048>(rbA[0][0]);                \
+  xb[u] = rd_imm<(u) * 2048>(rbB[0][0]);
+  RCA_RD0(0) RCA_RD0(1) RCA_RD0(2) RCA_RD0(3) RCA_RD0(4) RCA_RD0(5) RCA_RD0(6) RCA_RD0(7)
+#undef RCA_RD0
+  wait_lgkm0();
+
+#define RCA_MF(FA, FB, q) \
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[(q) >> 3][(q)&7]) : "v"(FB[(q)&7]), "v"(FA[(q) >> 3]))
+  // position p (0..127) of the iteration on buffer BUF
+#define RCA_Q(BUF, p)                                                                                \
+  {                                                                                                  \
+    fence_sched();                                                                                   \
+    if constexpr ((p) < 16) {                                                                        \
+      if constexpr ((p) < 8) ya[(p)&7] = rd_imm<((p)&7) * 2048>(rbA[BUF][1]);                        \
+      else yb[(p)&7] = rd_imm<((p)&7) * 2048>(rbB[BUF][1]);                                          \
+    }                                                                                                \
+    if constexpr ((p) == 24) {                                                                       \
+      wait_lgkm0();                                                                                  \
+      fence_sched();                                                                                 \
+      __builtin_amdgcn_s_barrier();                                                                  \
+    }                                                                                                \
+    if constexpr ((p) >= 24 && (p) <= 84 && ((p)-24) % 4 == 0) dma(t + (BUF) + 2, BUF, ((p)-24) / 4); \
+    if constexpr ((p) == 96) {                                                                       \
+      wait_vmcnt<16>();                                                                              \
+      fence_sched();                                                                                 \
+      __builtin_amdgcn_s_barrier();                                                                  \
+    }                                                                                                \
+    if constexpr ((p) >= 96 && ((p)&1) == 0) {                                                       \
+      constexpr int r_ = ((p)-96) >> 1;                                                              \
+      if constexpr (r_ < 8) xa[r_ & 7] = rd_imm<(r_ & 7) * 2048>(rbA[(BUF) ^ 1][0]);                 \
+      else xb[r_ & 7] = rd_imm<(r_ & 7) * 2048>(rbB[(BUF) ^ 1][0]);                                  \
+    }                                                                                                \
+    fence_sched();                                                                                   \
+    if constexpr ((p) < 64) RCA_MF(xa, xb, (p));                                                     \
+    else RCA_MF(ya, yb, (p)-64);                                                                     \
+  }
+#define RCA_Q8(BUF, b)                                                                              \
+  RCA_Q(BUF, (b) + 0) RCA_Q(BUF, (b) + 1) RCA_Q(BUF, (b) + 2) RCA_Q(BUF, (b) + 3) RCA_Q(BUF, (b) + 4) \
+  RCA_Q(BUF, (b) + 5) RCA_Q(BUF, (b) + 6) RCA_Q(BUF, (b) + 7)
+#define RCA_IT(BUF)                                                                                 \
+  {                                                                                                 \
+    RCA_Q8(BUF, 0) RCA_Q8(BUF, 8) RCA_Q8(BUF, 16) RCA_Q8(BUF, 24)                                   \
+    RCA_Q8(BUF, 32) RCA_Q8(BUF, 40) RCA_Q8(BUF, 48) RCA_Q8(BUF, 56)                                 \
+    RCA_Q8(BUF, 64) RCA_Q8(BUF, 72) RCA_Q8(BUF, 80) RCA_Q8(BUF, 88)                                 \
+    RCA_Q8(BUF, 96) RCA_Q8(BUF, 104) RCA_Q8(BUF, 112) RCA_Q8(BUF, 120)                              \
+    fence_sched();                                                                                  \
+    wait_lgkm0();                                                                                   \
+    fence_sched();                                                                                  \
+  }
+  for (int t = 0; t < nt; t += 2) {
+    RCA_IT(0)
+    RCA_IT(1)
+  }
+#undef RCA_IT
+#undef RCA_Q8
+#undef RCA_Q
+#undef RCA_MF
+  wait_lgkm0();
+  wait_vmcnt<0>();
+  drain_acc(acc);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4<ACC>(C, m * ldc + n0 + wc * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+template <bool ACC>
+int launch4c(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+             hipStream_t st) {
+  auto kern = gemm4c_kernel<ACC>;
+  constexpr int smem = 4 * 256 * 128;
+  static bool attr = [&] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+  }();
+  if (!attr) return -3;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
 template <bool AK, bool BKM, bool ACC, bool PW = false>
 int launch4s(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
              hipStream_t st) {
@@ -446,6 +777,19 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
     if (diag == 1) RCA_G4D(1)
     RCA_G4D(2)
 #undef RCA_G4D
+  }
+  // variants 6 / 7: k-contiguous A and B, K % 128 == 0, every wave's buffer range < 4 GB; else 3
+  if (diag == 6 || diag == 7) {
+    if (!a_kmaj && !b_kmaj && K % 128 == 0 && (double)M * lda * 2 < 4294967296.0 &&
+        (double)N * ldb * 2 < 4294967296.0) {
+      if (diag == 7) {
+        if (accumulate) return launch4c<true>(A, B, C, M, N, K, lda, ldb, ldc, st);
+        return launch4c<false>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      }
+      if (accumulate) return launch4b<true>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      return launch4b<false>(A, B, C, M, N, K, lda, ldb, ldc, st);
+    }
+    diag = 3;
   }
   if (diag == 5) {
 #define RCA_G4P(a, b, c) return launch4s<a, b, c, true>(A, B, C, M, N, K, lda, ldb, ldc, st)

@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
     ap.add_argument("--variants", default="2,0", help="hand-GEMM variants to time (gemm.hip launch_variant)")
+    ap.add_argument("--tn", action="store_true",
+                    help="also time every variant and torch on pre-transposed k-contiguous operands (keys *_tn, "
+                         "transpose time excluded): the kernel-against-kernel comparison on hipBLASLt's best layout")
     args = ap.parse_args()
     dev = "cuda"
     rows = []
@@ -87,6 +90,22 @@ def main():
         fns = {f"v{v}": mk(v) for v in variants}
         fns["torch"] = f_torch
         fns["torch+tr"] = f_tr
+        if args.tn:
+            at = a if not ak else ops.transpose(a)          # [M][K]
+            bt = b if not bk else ops.transpose(b)          # [N][K]
+            for v in variants:
+                lib.rca_gemm_set_variant(v)
+                o = ops.gemm(at, bt, False, False)
+                row_err[f"v{v}_tn_err"] = ((o.float() - ref).abs().max() / ref.abs().max()).item()
+                del o
+            def mk_tn(v):
+                def f():
+                    lib.rca_gemm_set_variant(v)
+                    ops.gemm(at, bt, False, False, out=out)
+                return f
+            for v in variants:
+                fns[f"v{v}_tn"] = mk_tn(v)
+            fns["torch_tn"] = lambda: torch.matmul(at, bt.t())
         for f in fns.values():
             f()
         res = {k: [] for k in fns}
@@ -103,6 +122,8 @@ def main():
         rows.append(row)
         print(json.dumps(row), flush=True)
         del a, b, out, ref
+        if args.tn:
+            del at, bt
         torch.cuda.empty_cache()
     tot = {k: round(sum(r[k + "_ms"] for r in rows), 4) for k in list(res)}
     print(json.dumps({"total_ms": tot}), flush=True)

@@ -453,7 +453,7 @@ def _gemm_excess(out, ref, absprod, K, base=None):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 192), (512, 768, 320),
                                    (1024, 512, 1024)])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(False, False), (False, True), (True, True), (True, False)])
-@pytest.mark.parametrize("variant", [5, 3, 2, 0])
+@pytest.mark.parametrize("variant", [7, 6, 5, 3, 2, 0])
 def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj, variant):
     """ops.gemm (hand-written gfx950 MFMA GEMM, LDS-DMA staging, swizzled row / transposed-read
     operand images, XCD-grouped tile order) vs an fp32 torch reference, all four operand
@@ -478,6 +478,32 @@ def test_gemm_bf16_all_layouts_match_fp32(M, N, K, a_kmaj, b_kmaj, variant):
         lib.rca_gemm_set_variant(prev)
     torch.cuda.synchronize()
     absprod = af.abs() @ bf.abs()
+    assert _gemm_excess(out, ref, absprod, K) <= 1.0
+    assert _gemm_excess(acc, ref, absprod, K, base.float()) <= 1.0
+
+
+@pytest.mark.parametrize("M,N,K", [(1280, 768, 2048), (2048, 2304, 4096), (512, 256, 128)])
+@pytest.mark.parametrize("variant", [6, 7])
+def test_gemm_buffer_dma_tn_variants(M, N, K, variant):
+    """Variants 6 (buffer-descriptor LDS-DMA, immediate-offset fragment reads, 4 slices per loop
+    iteration) and 7 (64-deep tiles, full-cache-line DMA, buffer refilled two tiles ahead) on
+    multi-tile k-contiguous shapes with many ring wraps (and the 2-tile minimum), plain and
+    accumulating."""
+    torch.manual_seed(M + K)
+    a = (torch.randn(M, K, device=DEV) + torch.arange(K, device=DEV) * 1e-3).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV) - torch.arange(N, device=DEV)[:, None] * 1e-3).to(torch.bfloat16)
+    ref = a.float() @ b.float().t()
+    absprod = a.float().abs() @ b.float().abs().t()
+    lib = ops._lib.lib()
+    prev = lib.rca_gemm_set_variant(variant)
+    try:
+        out = ops.gemm(a, b)
+        base = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        acc = base.clone()
+        ops.gemm(a, b, out=acc, accumulate=True)
+    finally:
+        lib.rca_gemm_set_variant(prev)
+    torch.cuda.synchronize()
     assert _gemm_excess(out, ref, absprod, K) <= 1.0
     assert _gemm_excess(acc, ref, absprod, K, base.float()) <= 1.0
 
