@@ -23,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..parallel.fused_linear import FusedEmbedding, FusedWgradLinear
+from ..parallel.fused_linear import FusedEmbedding, FusedWgradLinear, swiglu_down
 
 
 @dataclass
@@ -116,13 +116,10 @@ class MLP(nn.Module):
         self.down = FusedWgradLinear(cfg.intermediate_size, cfg.hidden_size)
 
     def forward(self, x):
-        gu = self.gate_up(x)
-        if gu.is_cuda and torch.is_grad_enabled() and getattr(self.down.weight, "_rca_flat_grad", False):
-            # SwiGLU also writes act^T (the down projection's wgrad operand) and, in backward,
-            # d(gate|up)^T for the gate_up wgrad: two transpose passes per layer folded away
-            act, act_t = ops.swiglu(gu, with_transposed=True)
-            return self.down(act, x_t=act_t)
-        return self.down(ops.swiglu(gu))
+        # On the flat-gradient GPU path SwiGLU also writes act^T (the down projection's wgrad
+        # operand), and the backward's down dgrad GEMM applies the SwiGLU backward in its epilogue,
+        # writing d(gate|up) and its transpose for the gate_up wgrad (parallel/fused_linear.py).
+        return swiglu_down(self.gate_up(x), self.down)
 
 
 class Block(nn.Module):

@@ -171,19 +171,26 @@ class _SwiGLU(torch.autograd.Function):
         (gu,) = ctx.saved_tensors
         if dout is None:
             return None, None
-        F2 = gu.shape[-1]
-        T = gu.numel() // F2
-        dgu = torch.empty_like(gu)
-        dout = dout.contiguous()
-        if ctx.tr:
-            dgu_t = torch.empty(F2, T, device=gu.device, dtype=gu.dtype)
-            check(lib().rca_swiglu_bwd_tr(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), dgu_t.data_ptr(), T,
-                                          F2 // 2, stream_ptr(gu.device)), "swiglu_bwd_tr")
-            put_grad_transposed(dgu, dgu_t)
-        else:
-            check(lib().rca_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), T, F2 // 2,
-                                       stream_ptr(gu.device)), "swiglu_bwd")
-        return dgu, None
+        return swiglu_backward(gu, dout, ctx.tr), None
+
+
+def swiglu_backward(gu, dout, with_transposed: bool = False):
+    """d(gate|up) of ``swiglu(gu)`` (GPU kernels). ``with_transposed`` (the ``_swiglu_tr_ok``
+    shapes) also writes its transpose and registers it for the producing linear's weight GEMM."""
+    gu = gu.contiguous()
+    F2 = gu.shape[-1]
+    T = gu.numel() // F2
+    dgu = torch.empty_like(gu)
+    dout = dout.contiguous()
+    if with_transposed and _swiglu_tr_ok(gu):
+        dgu_t = torch.empty(F2, T, device=gu.device, dtype=gu.dtype)
+        check(lib().rca_swiglu_bwd_tr(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), dgu_t.data_ptr(), T,
+                                      F2 // 2, stream_ptr(gu.device)), "swiglu_bwd_tr")
+        put_grad_transposed(dgu, dgu_t)
+    else:
+        check(lib().rca_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), T, F2 // 2,
+                                   stream_ptr(gu.device)), "swiglu_bwd")
+    return dgu
 
 
 def swiglu(gu, with_transposed: bool = False):
@@ -198,6 +205,33 @@ def swiglu(gu, with_transposed: bool = False):
         return (out, out_t) if with_transposed else out
     out = ref.swiglu_ref(gu)
     return (out, None) if with_transposed else out
+
+
+def gemm_swiglu_bwd_supported(dy, w_t, gu) -> bool:
+    """Shapes of the fused down-projection dgrad + SwiGLU backward (ops/csrc/gemm4.hip variant 7,
+    EPI 1): T, F multiples of 256, H of 128, bf16 CUDA, unit inner strides, contiguous gu."""
+    if not (dy.is_cuda and dy.dim() == 2 and w_t.dim() == 2 and gu.dim() == 2):
+        return False
+    T, H = dy.shape
+    F = w_t.shape[0]
+    return (T % 256 == 0 and F % 256 == 0 and H % 128 == 0 and w_t.shape[1] == H and tuple(gu.shape) == (T, 2 * F)
+            and gu.is_contiguous() and all(_gemm_operand_ok(t) for t in (dy, w_t, gu)))
+
+
+def gemm_swiglu_bwd(dy, w_t, gu):
+    """``(dgu, dgu^T)`` for ``y = swiglu(gu) @ W^T`` given ``dy``: the input gradient of the down
+    projection, ``dh = dy @ W`` (``w_t`` = ``W^T``, ``[F, H]``), stays in the GEMM's registers and
+    its epilogue applies the SwiGLU backward (``dgu = [dh * u * s(g)(1 + g(1 - s(g))), dh * silu(g)]``)
+    and writes ``dgu`` and its transpose; no ``dh`` tensor, no separate SwiGLU pass."""
+    if not gemm_swiglu_bwd_supported(dy, w_t, gu):
+        raise ValueError("gemm_swiglu_bwd: unsupported operands")
+    T, H = dy.shape
+    F = w_t.shape[0]
+    dgu = torch.empty_like(gu)
+    dgu_t = torch.empty(2 * F, T, device=gu.device, dtype=gu.dtype)
+    check(lib().rca_gemm_swiglu_bwd(dy.data_ptr(), w_t.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dgu_t.data_ptr(),
+                                    T, F, H, dy.stride(0), w_t.stride(0), stream_ptr(dy.device)), "gemm_swiglu_bwd")
+    return dgu, dgu_t
 
 
 def transpose_supported(x) -> bool:

@@ -32,6 +32,8 @@ _SIGS = {
     "rca_gemm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_int, c_int, c_int,
                               c_void_p]),
     "rca_gemm_set_variant": (c_int, [c_int]),
+    "rca_gemm_swiglu_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_ll,
+                                    c_void_p]),
     "rca_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_ll, c_void_p]),
     "rca_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rca_ce_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_ll, c_void_p]),

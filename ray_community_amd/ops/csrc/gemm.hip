@@ -175,7 +175,7 @@ RCA_API int rca_gemm_bf16(const void* A, const void* B, void* C, int M, int N, i
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -2;
   const int v = gemm_variant();
   if (v >= 90) return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, 0, st, v - 90);
-  if (v == 3 || v == 5 || v == 6 || v == 7)
+  if (v == 3 || v == 5 || v == 6 || v == 7 || (v >= 71 && v <= 78))
     return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, accumulate, st, v);
   if (v != 0) return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, accumulate, st, 0);
 #define RCA_G(a, b, c) return launch_variant<a, b, c>(v, A, B, C, M, N, K, lda, ldb, ldc, st)

@@ -580,10 +580,130 @@ int launch4b(const void* A, const void* B, void* C, int M, int N, int K, long ld
 //     M96-127 read F0(t+1) from b ^ 1, one per 2 MFMAs  end   lgkmcnt(0)
 // Image: row-major 256 x 128 B per operand; 16-B chunk c of row r at c ^ ((r >> 1) & 7) (the
 // variant-2 image: conflict-free ds_read_b128 fragment reads).
-template <bool ACC>
+// Fused epilogues of variant 7 (EPI): 0 = store C (+= C when ACC); 1 = SwiGLU backward (C is the
+// down projection's input gradient dh = dy W_down, never stored; see swiglu_bwd_epilogue).
+struct EpiArgs {
+  const bf16_t* gu;  // [M][2F] gate | up (the forward's gate_up output)
+  bf16_t* dgu;       // [M][2F]
+  bf16_t* dgu_t;     // [2F][M]
+  long ldg, ldd, ldt;
+  int F;
+};
+
+// SwiGLU-backward epilogue (variant 7, EPI 1). The wave's 128 x 128 accumulator tile is
+// dh[m][n] (token m, feature n) in fp32; with g = gu[m][n], u = gu[m][F + n]:
+//   dg = dh * u * s * (1 + g (1 - s)),  du = dh * bf16(g s),  s = sigmoid(g)
+// (elementwise.hip's swiglu_bwd, but from the fp32 dh instead of its bf16 rounding). dg, du go to
+// dgu[m][n], dgu[m][F + n] (8-B stores of 4 consecutive n) and, through a wave-private LDS tile
+// [128 n][128 m] (272-B rows: the 4 lane groups' rows land 16 banks apart), to the transposed
+// copy dgu_t[n][m], dgu_t[F + n][m] that the gate_up weight gradient reads, as 16-B row stores.
+// Replaces the dh store + the separate swiglu_bwd_tr pass (its dh read and write).
+constexpr int kEpiRow = 272, kEpiWaveLds = 128 * kEpiRow;
+
+__device__ __forceinline__ void epi_tile_store_t(const lds_char* tw, bf16_t* __restrict__ dst, long ldt, long row0,
+                                                 long m0, int lane) {
+#pragma unroll 8
+  for (int q = 0; q < 32; ++q) {
+    const int idx = q * 64 + lane, row = idx >> 4, ch = idx & 15;
+    const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(tw + row * kEpiRow + ch * 16);
+    *reinterpret_cast<u32x4*>(dst + (row0 + row) * ldt + m0 + ch * 8) = v;
+  }
+}
+
+__device__ __forceinline__ void swiglu_bwd_epilogue(f32x4 (&acc)[8][8], const EpiArgs& ep, lds_char* smem, int mw,
+                                                    int nw, int wid, int lane) {
+  __builtin_amdgcn_s_barrier();  // every wave has left the LDS ring (its waits came before)
+  lds_char* tw = smem + wid * kEpiWaveLds;
+  const int ml0 = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = mw + i * 16 + ml0;
+    const bf16_t* grow = ep.gu + m * ep.ldg;
+    bf16_t* drow = ep.dgu + m * ep.ldd;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int nl = j * 16 + nq, n = nw + nl;
+      const unsigned long long gv = *reinterpret_cast<const unsigned long long*>(grow + n);
+      const unsigned long long uv = *reinterpret_cast<const unsigned long long*>(grow + ep.F + n);
+      unsigned long long og = 0, ou = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float g = bf2f((bf16_t)(gv >> (16 * r))), u = bf2f((bf16_t)(uv >> (16 * r)));
+        const float d = acc[i][j][r];
+        const float sg = 1.f / (1.f + __expf(-g));
+        const float si = g * sg;
+        const bf16_t dgb = f2bf(d * u * sg * (1.f + g * (1.f - sg)));
+        const bf16_t dub = f2bf(d * bf2f(f2bf(si)));
+        og |= (unsigned long long)dgb << (16 * r);
+        ou |= (unsigned long long)dub << (16 * r);
+        *(__attribute__((address_space(3))) bf16_t*)(tw + (nl + r) * kEpiRow + (i * 16 + ml0) * 2) = dgb;
+        acc[i][j][r] = bf2f(dub);  // du kept for the second transposed pass
+      }
+      *reinterpret_cast<unsigned long long*>(drow + n) = og;
+      *reinterpret_cast<unsigned long long*>(drow + ep.F + n) = ou;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  epi_tile_store_t(tw, ep.dgu_t, ep.ldt, nw, mw, lane);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *(__attribute__((address_space(3))) bf16_t*)(tw + (j * 16 + nq + r) * kEpiRow + (i * 16 + ml0) * 2) =
+            f2bf(acc[i][j][r]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  epi_tile_store_t(tw, ep.dgu_t, ep.ldt, (long)ep.F + nw, mw, lane);
+}
+
+// Where each event of a variant-7 iteration sits (position p = index of the MFMA it precedes).
+// SPLIT = 0: the knob schedule below. SPLIT = 1: the buffer is freed in two halves (variant 77):
+// F1's A fragments are read first and a barrier frees the A region for the A DMAs while the B
+// fragments are still being read; a second barrier frees the B region; the F0(t+1) wait comes
+// after 13 of the iteration's 16 DMAs (vmcnt(13)), the last 3 B DMAs overlap the F0 reads.
+template <int B1, int DS, int W2, int RD, int R1, int SPLIT>
+struct Sch7 {
+  static constexpr int f1(int p) {  // F1(t) read index (0-7 A, 8-15 B) or -1
+    if (SPLIT) {
+      if (p >= 1 && p <= 15 && (p & 1)) return (p - 1) / 2;
+      constexpr int b[8] = {25, 28, 31, 34, 37, 39, 41, 43};
+      for (int i = 0; i < 8; ++i)
+        if (b[i] == p) return 8 + i;
+      return -1;
+    }
+    return (p % R1 == 0 && p / R1 < 16) ? p / R1 : -1;
+  }
+  static constexpr int dma(int p) {  // DMA step (0-7 A, 8-15 B) or -1
+    if (SPLIT) {
+      constexpr int d[16] = {23, 26, 29, 32, 35, 53, 56, 59, 62, 65, 86, 88, 90, 97, 101, 125};
+      for (int i = 0; i < 16; ++i)
+        if (d[i] == p) return i;
+      return -1;
+    }
+    return (p >= B1 && p <= B1 + 15 * DS && (p - B1) % DS == 0) ? (p - B1) / DS : -1;
+  }
+  static constexpr int wait(int p) {  // 1: lgkmcnt(0) + barrier, 2: vmcnt(VM) + barrier
+    if (SPLIT) return (p == 21 || p == 51) ? 1 : (p == 92 ? 2 : 0);
+    return p == B1 ? 1 : (p == W2 ? 2 : 0);
+  }
+  static constexpr int VM = SPLIT ? 13 : 16;
+  static constexpr int f0(int p) {  // F0(t+1) read index or -1
+    if (SPLIT) return (p >= 94 && p < 110) ? p - 94 : -1;
+    return (p >= W2 && (p - W2) % RD == 0 && (p - W2) / RD < 16) ? (p - W2) / RD : -1;
+  }
+};
+
+// Schedule knobs (positions in the iteration's 128 MFMAs): B1 = the lgkmcnt(0) + barrier that frees
+// the buffer, DMAs every DS MFMAs from B1, W2 = the vmcnt(16) + barrier before the F0(t+1) reads,
+// which then go one per RD MFMAs; F1 reads one per R1 MFMAs from M0; ORD 1 walks the MFMAs with
+// the B-tile fragment (the MFMA's first operand) fixed over 8 consecutive MFMAs instead of the
+// A-tile one. Defaults = variant 7; variants 71-76 are timing A/Bs.
+template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 0, int SPLIT = 0, int EPI = 0>
 __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         bf16_t* __restrict__ C, int M, int N, int K, long lda,
-                                                        long ldb, long ldc) {
+                                                        long ldb, long ldc, EpiArgs ep) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -653,35 +773,43 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
 #undef RCA_RD0
   wait_lgkm0();
 
-#define RCA_MF(FA, FB, q) \
-  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[(q) >> 3][(q)&7]) : "v"(FB[(q)&7]), "v"(FA[(q) >> 3]))
+#define RCA_MF(FA, FB, q)                                                                                  \
+  {                                                                                                        \
+    constexpr int i_ = ORD ? ((q)&7) : ((q) >> 3), j_ = ORD ? ((q) >> 3) : ((q)&7);                        \
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i_][j_]) : "v"(FB[j_]), "v"(FA[i_]));          \
+  }
   // position p (0..127) of the iteration on buffer BUF
 #define RCA_Q(BUF, p)                                                                                \
   {                                                                                                  \
+    using S_ = Sch7<B1, DS, W2, RD, R1, SPLIT>;                                                      \
     fence_sched();                                                                                   \
-    if constexpr ((p) < 16) {                                                                        \
-      if constexpr ((p) < 8) ya[(p)&7] = rd_imm<((p)&7) * 2048>(rbA[BUF][1]);                        \
-      else yb[(p)&7] = rd_imm<((p)&7) * 2048>(rbB[BUF][1]);                                          \
+    if constexpr (S_::f1(p) >= 0) {                                                                  \
+      constexpr int f_ = S_::f1(p);                                                                  \
+      if constexpr (f_ < 8) ya[f_ & 7] = rd_imm<(f_ & 7) * 2048>(rbA[BUF][1]);                       \
+      else yb[f_ & 7] = rd_imm<(f_ & 7) * 2048>(rbB[BUF][1]);                                        \
     }                                                                                                \
-    if constexpr ((p) == 24) {                                                                       \
+    if constexpr (S_::wait(p) == 1) {                                                                \
       wait_lgkm0();                                                                                  \
       fence_sched();                                                                                 \
       __builtin_amdgcn_s_barrier();                                                                  \
     }                                                                                                \
-    if constexpr ((p) >= 24 && (p) <= 84 && ((p)-24) % 4 == 0) dma(t + (BUF) + 2, BUF, ((p)-24) / 4); \
-    if constexpr ((p) == 96) {                                                                       \
-      wait_vmcnt<16>();                                                                              \
+    if constexpr (S_::dma(p) >= 0) dma(t + (BUF) + 2, BUF, S_::dma(p));                              \
+    if constexpr (S_::wait(p) == 2) {                                                                \
+      wait_vmcnt<S_::VM>();                                                                          \
       fence_sched();                                                                                 \
       __builtin_amdgcn_s_barrier();                                                                  \
     }                                                                                                \
-    if constexpr ((p) >= 96 && ((p)&1) == 0) {                                                       \
-      constexpr int r_ = ((p)-96) >> 1;                                                              \
+    if constexpr (S_::f0(p) >= 0) {                                                                  \
+      constexpr int r_ = S_::f0(p);                                                                  \
       if constexpr (r_ < 8) xa[r_ & 7] = rd_imm<(r_ & 7) * 2048>(rbA[(BUF) ^ 1][0]);                 \
       else xb[r_ & 7] = rd_imm<(r_ & 7) * 2048>(rbB[(BUF) ^ 1][0]);                                  \
     }                                                                                                \
     fence_sched();                                                                                   \
-    if constexpr ((p) < 64) RCA_MF(xa, xb, (p));                                                     \
-    else RCA_MF(ya, yb, (p)-64);                                                                     \
+    if constexpr ((p) < 64) {                                                                        \
+      RCA_MF(xa, xb, (p))                                                                            \
+    } else {                                                                                         \
+      RCA_MF(ya, yb, (p)-64)                                                                         \
+    }                                                                                                \
   }
 #define RCA_Q8(BUF, b)                                                                              \
   RCA_Q(BUF, (b) + 0) RCA_Q(BUF, (b) + 1) RCA_Q(BUF, (b) + 2) RCA_Q(BUF, (b) + 3) RCA_Q(BUF, (b) + 4) \
@@ -707,6 +835,10 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
   wait_lgkm0();
   wait_vmcnt<0>();
   drain_acc(acc);
+  if constexpr (EPI == 1) {
+    swiglu_bwd_epilogue(acc, ep, smem, m0 + wr * 128, n0 + wc * 128, wid, lane);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const long m = m0 + wr * 128 + i * 16 + (lane & 15);
@@ -715,18 +847,19 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
   }
 }
 
-template <bool ACC>
+template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 0, int SPLIT = 0, int EPI = 0>
 int launch4c(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
-             hipStream_t st) {
-  auto kern = gemm4c_kernel<ACC>;
-  constexpr int smem = 4 * 256 * 128;
+             hipStream_t st, EpiArgs ep = EpiArgs{}) {
+  static_assert(SPLIT || (B1 >= 16 * R1 && B1 + 15 * DS < W2 && W2 + 15 * RD < 128), "schedule positions");
+  auto kern = gemm4c_kernel<ACC, B1, DS, W2, RD, R1, ORD, SPLIT, EPI>;
+  constexpr int smem = EPI == 1 ? 4 * kEpiWaveLds : 4 * 256 * 128;
   static bool attr = [&] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
   }();
   if (!attr) return -3;
   const int nwg = (M / BM) * (N / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT4), smem, st, (const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, M, N, K,
-                     lda, ldb, ldc);
+                     lda, ldb, ldc, ep);
   return (int)hipGetLastError();
 }
 
@@ -778,10 +911,20 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
     RCA_G4D(2)
 #undef RCA_G4D
   }
-  // variants 6 / 7: k-contiguous A and B, K % 128 == 0, every wave's buffer range < 4 GB; else 3
-  if (diag == 6 || diag == 7) {
+  // variants 6 / 7 (71-73: variant-7 schedule A/Bs): k-contiguous A and B, K % 128 == 0, every
+  // wave's buffer range < 4 GB; else 3
+  if (diag == 6 || diag == 7 || (diag >= 71 && diag <= 78)) {
     if (!a_kmaj && !b_kmaj && K % 128 == 0 && (double)M * lda * 2 < 4294967296.0 &&
         (double)N * ldb * 2 < 4294967296.0) {
+      if (diag >= 71 && accumulate) diag = 7;
+      if (diag == 71) return launch4c<false, 20, 3, 88, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 72) return launch4c<false, 24, 4, 104, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 73) return launch4c<false, 32, 4, 100, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 74) return launch4c<false, 24, 4, 104, 1, 1, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 75) return launch4c<false, 36, 4, 100, 1, 2, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 76) return launch4c<false, 36, 4, 100, 1, 2, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 77) return launch4c<false, 24, 4, 96, 2, 1, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 78) return launch4c<false, 24, 4, 96, 2, 1, 1, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
       if (diag == 7) {
         if (accumulate) return launch4c<true>(A, B, C, M, N, K, lda, ldb, ldc, st);
         return launch4c<false>(A, B, C, M, N, K, lda, ldb, ldc, st);
@@ -816,4 +959,16 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
   if (accumulate) RCA_G4(true, false, true);
   RCA_G4(true, false, false);
 #undef RCA_G4
+}
+
+// dgu, dgu_t = SwiGLU-backward(gu, dh) with dh = dy W_down computed in registers (variant 7's
+// main loop, EPI 1): dy [T][H] (k = H contiguous, row stride ld_dy), w_t = W_down^T [F][H] (row
+// stride ld_w), gu / dgu [T][2F] contiguous, dgu_t [2F][T] contiguous.
+// Contract: T % 256 == 0, F % 256 == 0, H % 128 == 0, 16-B aligned rows; returns -1 otherwise.
+RCA_API int rca_gemm_swiglu_bwd(const void* dy, const void* w_t, const void* gu, void* dgu, void* dgu_t, int T, int F,
+                                int H, long long ld_dy, long long ld_w, hipStream_t st) {
+  if (T <= 0 || F <= 0 || H <= 0 || T % 256 || F % 256 || H % 128 || ld_dy % 8 || ld_w % 8) return -1;
+  if ((double)T * ld_dy * 2 >= 4294967296.0 || (double)F * ld_w * 2 >= 4294967296.0) return -1;
+  EpiArgs ep{(const bf16_t*)gu, (bf16_t*)dgu, (bf16_t*)dgu_t, 2L * F, 2L * F, (long)T, F};
+  return launch4c<false, 36, 4, 100, 1, 2, 1, 0, 1>(dy, w_t, nullptr, T, F, H, ld_dy, ld_w, 0, st, ep);
 }

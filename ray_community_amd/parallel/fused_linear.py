@@ -55,6 +55,60 @@ class _LinearWgradIntoFlat(torch.autograd.Function):
         return gx, None, None
 
 
+class _SwiGLUDownIntoFlat(torch.autograd.Function):
+    """``down(swiglu(gu))`` with the down projection's dW going into the flat gradient buffer and
+    its input gradient never materialised: backward runs the fused gfx950 GEMM whose epilogue
+    applies the SwiGLU backward (``ops.gemm_swiglu_bwd``: dgu and dgu^T straight from the dh
+    accumulators), replacing the dh GEMM output + the separate ``swiglu_bwd_tr`` pass.
+    Forward = ``ops.swiglu(gu, with_transposed=True)`` (act^T feeds the down wgrad) + ``F.linear``."""
+
+    @staticmethod
+    def forward(ctx, gu, weight):
+        act, act_t = ops.swiglu(gu.detach(), with_transposed=True)
+        ctx.save_for_backward(gu, act_t)
+        ctx.weight = weight
+        return F.linear(act, weight)
+
+    @staticmethod
+    def backward(ctx, gy):
+        gu, act_t = ctx.saved_tensors
+        w = ctx.weight
+        g2 = gy.reshape(-1, gy.shape[-1])
+        g_t = ops.pop_grad_transposed(g2)
+        dgu = None
+        if ctx.needs_input_grad[0]:
+            wt = weight_t(w)
+            if ops.gemm_swiglu_bwd_supported(g2, wt, gu):
+                dgu, dgu_t = ops.gemm_swiglu_bwd(g2, wt, gu)
+                ops.put_grad_transposed(dgu, dgu_t)
+            else:  # the unfused pair: dh GEMM, then the SwiGLU backward (+ transposed copy)
+                dgu = ops.swiglu_backward(gu, F.linear(g2, wt), with_transposed=True)
+        view = _flat_view(w, g2.dtype)
+        if view is None:
+            return dgu, _wgrad(g2, None, True, g_t=g_t, x_t=act_t).to(w.dtype)
+        _wgrad(g2, None, True, out=view, accumulate=not _take_fresh(w), g_t=g_t, x_t=act_t)
+        _notify(w)
+        return dgu, None
+
+
+def swiglu_down(gu, down: "FusedWgradLinear"):
+    """``down(swiglu(gu))``: the fused path when the down weight writes into a flat gradient
+    buffer and the operands fit the fused kernel's contract; otherwise the two separate ops."""
+    w = down.weight
+    if (gu.is_cuda and torch.is_grad_enabled() and w.requires_grad and getattr(w, "_rca_flat_grad", False)
+            and _FUSE_SWIGLU_BWD and gu.dim() == 2 and ops.transpose_supported(gu)
+            and gu.shape[0] % 256 == 0 and w.shape[1] % 256 == 0 and w.shape[0] % 128 == 0):
+        return _SwiGLUDownIntoFlat.apply(gu, w)
+    if gu.is_cuda and torch.is_grad_enabled() and getattr(w, "_rca_flat_grad", False):
+        act, act_t = ops.swiglu(gu, with_transposed=True)
+        return down(act, x_t=act_t)
+    return down(ops.swiglu(gu))
+
+
+# RCA_FUSE_SWIGLU_BWD=0 keeps the unfused down dgrad (hipBLASLt) + swiglu_bwd_tr pair, for A/B runs
+_FUSE_SWIGLU_BWD = os.environ.get("RCA_FUSE_SWIGLU_BWD", "1") != "0"
+
+
 def weight_t(w):
     """``w.t().contiguous()``: the W^T copy the fused AdamW update keeps current when it is valid
     (``parallel/optim.py::FlatAdamW._setup_transposed``), else a transpose pass (into that buffer
