@@ -130,12 +130,18 @@ class TaskState:
 
 
 class ActorState:
-    def __init__(self, aid, spec, owner):
+    """Runtime handles of one actor (call queue, in-flight calls, waiters). What the actor is
+    looked up by -- state, node, name, placement group, handle holders -- lives in the native
+    actor directory (``Head.actor_dir``, _native/actor_table.cpp); ``state`` and ``node`` write
+    through to it."""
+
+    def __init__(self, aid, spec, owner, directory=None):
         self.aid = aid
         self.spec = spec
-        self.state = A_PENDING
+        self._dir = None
+        self._state = A_PENDING
+        self._node = None
         self.worker = None
-        self.node = None
         self.queue: collections.deque = collections.deque()
         self.inflight: Dict[bytes, TaskState] = {}
         self.restarts_left = spec.get("max_restarts", 0)
@@ -152,6 +158,31 @@ class ActorState:
         self.pid = None
         self.killed = False
         self.addr_waiters: List[tuple] = []  # (Deferred, min incarnation) of direct-call channels
+        if directory is not None:
+            st = spec.get("strategy") or {}
+            directory.add(aid, self.name, self.namespace, owner, st.get("pg_id") if st.get("kind") == "pg" else None,
+                          A_PENDING, spec.get("class_name") or "", self.detached)
+            self._dir = directory
+
+    @property
+    def state(self):
+        return self._state
+
+    @state.setter
+    def state(self, v):
+        self._state = v
+        if self._dir is not None:
+            self._dir.set_state(self.aid, v)
+
+    @property
+    def node(self):
+        return self._node
+
+    @node.setter
+    def node(self, v):
+        self._node = v
+        if self._dir is not None:
+            self._dir.set_node(self.aid, v)
 
 
 class WorkerState:
@@ -224,7 +255,8 @@ class Head:
         self.task_keys: Dict[int, TaskState] = {}
         self._key = 0
         self.actors: Dict[bytes, ActorState] = {}
-        self.named_actors: Dict[tuple, bytes] = {}
+        # actor directory: name / node / placement-group / handle-holder indexes (C++)
+        self.actor_dir = native().ActorDirectory(A_DEAD)
         self.workers: Dict[bytes, WorkerState] = {}
         self.nodes: Dict[str, NodeState] = {}
         self.pgs: Dict[bytes, dict] = {}
@@ -537,7 +569,7 @@ class Head:
             if oid[:1] == b"A":
                 a = self.actors.get(oid[1:])
                 if a is not None:
-                    self._actor_handles(a).add(key)
+                    self.actor_dir.add_handle(a.aid, key)
             return
         if e.state != FREED:
             self.refs.add_holder(oid, key)
@@ -546,7 +578,7 @@ class Head:
         if oid[:1] == b"A" and len(oid) == 21:
             a = self.actors.get(oid[1:])
             if a is not None:
-                self._actor_handles(a).discard(key)
+                self.actor_dir.remove_handle(a.aid, key)
                 self._maybe_kill_unreferenced(a)
             return
         e = self.objects.get(oid)
@@ -554,13 +586,6 @@ class Head:
             return
         if self.refs.remove_holder(oid, key):
             self._maybe_free(e)
-
-    def _actor_handles(self, a):
-        hs = getattr(a, "handles", None)
-        if hs is None:
-            hs = set()
-            a.handles = hs
-        return hs
 
     def _pin(self, oid, n=1):
         e = self.objects.get(oid)
@@ -583,7 +608,7 @@ class Head:
                 self._maybe_kill_unreferenced(a)
 
     def _maybe_kill_unreferenced(self, a):
-        if self._actor_handles(a) or getattr(a, "pins", 0) > 0 or a.detached or a.state == A_DEAD or a.name:
+        if self.actor_dir.num_handles(a.aid) or getattr(a, "pins", 0) > 0 or a.detached or a.state == A_DEAD or a.name:
             return
         if a.queue or a.inflight:
             return  # submitted calls keep the actor alive until they finish (re-checked on completion)
@@ -634,10 +659,9 @@ class Head:
             e = self.objects.get(oid)
             if e is not None:
                 self._maybe_free(e)
-        for a in list(self.actors.values()):
-            hs = getattr(a, "handles", None)
-            if hs and key in hs:
-                hs.discard(key)
+        for aid in self.actor_dir.drop_holder(key):  # only the actors this holder had handles to
+            a = self.actors.get(aid)
+            if a is not None:
                 self._maybe_kill_unreferenced(a)
 
     def _set_ready(self, e: ObjEntry, desc, contained=(), gpu_owner=None, flags=0, gpu_info=None):
@@ -1078,10 +1102,9 @@ class Head:
     def _submit(self, spec, owner):
         tid = spec["tid"]
         if spec["kind"] == "actor_creation" and spec.get("actor_name"):
-            key = (spec.get("namespace", ""), spec["actor_name"])
-            old = self.named_actors.get(key)
-            if old is not None and self.actors.get(old) is not None and self.actors[old].state != A_DEAD:
-                raise ValueError(f"The name {spec['actor_name']} (namespace={key[0]}) is already taken.")
+            ns = spec.get("namespace", "")
+            if not self.actor_dir.name_available(ns, spec["actor_name"]):
+                raise ValueError(f"The name {spec['actor_name']} (namespace={ns}) is already taken.")
         if spec.get("fblob") is not None:
             self.functions.setdefault(spec["fid"], spec.pop("fblob"))
         ts = TaskState(tid, spec, owner)
@@ -1771,20 +1794,14 @@ class Head:
     # ================================================================== actors
     def _create_actor(self, spec, owner, ts):
         aid = spec["actor_id"]
-        a = ActorState(aid, spec, owner)
+        if aid in self.actor_dir:  # a re-submitted creation spec: keep the registered actor
+            self.actor_dir.remove(aid)
+        a = ActorState(aid, spec, owner, self.actor_dir)  # raises if the name is taken (live holder)
         a.creation_task = ts
-        self._actor_handles(a).add(owner)
         self.actors[aid] = a
-        if a.name:
-            key = (a.namespace, a.name)
-            if key in self.named_actors and self.actors.get(self.named_actors[key]) is not None and \
-                    self.actors[self.named_actors[key]].state != A_DEAD:
-                raise ValueError(f"The name {a.name} (namespace={a.namespace}) is already taken.")
-            self.named_actors[key] = aid
 
     def rpc_actor_name_available(self, caller, name, namespace):
-        aid = self.named_actors.get((namespace, name))
-        return aid is None or self.actors.get(aid) is None or self.actors[aid].state == A_DEAD
+        return self.actor_dir.name_available(namespace, name)
 
     def _pump_actor(self, a: ActorState):
         if a.state != A_ALIVE:
@@ -1927,11 +1944,11 @@ class Head:
         return True
 
     def rpc_get_actor(self, caller, name, namespace):
-        aid = self.named_actors.get((namespace, name))
+        aid = self.actor_dir.by_name(namespace, name)
         a = self.actors.get(aid) if aid else None
         if a is None or a.state == A_DEAD:
             return None
-        self._actor_handles(a).add(caller)
+        self.actor_dir.add_handle(a.aid, caller)
         return {"actor_id": a.aid, "meta": a.spec.get("class_meta")}
 
     def rpc_actor_handle(self, caller, aid):
@@ -1939,7 +1956,7 @@ class Head:
         a = self.actors.get(aid)
         if a is None or a.state == A_DEAD:
             return None
-        self._actor_handles(a).add(caller)
+        self.actor_dir.add_handle(a.aid, caller)
         return {"actor_id": a.aid, "meta": a.spec.get("class_meta")}
 
     def rpc_actor_ready(self, caller, aid):
@@ -2274,10 +2291,10 @@ class Head:
             return False
         if pg_id in self.pending_pgs:
             self.pending_pgs.remove(pg_id)
-        # kill actors placed in the group
-        for a in list(self.actors.values()):
-            st = a.spec.get("strategy") or {}
-            if st.get("kind") == "pg" and st.get("pg_id") == pg_id and a.state != A_DEAD:
+        # kill actors placed in the group (the directory's placement-group index)
+        for aid in self.actor_dir.in_pg(pg_id):
+            a = self.actors.get(aid)
+            if a is not None and a.state != A_DEAD:
                 self._kill_actor(a, no_restart=True, reason="placement group removed")
         if pg["state"] == "CREATED":
             self.sched.remove_pg(pg_id.hex())
@@ -2586,7 +2603,7 @@ class Head:
         gauge("rca_object_store_spilled_bytes", "Bytes spilled to disk", [({}, self.spilled_bytes)])
         tc = Counter(TASK_STATE_NAMES[t.state] for t in self.tasks.values())
         gauge("rca_tasks", "Tasks by state", [({"state": k}, v) for k, v in tc.items()])
-        ac = Counter(a.state for a in self.actors.values())
+        ac = self.actor_dir.state_counts()
         gauge("rca_actors", "Actors by state", [({"state": k}, v) for k, v in ac.items()])
         gauge("rca_workers", "Worker processes", [({"node_id": "all"}, len(self.workers))])
         # GPU object store (HBM-resident objects, per physical GPU) and its host spill traffic
