@@ -26,6 +26,8 @@
 // examples (python/ray/train/examples, release/train_tests) — the reference itself has no kernel.
 #include "attention_common.h"
 
+#include <cstdlib>
+
 // dK/dV lives in attention_dkdv.hip (its own register-form flags)
 void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                           const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
@@ -42,7 +44,9 @@ namespace {
 // 2-deep LDS ring so every LDS address is base register + immediate. The online-softmax rescale is
 // deferred (only when a row max grows by > 8 in log2 units: P <= 2^8, exact f32 accumulation)
 // and wave-uniform.
-template <int D, bool CAUSAL>
+// DMA: K/V tiles go HBM -> LDS by buffer_load ... lds (DmaStage) instead of the register-staged
+// global load + ds_write pair (Stage); RCA_ATTN_DMA=0 selects the latter (A/B).
+template <int D, bool CAUSAL, bool DMA>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     bf16_t* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
@@ -78,13 +82,19 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   float m = -INFINITY, lsum = 0.f;
 
   const int ntile = CAUSAL ? (q0 + BQ) / BK : S / BK;  // always even (S % 128 == 0)
-  Stage<D, BK> kst, vst;
+  std::conditional_t<DMA, DmaStage<D, BK>, Stage<D, BK>> kst, vst;
   kst.init(Kb, sk, S, tid);
   vst.init(Vb, sv, S, tid);
-  kst.load(0, sk);
-  vst.load(0, sv);
-  kst.store(smem);
-  vst.store(smem + TILE);
+  if constexpr (DMA) {
+    kst.issue(0, sk, smem);
+    vst.issue(0, sv, smem + TILE);
+    wait_dma();
+  } else {
+    kst.load(0, sk);
+    vst.load(0, sv);
+    kst.store(smem);
+    vst.store(smem + TILE);
+  }
   __syncthreads();
 
   auto tile = [&](auto bufc, int it) {
@@ -94,8 +104,13 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
     const int kb = it * BK;
     const bool more = it + 1 < ntile;
     if (more) {
-      kst.load(kb + BK, sk);
-      vst.load(kb + BK, sv);
+      if constexpr (DMA) {  // into the other buffer: every wave left it at the last barrier
+        kst.issue(kb + BK, sk, smem + (buf ^ 1) * 2 * TILE);
+        vst.issue(kb + BK, sv, smem + (buf ^ 1) * 2 * TILE + TILE);
+      } else {
+        kst.load(kb + BK, sk);
+        vst.load(kb + BK, sv);
+      }
     }
     if (!CAUSAL || kb <= qw0 + 31) {
       // Two 32-key halves, software-pipelined: half 1's S^T MFMAs issue beside half 0's softmax
@@ -149,8 +164,11 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
 #pragma unroll
           for (int db = 0; db < NDB; ++db) {
             const int ts = 2 * t + st;
-            fr[st * NDB + db] = lds_tr8(Vs + tb0 + G8 * (2 * ts) + 512 * db, Vs + tb1 + G8 * (2 * ts + 1) + 512 * db);
+            const char* a0 = Vs + tb0 + G8 * (2 * ts) + 512 * db;
+            const char* a1 = Vs + tb1 + G8 * (2 * ts + 1) + 512 * db;
+            fr[st * NDB + db] = DMA ? lds_tr8_asm(a0, a1) : lds_tr8(a0, a1);
           }
+        if constexpr (DMA) lds_tr_settle(fr);
 #pragma unroll
         for (int db = 0; db < NDB; ++db) o[db] = mfma32(fr[db], p0, o[db]);
 #pragma unroll
@@ -178,8 +196,12 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
       }
     }
     if (more) {
-      kst.store(smem + (buf ^ 1) * 2 * TILE);
-      vst.store(smem + (buf ^ 1) * 2 * TILE + TILE);
+      if constexpr (DMA) {
+        wait_dma();
+      } else {
+        kst.store(smem + (buf ^ 1) * 2 * TILE);
+        vst.store(smem + (buf ^ 1) * 2 * TILE + TILE);
+      }
     }
     __syncthreads();
   };
@@ -201,6 +223,20 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   }
   if (h == 0) LSE[(long)bh * S + qrow] = m + __log2f(lt);
 }
+
+// Explicit instantiations: hipcc (ROCm 7.2) referenced but did not emit the host launch stub of
+// one of the two DMA instances per head size when they were only instantiated through launch_fwd
+// (an undefined __device_stub__ symbol at load time).
+#define RCA_FWD_INST(DD, CC, MM)                                                                          \
+  template __global__ void attn_fwd_kernel<DD, CC, MM>(const bf16_t* __restrict__, const bf16_t* __restrict__, \
+                                                       const bf16_t* __restrict__, bf16_t* __restrict__,        \
+                                                       float* __restrict__, int, int, int, int, long, long, long,  \
+                                                       long, float);
+RCA_FWD_INST(128, false, true)
+RCA_FWD_INST(64, false, true)
+RCA_FWD_INST(128, true, true)
+RCA_FWD_INST(64, true, true)
+#undef RCA_FWD_INST
 
 // ---------------------------------------------------------------------------------------------
 // dQ (query-major twin of the forward: recomputes P from LSE and dP = dO.V^T, accumulates
@@ -353,12 +389,24 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(
   }
 }
 
+bool attn_dma() {
+  static const bool on = [] {
+    const char* e = getenv("RCA_ATTN_DMA");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <int D, bool C>
 void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                 int Hk, long sq, long sk, long sv, long so, float scale2, hipStream_t st) {
   const int grid = B * Hq * (S / 128);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, C>), dim3(grid), dim3(kThreads), 0, st, q, k, v, o, lse, B, S, Hq, Hk, sq,
-                     sk, sv, so, scale2);
+  if (attn_dma())
+    hipLaunchKernelGGL((attn_fwd_kernel<D, C, true>), dim3(grid), dim3(kThreads), 0, st, q, k, v, o, lse, B, S, Hq, Hk,
+                       sq, sk, sv, so, scale2);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<D, C, false>), dim3(grid), dim3(kThreads), 0, st, q, k, v, o, lse, B, S, Hq,
+                       Hk, sq, sk, sv, so, scale2);
 }
 
 template <int D, bool C>

@@ -63,6 +63,27 @@ __device__ __forceinline__ bf16x8_t lds_tr8(const char* p0, const char* p1) {
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// lds_tr8 as inline asm, for kernels that stage tiles by LDS-DMA: hipcc drains every in-flight
+// DMA (vmcnt(0)) before a ds_read_tr16 builtin it cannot prove disjoint from the DMA target,
+// which would serialise the next tile's prefetch with this tile's math. The asm read is invisible
+// to hipcc's counters: call lds_tr_settle() on the results before they are used (it waits
+// lgkmcnt(0) and redefines them, so no consumer is scheduled above the wait).
+__device__ __forceinline__ bf16x8_t lds_tr8_asm(const char* p0, const char* p1) {
+  s16x4 a, b;
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3"
+               : "=&v"(a), "=&v"(b)
+               : "v"((unsigned)(__UINTPTR_TYPE__)p0), "v"((unsigned)(__UINTPTR_TYPE__)p1));
+  s16x8 r = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+template <int N>
+__device__ __forceinline__ void lds_tr_settle(bf16x8_t (&fr)[N]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(fr[i]));
+}
+
 // registers 8s..8s+7 of an accumulator -> bf16 MFMA operand (k-step s)
 __device__ __forceinline__ bf16x8_t acc_to_bf16(const f32x16& x, int s) {
   bf16x8_t r;
@@ -122,6 +143,46 @@ struct Stage {
     for (int i = 0; i < N; ++i) *reinterpret_cast<u32x4*>(lds + loff + i * (RPI / 8) * Img<D>::G8) = r[i];
   }
 };
+
+// [ROWS x D] tile staging HBM -> LDS directly (buffer_load ... lds, no register round trip and
+// no ds_write): the image above is cut into 1-KB blocks, each one 64-lane DMA whose lane l lands
+// at byte 16 l of the block, so each lane fetches the (row, chunk) the image keeps there. Block b
+// (of D/64 per 8-row group): group b / (D/64), subtile pair b % (D/64); lane l -> row
+// 8 group + ((l >> 2) & 7), chunk 4 (2 sub + (l >> 5)) + ((l & 3) ^ ((2 group + ((l >> 4) & 1)) & 3)).
+// A DMA instruction reads 8 rows x 128 contiguous bytes (whole cache lines). Wave w issues
+// blocks w, w + 4, ...; the per-lane offsets depend on the block only through (group parity, sub),
+// so they are computed once and every tile changes one scalar offset.
+template <int D, int ROWS>
+struct DmaStage {
+  static constexpr int BPG = D / 64, NBLK = ROWS / 8 * BPG, NB = NBLK / 4;
+  static_assert(NB >= 1 && NBLK % 4 == 0, "tile must split into 4 waves of 1-KB blocks");
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff[NB];
+  int wave;
+  __device__ __forceinline__ void init(const bf16_t* base, long stride, int rows, int tid, int cols = D) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), (short)0,
+                                             (int)((long)(rows - 1) * stride * 2 + cols * 2), 0x00020000);
+    const int l = tid & 63;
+    wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int b = wave + 4 * i, group = b / BPG, sub = b % BPG;
+      const int row = 8 * group + ((l >> 2) & 7);
+      const int ch = 4 * (2 * sub + (l >> 5)) + ((l & 3) ^ ((2 * group + ((l >> 4) & 1)) & 3));
+      voff[i] = (int)(row * stride * 2 + ch * 16);
+    }
+  }
+  // DMA rows row0 .. row0 + ROWS - 1 (column offset ``extra`` bytes) into the image at ``lds``
+  __device__ __forceinline__ void issue(int row0, long stride, char* lds, int extra = 0) const {
+    const int soff = (int)(row0 * stride * 2) + extra;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(lds + (wave + 4 * i) * 1024), 16, voff[i], soff, 0, 0);
+  }
+};
+
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <int V>
 using IC = std::integral_constant<int, V>;

@@ -173,7 +173,10 @@ RCA_API int rca_gemm_bf16(const void* A, const void* B, void* C, int M, int N, i
   if (M % BM || N % BN || K % 64 || M <= 0 || N <= 0 || K <= 0) return -1;
   if ((lda | ldb | ldc) & 7) return -2;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -2;
-  const int v = gemm_variant();
+  int v = gemm_variant();
+  // k-contiguous (TN) operands: variant 7 (64-deep tiles, full-line DMA) is faster than 3 on
+  // every measured shape (profiles/gemm_r4.md); it falls back to 3 where its contract fails
+  if (v == 3 && !a_kmaj && !b_kmaj) v = 7;
   if (v >= 90) return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, 0, st, v - 90);
   if (v == 3 || v == 5 || v == 6 || v == 7 || (v >= 71 && v <= 78))
     return rca_gemm4_bf16_internal(A, B, C, M, N, K, lda, ldb, ldc, a_kmaj, b_kmaj, accumulate, st, v);

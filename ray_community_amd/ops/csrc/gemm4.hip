@@ -699,8 +699,9 @@ struct Sch7 {
 // the buffer, DMAs every DS MFMAs from B1, W2 = the vmcnt(16) + barrier before the F0(t+1) reads,
 // which then go one per RD MFMAs; F1 reads one per R1 MFMAs from M0; ORD 1 walks the MFMAs with
 // the B-tile fragment (the MFMA's first operand) fixed over 8 consecutive MFMAs instead of the
-// A-tile one. Defaults = variant 7; variants 71-76 are timing A/Bs.
-template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 0, int SPLIT = 0, int EPI = 0>
+// A-tile one. Defaults = variant 7 (= the split schedule, measured best: 24.42 vs 25.26 ms for the
+// 13 TN shapes, gemm_r4.md); variants 71-78 are the timing A/Bs.
+template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 1, int SPLIT = 1, int EPI = 0>
 __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         bf16_t* __restrict__ C, int M, int N, int K, long lda,
                                                         long ldb, long ldc, EpiArgs ep) {
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
   }
 }
 
-template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 0, int SPLIT = 0, int EPI = 0>
+template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 1, int SPLIT = 1, int EPI = 0>
 int launch4c(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
              hipStream_t st, EpiArgs ep = EpiArgs{}) {
   static_assert(SPLIT || (B1 >= 16 * R1 && B1 + 15 * DS < W2 && W2 + 15 * RD < 128), "schedule positions");
@@ -917,12 +918,12 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
     if (!a_kmaj && !b_kmaj && K % 128 == 0 && (double)M * lda * 2 < 4294967296.0 &&
         (double)N * ldb * 2 < 4294967296.0) {
       if (diag >= 71 && accumulate) diag = 7;
-      if (diag == 71) return launch4c<false, 20, 3, 88, 2>(A, B, C, M, N, K, lda, ldb, ldc, st);
-      if (diag == 72) return launch4c<false, 24, 4, 104, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
-      if (diag == 73) return launch4c<false, 32, 4, 100, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
-      if (diag == 74) return launch4c<false, 24, 4, 104, 1, 1, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
-      if (diag == 75) return launch4c<false, 36, 4, 100, 1, 2, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
-      if (diag == 76) return launch4c<false, 36, 4, 100, 1, 2, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 71) return launch4c<false, 20, 3, 88, 2, 1, 0, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 72) return launch4c<false, 24, 4, 104, 1, 1, 0, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 73) return launch4c<false, 32, 4, 100, 1, 1, 0, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 74) return launch4c<false, 24, 4, 104, 1, 1, 1, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 75) return launch4c<false, 36, 4, 100, 1, 2, 0, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
+      if (diag == 76) return launch4c<false, 36, 4, 100, 1, 2, 1, 0>(A, B, C, M, N, K, lda, ldb, ldc, st);
       if (diag == 77) return launch4c<false, 24, 4, 96, 2, 1, 0, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
       if (diag == 78) return launch4c<false, 24, 4, 96, 2, 1, 1, 1>(A, B, C, M, N, K, lda, ldb, ldc, st);
       if (diag == 7) {
@@ -970,5 +971,5 @@ RCA_API int rca_gemm_swiglu_bwd(const void* dy, const void* w_t, const void* gu,
   if (T <= 0 || F <= 0 || H <= 0 || T % 256 || F % 256 || H % 128 || ld_dy % 8 || ld_w % 8) return -1;
   if ((double)T * ld_dy * 2 >= 4294967296.0 || (double)F * ld_w * 2 >= 4294967296.0) return -1;
   EpiArgs ep{(const bf16_t*)gu, (bf16_t*)dgu, (bf16_t*)dgu_t, 2L * F, 2L * F, (long)T, F};
-  return launch4c<false, 36, 4, 100, 1, 2, 1, 0, 1>(dy, w_t, nullptr, T, F, H, ld_dy, ld_w, 0, st, ep);
+  return launch4c<false, 24, 4, 96, 2, 1, 1, 1, 1>(dy, w_t, nullptr, T, F, H, ld_dy, ld_w, 0, st, ep);
 }

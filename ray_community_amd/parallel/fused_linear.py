@@ -44,7 +44,7 @@ class _LinearWgradIntoFlat(torch.autograd.Function):
             x_t, x2 = None, xs.reshape(-1, xs.shape[-1])
         tr = _use_transposed(g2, x2, w, x_t)
         if ctx.needs_input_grad[0]:
-            gx = F.linear(gy, weight_t(w)) if tr else torch.matmul(gy, w)
+            gx = _dgrad(gy, g2, w) if tr else torch.matmul(gy, w)
         else:
             gx = None
         view = _flat_view(w, g2.dtype)
@@ -105,8 +105,27 @@ def swiglu_down(gu, down: "FusedWgradLinear"):
     return down(ops.swiglu(gu))
 
 
-# RCA_FUSE_SWIGLU_BWD=0 keeps the unfused down dgrad (hipBLASLt) + swiglu_bwd_tr pair, for A/B runs
-_FUSE_SWIGLU_BWD = os.environ.get("RCA_FUSE_SWIGLU_BWD", "1") != "0"
+# RCA_FUSE_SWIGLU_BWD=1 selects the fused down dgrad + SwiGLU backward. Off by default: in the 8B
+# step it measured 357.6 vs 354.1 ms/step unfused (profiles/gemm_r4.md): the epilogue still moves
+# g, u, dgu and dgu^T (1.4 GB per layer), so the fusion only saves dh's write + read, less than
+# the hand GEMM's gap to hipBLASLt on this product plus the epilogue's own issue cost.
+_FUSE_SWIGLU_BWD = os.environ.get("RCA_FUSE_SWIGLU_BWD", "0") == "1"
+
+
+# Per-shape input-gradient plans, (out_features, in_features) of the weight -> plan. "hand": the
+# gfx950 GEMM (variant 7) on gy and the W^T copy instead of hipBLASLt. gate_up of the 8B model:
+# 1,564-1,569 vs 1,533 TF/s (profiles/gemm_r4_v7.json, gpurun_out/r4h_gemm.json).
+_DGRAD_PLAN = {(28672, 4096): "hand"}
+_DGRAD_PLANS_ON = os.environ.get("RCA_DGRAD_PLAN", "1") != "0"
+
+
+def _dgrad(gy, g2, w):
+    """gy @ W on the reduction-contiguous W^T copy (hipBLASLt, or the hand GEMM per plan)."""
+    wt = weight_t(w)
+    if _DGRAD_PLANS_ON and _DGRAD_PLAN.get(tuple(w.shape)) == "hand" and ops.gemm_supported(
+            g2.shape[0], wt.shape[0], g2.shape[1], g2, wt):
+        return ops.gemm(g2, wt).view(*gy.shape[:-1], wt.shape[0])
+    return F.linear(gy, wt)
 
 
 def weight_t(w):

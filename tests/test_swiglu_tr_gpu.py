@@ -95,10 +95,12 @@ def test_gemm_swiglu_bwd_fused_matches_fp32(T, H, F):
     assert torch.equal(dgu_t, dgu.t().contiguous())
 
 
-def test_swiglu_down_fused_backward_matches_unfused():
-    """parallel.fused_linear.swiglu_down on the flat-gradient path (fused dgrad + SwiGLU
-    backward) gives the same gate|up gradient and down dW as the unfused ops."""
+def test_swiglu_down_fused_backward_matches_unfused(monkeypatch):
+    """parallel.fused_linear.swiglu_down on the flat-gradient path with the fused dgrad + SwiGLU
+    backward selected gives the same gate|up gradient and down dW as the unfused ops."""
     from ray_community_amd.parallel import fused_linear as fl
+
+    monkeypatch.setattr(fl, "_FUSE_SWIGLU_BWD", True)
 
     torch.manual_seed(5)
     T, H, F = 512, 256, 512
