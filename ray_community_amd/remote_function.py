@@ -34,13 +34,22 @@ def build_resources(opts: dict, default_cpus: float) -> Dict[str, float]:
     return {k: float(v) for k, v in res.items() if v}
 
 
+def _default_strategy():
+    from ._private import core_worker
+
+    core = core_worker._core
+    return getattr(core.ctx, "capture_pg", None) if core is not None else None
+
+
 def build_strategy(opts: dict):
+    s = opts.get("scheduling_strategy")
+    pg = opts.get("placement_group")
+    if (s is None or s == "DEFAULT") and (pg is None or pg == "default"):
+        return _default_strategy()  # the hot path: no per-call imports
     from .util.placement_group import PlacementGroup
     from .util.scheduling_strategies import (NodeAffinitySchedulingStrategy, NodeLabelSchedulingStrategy,
                                              PlacementGroupSchedulingStrategy)
 
-    s = opts.get("scheduling_strategy")
-    pg = opts.get("placement_group")
     if pg is not None and pg != "default" and s is None:
         s = PlacementGroupSchedulingStrategy(pg, opts.get("placement_group_bundle_index", -1),
                                              opts.get("placement_group_capture_child_tasks"))
@@ -75,9 +84,11 @@ def build_strategy(opts: dict):
 def _merge_runtime_env(opts):
     from ._private.worker import _state
 
+    job_env = _state.get("runtime_env") or {}
+    if not job_env and not opts.get("runtime_env"):
+        return None
     from .runtime_env import validate
 
-    job_env = _state.get("runtime_env") or {}
     env = validate(opts.get("runtime_env"))
     if not job_env and not env:
         return None
@@ -106,6 +117,8 @@ class RemoteFunction:
         self._blob = None
         self._fid = None
         self._name = getattr(function, "__name__", "task")
+        self._is_gen = inspect.isgeneratorfunction(function)
+        self._res = None  # build_resources(self._options): the default options never change
         functools.update_wrapper(self, function)
 
     def __call__(self, *args, **kwargs):
@@ -138,6 +151,13 @@ class RemoteFunction:
     def remote(self, *args, **kwargs):
         return self._remote(args, kwargs, self._options)
 
+    def _resources(self, opts):
+        if opts is not self._options:
+            return build_resources(opts, 1)
+        if self._res is None:
+            self._res = build_resources(opts, 1)
+        return dict(self._res)  # the spec may be mutated downstream
+
     def bind(self, *args, **kwargs):
         from .dag.function_node import FunctionNode
 
@@ -156,14 +176,14 @@ class RemoteFunction:
             generator, nret = "dynamic", 1
         else:
             nret = int(num_returns)
-        if inspect.isgeneratorfunction(self._function) and num_returns == 1 and "num_returns" not in opts:
+        if self._is_gen and num_returns == 1 and "num_returns" not in opts:
             generator, nret = "streaming", 1
         enc, kw_names, contained, deps = core.encode_args(args, kwargs)
         tid = new_id()
         rids = return_ids(tid, nret)
         spec = {
             "tid": tid, "kind": "task", "fid": fid, "name": opts.get("name") or self._name, "args": enc,
-            "kw_names": kw_names, "return_ids": rids, "resources": build_resources(opts, 1),
+            "kw_names": kw_names, "return_ids": rids, "resources": self._resources(opts),
             "strategy": build_strategy(opts), "max_retries": opts.get("max_retries", 3),
             "max_calls": int(opts.get("max_calls") or 0),
             "retry_exceptions": opts.get("retry_exceptions", False), "runtime_env": _merge_runtime_env(opts),

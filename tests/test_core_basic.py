@@ -523,3 +523,27 @@ def test_paused_producer_released_on_cancel_and_drop(shutdown_only, tmp_path):
     gc.collect()
     assert wait_closed(p2) == "closed"
     assert ray.get(probe.remote(), timeout=20) == "free"
+
+
+def test_wait_polling_fast_path_semantics(ray_start_regular):
+    """``ready, rest = ray.wait(rest)`` polling (answered from the remainder list without
+    re-validating it) returns every ref exactly once, and a remainder the caller changed is
+    validated again (a duplicate appended to it is rejected)."""
+    import ray_community_amd as ray
+
+    @ray.remote
+    def f(i):
+        return i
+
+    refs = [f.remote(i) for i in range(200)]
+    seen, rest = [], refs
+    while rest:
+        ready, rest = ray.wait(rest)
+        assert len(ready) == 1
+        seen.append(ray.get(ready[0]))
+    assert sorted(seen) == list(range(200))
+    refs = [f.remote(i) for i in range(5)]
+    ready, rest = ray.wait(refs)
+    rest.append(rest[0])
+    with pytest.raises(ValueError, match="unique"):
+        ray.wait(rest)
