@@ -701,7 +701,8 @@ struct Sch7 {
 // the B-tile fragment (the MFMA's first operand) fixed over 8 consecutive MFMAs instead of the
 // A-tile one. Defaults = variant 7 (= the split schedule, measured best: 24.42 vs 25.26 ms for the
 // 13 TN shapes, gemm_r4.md); variants 71-78 are the timing A/Bs.
-template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 1, int SPLIT = 1, int EPI = 0>
+template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 1, int SPLIT = 1, int EPI = 0,
+          int AUX = 0>
 __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         bf16_t* __restrict__ C, int M, int N, int K, long lda,
                                                         long ldb, long ldc, EpiArgs ep) {
@@ -752,11 +753,11 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
     lds_char* st = smem + buf * 2 * TBK;
     if (step < 8)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(st + (4 * step + wid) * 1024),
-                                               16, va[step], soff, 0, 0);
+                                               16, va[step], soff, 0, AUX);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rb, (__attribute__((address_space(3))) void*)(st + TBK + (4 * (step - 8) + wid) * 1024), 16, vb[step - 8],
-          soff, 0, 0);
+          soff, 0, AUX);
   };
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -848,11 +849,12 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
   }
 }
 
-template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 1, int SPLIT = 1, int EPI = 0>
+template <bool ACC, int B1 = 24, int DS = 4, int W2 = 96, int RD = 2, int R1 = 1, int ORD = 1, int SPLIT = 1, int EPI = 0,
+          int AUX = 0>
 int launch4c(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
              hipStream_t st, EpiArgs ep = EpiArgs{}) {
   static_assert(SPLIT || (B1 >= 16 * R1 && B1 + 15 * DS < W2 && W2 + 15 * RD < 128), "schedule positions");
-  auto kern = gemm4c_kernel<ACC, B1, DS, W2, RD, R1, ORD, SPLIT, EPI>;
+  auto kern = gemm4c_kernel<ACC, B1, DS, W2, RD, R1, ORD, SPLIT, EPI, AUX>;
   constexpr int smem = EPI == 1 ? 4 * kEpiWaveLds : 4 * 256 * 128;
   static bool attr = [&] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
