@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Hand-scheduled dK/dV (D = 128, RCA_ATTN_DKDV=hs). Same work split, LDS image and math as the
+// Hand-scheduled dK/dV (D = 128; the default, RCA_ATTN_DKDV=base for the kernel above). Same work split, LDS image and math as the
 // kernel above; what changes is who places the instructions. The compiler-scheduled kernel runs
 // at 38 % MFMA utilisation at one wave per SIMD (profiles/attention_bwd_r3.md): its P/dS VALU
 // work, operand reads and the S/dP -> P/dS -> dV/dK dependencies leave the matrix pipe idle. Here
@@ -231,13 +231,54 @@ __device__ __forceinline__ f32x4 ldsf4(const float* p) {
   return v;
 }
 __device__ __forceinline__ void hs_fence() { __builtin_amdgcn_sched_barrier(0); }
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// compile-time unrolled loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_(f, std::make_integer_sequence<int, N>{});
+}
+// LDS reads as base register + immediate offset (one base VGPR per lane pattern, no per-read
+// address registers)
+template <int OFF>
+__device__ __forceinline__ bf16x8_t ldsq_o(unsigned base) {
+  s16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(OFF));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+template <int OFF>
+__device__ __forceinline__ f32x4 ldsf4_o(unsigned base) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(OFF));
+  return v;
+}
+template <int OFF0, int OFF1>
+__device__ __forceinline__ bf16x8_t ldstr_o(unsigned b0, unsigned b1) {
+  static_assert(OFF0 < 65536 && OFF1 < 65536, "ds offset field is 16 bits");
+  s16x4 a, b;
+  asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%5"
+               : "=&v"(a), "=&v"(b)
+               : "v"(b0), "v"(b1), "n"(OFF0), "n"(OFF1));
+  s16x8 r = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
 __device__ __forceinline__ void hs_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // >= 18 wait states between an XDL write and a VALU read of the result (and the reverse)
 __device__ __forceinline__ void hs_xdl_gap() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory"); }
-#define HS_MFV(acc, a, b) asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
-#define HS_MFA(acc, a, b) asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
+// volatile: kept in the written order relative to the reads and the hazard gaps (a plain asm is
+// free to move across them before instruction selection)
+#define HS_MFV(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
+// S / dP chains with the K / V fragments (B operand) held in accumulator registers: 64 VGPRs freed
+#define HS_MFK(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b))
+#define HS_MFA(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
+// XDL <-> VALU hazard gap that the registers crossing it pass through: the producer stays above it
+// and the consumer below it whatever the compiler reorders
+#define HS_GAP "s_nop 7\n\ts_nop 7\n\ts_nop 4"
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool DMA = true>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
@@ -255,6 +296,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
   const int k0 = kbi * BKV, kw0 = k0 + 32 * w, key = kw0 + l32;
   const int rb0 = Img<D>::row_base(l32, h, 0), rb1 = Img<D>::row_base(l32, h, 1);
   const int tb0 = Img<D>::tr_base(lane, 0), tb1 = Img<D>::tr_base(lane, 1);
+  const unsigned sbase = (unsigned)(__UINTPTR_TYPE__)smem;
+  const unsigned uq0 = sbase + rb0, uq1 = sbase + rb1, ut0 = sbase + tb0, ut1 = sbase + tb1;
+  const unsigned ur = (unsigned)(__UINTPTR_TYPE__)&rowc[0][0][0] + 16 * h;
 
   bf16x8_t kf[NKS], vf[NKS];
   {
@@ -266,9 +310,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
       vf[kk] = gload8(Vr + 16 * kk + 8 * h);
     }
 #pragma unroll
-    for (int kk = 0; kk < NKS; ++kk) {
-      settle(kf[kk]);
-      settle(vf[kk]);
+    for (int kk = 0; kk < NKS; ++kk) {  // resident in accumulator registers (the asm operands are "a")
+      asm volatile("" : "+a"(kf[kk]));
+      asm volatile("" : "+a"(vf[kk]));
     }
   }
   f32x16 dk[NDB], dv[NDB];
@@ -281,19 +325,29 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
   const int qs0 = CAUSAL ? k0 : 0;
   const int nsl = (S - qs0) / BQS;
   const int total = G * nsl;  // even
-  DmaStage<D, BQS> qst, gst;
+  std::conditional_t<DMA, DmaStage<D, BQS>, Stage<D, BQS>> qst, gst;
   qst.init(Q + (long)b * S * sq + (long)hk * G * D, sq, S, tid, G * D);
   gst.init(dO + (long)b * S * sdo + (long)hk * G * D, sdo, S, tid, G * D);
   const float* rsrc = (tid < BQS ? LSE : Delta) + ((long)b * Hq + hk * G) * S + (tid & (BQS - 1));
   float rc = 0.f;
   auto stage_issue = [&](int g, int sl, int buf) {
     const int qa = qs0 + sl * BQS;
-    qst.issue(qa, sq, smem + buf * 2 * SL, g * D * 2);
-    gst.issue(qa, sdo, smem + buf * 2 * SL + SL, g * D * 2);
+    if constexpr (DMA) {
+      qst.issue(qa, sq, smem + buf * 2 * SL, g * D * 2);
+      gst.issue(qa, sdo, smem + buf * 2 * SL + SL, g * D * 2);
+    } else {
+      qst.load(qa, sq, g * D * 2);
+      gst.load(qa, sdo, g * D * 2);
+    }
     if (tid < 2 * BQS) rc = rsrc[(long)g * S + qa];
   };
   auto stage_finish = [&](int buf) {
-    wait_dma();
+    if constexpr (DMA) {
+      wait_dma();
+    } else {
+      qst.store(smem + buf * 2 * SL);
+      gst.store(smem + buf * 2 * SL + SL);
+    }
     if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = -rc;  // -lse, -delta
   };
   stage_issue(0, nsl - 1, 0);
@@ -311,52 +365,29 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
     if (!CAUSAL || qa + BQS - 1 >= kw0) {
       auto body = [&](auto diagc) {
         constexpr bool DIAG = decltype(diagc)::value;
-        auto roff = [&](int kk, int t) { return ((kk & 1) ? rb1 : rb0) + 4 * G8 * t + 512 * (kk >> 1); };
-        // ---- P0: R_0, the row constants of both halves
-        bf16x8_t fq[NKS], fg[NKS];
-#pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) {
-          fq[kk] = ldsq(Qs + roff(kk, 0));
-          fg[kk] = ldsq(Gs + roff(kk, 0));
-        }
-        f32x4 nl[2][4], nd[2][4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            nl[t][g4] = ldsf4(&rowc[buf][0][32 * t + 8 * g4 + 4 * h]);
-            nd[t][g4] = ldsf4(&rowc[buf][1][32 * t + 8 * g4 + 4 * h]);
-          }
-        hs_lgkm0();
-        hs_fence();
-        f32x16 s0 = zero16(), s1 = zero16(), dp0, dp1;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            dp0[4 * g4 + j] = nd[0][g4][j];
-            dp1[4 * g4 + j] = nd[1][g4][j];
-          }
-        hs_fence();
-        // ---- P1: S_0 / dP_0 chains + R_1 reads into the freed fragment registers
-        bf16x8_t fq1[NKS], fg1[NKS];
-#pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) {
-          hs_fence();
-          HS_MFV(s0, fq[kk], kf[kk]);
-          hs_fence();
-          fq1[kk] = ldsq(Qs + roff(kk, 1));
-          hs_fence();
-          HS_MFV(dp0, fg[kk], vf[kk]);
-          hs_fence();
-          fg1[kk] = ldsq(Gs + roff(kk, 1));
-        }
-        hs_fence();
-        hs_lgkm0();
-        hs_xdl_gap();
-        hs_fence();
-        // P/dS of half t, element r (one per MFMA slot): p = exp2(S c - lse), dS' = p (dP - delta)
+        constexpr int BO = buf * 2 * SL;  // this slice's buffer; Q image at BO, dO image at BO + SL
+        // row operand (kk, half t) of Q (G = 0) or dO (G = 1): base (kk odd ? uq1 : uq0) + immediate
+        auto rowread = [&](auto kkc, auto tc, auto gc) {
+          constexpr int kk = decltype(kkc)::value, t = decltype(tc)::value, g = decltype(gc)::value;
+          constexpr int off = BO + g * SL + 4 * G8 * t + 512 * (kk >> 1);
+          return ldsq_o<off>((kk & 1) ? uq1 : uq0);
+        };
+        // transposed operand f of half t: f = (2 st + isq) NDB + db; isq 0: dO^T, 1: Q^T
+        auto trread = [&](auto fc, auto tc) {
+          constexpr int f = decltype(fc)::value, t = decltype(tc)::value;
+          constexpr int st = (f / NDB) >> 1, db = f % NDB, isq = (f / NDB) & 1;
+          constexpr int base = BO + (isq ? 0 : SL) + 512 * db;
+          return ldstr_o<base + G8 * (4 * t + 2 * st), base + G8 * (4 * t + 2 * st + 1)>(ut0, ut1);
+        };
+        auto rowc4 = [&](auto cc, auto tc, auto g4c) {  // -lse (c 0) / -delta (c 1) of rows 32t + 8g4 + 4h ..
+          constexpr int c = decltype(cc)::value, t = decltype(tc)::value, g4 = decltype(g4c)::value;
+          return ldsf4_o<((buf * 2 + c) * BQS + 32 * t + 8 * g4) * 4>(ur);
+        };
+        // MFMA q (0..15) of a dV/dK phase reads transposed operand fq_of(q)
+        auto fq_of = [](int q) { return (2 * (q >> 3) + (q & 1)) * NDB + ((q >> 1) & 3); };
         const int kq0 = key - qa - 4 * h;
+        f32x4 nl[2][4], nd[4];
+        // P/dS of half t, element r (one per MFMA slot): p = exp2(S c - lse), dS' = p (dP - delta)
         auto pds1 = [&](f32x16& sx, f32x16& dx, int t, int r) {
           const int g4 = r >> 2, j = r & 3;
           float p = fast_exp2(fmaf(sx[r], scale2, nl[t][g4][j]));
@@ -364,97 +395,132 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
           sx[r] = p;
           dx[r] = p * dx[r];
         };
-        // transposed operand f (0..15) of half t: f = (2*st + isq) * NDB + db, st = k-step of the
-        // 32-row half, isq 0: dO^T (-> dV), 1: Q^T (-> dK); read just in time, TW operands ahead
-        constexpr int TW = 4;
-        auto trd = [&](int t, int f) {
-          const int st = (f / NDB) >> 1, db = f % NDB, isq = (f / NDB) & 1;
-          const int o0 = tb0 + G8 * (4 * t + 2 * st) + 512 * db, o1 = tb1 + G8 * (4 * t + 2 * st + 1) + 512 * db;
-          return lds_tr8_asm((isq ? Qs : Gs) + o0, (isq ? Qs : Gs) + o1);
-        };
-        // MFMA q (0..15) of the dV/dK phase: operand f = (2*st + isdk)*NDB + db with st = q >> 3,
-        // db = (q >> 1) & 3, isdk = q & 1 -> f order matches q order below (q -> f(q))
-        auto fq_of = [](int q) { return (2 * (q >> 3) + (q & 1)) * NDB + ((q >> 1) & 3); };
-        // ---- P2: S_1 / dP_1 chains + P/dS of half 0; the first TW T_0 operands at the end
-        bf16x8_t pa0, pb0, da0, db0;
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        // ---- P0: R_0 and half 0's row constants (half 1's are read at the end of P1, and its
+        // chains initialised at the start of P2: fewer registers live across P1)
+        bf16x8_t fq[NKS], fg[NKS];
+        sfor<NKS>([&](auto kkc) {
+          constexpr int kk = decltype(kkc)::value;
+          fq[kk] = rowread(kkc, I0{}, I0{});
+          fg[kk] = rowread(kkc, I0{}, I1{});
+        });
+        sfor<4>([&](auto g4c) {
+          constexpr int g4 = decltype(g4c)::value;
+          nl[0][g4] = rowc4(I0{}, I0{}, g4c);
+          nd[g4] = rowc4(I1{}, I0{}, g4c);
+        });
+        hs_lgkm0();
+        hs_fence();
+        f32x16 s0 = zero16(), s1, dp0, dp1;
 #pragma unroll
-        for (int kk = 0; kk < NKS; ++kk) {
+        for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dp0[4 * g4 + j] = nd[g4][j];
+        hs_fence();
+        asm volatile(HS_GAP : "+v"(s0), "+v"(dp0));  // chain inits (VALU) before the first MFMAs read them
+        hs_fence();
+        // ---- P1: S_0 / dP_0 chains + R_1 reads into the freed fragment registers
+        bf16x8_t fq1[NKS], fg1[NKS];
+        sfor<NKS>([&](auto kkc) {
+          constexpr int kk = decltype(kkc)::value;
           hs_fence();
-          HS_MFV(s1, fq1[kk], kf[kk]);
+          HS_MFK(s0, fq[kk], kf[kk]);
+          hs_fence();
+          fq1[kk] = rowread(kkc, I1{}, I0{});
+          hs_fence();
+          HS_MFK(dp0, fg[kk], vf[kk]);
+          hs_fence();
+          fg1[kk] = rowread(kkc, I1{}, I1{});
+        });
+        hs_fence();
+        sfor<4>([&](auto g4c) {
+          constexpr int g4 = decltype(g4c)::value;
+          nl[1][g4] = rowc4(I0{}, I1{}, g4c);
+          nd[g4] = rowc4(I1{}, I1{}, g4c);
+        });
+        hs_lgkm0();
+        hs_fence();
+        s1 = zero16();
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dp1[4 * g4 + j] = nd[g4][j];
+        hs_fence();
+        // S_0 / dP_0 results before the VALU reads them; S_1 / dP_1 inits before the MFMAs
+        asm volatile(HS_GAP : "+v"(s0), "+v"(dp0), "+v"(s1), "+v"(dp1));
+        hs_fence();
+        // ---- P2: S_1 / dP_1 chains + P/dS of half 0; the first TW T_0 operands at the end
+        constexpr int TW = 4;
+        bf16x8_t pa0, pb0, da0, db0;
+        sfor<NKS>([&](auto kkc) {
+          constexpr int kk = decltype(kkc)::value;
+          hs_fence();
+          HS_MFK(s1, fq1[kk], kf[kk]);
           hs_fence();
           pds1(s0, dp0, 0, 2 * kk);
           hs_fence();
-          HS_MFV(dp1, fg1[kk], vf[kk]);
+          HS_MFK(dp1, fg1[kk], vf[kk]);
           hs_fence();
           pds1(s0, dp0, 0, 2 * kk + 1);
-          if (kk == 3) {
+          if constexpr (kk == 3) {
             pa0 = acc_to_bf16(s0, 0);
             da0 = acc_to_bf16(dp0, 0);
           }
-        }
+        });
         hs_fence();
         pb0 = acc_to_bf16(s0, 1);
         db0 = acc_to_bf16(dp0, 1);
         bf16x8_t tw[16];
-#pragma unroll
-        for (int q = 0; q < TW; ++q) tw[q] = trd(0, fq_of(q));
-        hs_xdl_gap();
+        sfor<TW>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          tw[q] = trread(std::integral_constant<int, (2 * (q >> 3) + (q & 1)) * NDB + ((q >> 1) & 3)>{}, I0{});
+        });
+        asm volatile(HS_GAP : "+v"(s1), "+v"(dp1), "+v"(pa0), "+v"(pb0), "+v"(da0), "+v"(db0));
         hs_fence();
         // ---- P3: dV, dK += half 0 (T_0 read TW ahead) + P/dS of half 1
         bf16x8_t pa1, pb1, da1, db1;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
+        auto dvdk_slot = [&](auto qc, auto tc, const bf16x8_t& pa, const bf16x8_t& pb, const bf16x8_t& da,
+                             const bf16x8_t& dbb) {
+          constexpr int q = decltype(qc)::value;
+          constexpr int later = (q + TW < 16 ? TW - 1 : 15 - q);
           hs_fence();
-          // T_0 operand q landed: the 2 * (later reads in flight) newest LDS ops may stay pending
-          {
-            const int later = (q + TW < 16 ? TW - 1 : 15 - q);
-            if (later >= 3) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-            else if (later == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-            else if (later == 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * later) : "memory");  // operand q landed
+          hs_fence();
+          constexpr int st = q >> 3, db = (q >> 1) & 3;
+          if constexpr (q & 1) {
+            HS_MFA(dk[db], tw[q], st ? dbb : da);
+          } else {
+            HS_MFA(dv[db], tw[q], st ? pb : pa);
           }
           hs_fence();
-          {
-            const int st = q >> 3, db = (q >> 1) & 3;
-            if (q & 1) HS_MFA(dk[db], tw[q], st ? db0 : da0);
-            else HS_MFA(dv[db], tw[q], st ? pb0 : pa0);
-          }
-          hs_fence();
-          if (q + TW < 16) tw[q + TW] = trd(0, fq_of(q + TW));
+          if constexpr (q + TW < 16)
+            tw[q + TW] = trread(
+                std::integral_constant<int, (2 * ((q + TW) >> 3) + ((q + TW) & 1)) * NDB + (((q + TW) >> 1) & 3)>{},
+                tc);
+        };
+        sfor<16>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          dvdk_slot(qc, I0{}, pa0, pb0, da0, db0);
           pds1(s1, dp1, 1, q);
-          if (q == 7) {
+          if constexpr (q == 7) {
             pa1 = acc_to_bf16(s1, 0);
             da1 = acc_to_bf16(dp1, 0);
           }
-        }
+        });
         hs_fence();
         pb1 = acc_to_bf16(s1, 1);
         db1 = acc_to_bf16(dp1, 1);
-#pragma unroll
-        for (int q = 0; q < TW; ++q) tw[q] = trd(1, fq_of(q));
-        hs_xdl_gap();
+        sfor<TW>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          tw[q] = trread(std::integral_constant<int, (2 * (q >> 3) + (q & 1)) * NDB + ((q >> 1) & 3)>{}, I1{});
+        });
+        asm volatile(HS_GAP : "+v"(pa1), "+v"(pb1), "+v"(da1), "+v"(db1));
         hs_fence();
         // ---- P4: dV, dK += half 1 (T_1 read TW ahead)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          hs_fence();
-          {
-            const int later = (q + TW < 16 ? TW - 1 : 15 - q);
-            if (later >= 3) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-            else if (later == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-            else if (later == 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-          hs_fence();
-          {
-            const int st = q >> 3, db = (q >> 1) & 3;
-            if (q & 1) HS_MFA(dk[db], tw[q], st ? db1 : da1);
-            else HS_MFA(dv[db], tw[q], st ? pb1 : pa1);
-          }
-          hs_fence();
-          if (q + TW < 16) tw[q + TW] = trd(1, fq_of(q + TW));
-        }
+        sfor<16>([&](auto qc) { dvdk_slot(qc, I1{}, pa1, pb1, da1, db1); });
         hs_fence();
+        (void)fq_of;
       };
       if (CAUSAL && qa < kw0 + 31) body(std::integral_constant<bool, CAUSAL>{});
       else body(std::false_type{});
@@ -486,20 +552,39 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
   }
 }
 #undef HS_MFV
+#undef HS_MFK
+#undef HS_GAP
 #undef HS_MFA
 
-template __global__ void attn_bwd_dkdv_hs_kernel<true>(const bf16_t* __restrict__, const bf16_t* __restrict__,
-                                                        const bf16_t* __restrict__, const bf16_t* __restrict__,
-                                                        const float* __restrict__, const float* __restrict__,
-                                                        bf16_t* __restrict__, bf16_t* __restrict__, int, int, int,
-                                                        int, long, long, long, long, long, long, float, float);
-template __global__ void attn_bwd_dkdv_hs_kernel<false>(const bf16_t* __restrict__, const bf16_t* __restrict__,
-                                                         const bf16_t* __restrict__, const bf16_t* __restrict__,
-                                                         const float* __restrict__, const float* __restrict__,
-                                                         bf16_t* __restrict__, bf16_t* __restrict__, int, int, int,
-                                                         int, long, long, long, long, long, long, float, float);
+#define RCA_HS_INST(CC, MM)                                                                                       \
+  template __global__ void attn_bwd_dkdv_hs_kernel<CC, MM>(                                                     \
+      const bf16_t* __restrict__, const bf16_t* __restrict__, const bf16_t* __restrict__, const bf16_t* __restrict__, \
+      const float* __restrict__, const float* __restrict__, bf16_t* __restrict__, bf16_t* __restrict__, int, int, int, \
+      int, long, long, long, long, long, long, float, float);
+RCA_HS_INST(true, true)
+RCA_HS_INST(false, true)
+RCA_HS_INST(true, false)
+RCA_HS_INST(false, false)
+#undef RCA_HS_INST
 
 }  // namespace
+
+// The hand-scheduled dK/dV kernel is the default for D = 128 (RCA_ATTN_DKDV=base selects the
+// compiler-scheduled one); rca_attn_set_dkdv_hs switches at run time (same-process A/B and the
+// equivalence test), returning the previous setting.
+static bool g_dkdv_hs = [] {
+  const char* e = getenv("RCA_ATTN_DKDV");
+  return !(e && std::string(e) == "base");
+}();
+static bool g_dkdv_hs_stage = false;
+// 0: compiler-scheduled kernel; 1: hand-scheduled (LDS-DMA staging); 2: hand-scheduled with
+// register staging
+RCA_API int rca_attn_set_dkdv_hs(int on) {
+  const int old = g_dkdv_hs ? (g_dkdv_hs_stage ? 2 : 1) : 0;
+  g_dkdv_hs = on != 0;
+  g_dkdv_hs_stage = on == 2;
+  return old;
+}
 
 void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                           const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
@@ -511,18 +596,18 @@ void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, 
     const char* e = getenv("RCA_ATTN_DKDV_NH");
     return e && atoi(e) == 1 ? 1 : 2;
   }();
-  static const bool hs = [] {
-    const char* e = getenv("RCA_ATTN_DKDV");
-    return e && std::string(e) == "hs";
-  }();
+  const bool hs = g_dkdv_hs;
   const dim3 grid(B * Hk * (S / 128)), block(kThreads);
   if (hs && D == 128) {
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<true>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, B, S,
-                         Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<false>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, B,
-                         S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale);
+#define RCA_HS(CC, MM)                                                                                         \
+  hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<CC, MM>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, B, S, \
+                     Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale)
+    if (g_dkdv_hs_stage) {  // register staging (bisect / A/B)
+      if (causal) RCA_HS(true, false); else RCA_HS(false, false);
+    } else {
+      if (causal) RCA_HS(true, true); else RCA_HS(false, true);
+    }
+#undef RCA_HS
     return;
   }
 #define RCA_DKDV(DD, CC, NN)                                                                                           \
