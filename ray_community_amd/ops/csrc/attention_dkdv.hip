@@ -591,7 +591,7 @@ void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, 
                           long sq, long sk, long sv, long sdo, long sdk, long sdv, float scale2, float scale,
                           hipStream_t st) {
   // RCA_ATTN_DKDV_NH=1 selects the unpipelined 32-row-slice variant (A/B measurements);
-  // RCA_ATTN_DKDV=hs the hand-scheduled kernel (D = 128)
+  // the hand-scheduled kernel for D = 128 unless RCA_ATTN_DKDV=base (g_dkdv_hs)
   static const int nh = [] {
     const char* e = getenv("RCA_ATTN_DKDV_NH");
     return e && atoi(e) == 1 ? 1 : 2;
