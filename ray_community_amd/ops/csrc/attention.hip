@@ -33,6 +33,10 @@ void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, 
                           const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
                           long sq, long sk, long sv, long sdo, long sdk, long sdv, float scale2, float scale,
                           hipStream_t st);
+// 64-query-rows-per-wave forward (attention_fwd_wide.hip); false = not selected for this shape
+bool rca_attn_launch_fwd_wide(bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
+                              int B, int S, int Hq, int Hk, long sq, long sk, long sv, long so, float scale2,
+                              hipStream_t st);
 
 namespace {
 
@@ -400,6 +404,7 @@ bool attn_dma() {
 template <int D, bool C>
 void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                 int Hk, long sq, long sk, long sv, long so, float scale2, hipStream_t st) {
+  if (D == 128 && rca_attn_launch_fwd_wide(C, q, k, v, o, lse, B, S, Hq, Hk, sq, sk, sv, so, scale2, st)) return;
   const int grid = B * Hq * (S / 128);
   if (attn_dma())
     hipLaunchKernelGGL((attn_fwd_kernel<D, C, true>), dim3(grid), dim3(kThreads), 0, st, q, k, v, o, lse, B, S, Hq, Hk,
