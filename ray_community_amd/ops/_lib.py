@@ -33,7 +33,7 @@ _SIGS = {
                               c_void_p]),
     "rca_gemm_set_variant": (c_int, [c_int]),
     "rca_attn_set_dkdv_hs": (c_int, [c_int]),
-    "rca_attn_set_fwd_wide": (c_int, [c_int]),
+    "rca_attn_set_fwd_mode": (c_int, [c_int]),
     "rca_gemm_swiglu_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_ll,
                                     c_void_p]),
     "rca_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_ll, c_void_p]),

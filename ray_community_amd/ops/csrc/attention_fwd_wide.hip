@@ -1,4 +1,4 @@
-// Wide-row flash-attention forward for gfx950 (D = 128; RCA_ATTN_FWD=wide). Same math, LDS image
+// Wide-row flash-attention forward for gfx950 (D = 128; RCA_ATTN_FWD=wide, opt-in). Same math, LDS image
 // and LDS-DMA K/V staging as attn_fwd_kernel (attention.hip), but each wave owns 64 query rows
 // (two 32-row groups) instead of 32: every K fragment read from LDS feeds the S^T MFMAs of both
 // groups and every V^T fragment the P.V MFMAs of both, halving the LDS bytes per MFMA. The
@@ -121,9 +121,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_wide_kernel(
         p0 = acc_to_bf16(sx, 0);
         p1 = acc_to_bf16(sx, 1);
       };
-      // O^T += V^T P^T for half t, both groups: one V^T burst, each fragment feeds two MFMAs
-      auto pv = [&](int t, const bf16x8_t (&p)[2][2]) {
-        bf16x8_t fr[2 * NDB];
+      // O^T += V^T P^T for half t, both groups: one V^T burst, each fragment feeds two MFMAs. The
+      // reads go out a phase ahead of their MFMAs (vread), so their latency hides under the softmax.
+      auto vread = [&](int t, bf16x8_t (&fr)[2 * NDB]) {
 #pragma unroll
         for (int st = 0; st < 2; ++st)
 #pragma unroll
@@ -131,6 +131,8 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_wide_kernel(
             const int ts = 2 * t + st;
             fr[st * NDB + db] = lds_tr8_asm(Vs + tb0 + G8 * (2 * ts) + 512 * db, Vs + tb1 + G8 * (2 * ts + 1) + 512 * db);
           }
+      };
+      auto pv = [&](bf16x8_t (&fr)[2 * NDB], const bf16x8_t (&p)[2][2]) {
         lds_tr_settle(fr);
 #pragma unroll
         for (int st = 0; st < 2; ++st)
@@ -143,7 +145,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_wide_kernel(
       // half 1's S^T MFMAs beside half 0's softmax, half 0's P.V beside half 1's row maxima
       auto run = [&](auto diagc) {
         f32x16 s0[2], s1[2];
+        bf16x8_t v0[2 * NDB], v1[2 * NDB];
         qk(0, s0, diagc);
+        vread(0, v0);
         rescale(0, xhalf_max(max16(s0[0], -INFINITY)));
         rescale(1, xhalf_max(max16(s0[1], -INFINITY)));
         qk(1, s1, diagc);
@@ -151,13 +155,14 @@ __global__ __launch_bounds__(kThreads, 1) void attn_fwd_wide_kernel(
         softmax(0, s0[0], p0[0][0], p0[0][1]);
         softmax(1, s0[1], p0[1][0], p0[1][1]);
         const float mt10 = xhalf_max(max16(s1[0], -INFINITY)), mt11 = xhalf_max(max16(s1[1], -INFINITY));
-        pv(0, p0);
+        pv(v0, p0);
+        vread(1, v1);
         rescale(0, mt10);
         rescale(1, mt11);
         bf16x8_t p1[2][2];
         softmax(0, s1[0], p1[0][0], p1[0][1]);
         softmax(1, s1[1], p1[1][0], p1[1][1]);
-        pv(1, p1);
+        pv(v1, p1);
       };
       if (CAUSAL && kb + BK - 1 > qw0) {
         run(std::integral_constant<bool, CAUSAL>{});
@@ -202,14 +207,16 @@ template __global__ void attn_fwd_wide_kernel<false>(const bf16_t* __restrict__,
 
 }  // namespace
 
-// RCA_ATTN_FWD=wide (or rca_attn_set_fwd_wide) selects this kernel for D = 128, S % 256 == 0.
-static bool g_fwd_wide = [] {
+// Forward kernel choice for D = 128 (A/B): 0 = 32 rows per wave (default), 1 = this kernel
+// (RCA_ATTN_FWD=wide; S % 256 == 0). Also measured and dropped: the 32-row kernel with
+// s_setprio(1) around its MFMA clusters, 0.296 vs 0.288 ms (profiles/attn_fwd_wide_ab_r4.log).
+static int g_fwd_mode = [] {
   const char* e = getenv("RCA_ATTN_FWD");
-  return e && e[0] == 'w';
+  return e && e[0] == 'w' ? 1 : 0;
 }();
-RCA_API int rca_attn_set_fwd_wide(int on) {
-  const int old = g_fwd_wide ? 1 : 0;
-  g_fwd_wide = on != 0;
+RCA_API int rca_attn_set_fwd_mode(int mode) {
+  const int old = g_fwd_mode;
+  g_fwd_mode = mode;
   return old;
 }
 
@@ -217,7 +224,7 @@ RCA_API int rca_attn_set_fwd_wide(int on) {
 bool rca_attn_launch_fwd_wide(bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
                               int B, int S, int Hq, int Hk, long sq, long sk, long sv, long so, float scale2,
                               hipStream_t st) {
-  if (!g_fwd_wide || S % 256) return false;
+  if (g_fwd_mode != 1 || S % 256) return false;
   const dim3 grid(B * Hq * (S / 256)), block(kThreads);
   if (causal)
     hipLaunchKernelGGL((attn_fwd_wide_kernel<true>), grid, block, 0, st, q, k, v, o, lse, B, S, Hq, Hk, sq, sk, sv, so,

@@ -38,14 +38,14 @@ def main():
               f"(bwd {tfb - tf:.3f} ms, {2.5 * flops_f / (tfb - tf) / 1e9:.0f} TF)", flush=True)
 
     run("rca-hip", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
-    if os.environ.get("ATTN_WIDE_AB"):  # interleaved A/B of the 32- and 64-rows-per-wave forward
+    if os.environ.get("ATTN_WIDE_AB"):  # interleaved A/B of the forward variants
         lib = ops._lib.lib()
         for _ in range(3):
-            for wide in (0, 1):
-                prev = lib.rca_attn_set_fwd_wide(wide)
-                run(f"fwd-{'wide' if wide else 'narrow'}",
+            for mode in (0, 1):
+                prev = lib.rca_attn_set_fwd_mode(mode)
+                run(f"fwd-{('narrow', 'wide')[mode]}",
                     lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
-                lib.rca_attn_set_fwd_wide(prev)
+                lib.rca_attn_set_fwd_mode(prev)
 
     def sdpa():
         q = qkv[:, : Hq * D].view(B, S, Hq, D).transpose(1, 2)
