@@ -28,7 +28,7 @@ EXTRA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
 # max-memory-clause and iterative-minreg were 2-8 % slower; scripts/ab_sched_build.sh,
 # scripts/gpu_r3_q.sh, profiles/attn_sched_r3.log).
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-FILE_FLAGS = {"attention_dkdv.hip": _ILP, "attention_fwd_wide.hip": _ILP, "gemm4.hip": [],
+FILE_FLAGS = {"attention_dkdv.hip": _ILP, "attention_fwd_wide.hip": _ILP, "attention_fwd_hs.hip": _ILP, "gemm4.hip": [],
               "attention.hip": EXTRA_FLAGS + _ILP}
 
 

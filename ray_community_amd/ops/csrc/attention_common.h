@@ -172,6 +172,11 @@ struct DmaStage {
       voff[i] = (int)(row * stride * 2 + ch * 16);
     }
   }
+  // one of this wave's NB 1-KB pieces (hand-scheduled kernels spread them over MFMA phases)
+  __device__ __forceinline__ void issue_one(int i, int row0, long stride, char* lds) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + (wave + 4 * i) * 1024),
+                                             16, voff[i], __builtin_amdgcn_readfirstlane((int)(row0 * stride * 2)), 0, 0);
+  }
   // DMA rows row0 .. row0 + ROWS - 1 (column offset ``extra`` bytes) into the image at ``lds``
   __device__ __forceinline__ void issue(int row0, long stride, char* lds, int extra = 0) const {
     const int soff = (int)(row0 * stride * 2) + extra;

@@ -207,12 +207,13 @@ template __global__ void attn_fwd_wide_kernel<false>(const bf16_t* __restrict__,
 
 }  // namespace
 
-// Forward kernel choice for D = 128 (A/B): 0 = 32 rows per wave (default), 1 = this kernel
-// (RCA_ATTN_FWD=wide; S % 256 == 0). Also measured and dropped: the 32-row kernel with
+// Forward kernel choice for D = 128 (A/B): 0 = 32 rows per wave (attention.hip), 1 = this
+// kernel (RCA_ATTN_FWD=wide), 2 = the hand-scheduled 64-row kernel (attention_fwd_hs.hip,
+// RCA_ATTN_FWD=hs); 1 and 2 need S % 256 == 0. Also measured and dropped: the 32-row kernel with
 // s_setprio(1) around its MFMA clusters, 0.296 vs 0.288 ms (profiles/attn_fwd_wide_ab_r4.log).
 static int g_fwd_mode = [] {
   const char* e = getenv("RCA_ATTN_FWD");
-  return e && e[0] == 'w' ? 1 : 0;
+  return !e ? 0 : e[0] == 'w' ? 1 : e[0] == 'h' ? 2 : 0;
 }();
 RCA_API int rca_attn_set_fwd_mode(int mode) {
   const int old = g_fwd_mode;
@@ -220,10 +221,15 @@ RCA_API int rca_attn_set_fwd_mode(int mode) {
   return old;
 }
 
-// Returns false when the wide kernel does not take the shape (the caller runs the 32-row one).
+bool rca_attn_launch_fwd_hs(bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
+                            int B, int S, int Hq, int Hk, long sq, long sk, long sv, long so, float scale2,
+                            hipStream_t st);
+
+// Returns false when no 64-row kernel is selected for the shape (the caller runs the 32-row one).
 bool rca_attn_launch_fwd_wide(bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
                               int B, int S, int Hq, int Hk, long sq, long sk, long sv, long so, float scale2,
                               hipStream_t st) {
+  if (g_fwd_mode == 2) return rca_attn_launch_fwd_hs(causal, q, k, v, o, lse, B, S, Hq, Hk, sq, sk, sv, so, scale2, st);
   if (g_fwd_mode != 1 || S % 256) return false;
   const dim3 grid(B * Hq * (S / 256)), block(kThreads);
   if (causal)

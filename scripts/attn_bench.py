@@ -41,9 +41,9 @@ def main():
     if os.environ.get("ATTN_WIDE_AB"):  # interleaved A/B of the forward variants
         lib = ops._lib.lib()
         for _ in range(3):
-            for mode in (0, 1):
+            for mode in (0, 1, 2):
                 prev = lib.rca_attn_set_fwd_mode(mode)
-                run(f"fwd-{('narrow', 'wide')[mode]}",
+                run(f"fwd-{('narrow', 'wide', 'hs')[mode]}",
                     lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
                 lib.rca_attn_set_fwd_mode(prev)
 

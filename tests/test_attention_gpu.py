@@ -119,7 +119,7 @@ def test_flash_attention_bitwise_deterministic(B, S, Hq, Hk, D):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", [1])
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("B,S,Hq,Hk,causal", [(2, 256, 4, 2, True), (1, 384, 4, 4, False), (1, 512, 8, 2, True),
                                               (2, 256, 8, 1, False)])
 def test_dkdv_hand_scheduled_matches_compiler_scheduled(B, S, Hq, Hk, causal, mode):
@@ -144,11 +144,12 @@ def test_dkdv_hand_scheduled_matches_compiler_scheduled(B, S, Hq, Hk, causal, mo
     assert _err(k1, k0) < 1e-2 and _err(v1, v0) < 1e-2, (_err(k1, k0), _err(v1, v0))
 
 
-@pytest.mark.parametrize("mode", [1])
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("B,S,Hq,Hk,causal", [(2, 256, 4, 2, True), (1, 512, 4, 4, False), (1, 1024, 8, 2, True),
                                               (2, 768, 8, 1, False), (1, 4096, 2, 1, True)])
 def test_fwd_variants_match_reference_and_default(B, S, Hq, Hk, causal, mode):
-    """The opt-in forward variants (1: 64 rows per wave, attention_fwd_wide.hip) against the fp32 reference and the default kernel; the backward runs from
+    """The opt-in forward variants (1: 64 rows per wave, attention_fwd_wide.hip; 2: the hand-scheduled
+    64-row kernel, attention_fwd_hs.hip) against the fp32 reference and the default kernel; the backward runs from
     their O and LSE, so the grads are checked too."""
     D = 128
     q, k, v = _mk(B, S, Hq, D, 41), _mk(B, S, Hk, D, 42), _mk(B, S, Hk, D, 43)
@@ -169,3 +170,22 @@ def test_fwd_variants_match_reference_and_default(B, S, Hq, Hk, causal, mode):
     assert _err(outs[1][0], o_ref) < 2e-2
     for a, b in zip(outs[1], outs[0]):
         assert _err(a, b) < 1e-2, _err(a, b)
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("causal", [True, False])
+def test_fwd_large_logits_rescale(causal, mode):
+    """Scores spanning hundreds of log2 units: every deferred-rescale branch fires and a wrong row
+    max would overflow exp2 (inf / NaN) -- checked for the default and the hand-scheduled forward."""
+    B, S, Hq, Hk, D = 1, 1024, 4, 2, 128
+    q, k, v = _mk(B, S, Hq, D, 51) * 6, _mk(B, S, Hk, D, 52) * 6, _mk(B, S, Hk, D, 53)
+    lib = ops._lib.lib()
+    prev = lib.rca_attn_set_fwd_mode(mode)
+    try:
+        o = ops.flash_attention(q, k, v, causal)
+        torch.cuda.synchronize()
+    finally:
+        lib.rca_attn_set_fwd_mode(prev)
+    o_ref = ref.attention_ref(q.float(), k.float(), v.float(), causal)
+    assert torch.isfinite(o.float()).all()
+    assert _err(o, o_ref) < 2e-2
