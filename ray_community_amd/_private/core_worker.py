@@ -787,7 +787,15 @@ class CoreWorker:
                 if ch is None:
                     ch = ActorChannel(self, aid)
                     self.channels[aid] = ch
+        # object refs nested in the arguments stay pinned at the head until the call returns (the
+        # head-routed path pins ``contained`` in its submit; the caller may drop its refs first)
+        nested = tuple(o for o in spec.get("contained") or () if o[:1] != b"A")
+        rids = spec.get("return_ids")
+        if nested and rids:
+            self.client.call_async("pin_objects", nested, 1)
         ch.submit(spec, list(deps))
+        if nested and rids:
+            self.owned.on_ready(rids[0], lambda _d, c=nested: self.client.call_async("pin_objects", c, -1))
 
     def cancel(self, oid, force=False, recursive=True):
         e = self.owned.objs.get(oid)

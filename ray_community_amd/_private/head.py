@@ -2014,6 +2014,18 @@ class Head:
         self.refs.add_holder(oid, caller)
         return True
 
+    def rpc_pin_objects(self, caller, oids, n):
+        """Pin (n > 0) / unpin (n < 0) objects for the duration of a direct actor call that carries
+        them nested in its arguments: the head-routed path pins a spec's ``contained`` refs in
+        ``_submit``, but a direct call never passes the head, and the owner may drop its last ref
+        before the callee deserializes the argument."""
+        for o in oids:
+            if n > 0:
+                self._pin(o, n)
+            else:
+                self._unpin(o, -n)
+        return True
+
     def rpc_put_owned(self, caller, items, owner_key, lineage=None):
         """A worker registers direct-call results the head must manage (shm, GPU, nested refs) on
         behalf of the calling process ``owner_key`` before replying to it. ``lineage``: the spec

@@ -547,3 +547,31 @@ def test_wait_polling_fast_path_semantics(ray_start_regular):
     rest.append(rest[0])
     with pytest.raises(ValueError, match="unique"):
         ray.wait(rest)
+
+
+def test_nested_ref_in_direct_actor_call_outlives_caller_ref(ray_start_regular):
+    """A ref nested in a direct actor call's arguments stays alive until the call returns even when
+    the caller drops its own ref first (the head-routed path pins ``contained`` refs; direct actor
+    calls pin them at submit and unpin on the result)."""
+    import gc
+
+    @ray.remote
+    class Producer:
+        def produce(self, x):
+            return x + 1
+
+    @ray.remote
+    class Reader:
+        def read(self, box):
+            time.sleep(0.3)
+            return ray.get(box[0])
+
+    p, r = Producer.remote(), Reader.remote()
+    for i in range(3):
+        ref = p.produce.remote(40 + i)  # a direct actor-call result owned by this process
+        if i:
+            ray.wait([ref])  # ready when nested (i = 0: still pending)
+        out = r.read.remote([ref])
+        del ref
+        gc.collect()
+        assert ray.get(out, timeout=30) == 41 + i
