@@ -197,3 +197,16 @@ def test_operator_fusion_rules(ray8):
     assert sorted(r["id"] for r in ds2.take_all()) == list(range(1, 65))
     st2 = ds2.stats()
     assert "Optimized plan: Input -> ActorPoolMap[Map(<lambda>)->MapBatches(_AddOne)]" in st2 and "OperatorFusion" in st2
+
+
+def test_cpu_chain_not_fused_into_gpu_actor_pool():
+    """A CPU task chain stays a separate (parallel) task stage ahead of a GPU actor pool, and is
+    absorbed into a CPU-only pool."""
+    from ray_community_amd.data._internal.logical_optimizer import plan_stages
+
+    cpu = {"kind": "map_batches", "fn": "synth"}
+    gpu_pool = {"kind": "map_batches", "fn": "infer", "compute": "actors", "num_gpus": 0.25}
+    cpu_pool = {"kind": "map_batches", "fn": "infer", "compute": "actors"}
+    assert [s[0] for s in plan_stages([cpu, gpu_pool])] == ["task", "actor"]
+    st = plan_stages([cpu, cpu_pool])
+    assert [s[0] for s in st] == ["actor"] and st[0][2] == [cpu]
