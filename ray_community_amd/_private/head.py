@@ -259,8 +259,10 @@ class Head:
         self.actor_dir = native().ActorDirectory(A_DEAD)
         self.workers: Dict[bytes, WorkerState] = {}
         self.nodes: Dict[str, NodeState] = {}
-        self.pgs: Dict[bytes, dict] = {}
-        self.pending_pgs: List[bytes] = []
+        # placement-group table (C++: records, name index, pending FIFO, state counts); the
+        # pg.ready() waiters stay here
+        self.pg_dir = native().PgDirectory()
+        self.pg_waiters: Dict[bytes, list] = {}
         self.kv = native().KvTable()  # internal KV (GCS InternalKV)
         self.functions: Dict[bytes, bytes] = {}
         self.events: collections.deque = collections.deque(maxlen=int(self.config.get("task_events_max", 100000)))
@@ -1193,7 +1195,7 @@ class Head:
             soft = bool(strat.get("soft"))
         preferred = spec.get("caller_node") or self.head_node_id
         if not self.sched.is_feasible(ts.demand) and not (kind == "node_affinity" and soft):
-            if kind == "pg" and strat["pg_id"] in self.pgs and self.pgs[strat["pg_id"]]["state"] == "PENDING":
+            if kind == "pg" and self.pg_dir.state(strat["pg_id"]) == "PENDING":
                 pass  # wait for the placement group to be placed
             elif kind == "node_affinity" and not soft:
                 self._fail_task(ts, exc.TaskUnschedulableError(
@@ -2249,90 +2251,72 @@ class Head:
 
     # ================================================================== placement groups
     def rpc_create_pg(self, caller, pg_id, bundles, strategy, name="", lifetime=None):
-        pg = {"pg_id": pg_id, "bundles": bundles, "strategy": strategy, "name": name, "state": "PENDING",
-              "nodes": None, "waiters": [], "created": time.time(), "lifetime": lifetime}
-        self.pgs[pg_id] = pg
-        for b in bundles:
-            if not self.sched.is_feasible({k: v for k, v in b.items() if v > 0}):
-                pg["infeasible"] = True
-        self.pending_pgs.append(pg_id)
+        infeasible = any(not self.sched.is_feasible({k: v for k, v in b.items() if v > 0}) for b in bundles)
+        self.pg_dir.add(pg_id, name or "", strategy, list(bundles), lifetime, time.time(), infeasible)
         self._try_place_pgs()
         return True
 
     def _try_place_pgs(self):
-        if not self.pending_pgs:
+        pending = self.pg_dir.pending()
+        if not pending:
             return
-        still = []
         placed_any = False
-        for pg_id in self.pending_pgs:
-            pg = self.pgs.get(pg_id)
-            if pg is None or pg["state"] != "PENDING":
+        for pg_id in pending:
+            if self.pg_dir.state(pg_id) != "PENDING":
                 continue
-            bundles = [{k: float(v) for k, v in b.items() if v > 0} for b in pg["bundles"]]
-            nodes = self.sched.create_pg(pg_id.hex(), bundles, pg["strategy"])
+            bundles = [{k: float(v) for k, v in b.items() if v > 0} for b in self.pg_dir.bundles(pg_id)]
+            nodes = self.sched.create_pg(pg_id.hex(), bundles, self.pg_dir.strategy(pg_id))
             if nodes is None:
-                still.append(pg_id)
                 continue
-            pg["nodes"] = list(nodes)
-            pg["state"] = "CREATED"
+            self.pg_dir.set_nodes(pg_id, list(nodes))
+            self.pg_dir.set_state(pg_id, "CREATED")  # leaves the pending queue
             # per-bundle GPU bookkeeping happens at task grant time (node.gpu_free)
-            for d in pg["waiters"]:
+            for d in self.pg_waiters.pop(pg_id, ()):
                 d.resolve(True)
-            pg["waiters"] = []
             placed_any = True
-        self.pending_pgs = still
         if placed_any:
             self._schedule()
 
     def rpc_pg_ready(self, caller, pg_id, timeout=None):
-        pg = self.pgs.get(pg_id)
+        st = self.pg_dir.state(pg_id)
         d = Deferred()
-        if pg is None or pg["state"] == "REMOVED":
+        if st in ("", "REMOVED"):
             d.resolve(ValueError("placement group removed"), ok=False)
-        elif pg["state"] == "CREATED":
+        elif st == "CREATED":
             d.resolve(True)
         else:
-            pg["waiters"].append(d)
+            self.pg_waiters.setdefault(pg_id, []).append(d)
             if timeout is not None:
                 self._add_timer(timeout, lambda: d.resolve(False))
         return d
 
     def rpc_remove_pg(self, caller, pg_id):
-        pg = self.pgs.get(pg_id)
-        if pg is None:
+        st = self.pg_dir.state(pg_id)
+        if not st:
             return False
-        if pg_id in self.pending_pgs:
-            self.pending_pgs.remove(pg_id)
         # kill actors placed in the group (the directory's placement-group index)
         for aid in self.actor_dir.in_pg(pg_id):
             a = self.actors.get(aid)
             if a is not None and a.state != A_DEAD:
                 self._kill_actor(a, no_restart=True, reason="placement group removed")
-        if pg["state"] == "CREATED":
+        if st == "CREATED":
             self.sched.remove_pg(pg_id.hex())
-        pg["state"] = "REMOVED"
-        for d in pg["waiters"]:
+        self.pg_dir.set_state(pg_id, "REMOVED")  # also leaves the pending queue
+        for d in self.pg_waiters.pop(pg_id, ()):
             d.resolve(False)
-        pg["waiters"] = []
         self._schedule()
         return True
 
     def rpc_pg_table(self, caller, pg_id=None):
-        def info(pg):
-            return {"placement_group_id": pg["pg_id"].hex(), "name": pg["name"], "strategy": pg["strategy"],
-                    "state": pg["state"], "bundles": {i: dict(b) for i, b in enumerate(pg["bundles"])},
-                    "bundles_to_node_id": {i: n for i, n in enumerate(pg["nodes"] or [])}}
-
         if pg_id is not None:
-            pg = self.pgs.get(pg_id)
-            return info(pg) if pg else {}
-        return {pg["pg_id"].hex(): info(pg) for pg in self.pgs.values()}
+            return self.pg_dir.info(pg_id)
+        return self.pg_dir.table()
 
     def rpc_get_named_pg(self, caller, name):
-        for pg in self.pgs.values():
-            if pg["name"] == name and pg["state"] != "REMOVED":
-                return {"pg_id": pg["pg_id"], "bundles": pg["bundles"], "strategy": pg["strategy"]}
-        return None
+        pg_id = self.pg_dir.by_name(name)
+        if pg_id is None:
+            return None
+        return {"pg_id": pg_id, "bundles": self.pg_dir.bundles(pg_id), "strategy": self.pg_dir.strategy(pg_id)}
 
     # ================================================================== cluster info
     def rpc_cluster_resources(self, caller):
@@ -2366,11 +2350,10 @@ class Head:
             if d:
                 tasks.append(d)
         pgs = []
-        for pg_id in self.pending_pgs:
-            pg = self.pgs.get(pg_id)
-            if pg is not None and pg["state"] == "PENDING":
-                pgs.append({"strategy": pg["strategy"],
-                            "bundles": [{k: float(v) for k, v in b.items() if v > 0} for b in pg["bundles"]]})
+        for pg_id in self.pg_dir.pending():
+            if self.pg_dir.state(pg_id) == "PENDING":
+                pgs.append({"strategy": self.pg_dir.strategy(pg_id),
+                            "bundles": [{k: float(v) for k, v in b.items() if v > 0} for b in self.pg_dir.bundles(pg_id)]})
         return {"tasks": tasks, "placement_groups": pgs}
 
     def rpc_node_load(self, caller):
