@@ -1,5 +1,6 @@
 // _rca_native: C++ runtime core (shared-memory object store, cluster resource scheduler, I/O reactor,
-// object reference table, internal KV, actor directory, placement-group directory).
+// object reference table, internal KV, actor directory, placement-group directory,
+// worker-pool index).
 #include <pybind11/pybind11.h>
 
 namespace py = pybind11;
@@ -11,6 +12,7 @@ void register_ref_table(py::module_& m);
 void register_kv_table(py::module_& m);
 void register_actor_table(py::module_& m);
 void register_pg_table(py::module_& m);
+void register_worker_pool(py::module_& m);
 
 PYBIND11_MODULE(_rca_native, m) {
   m.doc() = "ray_community_amd native runtime core";
@@ -21,4 +23,5 @@ PYBIND11_MODULE(_rca_native, m) {
   register_kv_table(m);
   register_actor_table(m);
   register_pg_table(m);
+  register_worker_pool(m);
 }

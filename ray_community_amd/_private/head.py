@@ -207,14 +207,18 @@ class WorkerState:
         self.direct_addr: Optional[str] = None
 
 
+def _pool_key(env_key) -> str:
+    """The worker-pool index's flat string for a (runtime_env json, GPU ids) env key."""
+    env, gpus = env_key
+    return env + "\x00" + ",".join(str(g) for g in gpus)
+
+
 class NodeState:
     def __init__(self, node_id, resources, labels=None, is_head=False):
         self.node_id = node_id
         self.resources = dict(resources)
         self.labels = labels or {}
         self.is_head = is_head
-        self.idle: Dict[Any, List[WorkerState]] = collections.defaultdict(list)
-        self.starting: Dict[Any, int] = collections.defaultdict(int)
         self.dispatch_q: Dict[Any, collections.deque] = collections.defaultdict(collections.deque)
         self.gpu_free = [1.0] * int(resources.get("GPU", 0))
         self.alive = True
@@ -258,6 +262,9 @@ class Head:
         # actor directory: name / node / placement-group / handle-holder indexes (C++)
         self.actor_dir = native().ActorDirectory(A_DEAD)
         self.workers: Dict[bytes, WorkerState] = {}
+        # worker-pool index (C++: idle stacks per (node, env key), spawned-not-registered counts,
+        # idle reaping); the WorkerState objects stay in self.workers
+        self.wpool = native().WorkerPool()
         self.nodes: Dict[str, NodeState] = {}
         # placement-group table (C++: records, name index, pending FIFO, state counts); the
         # pg.ready() waiters stay here
@@ -395,6 +402,7 @@ class Head:
                 return
             node.alive = False
             self.sched.remove_node(node_id)
+            self.wpool.drop_node(node_id)
             self._cluster_event("ERROR", "NODE", f"node {node_id[:8]} removed", node_id=node_id)
             for w in list(self.workers.values()):
                 if w.node_id == node_id and not w.dead:
@@ -544,8 +552,7 @@ class Head:
             w.direct_addr = extra.get("direct_addr")
             w.pid = pid
             w.state = "idle"
-            node = self.nodes[w.node_id]
-            node.starting[w.env_key] = max(0, node.starting[w.env_key] - 1)
+            self.wpool.add_starting(w.node_id, _pool_key(w.env_key), -1)
             self._worker_available(w)
         else:  # client driver
             cc.client_key = "client:" + ident.hex()
@@ -1247,7 +1254,7 @@ class Head:
             else:
                 node.dispatch_q[env_key].append(ts)
                 need = len(node.dispatch_q[env_key])
-                if node.starting[env_key] < need:
+                if self.wpool.starting(node.node_id, _pool_key(env_key)) < need:
                     self._start_worker(node, env_key, ts.gpus, ts.spec.get("runtime_env") or {})
         self._try_place_pgs()
 
@@ -1290,12 +1297,14 @@ class Head:
         return (env, tuple(gpus))
 
     def _pop_idle(self, node, env_key):
-        lst = node.idle.get(env_key)
-        while lst:
-            w = lst.pop()
-            if not w.dead:
+        key = _pool_key(env_key)
+        while True:
+            wid = self.wpool.pop_idle(node.node_id, key)
+            if wid is None:
+                return None
+            w = self.workers.get(wid)
+            if w is not None and not w.dead:
                 return w
-        return None
 
     # ================================================================== worker pool
     def _start_worker(self, node, env_key, gpus, runtime_env=None):
@@ -1351,7 +1360,7 @@ class Head:
         w = WorkerState(wid, node.node_id, env_key, proc, gpus)
         w.log_path = out_path
         self.workers[wid] = w
-        node.starting[env_key] += 1
+        self.wpool.add_starting(node.node_id, _pool_key(env_key), 1)
         return w
 
     def _worker_available(self, w: WorkerState):
@@ -1371,7 +1380,7 @@ class Head:
         w.state = "idle"
         w.task = None
         w.idle_since = time.time()
-        node.idle[w.env_key].append(w)
+        self.wpool.push_idle(node.node_id, _pool_key(w.env_key), w.wid, w.idle_since)
 
     def _reap_idle(self):
         now = time.time()
@@ -1391,17 +1400,10 @@ class Head:
         timeout = float(self.config.get("idle_worker_timeout_s", 60))
         with self.lock:
             for node in self.nodes.values():
-                n_idle = sum(len(v) for v in node.idle.values())
-                if n_idle <= keep:
-                    continue
-                for key, lst in node.idle.items():
-                    for w in list(lst):
-                        if n_idle <= keep:
-                            break
-                        if now - w.idle_since > timeout:
-                            lst.remove(w)
-                            self._kill_worker(w)
-                            n_idle -= 1
+                for wid in self.wpool.reap(node.node_id, keep, timeout, now):
+                    w = self.workers.get(wid)
+                    if w is not None:
+                        self._kill_worker(w)
 
     def _fail_unstartable(self, w, reason):
         """Workers for this env keep crashing at startup: fail the work queued for them."""
@@ -1632,12 +1634,9 @@ class Head:
                                 f"{'killed by the memory monitor' if oom else reason}",
                                 node_id=w.node_id, pid=w.pid, worker_id=w.wid.hex())
         node = self.nodes.get(w.node_id)
-        if w.state == "starting" and node is not None:
-            node.starting[w.env_key] = max(0, node.starting[w.env_key] - 1)
-        if node is not None:
-            lst = node.idle.get(w.env_key)
-            if lst and w in lst:
-                lst.remove(w)
+        if w.state == "starting":
+            self.wpool.add_starting(w.node_id, _pool_key(w.env_key), -1)
+        self.wpool.remove(w.wid)
         self.workers.pop(w.wid, None)
         self._drop_streams_of("w:" + w.wid.hex())
         # GPU objects owned by the worker are lost
@@ -1686,7 +1685,7 @@ class Head:
         # keep the pool warm for queued work
         if node is not None and node.alive:
             for key, q in node.dispatch_q.items():
-                if q and node.starting[key] < len(q):
+                if q and self.wpool.starting(node.node_id, _pool_key(key)) < len(q):
                     self._start_worker(node, key, q[0].gpus, q[0].spec.get("runtime_env") or {})
 
     # ================================================================== streaming generators
@@ -2601,6 +2600,10 @@ class Head:
         ac = self.actor_dir.state_counts()
         gauge("rca_actors", "Actors by state", [({"state": k}, v) for k, v in ac.items()])
         gauge("rca_workers", "Worker processes", [({"node_id": "all"}, len(self.workers))])
+        ps = self.wpool.stats()
+        gauge("rca_idle_workers", "Idle pooled worker processes", [({"node_id": n}, v["idle"]) for n, v in ps.items()])
+        gauge("rca_starting_workers", "Worker processes spawned but not yet registered",
+              [({"node_id": n}, v["starting"]) for n, v in ps.items()])
         # GPU object store (HBM-resident objects, per physical GPU) and its host spill traffic
         gauge("rca_gpu_object_store_hbm_bytes", "HBM bytes held by GPU objects",
               [({"gpu": str(k)}, v) for k, v in self.gpu_usage.items()])
