@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import asyncio
 import threading
+import time
 import traceback
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -127,34 +128,29 @@ def _start_loop(actor, plan):
 
 
 class CompiledDAGRef:
-    """Result handle of one ``CompiledDAG.execute`` (``begin_read``/``end_read`` or ``get``)."""
+    """Result handle of one ``CompiledDAG.execute`` (``begin_read``/``end_read`` or ``get``).
+
+    Results leave the output channels in execution order; a ref read out of order, or an execute
+    that finds the input channel full, moves earlier results into the DAG's result buffer first
+    (reference: CompiledDAG._result_buffer / max_buffered_results,
+    /root/reference/python/ray/dag/compiled_dag_node.py), so any number of executions may be in
+    flight and refs may be read in any order."""
 
     def __init__(self, dag: "CompiledDAG", seq: int):
         self._dag = dag
         self._seq = seq
-        self._value = None
         self._read = False
 
     def begin_read(self, timeout: Optional[float] = None):
-        vals = []
-        for ch, r in self._dag._outputs:
-            vals.append(ch.begin_read(r, timeout))
+        vals = self._dag._result_of(self._seq, timeout)
         self._read = True
-        if self._dag._device_outputs:
-            from .torch_tensor import receiver
-
-            vals = [receiver().unpack(v) for v in vals]  # copied out before the channel is released
         for v in vals:
             if isinstance(v, _DAGTaskError):
-                self.end_read()
                 raise v.exc
         return vals if self._dag._multi else vals[0]
 
     def end_read(self):
-        if self._read:
-            for ch, r in self._dag._outputs:
-                ch.end_read(r)
-            self._read = False
+        self._read = False  # values were copied out of the channels when they were fetched
 
     def get(self, timeout: Optional[float] = None):
         try:
@@ -164,7 +160,8 @@ class CompiledDAGRef:
 
 
 class CompiledDAG:
-    def __init__(self, root: DAGNode, buffer_size_bytes: Optional[int] = None, enable_asyncio: bool = False):
+    def __init__(self, root: DAGNode, buffer_size_bytes: Optional[int] = None, enable_asyncio: bool = False,
+                 max_buffered_results: int = 1000):
         from .._private.worker import get
 
         self._enable_asyncio = enable_asyncio
@@ -257,7 +254,36 @@ class CompiledDAG:
         self._device_outputs = any(_on_device(o) for o in out_nodes)
         self._handles = handle_of
         self._seq = 0
+        self._next_read = 1          # seq of the next result waiting in the output channels
+        self._results: Dict[int, list] = {}
+        self._max_buffered = int(max_buffered_results)
         self._torn_down = False
+
+    def _fetch_next(self, timeout: Optional[float] = None):
+        """Moves the oldest unread execution's outputs from the channels into the result buffer."""
+        if len(self._results) >= self._max_buffered:
+            raise RuntimeError(f"compiled DAG holds {len(self._results)} unread results "
+                               f"(max_buffered_results={self._max_buffered}); read earlier refs first")
+        vals = []
+        for ch, r in self._outputs:
+            vals.append(ch.begin_read(r, timeout))
+        try:
+            if self._device_outputs:
+                from .torch_tensor import receiver
+
+                vals = [receiver().unpack(v) for v in vals]  # copied out before the channel is released
+        finally:
+            for ch, r in self._outputs:
+                ch.end_read(r)
+        self._results[self._next_read] = vals
+        self._next_read += 1
+
+    def _result_of(self, seq: int, timeout: Optional[float] = None) -> list:
+        if seq not in self._results and seq < self._next_read:
+            raise ValueError("this compiled DAG result was already read")
+        while seq >= self._next_read:
+            self._fetch_next(timeout)
+        return self._results.pop(seq)
 
     def execute(self, *args, **kwargs) -> CompiledDAGRef:
         if self._torn_down:
@@ -266,6 +292,13 @@ class CompiledDAG:
             raise ValueError("Use execute_async if enable_asyncio=True")
         value = args[0] if len(args) == 1 and not kwargs else DAGInputData(*args, **kwargs)
         if self._input is not None:
+            # a full input channel with results still unread means the pipeline is backed up behind
+            # the driver: drain results into the buffer until the input can take the value
+            while not self._input.can_write():
+                if self._next_read <= self._seq:
+                    self._fetch_next()
+                else:
+                    time.sleep(20e-6)
             self._input.write(value)
         self._seq += 1
         return CompiledDAGRef(self, self._seq)
@@ -305,5 +338,7 @@ class CompiledDAG:
             pass
 
 
-def build_compiled_dag(root: DAGNode, buffer_size_bytes=None, enable_asyncio=False) -> CompiledDAG:
-    return CompiledDAG(root, buffer_size_bytes, enable_asyncio)
+def build_compiled_dag(root: DAGNode, buffer_size_bytes=None, enable_asyncio=False,
+                       max_buffered_results=None) -> CompiledDAG:
+    return CompiledDAG(root, buffer_size_bytes, enable_asyncio,
+                       1000 if max_buffered_results is None else max_buffered_results)

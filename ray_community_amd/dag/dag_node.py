@@ -124,10 +124,10 @@ class DAGNode:
         raise NotImplementedError
 
     def experimental_compile(self, buffer_size_bytes: Optional[int] = None, enable_asyncio: bool = False,
-                             async_max_queue_size: Optional[int] = None):
+                             async_max_queue_size: Optional[int] = None, _max_buffered_results: Optional[int] = None):
         from .compiled_dag_node import build_compiled_dag
 
-        return build_compiled_dag(self, buffer_size_bytes, enable_asyncio)
+        return build_compiled_dag(self, buffer_size_bytes, enable_asyncio, _max_buffered_results)
 
     def clear_cache(self):
         self.cache_from_last_execute = {}

@@ -81,6 +81,12 @@ class Channel:
         hdr[1] = len(data)
         hdr[0] = seq + 1
 
+    def can_write(self) -> bool:
+        """Every reader has acknowledged the current value, so ``write`` would not block."""
+        hdr = self._hdr
+        seq = int(hdr[0])
+        return all(int(hdr[2 + r]) >= seq for r in range(self.num_readers))
+
     def close(self):
         try:
             self.write(_Closed(), timeout=5.0)
