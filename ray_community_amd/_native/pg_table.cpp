@@ -47,6 +47,10 @@ class PgDirectory {
            const py::object& lifetime, double created, bool infeasible) {
     const std::string pg = pg_b;
     if (recs_.count(pg)) throw py::value_error("placement group already registered");
+    // a live group already holds the name: reject, as the GCS does (a second registration would
+    // overwrite the index and orphan the first group's lookup once the newer one is removed)
+    if (!name.empty() && !by_name(name).is_none())
+      throw py::value_error("Failed to create placement group '" + name + "' because name already exists.");
     Rec& r = recs_[pg];
     r.name = name;
     r.strategy = strategy;

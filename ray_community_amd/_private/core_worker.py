@@ -252,6 +252,13 @@ class DirectClient:
         pass
 
 
+class _RefList(list):
+    """The remainder list ``wait()`` returns: a plain list that can be weakly referenced, so the
+    polling fast path can recognise it without keeping its refs alive."""
+
+    __slots__ = ("__weakref__",)
+
+
 class SocketClient:
     """Framed RPC client over the head's Unix socket (workers and external drivers), or over a
     pre-connected stream socket (``sock``: the TCP link of a ``ray://`` remote driver)."""
@@ -387,7 +394,7 @@ class CoreWorker:
         self._refs: Dict[bytes, int] = {}
         self._ref_lock = threading.Lock()
         self._ready_known = set()  # head-managed objects a wait() saw ready (dropped with the last ref)
-        self._wait_rest = None  # (list, len): the remainder the last wait() returned, all owned + unique
+        self._wait_rest = None  # (weakref to list, len): the remainder the last wait() returned, all owned + unique
         self.ctx = TaskContext()
         self.registered_functions = set()
         self.actor_id = None
@@ -633,12 +640,14 @@ class CoreWorker:
         # an earlier call returned, so its refs are known unique and all owned here; if its head
         # is already ready, answer with one slice instead of re-validating the whole list
         # (O(N) per call instead of five O(N) passes).
+        # Only a weak reference to that list is cached: a caller that drops ``rest`` must release
+        # its refs (free-on-last-ref), not have them pinned here until the next wait().
         last = self._wait_rest
-        if (num_returns == 1 and last is not None and refs is last[0] and len(refs) == last[1] and refs):
+        if (num_returns == 1 and last is not None and refs is last[0]() and len(refs) == last[1] and refs):
             e = self.owned.objs.get(refs[0]._id)
             if e is not None and e.desc is not None:
-                rest = refs[1:]
-                self._wait_rest = (rest, len(rest))
+                rest = _RefList(refs[1:])
+                self._wait_rest = (weakref.ref(rest), len(rest))
                 return [refs[0]], rest
         self._wait_rest = None
         refs = list(refs)
@@ -672,13 +681,13 @@ class CoreWorker:
         if len(got) <= 4:  # the polling case: split by position instead of two filtering passes
             idx = sorted(ids.index(o) for o in got)
             ready = [refs[i] for i in idx]
-            not_ready, prev = [], 0
+            not_ready, prev = _RefList(), 0
             for i in idx:
                 not_ready.extend(refs[prev:i])
                 prev = i + 1
             not_ready.extend(refs[prev:])
             if sids <= owned.keys():
-                self._wait_rest = (not_ready, len(not_ready))
+                self._wait_rest = (weakref.ref(not_ready), len(not_ready))
             return ready, not_ready
         rs = set(got)
         ready = [r for r in refs if r._id in rs]

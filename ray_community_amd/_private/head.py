@@ -1324,9 +1324,7 @@ class Head:
         env["RCA_GPU_IDS"] = ",".join(str(g) for g in gpus)
         env.setdefault("PYTHONUNBUFFERED", "1")
         if gpus:
-            vis = _parent_visible_devices()
-            phys = [vis[g] if vis and g < len(vis) else str(g) for g in gpus]
-            env["HIP_VISIBLE_DEVICES"] = ",".join(phys)
+            env["HIP_VISIBLE_DEVICES"] = worker_hip_visible_devices(gpus, os.environ)
             env.pop("CUDA_VISIBLE_DEVICES", None)
         else:
             if self.config.get("hide_gpus_from_cpu_workers", True):
@@ -2754,9 +2752,20 @@ def _default_gpu_budget() -> int:
     return 0
 
 
-def _parent_visible_devices():
-    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
+def worker_hip_visible_devices(gpus, environ) -> str:
+    """``HIP_VISIBLE_DEVICES`` for a worker that owns the head's logical GPUs ``gpus``.
+
+    The head's logical GPU ``g`` is the g-th device the head process itself sees. ROCm applies the
+    two masks in layers: ``ROCR_VISIBLE_DEVICES`` filters the agents the ROCr runtime exposes, and
+    ``HIP_VISIBLE_DEVICES`` (or ``CUDA_VISIBLE_DEVICES``) then indexes INTO that filtered set. The
+    worker inherits the parent's ``ROCR_VISIBLE_DEVICES`` unchanged, so its HIP-level ids are:
+      * the parent's HIP/CUDA mask entry ``g`` when the parent has one;
+      * otherwise plain ``g`` -- never a ROCR id (with ``ROCR_VISIBLE_DEVICES=4,5`` the worker's
+        devices are HIP 0 and 1; ``HIP_VISIBLE_DEVICES=4`` would select nothing).
+    """
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = environ.get(var)
         if v:
-            return [x.strip() for x in v.split(",") if x.strip()]
-    return None
+            vis = [x.strip() for x in v.split(",") if x.strip()]
+            return ",".join(vis[g] if g < len(vis) else str(g) for g in gpus)
+    return ",".join(str(g) for g in gpus)

@@ -146,8 +146,12 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
                                                 8265 if dashboard_port is None else int(dashboard_port))
             try:
                 os.makedirs(root, exist_ok=True)
-                with open(os.path.join(root, "latest_session.json"), "w") as f:
+                # temp file + rename: a concurrent ``address="auto"`` reader sees the old record or
+                # the new one, never a truncated file
+                tmp = os.path.join(root, f".latest_session.{os.getpid()}.tmp")
+                with open(tmp, "w") as f:
                     json.dump({"sock": head.sock_path, "pid": os.getpid(), "session": session}, f)
+                os.replace(tmp, os.path.join(root, "latest_session.json"))
             except OSError:
                 pass
         from ..runtime_env import validate as _validate_env

@@ -170,9 +170,18 @@ class FaultTolerantActorManager:
         from ..._private.worker import get, wait
 
         ids = list(remote_actor_ids) if remote_actor_ids is not None else self.actor_ids()
+        if isinstance(func, list):
+            # one callable per actor id: filter the (id, func) pairs together, so a skipped
+            # unhealthy actor does not shift the remaining actors onto each other's functions
+            if len(func) != len(ids):
+                raise ValueError(f"foreach_actor got {len(func)} functions for {len(ids)} actors")
+            pairs = list(zip(ids, func))
+        else:
+            pairs = [(i, func) for i in ids]
         if healthy_only:
-            ids = [i for i in ids if self._healthy.get(i)]
-        funcs = func if isinstance(func, list) else [func] * len(ids)
+            pairs = [(i, f) for i, f in pairs if self._healthy.get(i)]
+        ids = [i for i, _ in pairs]
+        funcs = [f for _, f in pairs]
         refs = {}
         out = RemoteCallResults()
         for i, f in zip(ids, funcs):

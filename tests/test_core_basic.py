@@ -490,8 +490,10 @@ def test_paused_producer_released_on_cancel_and_drop(shutdown_only, tmp_path):
             for i in range(n):
                 yield i
         finally:
-            with open(path, "w") as f:
+            # temp file + rename: the poller below never sees the file created but not yet written
+            with open(path + ".tmp", "w") as f:
                 f.write("closed")
+            os.replace(path + ".tmp", path)
 
     @ray.remote
     def probe():
@@ -501,7 +503,8 @@ def test_paused_producer_released_on_cancel_and_drop(shutdown_only, tmp_path):
         deadline = _t.time() + timeout
         while _t.time() < deadline:
             if os.path.exists(p):
-                return open(p).read()
+                with open(p) as f:
+                    return f.read()
             _t.sleep(0.05)
         return None
 
