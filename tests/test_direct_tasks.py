@@ -299,10 +299,16 @@ def test_leased_worker_of_a_dead_driver_is_killed(tmp_path):
                            timeout=180)
         assert r.returncode == 0, r.stderr
         pid = int(pidfile.read_text())
+        def alive(p):  # the pid can vanish between any two psutil calls
+            try:
+                return psutil.Process(p).status() != psutil.STATUS_ZOMBIE
+            except psutil.NoSuchProcess:
+                return False
+
         deadline = time.time() + 20
-        while time.time() < deadline and psutil.pid_exists(pid) and psutil.Process(pid).status() != "zombie":
+        while time.time() < deadline and alive(pid):
             time.sleep(0.1)
-        assert not psutil.pid_exists(pid) or psutil.Process(pid).status() == "zombie", "orphan worker still running"
+        assert not alive(pid), "orphan worker still running"
         drv2 = ("import sys; sys.path.insert(0, %r)\n"
                 "import ray_community_amd as ray\n"
                 "ray.init(address='auto')\n"
