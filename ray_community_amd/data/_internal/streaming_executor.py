@@ -379,6 +379,11 @@ class StreamingExecutor:
             with self._lock:
                 return self._out_count + op.pending_outputs() + len(op.running) < self.out_window
         d = op.downstream
+        if isinstance(d, AllToAllOp):
+            # a barrier consumes its whole input before it emits anything: bounding its input
+            # queue would stall the producer short of the barrier forever (more input blocks than
+            # the window)
+            return True
         return len(d.inq) + op.pending_outputs() + len(op.running) < op.out_limit
 
     def _can_run(self, op: PhysicalOp) -> bool:

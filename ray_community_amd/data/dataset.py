@@ -304,7 +304,14 @@ class Dataset:
         return a, b
 
     def streaming_split(self, n: int, *, equal: bool = False, locality_hints=None) -> List["DataIterator"]:
-        return [p.iterator() for p in self.split(n, equal=equal)]
+        """``n`` iterators over ONE streaming execution of this dataset, coordinated by a split
+        actor (``_internal/stream_split.py``): returns immediately, executes lazily, re-executes
+        every epoch (all ``n`` iterators must start it), ``equal=True`` gives every iterator
+        exactly ``count // n`` rows. Reference: ``python/ray/data/dataset.py:1141``."""
+        _ensure_init()
+        from ._internal.stream_split import streaming_split
+
+        return streaming_split(self, n, equal, locality_hints)
 
     # ------------------------------------------------------------------ consumption
     def iterator(self) -> "DataIterator":

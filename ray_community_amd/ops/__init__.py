@@ -822,9 +822,17 @@ def _attn_fwd(q, k, v, o, lse, B, S, Hq, Hk, D, sq, sk, sv, so, scale, causal):
           "rca_attn_fwd")
 
 
-def _attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, strides, scale, causal):
-    check(lib().rca_attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, *strides, scale, int(causal),
-                             stream_ptr()), "rca_attn_bwd")
+def _attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, strides, scale, causal, device=None):
+    """Attention backward. With a dS workspace (D = 128, default mode) the dK/dV kernel stores the
+    bf16 dS tiles and dQ = dS.K is read back from them (no S/P/dP recomputation for dQ); the
+    workspace is a transient caching-allocator block (1.08 GB at the Llama-3-8B shape, reused by
+    every layer's backward)."""
+    L = lib()
+    nbytes = L.rca_attn_bwd_ws_bytes(B, S, Hq, Hk, D, int(causal))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device) if nbytes > 0 else None
+    check(L.rca_attn_bwd2(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, *strides, scale, int(causal),
+                          ws.data_ptr() if ws is not None else None, nbytes, stream_ptr()), "rca_attn_bwd2")
+    del ws  # stream-ordered: the caching allocator reuses the block only for later work on this stream
 
 
 class _FlashAttnQKV(torch.autograd.Function):
@@ -854,7 +862,7 @@ class _FlashAttnQKV(torch.autograd.Function):
         base, gb, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
         _attn_bwd(base, base + es * Hq * D, base + es * (Hq + Hk) * D, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
                   delta.data_ptr(), gb, gb + es * Hq * D, gb + es * (Hq + Hk) * D, B, S, Hq, Hk, D,
-                  (W, W, W, Hq * D, Hq * D, W, W, W), scale, causal)
+                  (W, W, W, Hq * D, Hq * D, W, W, W), scale, causal, qkv.device)
         dqkv._rca_owned_grad = True  # fresh buffer: the RoPE backward may rotate it in place
         return dqkv, None, None, None, None, None, None, None
 
@@ -897,7 +905,7 @@ class _FlashAttn(torch.autograd.Function):
         _attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),
                   delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, S, Hq, Hk, D,
                   (q.stride(1), k.stride(1), v.stride(1), o.stride(1), do.stride(1), dq.stride(1), dk.stride(1),
-                   dv.stride(1)), scale, causal)
+                   dv.stride(1)), scale, causal, q.device)
         return dq, dk, dv, None, None
 
 

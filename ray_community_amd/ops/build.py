@@ -88,6 +88,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
     r = subprocess.run(cmd, capture_output=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout.decode()}{r.stderr.decode()}")
+    # resolve every symbol now (ctypes dlopens with RTLD_NOW): a kernel template whose host stub
+    # hipcc did not emit fails here, at build time, instead of at first use on a GPU box
+    import ctypes
+
+    try:
+        ctypes.CDLL(tmp_lib)
+    except OSError as e:
+        raise RuntimeError(f"built library does not load: {e}") from None
     os.replace(tmp_lib, LIB_PATH)
     with open(LIB_PATH + ".stamp", "w") as f:
         f.write(_digest())

@@ -32,7 +32,13 @@
 void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                           const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
                           long sq, long sk, long sv, long sdo, long sdk, long sdv, float scale2, float scale,
-                          hipStream_t st);
+                          hipStream_t st, bf16_t* dSw, long tiles_bh);
+// recompute-free dQ (attention_dq.hip)
+long rca_attn_ds_ws_bytes(int B, int S, int Hq, int D, bool causal);
+void rca_attn_launch_delta(const bf16_t* o, const bf16_t* dout, float* delta, int B, int S, int Hq, long so, long sdo,
+                           hipStream_t st);
+void rca_attn_launch_dq_ds(bool causal, const bf16_t* k, const bf16_t* dsw, bf16_t* dq, int B, int S, int Hq, int Hk,
+                           long sk, long sdq, float scale, hipStream_t st);
 // 64-query-rows-per-wave forward (attention_fwd_wide.hip); false = not selected for this shape
 bool rca_attn_launch_fwd_wide(bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
                               int B, int S, int Hq, int Hk, long sq, long sk, long sv, long so, float scale2,
@@ -418,12 +424,21 @@ template <int D, bool C>
 void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                 const float* lse, float* delta, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
                 long sq, long sk, long sv, long so, long sdo, long sdq, long sdk, long sdv, float scale2, float scale,
-                hipStream_t st) {
+                hipStream_t st, bf16_t* ws) {
+  if (ws != nullptr) {
+    // recompute-free: delta, then dK/dV (+ the dS tiles), then dQ = dS . K
+    const long nb = S / 32, tiles = C ? nb * (nb + 1) / 2 : nb * nb;
+    rca_attn_launch_delta(o, dout, delta, B, S, Hq, so, sdo, st);
+    rca_attn_launch_dkdv(D, C, q, k, v, dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2,
+                         scale, st, ws, tiles);
+    rca_attn_launch_dq_ds(C, k, ws, dq, B, S, Hq, Hk, sk, sdq, scale, st);
+    return;
+  }
   // dQ first: it also produces delta = rowsum(dO * O), which dK/dV reads
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3(B * Hq * (S / 128)), dim3(kThreads), 0, st, q, k, v, o, dout, lse,
                      delta, dq, B, S, Hq, Hk, sq, sk, sv, so, sdo, sdq, scale2, scale);
   rca_attn_launch_dkdv(D, C, q, k, v, dout, lse, delta, dk, dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale,
-                       st);
+                       st, nullptr, 0);
 }
 
 bool shapes_ok(int B, int S, int Hq, int Hk, int D) {
@@ -452,6 +467,56 @@ RCA_API int rca_attn_fwd(const void* q, const void* k, const void* v, void* o, f
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// Backward mode: 1 (default) = recompute-free dQ from the dS tiles the dK/dV kernel writes
+// (needs the workspace of rca_attn_bwd_ws_bytes; D = 128), 0 = the dQ kernel that recomputes S, P
+// and dP. RCA_ATTN_BWD=0 or rca_attn_set_bwd_mode(0) selects the latter (A/B, equivalence tests).
+static int g_bwd_mode = [] {
+  const char* e = getenv("RCA_ATTN_BWD");
+  return e && atoi(e) == 0 ? 0 : 1;
+}();
+RCA_API int rca_attn_set_bwd_mode(int mode) {
+  const int old = g_bwd_mode;
+  g_bwd_mode = mode;
+  return old;
+}
+
+// workspace bytes rca_attn_bwd2 wants for this shape (0: none, the recompute path runs)
+RCA_API long long rca_attn_bwd_ws_bytes(int B, int S, int Hq, int Hk, int D, int causal) {
+  if (g_bwd_mode != 1 || !shapes_ok(B, S, Hq, Hk, D)) return 0;
+  return rca_attn_ds_ws_bytes(B, S, Hq, D, causal != 0);
+}
+
+RCA_API int rca_attn_bwd2(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                          const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hk,
+                          int D, long long sq, long long sk, long long sv, long long so, long long sdo, long long sdq,
+                          long long sdk, long long sdv, float scale, int causal, void* ws, long long ws_bytes,
+                          hipStream_t st) {
+  if (!shapes_ok(B, S, Hq, Hk, D)) return 1;
+  const long need = rca_attn_ds_ws_bytes(B, S, Hq, D, causal != 0);
+  bf16_t* w = (ws != nullptr && need > 0 && ws_bytes >= need && D == 128) ? (bf16_t*)ws : nullptr;
+  const float scale2 = scale * 1.4426950408889634f;
+  auto Q = (const bf16_t*)q;
+  auto K = (const bf16_t*)k;
+  auto V = (const bf16_t*)v;
+  auto O = (const bf16_t*)o;
+  auto G = (const bf16_t*)dout;
+  auto dQ = (bf16_t*)dq;
+  auto dK = (bf16_t*)dk;
+  auto dV = (bf16_t*)dv;
+#define RCA_BWD(DD, CC)                                                                                            \
+  launch_bwd<DD, CC>(Q, K, V, O, G, lse, delta, dQ, dK, dV, B, S, Hq, Hk, sq, sk, sv, so, sdo, sdq, sdk, sdv, scale2, \
+                     scale, st, DD == 128 ? w : nullptr)
+  if (D == 128) {
+    if (causal) RCA_BWD(128, true);
+    else RCA_BWD(128, false);
+  } else {
+    if (causal) RCA_BWD(64, true);
+    else RCA_BWD(64, false);
+  }
+#undef RCA_BWD
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 RCA_API int rca_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hk,
                          int D, long long sq, long long sk, long long sv, long long so, long long sdo, long long sdq,
@@ -468,7 +533,7 @@ RCA_API int rca_attn_bwd(const void* q, const void* k, const void* v, const void
   auto dV = (bf16_t*)dv;
 #define RCA_BWD(DD, CC)                                                                                            \
   launch_bwd<DD, CC>(Q, K, V, O, G, lse, delta, dQ, dK, dV, B, S, Hq, Hk, sq, sk, sv, so, sdo, sdq, sdk, sdv, scale2, \
-                     scale, st)
+                     scale, st, nullptr)
   if (D == 128) {
     if (causal) RCA_BWD(128, true);
     else RCA_BWD(128, false);

@@ -272,18 +272,33 @@ __device__ __forceinline__ void hs_xdl_gap() { asm volatile("s_nop 7\n\ts_nop 7\
 // free to move across them before instruction selection)
 #define HS_MFV(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
 // S / dP chains with the K / V fragments (B operand) held in accumulator registers: 64 VGPRs freed
-#define HS_MFK(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b))
-#define HS_MFA(acc, a, b) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
+// The leading s_nop: hipcc is free to materialise an asm operand with a copy right in front of the
+// statement (v_accvgpr_write of a K/V fragment it keeps in VGPRs under register pressure, a
+// v_accvgpr_mov of an accumulator), and its hazard recognizer does not pad copies that feed an asm
+// MFMA: without these wait states an MFMA read a stale K fragment (11 wrong dS elements in one
+// diagonal tile, scripts/diag/attn_ds_diag.py). The s_nop sits in the MFMA gap with the fillers.
+#define HS_MFK(acc, a, b) \
+  asm volatile("s_nop 3\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b))
+#define HS_MFA(acc, a, b) \
+  asm volatile("s_nop 3\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
 // XDL <-> VALU hazard gap that the registers crossing it pass through: the producer stays above it
 // and the consumer below it whatever the compiler reorders
 #define HS_GAP "s_nop 7\n\ts_nop 7\n\ts_nop 4"
 
-template <bool CAUSAL, bool DMA = true>
+// DS: the kernel also writes every dS tile (bf16, the dK MFMA's own operand registers) to a workspace
+// for the dQ kernel (attention_dq.hip: dQ = dS.K without recomputing S, P and dP). Tile (query block
+// qb, key block kb) of 32 x 32 is 2 KB: fragment s (registers 8s..8s+7 of the dS accumulator) of
+// lane l at 16-B slot 64 s + (l ^ (4 (l >> 5) + 8 s)), an XOR swizzle under which the dQ kernel's
+// transposed reads are bank-conflict-free. Tiles of one (batch, query head) are stored
+// qb (qb + 1) / 2 + kb (causal, kb <= qb) or qb nb + kb. The four 16-B stores per query slice are
+// inline asm placed in MFMA gaps; the next slice's LDS-DMA is retired with a counted vmcnt(4), so
+// the stores stay in flight across the slice barrier.
+template <bool CAUSAL, bool DMA = true, bool DS = false>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
-    long sdo, long sdk, long sdv, float scale2, float scale) {
+    long sdo, long sdk, long sdv, float scale2, float scale, bf16_t* __restrict__ dSw, long tiles_bh) {
   constexpr int D = 128, BKV = 128, BQS = 64, NKS = 8, NDB = 4, SL = BQS * D * 2, G8 = Img<D>::G8;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * SL];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][BQS];  // [slot][-lse, -delta][row]
@@ -299,6 +314,10 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
   const unsigned sbase = (unsigned)(__UINTPTR_TYPE__)smem;
   const unsigned uq0 = sbase + rb0, uq1 = sbase + rb1, ut0 = sbase + tb0, ut1 = sbase + tb1;
   const unsigned ur = (unsigned)(__UINTPTR_TYPE__)&rowc[0][0][0] + 16 * h;
+  // DS: per-lane slots of fragments 0 / 1 inside a tile; this wave's key block (wave-uniform)
+  const unsigned dsv0 = 16u * (unsigned)(lane ^ (4 * h)), dsv1 = 1024u + 16u * (unsigned)(lane ^ (4 * h + 8));
+  const int nb32 = S >> 5, kb32 = __builtin_amdgcn_readfirstlane(kw0 >> 5);
+  char* const ds_trash = DS ? (char*)dSw + (long)B * Hq * tiles_bh * 2048 : nullptr;  // masked tiles land here
 
   bf16x8_t kf[NKS], vf[NKS];
   {
@@ -339,9 +358,26 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
       qst.load(qa, sq, g * D * 2);
       gst.load(qa, sdo, g * D * 2);
     }
-    if (tid < 2 * BQS) rc = rsrc[(long)g * S + qa];
+    if constexpr (DS) {  // invisible to hipcc's wait counting (retired by stage_finish's counted wait)
+      if (tid < 2 * BQS) {
+        const float* pr = rsrc + (long)g * S + qa;
+        asm volatile("global_load_dword %0, %1, off" : "=v"(rc) : "v"(pr) : "memory");
+      }
+    } else {
+      if (tid < 2 * BQS) rc = rsrc[(long)g * S + qa];
+    }
   };
-  auto stage_finish = [&](int buf) {
+  // stored: this wave issued its 4 dS stores after the DMA (they may stay in flight)
+  auto stage_finish = [&](int buf, bool stored) {
+    if constexpr (DS) {
+      if (stored) asm volatile("s_waitcnt vmcnt(4)" : "+v"(rc)::"memory");
+      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(rc)::"memory");
+      if (tid < 2 * BQS) {
+        const unsigned ra = (unsigned)(__UINTPTR_TYPE__)&rowc[buf][tid / BQS][tid & (BQS - 1)];
+        asm volatile("ds_write_b32 %0, %1" ::"v"(ra), "v"(-rc) : "memory");  // -lse, -delta
+      }
+      return;
+    }
     if constexpr (DMA) {
       wait_dma();
     } else {
@@ -350,9 +386,18 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
     }
     if (tid < 2 * BQS) rowc[buf][tid / BQS][tid & (BQS - 1)] = -rc;  // -lse, -delta
   };
+  // slice barrier: a bare s_barrier in the DS variant (__syncthreads' fence would drain the stores)
+  auto slice_barrier = [&]() {
+    if constexpr (DS) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
+  };
   stage_issue(0, nsl - 1, 0);
-  stage_finish(0);
-  __syncthreads();
+  stage_finish(0, false);
+  slice_barrier();
 
   auto slice = [&](auto bufc, int i) {
     constexpr int buf = decltype(bufc)::value;
@@ -362,7 +407,15 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
     const bool more = i + 1 < total;
     if (more) stage_issue((i + 1) % G, nsl - 1 - (i + 1) / G, buf ^ 1);
     const int qa = qs0 + sl * BQS;
-    if (!CAUSAL || qa + BQS - 1 >= kw0) {
+    const bool run = !CAUSAL || qa + BQS - 1 >= kw0;
+    if (run) {
+      // DS: tile base of half t (wave-uniform); a causally masked tile goes to the trash tile
+      auto ds_tile = [&](int t) -> char* {
+        const int qb = (qa >> 5) + t;
+        const long idx = CAUSAL ? (long)qb * (qb + 1) / 2 + kb32 : (long)qb * nb32 + kb32;
+        char* p = (char*)dSw + ((long)(b * Hq + hk * G + i % G) * tiles_bh + idx) * 2048;
+        return (!CAUSAL || qb >= kb32) ? p : ds_trash;
+      };
       auto body = [&](auto diagc) {
         constexpr bool DIAG = decltype(diagc)::value;
         constexpr int BO = buf * 2 * SL;  // this slice's buffer; Q image at BO, dO image at BO + SL
@@ -499,13 +552,23 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
                 std::integral_constant<int, (2 * ((q + TW) >> 3) + ((q + TW) & 1)) * NDB + (((q + TW) >> 1) & 3)>{},
                 tc);
         };
+        char* const dst0 = DS ? ds_tile(0) : nullptr;
         sfor<16>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
+          (void)dsv0, (void)dsv1, (void)dst0;  // odr-use outside the if constexpr (clang capture of nested generic lambdas)
           dvdk_slot(qc, I0{}, pa0, pb0, da0, db0);
           pds1(s1, dp1, 1, q);
           if constexpr (q == 7) {
             pa1 = acc_to_bf16(s1, 0);
             da1 = acc_to_bf16(dp1, 0);
+          }
+          if constexpr (DS && q == 2) {
+            hs_fence();
+            asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(dsv0), "v"(da0), "s"(dst0) : "memory");
+          }
+          if constexpr (DS && q == 6) {
+            hs_fence();
+            asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(dsv1), "v"(db0), "s"(dst0) : "memory");
           }
         });
         hs_fence();
@@ -518,15 +581,28 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
         asm volatile(HS_GAP : "+v"(pa1), "+v"(pb1), "+v"(da1), "+v"(db1));
         hs_fence();
         // ---- P4: dV, dK += half 1 (T_1 read TW ahead)
-        sfor<16>([&](auto qc) { dvdk_slot(qc, I1{}, pa1, pb1, da1, db1); });
+        char* const dst1 = DS ? ds_tile(1) : nullptr;
+        sfor<16>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          (void)dsv0, (void)dsv1, (void)dst1;
+          dvdk_slot(qc, I1{}, pa1, pb1, da1, db1);
+          if constexpr (DS && q == 2) {
+            hs_fence();
+            asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(dsv0), "v"(da1), "s"(dst1) : "memory");
+          }
+          if constexpr (DS && q == 6) {
+            hs_fence();
+            asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(dsv1), "v"(db1), "s"(dst1) : "memory");
+          }
+        });
         hs_fence();
         (void)fq_of;
       };
       if (CAUSAL && qa < kw0 + 31) body(std::integral_constant<bool, CAUSAL>{});
       else body(std::false_type{});
     }
-    if (more) stage_finish(buf ^ 1);
-    __syncthreads();
+    if (more) stage_finish(buf ^ 1, run);
+    slice_barrier();
   };
   for (int i = 0; i < total; i += 2) {
     slice(IC<0>{}, i);
@@ -556,15 +632,17 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
 #undef HS_GAP
 #undef HS_MFA
 
-#define RCA_HS_INST(CC, MM)                                                                                       \
-  template __global__ void attn_bwd_dkdv_hs_kernel<CC, MM>(                                                     \
+#define RCA_HS_INST(CC, MM, DD)                                                                                   \
+  template __global__ void attn_bwd_dkdv_hs_kernel<CC, MM, DD>(                                                 \
       const bf16_t* __restrict__, const bf16_t* __restrict__, const bf16_t* __restrict__, const bf16_t* __restrict__, \
       const float* __restrict__, const float* __restrict__, bf16_t* __restrict__, bf16_t* __restrict__, int, int, int, \
-      int, long, long, long, long, long, long, float, float);
-RCA_HS_INST(true, true)
-RCA_HS_INST(false, true)
-RCA_HS_INST(true, false)
-RCA_HS_INST(false, false)
+      int, long, long, long, long, long, long, float, float, bf16_t* __restrict__, long);
+RCA_HS_INST(true, true, false)
+RCA_HS_INST(false, true, false)
+RCA_HS_INST(true, false, false)
+RCA_HS_INST(false, false, false)
+RCA_HS_INST(true, true, true)
+RCA_HS_INST(false, true, true)
 #undef RCA_HS_INST
 
 }  // namespace
@@ -586,10 +664,11 @@ RCA_API int rca_attn_set_dkdv_hs(int on) {
   return old;
 }
 
+// dSw != nullptr: the hand-scheduled kernel also writes the dS tiles (D = 128 only; the caller checks)
 void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                           const float* lse, const float* delta, bf16_t* dk, bf16_t* dv, int B, int S, int Hq, int Hk,
                           long sq, long sk, long sv, long sdo, long sdk, long sdv, float scale2, float scale,
-                          hipStream_t st) {
+                          hipStream_t st, bf16_t* dSw, long tiles_bh) {
   // RCA_ATTN_DKDV_NH=1 selects the unpipelined 32-row-slice variant (A/B measurements);
   // the hand-scheduled kernel for D = 128 unless RCA_ATTN_DKDV=base (g_dkdv_hs)
   static const int nh = [] {
@@ -598,10 +677,19 @@ void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, 
   }();
   const bool hs = g_dkdv_hs;
   const dim3 grid(B * Hk * (S / 128)), block(kThreads);
+  if (dSw != nullptr) {
+    if (causal)
+      hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<true, true, true>), grid, block, 0, st, q, k, v, dout, lse, delta, dk,
+                         dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, dSw, tiles_bh);
+    else
+      hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<false, true, true>), grid, block, 0, st, q, k, v, dout, lse, delta, dk,
+                         dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, dSw, tiles_bh);
+    return;
+  }
   if (hs && D == 128) {
 #define RCA_HS(CC, MM)                                                                                         \
-  hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<CC, MM>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, B, S, \
-                     Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale)
+  hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<CC, MM, false>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, \
+                     B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, (bf16_t*)nullptr, 0L)
     if (g_dkdv_hs_stage) {  // register staging (bisect / A/B)
       if (causal) RCA_HS(true, false); else RCA_HS(false, false);
     } else {

@@ -1,0 +1,186 @@
+// Attention backward without recomputation for dQ (D = 128): the hand-scheduled dK/dV kernel
+// (attention_dkdv.hip, DS variant) already builds dS = P * (dP - delta) in registers as the bf16
+// operand of its dK^T MFMAs; it stores each 32 x 32 tile once (2 KB, fragment order, XOR-swizzled
+// slots), and this file's dQ kernel reads them back: dQ = dS . K is a plain GEMM over the key
+// dimension, memory-bound on the dS bytes. Against the query-major dQ kernel of attention.hip
+// (which recomputes S = Q K^T, P and dP = dO V^T: three MFMA products per tile), the backward does
+// four products plus one dS read instead of seven products (cdna_hip_programming.md Appendix B
+// 'Attention backward': 5 products per tile is the recompute-free count; the fifth is here).
+// Deterministic: every dQ element is summed in one wave's registers, in key order; no atomics.
+//
+// Also here: delta = rowsum(dO * O), which the dK/dV kernel reads (attention.hip fused it into
+// the dQ kernel, which now runs after dK/dV).
+#include "attention_common.h"
+
+namespace {
+
+// delta[b, h, s] = sum_d dO[b, s, h, d] * O[b, s, h, d]: one 16-lane group per (b, h, s) row, 16 B
+// per lane (D = 128); consecutive groups = consecutive tokens of one head (coalesced writes)
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                         float* __restrict__ Delta, int B, int S, int Hq, long so,
+                                                         long sdo) {
+  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);  // (b * Hq + h) * S + s
+  if (row >= (long)B * Hq * S) return;
+  const int c = threadIdx.x & 15;
+  const long s = row % S, bh = row / S;
+  const long b = bh / Hq, h = bh % Hq;
+  const long tok = b * S + s;
+  const u32x4 ov = *reinterpret_cast<const u32x4*>(O + tok * so + h * 128 + 8 * c);
+  const u32x4 gv = *reinterpret_cast<const u32x4*>(dO + tok * sdo + h * 128 + 8 * c);
+  float of[8], gf[8];
+  unpack8(ov, of);
+  unpack8(gv, gf);
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc = fmaf(of[j], gf[j], acc);
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (c == 0) Delta[row] = acc;
+}
+
+// dQ from the dS tiles: one workgroup = 4 waves = 128 query rows of one (batch, query head); wave w
+// owns query block qb32 = 4 qb + w (32 rows) and accumulates dQ^T = K^T . dS^T (d on the MFMA row,
+// query on the lane) over 64-key steps. Per step the workgroup stages the step's K tile (64 x 128,
+// shared by the 4 waves) and each wave its own two dS tiles (2 x 2 KB, fragment order: the LDS-DMA
+// lands them byte for byte) into a 2-deep ring; K^T fragments are ds_read_b64_tr_b16 reads of the
+// K image (as V^T in the forward), dS^T fragments ds_read_b64_tr_b16 reads of the fragment-order
+// tiles (conflict-free under the store-side XOR swizzle). Causal: the longest query blocks first.
+template <bool CAUSAL>
+__global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* __restrict__ K,
+                                                                 const bf16_t* __restrict__ dSw,
+                                                                 bf16_t* __restrict__ dQ, int B, int S, int Hq,
+                                                                 int Hk, long sk, long sdq, long tiles_bh,
+                                                                 float scale) {
+  constexpr int D = 128, BQ = 128, BK = 64, NDB = 4, KT = BK * D * 2, DST = 4 * 4096, SLOT = KT + DST,
+                G8 = Img<D>::G8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+
+  const int nqb = S / BQ, G = Hq / Hk, nb32 = S >> 5;
+  int bhk, item;
+  xcd_group_map(blockIdx.x, B * Hk, G * nqb, bhk, item);  // the G x nqb blocks of a kv head share K
+  const int qr = item / G, b = bhk / Hk, hk = bhk % Hk, hq = hk * G + item % G;
+  const int qb = CAUSAL ? nqb - 1 - qr : qr;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qb32 = 4 * qb + w;
+  const int nstep = CAUSAL ? 2 * (qb + 1) : S / BK;
+
+  DmaStage<D, BK> kst;
+  kst.init(K + (long)b * S * sk + (long)hk * D, sk, S, tid);
+  const char* dsb = (const char*)dSw + (long)(b * Hq + hq) * tiles_bh * 2048;
+  const __amdgpu_buffer_rsrc_t dsr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(dsb), (short)0, (int)(tiles_bh * 2048), 0x00020000);
+  const long trow = CAUSAL ? (long)qb32 * (qb32 + 1) / 2 : (long)qb32 * nb32;  // this wave's tile row
+
+  auto issue = [&](int st, int buf) {
+    char* base = smem + buf * SLOT;
+    kst.issue(st * BK, sk, base);
+    char* dl = base + KT + w * 4096;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int kb = 2 * st + tt;
+      if (!CAUSAL || kb <= qb32) {
+        const int so = __builtin_amdgcn_readfirstlane((int)((trow + kb) * 2048));
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              dsr, (__attribute__((address_space(3))) void*)(dl + tt * 2048 + pc * 1024), 16, lane * 16 + pc * 1024, so,
+              0, 0);
+      }
+    }
+  };
+
+  // per-lane read bases: K^T (the forward's V^T reads) and dS^T (two bases: read r of a k-step)
+  const int tb0 = Img<D>::tr_base(lane, 0), tb1 = Img<D>::tr_base(lane, 1);
+  int dsa[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int sp = (lane >> 4) & 1;
+    const int L = 8 * r + 4 * h + ((lane & 15) >> 2) + 32 * (lane & 1);
+    dsa[r] = sp * 1024 + 16 * (L ^ (4 * (lane & 1) + 8 * sp)) + 8 * ((lane >> 1) & 1);
+  }
+
+  f32x16 dq[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i) dq[i] = zero16();
+
+  issue(0, 0);
+  wait_dma();
+  __syncthreads();
+  auto step = [&](auto bufc, int st) {
+    constexpr int buf = decltype(bufc)::value;
+    if (st + 1 < nstep) issue(st + 1, buf ^ 1);
+    const char* Ks = smem + buf * SLOT;
+    const char* Ds = Ks + KT + w * 4096;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int kb = 2 * st + tt;
+      if (!CAUSAL || kb <= qb32) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int kk = 2 * tt + ks;  // 16-key step inside the 64-key K tile
+          bf16x8_t fr[NDB + 1];
+#pragma unroll
+          for (int db = 0; db < NDB; ++db)
+            fr[db] = lds_tr8_asm(Ks + tb0 + G8 * (2 * kk) + 512 * db, Ks + tb1 + G8 * (2 * kk + 1) + 512 * db);
+          fr[NDB] = lds_tr8_asm(Ds + tt * 2048 + dsa[0] + 256 * ks, Ds + tt * 2048 + dsa[1] + 256 * ks);
+          lds_tr_settle(fr);
+#pragma unroll
+          for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[db], fr[NDB], dq[db]);
+        }
+      }
+    }
+    if (st + 1 < nstep) wait_dma();
+    __syncthreads();
+  };
+  for (int st = 0; st < nstep; st += 2) {  // nstep is even (S % 128 == 0)
+    step(IC<0>{}, st);
+    step(IC<1>{}, st + 1);
+  }
+
+  // dQ^T accumulators: d = 32 db + (r & 3) + 8 (r >> 2) + 4 h on the registers, the query on the lane
+  const int qrow = qb32 * 32 + (lane & 31);
+  bf16_t* dQr = dQ + ((long)b * S + qrow) * sdq + (long)hq * D;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      store4(dQr + 32 * db + 8 * g + 4 * h, dq[db][4 * g] * scale, dq[db][4 * g + 1] * scale,
+             dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
+  }
+}
+
+// explicit instantiations: hipcc does not always emit the host launch stub of a kernel template
+// instantiated only through its launcher (an undefined __device_stub__ symbol at load time)
+template __global__ void attn_dq_ds_kernel<true>(const bf16_t* __restrict__, const bf16_t* __restrict__,
+                                                 bf16_t* __restrict__, int, int, int, int, long, long, long, float);
+template __global__ void attn_dq_ds_kernel<false>(const bf16_t* __restrict__, const bf16_t* __restrict__,
+                                                  bf16_t* __restrict__, int, int, int, int, long, long, long, float);
+
+}  // namespace
+
+// bytes of the dS workspace for this shape (0: the recompute path, attention.hip); the last 2 KB
+// tile is the dK/dV kernel's trash tile for causally masked halves
+long rca_attn_ds_ws_bytes(int B, int S, int Hq, int D, bool causal) {
+  if (D != 128 || S % 128) return 0;
+  const long nb = S / 32, tiles = causal ? nb * (nb + 1) / 2 : nb * nb;
+  if (tiles * 2048 >= (1L << 31)) return 0;  // the dQ kernel's per-(batch, head) buffer range is 32-bit
+  return ((long)B * Hq * tiles + 1) * 2048;
+}
+
+void rca_attn_launch_delta(const bf16_t* o, const bf16_t* dout, float* delta, int B, int S, int Hq, long so, long sdo,
+                           hipStream_t st) {
+  const long rows = (long)B * Hq * S;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, st, o, dout, delta, B, S, Hq,
+                     so, sdo);
+}
+
+void rca_attn_launch_dq_ds(bool causal, const bf16_t* k, const bf16_t* dsw, bf16_t* dq, int B, int S, int Hq, int Hk,
+                           long sk, long sdq, float scale, hipStream_t st) {
+  const long nb = S / 32, tiles = causal ? nb * (nb + 1) / 2 : nb * nb;
+  const dim3 grid(B * Hq * (S / 128)), block(kThreads);
+  if (causal)
+    hipLaunchKernelGGL((attn_dq_ds_kernel<true>), grid, block, 0, st, k, dsw, dq, B, S, Hq, Hk, sk, sdq, tiles, scale);
+  else
+    hipLaunchKernelGGL((attn_dq_ds_kernel<false>), grid, block, 0, st, k, dsw, dq, B, S, Hq, Hk, sk, sdq, tiles, scale);
+}

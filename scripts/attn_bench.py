@@ -38,6 +38,13 @@ def main():
               f"(bwd {tfb - tf:.3f} ms, {2.5 * flops_f / (tfb - tf) / 1e9:.0f} TF)", flush=True)
 
     run("rca-hip", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
+    if os.environ.get("ATTN_BWD_AB"):  # interleaved A/B of the backward modes (0: recompute dQ, 1: dS tiles)
+        lib = ops._lib.lib()
+        for _ in range(3):
+            for mode in (0, 1):
+                prev = lib.rca_attn_set_bwd_mode(mode)
+                run(f"bwd-mode{mode}", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
+                lib.rca_attn_set_bwd_mode(prev)
     if os.environ.get("ATTN_WIDE_AB"):  # interleaved A/B of the forward variants
         lib = ops._lib.lib()
         for _ in range(3):

@@ -130,15 +130,19 @@ def test_dkdv_hand_scheduled_matches_compiler_scheduled(B, S, Hq, Hk, causal, mo
     do = _mk(B, S, Hq, D, 14)
     lib = ops._lib.lib()
     grads = []
-    for hs in (0, mode):
-        prev = lib.rca_attn_set_dkdv_hs(hs)
-        try:
-            qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
-            ops.flash_attention(qq, kk, vv, causal).backward(do)
-            torch.cuda.synchronize()
-        finally:
-            lib.rca_attn_set_dkdv_hs(prev)
-        grads.append((qq.grad, kk.grad, vv.grad))
+    prev_bwd = lib.rca_attn_set_bwd_mode(0)  # the recompute path: the dkdv selector applies there
+    try:
+        for hs in (0, mode):
+            prev = lib.rca_attn_set_dkdv_hs(hs)
+            try:
+                qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+                ops.flash_attention(qq, kk, vv, causal).backward(do)
+                torch.cuda.synchronize()
+            finally:
+                lib.rca_attn_set_dkdv_hs(prev)
+            grads.append((qq.grad, kk.grad, vv.grad))
+    finally:
+        lib.rca_attn_set_bwd_mode(prev_bwd)
     (q0, k0, v0), (q1, k1, v1) = grads
     assert torch.equal(q0, q1)
     assert _err(k1, k0) < 1e-2 and _err(v1, v0) < 1e-2, (_err(k1, k0), _err(v1, v0))
@@ -189,3 +193,55 @@ def test_fwd_large_logits_rescale(causal, mode):
     o_ref = ref.attention_ref(q.float(), k.float(), v.float(), causal)
     assert torch.isfinite(o.float()).all()
     assert _err(o, o_ref) < 2e-2
+
+
+def _bwd(q, k, v, do, causal, mode):
+    lib = ops._lib.lib()
+    prev = lib.rca_attn_set_bwd_mode(mode)
+    try:
+        qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+        o = ops.flash_attention(qq, kk, vv, causal)
+        o.backward(do)
+        torch.cuda.synchronize()
+    finally:
+        lib.rca_attn_set_bwd_mode(prev)
+    return o.detach(), qq.grad, kk.grad, vv.grad
+
+
+@pytest.mark.parametrize("B,S,Hq,Hk,causal", [(2, 256, 4, 2, True), (1, 384, 4, 4, False), (1, 1024, 8, 2, True),
+                                              (2, 1024, 32, 8, True), (2, 512, 32, 8, False), (1, 4096, 8, 8, True)])
+def test_recompute_free_dq_matches_reference_and_recompute_path(B, S, Hq, Hk, causal):
+    """Backward mode 1 (default, D = 128): the dK/dV kernel stores the bf16 dS tiles and dQ = dS.K is
+    read back from them (attention_dq.hip). Against the fp32 reference; against mode 0 (the dQ kernel
+    that recomputes S, P and dP) dK and dV are bitwise equal (same hand-scheduled products) and dQ
+    agrees to bf16 rounding."""
+    D = 128
+    q, k, v = _mk(B, S, Hq, D, 61), _mk(B, S, Hk, D, 62), _mk(B, S, Hk, D, 63)
+    do = _mk(B, S, Hq, D, 64)
+    assert ops._lib.lib().rca_attn_bwd_ws_bytes(B, S, Hq, Hk, D, int(causal)) > 0
+    o1, dq1, dk1, dv1 = _bwd(q, k, v, do, causal, 1)
+    o0, dq0, dk0, dv0 = _bwd(q, k, v, do, causal, 0)
+    assert torch.equal(o1, o0)
+    assert torch.equal(dk1, dk0) and torch.equal(dv1, dv0)
+    assert _err(dq1, dq0) < 1e-2, _err(dq1, dq0)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref.attention_ref(qr, kr, vr, causal).backward(do.float())
+    assert _err(dq1, qr.grad) < 3e-2 and _err(dk1, kr.grad) < 3e-2 and _err(dv1, vr.grad) < 3e-2
+    assert torch.isfinite(dq1).all() and dq1.float().abs().amax(dim=(1, 3)).min() > 0
+
+
+def test_recompute_free_dq_large_logits_and_determinism():
+    """Scores spanning hundreds of log2 units (P saturates to 0/1 across tiles) through the dS-tile
+    path, and bitwise run-to-run reproducibility of dQ (each element summed by one wave, in key order)."""
+    B, S, Hq, Hk, D = 1, 2048, 8, 2, 128
+    q, k, v = _mk(B, S, Hq, D, 71) * 6, _mk(B, S, Hk, D, 72) * 6, _mk(B, S, Hk, D, 73)
+    do = _mk(B, S, Hq, D, 74)
+    runs = [_bwd(q, k, v, do, True, 1) for _ in range(3)]
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref.attention_ref(qr, kr, vr, True).backward(do.float())
+    _, dq, dk, dv = runs[0]
+    assert torch.isfinite(dq).all()
+    assert _err(dq, qr.grad) < 3e-2 and _err(dk, kr.grad) < 3e-2 and _err(dv, vr.grad) < 3e-2
