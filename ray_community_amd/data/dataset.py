@@ -79,6 +79,14 @@ class Dataset:
         self._name = name
         self._materialized: Optional[List[Tuple[Any, Any]]] = None
 
+    def __getstate__(self):
+        # the plan and any materialised refs travel; the last execution's executor / resource
+        # manager (threads, locks) stay with the process that ran it
+        st = dict(self.__dict__)
+        for k in ("_executor", "_exec_rm"):
+            st.pop(k, None)
+        return st
+
     # ------------------------------------------------------------------ plan helpers
     def _with(self, op) -> "Dataset":
         return Dataset(self._inputs, self._ops + [op], self._name)
