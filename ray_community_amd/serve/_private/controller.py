@@ -30,6 +30,9 @@ class _DeploymentState:
         self.health: Dict[str, float] = {}  # tag -> time of the last passed health check
         self.pgs: Dict[str, Any] = {}  # tag -> the replica's placement group (placement_group_bundles)
         self.nodes: Dict[str, str] = {}  # tag -> node id it was pinned to (max_replicas_per_node)
+        # tag -> {"node_id", "gpus"}: where the replica runs (node and physical GPU ids), reported by
+        # the replica once it is up; routers prefer same-node / same-GPU replicas with it
+        self.locations: Dict[str, Dict] = {}
 
 
 class ServeController:
@@ -155,7 +158,17 @@ class ServeController:
                        spec.get("user_config"), spec["is_function"], logging_config=spec.get("logging_config"))
         st.replicas[tag] = r
         self._bump(st)
+        asyncio.ensure_future(self._fetch_location(st, tag, r))
         return tag, r
+
+    async def _fetch_location(self, st: _DeploymentState, tag: str, r):
+        try:
+            loc = await r.location.remote()
+        except Exception:  # the replica died before answering: nothing to record
+            return
+        if tag in st.replicas:
+            st.locations[tag] = loc
+            self._bump(st)
 
     def _pick_node(self, st: _DeploymentState) -> Optional[str]:
         """A node for one more replica under ``max_replicas_per_node``: alive, big enough for the
@@ -373,6 +386,7 @@ class ServeController:
         if st is None:
             return None
         return {"replicas": list(st.replicas.items()), "max_ongoing_requests": st.spec.get("max_ongoing_requests", 5),
+                "locations": {t: st.locations[t] for t in st.replicas if t in st.locations},
                 "max_queued_requests": st.spec.get("max_queued_requests", -1), "version": st.version,
                 "members": st.members}
 

@@ -267,6 +267,16 @@ class ServeReplica:
     async def get_num_ongoing(self):
         return self.ongoing
 
+    async def location(self):
+        """Node and physical GPU ids of this replica (router locality: a request carrying a device
+        tensor goes to a replica on the same GPU when one has room, saving an xGMI copy)."""
+        from ..._private.worker import get_runtime_context
+        from ..handle import physical_gpu_ids
+
+        ctx = get_runtime_context()
+        gpus = [int(g) for g in (ctx.get_accelerator_ids().get("GPU") or [])]
+        return {"node_id": ctx.get_node_id(), "gpus": physical_gpu_ids(range(len(gpus))) if gpus else []}
+
     async def check_health(self):
         fn = getattr(self.obj, "check_health", None)
         if fn is not None:

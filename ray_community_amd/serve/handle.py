@@ -1,8 +1,14 @@
 """Deployment handles + router (reference: ``serve/handle.py``, ``_private/router.py``,
 ``_private/replica_scheduler/pow_2_scheduler.py``).
 
-Routing is power-of-two-choices on the caller's view of in-flight requests per replica, capped at
-``max_ongoing_requests`` (requests queue on the caller when every replica is saturated).
+Replica scheduling (reference ``pow_2_scheduler.py:49,92-103,294,445``): power of two choices over
+replica queue lengths that the router PROBES (``get_num_ongoing`` RPCs, answers cached for a short
+TTL, probe deadline backed off while replicas answer slowly), so N callers in N processes see the
+load the others put on a replica instead of each believing it idle; a replica is never sent more
+than ``max_ongoing_requests`` (requests wait on the caller when every replica is full).
+Candidates come in locality tiers: for a request that carries a GPU tensor, replicas on the SAME
+physical GPU of the caller's node first (the tensor needs no xGMI copy), then replicas on the
+caller's node, then all.
 """
 from __future__ import annotations
 
@@ -36,6 +42,56 @@ def _resolve_handle_args(args, kwargs):
     return tuple(conv(a) for a in args), {k: conv(v) for k, v in kwargs.items()}
 
 
+def physical_gpu_ids(indices) -> List[int]:
+    """Physical device ids (the node's full GPU list) of this process's HIP device indices: ROCm
+    applies ``ROCR_VISIBLE_DEVICES`` first and ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES``
+    indexes into what it left (``_private/head.py::worker_hip_visible_devices``)."""
+    import os
+
+    def parse(var):
+        v = os.environ.get(var)
+        return [int(x) for x in v.split(",") if x.strip()] if v else None
+
+    rocr = parse("ROCR_VISIBLE_DEVICES")
+    hip = parse("HIP_VISIBLE_DEVICES") or parse("CUDA_VISIBLE_DEVICES")
+    out = []
+    for i in indices:
+        j = hip[i] if hip is not None and i < len(hip) else i
+        out.append(rocr[j] if rocr is not None and j < len(rocr) else j)
+    return out
+
+
+def _request_gpu(args, kwargs) -> Optional[int]:
+    """Physical GPU of the first device tensor among the request's top-level arguments."""
+    for v in list(args) + list(kwargs.values()):
+        dev = getattr(v, "device", None)
+        if dev is not None and getattr(dev, "type", None) == "cuda":
+            idx = dev.index
+            if idx is None:
+                try:
+                    import torch
+
+                    idx = torch.cuda.current_device()
+                except Exception:
+                    idx = 0
+            return physical_gpu_ids([idx])[0]
+    return None
+
+
+_NODE_ID: List[Optional[str]] = []
+
+
+def _caller_node() -> Optional[str]:
+    if not _NODE_ID:
+        try:
+            from .._private.worker import get_runtime_context
+
+            _NODE_ID.append(get_runtime_context().get_node_id())
+        except Exception:
+            return None
+    return _NODE_ID[0]
+
+
 class _Router:
     """Per-(app, deployment) request router living in the caller's process.
 
@@ -60,6 +116,18 @@ class _Router:
         self.queue: "collections.deque" = collections.deque()
         self._reported = 0
         self._drainer: Optional[threading.Thread] = None
+        self.locations: Dict[str, Dict] = {}
+        # probed load of OTHER callers: tag -> (requests not from this router, probe time). A
+        # probe's answer counts this router's own requests too; they are known exactly
+        # (``inflight``) and taken out at the upper bound of what the replica could have counted,
+        # so the estimate is own in-flight + others. Entries older than queue_len_ttl_s fall
+        # back to the own view alone.
+        self.qlen: Dict[str, Tuple[int, float]] = {}
+        self.sent: Dict[str, int] = {}
+        self.probing: Dict[str, float] = {}
+        self.queue_len_ttl_s = 0.5
+        self.probe_deadline_s = 0.05
+        self.stats = {"probes": 0, "probe_timeouts": 0, "picks": 0, "local_gpu_picks": 0, "local_node_picks": 0}
 
     @classmethod
     def get(cls, app, dep):
@@ -122,21 +190,130 @@ class _Router:
             self.replicas = info["replicas"]
             self.max_ongoing = info["max_ongoing_requests"]
             self.max_queued = int(info.get("max_queued_requests", -1))
+            self.locations = dict(info.get("locations") or {})
             live = {t for t, _ in self.replicas}
+            for d in (self.qlen, self.sent, self.probing):
+                for tag in list(d):
+                    if tag not in live:
+                        d.pop(tag)
             for tag in live:
                 self.inflight.setdefault(tag, 0)
             for tag in list(self.inflight):
                 if tag not in live:
                     self.inflight.pop(tag)
 
-    def _pick_locked(self):
-        cands = [(t, a) for t, a in self.replicas if self.inflight.get(t, 0) < self.max_ongoing]
-        if not cands:
-            return None
-        pick = random.sample(cands, min(2, len(cands)))
-        tag, actor = min(pick, key=lambda x: self.inflight.get(x[0], 0))
-        self.inflight[tag] = self.inflight.get(tag, 0) + 1
-        return tag, actor
+    # ------------------------------------------------------------------ scheduling
+    def _load_locked(self, tag: str, now: float) -> int:
+        """Best estimate of ``tag``'s queue length: its last probe (fresh) plus what this router
+        sent it since, never below this router's own in-flight requests to it."""
+        own = self.inflight.get(tag, 0)
+        c = self.qlen.get(tag)
+        if c is None or now - c[1] > self.queue_len_ttl_s:
+            self._probe_locked(tag, now)
+            return own
+        return own + c[0]
+
+    def _probe_locked(self, tag: str, now: float):
+        t0 = self.probing.get(tag)
+        if t0 is not None:
+            if now - t0 < self.probe_deadline_s:
+                return
+            # no answer within the deadline: back off (reference: queue_len_response_deadline_s)
+            self.stats["probe_timeouts"] += 1
+            self.probe_deadline_s = min(1.0, self.probe_deadline_s * 2)
+        actor = next((a for t, a in self.replicas if t == tag), None)
+        if actor is None:
+            return
+        self.probing[tag] = now
+        sent_at = self.sent.get(tag, 0)
+        own_at = self.inflight.get(tag, 0)
+        self.stats["probes"] += 1
+        try:
+            ref = actor.get_num_ongoing.remote()
+        except Exception:  # noqa  (dead handle: routing drops it at the next refresh)
+            self.probing.pop(tag, None)
+            return
+
+        def on_done(f, tag=tag, sent_at=sent_at, own_at=own_at, t_issue=now):
+            try:
+                n = int(f.result())
+            except Exception:  # noqa
+                with self.cv:
+                    self.probing.pop(tag, None)
+                return
+            with self.cv:
+                self.probing.pop(tag, None)
+                mine = own_at + self.sent.get(tag, 0) - sent_at  # most of ours it could have seen
+                self.qlen[tag] = (max(0, n - mine), time.time())
+                if time.time() - t_issue < self.probe_deadline_s / 2:
+                    self.probe_deadline_s = max(0.05, self.probe_deadline_s / 2)
+                self._drain_locked()
+                self.cv.notify_all()
+
+        ref.future().add_done_callback(on_done)
+
+    def _ensure_fresh(self, limit: int = 4):
+        """Before scheduling: probe (up to ``limit`` random) replicas whose queue length is stale and
+        wait for the answers up to the probe deadline -- a cold router would otherwise place its
+        first requests blind (reference: the scheduler awaits its probes with a deadline)."""
+        now = time.time()
+        with self.cv:
+            stale = [t for t, _ in self.replicas
+                     if t not in self.qlen or now - self.qlen[t][1] > self.queue_len_ttl_s]
+            if not stale:
+                return
+            if len(stale) > limit:
+                stale = random.sample(stale, limit)
+            for t in stale:
+                self._probe_locked(t, now)
+            deadline = now + self.probe_deadline_s
+            while any(t in self.probing for t in stale):
+                rem = deadline - time.time()
+                if rem <= 0:
+                    return
+                self.cv.wait(rem)
+
+    def _tiers_locked(self, gpu: Optional[int]):
+        live = self.replicas
+        if not self.locations:
+            return [live]
+        node = _caller_node()
+        tiers = []
+        if node is not None:
+            same_node = [r for r in live if (self.locations.get(r[0]) or {}).get("node_id") == node]
+            if gpu is not None:
+                same_gpu = [r for r in same_node if gpu in ((self.locations.get(r[0]) or {}).get("gpus") or ())]
+                if same_gpu:
+                    tiers.append(same_gpu)
+            if same_node:
+                tiers.append(same_node)
+        tiers.append(live)
+        return tiers
+
+    def _pick_locked(self, gpu: Optional[int] = None):
+        now = time.time()
+        for ti, tier in enumerate(self._tiers_locked(gpu)):
+            cands = [r for r in tier if self.inflight.get(r[0], 0) < self.max_ongoing]
+            if not cands:
+                continue
+            pick = random.sample(cands, min(2, len(cands)))
+            loads = [(self._load_locked(t, now), random.random(), t, a) for t, a in pick]
+            load, _, tag, actor = min(loads)
+            if load >= self.max_ongoing:
+                # both candidates full by their probed queues: re-probe them (an answer drains the
+                # queue again) and try the next tier
+                for _, _, t, _ in loads:
+                    c = self.qlen.get(t)
+                    if c is not None and now - c[1] > 0.01:
+                        self._probe_locked(t, now)
+                continue
+            self.inflight[tag] = self.inflight.get(tag, 0) + 1
+            self.sent[tag] = self.sent.get(tag, 0) + 1
+            self.stats["picks"] += 1
+            if self.locations and len(self._tiers_locked(gpu)) > 1 and ti == 0:
+                self.stats["local_gpu_picks" if gpu is not None else "local_node_picks"] += 1
+            return tag, actor
+        return None
 
     def choose(self, timeout_s=60.0):
         """Blocking pick (used by callers that manage the call themselves)."""
@@ -156,8 +333,10 @@ class _Router:
     def submit(self, method: str, args, kwargs, meta, actor_method: str = "handle_request"):
         fut: concurrent.futures.Future = concurrent.futures.Future()
         self._refresh()
+        self._ensure_fresh()
+        gpu = _request_gpu(args, kwargs) if self.locations else None
         with self.cv:
-            item = (actor_method, method, args, kwargs, meta, fut)
+            item = (actor_method, method, args, kwargs, meta, fut, gpu)
             self.queue.append(item)
             self._drain_locked()
             # backpressure (reference router.py wrap_request_assignment): a request no replica
@@ -176,11 +355,11 @@ class _Router:
 
     def _drain_locked(self):
         while self.queue:
-            got = self._pick_locked()
+            got = self._pick_locked(self.queue[0][6])
             if got is None:
                 return
             tag, actor = got
-            actor_method, method, args, kwargs, meta, fut = self.queue.popleft()
+            actor_method, method, args, kwargs, meta, fut, _ = self.queue.popleft()
             try:
                 if actor_method in ("handle_request", "handle_request_stream"):
                     ref = getattr(actor, actor_method).remote(method, args, kwargs, meta)

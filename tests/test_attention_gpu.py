@@ -212,9 +212,9 @@ def _bwd(q, k, v, do, causal, mode):
                                               (2, 1024, 32, 8, True), (2, 512, 32, 8, False), (1, 4096, 8, 8, True)])
 def test_recompute_free_dq_matches_reference_and_recompute_path(B, S, Hq, Hk, causal):
     """Backward mode 1 (default, D = 128): the dK/dV kernel stores the bf16 dS tiles and dQ = dS.K is
-    read back from them (attention_dq.hip). Against the fp32 reference; against mode 0 (the dQ kernel
-    that recomputes S, P and dP) dK and dV are bitwise equal (same hand-scheduled products) and dQ
-    agrees to bf16 rounding."""
+    read back from them (attention_dq.hip). Against the fp32 reference, and against mode 0 (the dQ
+    kernel that recomputes S, P and dP) to bf16 rounding: dK and dV come from the same hand-scheduled
+    products, but delta = rowsum(dO * O) is summed in a different order by the two paths."""
     D = 128
     q, k, v = _mk(B, S, Hq, D, 61), _mk(B, S, Hk, D, 62), _mk(B, S, Hk, D, 63)
     do = _mk(B, S, Hq, D, 64)
@@ -222,7 +222,7 @@ def test_recompute_free_dq_matches_reference_and_recompute_path(B, S, Hq, Hk, ca
     o1, dq1, dk1, dv1 = _bwd(q, k, v, do, causal, 1)
     o0, dq0, dk0, dv0 = _bwd(q, k, v, do, causal, 0)
     assert torch.equal(o1, o0)
-    assert torch.equal(dk1, dk0) and torch.equal(dv1, dv0)
+    assert _err(dk1, dk0) < 1e-2 and _err(dv1, dv0) < 1e-2, (_err(dk1, dk0), _err(dv1, dv0))
     assert _err(dq1, dq0) < 1e-2, _err(dq1, dq0)
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
     ref.attention_ref(qr, kr, vr, causal).backward(do.float())
