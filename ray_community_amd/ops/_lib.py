@@ -60,6 +60,7 @@ _SIGS = {
     "rca_attn_bwd2": (c_int, [c_void_p] * 10 + [c_int] * 5 + [c_ll] * 8 + [c_float, c_int, c_void_p, c_ll, c_void_p]),
     "rca_attn_bwd_ws_bytes": (c_ll, [c_int] * 6),
     "rca_attn_set_bwd_mode": (c_int, [c_int]),
+    "rca_attn_set_hs_nops": (c_int, [c_int]),
     "rca_crop_resize_normalize": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "rca_bn_workspace": (c_ll, [c_ll, c_int]),
     "rca_bn_fwd": (c_int, [c_void_p] * 9 + [c_ll, c_int, c_float, c_float, c_int, c_void_p]),

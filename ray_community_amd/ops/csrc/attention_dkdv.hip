@@ -277,10 +277,21 @@ __device__ __forceinline__ void hs_xdl_gap() { asm volatile("s_nop 7\n\ts_nop 7\
 // v_accvgpr_mov of an accumulator), and its hazard recognizer does not pad copies that feed an asm
 // MFMA: without these wait states an MFMA read a stale K fragment (11 wrong dS elements in one
 // diagonal tile, scripts/diag/attn_ds_diag.py). The s_nop sits in the MFMA gap with the fillers.
-#define HS_MFK(acc, a, b) \
-  asm volatile("s_nop 3\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b))
-#define HS_MFA(acc, a, b) \
-  asm volatile("s_nop 3\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
+// NOPS: the s_nop operand (3 = 4 wait states; 1 = 2, LLVM's VALU-write -> MFMA-read count)
+#define HS_MFK(acc, a, b)                                                                                  \
+  do {                                                                                                     \
+    if constexpr (NOPS == 1)                                                                               \
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));      \
+    else                                                                                                   \
+      asm volatile("s_nop 3\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));      \
+  } while (0)
+#define HS_MFA(acc, a, b)                                                                                  \
+  do {                                                                                                     \
+    if constexpr (NOPS == 1)                                                                               \
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));      \
+    else                                                                                                   \
+      asm volatile("s_nop 3\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));      \
+  } while (0)
 // XDL <-> VALU hazard gap that the registers crossing it pass through: the producer stays above it
 // and the consumer below it whatever the compiler reorders
 #define HS_GAP "s_nop 7\n\ts_nop 7\n\ts_nop 4"
@@ -293,7 +304,7 @@ __device__ __forceinline__ void hs_xdl_gap() { asm volatile("s_nop 7\n\ts_nop 7\
 // qb (qb + 1) / 2 + kb (causal, kb <= qb) or qb nb + kb. The four 16-B stores per query slice are
 // inline asm placed in MFMA gaps; the next slice's LDS-DMA is retired with a counted vmcnt(4), so
 // the stores stay in flight across the slice barrier.
-template <bool CAUSAL, bool DMA = true, bool DS = false>
+template <bool CAUSAL, bool DMA = true, bool DS = false, int NOPS = 3>
 __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
@@ -632,17 +643,19 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_hs_kernel(
 #undef HS_GAP
 #undef HS_MFA
 
-#define RCA_HS_INST(CC, MM, DD)                                                                                   \
-  template __global__ void attn_bwd_dkdv_hs_kernel<CC, MM, DD>(                                                 \
+#define RCA_HS_INST(CC, MM, DD, NN)                                                                               \
+  template __global__ void attn_bwd_dkdv_hs_kernel<CC, MM, DD, NN>(                                             \
       const bf16_t* __restrict__, const bf16_t* __restrict__, const bf16_t* __restrict__, const bf16_t* __restrict__, \
       const float* __restrict__, const float* __restrict__, bf16_t* __restrict__, bf16_t* __restrict__, int, int, int, \
       int, long, long, long, long, long, long, float, float, bf16_t* __restrict__, long);
-RCA_HS_INST(true, true, false)
-RCA_HS_INST(false, true, false)
-RCA_HS_INST(true, false, false)
-RCA_HS_INST(false, false, false)
-RCA_HS_INST(true, true, true)
-RCA_HS_INST(false, true, true)
+RCA_HS_INST(true, true, false, 3)
+RCA_HS_INST(false, true, false, 3)
+RCA_HS_INST(true, false, false, 3)
+RCA_HS_INST(false, false, false, 3)
+RCA_HS_INST(true, true, true, 3)
+RCA_HS_INST(false, true, true, 3)
+RCA_HS_INST(true, true, true, 1)
+RCA_HS_INST(false, true, true, 1)
 #undef RCA_HS_INST
 
 }  // namespace
@@ -655,6 +668,16 @@ static bool g_dkdv_hs = [] {
   return !(e && std::string(e) == "base");
 }();
 static bool g_dkdv_hs_stage = false;
+// wait states ahead of each asm MFMA of the dS-storing kernel (A/B: 1 or 3, the s_nop operand)
+static int g_hs_nops = [] {
+  const char* e = getenv("RCA_ATTN_HS_NOPS");
+  return e && atoi(e) == 1 ? 1 : 3;
+}();
+RCA_API int rca_attn_set_hs_nops(int n) {
+  const int old = g_hs_nops;
+  g_hs_nops = n;
+  return old;
+}
 // 0: compiler-scheduled kernel; 1: hand-scheduled (LDS-DMA staging); 2: hand-scheduled with
 // register staging
 RCA_API int rca_attn_set_dkdv_hs(int on) {
@@ -678,17 +701,20 @@ void rca_attn_launch_dkdv(int D, bool causal, const bf16_t* q, const bf16_t* k, 
   const bool hs = g_dkdv_hs;
   const dim3 grid(B * Hk * (S / 128)), block(kThreads);
   if (dSw != nullptr) {
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<true, true, true>), grid, block, 0, st, q, k, v, dout, lse, delta, dk,
-                         dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, dSw, tiles_bh);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<false, true, true>), grid, block, 0, st, q, k, v, dout, lse, delta, dk,
-                         dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, dSw, tiles_bh);
+#define RCA_DS(CC, NN)                                                                                           \
+  hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<CC, true, true, NN>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, \
+                     dv, B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, dSw, tiles_bh)
+    if (g_hs_nops == 1) {
+      if (causal) RCA_DS(true, 1); else RCA_DS(false, 1);
+    } else {
+      if (causal) RCA_DS(true, 3); else RCA_DS(false, 3);
+    }
+#undef RCA_DS
     return;
   }
   if (hs && D == 128) {
 #define RCA_HS(CC, MM)                                                                                         \
-  hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<CC, MM, false>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, \
+  hipLaunchKernelGGL((attn_bwd_dkdv_hs_kernel<CC, MM, false, 3>), grid, block, 0, st, q, k, v, dout, lse, delta, dk, dv, \
                      B, S, Hq, Hk, sq, sk, sv, sdo, sdk, sdv, scale2, scale, (bf16_t*)nullptr, 0L)
     if (g_dkdv_hs_stage) {  // register staging (bisect / A/B)
       if (causal) RCA_HS(true, false); else RCA_HS(false, false);

@@ -45,6 +45,13 @@ def main():
                 prev = lib.rca_attn_set_bwd_mode(mode)
                 run(f"bwd-mode{mode}", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
                 lib.rca_attn_set_bwd_mode(prev)
+    if os.environ.get("ATTN_NOPS_AB"):  # interleaved A/B of the dS kernel's MFMA wait states
+        lib = ops._lib.lib()
+        for _ in range(3):
+            for n in (3, 1):
+                prev = lib.rca_attn_set_hs_nops(n)
+                run(f"nops-{n}", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
+                lib.rca_attn_set_hs_nops(prev)
     if os.environ.get("ATTN_WIDE_AB"):  # interleaved A/B of the forward variants
         lib = ops._lib.lib()
         for _ in range(3):

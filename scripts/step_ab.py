@@ -41,10 +41,13 @@ def _toggles():
         # gate_up input gradient on hipBLASLt instead of the hand GEMM
         "noplan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", False),
         "plan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", True),
-        # attention backward: 0 = delta/dQ kernel + dK/dV kernel, 1 = one fused dK/dV/dQ pass
+        # attention backward: 0 = delta/dQ kernel (recomputes S, P, dP) + dK/dV, 1 = delta, dK/dV + dS tiles, dQ = dS.K
         "attn_split": lambda: _set_lib("rca_attn_set_bwd_mode", 0),
         "attn_fused": lambda: _set_lib("rca_attn_set_bwd_mode", 1),
         "attn_fwd_hs": lambda: _set_lib("rca_attn_set_fwd_mode", 2),
+        # wait states ahead of the hand-scheduled dK/dV kernel's asm MFMAs (s_nop 1 vs s_nop 3)
+        "nop1": lambda: _set_lib("rca_attn_set_hs_nops", 1),
+        "nop3": lambda: _set_lib("rca_attn_set_hs_nops", 3),
     }
 
 

@@ -245,3 +245,22 @@ def test_recompute_free_dq_large_logits_and_determinism():
     _, dq, dk, dv = runs[0]
     assert torch.isfinite(dq).all()
     assert _err(dq, qr.grad) < 3e-2 and _err(dk, kr.grad) < 3e-2 and _err(dv, vr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_ds_kernel_wait_state_variants_agree_bitwise(causal):
+    """The dS-storing dK/dV kernel with 2 (s_nop 1) and 4 (s_nop 3) wait states ahead of each asm MFMA
+    computes bit-identical gradients (a missing wait state shows up as stale MFMA operands)."""
+    B, S, Hq, Hk, D = 2, 1024, 8, 2, 128
+    q, k, v = _mk(B, S, Hq, D, 81), _mk(B, S, Hk, D, 82), _mk(B, S, Hk, D, 83)
+    do = _mk(B, S, Hq, D, 84)
+    lib = ops._lib.lib()
+    outs = []
+    for n in (3, 1):
+        prev = lib.rca_attn_set_hs_nops(n)
+        try:
+            outs.append(_bwd(q, k, v, do, causal, 1))
+        finally:
+            lib.rca_attn_set_hs_nops(prev)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
