@@ -119,6 +119,10 @@ def main():
                 "model_tflops_per_gpu": round(m["tokens_per_s"] / world * m["flops_per_token"] / 1e12, 1),
                 # per-step compute-stream stall on gradient/parameter collectives (max over ranks)
                 "exposed_comm_ms": round(float(m.get("exposed_comm_ms", 0.0)), 3),
+                # each rank's own ms/step over the timed steps (the job's number is the max)
+                "rank_ms_per_step_min": min(m.get("rank_ms_per_step") or [m["ms_per_step"]]),
+                "rank_ms_per_step_max": max(m.get("rank_ms_per_step") or [m["ms_per_step"]]),
+                "rank_ms_per_step": m.get("rank_ms_per_step"),
             },
         }
         print(json.dumps(out), flush=True)

@@ -668,10 +668,13 @@ static bool g_dkdv_hs = [] {
   return !(e && std::string(e) == "base");
 }();
 static bool g_dkdv_hs_stage = false;
-// wait states ahead of each asm MFMA of the dS-storing kernel (A/B: 1 or 3, the s_nop operand)
+// wait states ahead of each asm MFMA of the dS-storing kernel: the s_nop operand, 1 (2 wait
+// states, LLVM's VALU-write -> MFMA-read count; the default) or 3. Same-process A/B: bwd 1.025-1.050
+// vs 1.058-1.081 ms, 8B step 345.7 vs 349.0 ms median; gradients bitwise equal
+// (tests/test_attention_gpu.py::test_ds_kernel_wait_state_variants_agree_bitwise).
 static int g_hs_nops = [] {
   const char* e = getenv("RCA_ATTN_HS_NOPS");
-  return e && atoi(e) == 1 ? 1 : 3;
+  return e && atoi(e) == 3 ? 3 : 1;
 }();
 RCA_API int rca_attn_set_hs_nops(int n) {
   const int old = g_hs_nops;

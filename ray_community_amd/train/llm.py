@@ -127,10 +127,16 @@ def llama_train_loop_per_worker(config: dict):
     if world > 1:
         dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)
     exposed = float(ex_t.item())
-    el_t = torch.tensor([el], device="cuda" if dev_kind == "cuda" else "cpu", dtype=torch.float64)
+    # every rank's own timed-loop wall time (stragglers show up as a max/min spread); the job's
+    # elapsed time is the slowest rank's
+    dev = "cuda" if dev_kind == "cuda" else "cpu"
     if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = float(el_t.item())
+        all_el = [torch.zeros(1, device=dev, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(all_el, torch.tensor([el], device=dev, dtype=torch.float64))
+        rank_el = [float(t.item()) for t in all_el]
+    else:
+        rank_el = [el]
+    el = max(rank_el)
     tokens = steps * mb * seq_len * world
     metrics = {
         "loss": float(loss.item()) if loss is not None else float("nan"),
@@ -143,6 +149,7 @@ def llama_train_loop_per_worker(config: dict):
         "parallel": net.parallel_mode,
         "grad_reduce_dtype": config.get("grad_reduce_dtype", "bf16"),
         "exposed_comm_ms": exposed,
+        "rank_ms_per_step": [round(1000.0 * e / max(steps, 1), 3) for e in rank_el],
     }
     if dev_kind == "cuda":
         from .torch.config import group_info

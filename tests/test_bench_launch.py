@@ -24,6 +24,10 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["higher_is_better"] is True
     assert "ZeRO" in rec["config"]["data_parallel"] and rec["config"]["parallel_mode"] == "zero"
     assert rec["config"]["launch"] == "torchrun" and rec["config"]["grad_reduce_dtype"] == "fp32"
+    # per-rank step times: the job's ms/step is the slowest rank's
+    ranks = rec["extra"]["rank_ms_per_step"]
+    assert len(ranks) == 2 and rec["extra"]["rank_ms_per_step_max"] == max(ranks)
+    assert abs(rec["ms_per_step"] - max(ranks)) < 1e-2 and rec["extra"]["rank_ms_per_step_min"] == min(ranks)
 
 
 def test_bench_self_launch_two_workers_cpu(tmp_path):
