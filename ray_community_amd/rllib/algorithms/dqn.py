@@ -7,7 +7,7 @@ from typing import Dict
 import numpy as np
 
 from ..policy.sample_batch import SampleBatch, concat_samples
-from ..utils.replay_buffers import ReplayBuffer
+from ..utils.replay_buffers import EpisodeReplayBuffer, ReplayBuffer
 from .algorithm import Algorithm
 from .algorithm_config import AlgorithmConfig
 
@@ -27,6 +27,9 @@ class DQNConfig(AlgorithmConfig):
         self.rollout_fragment_length = 4
         self.td_error_loss_fn = "huber"
         self.model = {"fcnet_hiddens": [256, 256], "fcnet_activation": "relu", "vf_share_layers": True}
+        # frames stacked from the episodes' observations (the episode path: replay_buffer_config
+        # {"type": "EpisodeReplayBuffer"}; the module sees frame_stack x the observation)
+        self.frame_stack = 1
 
 
 class DQN(Algorithm):
@@ -37,11 +40,25 @@ class DQN(Algorithm):
         return DQNConfig()
 
     def _runner_extra(self):
-        return {"q_head": True}
+        extra = {"q_head": True}
+        if self._episode_mode():
+            extra["episode_frame_stack"] = int(getattr(self.config, "frame_stack", 1) or 1)
+        return extra
+
+    def _episode_mode(self) -> bool:
+        rb = self.config.replay_buffer_config or {}
+        t = rb.get("type")
+        return t is EpisodeReplayBuffer or t == "EpisodeReplayBuffer"
 
     def setup(self, config):
         super().setup(config)
-        self.buffer = ReplayBuffer(self.config.replay_buffer_config.get("capacity", 50000), seed=self.config.seed)
+        cap = self.config.replay_buffer_config.get("capacity", 50000)
+        if self._episode_mode():
+            # episodes path (reference: the new API stack's DQN): runners return episode chunks,
+            # the buffer samples n-step transitions with frame stacks read from the episodes
+            self.buffer = EpisodeReplayBuffer(cap, seed=self.config.seed)
+        else:
+            self.buffer = ReplayBuffer(cap, seed=self.config.seed)
         self._last_target = 0
 
     def _epsilon(self):
@@ -56,10 +73,18 @@ class DQN(Algorithm):
         cfg = self.config
         eps = self._epsilon()
         steps = max(1, cfg.get_rollout_fragment_length()) * self.local_runner.N
-        batches = self._foreach_runner("sample_transitions", steps, eps)
-        b = concat_samples(batches)
-        self.buffer.add(b)
-        n = b.count
+        episodic = self._episode_mode()
+        if episodic:
+            fs = int(getattr(cfg, "frame_stack", 1) or 1)
+            per_runner = self._foreach_runner("sample_episodes", steps, True, eps, fs)
+            eps_list = [e for lst in per_runner for e in lst]
+            self.buffer.add(eps_list)
+            n = sum(len(e) for e in eps_list)
+        else:
+            batches = self._foreach_runner("sample_transitions", steps, eps)
+            b = concat_samples(batches)
+            self.buffer.add(b)
+            n = b.count
         self._timesteps_total += n
         info = {"epsilon": eps}
         if self._timesteps_total >= cfg.num_steps_sampled_before_learning_starts:
@@ -67,7 +92,11 @@ class DQN(Algorithm):
             if cfg.training_intensity:
                 k = max(1, int(round(cfg.training_intensity * n / cfg.train_batch_size)))
             for _ in range(k):
-                mb = self.buffer.sample(cfg.train_batch_size)
+                if episodic:
+                    mb = self.buffer.sample(batch_size_B=cfg.train_batch_size, n_step=int(cfg.n_step),
+                                            gamma=float(cfg.gamma), frame_stack=fs)
+                else:
+                    mb = self.buffer.sample(cfg.train_batch_size)
                 mb.pop("batch_indexes", None)
                 info.update(self.learner_group.update("dqn", mb))
             if self._timesteps_total - self._last_target >= cfg.target_network_update_freq:

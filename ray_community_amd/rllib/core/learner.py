@@ -360,7 +360,10 @@ class Learner:
                 qn = qn_t.gather(1, an).squeeze(1)
             else:
                 qn = qn_t.max(1).values
-            y = b["rewards"] + cfg.get("gamma", 0.99) ** cfg.get("n_step", 1) * (1 - b["terminateds"].float()) * qn
+            # episode replay gives each sample's own step count (n-step returns clipped at the
+            # episode's end); the transition buffer uses the configured n_step for all
+            n = b["n_step"].float() if "n_step" in b else float(cfg.get("n_step", 1))
+            y = b["rewards"] + cfg.get("gamma", 0.99) ** n * (1 - b["terminateds"].float()) * qn
         td = qa - y
         loss = torch.nn.functional.huber_loss(qa, y, delta=1.0) if cfg.get("td_error_loss_fn", "huber") == "huber" \
             else (td ** 2).mean()

@@ -42,7 +42,16 @@ class EnvRunner:
         self.has_stateful_connectors = len(self.env_to_module) > 0
         self._ctx = VectorEnvContext(self.N)
         self._pending_mobs = None  # connector output for self.obs computed at the previous fragment's end
-        self.module = make_module(config, self.env_to_module.observation_space, self.env.action_space)
+        self._module_obs_space = self.env_to_module.observation_space
+        fs = int(config.get("episode_frame_stack", 1) or 1)
+        if fs > 1:  # episode-path frame stacking: the module sees fs observations concatenated
+            from ..utils.spaces import Box
+
+            sp = self._module_obs_space
+            self._module_obs_space = Box(np.concatenate([np.asarray(sp.low, np.float32)] * fs, -1),
+                                         np.concatenate([np.asarray(sp.high, np.float32)] * fs, -1),
+                                         dtype=np.float32)
+        self.module = make_module(config, self._module_obs_space, self.env.action_space)
         self.module.eval()
         self.stateful = bool(getattr(self.module, "is_stateful", False))
         # GPU inference (num_gpus_per_env_runner > 0): the module lives on the runner's GPU share,
@@ -73,8 +82,9 @@ class EnvRunner:
                 self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i)
 
     def spaces(self):
-        """(module observation space = the env-to-module pipeline's output, action space)."""
-        return self.env_to_module.observation_space, self.env.action_space
+        """(module observation space = the env-to-module pipeline's output, frame-stacked on the
+        episode path; action space)."""
+        return self._module_obs_space, self.env.action_space
 
     # ------------------------------------------------------------------ connectors
     def get_connector_state(self):
@@ -324,6 +334,79 @@ class EnvRunner:
         if self.callbacks is not None:
             self.callbacks.on_sample_end(env_runner=self, samples=b)
         return b
+
+    # ------------------------------------------------------------------ episodes (new API stack)
+    @torch.no_grad()
+    def sample_episodes(self, num_timesteps: int, explore: bool = True, epsilon: float = 0.0,
+                        frame_stack: int = 1):
+        """Sample ``num_timesteps`` env steps as ``SingleAgentEpisode`` chunks (reference:
+        ``SingleAgentEnvRunner.sample`` returning episodes). One episode per sub-env is kept
+        across calls; the call returns every episode that finished plus the chunk of every
+        ongoing one, and continues those with ``cut(frame_stack - 1)`` so the next chunk's
+        lookback holds the frames its first stack needs. The module's input is read FROM the
+        episodes: the last observation, or with ``frame_stack > 1`` the stack of the last
+        ``frame_stack`` observations (zeros before the episode's start) -- an episode-reading
+        frame-stacking connector, no per-env history kept anywhere else. Q-modules (DQN) act
+        epsilon-greedy; policy modules sample and record ``action_logp`` / ``vf_preds``."""
+        from .single_agent_episode import SingleAgentEpisode
+
+        N = self.N
+        fs = max(1, int(frame_stack))
+        if getattr(self, "_episodes", None) is None or getattr(self, "_episodes_fs", None) != fs:
+            self._episodes = []
+            for i in range(N):
+                ep = SingleAgentEpisode(observation_space=self.env.observation_space,
+                                        action_space=self.env.action_space)
+                ep.add_env_reset(np.asarray(self.obs[i]))
+                self._episodes.append(ep)
+            self._episodes_fs = fs
+        T = max(1, int(num_timesteps) // N)
+        done_eps = []
+        q_mode = hasattr(self.module, "q_values")
+        space = self.env.action_space
+        for _ in range(T):
+            if fs > 1:
+                mobs = np.stack([ep.get_frame_stack(fs) for ep in self._episodes]).astype(np.float32)
+            else:
+                mobs = np.stack([np.asarray(ep.get_observations(-1)) for ep in self._episodes]).astype(np.float32)
+            o = torch.from_numpy(np.ascontiguousarray(mobs))
+            extra = None
+            if q_mode:
+                a = self.module.q_values(o).argmax(-1).numpy()
+                if explore and epsilon > 0:
+                    rnd = self._rng.random(N) < epsilon
+                    if rnd.any():
+                        a[rnd] = self._rng.integers(0, space.n, int(rnd.sum()))
+            elif explore:
+                at, lp, v, _ = self.module.forward_exploration(o)
+                a = at.numpy()
+                extra = {"action_logp": lp.numpy(), "vf_preds": v.numpy()}
+            else:
+                at, v = self.module.forward_inference(o)
+                a = at.numpy()
+            nobs, r, te, tr, info = self.env.step(a)
+            for i, ep in enumerate(self._episodes):
+                done = bool(te[i] or tr[i])
+                fin = np.asarray(info["final_obs"][i] if done else nobs[i])
+                ep.add_env_step(fin, a[i], float(r[i]), terminated=bool(te[i]), truncated=bool(tr[i]) and not te[i],
+                                extra_model_outputs=None if extra is None else {k: v[i] for k, v in extra.items()})
+                if done:
+                    done_eps.append(ep)
+                    nxt = SingleAgentEpisode(observation_space=self.env.observation_space,
+                                             action_space=self.env.action_space)
+                    nxt.add_env_reset(np.asarray(nobs[i]))
+                    self._episodes[i] = nxt
+            self._track(r, te, tr, info)
+            self.obs = nobs
+        self.steps_sampled += N * T
+        out = [ep.finalize() for ep in done_eps]
+        for i, ep in enumerate(self._episodes):
+            if len(ep):
+                out.append(ep)
+                self._episodes[i] = ep.cut(len_lookback_buffer=fs - 1)
+        for ep in out:
+            ep.finalize()
+        return out
 
     def get_metrics(self) -> Dict:
         eps, cms = self.new_episodes, self.new_custom_metrics

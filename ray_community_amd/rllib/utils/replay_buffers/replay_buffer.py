@@ -6,7 +6,7 @@ from typing import Dict, Optional
 
 import numpy as np
 
-from ..policy.sample_batch import SampleBatch
+from ...policy.sample_batch import SampleBatch
 
 
 class ReplayBuffer:
