@@ -283,7 +283,11 @@ class Algorithm(Trainable):
         cb = getattr(self, "callbacks", None)
         if cb is not None:
             cb.on_evaluate_start(algorithm=self)
-        out = self._evaluate()
+        if getattr(self.config, "off_policy_estimation_methods", None) and getattr(self, "reader", None) is not None:
+            out = self._evaluate()
+            out["off_policy_estimator"] = self.estimate_off_policy()
+        else:
+            out = self._evaluate()
         if cb is not None:
             cb.on_evaluate_end(algorithm=self, evaluation_metrics=out)
         return out
@@ -308,6 +312,33 @@ class Algorithm(Trainable):
         return {"episode_reward_mean": float(np.mean(rets)) if rets else float("nan"),
                 "env_runners": {"episode_return_mean": float(np.mean(rets)) if rets else float("nan")},
                 "num_episodes": len(eps)}
+
+    def estimate_off_policy(self, batches: int = 8) -> Dict:
+        """Off-policy estimates of the current policy's value from ``batches`` offline batches,
+        one entry per ``config.off_policy_estimation_methods`` (reference:
+        ``Algorithm._run_offline_evaluation`` with ``rllib/offline/estimators``)."""
+        from ..policy.sample_batch import concat_samples
+
+        from ..offline.estimators import split_by_episode
+
+        methods = self.config.off_policy_estimation_methods or {}
+        stored = getattr(self.reader, "batches", None)  # JsonReader: the logged batches, in order (no repeats)
+        data = list(stored[:batches]) if stored is not None else [self.reader.next() for _ in range(batches)]
+        # episodes whole: with eps_id an episode logged across several batches is joined, and
+        # pieces the log cut off (no terminal step) are left out
+        flat = [b.flatten() if getattr(b, "fragment_shape", None) is not None else b for b in data]
+        joined = concat_samples(flat) if len(flat) > 1 else flat[0]
+        episodes = split_by_episode(joined, complete_only=True) or split_by_episode(joined)
+        module = self.get_module()
+        out = {}
+        for name, spec in methods.items():
+            spec = dict(spec)
+            cls = spec.pop("type")
+            est = cls(module, gamma=spec.pop("gamma", self.config.gamma), **spec)
+            for b in data:
+                est.train(b)
+            out[name] = est.estimate_episodes(episodes)
+        return out
 
     def compute_single_action(self, observation, state=None, explore: bool = False, policy_id=None, **kw):
         """One action for one observation. Recurrent modules: pass ``state`` (None = initial) and

@@ -20,6 +20,9 @@ class AlgorithmConfig:
         self.num_env_runners = 0
         self.input_ = "sampler"
         self.output = None
+        self.input_config = {}
+        self.output_config = {}
+        self.off_policy_estimation_methods = {}
         self.num_envs_per_env_runner = 1
         self.rollout_fragment_length: Any = "auto"
         self.batch_mode = "truncate_episodes"
@@ -153,11 +156,14 @@ class AlgorithmConfig:
         return self
 
     def evaluation(self, *, evaluation_interval=None, evaluation_duration=None, evaluation_duration_unit=None,
-                   evaluation_num_env_runners=None, evaluation_config=None, **kw):
+                   evaluation_num_env_runners=None, evaluation_config=None, off_policy_estimation_methods=None, **kw):
+        """``off_policy_estimation_methods``: {name: {"type": ImportanceSampling | ..., **kwargs}}:
+        ``evaluate()`` then also estimates the current policy's value from the offline input."""
         for k, v in dict(evaluation_interval=evaluation_interval, evaluation_duration=evaluation_duration,
                          evaluation_duration_unit=evaluation_duration_unit,
                          evaluation_num_env_runners=evaluation_num_env_runners,
-                         evaluation_config=evaluation_config).items():
+                         evaluation_config=evaluation_config,
+                         off_policy_estimation_methods=off_policy_estimation_methods).items():
             if v is not None:
                 setattr(self, k, v)
         return self
@@ -319,6 +325,10 @@ class AlgorithmConfig:
             self.input_ = input_
         if output is not None:
             self.output = output
+        if input_config is not None:
+            self.input_config = dict(input_config)
+        if output_config is not None:
+            self.output_config = dict(output_config)
         return self
 
     def callbacks(self, callbacks_class=None, **kw):

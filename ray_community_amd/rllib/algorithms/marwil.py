@@ -32,11 +32,16 @@ class MARWIL(Algorithm):
 
     def setup(self, config):
         super().setup(config)
-        from ..offline import JsonReader
+        from ..offline import DatasetReader, JsonReader, get_dataset_and_shards
 
         if not self.config.input_ or self.config.input_ == "sampler":
-            raise ValueError("MARWIL/BC need offline data: config.offline_data(input_=<dir or glob>)")
-        self.reader = JsonReader(self.config.input_, seed=self.config.seed)
+            raise ValueError("MARWIL/BC need offline data: config.offline_data(input_=<dir or glob> | \"dataset\")")
+        if self.config.input_ == "dataset":  # Ray Data rows (reference DatasetReader)
+            ds, _ = get_dataset_and_shards(self.config)
+            self.reader = DatasetReader(ds, batch_size=min(self.config.train_batch_size, 4096),
+                                        gamma=self.config.gamma, seed=self.config.seed)
+        else:
+            self.reader = JsonReader(self.config.input_, seed=self.config.seed)
 
     def training_step(self) -> Dict:
         batch = self.reader.sample(self.config.train_batch_size)

@@ -182,6 +182,10 @@ class EnvRunner:
         term = np.empty((N, T), dtype=bool)
         trunc = np.empty((N, T), dtype=bool)
         first_buf = np.empty((N, T), dtype=bool)
+        eid_buf = np.empty((N, T), dtype=np.int64)
+        if getattr(self, "_eps_ids", None) is None:  # running episode ids, unique per runner and sub-env
+            self._eps_ids = np.arange(N, dtype=np.int64) + (self.worker_index * 1_000_003 + 1) * (1 << 32)
+            self._eps_next = int(self._eps_ids.max()) + 1
         obs_buf = logits_buf = state_buf = None
         trunc_fix = []  # (t, env indices, module-input final obs, state after the step)
         gpu = self.device.type == "cuda"
@@ -229,6 +233,10 @@ class EnvRunner:
             rew[:, t] = r
             term[:, t] = te
             trunc[:, t] = tr
+            eid_buf[:, t] = self._eps_ids
+            for i in np.nonzero(te | tr)[0]:
+                self._eps_ids[i] = self._eps_next
+                self._eps_next += 1
             if tr.any():
                 idx = np.nonzero(tr)[0]
                 fo = self._peek_obs(info["final_obs"][idx], idx, an, r)
@@ -254,7 +262,8 @@ class EnvRunner:
         self.steps_sampled += N * T
         b = SampleBatch({SampleBatch.OBS: obs_buf, SampleBatch.ACTIONS: acts, SampleBatch.ACTION_LOGP: logp,
                          SampleBatch.VF_PREDS: vf, SampleBatch.REWARDS: rew, SampleBatch.TERMINATEDS: term,
-                         SampleBatch.TRUNCATEDS: trunc, SampleBatch.NEXT_VF_PREDS: next_vf})
+                         SampleBatch.TRUNCATEDS: trunc, SampleBatch.NEXT_VF_PREDS: next_vf,
+                         SampleBatch.EPS_ID: eid_buf})
         if logits_buf is not None:
             b[SampleBatch.ACTION_DIST_INPUTS] = logits_buf
         if self.stateful:

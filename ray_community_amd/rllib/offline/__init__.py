@@ -1,4 +1,5 @@
-"""Offline data I/O (reference: ``rllib/offline/json_writer.py``, ``json_reader.py``).
+"""Offline data I/O (reference: ``rllib/offline/json_writer.py``, ``json_reader.py``,
+``dataset_reader.py``, ``estimators/``).
 
 Batches are written as JSON lines (one flattened SampleBatch per line, arrays as nested lists);
 the reader samples whole lines or concatenates them into train batches.
@@ -90,3 +91,6 @@ class JsonReader:
 
     def __iter__(self):
         return iter(self.batches)
+
+
+from .dataset_reader import DatasetReader, get_dataset_and_shards, write_dataset_rows  # noqa: E402
