@@ -295,12 +295,131 @@ class RLModuleSpec:
 SingleAgentRLModuleSpec = RLModuleSpec
 
 
+class MultiRLModule(nn.Module):
+    """Container of per-module RLModules (reference ``rllib/core/rl_module/marl_module.py:45``
+    ``MultiAgentRLModule``): one RLModule per module (policy) id, registered as torch submodules
+    (``parameters()`` / ``to()`` / ``state_dict()`` cover all of them). Dict-like access
+    (``m[mid]``, ``in``, ``keys`` / ``values`` / ``items``, item assignment), ``add_module`` /
+    ``remove_module``, ``foreach_module``; the forward passes take and return
+    ``{module_id: ...}`` dicts, each module seeing only its own batch."""
+
+    def __init__(self, rl_modules: Optional[Dict] = None):
+        super().__init__()
+        self._rl_modules = nn.ModuleDict()
+        self._ids: list = []  # module ids in insertion order (ModuleDict keys must be strings)
+        for mid, m in (rl_modules or {}).items():
+            self.add_module(mid, m)
+
+    # -------------------------------------------------------------- container API
+    def add_module(self, module_id, module, *, override: bool = False):  # noqa: D401 (shadows nn.Module's)
+        if not isinstance(module, nn.Module):
+            return super().add_module(module_id, module)
+        key = str(module_id)
+        if module_id in self._ids and not override:
+            raise ValueError(f"module {module_id!r} already exists (pass override=True to replace it)")
+        self._rl_modules[key] = module
+        if module_id not in self._ids:
+            self._ids.append(module_id)
+        return self
+
+    def remove_module(self, module_id, *, raise_err_if_not_found: bool = True):
+        if module_id not in self._ids:
+            if raise_err_if_not_found:
+                raise KeyError(f"no module {module_id!r}")
+            return None
+        self._ids.remove(module_id)
+        return self._rl_modules.pop(str(module_id))
+
+    def __getitem__(self, module_id):
+        if module_id not in self._ids:
+            raise KeyError(module_id)
+        return self._rl_modules[str(module_id)]
+
+    def __setitem__(self, module_id, module):
+        self.add_module(module_id, module, override=True)
+
+    def __contains__(self, module_id):
+        return module_id in self._ids
+
+    def __iter__(self):
+        return iter(list(self._ids))
+
+    def __len__(self):
+        return len(self._ids)
+
+    def keys(self):
+        return list(self._ids)
+
+    def values(self):
+        return [self[m] for m in self._ids]
+
+    def items(self):
+        return [(m, self[m]) for m in self._ids]
+
+    def pop(self, module_id, *default):
+        if module_id not in self._ids and default:
+            return default[0]
+        return self.remove_module(module_id)
+
+    def foreach_module(self, func):
+        """[func(module_id, module)] over all modules."""
+        return [func(mid, m) for mid, m in self.items()]
+
+    # -------------------------------------------------------------- forward passes
+    def _each(self, method: str, batch: Dict, *args):
+        return {mid: getattr(self[mid], method)(b, *args) for mid, b in batch.items() if mid in self}
+
+    def forward(self, batch: Dict):
+        return self._each("forward", batch)
+
+    def forward_inference(self, batch: Dict):
+        return self._each("forward_inference", batch)
+
+    def forward_exploration(self, batch: Dict):
+        return self._each("forward_exploration", batch)
+
+    def forward_train(self, batch: Dict):
+        return self._each("forward", batch)
+
+    # -------------------------------------------------------------- state
+    def get_state(self, module_ids=None):
+        ids = self._ids if module_ids is None else [m for m in module_ids if m in self]
+        return {mid: self[mid].get_state() for mid in ids}
+
+    def set_state(self, state: Dict):
+        for mid, st in state.items():
+            if mid in self:
+                self[mid].set_state(st)
+
+    def as_multi_agent(self):
+        return self
+
+    def __repr__(self):
+        return f"MultiRLModule({', '.join(f'{m!r}: {type(self[m]).__name__}' for m in self._ids)})"
+
+
+MultiAgentRLModule = MultiRLModule
+
+
 class MultiRLModuleSpec:
-    """{module_id: RLModuleSpec} for multi-agent algorithms (reference MultiRLModuleSpec)."""
+    """{module_id: RLModuleSpec} for multi-agent algorithms (reference MultiRLModuleSpec); ``build``
+    makes the ``MultiRLModule`` (or ``multi_rl_module_class``) holding every module."""
 
     def __init__(self, module_specs: Optional[Dict] = None, multi_rl_module_class=None, **kw):
         self.module_specs = dict(module_specs or {})
         self.multi_rl_module_class = multi_rl_module_class
+
+    def build(self, module_id=None):
+        if module_id is not None:
+            return self.module_specs[module_id].build()
+        cls = self.multi_rl_module_class or MultiRLModule
+        return cls({mid: spec.build() for mid, spec in self.module_specs.items()})
+
+    def add_modules(self, module_specs: Dict, override: bool = True):
+        for mid, spec in module_specs.items():
+            if mid in self.module_specs and not override:
+                raise ValueError(f"module spec {mid!r} already exists")
+            self.module_specs[mid] = spec
 
 
 MultiAgentRLModuleSpec = MultiRLModuleSpec

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
-from ..core.rl_module import make_module
+from ..core.rl_module import MultiRLModule, make_module
 from ..policy.sample_batch import DEFAULT_POLICY_ID, MultiAgentBatch, SampleBatch
 from .multi_agent_env import make_multi_agent_env
 
@@ -60,8 +60,9 @@ class MultiAgentEnvRunner:
                 obs_sp = obs_sp or env0.get_observation_space(agents[0])
                 act_sp = act_sp or env0.get_action_space(agents[0])
             self.spaces_[p] = (obs_sp, act_sp)
-        self.modules = {p: make_module(config, *self.spaces_[p], module_id=p) for p in self.policy_ids
-                        if self.spaces_[p][0]}
+        # one MultiRLModule holding every policy's RLModule (reference MultiAgentRLModule)
+        self.modules = MultiRLModule({p: make_module(config, *self.spaces_[p], module_id=p) for p in self.policy_ids
+                                      if self.spaces_[p][0]})
         for m in self.modules.values():
             m.eval()
         # fixed row layout per policy: (sub-env, agent)
@@ -112,7 +113,7 @@ class MultiAgentEnvRunner:
         if policy_id not in self.modules:
             raise KeyError(f"unknown policy {policy_id!r}")
         fn = policy_mapping_fn or self.cfg.get("policy_mapping_fn") or default_policy_mapping_fn
-        keep = dict(self.modules)
+        keep = MultiRLModule(dict(self.modules.items()))
         keep.pop(policy_id)
         for a in self.agent_ids:
             if fn(a, None, worker=self) not in keep:
