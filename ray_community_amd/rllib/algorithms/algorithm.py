@@ -54,6 +54,11 @@ class Algorithm(Trainable):
         if self.multi_agent and (cfg.model or {}).get("use_lstm"):
             raise ValueError("use_lstm is supported for single-agent PPO only")
         runner_cls = EnvRunner
+        if callable(cfg.input_):  # a reader factory (PolicyServerInput): no env to step
+            from ..env.env_runner import ExternalInputRunner
+
+            runner_cls = ExternalInputRunner
+            rd["input_"] = cfg.input_
         if self.multi_agent:
             from ..env.multi_agent_env_runner import MultiAgentEnvRunner
 
@@ -605,6 +610,9 @@ class Algorithm(Trainable):
         g = getattr(self, "env_runner_group", None)
         if g is not None:
             g.stop()
+        reader = getattr(getattr(self, "local_runner", None), "reader", None)
+        if reader is not None and hasattr(reader, "stop"):  # e.g. a PolicyServerInput's HTTP server
+            reader.stop()
         for g in (self.learner_groups.values() if self.multi_agent else [self.learner_group]):
             g.shutdown()
 

@@ -184,7 +184,7 @@ class EnvRunner:
         first_buf = np.empty((N, T), dtype=bool)
         eid_buf = np.empty((N, T), dtype=np.int64)
         if getattr(self, "_eps_ids", None) is None:  # running episode ids, unique per runner and sub-env
-            self._eps_ids = np.arange(N, dtype=np.int64) + (self.worker_index * 1_000_003 + 1) * (1 << 32)
+            self._eps_ids = np.arange(N, dtype=np.int64) + ((int(self.worker_index) + 1) << 40)
             self._eps_next = int(self._eps_ids.max()) + 1
         obs_buf = logits_buf = state_buf = None
         trunc_fix = []  # (t, env indices, module-input final obs, state after the step)
@@ -428,3 +428,62 @@ class EnvRunner:
     def apply(self, func, *args, **kwargs):
         """``func(self, *args)`` (``EnvRunnerGroup.foreach_env_runner`` with a callable)."""
         return func(self, *args, **kwargs)
+
+
+class ExternalInputRunner(EnvRunner):
+    """Env runner fed by an input reader instead of an env (reference: a RolloutWorker whose
+    ``input_`` is a reader factory, e.g. ``PolicyServerInput``): ``config["input_"]`` is called
+    with an ``IOContext`` (config + this runner, whose module answers the reader's action
+    requests); ``sample`` returns the reader's next batch. Spaces come from
+    ``config.environment(observation_space=..., action_space=...)``."""
+
+    def __init__(self, config: Dict, worker_index: int = 0):
+        import threading
+
+        from .policy_server_input import IOContext
+
+        torch.set_num_threads(int(config.get("num_cpus_per_env_runner_threads", 1)))
+        self.cfg = config
+        self.worker_index = worker_index
+        self.observation_space = config.get("observation_space")
+        self.action_space = config.get("action_space")
+        if self.observation_space is None or self.action_space is None:
+            raise ValueError("an external input needs config.environment(observation_space=..., action_space=...)")
+        self._module_obs_space = self.observation_space
+        self.N = 1
+        self.env = None
+        self.module = make_module(config, self.observation_space, self.action_space)
+        self.module.eval()
+        self.stateful = False
+        self.device = torch.device("cpu")
+        self._module_lock = threading.Lock()
+        self.weights_version = -1
+        self.steps_sampled = 0
+        self.completed = collections.deque(maxlen=int(config.get("metrics_num_episodes_for_smoothing", 100)))
+        self.new_episodes = []
+        self.new_custom_metrics = []
+        self.callbacks = None
+        self.env_to_module = self.module_to_env = []
+        self.reader = config["input_"](IOContext(config, self, worker_index))
+
+    def spaces(self):
+        return self.observation_space, self.action_space
+
+    def set_weights(self, state, version: int = 0):
+        with self._module_lock:
+            return super().set_weights(state, version)
+
+    def get_connector_state(self):
+        return {}
+
+    def set_connector_state(self, state):
+        return True
+
+    def sample(self, num_steps: Optional[int] = None, explore: bool = True) -> SampleBatch:
+        b = self.reader.next(num_steps)
+        self.steps_sampled += b.count
+        pop = getattr(self.reader, "pop_episode_returns", None)
+        for ret, n in (pop() if pop is not None else []):
+            self.completed.append((ret, n))
+            self.new_episodes.append((ret, n))
+        return b
