@@ -14,46 +14,60 @@
 
 namespace {
 
-// delta[b, h, s] = sum_d dO[b, s, h, d] * O[b, s, h, d]: one 16-lane group per (b, h, s) row, 16 B
-// per lane (D = 128); consecutive groups = consecutive tokens of one head (coalesced writes)
+// delta[b, h, s] = sum_d dO[b, s, h, d] * O[b, s, h, d]: one 16-lane group per 4 consecutive
+// (b, h, s) rows (all four rows' loads in flight before any math), 16 B per lane (D = 128);
+// consecutive groups = consecutive tokens of one head (coalesced writes)
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
                                                          float* __restrict__ Delta, int B, int S, int Hq, long so,
                                                          long sdo) {
-  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);  // (b * Hq + h) * S + s
-  if (row >= (long)B * Hq * S) return;
+  constexpr int R = 4;
+  const long row0 = ((long)blockIdx.x * 16 + (threadIdx.x >> 4)) * R;  // (b * Hq + h) * S + s
+  const long rows = (long)B * Hq * S;
+  if (row0 >= rows) return;
   const int c = threadIdx.x & 15;
-  const long s = row % S, bh = row / S;
-  const long b = bh / Hq, h = bh % Hq;
-  const long tok = b * S + s;
-  const u32x4 ov = *reinterpret_cast<const u32x4*>(O + tok * so + h * 128 + 8 * c);
-  const u32x4 gv = *reinterpret_cast<const u32x4*>(dO + tok * sdo + h * 128 + 8 * c);
-  float of[8], gf[8];
-  unpack8(ov, of);
-  unpack8(gv, gf);
-  float acc = 0.f;
+  u32x4 ov[R], gv[R];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc = fmaf(of[j], gf[j], acc);
+  for (int i = 0; i < R; ++i) {
+    const long row = row0 + i < rows ? row0 + i : row0;
+    const long s = row % S, bh = row / S;
+    const long tok = (bh / Hq) * S + s, h = bh % Hq;
+    ov[i] = *reinterpret_cast<const u32x4*>(O + tok * so + h * 128 + 8 * c);
+    gv[i] = *reinterpret_cast<const u32x4*>(dO + tok * sdo + h * 128 + 8 * c);
+  }
 #pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (c == 0) Delta[row] = acc;
+  for (int i = 0; i < R; ++i) {
+    float of[8], gf[8];
+    unpack8(ov[i], of);
+    unpack8(gv[i], gf);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(of[j], gf[j], acc);
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (c == 0 && row0 + i < rows) Delta[row0 + i] = acc;
+  }
 }
 
 // dQ from the dS tiles: one workgroup = 4 waves = 128 query rows of one (batch, query head); wave w
 // owns query block qb32 = 4 qb + w (32 rows) and accumulates dQ^T = K^T . dS^T (d on the MFMA row,
-// query on the lane) over 64-key steps. Per step the workgroup stages the step's K tile (64 x 128,
-// shared by the 4 waves) and each wave its own two dS tiles (2 x 2 KB, fragment order: the LDS-DMA
-// lands them byte for byte) into a 2-deep ring; K^T fragments are ds_read_b64_tr_b16 reads of the
-// K image (as V^T in the forward), dS^T fragments ds_read_b64_tr_b16 reads of the fragment-order
-// tiles (conflict-free under the store-side XOR swizzle). Causal: the longest query blocks first.
+// query on the lane) over 32-key steps. Each step stages the step's K tile (32 x 128, shared by the
+// 4 waves) and each wave's own dS tile (2 KB, fragment order: the LDS-DMA lands it byte for byte)
+// into a 4-deep ring kept THREE steps ahead (counted vmcnt, bare s_barrier): the kernel is bound by
+// the dS bytes, and the ring keeps ~3 x 8 KB of them in flight per workgroup. K^T fragments are
+// ds_read_b64_tr_b16 reads of the K image (as V^T in the forward), dS^T fragments
+// ds_read_b64_tr_b16 reads of the fragment-order tiles (conflict-free under the store-side XOR
+// swizzle). Causally masked tiles still issue their DMA (of the diagonal tile, never read), so
+// every wave's vmcnt counts are the same. Causal: the longest query blocks first.
 template <bool CAUSAL>
 __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* __restrict__ K,
                                                                  const bf16_t* __restrict__ dSw,
                                                                  bf16_t* __restrict__ dQ, int B, int S, int Hq,
                                                                  int Hk, long sk, long sdq, long tiles_bh,
                                                                  float scale) {
-  constexpr int D = 128, BQ = 128, BK = 64, NDB = 4, KT = BK * D * 2, DST = 4 * 4096, SLOT = KT + DST,
+  constexpr int D = 128, BQ = 128, BK = 32, NDB = 4, KT = BK * D * 2, DST = 4 * 2048, SLOT = KT + DST, NBUF = 4,
+                AHEAD = NBUF - 1, OPS = 4 /* DMA ops per wave per step: 2 K pieces + 2 dS pieces */,
                 G8 = Img<D>::G8;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * SLOT];
 
   const int nqb = S / BQ, G = Hq / Hk, nb32 = S >> 5;
   int bhk, item;
@@ -63,7 +77,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* _
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int qb32 = 4 * qb + w;
-  const int nstep = CAUSAL ? 2 * (qb + 1) : S / BK;
+  const int nstep = CAUSAL ? 4 * (qb + 1) : nb32;
 
   DmaStage<D, BK> kst;
   kst.init(K + (long)b * S * sk + (long)hk * D, sk, S, tid);
@@ -72,22 +86,16 @@ __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* _
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(dsb), (short)0, (int)(tiles_bh * 2048), 0x00020000);
   const long trow = CAUSAL ? (long)qb32 * (qb32 + 1) / 2 : (long)qb32 * nb32;  // this wave's tile row
 
-  auto issue = [&](int st, int buf) {
-    char* base = smem + buf * SLOT;
+  auto issue = [&](int st) {
+    char* base = smem + (st % NBUF) * SLOT;
     kst.issue(st * BK, sk, base);
-    char* dl = base + KT + w * 4096;
+    const int kb = (!CAUSAL || st <= qb32) ? st : qb32;  // a masked tile: any valid tile (never read)
+    const int so = __builtin_amdgcn_readfirstlane((int)((trow + kb) * 2048));
+    char* dl = base + KT + w * 2048;
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int kb = 2 * st + tt;
-      if (!CAUSAL || kb <= qb32) {
-        const int so = __builtin_amdgcn_readfirstlane((int)((trow + kb) * 2048));
-#pragma unroll
-        for (int pc = 0; pc < 2; ++pc)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              dsr, (__attribute__((address_space(3))) void*)(dl + tt * 2048 + pc * 1024), 16, lane * 16 + pc * 1024, so,
-              0, 0);
-      }
-    }
+    for (int pc = 0; pc < 2; ++pc)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsr, (__attribute__((address_space(3))) void*)(dl + pc * 1024), 16,
+                                               lane * 16 + pc * 1024, so, 0, 0);
   };
 
   // per-lane read bases: K^T (the forward's V^T reads) and dS^T (two bases: read r of a k-step)
@@ -104,38 +112,30 @@ __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* _
 #pragma unroll
   for (int i = 0; i < NDB; ++i) dq[i] = zero16();
 
-  issue(0, 0);
-  wait_dma();
-  __syncthreads();
-  auto step = [&](auto bufc, int st) {
-    constexpr int buf = decltype(bufc)::value;
-    if (st + 1 < nstep) issue(st + 1, buf ^ 1);
-    const char* Ks = smem + buf * SLOT;
-    const char* Ds = Ks + KT + w * 4096;
+  for (int st = 0; st < AHEAD && st < nstep; ++st) issue(st);
+  for (int st = 0; st < nstep; ++st) {
+    // stage st landed: at most (stages issued after it) x OPS of this wave's DMAs still pending
+    const int later = nstep - 1 - st < AHEAD - 1 ? nstep - 1 - st : AHEAD - 1;
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage st are in; stage st-1 is read
+    if (st + AHEAD < nstep) issue(st + AHEAD);  // into the buffer stage st-1 used
+    if (!CAUSAL || st <= qb32) {
+      const char* Ks = smem + (st % NBUF) * SLOT;
+      const char* Ds = Ks + KT + w * 2048;
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int kb = 2 * st + tt;
-      if (!CAUSAL || kb <= qb32) {
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t fr[NDB + 1];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int kk = 2 * tt + ks;  // 16-key step inside the 64-key K tile
-          bf16x8_t fr[NDB + 1];
+        for (int db = 0; db < NDB; ++db)
+          fr[db] = lds_tr8_asm(Ks + tb0 + G8 * (2 * ks) + 512 * db, Ks + tb1 + G8 * (2 * ks + 1) + 512 * db);
+        fr[NDB] = lds_tr8_asm(Ds + dsa[0] + 256 * ks, Ds + dsa[1] + 256 * ks);
+        lds_tr_settle(fr);
 #pragma unroll
-          for (int db = 0; db < NDB; ++db)
-            fr[db] = lds_tr8_asm(Ks + tb0 + G8 * (2 * kk) + 512 * db, Ks + tb1 + G8 * (2 * kk + 1) + 512 * db);
-          fr[NDB] = lds_tr8_asm(Ds + tt * 2048 + dsa[0] + 256 * ks, Ds + tt * 2048 + dsa[1] + 256 * ks);
-          lds_tr_settle(fr);
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[db], fr[NDB], dq[db]);
-        }
+        for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[db], fr[NDB], dq[db]);
       }
     }
-    if (st + 1 < nstep) wait_dma();
-    __syncthreads();
-  };
-  for (int st = 0; st < nstep; st += 2) {  // nstep is even (S % 128 == 0)
-    step(IC<0>{}, st);
-    step(IC<1>{}, st + 1);
   }
 
   // dQ^T accumulators: d = 32 db + (r & 3) + 8 (r >> 2) + 4 h on the registers, the query on the lane
@@ -171,7 +171,7 @@ long rca_attn_ds_ws_bytes(int B, int S, int Hq, int D, bool causal) {
 void rca_attn_launch_delta(const bf16_t* o, const bf16_t* dout, float* delta, int B, int S, int Hq, long so, long sdo,
                            hipStream_t st) {
   const long rows = (long)B * Hq * S;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, st, o, dout, delta, B, S, Hq,
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(256), 0, st, o, dout, delta, B, S, Hq,
                      so, sdo);
 }
 
