@@ -21,11 +21,20 @@ bucket view:
 
 On xGMI's point-to-point links reduce-scatter + all-gather move the same bytes as one ring
 all-reduce, so the win is the optimizer pass (and HBM), not the wire.
+
+W^T copies: the backward's input-gradient GEMMs read each fused linear weight transposed
+(``fused_linear.weight_t``). Under DDP the replicated optimizer writes W^T in its update pass;
+here a rank updates only its chunks and the full W arrives by all-gather, so W^T is produced by
+one LDS-tiled transpose per weight on a side stream, launched by the forward pre-hook right
+after the weight's gather is waited on. It overlaps the (compute-bound) forward GEMMs instead of
+sitting in front of the backward's dgrad, which waits on its event only when it needs W^T.
+``RCA_ZERO_WT=0`` turns it off (dgrad then transposes in line, as before).
 """
 from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -64,11 +73,27 @@ class ShardedDataParallel(nn.Module):
                 for b in module.buffers():
                     dist.broadcast(b, src=src, group=process_group)
             self._hooks += register_grad_ready(self.flat.params, self._on_grad)
+        # W^T copies of the fused linear weights, refreshed on a side stream after each gather
+        self._wt_epoch = [0]  # bumped by every optimizer update / weight load (W changed)
+        self._wt_stream = None
+        self._module_wt: Dict[int, List[nn.Parameter]] = {}
+        wt_ids = set()
+        if os.environ.get("RCA_ZERO_WT", "1") != "0" and self.flat.data.is_cuda:
+            for p in self.flat.fused:
+                if p.dim() == 2 and p.shape[0] % 128 == 0 and p.shape[1] % 128 == 0:
+                    p._rca_wt = torch.empty(p.shape[1], p.shape[0], dtype=p.dtype, device=p.device)
+                    p._rca_wt_key = None
+                    p._rca_wt_epoch = self._wt_epoch
+                    p._rca_wt_ev = None
+                    wt_ids.add(id(p))
         # forward pre-hooks: wait for the all-gathers of the buckets this module's own params live in
         self._module_buckets: Dict[int, List[int]] = {}
         for m in module.modules():
-            bis = sorted({self.flat.param_bucket[id(p)] for p in m.parameters(recurse=False)
-                          if id(p) in self.flat.param_bucket})
+            own = [p for p in m.parameters(recurse=False) if id(p) in self.flat.param_bucket]
+            bis = sorted({self.flat.param_bucket[id(p)] for p in own})
+            wts = [p for p in own if id(p) in wt_ids]
+            if wts:
+                self._module_wt[id(m)] = wts
             if bis:
                 self._module_buckets[id(m)] = bis
                 self._hooks.append(m.register_forward_pre_hook(self._pre_forward))
@@ -142,6 +167,38 @@ class ShardedDataParallel(nn.Module):
         bis = self._module_buckets.get(id(m))
         if bis and any(self._ag[bi] is not None for bi in bis):
             self.wait_all_gathers(bis)
+        wts = self._module_wt.get(id(m))
+        if wts and torch.is_grad_enabled():
+            self._refresh_wt(wts)
+
+    def _refresh_wt(self, wts):
+        """Transpose the stale W^T copies of ``wts`` on the side stream (after everything the
+        current stream has queued, i.e. the gathers just waited on); the dgrad waits on the
+        recorded event (``fused_linear.weight_t``)."""
+        ep = self._wt_epoch[0]
+        stale = [p for p in wts if p._rca_wt_key != (p._version, ep)]
+        if not stale:
+            return
+        main = torch.cuda.current_stream(self.flat.device)
+        if self._wt_stream is None:
+            self._wt_stream = torch.cuda.Stream(self.flat.device)
+        side = self._wt_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for p in stale:
+                ops.transpose(p.detach(), out=p._rca_wt)
+                p._rca_wt_key = (p._version, ep)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for p in stale:
+            p._rca_wt_ev = ev
+
+    def invalidate_wt(self):
+        """The weights are about to change (optimizer update, load): every W^T copy is stale, and
+        transposes still reading the old W (a dgrad that never ran) must finish first."""
+        self._wt_epoch[0] += 1
+        if self._wt_stream is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._wt_stream)
 
     # ------------------------------------------------------------------ module API
     def forward(self, *args, **kwargs):
@@ -171,6 +228,7 @@ class ShardedDataParallel(nn.Module):
 
     def load_state_dict(self, sd, strict=True):
         self.wait_all_gathers()
+        self.invalidate_wt()
         return self.module.load_state_dict(sd, strict=strict)
 
 
@@ -242,6 +300,7 @@ class ShardedAdamW:
         lr = self.current_lr()
         bc1, bc2 = 1.0 - self.b1 ** t, 1.0 - self.b2 ** t
         flat.finalize_fresh()
+        sdp.invalidate_wt()
         g = flat.step_grad
         clip = self.max_grad_norm if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
         if clip:
@@ -313,6 +372,7 @@ class ShardedAdamW:
         self.step_count = sd["step"]
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
+        self.sdp.invalidate_wt()
         flat = self.sdp.flat
         master = sd["master"].to(flat.device)
         with torch.no_grad():

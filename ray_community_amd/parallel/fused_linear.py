@@ -129,13 +129,17 @@ def _dgrad(gy, g2, w):
 
 
 def weight_t(w):
-    """``w.t().contiguous()``: the W^T copy the fused AdamW update keeps current when it is valid
-    (``parallel/optim.py::FlatAdamW._setup_transposed``), else a transpose pass (into that buffer
+    """``w.t().contiguous()``: the W^T copy the fused AdamW update (``parallel/optim.py::
+    FlatAdamW._setup_transposed``) or the ZeRO forward pre-hook keeps current when it is valid, else a transpose pass (into that buffer
     when the weight has one, so later uses in the same step reuse it)."""
     wt = getattr(w, "_rca_wt", None)
     if wt is None:
         return ops.transpose(w)
     key = (w._version, w._rca_wt_epoch[0])
+    ev = getattr(w, "_rca_wt_ev", None)
+    if ev is not None:  # produced on a side stream (ZeRO: fsdp.ShardedDataParallel._refresh_wt)
+        torch.cuda.current_stream(wt.device).wait_event(ev)
+        w._rca_wt_ev = None
     if w._rca_wt_key != key:
         ops.transpose(w, out=wt)
         w._rca_wt_key = key

@@ -300,6 +300,46 @@ def test_sharded_adamw_matches_flat_adamw_gpu(clip):
         assert torch.allclose(a, b, atol=1e-5, rtol=8e-3), (a - b).abs().max()
 
 
+def test_zero_side_stream_weight_transposes_track_updates():
+    """ZeRO's W^T copies (transposed on a side stream by the forward pre-hook) equal W^T after every
+    optimizer update, and the gradients match the in-line-transpose path (``_module_wt`` cleared)."""
+    from ray_community_amd.models import build_llama
+    from ray_community_amd.parallel import ShardedAdamW, ShardedDataParallel
+
+    runs = []
+    for side in (True, False):
+        torch.manual_seed(0)
+        m = ShardedDataParallel(build_llama("llama3-tiny", device=DEV), bucket_cap_mb=0.2)
+        wts = [p for p in m.flat.fused if getattr(p, "_rca_wt", None) is not None]
+        assert len(wts) >= 4 * 2  # qkv, o, gate_up, down per layer
+        if not side:
+            m._module_wt = {}
+        opt = ShardedAdamW(m, lr=1e-2)
+        g = torch.Generator(device=DEV)
+        g.manual_seed(1)
+        grads = []
+        for step in range(3):
+            tok = torch.randint(0, 1024, (2, 128), device=DEV, generator=g)
+            loss = m(tok, labels=tok)
+            if side:
+                torch.cuda.synchronize()
+                for p in wts:  # refreshed before the backward needs it, from the updated weights
+                    assert p._rca_wt_ev is not None
+                    assert torch.equal(p._rca_wt, p.detach().t())
+            loss.backward()
+            m.finish_gradient_sync()
+            if side:
+                assert all(p._rca_wt_ev is None for p in wts)  # every dgrad waited on its event
+            grads.append(m.flat.grad.float().clone())
+            opt.step()
+            opt.zero_grad()
+        torch.cuda.synchronize()
+        runs.append((grads, m.flat.data.float().clone()))
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert torch.allclose(a, b, atol=2e-3, rtol=2e-2), (a - b).abs().max()
+    assert torch.allclose(runs[0][1], runs[1][1], atol=1e-3, rtol=1e-2)
+
+
 @pytest.mark.parametrize("N,C,H,W", [(4, 64, 12, 10), (2, 256, 7, 7), (3, 2048, 3, 3), (2, 8, 5, 5), (1, 128, 1, 33)])
 @pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, False), (False, True)])
 def test_batch_norm_act_matches_fp32(N, C, H, W, relu, with_res):
