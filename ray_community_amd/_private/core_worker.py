@@ -416,6 +416,16 @@ class CoreWorker:
         # process submitted, batched to the head (state API / timeline)
         self.task_records: List[tuple] = []
         self._records_armed = False
+        # ray.put of host objects does not wait for the head: the registration is sent on this
+        # process's (ordered) head connection and acknowledged later. A ref that escapes this
+        # process -- serialized into any value, or passed as a task / actor argument over a direct
+        # channel -- first waits for the acks of the puts it names (``sync_puts``), so no other
+        # process can ask the head for an object it has not registered yet.
+        self._unacked: Dict[bytes, Any] = {}
+        self._put_lock = threading.Lock()
+        # inline descriptors of this process's own live puts: ray.get on them is local
+        self._put_cache: Dict[bytes, tuple] = {}
+        ser.set_escape_hook(self.sync_puts)
 
     # -------------------------------------------------------------- reference counting
     def ref_add(self, oid):
@@ -438,6 +448,7 @@ class CoreWorker:
                 self._refs[oid] = n
         if n == 0:
             self._ready_known.discard(oid)
+            self._put_cache.pop(oid, None)
             if oid in self.owned.objs and not self.owned.drop(oid):
                 return  # a caller-owned result the head never heard of
             self.client.ref_delta((), (oid,))
@@ -490,8 +501,37 @@ class CoreWorker:
         ref = ObjectRef(oid, _register=False)
         with self._ref_lock:
             self._refs[oid] = self._refs.get(oid, 0) + 1
-        self.client.call("put", oid, desc, s.contained, self.gpu_info(oid) if is_gpu else False, s.flags)
+        if is_gpu:
+            self.client.call("put", oid, desc, s.contained, self.gpu_info(oid), s.flags)
+            return ref
+        fut = self.client.call_async("put", oid, desc, s.contained, False, s.flags)
+        if not fut.done():
+            with self._put_lock:
+                self._unacked[oid] = fut
+            fut.add_done_callback(lambda _f, o=oid: self._acked(o))
+        elif fut.exception() is not None:
+            raise fut.exception()
+        if desc[0] == "inline":
+            self._put_cache[oid] = (desc[0], desc[1], desc[2], s.flags)
         return ref
+
+    def _acked(self, oid):
+        with self._put_lock:
+            self._unacked.pop(oid, None)
+
+    def sync_puts(self, oids=None):
+        """Wait until the head has registered this process's puts among ``oids`` (all if None)."""
+        if not self._unacked:
+            return
+        if threading.current_thread() is getattr(self.client, "_reader", None):
+            return  # the acks arrive on this very thread; its messages are ordered after the puts anyway
+        with self._put_lock:
+            if oids is None:
+                futs = list(self._unacked.values())
+            else:
+                futs = [f for f in (self._unacked.get(o) for o in oids) if f is not None]
+        for f in futs:
+            f.result()
 
     def free_gpu_objects(self, oids):
         from .gpu_store import local_store
@@ -561,6 +601,11 @@ class CoreWorker:
     def _get_descs(self, oids, timeout):
         """Descriptors for ``oids``: caller-owned results from the local table (no head round
         trip), the rest from the head."""
+        pc = self._put_cache
+        if pc:
+            hit = [pc.get(o) for o in oids]
+            if None not in hit:
+                return hit
         owned = self.owned.objs
         local = [o for o in oids if o in owned]
         if not local:
@@ -707,6 +752,8 @@ class CoreWorker:
             if isinstance(a, ObjectRef):
                 out.append(("r", a._id))
                 deps.append(a)
+                if self._unacked:
+                    self.sync_puts((a._id,))
                 continue
             s = ser.serialize(a)
             if s.gpu_tensors:

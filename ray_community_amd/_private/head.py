@@ -277,6 +277,9 @@ class Head:
         # lineage of reconstructable task outputs: tid -> [spec, owner, attempts left]; bounded LRU
         self.lineage: "collections.OrderedDict[bytes, list]" = collections.OrderedDict()
         self.lineage_max = int(self.config.get("max_lineage_entries", 100000))
+        # caller key -> {oid: n}: pins taken for direct actor calls' nested refs (rpc_pin_objects),
+        # released here if the caller dies before its own unpin
+        self.call_pins: Dict[str, Dict[bytes, int]] = {}
         self.num_reconstructions = 0
         # records of directly transported actor calls (state API / timeline), batched by workers
         self.direct_tasks: collections.deque = collections.deque(maxlen=int(self.config.get("direct_task_records", 10000)))
@@ -490,6 +493,7 @@ class Head:
                 if getattr(cc, "log_sink", None) is not None:
                     self.log_monitor.remove_sink(cc.log_sink)
                 self._return_leases_of(cc.client_key)
+                self._release_call_pins(cc.client_key)
                 self._drop_streams_of(cc.client_key)
                 self._drop_holder_everywhere(cc.client_key)
                 self._schedule()
@@ -596,14 +600,17 @@ class Head:
         if self.refs.remove_holder(oid, key):
             self._maybe_free(e)
 
-    def _pin(self, oid, n=1):
+    def _pin(self, oid, n=1) -> bool:
         e = self.objects.get(oid)
         if e is not None:
             self.refs.pin(oid, n)
-        elif oid[:1] == b"A" and len(oid) == 21:
+            return True
+        if oid[:1] == b"A" and len(oid) == 21:
             a = self.actors.get(oid[1:])
             if a is not None:
                 a.pins = getattr(a, "pins", 0) + n
+                return True
+        return False
 
     def _unpin(self, oid, n=1):
         e = self.objects.get(oid)
@@ -1656,6 +1663,7 @@ class Head:
             reason = f"killed by the memory monitor (node memory usage {w.oom_killed[0]:.2f} >= " \
                      f"threshold {w.oom_killed[1]:.2f})"
         self._return_leases_of("w:" + w.wid.hex())  # leases this worker held as a submitter
+        self._release_call_pins("w:" + w.wid.hex())
         if w.actor is not None:
             a = w.actor
             self._on_actor_worker_death(a, reason, ts)
@@ -2018,12 +2026,28 @@ class Head:
         them nested in its arguments: the head-routed path pins a spec's ``contained`` refs in
         ``_submit``, but a direct call never passes the head, and the owner may drop its last ref
         before the callee deserializes the argument."""
+        held = self.call_pins.setdefault(caller, {})
         for o in oids:
             if n > 0:
-                self._pin(o, n)
+                if self._pin(o, n):
+                    held[o] = held.get(o, 0) + n
             else:
-                self._unpin(o, -n)
+                k = min(-n, held.get(o, 0))
+                if k <= 0:
+                    continue
+                self._unpin(o, k)
+                if held[o] == k:
+                    del held[o]
+                else:
+                    held[o] -= k
+        if not held:
+            self.call_pins.pop(caller, None)
         return True
+
+    def _release_call_pins(self, key):
+        """The caller died: drop the pins its in-flight direct actor calls held."""
+        for o, k in (self.call_pins.pop(key, None) or {}).items():
+            self._unpin(o, k)
 
     def rpc_put_owned(self, caller, items, owner_key, lineage=None):
         """A worker registers direct-call results the head must manage (shm, GPU, nested refs) on

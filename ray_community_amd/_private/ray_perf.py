@@ -5,13 +5,30 @@ Same workloads and the same names as the reference suite (reference:
 ``python/ray/_private/ray_microbenchmark_helpers.py:15-47``) so results line up row by row with
 ``release/release_logs/2.9.3/microbenchmark.json``; the timing windows are shorter (``--quick``
 shrinks them further for CI). Reported as ops/s (GB/s for the gigabyte rows).
+
+Two driver placements (``mode``):
+
+* ``colocated``: ``ray.init()`` starts the head inside the benchmark process (the default of
+  ``ray.init`` here), so driver -> head calls are in-process calls under the head's lock;
+* ``separate``: a head started by ``python -m ray_community_amd start --head`` in its own
+  process, the benchmark connecting with ``ray.init(address="auto")`` like the reference's
+  ``ray microbenchmark`` driver does: every control call crosses a Unix socket.
+
+In both modes ``ray.put`` of an object <= 100 KB is stored inline in the owner (this process),
+not in the shared-memory store, so the two "Plasma Store" put/get rows measure the owner's
+in-process store; the extra ``(shm store, 128 KB)`` rows put / get objects just above the inline
+threshold, which go through the native shm store (no reference row).
 """
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import multiprocessing
 import os
+import subprocess
+import sys
+import tempfile
 import time
 from typing import Callable, List, Optional, Tuple
 
@@ -137,15 +154,55 @@ def create_object_containing_ref():
     return obj_refs
 
 
-def run(window: float = 2.0, rounds: int = 4, pattern: str = "", scale: float = 1.0) -> List[Tuple[str, float, float]]:
-    """Run the suite. ``scale`` < 1 shrinks batch sizes (CI); the ops/s definition is unchanged."""
+@contextlib.contextmanager
+def _session(mode: str, ncpu: int, resources: Optional[dict] = None):
+    if mode == "colocated":
+        ray.init(num_cpus=ncpu, resources=resources, log_to_driver=False)
+        try:
+            yield
+        finally:
+            ray.shutdown()
+        return
+    if mode != "separate":
+        raise ValueError(f"mode must be 'colocated' or 'separate', not {mode!r}")
+    tmp = tempfile.mkdtemp(prefix="rca_perf_")
+    prev = os.environ.get("RCA_TEMP_DIR")
+    env = dict(os.environ, RCA_TEMP_DIR=tmp)
+    cli = [sys.executable, "-m", "ray_community_amd"]
+    args = ["start", "--head", "--num-cpus", str(ncpu)] + (["--resources", json.dumps(resources)] if resources else [])
+    r = subprocess.run(cli + args, env=env, capture_output=True, text=True, timeout=120)
+    if r.returncode != 0:
+        raise RuntimeError(f"head start failed: {r.stderr[-2000:]}")
+    os.environ["RCA_TEMP_DIR"] = tmp
+    try:
+        ray.init(address="auto", log_to_driver=False)
+        try:
+            yield
+        finally:
+            ray.shutdown()
+    finally:
+        subprocess.run(cli + ["stop", "--force"], env=env, capture_output=True, text=True, timeout=120)
+        if prev is None:
+            os.environ.pop("RCA_TEMP_DIR", None)
+        else:
+            os.environ["RCA_TEMP_DIR"] = prev
+
+
+def run(window: float = 2.0, rounds: int = 4, pattern: str = "", scale: float = 1.0,
+        mode: str = "colocated") -> List[Tuple[str, float, float]]:
+    """Run the suite. ``scale`` < 1 shrinks batch sizes (CI); the ops/s definition is unchanged.
+    ``mode``: ``colocated`` (head in this process) or ``separate`` (head in its own process)."""
     t = _Timer(window, rounds, pattern)
     ncpu = max(2, multiprocessing.cpu_count())
-    ray.init(num_cpus=ncpu, log_to_driver=False)
-    try:
+    with _session(mode, ncpu):
         value = ray.put(0)
         t("single client get calls (Plasma Store)", lambda: ray.get(value))
         t("single client put calls (Plasma Store)", lambda: ray.put(0))
+        big = np.zeros(128 * 1024 // 8, dtype=np.int64)  # above the 100 KB inline threshold
+        shm_value = ray.put(big)
+        t("single client get calls (shm store, 128 KB)", lambda: ray.get(shm_value))
+        t("single client put calls (shm store, 128 KB)", lambda: ray.put(big))
+        del shm_value
 
         @ray.remote
         def do_put_small():
@@ -231,11 +288,8 @@ def run(window: float = 2.0, rounds: int = 4, pattern: str = "", scale: float = 
             ray.get([actors[i % n_half].small_value.remote() for i in range(n)])
 
         t("n:n async-actor calls async", lambda: ray.get([async_actor_work.remote(a) for _ in range(m)]), m * n)
-    finally:
-        ray.shutdown()
 
-    ray.init(num_cpus=ncpu, resources={"custom": 100}, log_to_driver=False)
-    try:
+    with _session(mode, ncpu, {"custom": 100}):
         from ..util.placement_group import placement_group, remove_placement_group
 
         npg = 100
@@ -248,19 +302,17 @@ def run(window: float = 2.0, rounds: int = 4, pattern: str = "", scale: float = 
                 remove_placement_group(pg)
 
         t("placement group create/removal", pg_create_removal, npg)
-    finally:
-        ray.shutdown()
     return t.results
 
 
-def report(results, out: Optional[str] = None) -> dict:
+def report(results, out: Optional[str] = None, mode: str = "colocated") -> dict:
     rows = {}
     for name, mean, sd in results:
         k = _key(name)
         ref = REFERENCE.get(k)
         rows[k] = {"value": round(mean, 2), "sd": round(sd, 2), "reference": ref,
                    "vs_reference": round(mean / ref, 3) if ref else None}
-    doc = {"suite": "core_microbenchmark", "cpus": multiprocessing.cpu_count(),
+    doc = {"suite": "core_microbenchmark", "mode": mode, "cpus": multiprocessing.cpu_count(),
            "reference_hw": "m5.16xlarge (64 vCPU)", "results": rows}
     if out:
         os.makedirs(os.path.dirname(out) or ".", exist_ok=True)

@@ -221,6 +221,16 @@ class Serialized:
         return t.to_bytes()
 
 
+_ESCAPE_HOOK = [None]
+
+
+def set_escape_hook(fn):
+    """``fn(oids)`` runs whenever a serialized value contains ObjectRefs (the refs may leave this
+    process with it): the core worker waits there for the head to have registered its own
+    not-yet-acknowledged puts among them (``CoreWorker.sync_puts``)."""
+    _ESCAPE_HOOK[0] = fn
+
+
 def serialize(value: Any, error: bool = False) -> Serialized:
     ctx = SerializationContext()
     prev = getattr(_tls, "ctx", None)
@@ -230,6 +240,8 @@ def serialize(value: Any, error: bool = False) -> Serialized:
         inband = _dumps(value, buffers)
     finally:
         _tls.ctx = prev
+    if ctx.contained and _ESCAPE_HOOK[0] is not None:
+        _ESCAPE_HOOK[0](ctx.contained)
     flags = (FLAG_ERROR if error else 0) | (FLAG_GPU if ctx.gpu_tensors else 0)
     return Serialized(inband, buffers, flags, ctx.contained, ctx.gpu_tensors)
 

@@ -255,6 +255,7 @@ class CompiledDAG:
         self._handles = handle_of
         self._seq = 0
         self._next_read = 1          # seq of the next result waiting in the output channels
+        self._partial: list = []     # outputs of execution ``_next_read`` read before a timeout
         self._results: Dict[int, list] = {}
         self._max_buffered = int(max_buffered_results)
         self._torn_down = False
@@ -264,17 +265,21 @@ class CompiledDAG:
         if len(self._results) >= self._max_buffered:
             raise RuntimeError(f"compiled DAG holds {len(self._results)} unread results "
                                f"(max_buffered_results={self._max_buffered}); read earlier refs first")
-        vals = []
-        for ch, r in self._outputs:
-            vals.append(ch.begin_read(r, timeout))
-        try:
-            if self._device_outputs:
-                from .torch_tensor import receiver
+        # channel by channel: each value is copied out and its channel released before the next
+        # read, and the values already read are kept in ``_partial``, so a timeout on a later
+        # output leaves no channel half-read and the retry resumes at the output that timed out
+        vals = self._partial
+        for ch, r in self._outputs[len(vals):]:
+            v = ch.begin_read(r, timeout)
+            try:
+                if self._device_outputs:
+                    from .torch_tensor import receiver
 
-                vals = [receiver().unpack(v) for v in vals]  # copied out before the channel is released
-        finally:
-            for ch, r in self._outputs:
+                    v = receiver().unpack(v)  # copied out before the channel is released
+            finally:
                 ch.end_read(r)
+            vals.append(v)
+        self._partial = []
         self._results[self._next_read] = vals
         self._next_read += 1
 

@@ -141,6 +141,21 @@ def _truncate(block, k):
     return out, _meta(out)
 
 
+def _zip_columns(a, b):
+    da = BlockAccessor(a).to_numpy()
+    db = BlockAccessor(b).to_numpy()
+    out = dict(da)
+    for k, v in db.items():
+        out[k if k not in out else f"{k}_1"] = v
+    return out
+
+
+def _zip_slices(a, a0, b, b0, n):
+    """Rows [a0, a0+n) of ``a`` side by side with rows [b0, b0+n) of ``b`` (streaming zip)."""
+    out = _zip_columns(BlockAccessor(a).slice(a0, a0 + n), BlockAccessor(b).slice(b0, b0 + n))
+    return out, _meta(out)
+
+
 # ------------------------------------------------------------------------------ exchanges
 def _split_by_ranges(block, start_row, bounds):
     """Slice ``block`` (global rows [start_row, start_row+n)) into len(bounds)-1 pieces."""

@@ -71,7 +71,8 @@ def _cpu_only(chain: List[Dict]) -> bool:
 
 
 def plan_stages(ops: List[Dict], fuse: bool = True) -> List[Tuple]:
-    """Physical stages: ("task", chain) | ("actor", op, pre_chain) | ("limit", n) | ("alltoall", op).
+    """Physical stages: ("task", chain) | ("actor", op, pre_chain) | ("limit", n) | ("alltoall", op)
+    | ("nary", op) (streaming union / zip with other datasets).
     ``fuse=False``: one stage per operator."""
     stages: List[Tuple] = []
     chain: List[Dict] = []
@@ -101,6 +102,8 @@ def plan_stages(ops: List[Dict], fuse: bool = True) -> List[Tuple]:
             stages.append(("limit", int(op["n"])))
         elif k == "alltoall":
             stages.append(("alltoall", op))
+        elif k in ("union", "zip"):
+            stages.append(("nary", op))
         else:
             raise ValueError(f"unknown operator kind {k!r}")
     flush()

@@ -23,6 +23,7 @@ object store streams through: the executor's output window bounds what is in fli
 from __future__ import annotations
 
 import collections
+import itertools
 import threading
 import time
 from typing import Any, List, Optional
@@ -43,6 +44,7 @@ class SplitCoordinator:
         self._split_epoch = [-1] * n
         self._arrived = collections.defaultdict(set)
         self._queues = [collections.deque() for _ in range(n)]
+        self._turn = [0] * n  # per consumer: seq of the get() call answered next
         self._it = None
         self._done = True
         self._pulling = False
@@ -69,6 +71,7 @@ class SplitCoordinator:
         self._arrived.pop(e, None)
         self._epoch = e
         self._queues = [collections.deque() for _ in range(self._n)]
+        self._turn = [0] * self._n
         self._buffer.clear()
         self._buffer_rows = 0
         self._assigned = [0] * self._n
@@ -78,19 +81,28 @@ class SplitCoordinator:
         self._stats["epochs"] += 1
 
     # ---------------------------------------------------------------- blocks
-    def get(self, epoch: int, split_idx: int):
-        """The next ``[block_ref, meta_ref]`` of this consumer in ``epoch``, or None at its end."""
+    def get(self, epoch: int, split_idx: int, seq: int = 0):
+        """The ``seq``-th ``[block_ref, meta_ref]`` of this consumer in ``epoch``, or None at its
+        end. A consumer keeps several calls in flight (prefetch) and reads their replies in
+        order, so the calls are answered in ``seq`` order whatever order they run in."""
         while True:
             with self._cv:
                 while True:
                     if epoch != self._epoch:
                         return None
+                    if self._turn[split_idx] != seq:
+                        self._cv.wait(_POLL_S)
+                        continue
                     q = self._queues[split_idx]
                     if q:
                         b, m = q.popleft()
                         self._stats["blocks"][split_idx] += 1
+                        self._turn[split_idx] += 1
+                        self._cv.notify_all()
                         return [b, m]
                     if self._done:
+                        self._turn[split_idx] += 1
+                        self._cv.notify_all()
                         return None
                     if not self._pulling:
                         self._pulling = True
@@ -222,14 +234,16 @@ class StreamSplitDataIterator(DataIterator):
         from ..._private.worker import get
 
         epoch = get(self._coord.start_epoch.remote(self._idx))
-        pending = collections.deque(self._coord.get.remote(epoch, self._idx) for _ in range(max(1, prefetch + 1)))
+        seq = itertools.count()
+        pending = collections.deque(self._coord.get.remote(epoch, self._idx, next(seq))
+                                    for _ in range(max(1, prefetch + 1)))
         while pending:
             r = get(pending.popleft())
             if r is None:
-                for p in pending:  # drain: the rest answer None too
+                for p in pending:  # drain: the later calls answer None too
                     get(p)
                 return
-            pending.append(self._coord.get.remote(epoch, self._idx))
+            pending.append(self._coord.get.remote(epoch, self._idx, next(seq)))
             yield r[0], r[1]
 
     def _blocks(self, prefetch: int):

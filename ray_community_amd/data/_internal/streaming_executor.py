@@ -8,8 +8,9 @@ over ``OpState`` queues; this one does the same against this runtime's task/acto
 
 * The plan is a chain of physical operators: ``InputOp`` (read tasks or existing refs),
   ``TaskMapOp`` (fused task-compute map chain, one task per block), ``ActorPoolMapOp``
-  (callable-class UDFs on an autoscaling actor pool), ``LimitOp`` and ``AllToAllOp`` (barrier:
-  repartition / shuffle / sort / groupby exchanges).
+  (callable-class UDFs on an autoscaling actor pool), ``LimitOp``, ``AllToAllOp`` (barrier:
+  repartition / shuffle / sort / groupby exchanges) and the streaming n-ary ``UnionOp`` /
+  ``ZipOp``, whose other inputs are datasets executing concurrently (``_SideInput``).
 * One background thread runs the loop: retire finished tasks (one non-blocking ``wait`` over
   every operator's outstanding metadata refs), move outputs downstream, autoscale actor pools,
   and dispatch new tasks downstream-first while the resource manager's budgets
@@ -325,6 +326,204 @@ class AllToAllOp(PhysicalOp):
 
     def done(self) -> bool:
         return self._fired and not self.ready_out
+
+
+class _SideInput:
+    """Another dataset streamed into an n-ary operator: a pump thread pulls ``(block, meta)``
+    pairs from that dataset's own streaming execution into a queue of at most ``window`` items,
+    so the side input runs concurrently with this pipeline and is backpressured by it."""
+
+    def __init__(self, ds, window: int):
+        self.ds = ds
+        self.items: collections.deque = collections.deque()
+        self.room = threading.Semaphore(max(1, window))
+        self.exhausted = False
+        self.error: Optional[BaseException] = None
+        self._stop = threading.Event()
+        self._t: Optional[threading.Thread] = None
+
+    def start(self):
+        if self._t is None:
+            self._t = threading.Thread(target=self._pump, name="rca-data-side-input", daemon=True)
+            self._t.start()
+
+    def _pump(self):
+        gen = None
+        try:
+            gen = self.ds._iter_refs()
+            while not self._stop.is_set():
+                self.room.acquire()
+                if self._stop.is_set():
+                    break
+                try:
+                    item = next(gen)
+                except StopIteration:
+                    break
+                self.items.append(item)
+        except BaseException as e:  # noqa  (re-raised by the operator in the executor loop)
+            self.error = e
+        finally:
+            self.exhausted = True
+            if gen is not None and hasattr(gen, "close"):
+                try:
+                    gen.close()
+                except Exception:
+                    pass
+
+    def poll(self):
+        if self.error is not None:
+            raise self.error
+        if self.items:
+            item = self.items.popleft()
+            self.room.release()
+            return item
+        return None
+
+    def drained(self) -> bool:
+        return self.exhausted and not self.items
+
+    def close(self):
+        self._stop.set()
+        self.room.release()
+        ex = getattr(self.ds, "_executor", None)
+        if ex is not None and not self.exhausted:
+            ex._stop.set()
+
+
+class UnionOp(PhysicalOp):
+    """Streaming union (reference ``operators/union_operator.py``): this pipeline's blocks and
+    the other datasets' blocks, each other dataset executing concurrently through its own
+    streaming execution. Ordered mode emits the inputs one after another (this dataset's
+    blocks first); otherwise blocks flow out as they become available."""
+
+    def __init__(self, others, ordered, window):
+        super().__init__("Union", ordered)
+        self.sides = [_SideInput(o, 2) for o in others]  # each other dataset's executor window sits behind it
+        self._out = 0
+
+    def _start(self):
+        for sd in self.sides:
+            sd.start()
+
+    def _pass(self, block, meta):
+        self.ready_out.append(_Bundle(self._out, block, meta))
+        self._out += 1
+
+    def _side(self) -> Optional[_SideInput]:
+        """The side input the next block may come from (None: nothing available now)."""
+        for sd in self.sides:
+            if sd.error is not None:
+                raise sd.error
+        if self.ordered:
+            if not self.upstream_done or self.inq:
+                return None
+            for sd in self.sides:
+                if sd.items:
+                    return sd
+                if not sd.drained():
+                    return None  # keep the order: wait for this input before the next one
+            return None
+        return next((sd for sd in self.sides if sd.items), None)
+
+    def can_dispatch(self) -> bool:
+        self._start()
+        return bool(self.inq) or self._side() is not None
+
+    def dispatch_one(self):
+        if self.inq:
+            b = self.inq.popleft()
+            self._pass(b.block, b.meta)
+            return
+        self._pass(*self._side().poll())
+
+    def done(self) -> bool:
+        self._start()
+        return (self.upstream_done and not self.inq and not self.ready_out
+                and all(sd.drained() for sd in self.sides))
+
+    def shutdown(self):
+        for sd in self.sides:
+            sd.close()
+
+
+class ZipOp(PhysicalOp):
+    """Streaming zip: row-aligns this pipeline's blocks with another dataset's (executing
+    concurrently) and launches one zip task per aligned run of rows as soon as both sides have
+    it -- no barrier (the reference's ``operators/zip_operator.py`` materialises both inputs
+    first). Row counts come from the block metadata; a row-count mismatch raises at the end."""
+
+    def __init__(self, other, ordered, window):
+        super().__init__("Zip", ordered)
+        self.side = _SideInput(other, 2)  # the other dataset's own executor window sits behind it
+        self.left: collections.deque = collections.deque()   # [block, rows, offset]
+        self.right: collections.deque = collections.deque()
+        self._out = 0
+        self._zip = None
+
+    @staticmethod
+    def _rows(meta):
+        from ..._private.worker import get
+
+        return int(get(meta)["num_rows"])
+
+    def _refill(self):
+        """Hold at most two blocks of each side here: the rest stays upstream (this op's input
+        queue, the side input's bounded queue), where the executor's windows bound it."""
+        self.side.start()
+        for q in (self.left, self.right):
+            while q and q[0][1] - q[0][2] <= 0:
+                q.popleft()
+        while self.inq and len(self.left) < 2:
+            b = self.inq.popleft()
+            self.left.append([b.block, self._rows(b.meta), 0])
+        while len(self.right) < 2:
+            it = self.side.poll()
+            if it is None:
+                break
+            self.right.append([it[0], self._rows(it[1]), 0])
+        for q in (self.left, self.right):
+            while q and q[0][1] - q[0][2] <= 0:
+                q.popleft()
+
+    def can_dispatch(self) -> bool:
+        self._refill()
+        return bool(self.left and self.right)
+
+    def dispatch_one(self):
+        from .execution import _remote_fn, _zip_slices
+
+        if self._zip is None:
+            self._zip = _remote_fn(_zip_slices, {"num_cpus": 0.5})
+        lb, rb = self.left[0], self.right[0]
+        k = min(lb[1] - lb[2], rb[1] - rb[2])
+        blk, meta = self._zip.remote(lb[0], lb[2], rb[0], rb[2], k)
+        self.running[meta] = (self._out, blk, None)
+        self._out += 1
+        self.stats["tasks"] += 1
+        lb[2] += k
+        rb[2] += k
+        for q in (self.left, self.right):
+            if q[0][2] >= q[0][1]:
+                q.popleft()
+
+    def done(self) -> bool:
+        self._refill()
+        if not (self.upstream_done and self.side.drained() and not self.inq):
+            return False
+        self._refill()
+        if self.left and self.right:
+            return False  # more aligned rows to dispatch (waiting for downstream room)
+        if self.left or self.right:
+            if not self.running:
+                n_l = sum(x[1] - x[2] for x in self.left)
+                n_r = sum(x[1] - x[2] for x in self.right)
+                raise ValueError(f"Cannot zip datasets of different number of rows: {n_l} left over on "
+                                 f"one side, {n_r} on the other")
+            return False
+        return not self.running and not self.finished and not self.ready_out
+
+    def shutdown(self):
+        self.side.close()
 
 
 class StreamingExecutor:

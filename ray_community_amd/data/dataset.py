@@ -143,6 +143,12 @@ class Dataset:
                                              ctx.actor_pool_idle_timeout_s, ordered, rm, st_rm, pre_ops=pre))
             elif st[0] == "limit":
                 ops.append(SE.LimitOp(st[1], ordered, ex))
+            elif st[0] == "nary":
+                op = st[1]
+                if op["kind"] == "union":
+                    ops.append(SE.UnionOp(op["others"], ordered, window))
+                else:
+                    ops.append(SE.ZipOp(op["other"], ordered, window))
             else:
                 ops.append(SE.AllToAllOp(st[1].get("name", "AllToAll"), st[1]["fn"], ordered))
         ex.__init__(ops, rm, window)
@@ -243,27 +249,15 @@ class Dataset:
         return GroupedData(self, key)
 
     def union(self, *others: "Dataset") -> "Dataset":
-        parts = [self] + list(others)
-
-        def fn(refs, parts=parts):
-            out = list(refs)
-            for o in parts[1:]:
-                out.extend(o._refs())
-            return out
-
-        return self._with({"kind": "alltoall", "fn": fn})
+        """Streaming union (``_internal/streaming_executor.py::UnionOp``): the other datasets
+        execute concurrently with this one; with ``preserve_order`` the result is this dataset's
+        rows, then each other's in argument order."""
+        return self._with({"kind": "union", "others": list(others), "name": "Union"})
 
     def zip(self, other: "Dataset") -> "Dataset":
-        def fn(refs):
-            from .._private.worker import get
-
-            mine = get([m for _, m in refs])
-            counts = [m["num_rows"] for m in mine]
-            theirs = _repartition_to_sizes(other._refs(), counts)
-            z = X._remote_fn(_zip_blocks, {"num_cpus": 1})
-            return [tuple(z.remote(a[0], b[0])) for a, b in zip(refs, theirs)]
-
-        return self._with({"kind": "alltoall", "fn": fn})
+        """Streaming zip (``ZipOp``): rows are aligned across the two block streams as they
+        arrive (no materialisation of either side); both must have the same row count."""
+        return self._with({"kind": "zip", "other": other, "name": "Zip"})
 
     def random_sample(self, fraction: float, *, seed: Optional[int] = None) -> "Dataset":
         def sample(batch, fraction=fraction, seed=seed):
@@ -738,15 +732,6 @@ def _sample_keys(block, key):
     v = d[key]
     idx = np.random.default_rng(0).choice(len(v), size=min(len(v), 64), replace=False)
     return v[idx], {}
-
-
-def _zip_blocks(a, b):
-    da = BlockAccessor(a).to_numpy()
-    db = BlockAccessor(b).to_numpy()
-    out = dict(da)
-    for k, v in db.items():
-        out[k if k not in out else f"{k}_1"] = v
-    return out, X._meta(out)
 
 
 def _pa_table(df):

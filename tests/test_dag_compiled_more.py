@@ -83,3 +83,29 @@ def test_refs_read_out_of_order_and_buffer_cap(session):
             refs[-1].get(timeout=30)
     finally:
         cd.teardown()
+
+
+@ray.remote
+class Sleeper:
+    def run(self, x):
+        import time
+
+        time.sleep(x)
+        return x
+
+
+def test_multi_output_timeout_then_retry_keeps_outputs_paired(session):
+    """A get() that times out on the second output leaves the first output's channel released and
+    its value kept: the retry returns this execution's outputs, and the next execution's after."""
+    fast, slow = Worker.remote(1), Sleeper.remote()
+    with InputNode() as inp:
+        dag = MultiOutputNode([fast.scale.bind(inp), slow.run.bind(inp)])
+    cd = dag.experimental_compile()
+    try:
+        r1 = cd.execute(1.5)
+        with pytest.raises(Exception):
+            r1.get(timeout=0.3)          # fast output read, the slow one times out
+        assert r1.get(timeout=30) == [1.5, 1.5]
+        assert cd.execute(0.1).get(timeout=30) == [0.1, 0.1]
+    finally:
+        cd.teardown()

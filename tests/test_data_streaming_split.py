@@ -140,3 +140,24 @@ def test_train_shards_come_from_streaming_split(shutdown_only):
     assert res.metrics["n0"] == 300 and res.metrics["n1"] == 300
     assert res.metrics["kind"] == "StreamSplitDataIterator"
     assert res.metrics["differ"]
+
+
+def test_streaming_split_prefetched_calls_keep_their_order(shutdown_only):
+    """One block split equally between two consumers: each consumer's prefetched get() calls run
+    concurrently in the coordinator but are answered in call order, so no slice is dropped by a
+    later call overtaking an earlier one."""
+    ray.init(num_cpus=4, include_dashboard=False, log_to_driver=False)
+    for _ in range(3):
+        its = ray.data.range(400, override_num_blocks=1).streaming_split(2, equal=True)
+        out = {}
+
+        def run(i):
+            out[i] = sorted(r["id"] for r in its[i].materialize().take_all())
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert len(out[0]) == len(out[1]) == 200
+        assert sorted(out[0] + out[1]) == list(range(400))

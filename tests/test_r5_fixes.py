@@ -105,3 +105,95 @@ def test_session_file_written_atomically(shutdown_only, tmp_path, monkeypatch):
     rec = json.loads(path.read_text())
     assert rec["pid"] == os.getpid() and rec["sock"]
     assert not [p for p in os.listdir(tmp_path) if p.endswith(".tmp")]
+
+
+def test_async_puts_are_registered_before_their_refs_escape(shutdown_only):
+    """Worker-side ray.put returns before the head acknowledges it; a ref passed on (nested in an
+    actor argument, as a top-level argument, inside a returned value) still resolves everywhere,
+    and a process's own puts are read back locally."""
+    ray.init(num_cpus=3, include_dashboard=False, log_to_driver=False)
+
+    @ray.remote
+    class Sink:
+        def take(self, refs):
+            return sum(ray.get(refs))
+
+        def take_one(self, v):
+            return v
+
+    @ray.remote
+    def producer(sink):
+        from ray_community_amd._private.worker import _core
+
+        core = _core()
+        out = []
+        for i in range(100):
+            out.append(ray.get(sink.take.remote([ray.put(i), ray.put(2 * i)])))
+            out.append(ray.get(sink.take_one.remote(ray.put(i))))
+            r = ray.put({"k": i})
+            assert ray.get(r) == {"k": i} and r._id in core._put_cache  # local read of an own put
+        return out, [ray.put(i) for i in range(50)]
+
+    sink = Sink.remote()
+    out, refs = ray.get(producer.remote(sink))
+    assert out[0::2] == [3 * i for i in range(100)] and out[1::2] == list(range(100))
+    assert ray.get(refs) == list(range(50))
+
+
+def test_core_microbenchmark_separate_driver_mode():
+    """bench_core --mode separate: the head runs in its own process (CLI), the driver connects with
+    address='auto' and the put/get rows work across the socket."""
+    from ray_community_amd._private import ray_perf
+
+    with ray_perf._session("separate", 2):
+        from ray_community_amd._private.worker import _core
+
+        core = _core()
+        assert type(core.client).__name__ == "SocketClient"
+        refs = [ray.put(i) for i in range(200)]
+        assert ray.get(refs) == list(range(200))
+
+        @ray.remote
+        def add(xs):
+            return sum(ray.get(xs))
+
+        assert ray.get(add.remote(refs)) == sum(range(200))
+    assert not ray.is_initialized()
+
+
+def test_direct_call_pins_released_when_caller_dies(shutdown_only):
+    """Nested refs of a direct actor call are pinned at the head for the caller; when the caller
+    process dies before its unpin, the head drops those pins itself."""
+    import time
+
+    ray.init(num_cpus=3, include_dashboard=False, log_to_driver=False)
+    from ray_community_amd._private.worker import _core
+
+    head = _core().client.head
+
+    @ray.remote
+    class Slow:
+        def hold(self, refs):
+            time.sleep(3)
+            return len(refs)
+
+    @ray.remote(max_retries=0)
+    def caller(a):
+        import numpy as np
+
+        r = ray.put(np.zeros(200_000))
+        a.hold.remote([r])
+        time.sleep(1.0)
+        os._exit(1)
+
+    a = Slow.remote()
+    with pytest.raises(Exception):
+        ray.get(caller.remote(a))
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        with head.lock:
+            left = {k: dict(v) for k, v in head.call_pins.items() if k.startswith("w:")}
+        if not left:
+            break
+        time.sleep(0.1)
+    assert not left, left
