@@ -1,0 +1,32 @@
+"""The Data->Serve pipeline's replica work alone: bench_data_serve.Classifier on a device-resident
+bf16 NHWC batch of 256, in-process (no Data, no Serve). Prints ms per batch and images/s, the
+ceiling of bench_data_serve.py with one replica."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from bench_data_serve import Classifier  # noqa: E402
+
+bs = int(os.environ.get("BS", 256))
+c = Classifier("resnet50", 224, bs, "cuda")
+x = torch.randn(bs, 3, 224, 224, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+for _ in range(3):
+    c(x)
+torch.cuda.synchronize()
+res = {}
+for name, fn in (("forward_only", lambda: c.net(x)), ("call_with_argmax_to_host", lambda: c(x))):
+    ts = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        with torch.inference_mode():
+            fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2] * 1e3
+    res[name] = {"ms_median": round(med, 3), "images_per_s": round(bs / med * 1e3, 1)}
+print(json.dumps(res))
