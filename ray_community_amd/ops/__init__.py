@@ -811,6 +811,28 @@ def batch_norm_act(x, weight, bias, running_mean=None, running_var=None, trainin
     return _BatchNormAct.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu)
 
 
+def affine_act_(x, stats, residual=None, relu: bool = True):
+    """In place: ``x = act(x * stats[2] + stats[3] [+ residual])`` per channel, for a channels_last
+    bf16 CUDA tensor (the folded-BatchNorm inference epilogue: bias, residual add and ReLU of a
+    convolution's output in ONE NHWC pass, ``rca_bn_apply``). ``stats`` is a float32 [4, C]
+    tensor (rows 2 / 3: scale / shift; rows 0 / 1 unused). Other inputs: the torch composition."""
+    C = x.shape[1] if x.dim() == 4 else 0
+    if bn_supported(x) and stats.is_cuda and (residual is None or (residual.shape == x.shape and residual.dtype ==
+                                                                   x.dtype and residual.is_contiguous(
+                                                                       memory_format=torch.channels_last))):
+        R = x.numel() // C
+        check(lib().rca_bn_apply(x.data_ptr(), residual.data_ptr() if residual is not None else None,
+                                 stats.data_ptr(), x.data_ptr(), R, C, int(relu), stream_ptr(x.device)),
+              "bn_apply")
+        return x
+    y = x.float() * stats[2].view(1, -1, 1, 1) + stats[3].view(1, -1, 1, 1)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return x.copy_(y.to(x.dtype))
+
+
 # --------------------------------------------------------------------------------- attention
 def flash_attention_supported(seq_len: int, head_dim: int, n_q_heads: int, n_kv_heads: int) -> bool:
     """Shapes the gfx950 flash-attention kernels cover (others use torch SDPA)."""

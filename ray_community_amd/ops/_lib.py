@@ -65,6 +65,7 @@ _SIGS = {
     "rca_bn_workspace": (c_ll, [c_ll, c_int]),
     "rca_bn_fwd": (c_int, [c_void_p] * 9 + [c_ll, c_int, c_float, c_float, c_int, c_void_p]),
     "rca_bn_apply": (c_int, [c_void_p] * 4 + [c_ll, c_int, c_int, c_void_p]),
+    "rca_bn_set_unroll": (c_int, [c_int]),
     "rca_bn_bwd": (c_int, [c_void_p] * 11 + [c_ll, c_int, c_int, c_void_p]),
     "rca_gbdt_hist_workspace": (c_ll, [c_int, c_ll, c_int, c_int]),
     "rca_gbdt_hist_exact_workspace": (c_ll, [c_int, c_ll, c_int, c_int]),

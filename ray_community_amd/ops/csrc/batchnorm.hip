@@ -183,6 +183,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
 
 // out = act(x*scale + shift [+ res]); grid-stride step is a multiple of C/8, so each thread
 // keeps one channel group (and its 16 coefficients in registers) for the whole launch.
+template <int U>
 __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                                const float* __restrict__ stats, int relu, long long nvec,
                                                                int C, bf16_t* __restrict__ out) {
@@ -196,22 +197,48 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(const bf16_t* __
     sc[j] = stats[2 * C + cg * 8 + j];
     sh[j] = stats[3 * C + cg * 8 + j];
   }
-  for (long long v = gt; v < nvec; v += T) {
+  // four 16-B vectors per lane in flight (T is a multiple of C/8, so all four share the channel
+  // group): one load per iteration left this pass latency-bound well under the HBM rate
+  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+  const u32x4* rv = reinterpret_cast<const u32x4*>(res);
+  u32x4* ov = reinterpret_cast<u32x4*>(out);
+  auto one = [&](const u32x4& xx, const u32x4* rr, long long v) {
     float f[8];
-    unpack8(reinterpret_cast<const u32x4*>(x)[v], f);
+    unpack8(xx, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], sc[j], sh[j]);
-    if (res) {
-      float rr[8];
-      unpack8(reinterpret_cast<const u32x4*>(res)[v], rr);
+    if (rr) {
+      float r8[8];
+      unpack8(*rr, r8);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += rr[j];
+      for (int j = 0; j < 8; ++j) f[j] += r8[j];
     }
     if (relu) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
     }
-    reinterpret_cast<u32x4*>(out)[v] = pack8(f);
+    ov[v] = pack8(f);
+  };
+  long long v = gt;
+  for (; U == 4 && v + 3 * T < nvec; v += 4 * T) {
+    const u32x4 x0 = xv[v], x1 = xv[v + T], x2 = xv[v + 2 * T], x3 = xv[v + 3 * T];
+    u32x4 r0, r1, r2, r3;
+    if (res) {
+      r0 = rv[v];
+      r1 = rv[v + T];
+      r2 = rv[v + 2 * T];
+      r3 = rv[v + 3 * T];
+    }
+    one(x0, res ? &r0 : nullptr, v);
+    one(x1, res ? &r1 : nullptr, v + T);
+    one(x2, res ? &r2 : nullptr, v + 2 * T);
+    one(x3, res ? &r3 : nullptr, v + 3 * T);
+  }
+  for (; v < nvec; v += T) {
+    const u32x4 x0 = xv[v];
+    u32x4 r0;
+    if (res) r0 = rv[v];
+    one(x0, res ? &r0 : nullptr, v);
   }
 }
 
@@ -267,6 +294,21 @@ Plan reduce_plan(long long R, int C) {
   return p;
 }
 
+// 4 (default) or 1 vectors in flight per lane in the forward apply pass (RCA_BN_UNROLL; run-time
+// switch rca_bn_set_unroll for same-process A/Bs)
+int g_bn_unroll = [] {
+  const char* e = getenv("RCA_BN_UNROLL");
+  return e && atoi(e) == 1 ? 1 : 4;
+}();
+
+template <typename... A>
+void launch_apply(dim3 grid, dim3 block, int shm, hipStream_t st, A... args) {
+  if (g_bn_unroll == 1)
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<1>, grid, block, shm, st, args...);
+  else
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<4>, grid, block, shm, st, args...);
+}
+
 int apply_grid(long long nvec) {
   long long g = (nvec + kThreads - 1) / kThreads;
   if (g > 4096) g = 4096;  // 16 blocks per CU; step stays a multiple of 256 >= C/8
@@ -277,6 +319,12 @@ int apply_grid(long long nvec) {
 bool supported(int C) { return C >= 8 && C <= 2048 && C % 8 == 0 && (kThreads % (C >> 3)) == 0; }
 
 }  // namespace
+
+RCA_API int rca_bn_set_unroll(int u) {
+  const int old = g_bn_unroll;
+  g_bn_unroll = u == 1 ? 1 : 4;
+  return old;
+}
 
 // Workspace floats needed by the partial sums of a reduction over [R, C].
 RCA_API long long rca_bn_workspace(long long R, int C) {
@@ -296,7 +344,7 @@ RCA_API int rca_bn_fwd(const void* x, const void* res, const float* gamma, const
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(C / 8), dim3(kThreads), 0, stream, ws, p.nblk, R, C, (const bf16_t*)x,
                      gamma, beta, eps, momentum, running_mean, running_var, stats);
   const long long nvec = R * C / 8;
-  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(apply_grid(nvec)), dim3(kThreads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
+  launch_apply(dim3(apply_grid(nvec)), dim3(kThreads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
                      stats, relu, nvec, C, (bf16_t*)out);
   return (int)hipGetLastError();
 }
@@ -306,7 +354,7 @@ RCA_API int rca_bn_apply(const void* x, const void* res, const float* stats, voi
                          hipStream_t stream) {
   if (!supported(C) || R < 1) return -1;
   const long long nvec = R * C / 8;
-  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(apply_grid(nvec)), dim3(kThreads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
+  launch_apply(dim3(apply_grid(nvec)), dim3(kThreads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
                      stats, relu, nvec, C, (bf16_t*)out);
   return (int)hipGetLastError();
 }

@@ -12,12 +12,34 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from bench_data_serve import Classifier  # noqa: E402
 
 bs = int(os.environ.get("BS", 256))
+layout = os.environ.get("LAYOUT", "nhwc")
 c = Classifier("resnet50", 224, bs, "cuda")
-x = torch.randn(bs, 3, 224, 224, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+x = torch.randn(bs, 3, 224, 224, device="cuda", dtype=torch.bfloat16)
+if layout == "nhwc":
+    x = x.contiguous(memory_format=torch.channels_last)
+else:
+    c.net = c.net.to(memory_format=torch.contiguous_format)
 for _ in range(3):
     c(x)
 torch.cuda.synchronize()
+time.sleep(float(os.environ.get("GAP_S", 0)))  # an idle gap that marks the steady state in a trace
 res = {}
+if os.environ.get("AB_UNROLL"):  # same-process A/B of the BN apply pass: 1 vs 4 vectors in flight per lane
+    from ray_community_amd.ops._lib import lib
+
+    for rnd in range(3):
+        for u in (1, 4):
+            lib().rca_bn_set_unroll(u)
+            ts = []
+            for _ in range(15):
+                t0 = time.perf_counter()
+                with torch.inference_mode():
+                    c.net(x)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            res.setdefault(f"unroll{u}_ms", []).append(round(ts[len(ts) // 2] * 1e3, 3))
+    lib().rca_bn_set_unroll(4)
 for name, fn in (("forward_only", lambda: c.net(x)), ("call_with_argmax_to_host", lambda: c(x))):
     ts = []
     for _ in range(20):
@@ -29,4 +51,4 @@ for name, fn in (("forward_only", lambda: c.net(x)), ("call_with_argmax_to_host"
     ts.sort()
     med = ts[len(ts) // 2] * 1e3
     res[name] = {"ms_median": round(med, 3), "images_per_s": round(bs / med * 1e3, 1)}
-print(json.dumps(res))
+print(json.dumps({"layout": layout, "bs": bs, **res}))

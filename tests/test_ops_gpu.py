@@ -203,6 +203,51 @@ def test_image_normalize_channels_last(shape, dtype):
     _close(out, r, atol=1e-5 if dtype == torch.float32 else 2e-2, rtol=1e-5 if dtype == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("relu,with_res", [(True, False), (False, False), (True, True)])
+def test_affine_act_inplace_matches_fp32(relu, with_res):
+    torch.manual_seed(0)
+    for C in (64, 256, 2048):
+        x = torch.randn(3, C, 7, 9, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        res = torch.randn_like(x) if with_res else None
+        stats = torch.zeros(4, C, device=DEV)
+        stats[2] = torch.rand(C, device=DEV) + 0.5
+        stats[3] = torch.randn(C, device=DEV)
+        want = x.float() * stats[2].view(1, -1, 1, 1) + stats[3].view(1, -1, 1, 1)
+        if with_res:
+            want = want + res.float()
+        if relu:
+            want = torch.relu(want)
+        ptr = x.data_ptr()
+        out = ops.affine_act_(x, stats, res, relu)
+        assert out.data_ptr() == ptr  # in place
+        _close(out, want, atol=3e-2, rtol=1e-2)
+
+
+def test_folded_resnet50_inference_matches_fp32():
+    """Serving graph (BN folded, shift + residual + ReLU in one NHWC pass per conv) in bf16 against
+    the unfolded fp32 eval-mode network."""
+    from ray_community_amd.models.resnet import BiasAct, fold_batchnorm, resnet50
+
+    torch.manual_seed(0)
+    ref = resnet50(num_classes=10).to(DEV).eval()
+    for m in ref.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.3, 0.3)
+            m.running_var.uniform_(0.5, 1.5)
+            m.weight.data.uniform_(0.5, 1.2)
+            m.bias.data.uniform_(-0.1, 0.1)
+    x = torch.randn(4, 3, 96, 96, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        want = ref(x)
+        import copy
+
+        net = fold_batchnorm(copy.deepcopy(ref)).to(torch.bfloat16)
+        assert isinstance(net.blocks[0].bn3, BiasAct) and net.blocks[0].bn3.stats.dtype == torch.float32
+        got = net(x.to(torch.bfloat16)).float()
+    err = (got - want).abs().max() / want.abs().max()
+    assert err < 5e-2, float(err)
+
+
 def test_resnet50_train_step_gpu():
     from ray_community_amd.train.vision import build_resnet_training
 
