@@ -197,8 +197,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(const bf16_t* __
     sc[j] = stats[2 * C + cg * 8 + j];
     sh[j] = stats[3 * C + cg * 8 + j];
   }
-  // four 16-B vectors per lane in flight (T is a multiple of C/8, so all four share the channel
-  // group): one load per iteration left this pass latency-bound well under the HBM rate
+  // U = 4: four 16-B vectors per lane in flight (T is a multiple of C/8, so all four share the
+  // channel group); measured slower than U = 1 (g_bn_unroll below)
   const u32x4* xv = reinterpret_cast<const u32x4*>(x);
   const u32x4* rv = reinterpret_cast<const u32x4*>(res);
   u32x4* ov = reinterpret_cast<u32x4*>(out);
@@ -294,11 +294,13 @@ Plan reduce_plan(long long R, int C) {
   return p;
 }
 
-// 4 (default) or 1 vectors in flight per lane in the forward apply pass (RCA_BN_UNROLL; run-time
-// switch rca_bn_set_unroll for same-process A/Bs)
+// 1 (default) or 4 vectors in flight per lane in the forward apply pass (RCA_BN_UNROLL=4; run-time
+// switch rca_bn_set_unroll for same-process A/Bs). Measured in the folded ResNet-50 inference
+// forward (bs 256, 3 interleaved rounds, scripts/diag/replica_alone.py AB_UNROLL=1): 1 vector
+// 7.38-7.43 ms, 4 vectors 7.62-7.67 ms, so the single-vector loop stays the default.
 int g_bn_unroll = [] {
   const char* e = getenv("RCA_BN_UNROLL");
-  return e && atoi(e) == 1 ? 1 : 4;
+  return e && atoi(e) == 4 ? 4 : 1;
 }();
 
 template <typename... A>
@@ -322,7 +324,7 @@ bool supported(int C) { return C >= 8 && C <= 2048 && C % 8 == 0 && (kThreads % 
 
 RCA_API int rca_bn_set_unroll(int u) {
   const int old = g_bn_unroll;
-  g_bn_unroll = u == 1 ? 1 : 4;
+  g_bn_unroll = u == 4 ? 4 : 1;
   return old;
 }
 

@@ -5,10 +5,24 @@ import copy
 from typing import Any, Dict, Optional
 
 
+def _default_mapping_fn(agent_id, episode=None, worker=None, **kw):
+    return "default_policy"
+
+
 class AlgorithmConfig:
     algo_class = None
 
+    # reference: every agent maps to the single default policy / module
+    DEFAULT_POLICY_MAPPING_FN = staticmethod(_default_mapping_fn)
+    DEFAULT_AGENT_TO_MODULE_MAPPING_FN = staticmethod(_default_mapping_fn)
+
+    def __setattr__(self, k, v):
+        if self.__dict__.get("_is_frozen") and k != "_is_frozen":
+            raise AttributeError(f"Cannot set attribute ({k}) of an already frozen AlgorithmConfig")
+        object.__setattr__(self, k, v)
+
     def __init__(self, algo_class=None):
+        self._is_frozen = False
         if algo_class is not None:
             self.algo_class = algo_class
         # environment
@@ -76,6 +90,15 @@ class AlgorithmConfig:
         self.checkpoint_trainable_policies_only = False
         # custom RLModule (reference rl_module():2737)
         self._rl_module_spec = None
+        # exploration / experimental / python environment (reference exploration():2141,
+        # experimental():2806, python_environment():1431)
+        self.exploration_config: Dict = {}
+        self._experimental: Dict = {}
+        self.extra_python_environs_for_driver: Dict = {}
+        self.extra_python_environs_for_worker: Dict = {}
+        self.train_batch_size_per_learner = None
+        self.in_evaluation = False
+        self._per_module_overrides: Dict = {}
 
     # ------------------------------------------------------------------ builder methods
     def environment(self, env=None, *, env_config=None, observation_space=None, action_space=None, **kw):
@@ -344,12 +367,256 @@ class AlgorithmConfig:
     def callbacks_class(self, v):
         self._callbacks = v
 
+    def exploration(self, *, explore=None, exploration_config=None, **kw):
+        if explore is not None:
+            self.explore = bool(explore)
+        if exploration_config is not None:
+            self.exploration_config = {**self.exploration_config, **dict(exploration_config)}
+        return self
+
+    def experimental(self, **kw):
+        """Experimental switches (``_torch_grad_scaler_class``, ``_tf_policy_handles_more_than_one_loss``,
+        ...): stored under their names; unknown ones are kept too, as in the reference."""
+        self._experimental.update(kw)
+        return self
+
+    def python_environment(self, *, extra_python_environs_for_driver=None, extra_python_environs_for_worker=None):
+        """Environment variables set in the driver / every env runner process."""
+        if extra_python_environs_for_driver is not None:
+            self.extra_python_environs_for_driver = dict(extra_python_environs_for_driver)
+        if extra_python_environs_for_worker is not None:
+            self.extra_python_environs_for_worker = dict(extra_python_environs_for_worker)
+        return self
+
+    @classmethod
+    def overrides(cls, **kwargs) -> Dict:
+        """A dict of setting overrides (for ``evaluation(evaluation_config=...)`` and per-module
+        overrides), checked against the config's attribute names."""
+        default = cls()
+        for k in kwargs:
+            if not hasattr(default, k) and k != "lambda":
+                raise KeyError(f"Invalid property name {k!r} for config class {cls.__name__}")
+        return dict(kwargs)
+
+    # ------------------------------------------------------------------ derived views
+    @property
+    def num_workers(self) -> int:  # old-stack name of num_env_runners
+        return self.num_env_runners
+
+    @property
+    def uses_new_env_runners(self) -> bool:
+        return True
+
+    @property
+    def total_train_batch_size(self) -> int:
+        """The batch one training iteration learns from: per-learner size x learners, or
+        ``train_batch_size``."""
+        if self.train_batch_size_per_learner:
+            return int(self.train_batch_size_per_learner) * max(1, int(self.num_learners))
+        return int(self.train_batch_size)
+
+    @property
+    def is_atari(self) -> bool:
+        e = self.env
+        if isinstance(e, str) and (e.startswith("ALE/") or "NoFrameskip" in e or "Atari" in e):
+            return True
+        shp = getattr(self.observation_space, "shape", None)
+        return bool(shp) and tuple(shp)[:2] == (84, 84)
+
+    @property
+    def multiagent(self) -> Dict:
+        """Old-stack dict view of the multi-agent settings."""
+        return {"policies": self.policies, "policy_mapping_fn": self.policy_mapping_fn,
+                "policies_to_train": self.policies_to_train}
+
+    @property
+    def learner_class(self):
+        return self.get_default_learner_class()
+
+    def get_default_learner_class(self):
+        from ..core.learner import Learner
+
+        return Learner
+
+    def get_default_rl_module_spec(self):
+        from ..core.rl_module import RecurrentRLModule, RLModule, RLModuleSpec
+
+        m = self.model or {}
+        return RLModuleSpec(module_class=RecurrentRLModule if m.get("use_lstm") else RLModule, model_config=dict(m))
+
+    def get_multi_agent_setup(self, *, env=None, spaces=None):
+        """(policies {id: PolicySpec-like tuple}, is_policy_to_train(policy_id) callable)."""
+        pols = dict(self.policies) if self.policies else {"default_policy": None}
+        if spaces:
+            pols = {p: (v if v is not None else (None, *spaces.get(p, (None, None)), {})) for p, v in pols.items()}
+        ptt = self.policies_to_train
+
+        def is_policy_to_train(pid, batch=None):
+            if ptt is None:
+                return True
+            return ptt(pid, batch) if callable(ptt) else pid in ptt
+
+        return pols, is_policy_to_train
+
+    def get_marl_module_spec(self, *, policy_dict=None, single_agent_rl_module_spec=None, env=None, spaces=None):
+        """The MultiRLModuleSpec of this config: one spec per policy (a user ``rl_module_spec`` per
+        module id wins, else the default module spec)."""
+        from ..core.rl_module import MultiRLModuleSpec, RLModuleSpec
+
+        user = self._rl_module_spec
+        if isinstance(user, MultiRLModuleSpec):
+            return user
+        pols = policy_dict or self.get_multi_agent_setup(spaces=spaces)[0]
+        base = single_agent_rl_module_spec or self.get_default_rl_module_spec()
+        specs = {}
+        for pid in pols:
+            spec = user.get(pid) if isinstance(user, dict) else (user if isinstance(user, RLModuleSpec) else None)
+            if spec is None:
+                spec = RLModuleSpec(base.module_class, model_config=dict(base.model_config))
+                if spaces and pid in spaces:
+                    spec.observation_space, spec.action_space = spaces[pid]
+            specs[pid] = spec
+        return MultiRLModuleSpec(specs)
+
+    get_multi_rl_module_spec = get_marl_module_spec
+
+    def get_config_for_module(self, module_id):
+        """A copy of this config with the overrides registered for ``module_id`` applied."""
+        c = self.copy(copy_frozen=False)
+        for k, v in (self._per_module_overrides.get(module_id) or {}).items():
+            setattr(c, k, v)
+        return c
+
+    def get_evaluation_config_object(self):
+        """The config evaluation runs with: a copy with ``evaluation_config`` applied, ``in_evaluation``
+        set and the evaluation runner count as ``num_env_runners``."""
+        c = self.copy(copy_frozen=False)
+        ov = self.evaluation_config
+        if isinstance(ov, AlgorithmConfig):
+            ov = {k: v for k, v in ov.to_dict().items() if k != "framework"}
+        c.update_from_dict(dict(ov or {}))
+        c.in_evaluation = True
+        c.num_env_runners = self.evaluation_num_env_runners
+        return c
+
+    def get_torch_compile_worker_config(self) -> Dict:
+        """No tracing compiler on this stack (HIP graphs and hand-written kernels instead): the
+        compile config is reported disabled."""
+        return {"torch_compile": False, "torch_compile_backend": None, "torch_compile_mode": None}
+
+    def validate_train_batch_size_vs_rollout_fragment_length(self) -> None:
+        """A fixed rollout_fragment_length must let the runners fill train_batch_size within a
+        factor of 10 (reference check of the same name)."""
+        if self.rollout_fragment_length == "auto" or self.batch_mode != "truncate_episodes":
+            return
+        per_round = int(self.rollout_fragment_length) * max(1, int(self.num_env_runners)) * \
+            int(self.num_envs_per_env_runner)
+        tbs = self.total_train_batch_size
+        if tbs > 0 and (per_round > 10 * tbs or per_round * 10 < tbs and tbs % per_round != 0 and per_round < tbs // 10):
+            raise ValueError(f"rollout_fragment_length ({self.rollout_fragment_length}) x runners x envs "
+                             f"({per_round} per round) does not fit train_batch_size ({tbs})")
+
+    # ------------------------------------------------------------------ component builders
+    def build_env_to_module_connector(self, env):
+        from ..connectors import build_env_to_module
+
+        return build_env_to_module(dict(self.to_dict(), **self._connector_dict()), env)
+
+    def build_module_to_env_connector(self, env):
+        from ..connectors import build_module_to_env
+
+        return build_module_to_env(dict(self.to_dict(), **self._connector_dict()), env)
+
+    def build_learner_connector(self, input_observation_space, input_action_space, device=None):
+        from ..connectors import build_learner_connector
+
+        return build_learner_connector(dict(self.to_dict(), **self._connector_dict()), input_observation_space,
+                                       input_action_space)
+
+    def _learner_config(self) -> Dict:
+        d = self.to_dict()
+        d.update(self._connector_dict())
+        if self.algo_class is not None:
+            d["_algo"] = getattr(self.algo_class, "__name__", None)
+        return d
+
+    def build_learner(self, *, env=None, spaces=None, observation_space=None, action_space=None, use_gpu=False):
+        """One Learner (RLModule + optimizer + learner connector) for this config."""
+        obs, act = self._spaces(env, spaces, observation_space, action_space)
+        return self.get_default_learner_class()(self._learner_config(), obs, act, use_gpu)
+
+    def build_learner_group(self, *, env=None, spaces=None, observation_space=None, action_space=None):
+        """The LearnerGroup an Algorithm trains with (local learner, or ``num_learners`` GPU learner
+        actors over one RCCL process group)."""
+        from ..core.learner import LearnerGroup
+
+        obs, act = self._spaces(env, spaces, observation_space, action_space)
+        return LearnerGroup(self._learner_config(), obs, act)
+
+    def _spaces(self, env, spaces, obs, act):
+        if spaces:
+            obs, act = next(iter(spaces.values())) if isinstance(spaces, dict) else spaces
+        if (obs is None or act is None) and env is not None:
+            obs, act = env.observation_space, env.action_space
+        obs, act = obs or self.observation_space, act or self.action_space
+        if obs is None or act is None:
+            from ..env.envs import make_vector_env
+
+            e = make_vector_env(self.env, 1, self.env_config)
+            obs, act = e.observation_space, e.action_space
+        return obs, act
+
     # ------------------------------------------------------------------ misc
+    def freeze(self) -> None:
+        """No further changes (the Algorithm freezes the config it runs with)."""
+        self._is_frozen = True
+
     def copy(self, copy_frozen=None):
-        return copy.deepcopy(self)
+        c = copy.deepcopy(self)
+        if copy_frozen is not True:
+            c._is_frozen = False
+        return c
+
+    def keys(self):
+        return self.to_dict().keys()
+
+    def values(self):
+        return self.to_dict().values()
+
+    def items(self):
+        return self.to_dict().items()
+
+    def pop(self, k, default=None):
+        """Reset ``k`` to the default config's value and return the current one."""
+        v = getattr(self, k, default)
+        if hasattr(type(self)(), k):
+            setattr(self, k, getattr(type(self)(), k))
+        return v
+
+    def serialize(self) -> Dict:
+        """A JSON-able dict of the config: classes and callables by import path / name."""
+        import json
+
+        def conv(v):
+            if isinstance(v, (str, int, float, bool)) or v is None:
+                return v
+            if isinstance(v, dict):
+                return {str(k): conv(x) for k, x in v.items()}
+            if isinstance(v, (list, tuple, set)):
+                return [conv(x) for x in v]
+            if isinstance(v, type) or callable(v):
+                return f"{getattr(v, '__module__', '?')}.{getattr(v, '__qualname__', repr(v))}"
+            try:
+                json.dumps(v)
+                return v
+            except TypeError:
+                return repr(v)
+
+        return {k: conv(v) for k, v in self.to_dict().items()}
 
     def to_dict(self) -> Dict:
         d = {k: v for k, v in self.__dict__.items() if not k.startswith("_")}
+        d.pop("in_evaluation", None) if not self.__dict__.get("in_evaluation") else None
         d["framework"] = self.framework_str
         return d
 

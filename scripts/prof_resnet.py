@@ -26,6 +26,7 @@ def main():
     for _ in range(a.warmup):
         step(*data)
     torch.cuda.synchronize()
+    time.sleep(float(os.environ.get("GAP_S", 0)))  # idle gap marking the steady state in a trace
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step(*data)
