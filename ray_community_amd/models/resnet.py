@@ -15,6 +15,8 @@ stem's uint8 -> normalised bf16 NHWC conversion is the HIP ``image_normalize`` k
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -49,6 +51,26 @@ class BiasAct(nn.Module):
                 y = y + residual
             return F.relu(y) if relu else y
         return ops.affine_act_(x, self.stats, residual, relu)
+
+
+# Folded inference graph, opt-in (RCA_RESNET_GEMM_1X1=1 or GEMM_1X1[0] = True): 1x1 stride-1
+# convolutions whose shape the in-tree GEMM covers run as ONE kernel with the shift / residual /
+# ReLU in its epilogue (ops.conv1x1_affine_act) instead of a MIOpen convolution + the BiasAct pass.
+# Off by default: the bs-256 forward measured 7.79-7.85 ms with it against 7.48-7.51 ms without
+# (same process, 3 interleaved rounds, profiles/resnet_infer_r5.md) -- the GEMM's pipeline is built
+# for long K, and these convolutions have K = 128-2048 with short, wide outputs.
+GEMM_1X1 = [os.environ.get("RCA_RESNET_GEMM_1X1", "0") == "1"]
+
+
+def conv_act(conv: nn.Conv2d, bn, x, residual=None, relu=True):
+    """``act(bn(conv(x)) [+ residual])``; a folded 1x1 convolution goes through the GEMM epilogue
+    when the shapes allow it and no gradient is needed."""
+    if (GEMM_1X1[0] and isinstance(bn, BiasAct) and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None
+            and not (torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad))
+            and ops.conv1x1_affine_act_supported(x, conv.weight)):
+        return ops.conv1x1_affine_act(x, conv.weight, bn.stats[3], residual, relu)
+    return bn_act(bn, conv(x), residual=residual, relu=relu)
 
 
 def bn_act(bn: nn.BatchNorm2d, x, residual=None, relu=True):
@@ -88,10 +110,10 @@ class Bottleneck(nn.Module):
             self.down = nn.Sequential(nn.Conv2d(in_ch, out_ch, 1, stride=stride, bias=False), nn.BatchNorm2d(out_ch))
 
     def forward(self, x):
-        idt = x if self.down is None else bn_act(self.down[1], self.down[0](x), relu=False)
-        y = bn_act(self.bn1, self.conv1(x))
-        y = bn_act(self.bn2, self.conv2(y))
-        return bn_act(self.bn3, self.conv3(y), residual=idt)  # relu(bn3(conv3(y)) + identity), one kernel
+        idt = x if self.down is None else conv_act(self.down[0], self.down[1], x, relu=False)
+        y = conv_act(self.conv1, self.bn1, x)
+        y = conv_act(self.conv2, self.bn2, y)
+        return conv_act(self.conv3, self.bn3, y, residual=idt)  # relu(bn3(conv3(y)) + identity)
 
 
 class ResNet(nn.Module):

@@ -833,6 +833,42 @@ def affine_act_(x, stats, residual=None, relu: bool = True):
     return x.copy_(y.to(x.dtype))
 
 
+def conv1x1_affine_act_supported(x, weight) -> bool:
+    """1x1 / stride-1 NHWC convolutions the in-tree GEMM runs with the affine epilogue:
+    M = N*H*W % 256, Cout % 256, Cin % 128 (``rca_gemm_affine_act``)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and weight.dim() == 4
+            and tuple(weight.shape[2:]) == (1, 1)):
+        return False
+    n, c, h, w = x.shape
+    return (n * h * w) % 256 == 0 and weight.shape[0] % 256 == 0 and c % 128 == 0 and c == weight.shape[1] and \
+        n * h * w * c * 2 < 2 ** 32
+
+
+def conv1x1_affine_act(x, weight, shift, residual=None, relu: bool = True):
+    """``act(conv1x1(x, weight) + shift [+ residual])`` for a channels_last bf16 CUDA tensor: ONE
+    kernel, the convolution as a GEMM [N*H*W, Cin] x [Cout, Cin]^T with the shift / residual /
+    ReLU applied to the fp32 accumulators (``ops/csrc/gemm4.hip`` EPI 2). ``shift``: fp32 [Cout]
+    (the folded BatchNorm shift). Unsupported shapes raise (check ``conv1x1_affine_act_supported``)."""
+    if not conv1x1_affine_act_supported(x, weight):
+        raise ValueError("conv1x1_affine_act: unsupported shape / layout")
+    n, c, h, w = x.shape
+    co = weight.shape[0]
+    wm = weight.reshape(co, c)
+    if not wm.is_contiguous():
+        wm = wm.contiguous()
+    out = torch.empty((n, co, h, w), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    sh = shift.contiguous().float()
+    if residual is not None and (residual.shape != out.shape or residual.dtype != out.dtype
+                                 or not residual.is_contiguous(memory_format=torch.channels_last)):
+        residual = residual.to(out.dtype).contiguous(memory_format=torch.channels_last)
+    M = n * h * w
+    check(lib().rca_gemm_affine_act(x.data_ptr(), wm.data_ptr(), sh.data_ptr(),
+                                    residual.data_ptr() if residual is not None else None, out.data_ptr(), M, co, c,
+                                    c, c, co, co, int(relu), stream_ptr(x.device)), "gemm_affine_act")
+    return out
+
+
 # --------------------------------------------------------------------------------- attention
 def flash_attention_supported(seq_len: int, head_dim: int, n_q_heads: int, n_kv_heads: int) -> bool:
     """Shapes the gfx950 flash-attention kernels cover (others use torch SDPA)."""

@@ -588,6 +588,11 @@ struct EpiArgs {
   bf16_t* dgu_t;     // [2F][M]
   long ldg, ldd, ldt;
   int F;
+  // EPI 2 (per-column affine epilogue): C = act(acc + shift[n] (+ res[m][n]))
+  const float* shift;
+  const bf16_t* res;
+  long ldr;
+  int relu;
 };
 
 // SwiGLU-backward epilogue (variant 7, EPI 1). The wave's 128 x 128 accumulator tile is
@@ -841,6 +846,34 @@ __global__ __launch_bounds__(NT4, 1) void gemm4c_kernel(const bf16_t* __restrict
     swiglu_bwd_epilogue(acc, ep, smem, m0 + wr * 128, n0 + wc * 128, wid, lane);
     return;
   }
+  if constexpr (EPI == 2) {
+    // conv-as-GEMM epilogue (1x1 NHWC convolution with the folded BatchNorm): the per-channel
+    // shift, the residual and the ReLU applied to the fp32 accumulators before the one bf16 store,
+    // instead of a separate read-modify-write pass over the output
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + wc * 128 + j * 16 + 4 * (lane >> 4);
+      const f32x4 sh = *reinterpret_cast<const f32x4*>(ep.shift + n);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const long m = m0 + wr * 128 + i * 16 + (lane & 15);
+        f32x4 v = acc[i][j] + sh;
+        if (ep.res) {
+          const unsigned long long r = *reinterpret_cast<const unsigned long long*>(ep.res + m * ep.ldr + n);
+          v[0] += bf2f((bf16_t)(r & 0xffff));
+          v[1] += bf2f((bf16_t)((r >> 16) & 0xffff));
+          v[2] += bf2f((bf16_t)((r >> 32) & 0xffff));
+          v[3] += bf2f((bf16_t)((r >> 48) & 0xffff));
+        }
+        if (ep.relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        store4<false>(C, m * ldc + n, v);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const long m = m0 + wr * 128 + i * 16 + (lane & 15);
@@ -968,6 +1001,26 @@ extern "C" int rca_gemm4_bf16_internal(const void* A, const void* B, void* C, in
 // main loop, EPI 1): dy [T][H] (k = H contiguous, row stride ld_dy), w_t = W_down^T [F][H] (row
 // stride ld_w), gu / dgu [T][2F] contiguous, dgu_t [2F][T] contiguous.
 // Contract: T % 256 == 0, F % 256 == 0, H % 128 == 0, 16-B aligned rows; returns -1 otherwise.
+// out[m][n] = act(sum_k x[m][k] w[n][k] + shift[n] (+ res[m][n])): a 1x1 NHWC convolution with the
+// folded-BatchNorm shift, residual add and ReLU in the epilogue (variant 7's main loop, EPI 2).
+// x [M][K] (row stride ldx), w [N][K] (ldw), out / res [M][N] (ldo / ldr), shift fp32 [N].
+// Contract: M % 256 == 0, N % 256 == 0, K % 128 == 0, 16-B aligned rows, each operand < 4 GB;
+// returns -1 otherwise.
+RCA_API int rca_gemm_affine_act(const void* x, const void* w, const float* shift, const void* res, void* out, int M,
+                                int N, int K, long long ldx, long long ldw, long long ldo, long long ldr, int relu,
+                                hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 128 || ldx % 8 || ldw % 8 || ldo % 4 ||
+      (res && ldr % 4))
+    return -1;
+  if ((double)M * ldx * 2 >= 4294967296.0 || (double)N * ldw * 2 >= 4294967296.0) return -1;
+  EpiArgs ep{};
+  ep.shift = shift;
+  ep.res = (const bf16_t*)res;
+  ep.ldr = (long)ldr;
+  ep.relu = relu;
+  return launch4c<false, 24, 4, 96, 2, 1, 1, 1, 2>(x, w, out, M, N, K, ldx, ldw, ldo, st, ep);
+}
+
 RCA_API int rca_gemm_swiglu_bwd(const void* dy, const void* w_t, const void* gu, void* dgu, void* dgu_t, int T, int F,
                                 int H, long long ld_dy, long long ld_w, hipStream_t st) {
   if (T <= 0 || F <= 0 || H <= 0 || T % 256 || F % 256 || H % 128 || ld_dy % 8 || ld_w % 8) return -1;

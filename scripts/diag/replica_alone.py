@@ -40,6 +40,25 @@ if os.environ.get("AB_UNROLL"):  # same-process A/B of the BN apply pass: 1 vs 4
             ts.sort()
             res.setdefault(f"unroll{u}_ms", []).append(round(ts[len(ts) // 2] * 1e3, 3))
     lib().rca_bn_set_unroll(4)
+if os.environ.get("AB_GEMM"):  # same-process A/B: folded 1x1 convolutions on the GEMM epilogue vs MIOpen + BiasAct
+    from ray_community_amd.models import resnet as R
+
+    for rnd in range(3):
+        for on in (False, True):
+            R.GEMM_1X1[0] = on
+            for _ in range(2):
+                with torch.inference_mode():
+                    c.net(x)
+            ts = []
+            for _ in range(15):
+                t0 = time.perf_counter()
+                with torch.inference_mode():
+                    c.net(x)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            res.setdefault(f"gemm1x1_{int(on)}_ms", []).append(round(ts[len(ts) // 2] * 1e3, 3))
+    R.GEMM_1X1[0] = False
 for name, fn in (("forward_only", lambda: c.net(x)), ("call_with_argmax_to_host", lambda: c(x))):
     ts = []
     for _ in range(20):

@@ -223,6 +223,27 @@ def test_affine_act_inplace_matches_fp32(relu, with_res):
         _close(out, want, atol=3e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("N,Cin,Cout,HW", [(2, 128, 256, 16), (4, 512, 2048, 7), (1, 1024, 256, 16)])
+@pytest.mark.parametrize("with_res,relu", [(False, True), (True, True), (False, False)])
+def test_conv1x1_affine_act_matches_fp32(N, Cin, Cout, HW, with_res, relu):
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, HW, HW, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 1, 1, device=DEV) / Cin ** 0.5).to(torch.bfloat16)
+    shift = torch.randn(Cout, device=DEV)
+    res = torch.randn(N, Cout, HW, HW, device=DEV).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last) if with_res else None
+    if not ops.conv1x1_affine_act_supported(x, w):
+        pytest.skip("M = N*H*W not a multiple of 256")
+    out = ops.conv1x1_affine_act(x, w, shift, res, relu)
+    assert out.is_contiguous(memory_format=torch.channels_last) and out.shape == (N, Cout, HW, HW)
+    want = torch.nn.functional.conv2d(x.float(), w.float()) + shift.view(1, -1, 1, 1)
+    if with_res:
+        want = want + res.float()
+    if relu:
+        want = torch.relu(want)
+    _close(out, want, atol=3e-2, rtol=2e-2)
+
+
 def test_folded_resnet50_inference_matches_fp32():
     """Serving graph (BN folded, shift + residual + ReLU in one NHWC pass per conv) in bf16 against
     the unfolded fp32 eval-mode network."""
@@ -243,9 +264,17 @@ def test_folded_resnet50_inference_matches_fp32():
 
         net = fold_batchnorm(copy.deepcopy(ref)).to(torch.bfloat16)
         assert isinstance(net.blocks[0].bn3, BiasAct) and net.blocks[0].bn3.stats.dtype == torch.float32
-        got = net(x.to(torch.bfloat16)).float()
-    err = (got - want).abs().max() / want.abs().max()
-    assert err < 5e-2, float(err)
+        from ray_community_amd.models import resnet as R
+
+        got = net(x.to(torch.bfloat16)).float()  # MIOpen convolutions + the BiasAct pass (default)
+        R.GEMM_1X1[0] = True
+        try:
+            got_gemm = net(x.to(torch.bfloat16)).float()  # 1x1 convolutions on the GEMM epilogue where covered
+        finally:
+            R.GEMM_1X1[0] = False
+    for g in (got, got_gemm):
+        err = (g - want).abs().max() / want.abs().max()
+        assert err < 5e-2, float(err)
 
 
 def test_resnet50_train_step_gpu():
