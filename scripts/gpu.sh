@@ -69,7 +69,7 @@ for step in "$@"; do
       ctr=${arg%%:*}
       prog=${arg#*:}
       rm -rf "gpurun_out/${TAG}_pmc$n"
-      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d "gpurun_out/${TAG}_pmc$n" -o run -- python -u $prog > "$log" 2>&1
+      timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc ${ctr//,/ } -d "gpurun_out/${TAG}_pmc$n" -o run -- python -u $prog > "$log" 2>&1
       rc=$?
       tail -5 "$log" ;;
     sh)
