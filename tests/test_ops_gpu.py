@@ -622,6 +622,35 @@ def test_gemm_buffer_dma_tn_variants(M, N, K, variant):
     assert _gemm_excess(acc, ref, absprod, K, base.float()) <= 1.0
 
 
+@pytest.mark.parametrize("M,N,K", [(8192, 4096, 28672), (8192, 4096, 14336), (8192, 6144, 4096)])
+def test_gemm_variant7_at_llama8b_shapes(M, N, K):
+    """Variant 7 at the production shapes of the 8B step: the gate_up input gradient it runs in
+    the step (8192 x 4096 x 28672, K = 2 x FFN), the down-projection reduction (K = 14336) and the
+    qkv width, against fp32 with the per-element bound above (plain and accumulating)."""
+    torch.manual_seed(K)
+    a = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV) * 0.5 + torch.arange(N, device=DEV)[:, None] * 1e-4).to(torch.bfloat16)
+    lib = ops._lib.lib()
+    prev = lib.rca_gemm_set_variant(7)
+    try:
+        out = ops.gemm(a, b)
+        base = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        acc = base.clone()
+        ops.gemm(a, b, out=acc, accumulate=True)
+    finally:
+        lib.rca_gemm_set_variant(prev)
+    torch.cuda.synchronize()
+    # reference in row blocks (fp32 operands of this size are 0.5-1 GB each)
+    af, bf = a.float(), b.float()
+    worst = 0.0
+    for r in range(0, M, 2048):
+        ref = af[r:r + 2048] @ bf.t()
+        absprod = af[r:r + 2048].abs() @ bf.abs().t()
+        worst = max(worst, _gemm_excess(out[r:r + 2048], ref, absprod, K),
+                    _gemm_excess(acc[r:r + 2048], ref, absprod, K, base[r:r + 2048].float()))
+    assert worst <= 1.0, worst
+
+
 def test_gemm_check_catches_a_corrupted_k_slice():
     """The per-element bound above is tight enough to fail a kernel that drops K-tiles: variant 91
     (timing diagnostic: no LDS-DMA inside the K loop, so every tile after the first two re-reads
