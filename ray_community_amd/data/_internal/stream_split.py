@@ -194,6 +194,9 @@ class SplitCoordinator:
     def stats(self):
         return dict(self._stats, epoch=self._epoch)
 
+    def schema(self):
+        return self._ds.schema()
+
 
 def _slice_block(block, start, end):
     from ..block import BlockAccessor
@@ -226,6 +229,11 @@ class StreamSplitDataIterator(DataIterator):
 
     def __reduce__(self):
         return StreamSplitDataIterator, (self._coord, self._idx, self._n, self._name)
+
+    def schema(self):
+        from ..._private.worker import get
+
+        return get(self._coord.schema.remote())
 
     def __repr__(self):
         return f"StreamSplitDataIterator(split={self._idx}/{self._n}, dataset={self._name})"

@@ -432,6 +432,87 @@ class Dataset:
 
         return _It()
 
+    # ------------------------------------------------------------------ lineage
+    def has_serializable_lineage(self) -> bool:
+        """True when the dataset can be re-created from its plan alone: every input is a read
+        task (not an in-memory block ref) and nothing is materialised (reference
+        ``Dataset.has_serializable_lineage``)."""
+        if self._materialized is not None:
+            return False
+        return all(x[0] != "ref" for x in self._inputs) and all(
+            not isinstance(o.get(k), Dataset) or o[k].has_serializable_lineage()
+            for o in self._ops for k in ("other",)) and all(
+            d.has_serializable_lineage() for o in self._ops for d in (o.get("others") or ()))
+
+    def serialize_lineage(self) -> bytes:
+        """The dataset's plan (read tasks + operators), without any block refs: a bytes object a
+        later session (or another cluster) turns back into the same dataset with
+        ``Dataset.deserialize_lineage`` and re-executes."""
+        if not self.has_serializable_lineage():
+            raise ValueError("Lineage-based serialization is not supported for this dataset: it has in-memory "
+                             "(from_* / materialized) inputs; only read_* datasets carry their full lineage")
+        import cloudpickle
+
+        return cloudpickle.dumps(Dataset(self._inputs, self._ops, self._name))
+
+    @staticmethod
+    def deserialize_lineage(serialized_ds: bytes) -> "Dataset":
+        import cloudpickle
+
+        ds = cloudpickle.loads(serialized_ds)
+        if not isinstance(ds, Dataset):
+            raise TypeError("not a serialized Dataset lineage")
+        return ds
+
+    # ------------------------------------------------------------------ other frameworks
+    def _absent(self, what: str, lib: str):
+        raise ImportError(f"Dataset.{what} needs {lib}, which is not installed in this MI355X image")
+
+    def to_tf(self, *a, **k):
+        self._absent("to_tf", "TensorFlow")
+
+    def iter_tf_batches(self, *a, **k):
+        self._absent("iter_tf_batches", "TensorFlow")
+
+    def to_dask(self, *a, **k):
+        self._absent("to_dask", "dask")
+
+    def to_mars(self, *a, **k):
+        self._absent("to_mars", "mars")
+
+    def to_modin(self, *a, **k):
+        self._absent("to_modin", "modin")
+
+    def to_spark(self, *a, **k):
+        self._absent("to_spark", "raydp / pyspark")
+
+    def write_bigquery(self, *a, **k):
+        self._absent("write_bigquery", "google-cloud-bigquery")
+
+    def write_mongo(self, *a, **k):
+        self._absent("write_mongo", "pymongo")
+
+    def write_datasource(self, datasource, *, ray_remote_args=None, **write_args):
+        """Legacy write API (reference ``write_datasource``, superseded by ``write_datasink``): a
+        datasource object with ``write(blocks, ctx, **write_args)`` (and optional
+        ``on_write_complete`` / ``on_write_failed``) receives the blocks, one write task per block."""
+        from .._private.worker import get
+        from ..remote_function import RemoteFunction
+
+        def _write_one(block, i):
+            return datasource.write([block], {"task_idx": i}, **write_args)
+
+        rf = RemoteFunction(_write_one, dict(ray_remote_args or {}, num_cpus=(ray_remote_args or {}).get("num_cpus", 1)))
+        try:
+            results = get([rf.remote(b, i) for i, (b, _) in enumerate(self._iter_refs())])
+        except Exception as e:
+            if hasattr(datasource, "on_write_failed"):
+                datasource.on_write_failed([], e)
+            raise
+        if hasattr(datasource, "on_write_complete"):
+            datasource.on_write_complete(results)
+        return results
+
     # ------------------------------------------------------------------ aggregations
     def aggregate(self, *aggs):
         return self.groupby(None).aggregate(*aggs).take(1)[0]

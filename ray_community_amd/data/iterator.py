@@ -114,7 +114,34 @@ class DataIterator:
             yield out
 
     def to_tf(self, *a, **k):  # pragma: no cover
-        raise NotImplementedError("TensorFlow is not supported on this platform")
+        raise ImportError("DataIterator.to_tf needs TensorFlow, which is not installed in this MI355X image")
+
+    def iter_tf_batches(self, *a, **k):  # pragma: no cover
+        raise ImportError("DataIterator.iter_tf_batches needs TensorFlow, which is not installed in this MI355X image")
+
+    def schema(self):
+        """Schema of the underlying dataset (reference ``DataIterator.schema``)."""
+        ds = self._ds
+        return ds.schema() if hasattr(ds, "schema") else None
+
+    def to_torch(self, *, label_column=None, feature_columns=None, batch_size: int = 1, **kw):
+        """A ``torch.utils.data.IterableDataset`` over this iterator's batches: ``(features,
+        label)`` tensors with ``label_column``, else the batch dicts (reference ``to_torch``)."""
+        import torch
+
+        it = self
+
+        class _It(torch.utils.data.IterableDataset):
+            def __iter__(_s):
+                for b in it.iter_torch_batches(batch_size=batch_size):
+                    if label_column:
+                        y = b.pop(label_column)
+                        cols = feature_columns or list(b)
+                        yield torch.stack([b[c].float() for c in cols], dim=1), y
+                    else:
+                        yield b
+
+        return _It()
 
     def materialize(self):
         return self._ds.materialize()
