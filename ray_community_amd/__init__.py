@@ -102,7 +102,35 @@ class ClientBuilder:
 
 
 _LAZY = {"util", "train", "tune", "data", "serve", "rllib", "dag", "air", "experimental", "models", "ops", "parallel",
-         "cluster_utils", "job_submission", "workflow", "runtime_env", "autoscaler", "utils", "job_config", "scripts"}
+         "cluster_utils", "job_submission", "workflow", "runtime_env", "autoscaler", "utils", "job_config", "scripts",
+         "internal", "widgets"}
+
+
+class _SystemConfig:
+    """``ray._config`` (reference: the raylet's ``Config`` object): read-only access to the
+    session's ``_system_config`` values by attribute (``ray._config.object_spilling_threshold()``
+    style calls return the value)."""
+
+    def _values(self):
+        try:
+            from ._private.worker import _state
+
+            head = _state.get("head")
+            return dict(getattr(head, "config", {}) or {}) if head is not None else {}
+        except Exception:
+            return {}
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        vals = self._values()
+        if name not in vals:
+            raise AttributeError(f"system config has no entry {name!r}")
+        v = vals[name]
+        return lambda: v
+
+
+_config = _SystemConfig()
 
 
 def __getattr__(name):

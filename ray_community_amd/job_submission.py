@@ -65,6 +65,15 @@ class JobInfo:
 JobDetails = JobInfo
 
 
+@dataclasses.dataclass
+class DriverInfo:
+    """The driver process of a job (reference ``dashboard/modules/job/pydantic_models.py``
+    ``DriverInfo``): its job id, the node address it runs on and its pid."""
+    id: str
+    node_ip_address: str
+    pid: str
+
+
 class JobManager:
     """Detached actor owning the job processes."""
 
@@ -350,4 +359,4 @@ class JobSubmissionClient:
         raise TimeoutError(f"job {job_id} did not finish in {timeout_s}s")
 
 
-__all__ = ["JobSubmissionClient", "JobStatus", "JobInfo", "JobDetails", "JobType"]
+__all__ = ["JobSubmissionClient", "JobStatus", "JobInfo", "JobDetails", "JobType", "DriverInfo"]

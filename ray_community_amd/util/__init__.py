@@ -49,7 +49,7 @@ def __getattr__(name):
     import importlib
 
     if name in ("collective", "queue", "actor_pool", "multiprocessing", "metrics", "state", "iter", "serialization",
-                "annotations", "timer", "tracing", "accelerators", "pdb", "debug", "client"):
+                "annotations", "timer", "tracing", "accelerators", "pdb", "debug", "client", "ray_debugpy"):
         return importlib.import_module("." + name, __name__)
     if name == "ActorPool":
         from .actor_pool import ActorPool

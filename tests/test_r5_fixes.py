@@ -197,3 +197,23 @@ def test_direct_call_pins_released_when_caller_dies(shutdown_only):
             break
         time.sleep(0.1)
     assert not left, left
+
+
+def test_remaining_top_level_api_names(shutdown_only):
+    """ray.internal (free / memory_summary), ray.widgets, ray._config, ray.util.ray_debugpy,
+    ray.job_submission.DriverInfo: the last names of the reference's public __all__ lists."""
+    ray.init(num_cpus=1, include_dashboard=False, log_to_driver=False)
+    import numpy as np
+
+    big = ray.put(np.zeros(200_000))
+    s = ray.internal.memory_summary()
+    assert "Objects:" in s and big.hex()[:16] in s.replace("-", "")
+    ray.internal.free([big])
+    assert "<table>" in ray.widgets.make_table_html_repr({"a": 1}, title="t")
+    assert ray.widgets.Template("{{ x }}!").render(x=3) == "3!"
+    assert callable(ray.util.ray_debugpy.set_trace)
+    from ray_community_amd.job_submission import DriverInfo
+
+    assert DriverInfo(id="j", node_ip_address="127.0.0.1", pid="1").pid == "1"
+    with pytest.raises(AttributeError):
+        ray._config.not_a_config_entry()
