@@ -622,6 +622,160 @@ class Algorithm(Trainable):
     def iteration(self):
         return self._iteration
 
+    # ------------------------------------------------------------------ reference API surface
+    @classmethod
+    def get_default_config(cls):
+        return cls._default_config_cls()
+
+    def get_default_policy_class(self, config=None):
+        """Old-API-stack policy class of this algorithm: the torch policy view over its RLModule."""
+        from ..policy.policy import TorchPolicy
+
+        return TorchPolicy
+
+    @staticmethod
+    def validate_env(env, env_context=None) -> None:
+        """An env must expose observation and action spaces (reference hook; algorithms override)."""
+        if env is None:
+            return
+        if getattr(env, "observation_space", None) is None or getattr(env, "action_space", None) is None:
+            raise ValueError(f"env {env!r} has no observation_space / action_space")
+
+    def validate_config(self, config=None) -> None:
+        (config or self.config).validate()
+
+    @classmethod
+    def merge_algorithm_configs(cls, config1, config2, _allow_unknown_configs=None) -> Dict:
+        """Deep-merge two config dicts (``config2`` wins; nested dicts merge key by key)."""
+        def to_d(c):
+            return c.to_dict() if isinstance(c, AlgorithmConfig) else dict(c or {})
+
+        def merge(a, b):
+            out = dict(a)
+            for k, v in b.items():
+                out[k] = merge(out[k], v) if isinstance(out.get(k), dict) and isinstance(v, dict) else v
+            return out
+
+        base, over = to_d(config1), to_d(config2)
+        if _allow_unknown_configs is False:
+            unknown = set(over) - set(base)
+            if unknown:
+                raise KeyError(f"unknown config keys {sorted(unknown)}")
+        return merge(base, over)
+
+    @classmethod
+    def default_resource_request(cls, config):
+        """The placement group one trial of this algorithm needs under Tune: the driver (plus its
+        GPU when it trains locally), one bundle per env runner, one per GPU learner."""
+        from ...tune import PlacementGroupFactory
+
+        c = config if isinstance(config, AlgorithmConfig) else cls._default_config_cls().update_from_dict(dict(config))
+        n_learn = int(c.num_learners)
+        head = {"CPU": 1.0}
+        if n_learn == 0 and float(c.num_gpus or 0) > 0:
+            head["GPU"] = float(c.num_gpus)
+        bundles = [head]
+        for _ in range(int(c.num_env_runners)):
+            b = {"CPU": float(c.num_cpus_per_env_runner)}
+            if float(c.num_gpus_per_env_runner or 0) > 0:
+                b["GPU"] = float(c.num_gpus_per_env_runner)
+            bundles.append(b)
+        for _ in range(n_learn):
+            b = {"CPU": 1.0}
+            if float(c.num_gpus_per_learner or 0) > 0:
+                b["GPU"] = float(c.num_gpus_per_learner)
+            bundles.append(b)
+        return PlacementGroupFactory(bundles, strategy="PACK")
+
+    @classmethod
+    def resource_help(cls, config) -> str:
+        return ("\n\nYou can adjust the resource requests of RLlib Algorithms by calling "
+                "`AlgorithmConfig.env_runners(num_env_runners=.., num_cpus_per_env_runner=.., "
+                "num_gpus_per_env_runner=..)` and `AlgorithmConfig.learners(num_learners=.., "
+                "num_gpus_per_learner=..)`. This trial asks for "
+                f"{cls.default_resource_request(config).bundles}.")
+
+    def get_auto_filled_metrics(self, now=None, time_this_iter=None, timestamp=None, debug_metrics_only=False) -> Dict:
+        import datetime
+
+        now = now or datetime.datetime.now()
+        out = {"training_iteration": self._iteration, "timesteps_total": self._timesteps_total,
+               "episodes_total": self._episodes_total}
+        if not debug_metrics_only:
+            out.update({"date": now.strftime("%Y-%m-%d_%H-%M-%S"), "timestamp": int(timestamp or time.time()),
+                        "time_this_iter_s": time_this_iter, "pid": os.getpid()})
+        return out
+
+    def log_result(self, result: Dict) -> None:
+        """Record a result dict (reference: Trainable.log_result, after the callbacks saw it)."""
+        self._last_result = dict(result)
+
+    def get_state(self) -> Dict:
+        """Learner states, counters and the config: everything ``from_state`` / ``set_state`` need."""
+        if self.multi_agent:
+            learner = {p: g.call("get_state") for p, g in self.learner_groups.items()}
+        else:
+            learner = self.learner_group.call("get_state")
+        return {"learner": learner, "iteration": self._iteration, "multi_agent": self.multi_agent,
+                "timesteps_total": self._timesteps_total, "config": self.config.to_dict(),
+                "algorithm_class": type(self), "extra": self._extra_state()}
+
+    def set_state(self, state: Dict) -> None:
+        if state.get("multi_agent"):
+            for p, ls in state["learner"].items():
+                if p in self.learner_groups:
+                    self.learner_groups[p].call("set_state", ls)
+        else:
+            self.learner_group.call("set_state", state["learner"])
+        self._iteration = state.get("iteration", self._iteration)
+        self._timesteps_total = state.get("timesteps_total", self._timesteps_total)
+        self._load_extra_state(state.get("extra") or {})
+        self._sync_weights()
+
+    @staticmethod
+    def from_state(state: Dict) -> "Algorithm":
+        """A new Algorithm built from ``get_state()`` output (class, config, weights, counters)."""
+        cls = state.get("algorithm_class")
+        if cls is None:
+            raise ValueError("state has no algorithm_class")
+        algo = cls(config=cls._default_config_cls().update_from_dict(state["config"]))
+        algo.set_state(state)
+        return algo
+
+    def export_policy_checkpoint(self, export_dir: str, policy_id=None) -> str:
+        """A policy checkpoint: the module's weights (``policy_state.pt``, ``weights_only``-loadable)
+        plus its spaces / config summary (``policy_info.json``)."""
+        os.makedirs(export_dir, exist_ok=True)
+        m = self.get_module(policy_id)
+        torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, os.path.join(export_dir, "policy_state.pt"))
+        info = {"policy_id": policy_id or "default_policy", "module_class": type(m).__name__,
+                "algorithm": type(self).__name__, "model": self.config.model}
+        with open(os.path.join(export_dir, "policy_info.json"), "w") as f:
+            json.dump(info, f, default=str)
+        with open(os.path.join(export_dir, "rllib_checkpoint.json"), "w") as f:
+            json.dump({"type": "Policy", "format": "rca-1"}, f)
+        return export_dir
+
+    def import_model(self, import_file: str):
+        """Load policy weights exported by ``export_policy_model`` / ``export_policy_checkpoint``
+        (``model.pt`` / ``policy_state.pt``; Keras h5 files are TensorFlow-only)."""
+        if str(import_file).endswith(".h5"):
+            return self.import_policy_model_from_h5(import_file)
+        path = import_file
+        if os.path.isdir(path):
+            for name in ("policy_state.pt", "model.pt"):
+                if os.path.exists(os.path.join(path, name)):
+                    path = os.path.join(path, name)
+                    break
+        sd = torch.load(path, weights_only=True)
+        m = self.get_module()
+        m.load_state_dict(sd)
+        self.set_weights(m.get_state() if hasattr(m, "get_state") else {k: v for k, v in sd.items()})
+
+    def import_policy_model_from_h5(self, import_file: str, policy_id=None):
+        raise NotImplementedError("Keras .h5 policy models are TensorFlow-only; export/import torch "
+                                  "state_dicts with export_policy_model / import_model")
+
 
 class _SaveResult:
     def __init__(self, checkpoint):

@@ -81,6 +81,20 @@ class DefaultCallbacks:
     def on_sample_end(self, *, env_runner=None, samples=None, **kwargs) -> None:
         pass
 
+    def on_create_policy(self, *, policy_id, policy, **kwargs) -> None:
+        """A policy was created (add_policy / multi-agent setup)."""
+
+    def on_episode_created(self, *, episode, env_runner=None, env_index: int = 0, env=None, **kwargs) -> None:
+        """A new episode object exists, before its first reset observation."""
+
+    def on_postprocess_trajectory(self, *, episode=None, agent_id=None, policy_id=None, policies=None,
+                                  postprocessed_batch=None, original_batches=None, **kwargs) -> None:
+        """A trajectory's batch was post-processed (advantages etc.); may edit it in place."""
+
+    def on_sub_environment_created(self, *, worker=None, sub_environment=None, env_context=None, env_index=None,
+                                   **kwargs) -> None:
+        """One sub-environment of a vectorised env was created."""
+
     def on_learn_on_batch(self, *, policy=None, train_batch=None, result=None, **kwargs) -> None:
         pass
 

@@ -42,6 +42,100 @@ class MultiAgentEnv:
     def close(self):
         pass
 
+    # reference MultiAgentEnv helpers (rllib/env/multi_agent_env.py)
+    def get_agent_ids(self) -> set:
+        return set(self.possible_agents or self.agents or self.observation_spaces or ())
+
+    def observation_space_sample(self, agent_ids=None) -> Dict:
+        ids = agent_ids if agent_ids is not None else self.get_agent_ids()
+        return {a: self.get_observation_space(a).sample() for a in ids}
+
+    def action_space_sample(self, agent_ids=None) -> Dict:
+        ids = agent_ids if agent_ids is not None else self.get_agent_ids()
+        return {a: self.get_action_space(a).sample() for a in ids}
+
+    def observation_space_contains(self, x: Dict) -> bool:
+        return isinstance(x, dict) and all(self.get_observation_space(a).contains(v) for a, v in x.items())
+
+    def action_space_contains(self, x: Dict) -> bool:
+        return isinstance(x, dict) and all(self.get_action_space(a).contains(v) for a, v in x.items())
+
+    def render(self):
+        return None
+
+    def with_agent_groups(self, groups: Dict, obs_space=None, act_space=None) -> "MultiAgentEnv":
+        """Agents grouped into super-agents (reference ``with_agent_groups``): group id -> list of
+        agent ids; a group observes / acts with the tuple of its members' observations / actions
+        and receives the sum of their rewards."""
+        return _GroupedAgents(self, groups, obs_space, act_space)
+
+    def to_base_env(self, make_env=None, num_envs: int = 1, remote_envs: bool = False,
+                    remote_env_batch_wait_ms: int = 0, restart_failed_sub_environments: bool = False):
+        from .base_env import convert_to_base_env
+
+        return convert_to_base_env(self, make_env=make_env, num_envs=num_envs)
+
+
+class _GroupedAgents(MultiAgentEnv):
+    def __init__(self, env: MultiAgentEnv, groups: Dict, obs_space=None, act_space=None):
+        self.env = env
+        self.groups = {g: list(m) for g, m in groups.items()}
+        grouped = {a for m in self.groups.values() for a in m}
+        self._single = [a for a in env.get_agent_ids() if a not in grouped]
+        self.possible_agents = list(self.groups) + self._single
+        self.agents = list(self.possible_agents)
+        self._obs_space, self._act_space = obs_space, act_space
+
+    def get_observation_space(self, agent_id):
+        if agent_id in self.groups:
+            if self._obs_space is not None:
+                return self._obs_space
+            from ..utils.spaces import Tuple as _Tuple
+
+            return _Tuple([self.env.get_observation_space(a) for a in self.groups[agent_id]])
+        return self.env.get_observation_space(agent_id)
+
+    def get_action_space(self, agent_id):
+        if agent_id in self.groups:
+            if self._act_space is not None:
+                return self._act_space
+            from ..utils.spaces import Tuple as _Tuple
+
+            return _Tuple([self.env.get_action_space(a) for a in self.groups[agent_id]])
+        return self.env.get_action_space(agent_id)
+
+    def _group_dict(self, d, reduce=None):
+        out = {}
+        for g, members in self.groups.items():
+            vals = [d[a] for a in members if a in d]
+            if vals:
+                out[g] = reduce(vals) if reduce else tuple(vals)
+        for a in self._single:
+            if a in d:
+                out[a] = d[a]
+        return out
+
+    def reset(self, *, seed=None, options=None):
+        obs, infos = self.env.reset(seed=seed, options=options)
+        return self._group_dict(obs), self._group_dict(infos, reduce=lambda v: v[0])
+
+    def step(self, action_dict):
+        flat = {}
+        for k, a in action_dict.items():
+            if k in self.groups:
+                for member, act in zip(self.groups[k], a):
+                    flat[member] = act
+            else:
+                flat[k] = a
+        obs, rew, term, trunc, infos = self.env.step(flat)
+        o = self._group_dict(obs)
+        r = self._group_dict(rew, reduce=lambda v: float(sum(v)))
+        te = self._group_dict({k: v for k, v in term.items() if k != "__all__"}, reduce=all)
+        tr = self._group_dict({k: v for k, v in trunc.items() if k != "__all__"}, reduce=all)
+        te["__all__"] = term.get("__all__", False)
+        tr["__all__"] = trunc.get("__all__", False)
+        return o, r, te, tr, self._group_dict(infos, reduce=lambda v: v[0])
+
 
 def make_multi_agent(env_name_or_creator: Union[str, Callable]) -> Callable[[Optional[dict]], MultiAgentEnv]:
     """Class factory: ``make_multi_agent("CartPole-v1")({"num_agents": 2})`` -> an env whose agents

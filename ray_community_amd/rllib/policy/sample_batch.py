@@ -75,7 +75,9 @@ class SampleBatch(dict):
     def __getitem__(self, key):
         if isinstance(key, slice):
             return self.slice(key.start or 0, key.stop if key.stop is not None else self.count)
-        return dict.__getitem__(self, key)
+        v = dict.__getitem__(self, key)
+        f = self._get_interceptor
+        return f(v) if f is not None else v
 
     def shuffle(self, rng=None) -> "SampleBatch":
         n = self.count
@@ -117,6 +119,161 @@ class SampleBatch(dict):
 
     def as_multi_agent(self, policy_id="default_policy"):
         return MultiAgentBatch({policy_id: self}, self.count)
+
+    # ------------------------------------------------------------------ reference API surface
+    # (rllib/policy/sample_batch.py: columns / rows / concat / split_by_episode / right_zero_pad /
+    # compress / training flag / single-step input dicts)
+    is_training = False
+    zero_padded = False
+    max_seq_len = None
+    _slice_by_batch_id = False
+    _get_interceptor = None
+
+    def set_training(self, training: bool = True):
+        self.is_training = bool(training)
+        return self
+
+    def columns(self, keys) -> List:
+        return [self[k] for k in keys]
+
+    def rows(self) -> Iterator[Dict]:
+        """One dict per timestep (flattened fragment blocks; seq_lens and state columns skipped)."""
+        flat = self.flatten()
+        n = flat.count
+        keys = [k for k in flat if k != SampleBatch.SEQ_LENS and not str(k).startswith("state_in")]
+        for i in range(n):
+            yield {k: flat[k][i] for k in keys}
+
+    def size_bytes(self) -> int:
+        tot = 0
+        for v in self.values():
+            if hasattr(v, "nbytes"):
+                tot += int(v.nbytes)
+            elif hasattr(v, "element_size"):
+                tot += int(v.element_size() * v.numel())
+        return tot
+
+    def concat(self, other: "SampleBatch") -> "SampleBatch":
+        return concat_samples([self, other])
+
+    concat_samples = staticmethod(lambda batches: concat_samples(batches))
+
+    def is_terminated_or_truncated(self) -> bool:
+        flat = self.flatten()
+        if flat.count == 0:
+            return False
+        for k in (SampleBatch.TERMINATEDS, SampleBatch.TRUNCATEDS, SampleBatch.DONES):
+            if k in flat and bool(np.asarray(flat[k])[-1]):
+                return True
+        return False
+
+    def is_single_trajectory(self) -> bool:
+        """One episode (or a chunk of one): a single eps_id and no episode end before the last row."""
+        flat = self.flatten()
+        if SampleBatch.EPS_ID in flat and len(np.unique(np.asarray(flat[SampleBatch.EPS_ID]))) > 1:
+            return False
+        ends = np.zeros(flat.count, bool)
+        for k in (SampleBatch.TERMINATEDS, SampleBatch.TRUNCATEDS, SampleBatch.DONES):
+            if k in flat:
+                ends |= np.asarray(flat[k], bool)
+        return not ends[:-1].any()
+
+    def split_by_episode(self, key: Optional[str] = None) -> List["SampleBatch"]:
+        """Consecutive rows of one episode per batch: on changes of ``eps_id`` (or of ``key``), else
+        after every terminated / truncated row."""
+        flat = self.flatten()
+        n = flat.count
+        if n == 0:
+            return []
+        col = key or (SampleBatch.EPS_ID if SampleBatch.EPS_ID in flat else None)
+        if col is not None and col in flat:
+            ids = np.asarray(flat[col])
+            cuts = list(np.nonzero(ids[1:] != ids[:-1])[0] + 1)
+        else:
+            ends = np.zeros(n, bool)
+            for k in (SampleBatch.TERMINATEDS, SampleBatch.TRUNCATEDS, SampleBatch.DONES):
+                if k in flat:
+                    ends |= np.asarray(flat[k], bool)
+            cuts = list(np.nonzero(ends[:-1])[0] + 1)
+        bounds = [0] + cuts + [n]
+        return [flat.slice(a, b) for a, b in zip(bounds[:-1], bounds[1:])]
+
+    def right_zero_pad(self, max_seq_len: int, exclude_states: bool = True) -> "SampleBatch":
+        """In place: every sequence (``seq_lens``) padded with zeros at its end to ``max_seq_len``
+        rows; ``state_in_*`` columns (one row per sequence) stay as they are unless
+        ``exclude_states=False``."""
+        seq_lens = self.get(SampleBatch.SEQ_LENS)
+        if seq_lens is None:
+            raise ValueError("Cannot right-zero-pad a SampleBatch without a `seq_lens` column")
+        lens = np.asarray(seq_lens, dtype=np.int64)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        for k in list(self.keys()):
+            if k == SampleBatch.SEQ_LENS or (exclude_states and str(k).startswith("state_in")):
+                continue
+            v = self[k]
+            if isinstance(v, list):
+                v = np.asarray(v)
+            if not hasattr(v, "shape") or v.shape[:1] != (int(lens.sum()),):
+                continue
+            out = np.zeros((len(lens) * max_seq_len,) + tuple(v.shape[1:]), dtype=v.dtype)
+            for i, (s0, ln) in enumerate(zip(starts, lens)):
+                out[i * max_seq_len: i * max_seq_len + ln] = v[s0: s0 + ln]
+            self[k] = out
+        self.zero_padded = True
+        self.max_seq_len = int(max_seq_len)
+        return self
+
+    zero_pad = right_zero_pad
+
+    def compress(self, bulk: bool = False, columns=frozenset(["obs", "new_obs"])) -> "SampleBatch":
+        """In place: the given columns become zlib-compressed bytes (one blob per column with
+        ``bulk``, else one per row), restored by ``decompress_if_needed``."""
+        import pickle
+        import zlib
+
+        for k in columns:
+            if k in self and isinstance(self[k], np.ndarray):
+                v = self[k]
+                if bulk:
+                    self[k] = {"__zlib__": zlib.compress(pickle.dumps(v, protocol=5), 1)}
+                else:
+                    self[k] = np.array([zlib.compress(pickle.dumps(r, protocol=5), 1) for r in v], dtype=object)
+        return self
+
+    def decompress_if_needed(self, columns=frozenset(["obs", "new_obs"])) -> "SampleBatch":
+        import pickle
+        import zlib
+
+        for k in columns:
+            if k not in self:
+                continue
+            v = self[k]
+            if isinstance(v, dict) and "__zlib__" in v:
+                self[k] = pickle.loads(zlib.decompress(v["__zlib__"]))
+            elif isinstance(v, np.ndarray) and v.dtype == object and len(v) and isinstance(v[0], bytes):
+                self[k] = np.stack([pickle.loads(zlib.decompress(r)) for r in v])
+        return self
+
+    def get_single_step_input_dict(self, view_requirements=None, index="last") -> "SampleBatch":
+        """A batch of one row (the last, or ``index``) with ``obs`` taken from that row's
+        ``new_obs``: the input of the next forward pass after this trajectory."""
+        flat = self.flatten()
+        i = flat.count - 1 if index == "last" else int(index)
+        out = SampleBatch({k: flat[k][i: i + 1] for k in flat if hasattr(flat[k], "shape") and k != SampleBatch.SEQ_LENS})
+        if SampleBatch.NEXT_OBS in flat and index == "last":
+            out[SampleBatch.OBS] = flat[SampleBatch.NEXT_OBS][i: i + 1]
+        return out
+
+    def enable_slicing_by_batch_id(self):
+        self._slice_by_batch_id = True
+
+    def disable_slicing_by_batch_id(self):
+        self._slice_by_batch_id = False
+
+    def set_get_interceptor(self, fn):
+        """``fn(value)`` is applied to every column read through ``[key]`` (e.g. to move it to a
+        device lazily)."""
+        self._get_interceptor = fn
 
 
 def _to_index(idx, v):

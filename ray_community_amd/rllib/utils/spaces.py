@@ -64,3 +64,53 @@ class Box(Space):
 
     def __repr__(self):
         return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+
+class Tuple(Space):
+    """A tuple of spaces (grouped agents' observations / actions)."""
+
+    def __init__(self, spaces: Sequence[Space]):
+        self.spaces = tuple(spaces)
+        self.shape = None
+        self.dtype = None
+
+    def sample(self):
+        return tuple(s.sample() for s in self.spaces)
+
+    def contains(self, x) -> bool:
+        return isinstance(x, (tuple, list)) and len(x) == len(self.spaces) and all(
+            s.contains(v) for s, v in zip(self.spaces, x))
+
+    def __len__(self):
+        return len(self.spaces)
+
+    def __getitem__(self, i):
+        return self.spaces[i]
+
+    def __repr__(self):
+        return "Tuple(" + ", ".join(repr(s) for s in self.spaces) + ")"
+
+    def __eq__(self, o):
+        return isinstance(o, Tuple) and o.spaces == self.spaces
+
+
+class Dict(Space):
+    """A dict of named spaces."""
+
+    def __init__(self, spaces=None, **kw):
+        self.spaces = dict(spaces or {}, **kw)
+        self.shape = None
+        self.dtype = None
+
+    def sample(self):
+        return {k: s.sample() for k, s in self.spaces.items()}
+
+    def contains(self, x) -> bool:
+        return isinstance(x, dict) and set(x) == set(self.spaces) and all(
+            self.spaces[k].contains(v) for k, v in x.items())
+
+    def __getitem__(self, k):
+        return self.spaces[k]
+
+    def __repr__(self):
+        return "Dict(" + ", ".join(f"{k}: {s!r}" for k, s in self.spaces.items()) + ")"

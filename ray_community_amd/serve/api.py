@@ -43,6 +43,52 @@ class Deployment:
     def max_ongoing_requests(self):
         return self._config.get("max_ongoing_requests", 5)
 
+    @property
+    def max_concurrent_queries(self):  # the pre-2.10 name of max_ongoing_requests
+        return self.max_ongoing_requests
+
+    @property
+    def max_queued_requests(self):
+        return self._config.get("max_queued_requests", -1)
+
+    @property
+    def version(self):
+        return self._config.get("version")
+
+    @property
+    def ray_actor_options(self):
+        return self._config.get("ray_actor_options")
+
+    @property
+    def route_prefix(self):
+        return self._config.get("route_prefix")
+
+    @property
+    def url(self):
+        """HTTP URL of an ingress deployment, None without a route prefix (reference ``url``)."""
+        rp = self.route_prefix
+        if rp is None:
+            return None
+        from ._private import proxy
+
+        host, port = getattr(proxy, "DEFAULT_HTTP_HOST", "127.0.0.1"), getattr(proxy, "DEFAULT_HTTP_PORT", 8000)
+        return f"http://{host}:{port}{rp}"
+
+    @property
+    def init_args(self):
+        return tuple(self._config.get("init_args") or ())
+
+    @property
+    def init_kwargs(self):
+        return dict(self._config.get("init_kwargs") or {})
+
+    @property
+    def logging_config(self):
+        return self._config.get("logging_config")
+
+    def set_logging_config(self, logging_config) -> None:
+        self._config["logging_config"] = logging_config
+
     def options(self, **kw) -> "Deployment":
         bad = set(kw) - _DEP_OPTS
         if bad:
@@ -177,7 +223,8 @@ def deployment(_func_or_class=None, *, name: Optional[str] = None, num_replicas:
                                  placement_group_bundles=placement_group_bundles,
                                  placement_group_strategy=placement_group_strategy,
                                  max_replicas_per_node=max_replicas_per_node,
-                                 logging_config=logging_config).items()
+                                 logging_config=logging_config, version=version,
+                                 route_prefix=route_prefix).items()
            if v is not None}
     _placement_options(cfg)  # validate at decoration time, as the reference does
     if num_replicas is not None and autoscaling_config is not None and num_replicas != "auto":

@@ -41,6 +41,15 @@ class BaseTrainer:
     def fit(self) -> Result:
         raise NotImplementedError
 
+    def preprocess_datasets(self) -> None:
+        """Deprecated in the reference (preprocessors are applied to datasets before passing them
+        in); kept as a no-op hook that subclasses may still override."""
+
+    def training_loop(self) -> None:
+        """The trainer's main loop (reference: the method ``fit`` runs inside its Tune trial);
+        here ``fit`` drives the worker group directly, so this runs it and keeps the result."""
+        self._training_loop_result = self.fit()
+
     def as_trainable(self):
         trainer = self
 

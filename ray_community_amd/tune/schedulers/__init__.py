@@ -38,6 +38,32 @@ class TrialScheduler:
     def on_trial_add(self, controller, trial):
         pass
 
+    supports_buffered_results = True
+
+    def debug_string(self) -> str:
+        return f"Using {type(self).__name__} (metric={self.metric!r}, mode={self.mode!r})."
+
+    def save(self, checkpoint_path: str) -> None:
+        import pickle
+
+        import cloudpickle
+
+        state = {}
+        for k, v in self.__dict__.items():
+            try:
+                cloudpickle.dumps(v)
+            except Exception:
+                continue
+            state[k] = v
+        with open(checkpoint_path, "wb") as f:
+            cloudpickle.dump(state, f)
+
+    def restore(self, checkpoint_path: str) -> None:
+        import pickle
+
+        with open(checkpoint_path, "rb") as f:  # a file this framework's save() wrote
+            self.__dict__.update(pickle.load(f))
+
     def on_trial_result(self, controller, trial, result) -> str:
         return TrialScheduler.CONTINUE
 

@@ -71,10 +71,76 @@ class Searcher:
         pass
 
     def save(self, path):
-        pass
+        """Pickle ``get_state()`` to ``path`` (searchers with extra state override get/set_state)."""
+        import pickle
+
+        import cloudpickle
+
+        with open(path, "wb") as f:
+            cloudpickle.dump(self.get_state(), f)
 
     def restore(self, path):
-        pass
+        import pickle
+
+        with open(path, "rb") as f:  # a file this framework's save() wrote
+            self.set_state(pickle.load(f))
+
+    def get_state(self) -> Dict:
+        """The searcher's picklable attributes (modules, locks and the like are left out)."""
+        import cloudpickle
+
+        out = {}
+        for k, v in self.__dict__.items():
+            try:
+                cloudpickle.dumps(v)
+            except Exception:
+                continue
+            out[k] = v
+        return out
+
+    def set_state(self, state: Dict) -> None:
+        self.__dict__.update(state)
+
+    CKPT_FILE_TMPL = "searcher-state-{}.pkl"
+
+    def save_to_dir(self, checkpoint_dir: str, session_str: str = "default") -> None:
+        import os
+
+        self.save(os.path.join(checkpoint_dir, self.CKPT_FILE_TMPL.format(session_str)))
+
+    def restore_from_dir(self, checkpoint_dir: str) -> None:
+        import glob
+        import os
+
+        files = sorted(glob.glob(os.path.join(checkpoint_dir, self.CKPT_FILE_TMPL.format("*"))))
+        if not files:
+            raise RuntimeError(f"no searcher checkpoint in {checkpoint_dir}")
+        self.restore(files[-1])
+
+    def set_max_concurrency(self, max_concurrent: int) -> bool:
+        """Searchers that limit concurrency themselves return True (the default lets a
+        ConcurrencyLimiter wrap them)."""
+        return False
+
+    def add_evaluated_point(self, parameters: Dict, value: float, error: bool = False, pruned: bool = False,
+                            intermediate_values=None) -> None:
+        """Seed the searcher with a finished evaluation (reference API). Searchers that learn from
+        history override this; the base records it and replays it as a completed trial."""
+        import uuid
+
+        tid = "evaluated_" + uuid.uuid4().hex[:8]
+        self._evaluated = getattr(self, "_evaluated", []) + [(dict(parameters), value)]
+        self.on_trial_complete(tid, result={**dict(parameters), **({self._metric: value} if self._metric else {}),
+                                            "config": dict(parameters)}, error=error)
+
+    def add_evaluated_trials(self, trials_or_analysis, metric: str) -> None:
+        """Seed from finished trials / a ResultGrid: each result's config and ``metric``."""
+        items = list(trials_or_analysis)
+        for t in items:
+            cfg = getattr(t, "config", None) or {}
+            res = getattr(t, "metrics", None) or getattr(t, "last_result", None) or {}
+            if metric in res:
+                self.add_evaluated_point(cfg, res[metric])
 
 
 def generate_variants(spec: Dict, num_samples: int = 1, rng=None) -> List[Dict]:

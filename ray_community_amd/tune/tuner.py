@@ -101,6 +101,127 @@ class Trainable:
     def training_iteration(self):
         return self._iteration
 
+    # ------------------------------------------------------------------ direct-use API
+    # (reference python/ray/tune/trainable/trainable.py: a class trainable can also be driven by
+    # hand -- train / save / restore / reset / stop -- outside a Tuner)
+    def get_config(self) -> Dict:
+        return self.config
+
+    def get_current_ip_pid(self):
+        from ..util import get_node_ip_address
+
+        return get_node_ip_address(), os.getpid()
+
+    def is_actor(self) -> bool:
+        return bool(os.environ.get("RCA_WORKER_ID"))
+
+    @property
+    def trial_resources(self):
+        return self._info().get("resources")
+
+    @classmethod
+    def default_resource_request(cls, config):
+        return None
+
+    @classmethod
+    def resource_help(cls, config) -> str:
+        return ""
+
+    def get_auto_filled_metrics(self, now=None, time_this_iter=None, timestamp=None, debug_metrics_only=False) -> Dict:
+        out = {"training_iteration": self._iteration, "trial_id": self.trial_id}
+        if not debug_metrics_only:
+            out.update({"time_this_iter_s": time_this_iter, "timestamp": int(timestamp or time.time()),
+                        "time_total_s": getattr(self, "_time_total", 0.0), "pid": os.getpid()})
+        return out
+
+    def log_result(self, result: Dict) -> None:
+        self._last_result = dict(result)
+
+    def train(self) -> Dict:
+        """One ``step()`` with the auto-filled fields (training_iteration, timings, done)."""
+        t0 = time.time()
+        result = self.step()
+        if not isinstance(result, dict):
+            raise ValueError(f"step() must return a dict, got {type(result).__name__}")
+        dt = time.time() - t0
+        self._iteration += 1
+        self._time_total = getattr(self, "_time_total", 0.0) + dt
+        result = dict(result)
+        result.setdefault("done", False)
+        result.update(self.get_auto_filled_metrics(time_this_iter=dt))
+        self.log_result(result)
+        return result
+
+    def train_buffered(self, buffer_time_s: float, max_buffer_length: int = 1000) -> List[Dict]:
+        out, t0 = [], time.time()
+        while len(out) < max_buffer_length and (not out or time.time() - t0 < buffer_time_s):
+            r = self.train()
+            out.append(r)
+            if r.get("done"):
+                break
+        return out
+
+    def get_state(self) -> Dict:
+        return {"iteration": self._iteration, "time_total": getattr(self, "_time_total", 0.0),
+                "config": self.config}
+
+    def save(self, checkpoint_dir: Optional[str] = None):
+        """``save_checkpoint`` into ``checkpoint_dir`` (a fresh temp dir by default); a returned dict
+        is stored next to the files. Returns the checkpoint."""
+        import pickle
+        import tempfile
+
+        from ..train._checkpoint import Checkpoint
+
+        d = checkpoint_dir or tempfile.mkdtemp(prefix=f"checkpoint_{self._iteration:06d}_")
+        os.makedirs(d, exist_ok=True)
+        state = self.save_checkpoint(d)
+        if isinstance(state, dict):
+            with open(os.path.join(d, "_rca_trainable_state.pkl"), "wb") as f:
+                pickle.dump(state, f)
+        with open(os.path.join(d, "_rca_trainable_meta.json"), "w") as f:
+            json.dump({"iteration": self._iteration, "time_total": getattr(self, "_time_total", 0.0)}, f)
+        return Checkpoint.from_directory(d)
+
+    def restore(self, checkpoint_path):
+        """Inverse of ``save``: ``load_checkpoint`` gets the saved dict (or the directory) and the
+        iteration counter is restored."""
+        import pickle
+
+        d = checkpoint_path if isinstance(checkpoint_path, str) else getattr(checkpoint_path, "path", checkpoint_path)
+        meta = os.path.join(d, "_rca_trainable_meta.json")
+        if os.path.exists(meta):
+            with open(meta) as f:
+                m = json.load(f)
+            self._iteration, self._time_total = int(m["iteration"]), float(m["time_total"])
+        st = os.path.join(d, "_rca_trainable_state.pkl")
+        if os.path.exists(st):
+            with open(st, "rb") as f:  # written by save() above, in this framework
+                self.load_checkpoint(pickle.load(f))
+        else:
+            self.load_checkpoint(d)
+
+    def reset(self, new_config, logger_creator=None, storage=None) -> bool:
+        """Reuse this instance for a new config (``reset_config``); counters restart."""
+        ok = self.reset_config(new_config)
+        if ok:
+            self.config = new_config
+            self._iteration = 0
+            self._time_total = 0.0
+        return ok
+
+    def stop(self) -> None:
+        self.cleanup()
+
+    def export_model(self, export_formats, export_dir: Optional[str] = None):
+        if isinstance(export_formats, str):
+            export_formats = [export_formats]
+        export_dir = export_dir or self.logdir or "."
+        return self._export_model(export_formats, export_dir)
+
+    def _export_model(self, export_formats, export_dir):
+        return {}
+
 
 class Stopper:
     def __call__(self, trial_id: str, result: Dict) -> bool:
@@ -251,6 +372,17 @@ class ResultGrid:
         self._metric = metric
         self._mode = mode
         self.experiment_path = experiment_path
+
+    @property
+    def filesystem(self):
+        """The filesystem the experiment lives on (local: ``pyarrow.fs.LocalFileSystem`` when
+        pyarrow is importable, else None)."""
+        try:
+            import pyarrow.fs as pafs
+
+            return pafs.LocalFileSystem()
+        except Exception:
+            return None
 
     def __len__(self):
         return len(self._results)
