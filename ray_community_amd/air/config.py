@@ -49,6 +49,22 @@ class ScalingConfig:
         bundles = [dict(self._resources_per_worker_not_none) for _ in range(self.num_workers or 1)]
         return {"bundles": bundles, "strategy": self.placement_strategy}
 
+    @classmethod
+    def from_placement_group_factory(cls, pgf) -> "ScalingConfig":
+        """Inverse of ``as_placement_group_factory``: bundles (or a PlacementGroupFactory) whose
+        first bundle may be the trainer's own and the rest identical worker bundles."""
+        bundles = list(getattr(pgf, "bundles", None) or (pgf.get("bundles") if isinstance(pgf, dict) else pgf))
+        strategy = getattr(pgf, "strategy", None) or (pgf.get("strategy") if isinstance(pgf, dict) else None) or "PACK"
+        if not bundles:
+            raise ValueError("placement group factory without bundles")
+        trainer = None
+        workers = bundles
+        if len(bundles) > 1 and bundles[0] != bundles[1]:
+            trainer, workers = bundles[0], bundles[1:]
+        w = dict(workers[0])
+        return cls(num_workers=len(workers), use_gpu=w.get("GPU", 0) > 0, resources_per_worker=w,
+                   placement_strategy=strategy, trainer_resources=trainer)
+
     @property
     def total_resources(self):
         out = {}
@@ -91,6 +107,10 @@ class RunConfig:
     verbose: Optional[int] = None
     log_to_file: Union[bool, str] = False
     progress_reporter: Any = None
+
+    @property
+    def local_dir(self) -> Optional[str]:  # the pre-2.7 name of storage_path
+        return self.storage_path
 
     def __post_init__(self):
         if self.failure_config is None:

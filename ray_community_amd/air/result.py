@@ -27,6 +27,17 @@ class Result:
 
         return pd.DataFrame(self.metrics_history) if self.metrics_history else None
 
+    def get_best_checkpoint(self, metric: str, mode: str):
+        """The kept checkpoint whose reported ``metric`` is best (``mode`` "max" / "min"); None if
+        no kept checkpoint reported it."""
+        if mode not in ("max", "min"):
+            raise ValueError("mode must be 'max' or 'min'")
+        scored = [(m[metric], c) for c, m in self.best_checkpoints if isinstance(m, dict) and metric in m]
+        if not scored:
+            return None
+        pick = max if mode == "max" else min
+        return pick(scored, key=lambda t: t[0])[1]
+
     @classmethod
     def from_path(cls, path: str) -> "Result":
         from ..train._checkpoint import Checkpoint

@@ -154,6 +154,111 @@ class BlockAccessor:
         for i in range(n):
             yield {k: _py(cols[k][i]) for k in keys}
 
+    # ------------------------------------------------------------------ reference API surface
+    # (python/ray/data/block.py BlockAccessor; sorting / aggregation helpers live in the exchange
+    # code of _internal/execution.py and work on these same blocks)
+    def to_batch_format(self, batch_format: Optional[str]):
+        return self.to_batch(batch_format)
+
+    def to_default(self) -> Block:
+        return self.b
+
+    def to_block(self) -> Block:
+        return self.b
+
+    @staticmethod
+    def batch_to_block(batch) -> Block:
+        return normalize_block(batch)
+
+    @staticmethod
+    def builder():
+        """A block builder: ``add(row)`` / ``add_block(block)`` then ``build()``."""
+        return _BlockBuilder()
+
+    def select(self, columns: List[str]) -> Block:
+        if _is_arrow(self.b):
+            return self.b.select(columns)
+        return {c: self.b[c] for c in columns}
+
+    def get_metadata(self, input_files=None, exec_stats=None) -> Dict[str, Any]:
+        return {"num_rows": self.num_rows(), "size_bytes": self.size_bytes(), "schema": self.schema(),
+                "input_files": list(input_files or []), "exec_stats": exec_stats}
+
+    def random_shuffle(self, random_seed: Optional[int] = None) -> Block:
+        perm = np.random.default_rng(random_seed).permutation(self.num_rows())
+        return self.take(perm)
+
+    def sample(self, n_samples: int, sort_key=None) -> Block:
+        """``n_samples`` random rows (of the ``sort_key`` columns when given)."""
+        n = self.num_rows()
+        idx = np.random.default_rng().choice(n, size=min(int(n_samples), n), replace=False) if n else np.arange(0)
+        out = BlockAccessor(self.take(np.sort(idx)))
+        if sort_key is not None:
+            cols = [sort_key] if isinstance(sort_key, str) else list(getattr(sort_key, "get_columns", lambda: sort_key)())
+            return out.select(cols)
+        return out.b
+
+    def zip(self, other: Block) -> Block:
+        """Columns of both blocks side by side (equal row counts; clashing names get a suffix)."""
+        a, o = self.to_numpy(), BlockAccessor.for_block(other).to_numpy()
+        if self.num_rows() != BlockAccessor.for_block(other).num_rows():
+            raise ValueError("cannot zip blocks of different row counts")
+        out = dict(a)
+        for k, v in o.items():
+            out[k if k not in out else f"{k}_1"] = v
+        return out
+
+    def sort_and_partition(self, boundaries: List[Any], sort_key) -> List[Block]:
+        """Sort by ``sort_key`` (a column name) and cut at the boundary values."""
+        key = sort_key if isinstance(sort_key, str) else list(getattr(sort_key, "get_columns", lambda: [sort_key])())[0]
+        cols = self.to_numpy()
+        order = np.argsort(cols[key], kind="stable")
+        srt = {k: v[order] for k, v in cols.items()}
+        cuts = np.searchsorted(srt[key], np.asarray(boundaries), side="left") if len(boundaries) else []
+        bounds = [0] + list(cuts) + [len(order)]
+        return [{k: v[a:b] for k, v in srt.items()} for a, b in zip(bounds[:-1], bounds[1:])]
+
+    @staticmethod
+    def merge_sorted_blocks(blocks: List[Block], sort_key) -> Block:
+        key = sort_key if isinstance(sort_key, str) else list(getattr(sort_key, "get_columns", lambda: [sort_key])())[0]
+        merged = BlockAccessor.for_block(concat_blocks(list(blocks))).to_numpy()
+        if not merged:
+            return {}
+        order = np.argsort(merged[key], kind="stable")
+        return {k: v[order] for k, v in merged.items()}
+
+    def combine(self, key, aggs) -> Block:
+        """Group this block by ``key`` and apply ``aggs`` (``AggregateFn`` objects from
+        ``ray.data.aggregate``) into one row per group: the partial-aggregation step."""
+        from .grouped_data import _aggregate_block
+
+        return _aggregate_block(self.b, key, aggs)
+
+    @staticmethod
+    def aggregate_combined_blocks(blocks: List[Block], key, aggs) -> Block:
+        from .grouped_data import _aggregate_block
+
+        return _aggregate_block(concat_blocks(list(blocks)), key, aggs)
+
+
+class _BlockBuilder:
+    def __init__(self):
+        self._rows: List[Dict] = []
+        self._blocks: List[Block] = []
+
+    def add(self, row: Dict) -> None:
+        self._rows.append(dict(row))
+
+    def add_block(self, block: Block) -> None:
+        self._blocks.append(normalize_block(block))
+
+    def num_rows(self) -> int:
+        return len(self._rows) + sum(BlockAccessor(b).num_rows() for b in self._blocks)
+
+    def build(self) -> Block:
+        parts = list(self._blocks) + ([rows_to_block(self._rows)] if self._rows else [])
+        return concat_blocks(parts) if parts else {}
+
 
 def _py(x):
     if isinstance(x, np.generic):

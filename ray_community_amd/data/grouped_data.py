@@ -61,6 +61,22 @@ def _all_in_one(block):
     return [block]
 
 
+def _aggregate_block(block, key, aggs):
+    """One row per group of ``block`` (pandas groupby), each AggregateFn as a column; ``key`` None
+    aggregates the whole block into one row."""
+    import pandas as pd
+
+    from .block import BlockAccessor, normalize_block
+
+    df = BlockAccessor.for_block(block).to_pandas()
+    keys = [key] if isinstance(key, str) else (list(key) if key else [])
+    if not keys:
+        return normalize_block(pd.DataFrame([{a.name: a.pandas_agg_all(df) for a in aggs}]))
+    gb = df.groupby(keys, sort=True)
+    out = pd.DataFrame({a.name: a.pandas_agg(gb) for a in aggs}).reset_index()
+    return normalize_block(out)
+
+
 def _cols(on):
     if on is None:
         raise ValueError("specify the column(s) to aggregate with on=")

@@ -283,12 +283,52 @@ def read_images(paths, *, size=None, mode="RGB", include_paths=False, **kw) -> D
 
 
 def read_datasource(datasource, *, parallelism: int = -1, **read_args) -> Dataset:
-    tasks = datasource.get_read_tasks(parallelism if parallelism > 0 else 2 * _cpus(), **read_args)
+    par = parallelism if parallelism > 0 else 2 * _cpus()
+    if getattr(datasource, "should_create_reader", lambda: False)():  # legacy Reader-style sources
+        tasks = datasource.create_reader(**read_args).get_read_tasks(par)
+    else:
+        tasks = datasource.get_read_tasks(par, **read_args)
     return Dataset([("read", t) for t in tasks])
 
 
 class Datasource:
-    """Custom datasource: implement ``get_read_tasks(parallelism) -> list of zero-arg callables``."""
+    """Custom datasource (reference ``python/ray/data/datasource/datasource.py``): implement
+    ``get_read_tasks(parallelism) -> list of zero-arg callables`` returning blocks. The legacy
+    Reader API (``create_reader(**read_args)`` -> an object with ``get_read_tasks`` /
+    ``estimate_inmemory_data_size``) is accepted too."""
 
     def get_read_tasks(self, parallelism: int, **kw):
         raise NotImplementedError
+
+    def get_name(self) -> str:
+        name = type(self).__name__
+        return name[: -len("Datasource")] if name.endswith("Datasource") and len(name) > 10 else name
+
+    def estimate_inmemory_data_size(self) -> Optional[int]:
+        return None
+
+    @property
+    def supports_distributed_reads(self) -> bool:
+        return True
+
+    def should_create_reader(self) -> bool:
+        """True for sources written against the legacy Reader API (they override create_reader)."""
+        return type(self).create_reader is not Datasource.create_reader
+
+    def create_reader(self, **read_args):
+        return _DatasourceReader(self, read_args)
+
+    def prepare_read(self, parallelism: int, **read_args):
+        """Deprecated reference alias of ``get_read_tasks``."""
+        return self.get_read_tasks(parallelism, **read_args)
+
+
+class _DatasourceReader:
+    def __init__(self, ds, read_args):
+        self._ds, self._args = ds, read_args
+
+    def get_read_tasks(self, parallelism: int):
+        return self._ds.get_read_tasks(parallelism, **self._args)
+
+    def estimate_inmemory_data_size(self):
+        return self._ds.estimate_inmemory_data_size()

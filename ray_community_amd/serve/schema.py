@@ -39,6 +39,27 @@ class LoggingConfig(_Model):
     logs_dir: Optional[str] = None
     enable_access_log: bool = True
 
+    @field_validator("encoding")
+    @classmethod
+    def valid_encoding_format(cls, v):
+        if v not in ("TEXT", "JSON"):
+            raise ValueError(f"Got '{v}' for encoding. Encoding must be one of ('TEXT', 'JSON').")
+        return v
+
+    @field_validator("log_level")
+    @classmethod
+    def valid_log_level(cls, v):
+        import logging
+
+        if isinstance(v, int):
+            if v not in (logging.DEBUG, logging.INFO, logging.WARNING, logging.ERROR, logging.CRITICAL, logging.NOTSET):
+                raise ValueError(f"Got '{v}' for log_level: not a logging level")
+            return logging.getLevelName(v)
+        if v not in ("DEBUG", "INFO", "WARNING", "ERROR", "CRITICAL", "NOTSET"):
+            raise ValueError(f'Got "{v}" for log_level. log_level must be one of DEBUG, INFO, WARNING, ERROR, '
+                             f"CRITICAL, NOTSET.")
+        return v
+
 
 class RayActorOptionsSchema(_Model):
     runtime_env: Dict[str, Any] = Field(default_factory=dict)

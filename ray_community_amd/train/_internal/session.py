@@ -27,6 +27,19 @@ class TrainContext:
     storage_path: str = ""
     metadata: Dict[str, Any] = field(default_factory=dict)
 
+    def get_trial_resources(self):
+        """The trial's resource request (its PlacementGroupFactory) under Tune, else the worker's
+        assigned resources."""
+        r = (self.metadata or {}).get("_trial_resources")
+        if r is not None:
+            return r
+        from ..._private.worker import get_runtime_context
+
+        try:
+            return get_runtime_context().get_assigned_resources()
+        except Exception:
+            return {}
+
     def get_world_rank(self):
         return self.world_rank
 

@@ -24,6 +24,28 @@ class TorchConfig(BackendConfig):
     def backend_cls(self):
         return _TorchBackend
 
+    @property
+    def train_func_context(self):
+        """Context manager the training function runs under on each worker (reference
+        ``TorchConfig.train_func_context``): it makes the worker's HIP device the current device."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            import torch
+
+            if torch.cuda.is_available():
+                from .train_loop_utils import get_device
+
+                dev = get_device()
+                if getattr(dev, "type", None) == "cuda":
+                    with torch.cuda.device(dev):
+                        yield
+                    return
+            yield
+
+        return ctx
+
 
 def _free_port():
     import socket

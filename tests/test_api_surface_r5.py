@@ -137,3 +137,63 @@ def test_serve_deployment_properties():
     assert D.max_concurrent_queries == 7 and D.route_prefix == "/x" and D.url.endswith("/x")
     D.set_logging_config({"log_level": "DEBUG"})
     assert D.logging_config == {"log_level": "DEBUG"}
+
+
+def test_config_and_block_apis():
+    import numpy as np
+
+    from ray_community_amd import data
+    from ray_community_amd.air import Result, RunConfig, ScalingConfig
+    from ray_community_amd.data import aggregate as A
+    from ray_community_amd.data.block import BlockAccessor
+    from ray_community_amd.serve.config import AutoscalingConfig, HTTPOptions
+    from ray_community_amd.serve.schema import LoggingConfig
+
+    sc = ScalingConfig.from_placement_group_factory({"bundles": [{"CPU": 1}, {"CPU": 2, "GPU": 1}, {"CPU": 2, "GPU": 1}]})
+    assert sc.num_workers == 2 and sc.use_gpu and sc.trainer_resources == {"CPU": 1}
+    assert RunConfig(storage_path="/tmp/x").local_dir == "/tmp/x"
+    r = Result(metrics={}, checkpoint=None, best_checkpoints=[("a", {"acc": 0.5}), ("b", {"acc": 0.9})])
+    assert r.get_best_checkpoint("acc", "max") == "b" and r.get_best_checkpoint("acc", "min") == "a"
+    ctx = data.DataContext.get_current()
+    ctx.set_config("plugin.x", 3)
+    assert ctx.get_config("plugin.x") == 3
+    ctx.remove_config("plugin.x")
+    assert ctx.get_config("plugin.x") is None and ctx.min_parallelism == 200
+    ctx.execution_options.validate()
+    ac = AutoscalingConfig(min_replicas=1, max_replicas=4, upscale_smoothing_factor=0.5)
+    assert ac.get_upscaling_factor() == 0.5 and ac.get_downscaling_factor() == 1.0
+    with pytest.raises(ValueError):
+        AutoscalingConfig(min_replicas=3, max_replicas=2)
+    assert HTTPOptions(location="NoServer").location_backfill_no_server().location == "NoServer"
+    assert LoggingConfig(log_level=10).log_level == "DEBUG"
+    with pytest.raises(Exception):
+        LoggingConfig(encoding="XML")
+    b = {"k": np.array([1, 2, 1, 3]), "v": np.array([1.0, 2.0, 3.0, 4.0])}
+    acc = BlockAccessor.for_block(b)
+    assert [x["k"].tolist() for x in acc.sort_and_partition([2, 3], "k")] == [[1, 1], [2], [3]]
+    comb = BlockAccessor.for_block(acc.combine("k", [A.Sum("v"), A.Count()])).to_numpy()
+    assert comb["sum(v)"].tolist() == [4.0, 2.0, 4.0] and comb["count()"].tolist() == [2, 1, 1]
+    bld = BlockAccessor.builder()
+    bld.add({"k": 9, "v": 1.0})
+    bld.add_block(b)
+    assert BlockAccessor(bld.build()).num_rows() == 5
+    assert set(acc.zip({"w": np.arange(4)})) == {"k", "v", "w"}
+
+
+def test_legacy_reader_datasource(shutdown_only):
+    ray.init(num_cpus=2, include_dashboard=False, log_to_driver=False)
+    from ray_community_amd.data import Datasource
+
+    class Legacy(Datasource):
+        def create_reader(self, n=10):
+            class R:
+                def get_read_tasks(self, parallelism):
+                    return [lambda i=i: {"x": [i]} for i in range(n)]
+
+                def estimate_inmemory_data_size(self):
+                    return 8 * n
+            return R()
+
+    src = Legacy()
+    assert src.should_create_reader() and src.get_name() == "Legacy"
+    assert sorted(r["x"] for r in ray.data.read_datasource(src, n=5).take_all()) == [0, 1, 2, 3, 4]
