@@ -66,6 +66,8 @@ _SIGS = {
     "rca_bn_fwd": (c_int, [c_void_p] * 9 + [c_ll, c_int, c_float, c_float, c_int, c_void_p]),
     "rca_bn_apply": (c_int, [c_void_p] * 4 + [c_ll, c_int, c_int, c_void_p]),
     "rca_bn_set_unroll": (c_int, [c_int]),
+    "rca_attn_set_dq_qw": (c_int, [c_int]),
+    "rca_attn_set_fwd_nw": (c_int, [c_int]),
     "rca_gemm_affine_act": (c_int, [c_void_p] * 5 + [c_int] * 3 + [c_ll] * 4 + [c_int, c_void_p]),
     "rca_bn_bwd": (c_int, [c_void_p] * 11 + [c_ll, c_int, c_int, c_void_p]),
     "rca_gbdt_hist_workspace": (c_ll, [c_int, c_ll, c_int, c_int]),

@@ -56,12 +56,16 @@ namespace {
 // and wave-uniform.
 // DMA: K/V tiles go HBM -> LDS by buffer_load ... lds (DmaStage) instead of the register-staged
 // global load + ds_write pair (Stage); RCA_ATTN_DMA=0 selects the latter (A/B).
-template <int D, bool CAUSAL, bool DMA>
-__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
+// NW = 8: one 512-thread workgroup of 8 waves (two per SIMD) covers 256 query rows, so each K/V
+// tile staged into LDS serves twice the rows: half the L2 -> LDS DMA bytes per MFMA of the 4-wave
+// form (whose two co-resident workgroups each stage their own copy). Waves 0-3 issue the DMA.
+template <int D, bool CAUSAL, bool DMA, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     bf16_t* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hk, long sq, long sk, long sv,
     long so, float scale2) {
-  constexpr int BQ = 128, BK = 64, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2, G8 = Img<D>::G8;
+  static_assert(NW == 4 || (NW == 8 && DMA), "the 8-wave form stages by LDS-DMA");
+  constexpr int BQ = 32 * NW, BK = 64, NKS = D / 16, NDB = D / 32, TILE = BK * D * 2, G8 = Img<D>::G8;
   constexpr float THR = 8.f;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
 
@@ -95,9 +99,12 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
   std::conditional_t<DMA, DmaStage<D, BK>, Stage<D, BK>> kst, vst;
   kst.init(Kb, sk, S, tid);
   vst.init(Vb, sv, S, tid);
+  const bool dma_wave = NW == 4 || __builtin_amdgcn_readfirstlane(w) < 4;  // the staging waves
   if constexpr (DMA) {
-    kst.issue(0, sk, smem);
-    vst.issue(0, sv, smem + TILE);
+    if (dma_wave) {
+      kst.issue(0, sk, smem);
+      vst.issue(0, sv, smem + TILE);
+    }
     wait_dma();
   } else {
     kst.load(0, sk);
@@ -115,8 +122,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
     const bool more = it + 1 < ntile;
     if (more) {
       if constexpr (DMA) {  // into the other buffer: every wave left it at the last barrier
-        kst.issue(kb + BK, sk, smem + (buf ^ 1) * 2 * TILE);
-        vst.issue(kb + BK, sv, smem + (buf ^ 1) * 2 * TILE + TILE);
+        if (dma_wave) {
+          kst.issue(kb + BK, sk, smem + (buf ^ 1) * 2 * TILE);
+          vst.issue(kb + BK, sv, smem + (buf ^ 1) * 2 * TILE + TILE);
+        }
       } else {
         kst.load(kb + BK, sk);
         vst.load(kb + BK, sv);
@@ -237,15 +246,19 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(
 // Explicit instantiations: hipcc (ROCm 7.2) referenced but did not emit the host launch stub of
 // one of the two DMA instances per head size when they were only instantiated through launch_fwd
 // (an undefined __device_stub__ symbol at load time).
-#define RCA_FWD_INST(DD, CC, MM)                                                                          \
-  template __global__ void attn_fwd_kernel<DD, CC, MM>(const bf16_t* __restrict__, const bf16_t* __restrict__, \
-                                                       const bf16_t* __restrict__, bf16_t* __restrict__,        \
-                                                       float* __restrict__, int, int, int, int, long, long, long,  \
-                                                       long, float);
-RCA_FWD_INST(128, false, true)
-RCA_FWD_INST(64, false, true)
-RCA_FWD_INST(128, true, true)
-RCA_FWD_INST(64, true, true)
+#define RCA_FWD_INST(DD, CC, MM, NN)                                                                          \
+  template __global__ void attn_fwd_kernel<DD, CC, MM, NN>(const bf16_t* __restrict__, const bf16_t* __restrict__, \
+                                                           const bf16_t* __restrict__, bf16_t* __restrict__,        \
+                                                           float* __restrict__, int, int, int, int, long, long, long,  \
+                                                           long, float);
+RCA_FWD_INST(128, false, true, 4)
+RCA_FWD_INST(64, false, true, 4)
+RCA_FWD_INST(128, true, true, 4)
+RCA_FWD_INST(64, true, true, 4)
+RCA_FWD_INST(128, false, true, 8)
+RCA_FWD_INST(64, false, true, 8)
+RCA_FWD_INST(128, true, true, 8)
+RCA_FWD_INST(64, true, true, 8)
 #undef RCA_FWD_INST
 
 // ---------------------------------------------------------------------------------------------
@@ -407,10 +420,24 @@ bool attn_dma() {
   return on;
 }
 
+// waves per forward workgroup: 8 (default: one 256-row workgroup per CU, K/V staged once for all
+// 8 waves) or 4 (two 128-row workgroups per CU) (RCA_ATTN_FWD_NW; run-time switch
+// rca_attn_set_fwd_nw). Interleaved A/B at the 8B shape, 3 rounds: 0.273 / 0.273 / 0.273 ms vs
+// 0.279 / 0.278 / 0.279; bitwise-equal outputs (tests/test_attention_gpu.py).
+int g_fwd_nw = [] {
+  const char* e = getenv("RCA_ATTN_FWD_NW");
+  return e && atoi(e) == 4 ? 4 : 8;
+}();
+
 template <int D, bool C>
 void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                 int Hk, long sq, long sk, long sv, long so, float scale2, hipStream_t st) {
   if (D == 128 && rca_attn_launch_fwd_wide(C, q, k, v, o, lse, B, S, Hq, Hk, sq, sk, sv, so, scale2, st)) return;
+  if (g_fwd_nw == 8 && S % 256 == 0 && attn_dma()) {
+    hipLaunchKernelGGL((attn_fwd_kernel<D, C, true, 8>), dim3(B * Hq * (S / 256)), dim3(512), 0, st, q, k, v, o, lse, B,
+                       S, Hq, Hk, sq, sk, sv, so, scale2);
+    return;
+  }
   const int grid = B * Hq * (S / 128);
   if (attn_dma())
     hipLaunchKernelGGL((attn_fwd_kernel<D, C, true>), dim3(grid), dim3(kThreads), 0, st, q, k, v, o, lse, B, S, Hq, Hk,
@@ -477,6 +504,12 @@ static int g_bwd_mode = [] {
 RCA_API int rca_attn_set_bwd_mode(int mode) {
   const int old = g_bwd_mode;
   g_bwd_mode = mode;
+  return old;
+}
+
+RCA_API int rca_attn_set_fwd_nw(int nw) {
+  const int old = g_fwd_nw;
+  g_fwd_nw = nw == 8 ? 8 : 4;
   return old;
 }
 

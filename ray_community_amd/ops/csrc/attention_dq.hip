@@ -12,6 +12,8 @@
 // the dQ kernel, which now runs after dK/dV).
 #include "attention_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 // delta[b, h, s] = sum_d dO[b, s, h, d] * O[b, s, h, d]: one 16-lane group per 4 consecutive
@@ -58,15 +60,17 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 // ds_read_b64_tr_b16 reads of the fragment-order tiles (conflict-free under the store-side XOR
 // swizzle). Causally masked tiles still issue their DMA (of the diagonal tile, never read), so
 // every wave's vmcnt counts are the same. Causal: the longest query blocks first.
-template <bool CAUSAL>
+template <bool CAUSAL, int QW = 1>
 __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* __restrict__ K,
                                                                  const bf16_t* __restrict__ dSw,
                                                                  bf16_t* __restrict__ dQ, int B, int S, int Hq,
                                                                  int Hk, long sk, long sdq, long tiles_bh,
                                                                  float scale) {
-  constexpr int D = 128, BQ = 128, BK = 32, NDB = 4, KT = BK * D * 2, DST = 4 * 2048, SLOT = KT + DST, NBUF = 4,
-                AHEAD = NBUF - 1, OPS = 4 /* DMA ops per wave per step: 2 K pieces + 2 dS pieces */,
-                G8 = Img<D>::G8;
+  // QW query blocks (32 rows each) per wave: the step's K tile is staged once for 4 QW blocks,
+  // so QW = 2 halves the K bytes per dS byte through the LDS-DMA path
+  constexpr int D = 128, BQ = 128 * QW, BK = 32, NDB = 4, KT = BK * D * 2, DST = 4 * QW * 2048, SLOT = KT + DST,
+                NBUF = QW == 1 ? 4 : 3, AHEAD = NBUF - 1,
+                OPS = 2 + 2 * QW /* DMA ops per wave per step: 2 K pieces + 2 per dS tile */, G8 = Img<D>::G8;
   __shared__ __attribute__((aligned(16))) char smem[NBUF * SLOT];
 
   const int nqb = S / BQ, G = Hq / Hk, nb32 = S >> 5;
@@ -76,26 +80,30 @@ __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* _
   const int qb = CAUSAL ? nqb - 1 - qr : qr;
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qb32 = 4 * qb + w;
-  const int nstep = CAUSAL ? 4 * (qb + 1) : nb32;
+  const int qb0 = 4 * QW * qb + QW * w;  // this wave's first 32-row query block (QW consecutive)
+  const int nstep = CAUSAL ? 4 * QW * (qb + 1) : nb32;
 
   DmaStage<D, BK> kst;
   kst.init(K + (long)b * S * sk + (long)hk * D, sk, S, tid);
   const char* dsb = (const char*)dSw + (long)(b * Hq + hq) * tiles_bh * 2048;
   const __amdgpu_buffer_rsrc_t dsr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(dsb), (short)0, (int)(tiles_bh * 2048), 0x00020000);
-  const long trow = CAUSAL ? (long)qb32 * (qb32 + 1) / 2 : (long)qb32 * nb32;  // this wave's tile row
 
   auto issue = [&](int st) {
     char* base = smem + (st % NBUF) * SLOT;
     kst.issue(st * BK, sk, base);
-    const int kb = (!CAUSAL || st <= qb32) ? st : qb32;  // a masked tile: any valid tile (never read)
-    const int so = __builtin_amdgcn_readfirstlane((int)((trow + kb) * 2048));
-    char* dl = base + KT + w * 2048;
 #pragma unroll
-    for (int pc = 0; pc < 2; ++pc)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsr, (__attribute__((address_space(3))) void*)(dl + pc * 1024), 16,
-                                               lane * 16 + pc * 1024, so, 0, 0);
+    for (int j = 0; j < QW; ++j) {
+      const int q32 = qb0 + j;
+      const long trow = CAUSAL ? (long)q32 * (q32 + 1) / 2 : (long)q32 * nb32;  // tile row of block q32
+      const int kb = (!CAUSAL || st <= q32) ? st : q32;  // a masked tile: any valid tile (never read)
+      const int so = __builtin_amdgcn_readfirstlane((int)((trow + kb) * 2048));
+      char* dl = base + KT + (QW * w + j) * 2048;
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dsr, (__attribute__((address_space(3))) void*)(dl + pc * 1024), 16,
+                                                 lane * 16 + pc * 1024, so, 0, 0);
+    }
   };
 
   // per-lane read bases: K^T (the forward's V^T reads) and dS^T (two bases: read r of a k-step)
@@ -108,54 +116,71 @@ __global__ __launch_bounds__(kThreads, 2) void attn_dq_ds_kernel(const bf16_t* _
     dsa[r] = sp * 1024 + 16 * (L ^ (4 * (lane & 1) + 8 * sp)) + 8 * ((lane >> 1) & 1);
   }
 
-  f32x16 dq[NDB];
+  f32x16 dq[QW][NDB];
 #pragma unroll
-  for (int i = 0; i < NDB; ++i) dq[i] = zero16();
+  for (int j = 0; j < QW; ++j)
+#pragma unroll
+    for (int i = 0; i < NDB; ++i) dq[j][i] = zero16();
 
   for (int st = 0; st < AHEAD && st < nstep; ++st) issue(st);
   for (int st = 0; st < nstep; ++st) {
     // stage st landed: at most (stages issued after it) x OPS of this wave's DMAs still pending
     const int later = nstep - 1 - st < AHEAD - 1 ? nstep - 1 - st : AHEAD - 1;
-    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's pieces of stage st are in; stage st-1 is read
     if (st + AHEAD < nstep) issue(st + AHEAD);  // into the buffer stage st-1 used
-    if (!CAUSAL || st <= qb32) {
+    if (!CAUSAL || st <= qb0 + QW - 1) {
       const char* Ks = smem + (st % NBUF) * SLOT;
-      const char* Ds = Ks + KT + w * 2048;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t fr[NDB + 1];
+        bf16x8_t fr[NDB + QW];
 #pragma unroll
         for (int db = 0; db < NDB; ++db)
           fr[db] = lds_tr8_asm(Ks + tb0 + G8 * (2 * ks) + 512 * db, Ks + tb1 + G8 * (2 * ks + 1) + 512 * db);
-        fr[NDB] = lds_tr8_asm(Ds + dsa[0] + 256 * ks, Ds + dsa[1] + 256 * ks);
+#pragma unroll
+        for (int j = 0; j < QW; ++j) {
+          const char* Ds = Ks + KT + (QW * w + j) * 2048;
+          fr[NDB + j] = lds_tr8_asm(Ds + dsa[0] + 256 * ks, Ds + dsa[1] + 256 * ks);
+        }
         lds_tr_settle(fr);
 #pragma unroll
-        for (int db = 0; db < NDB; ++db) dq[db] = mfma32(fr[db], fr[NDB], dq[db]);
+        for (int j = 0; j < QW; ++j) {
+          if (CAUSAL && st > qb0 + j) continue;  // block j's row is complete (wave-uniform)
+#pragma unroll
+          for (int db = 0; db < NDB; ++db) dq[j][db] = mfma32(fr[db], fr[NDB + j], dq[j][db]);
+        }
       }
     }
   }
 
   // dQ^T accumulators: d = 32 db + (r & 3) + 8 (r >> 2) + 4 h on the registers, the query on the lane
-  const int qrow = qb32 * 32 + (lane & 31);
-  bf16_t* dQr = dQ + ((long)b * S + qrow) * sdq + (long)hq * D;
 #pragma unroll
-  for (int db = 0; db < NDB; ++db) {
+  for (int j = 0; j < QW; ++j) {
+    const int qrow = (qb0 + j) * 32 + (lane & 31);
+    bf16_t* dQr = dQ + ((long)b * S + qrow) * sdq + (long)hq * D;
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      store4(dQr + 32 * db + 8 * g + 4 * h, dq[db][4 * g] * scale, dq[db][4 * g + 1] * scale,
-             dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
+    for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(dQr + 32 * db + 8 * g + 4 * h, dq[j][db][4 * g] * scale, dq[j][db][4 * g + 1] * scale,
+               dq[j][db][4 * g + 2] * scale, dq[j][db][4 * g + 3] * scale);
+    }
   }
 }
 
 // explicit instantiations: hipcc does not always emit the host launch stub of a kernel template
 // instantiated only through its launcher (an undefined __device_stub__ symbol at load time)
-template __global__ void attn_dq_ds_kernel<true>(const bf16_t* __restrict__, const bf16_t* __restrict__,
-                                                 bf16_t* __restrict__, int, int, int, int, long, long, long, float);
-template __global__ void attn_dq_ds_kernel<false>(const bf16_t* __restrict__, const bf16_t* __restrict__,
-                                                  bf16_t* __restrict__, int, int, int, int, long, long, long, float);
+#define RCA_DQ_INST(CC, QQ)                                                                                       \
+  template __global__ void attn_dq_ds_kernel<CC, QQ>(const bf16_t* __restrict__, const bf16_t* __restrict__,      \
+                                                     bf16_t* __restrict__, int, int, int, int, long, long, long, \
+                                                     float);
+RCA_DQ_INST(true, 1)
+RCA_DQ_INST(false, 1)
+RCA_DQ_INST(true, 2)
+RCA_DQ_INST(false, 2)
+#undef RCA_DQ_INST
 
 }  // namespace
 
@@ -175,12 +200,32 @@ void rca_attn_launch_delta(const bf16_t* o, const bf16_t* dout, float* delta, in
                      so, sdo);
 }
 
+// query blocks per wave of the dQ-from-dS kernel: 2 (default: the K tile staged once per 256 query
+// rows) or 1 (RCA_ATTN_DQ_QW; run-time switch rca_attn_set_dq_qw). Interleaved A/B, attention
+// backward at the 8B shape: 1.019 / 1.054 / 1.064 ms vs 1.036 / 1.051 / 1.073; with the 8-wave
+// forward the 8B step measured 346.25 vs 348.08 ms median (scripts/step_ab.py, 3 rounds); dQ bitwise
+// equal to the 1-block form.
+static int g_dq_qw = [] {
+  const char* e = getenv("RCA_ATTN_DQ_QW");
+  return e && atoi(e) == 1 ? 1 : 2;
+}();
+RCA_API int rca_attn_set_dq_qw(int q) {
+  const int old = g_dq_qw;
+  g_dq_qw = q == 2 ? 2 : 1;
+  return old;
+}
+
 void rca_attn_launch_dq_ds(bool causal, const bf16_t* k, const bf16_t* dsw, bf16_t* dq, int B, int S, int Hq, int Hk,
                            long sk, long sdq, float scale, hipStream_t st) {
   const long nb = S / 32, tiles = causal ? nb * (nb + 1) / 2 : nb * nb;
-  const dim3 grid(B * Hq * (S / 128)), block(kThreads);
-  if (causal)
-    hipLaunchKernelGGL((attn_dq_ds_kernel<true>), grid, block, 0, st, k, dsw, dq, B, S, Hq, Hk, sk, sdq, tiles, scale);
-  else
-    hipLaunchKernelGGL((attn_dq_ds_kernel<false>), grid, block, 0, st, k, dsw, dq, B, S, Hq, Hk, sk, sdq, tiles, scale);
+  const int qw = (g_dq_qw == 2 && S % 256 == 0) ? 2 : 1;
+  const dim3 grid(B * Hq * (S / (128 * qw))), block(kThreads);
+#define RCA_DQ(CC, QQ) \
+  hipLaunchKernelGGL((attn_dq_ds_kernel<CC, QQ>), grid, block, 0, st, k, dsw, dq, B, S, Hq, Hk, sk, sdq, tiles, scale)
+  if (qw == 2) {
+    if (causal) RCA_DQ(true, 2); else RCA_DQ(false, 2);
+  } else {
+    if (causal) RCA_DQ(true, 1); else RCA_DQ(false, 1);
+  }
+#undef RCA_DQ
 }

@@ -52,6 +52,20 @@ def main():
                 prev = lib.rca_attn_set_hs_nops(n)
                 run(f"nops-{n}", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
                 lib.rca_attn_set_hs_nops(prev)
+    if os.environ.get("ATTN_DQQW_AB"):  # interleaved A/B: dQ-from-dS with 1 or 2 query blocks per wave
+        lib = ops._lib.lib()
+        for _ in range(3):
+            for qw in (1, 2):
+                prev = lib.rca_attn_set_dq_qw(qw)
+                run(f"dq-qw{qw}", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
+                lib.rca_attn_set_dq_qw(prev)
+    if os.environ.get("ATTN_FWDNW_AB"):  # interleaved A/B: 4-wave (2 WG/CU) vs 8-wave (256-row WG) forward
+        lib = ops._lib.lib()
+        for _ in range(3):
+            for nw in (4, 8):
+                prev = lib.rca_attn_set_fwd_nw(nw)
+                run(f"fwd-nw{nw}", lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hk, D, causal=True))
+                lib.rca_attn_set_fwd_nw(prev)
     if os.environ.get("ATTN_WIDE_AB"):  # interleaved A/B of the forward variants
         lib = ops._lib.lib()
         for _ in range(3):

@@ -48,7 +48,16 @@ def _toggles():
         # wait states ahead of the hand-scheduled dK/dV kernel's asm MFMAs (s_nop 1 vs s_nop 3)
         "nop1": lambda: _set_lib("rca_attn_set_hs_nops", 1),
         "nop3": lambda: _set_lib("rca_attn_set_hs_nops", 3),
+        # attention forward: 4-wave workgroups (2 per CU) vs 8-wave 256-row workgroups; dQ-from-dS
+        # with 1 or 2 query blocks per wave
+        "fwd_nw4": lambda: _set_lib("rca_attn_set_fwd_nw", 4),
+        "nw8_qw2": lambda: _both(_set_lib("rca_attn_set_fwd_nw", 8), _set_lib("rca_attn_set_dq_qw", 2)),
+        "qw1": lambda: _set_lib("rca_attn_set_dq_qw", 1),
     }
+
+
+def _both(undo_a, undo_b):
+    return lambda: (undo_b(), undo_a())
 
 
 def main():

@@ -247,6 +247,47 @@ def test_recompute_free_dq_large_logits_and_determinism():
     assert _err(dq, qr.grad) < 3e-2 and _err(dk, kr.grad) < 3e-2 and _err(dv, vr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("D", [128, 64])
+@pytest.mark.parametrize("S,causal", [(256, True), (1024, True), (768, False), (4096, True)])
+def test_forward_eight_wave_workgroup_is_bitwise_equal(S, causal, D):
+    """The 8-wave forward (256 query rows per workgroup, K/V staged once for all 8 waves) runs the
+    same per-wave schedule over the same tiles as the 4-wave form: bitwise equal O and LSE."""
+    B, Hq, Hk = 1, 8, 2
+    q, k, v = _mk(B, S, Hq, D, 91), _mk(B, S, Hk, D, 92), _mk(B, S, Hk, D, 93)
+    lib = ops._lib.lib()
+    prev = lib.rca_attn_set_fwd_nw(4)
+    try:
+        o4 = ops.flash_attention(q, k, v, causal)
+        lib.rca_attn_set_fwd_nw(8)
+        o8 = ops.flash_attention(q, k, v, causal)
+    finally:
+        lib.rca_attn_set_fwd_nw(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(o4, o8)  # (S % 256 != 0 runs the 4-wave kernel in both)
+    qr, kr, vr = (t.detach().float() for t in (q, k, v))
+    assert _err(o8, ref.attention_ref(qr, kr, vr, causal)) < 2e-2
+
+
+@pytest.mark.parametrize("S,causal", [(256, True), (1024, True), (2048, False), (4096, True)])
+def test_dq_from_ds_two_blocks_per_wave_is_bitwise_equal(S, causal):
+    """The dQ-from-dS kernel with 2 query blocks per wave (the K tile staged once for 256 query
+    rows) sums every dQ element over the same tiles in the same key order as the 1-block variant:
+    bitwise equal gradients, causal and not."""
+    B, Hq, Hk, D = 1, 8, 2, 128
+    q, k, v = _mk(B, S, Hq, D, 81), _mk(B, S, Hk, D, 82), _mk(B, S, Hk, D, 83)
+    do = _mk(B, S, Hq, D, 84)
+    lib = ops._lib.lib()
+    prev = lib.rca_attn_set_dq_qw(1)
+    try:
+        a = _bwd(q, k, v, do, causal, 1)
+        lib.rca_attn_set_dq_qw(2)
+        b2 = _bwd(q, k, v, do, causal, 1)
+    finally:
+        lib.rca_attn_set_dq_qw(prev)
+    for x, y in zip(a, b2):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_ds_kernel_wait_state_variants_agree_bitwise(causal):
     """The dS-storing dK/dV kernel with 2 (s_nop 1) and 4 (s_nop 3) wait states ahead of each asm MFMA
