@@ -17,13 +17,15 @@
 namespace {
 
 // delta[b, h, s] = sum_d dO[b, s, h, d] * O[b, s, h, d]: one 16-lane group per 4 consecutive
-// (b, h, s) rows (all four rows' loads in flight before any math), 16 B per lane (D = 128);
-// consecutive groups = consecutive tokens of one head (coalesced writes)
+// (b, s, h) rows (all four rows' loads in flight before any math), 16 B per lane (D = 128). Rows
+// run in the tensors' own (token, head) order, so a wave reads 4 KB of consecutive heads of
+// consecutive tokens: in the training step O and dO come from HBM, and the (head, token) order
+// (an 8 KB stride between a group's rows) read them at ~2 TB/s (66 us per layer at the 8B shape).
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
                                                          float* __restrict__ Delta, int B, int S, int Hq, long so,
                                                          long sdo) {
   constexpr int R = 4;
-  const long row0 = ((long)blockIdx.x * 16 + (threadIdx.x >> 4)) * R;  // (b * Hq + h) * S + s
+  const long row0 = ((long)blockIdx.x * 16 + (threadIdx.x >> 4)) * R;  // (b * S + s) * Hq + h
   const long rows = (long)B * Hq * S;
   if (row0 >= rows) return;
   const int c = threadIdx.x & 15;
@@ -31,8 +33,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const long row = row0 + i < rows ? row0 + i : row0;
-    const long s = row % S, bh = row / S;
-    const long tok = (bh / Hq) * S + s, h = bh % Hq;
+    const long tok = row / Hq, h = row % Hq;
     ov[i] = *reinterpret_cast<const u32x4*>(O + tok * so + h * 128 + 8 * c);
     gv[i] = *reinterpret_cast<const u32x4*>(dO + tok * sdo + h * 128 + 8 * c);
   }
@@ -46,7 +47,10 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
     for (int j = 0; j < 8; ++j) acc = fmaf(of[j], gf[j], acc);
 #pragma unroll
     for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (c == 0 && row0 + i < rows) Delta[row0 + i] = acc;
+    if (c == 0 && row0 + i < rows) {
+      const long row = row0 + i, tok = row / Hq, h = row % Hq, b = tok / S, s = tok % S;
+      Delta[(b * Hq + h) * S + s] = acc;
+    }
   }
 }
 
