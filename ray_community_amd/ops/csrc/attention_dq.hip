@@ -19,8 +19,9 @@ namespace {
 // delta[b, h, s] = sum_d dO[b, s, h, d] * O[b, s, h, d]: one 16-lane group per 4 consecutive
 // (b, s, h) rows (all four rows' loads in flight before any math), 16 B per lane (D = 128). Rows
 // run in the tensors' own (token, head) order, so a wave reads 4 KB of consecutive heads of
-// consecutive tokens: in the training step O and dO come from HBM, and the (head, token) order
-// (an 8 KB stride between a group's rows) read them at ~2 TB/s (66 us per layer at the 8B shape).
+// consecutive tokens. (In the 8B step the kernel measures ~67 us per layer in either row order,
+// against 24 us in isolation: it runs while the side-stream gradient-norm pass streams the
+// finished gradient buckets, and both share HBM; profiles/llama8b_r5_perstep_final.md.)
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
                                                          float* __restrict__ Delta, int B, int S, int Hq, long so,
                                                          long sdo) {
