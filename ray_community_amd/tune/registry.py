@@ -94,6 +94,10 @@ class Experiment:
         return cls(name=name, run=spec.pop("run"), **spec)
 
 
+_RUN_EXPERIMENTS_PASSTHROUGH = ("resume", "resume_config", "reuse_actors", "callbacks", "progress_reporter",
+                                "trial_name_creator", "trial_dirname_creator", "max_concurrent_trials")
+
+
 def run_experiments(experiments: Union[Experiment, List[Experiment], Dict[str, Dict]], scheduler=None,
                     verbose: int = 2, raise_on_failed_trial: bool = True, **kw) -> List:
     """Run one or more experiments one after another; returns every trial's result."""
@@ -108,7 +112,8 @@ def run_experiments(experiments: Union[Experiment, List[Experiment], Dict[str, D
         ana = _run(resolve_trainable(e.run), name=e.name, stop=e.stop, config=e.config,
                    resources_per_trial=e.resources_per_trial, num_samples=e.num_samples, storage_path=e.storage_path,
                    scheduler=scheduler, checkpoint_config=e.checkpoint_config, max_failures=e.max_failures,
-                   raise_on_failed_trial=raise_on_failed_trial)
+                   raise_on_failed_trial=raise_on_failed_trial, verbose=verbose,
+                   **{k: v for k, v in kw.items() if k in _RUN_EXPERIMENTS_PASSTHROUGH})
         trials.extend(ana.trials)
     return trials
 
@@ -148,10 +153,43 @@ def create_scheduler(scheduler: str, **kwargs):
 
 @dataclass
 class ResumeConfig:
-    """What ``Tuner.restore`` does with unfinished / errored trials."""
+    """What ``Tuner.restore`` does with unfinished / errored trials
+    (reference: python/ray/tune/execution/experiment_state.py ResumeConfig)."""
+
+    class ResumeType:
+        RESUME = "resume"
+        RESTART = "restart"
+        SKIP = "skip"
+
     finished: str = "restore"
     unfinished: str = "resume"
     errored: str = "skip"
+
+    def _restore_kwargs(self) -> Dict:
+        """``Tuner.restore`` keyword arguments for this config."""
+        return {"resume_unfinished": str(self.unfinished) != "skip",
+                "resume_errored": str(self.errored) == "resume",
+                "restart_errored": str(self.errored) == "restart"}
+
+    @classmethod
+    def _from_legacy(cls, resume) -> Optional["ResumeConfig"]:
+        """``tune.run(resume=...)``: True / "AUTO", with an optional "+ERRORED", "+RESTART_ERRORED",
+        "+ERRORED_ONLY" or "+RESTART_ERRORED_ONLY" suffix."""
+        if resume is False or resume is None:
+            return None
+        if resume is True:
+            return cls()
+        head, *suffixes = str(resume).split("+")
+        if head != "AUTO":
+            raise ValueError(f"resume must be True, False or 'AUTO[+...]', got {resume!r}")
+        rc = cls()
+        for s in suffixes:
+            table = {"ERRORED": ("resume", "resume"), "RESTART_ERRORED": ("resume", "restart"),
+                     "ERRORED_ONLY": ("skip", "resume"), "RESTART_ERRORED_ONLY": ("skip", "restart")}
+            if s not in table:
+                raise ValueError(f"Invalid resume setting: {s!r}")
+            rc = cls(unfinished=table[s][0], errored=table[s][1])
+        return rc
 
 
 # ------------------------------------------------------------------------- progress reporting

@@ -539,6 +539,8 @@ class TuneController:
         # TuneConfig.trial_name_creator: the trial's display name (train.get_context().get_trial_name())
         t.trial_name = str(self.tc.trial_name_creator(_TrialView(tid, cfg))) if self.tc.trial_name_creator else name
         os.makedirs(t.local_path, exist_ok=True)
+        if getattr(self, "_initial_restore", None):
+            t.restore_path = self._initial_restore
         self.trials.append(t)
         self.scheduler.on_trial_add(self, t)
         return t
@@ -739,7 +741,7 @@ class TuneController:
                 try:
                     p = get(trial.runner.save.remote(os.path.join(
                         trial.local_path, f"checkpoint_{_next_ckpt_index(trial.local_path):06d}")))
-                    trial.checkpoint = _ckpt(p)
+                    self._register_ckpt(trial, p, trial.last_result)
                 except Exception:
                     pass
             if reuse and self._try_cache(trial):
@@ -815,7 +817,7 @@ class TuneController:
         trial.last_result = m
         trial.metrics_history.append(m)
         if ckpt_path:
-            trial.checkpoint = _ckpt(ckpt_path)
+            self._register_ckpt(trial, ckpt_path, m)
         with open(os.path.join(trial.local_path, "result.json"), "a") as f:
             f.write(json.dumps(_jsonable(m)) + "\n")
         self.searcher.on_trial_result(trial.trial_id, m)
@@ -825,6 +827,28 @@ class TuneController:
         if self._should_stop(trial, m):
             return TrialScheduler.STOP
         return self.scheduler.on_trial_result(self, trial, m)
+
+    def _register_ckpt(self, trial: Trial, path: str, metrics: Dict):
+        """A new persisted checkpoint of ``trial``: it becomes the trial's latest, and
+        CheckpointConfig(num_to_keep, checkpoint_score_attribute) prunes the older ones (the
+        latest always stays, for resume) -- reference: tune/execution/tune_controller.py +
+        train/_internal/checkpoint_manager.py."""
+        from ..train._internal.backend_executor import CheckpointManager
+
+        trial.checkpoint = _ckpt(path)
+        mgr = getattr(trial, "_ckpt_mgr", None)
+        if mgr is None:
+            mgr = trial._ckpt_mgr = CheckpointManager(self.rc.checkpoint_config)
+        mgr.register(trial.checkpoint, dict(metrics or {}))
+
+    def _save_at_end(self, trial: Trial) -> bool:
+        """CheckpointConfig(checkpoint_at_end=True): a class trainable that ends cleanly saves
+        once more unless its last result was just checkpointed."""
+        if self.kind != "class" or not self.rc.checkpoint_config.checkpoint_at_end:
+            return False
+        mgr = getattr(trial, "_ckpt_mgr", None)
+        return not (mgr and mgr.entries and mgr.entries[-1][1].get("training_iteration")
+                    == trial.last_result.get("training_iteration"))
 
     def _complete(self, trial: Trial, err=None):
         if err is not None:
@@ -888,7 +912,7 @@ class TuneController:
                     if ev[0] == "result":
                         decision = self._on_result(t, ev[1], ev[2])
                         if decision == TrialScheduler.STOP:
-                            self._stop_runner(t, reuse=True)
+                            self._stop_runner(t, save=self._save_at_end(t), reuse=True)
                             self._complete(t)
                             break
                         if decision == TrialScheduler.PAUSE:
@@ -900,7 +924,7 @@ class TuneController:
                         if self.kind == "class" and t.status == RUNNING and t.runner is not None:
                             t.pending = t.runner.step.remote()
                     else:
-                        self._stop_runner(t, reuse=ev[1] is None)
+                        self._stop_runner(t, save=ev[1] is None and self._save_at_end(t), reuse=ev[1] is None)
                         self._complete(t, ev[1])
                         break
             self._save_state()
@@ -929,8 +953,10 @@ class TuneController:
     def _results(self):
         out = []
         for t in self.trials:
+            mgr = getattr(t, "_ckpt_mgr", None)
             out.append(Result(metrics=t.last_result or None, checkpoint=t.checkpoint, error=t.error,
-                              path=t.local_path, metrics_history=t.metrics_history))
+                              path=t.local_path, metrics_history=t.metrics_history,
+                              best_checkpoints=list(mgr.entries) if mgr else []))
         return ResultGrid(out, self.tc.metric, self.tc.mode, self.exp_dir)
 
     def _save_state(self):
@@ -1000,6 +1026,7 @@ class Tuner:
         if rep is not None and rep not in (rc.callbacks or []):
             rc.callbacks = list(rc.callbacks or []) + [rep]
         ctrl = TuneController(self.trainable, self.param_space, self.tune_config, rc, exp_dir, self._restored)
+        ctrl._initial_restore = getattr(self, "_initial_restore", None)  # tune.run(restore=<checkpoint dir>)
         grid = ctrl.run()
         for cb in (rc.callbacks or []):
             if hasattr(cb, "on_experiment_end"):
@@ -1033,6 +1060,8 @@ class Tuner:
             elif status == ERROR and not (resume_errored or restart_errored):
                 t.status = ERROR
                 t.error = RuntimeError(d.get("error") or "trial errored")
+            elif status != ERROR and not resume_unfinished:  # ResumeConfig(unfinished=SKIP)
+                t.status = TERMINATED
             else:
                 t.status = PENDING
                 if not restart_errored and t.checkpoint is not None:

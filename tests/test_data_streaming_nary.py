@@ -86,3 +86,19 @@ def test_zip_streams_larger_than_object_store(shutdown_only):
     head = ray._private.worker._state.get("head") if hasattr(ray._private.worker, "_state") else None
     if head is not None:
         assert head.spilled_bytes == 0, head.spilled_bytes
+
+
+def test_union_and_zip_stop_early_without_hanging(ray4):
+    """A limit downstream of a streaming union / zip stops the side inputs' executions too."""
+    def slow(batch):
+        time.sleep(0.05)
+        return batch
+
+    a = ray.data.range(1000, override_num_blocks=50).map_batches(slow, batch_size=None)
+    b = ray.data.range(1000, override_num_blocks=50).map_batches(slow, batch_size=None)
+    t0 = time.time()
+    assert len(a.union(b).limit(25).take_all()) == 25
+    assert len(a.zip(b.map(lambda r: {"w": r["id"]})).limit(7).take_all()) == 7
+    assert time.time() - t0 < 30
+    # the session stays usable after the early stops
+    assert ray.data.range(10).union(ray.data.range(5)).count() == 15

@@ -1,0 +1,149 @@
+"""``tune.run``'s pre-2.7 keyword arguments (reference: python/ray/tune/tune.py:277 and
+tune/tests/test_api.py): local_dir, keep_checkpoints_num / checkpoint_score_attr / checkpoint_freq /
+checkpoint_at_end, resume / resume_config, restore, trial name creators."""
+import json
+import os
+
+import pytest
+
+from ray_community_amd import train, tune
+from ray_community_amd.tune.registry import ResumeConfig
+
+
+class _Counter(tune.Trainable):
+    def setup(self, config):
+        self.n = 0
+
+    def step(self):
+        self.n += 1
+        return {"score": self.n * self.config["k"], "done": self.n >= 4}
+
+    def save_checkpoint(self, d):
+        with open(os.path.join(d, "n.json"), "w") as f:
+            json.dump({"n": self.n}, f)
+
+    def load_checkpoint(self, d):
+        with open(os.path.join(d, "n.json")) as f:
+            self.n = json.load(f)["n"]
+
+
+def _ckpt_dirs(trial_path):
+    return sorted(x for x in os.listdir(trial_path) if x.startswith("checkpoint_"))
+
+
+def test_legacy_checkpoint_kwargs_and_local_dir(ray_start_regular, tmp_path):
+    ana = tune.run(_Counter, name="legacy", config={"k": tune.grid_search([1, 2])}, metric="score", mode="max",
+                   local_dir=str(tmp_path), checkpoint_freq=1, keep_checkpoints_num=2,
+                   checkpoint_score_attr="score", checkpoint_at_end=True,
+                   trial_name_creator=lambda t: f"k{t.config['k']}",
+                   trial_dirname_creator=lambda t: f"dir_k{t.config['k']}")
+    assert ana.best_config["k"] == 2
+    for k in (1, 2):
+        path = tmp_path / "legacy" / f"dir_k{k}"
+        assert path.is_dir()
+        kept = _ckpt_dirs(path)
+        assert 1 <= len(kept) <= 2, kept  # keep_checkpoints_num
+    with pytest.raises(ValueError):
+        tune.run(_Counter, local_dir=str(tmp_path), storage_path=str(tmp_path / "other"))
+    with pytest.raises(TypeError):
+        tune.run(_Counter, not_an_argument=1)
+
+
+def test_checkpoint_score_attr_min_prefix(ray_start_regular, tmp_path):
+    seen = {}
+
+    class _Probe(_Counter):
+        def setup(self, config):
+            super().setup(config)
+
+    ana = tune.run(_Probe, name="minattr", config={"k": 1}, local_dir=str(tmp_path), checkpoint_freq=1,
+                   keep_checkpoints_num=1, checkpoint_score_attr="min-score")
+    trial_dir = ana.trials[0].path
+    seen["kept"] = _ckpt_dirs(trial_dir)
+    # min-score keeps the lowest-score checkpoint (the first) besides the latest one kept for resume
+    assert seen["kept"] and "checkpoint_000000" in seen["kept"]
+
+
+def test_resume_auto_restores_finished_experiment(ray_start_regular, tmp_path):
+    marker = tmp_path / "runs.txt"
+
+    def f(config):
+        with open(marker, "a") as fh:
+            fh.write("x\n")
+        tune.report({"v": config["a"]})
+
+    kw = dict(name="resumable", config={"a": tune.grid_search([1, 2, 3])}, local_dir=str(tmp_path))
+    tune.run(f, resume="AUTO", **kw)  # nothing to resume yet: a fresh run
+    assert marker.read_text().count("x") == 3
+    ana = tune.run(f, resume="AUTO", **kw)  # every trial finished: nothing runs again
+    assert marker.read_text().count("x") == 3
+    assert sorted(t.config["a"] for t in ana.trials) == [1, 2, 3]
+    with pytest.raises(ValueError):
+        tune.run(f, name="never_ran", local_dir=str(tmp_path), resume=True)
+
+
+def test_resume_string_parsing():
+    assert ResumeConfig._from_legacy(False) is None
+    assert ResumeConfig._from_legacy(True)._restore_kwargs() == {
+        "resume_unfinished": True, "resume_errored": False, "restart_errored": False}
+    rc = ResumeConfig._from_legacy("AUTO+RESTART_ERRORED_ONLY")
+    assert (rc.unfinished, rc.errored) == (ResumeConfig.ResumeType.SKIP, ResumeConfig.ResumeType.RESTART)
+    assert ResumeConfig._from_legacy("AUTO+ERRORED")._restore_kwargs()["resume_errored"]
+    with pytest.raises(ValueError):
+        ResumeConfig._from_legacy("AUTO+BOGUS")
+    with pytest.raises(ValueError):
+        ResumeConfig._from_legacy("LOCAL")
+
+
+def test_restore_seeds_every_trial(ray_start_regular, tmp_path):
+    ck = tmp_path / "seed"
+    ck.mkdir()
+    (ck / "state.json").write_text(json.dumps({"start": 10}))
+
+    def f(config):
+        c = train.get_checkpoint()
+        assert c is not None
+        with c.as_directory() as d:
+            start = json.load(open(os.path.join(d, "state.json")))["start"]
+        tune.report({"v": start + config["a"]})
+
+    ana = tune.run(f, name="seeded", config={"a": tune.grid_search([1, 2])}, local_dir=str(tmp_path),
+                   restore=str(ck), metric="v", mode="max")
+    assert sorted(t.last_result["v"] for t in ana.trials) == [11, 12]
+
+
+def test_experiment_analysis_api(ray_start_regular, tmp_path):
+    def f(config):
+        for i in range(4):
+            tune.report({"acc": config["q"] * (i + 1) - (3 if i == 3 else 0)})
+
+    ana = tune.run(f, name="ana", config={"q": tune.grid_search([1.0, 2.0, 3.0])}, local_dir=str(tmp_path),
+                   metric="acc", mode="max")
+    assert ana.best_trial.config["q"] == 3.0 and ana.best_result["acc"] == 9.0
+    assert ana.get_best_trial("acc", "max", scope="all").config["q"] == 3.0
+    assert ana.get_best_trial("acc", "min", scope="avg").config["q"] == 1.0
+    assert set(ana.results) == {t.trial_id for t in ana.trials}
+    assert len(ana.results_df) == 3 and "config/q" in ana.results_df.columns
+    dfs = ana.trial_dataframes
+    assert len(dfs) == 3 and all(len(d) == 4 for d in dfs.values())
+    best_rows = ana.dataframe(metric="acc", mode="max")
+    assert sorted(best_rows["acc"]) == [3.0, 6.0, 9.0]
+    assert len(ana.get_all_configs(prefix=True)) == 3
+    assert ana.best_path == ana.best_trial.path and len(ana.best_dataframe) == 4
+    # the same analysis, loaded back from the experiment directory
+    from ray_community_amd.tune.analysis import ExperimentAnalysis
+
+    again = ExperimentAnalysis(ana.experiment_path, default_metric="acc", default_mode="max")
+    assert again.best_config == ana.best_config and len(again.trials) == 3
+
+
+def test_analysis_best_checkpoint_by_metric(ray_start_regular, tmp_path):
+    ana = tune.run(_Counter, name="bestck", config={"k": -1}, local_dir=str(tmp_path), checkpoint_freq=1,
+                   metric="score", mode="max")
+    trial = ana.trials[0]
+    best = ana.get_best_checkpoint(trial, "score", "max")  # score = -n: the first checkpoint
+    with best.as_directory() as d:
+        assert json.load(open(os.path.join(d, "n.json")))["n"] == 1
+    last = ana.get_last_checkpoint(trial)
+    with last.as_directory() as d:
+        assert json.load(open(os.path.join(d, "n.json")))["n"] == 4
