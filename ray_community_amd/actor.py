@@ -59,8 +59,17 @@ def _class_meta(cls, opts):
             "module": cls.__module__, "max_pending_calls": int(opts.get("max_pending_calls", -1) or -1)}
 
 
+class ActorClassInheritanceException(TypeError):
+    """Raised on ``class B(A)`` where ``A`` is a ``@remote`` actor class: subclass the plain class
+    and decorate the subclass instead."""
+
+
 class ActorClass:
-    def __init__(self, cls, options: Optional[dict] = None):
+    def __init__(self, cls, options: Optional[dict] = None, *extra):
+        if extra or isinstance(cls, str):  # class B(A) with A an ActorClass: type(A)(name, bases, ns)
+            raise ActorClassInheritanceException(
+                f"Cannot inherit from the actor class {getattr(options[0], '__name__', '?') if options else '?'}: "
+                "inherit from the undecorated class and apply @remote to the subclass")
         self._cls = cls
         self._options = dict(options or {})
         bad = set(self._options) - _ACTOR_OPTIONS

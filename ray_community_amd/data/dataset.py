@@ -557,16 +557,17 @@ class Dataset:
     def write_parquet(self, path: str, *, partition_cols: Optional[List[str]] = None, **kw):
         """``partition_cols``: hive layout ``path/col=value/...`` with those columns moved into
         the directory names (reference ``Dataset.write_parquet``); ``read_parquet`` restores them."""
-        self._sized(kw)._write(path, "parquet", partition_cols=list(partition_cols or []))
+        self._sized(kw)._write(path, "parquet", partition_cols=list(partition_cols or []),
+                             filename_provider=kw.get("filename_provider"))
 
     def write_csv(self, path: str, **kw):
-        self._sized(kw)._write(path, "csv")
+        self._sized(kw)._write(path, "csv", filename_provider=kw.get("filename_provider"))
 
     def write_json(self, path: str, **kw):
-        self._sized(kw)._write(path, "json")
+        self._sized(kw)._write(path, "json", filename_provider=kw.get("filename_provider"))
 
     def write_numpy(self, path: str, *, column: str = "data", **kw):
-        self._sized(kw)._write(path, "npy", column=column)
+        self._sized(kw)._write(path, "npy", column=column, filename_provider=kw.get("filename_provider"))
 
     def _sized(self, kw) -> "Dataset":
         """``min_rows_per_file`` / ``num_rows_per_file`` (reference writers): coalesce blocks so
@@ -622,12 +623,15 @@ class Dataset:
 
         return _copy.copy(self)
 
-    def _write(self, path, fmt, column=None, partition_cols=None):
+    def _write(self, path, fmt, column=None, partition_cols=None, filename_provider=None):
+        """One file per block; ``filename_provider`` (a ``FilenameProvider``) names them
+        (``get_filename_for_block(block, task_index, block_index)``), else ``{index:06d}.{fmt}``."""
         from .._private.worker import get
 
         os.makedirs(path, exist_ok=True)
         w = X._remote_fn(_write_block, {"num_cpus": 1})
-        refs = [w.remote(b, path, i, fmt, column, partition_cols)[0] for i, (b, _) in enumerate(self._refs())]
+        refs = [w.remote(b, path, i, fmt, column, partition_cols, filename_provider)[0]
+                for i, (b, _) in enumerate(self._refs())]
         get(refs)
 
     # ------------------------------------------------------------------ misc
@@ -821,11 +825,12 @@ def _pa_table(df):
     return pa.Table.from_pandas(df, preserve_index=False)
 
 
-def _write_block(block, path, i, fmt, column, partition_cols=None):
+def _write_block(block, path, i, fmt, column, partition_cols=None, filename_provider=None):
     acc = BlockAccessor(block)
     if acc.num_rows() == 0:
         return None, {}
-    fn = os.path.join(path, f"{i:06d}.{fmt}")
+    name = filename_provider.get_filename_for_block(block, i, 0) if filename_provider is not None else None
+    fn = os.path.join(path, name or f"{i:06d}.{fmt}")
     if fmt == "parquet" and partition_cols:
         import pyarrow.parquet as pq
 
@@ -838,7 +843,7 @@ def _write_block(block, path, i, fmt, column, partition_cols=None):
             key = key if isinstance(key, tuple) else (key,)
             d = os.path.join(path, *[f"{c}={v}" for c, v in zip(partition_cols, key)])
             os.makedirs(d, exist_ok=True)
-            f = os.path.join(d, f"{i:06d}.parquet")
+            f = os.path.join(d, name or f"{i:06d}.parquet")
             pq.write_table(_pa_table(part.drop(columns=partition_cols).reset_index(drop=True)), f)
             out.append(f)
         return out, {}

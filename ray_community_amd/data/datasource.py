@@ -118,8 +118,12 @@ def read_sql(sql: str, connection_factory: Callable[[], Any], *, parallelism: in
     ``SELECT * FROM (sql) LIMIT n OFFSET k`` over ``SELECT COUNT(*) FROM (sql)`` rows (the query
     must be deterministic for that, as in the reference)."""
     k = override_num_blocks or (parallelism if parallelism and parallelism > 0 else 1)
+    return Dataset([("read", t) for t in _sql_read_tasks(sql, connection_factory, k)])
+
+
+def _sql_read_tasks(sql: str, connection_factory: Callable[[], Any], k: int) -> List[_SQLRead]:
     if k <= 1:
-        return Dataset([("read", _SQLRead(sql, connection_factory))])
+        return [_SQLRead(sql, connection_factory)]
     conn = connection_factory()
     try:
         cur = conn.cursor()
@@ -129,8 +133,7 @@ def read_sql(sql: str, connection_factory: Callable[[], Any], *, parallelism: in
         conn.close()
     k = max(1, min(k, n))
     bounds = [n * i // k for i in range(k + 1)]
-    return Dataset([("read", _SQLRead(sql, connection_factory, bounds[i + 1] - bounds[i], bounds[i]))
-                    for i in range(k)])
+    return [_SQLRead(sql, connection_factory, bounds[i + 1] - bounds[i], bounds[i]) for i in range(k)]
 
 
 class SQLDatasink(Datasink):
@@ -556,3 +559,12 @@ from_tf = _absent("tensorflow")
 read_mongo = _absent("pymongo")
 read_bigquery = _absent("google-cloud-bigquery")
 read_databricks_tables = _absent("databricks-sql-connector")
+
+
+# the datasource / partitioning / filename-provider classes live in their own modules; this module
+# is the ``ray.data.datasource`` import path for all of them (reference datasource/__init__.py)
+from .file_datasources import *  # noqa: E402,F401,F403
+from .file_datasources import __all__ as _file_all  # noqa: E402
+from .partitioning import (FileExtensionFilter, PartitionStyle, Partitioning, PathPartitionFilter,  # noqa: E402,F401
+                           PathPartitionParser)
+from .read_api import Datasource  # noqa: E402,F401

@@ -209,13 +209,23 @@ class _FileRead:
             return b
         else:
             raise ValueError(fmt)
-        if kw.get("partitioning", "hive") == "hive":
+        part = kw.get("partitioning", "hive")
+        if part is not None:
             import pyarrow as pa
 
             cols = kw.get("columns")
-            for k, v in _hive_fields(p, self.base):
+            if part == "hive":
+                fields = _hive_fields(p, self.base)
+            else:  # a Partitioning object (HIVE or DIRECTORY; base_dir defaults to the read root)
+                from .partitioning import Partitioning, PathPartitionParser
+
+                if not part.base_dir and self.base:
+                    part = Partitioning(part.style, self.base, part.field_names, part.field_types)
+                fields = list(PathPartitionParser(part)(p).items())
+            for k, v in fields:
                 if k not in t.column_names and (cols is None or k in cols):
-                    t = t.append_column(k, pa.array([v] * t.num_rows, type=pa.string()))
+                    t = t.append_column(k, pa.array([v] * t.num_rows) if not isinstance(v, str)
+                                        else pa.array([v] * t.num_rows, type=pa.string()))
             if cols is not None and fmt == "parquet":
                 t = t.select([c for c in cols if c in t.column_names])
         if self.include_paths:
@@ -225,30 +235,64 @@ class _FileRead:
         return t
 
 
-def _read(paths, fmt, exts, include_paths=False, **kw) -> Dataset:
+def _read(paths, fmt, exts, include_paths=False, partition_filter=None, file_extensions=None,
+          **kw) -> Dataset:
+    """``partition_filter``: a ``PathPartitionFilter`` pruning files by partition values;
+    ``file_extensions``: overrides the format's default extensions."""
     bases = {}
+    if file_extensions is not None:
+        exts = ["." + e.lstrip(".") for e in ([file_extensions] if isinstance(file_extensions, str)
+                                              else file_extensions)]
     files = _expand_paths(paths, exts, bases)
+    if partition_filter is not None:
+        files = _filter_partitions(partition_filter, files, bases)
     if not files:
         raise ValueError(f"No input files found to read from paths {paths}")
     return Dataset([("read", _FileRead(f, fmt, kw, include_paths, bases.get(f))) for f in files])
 
 
+def _file_kw(kw):
+    """The file-selection options every read_* accepts (``partition_filter``, ``file_extensions``)."""
+    return {k: kw[k] for k in ("partition_filter", "file_extensions") if kw.get(k) is not None}
+
+
+def _filter_partitions(pf, files, bases):
+    """Apply a PathPartitionFilter; its parser's base_dir defaults to each file's read root."""
+    from .partitioning import Partitioning, PathPartitionFilter, PathPartitionParser
+
+    scheme = pf.parser.scheme
+    if scheme.base_dir:
+        return pf(files)
+    keep = []
+    for f in files:
+        parser = PathPartitionParser(Partitioning(scheme.style, bases.get(f, ""), scheme.field_names,
+                                                  scheme.field_types))
+        keep.extend(PathPartitionFilter(parser, pf._fn)([f]))
+    return keep
+
+
 def _partitioning(p):
-    """``partitioning``: "hive" / a reference ``Partitioning("hive")`` object (default) or None."""
+    """``partitioning``: "hive" (default), None, or a ``Partitioning`` (HIVE, or DIRECTORY with
+    ``field_names``); a base_dir-less HIVE scheme without field checks is the plain "hive" path."""
     if p is None:
         return None
-    style = getattr(p, "style", p)
-    style = getattr(style, "value", style)
-    if str(style).lower() != "hive":
-        raise NotImplementedError(f"only hive partitioning is supported, got {p!r}")
-    return "hive"
+    from .partitioning import Partitioning, PartitionStyle
+
+    if isinstance(p, Partitioning):
+        if p.style == PartitionStyle.HIVE and not p.base_dir and not p.field_names and not p.field_types:
+            return "hive"
+        return p
+    style = getattr(p, "value", p)
+    if str(style).lower() == "hive":
+        return "hive"
+    raise ValueError(f"partitioning must be 'hive', None or a Partitioning, got {p!r}")
 
 
 def read_parquet(paths, *, columns=None, include_paths=False, partitioning="hive", filter=None, **kw) -> Dataset:
     """Parquet files; hive ``col=value`` directories become string columns (reference default
     ``Partitioning("hive")``); ``filter``: a pyarrow filter expression / DNF list."""
     return _read(paths, "parquet", [".parquet"], include_paths, columns=columns, filter=filter,
-                 partitioning=_partitioning(partitioning))
+                 partitioning=_partitioning(partitioning), **_file_kw(kw))
 
 
 def read_csv(paths, *, include_paths=False, partitioning="hive", parse_options=None, read_options=None,
@@ -256,30 +300,32 @@ def read_csv(paths, *, include_paths=False, partitioning="hive", parse_options=N
     """CSV files through ``pyarrow.csv`` (``parse_options`` / ``read_options`` / ``convert_options``
     forwarded, e.g. ``ParseOptions(delimiter="\t")``)."""
     return _read(paths, "csv", [".csv"], include_paths, partitioning=_partitioning(partitioning),
-                 parse_options=parse_options, read_options=read_options, convert_options=convert_options)
+                 parse_options=parse_options, read_options=read_options, convert_options=convert_options,
+                 **_file_kw(kw))
 
 
 def read_json(paths, *, include_paths=False, partitioning="hive", parse_options=None, read_options=None,
               **kw) -> Dataset:
     return _read(paths, "json", [".json", ".jsonl"], include_paths, partitioning=_partitioning(partitioning),
-                 parse_options=parse_options, read_options=read_options)
+                 parse_options=parse_options, read_options=read_options, **_file_kw(kw))
 
 
 def read_text(paths, *, encoding="utf-8", drop_empty_lines=True, include_paths=False, **kw) -> Dataset:
-    return _read(paths, "text", None, include_paths, encoding=encoding, drop_empty_lines=drop_empty_lines)
+    return _read(paths, "text", None, include_paths, encoding=encoding, drop_empty_lines=drop_empty_lines,
+                 **_file_kw(kw))
 
 
 def read_numpy(paths, **kw) -> Dataset:
-    return _read(paths, "numpy", [".npy"])
+    return _read(paths, "numpy", [".npy"], **_file_kw(kw))
 
 
 def read_binary_files(paths, *, include_paths=False, **kw) -> Dataset:
-    return _read(paths, "binary", None, include_paths)
+    return _read(paths, "binary", None, include_paths, **_file_kw(kw))
 
 
 def read_images(paths, *, size=None, mode="RGB", include_paths=False, **kw) -> Dataset:
     return _read(paths, "images", [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".tif", ".tiff"], include_paths,
-                 size=size, mode=mode)
+                 size=size, mode=mode, **_file_kw(kw))
 
 
 def read_datasource(datasource, *, parallelism: int = -1, **read_args) -> Dataset:

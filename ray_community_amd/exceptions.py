@@ -218,3 +218,30 @@ class RayChannelTimeoutError(RayChannelError, TimeoutError):
 
 RAY_EXCEPTION_TYPES = [RayError, RayTaskError, WorkerCrashedError, RayActorError, ObjectStoreFullError, ObjectLostError,
                        GetTimeoutError, TaskCancelledError]
+
+
+class UserCodeException(RayError):
+    """An exception raised by user code (a task / actor body); retry_exceptions looks at its cause."""
+
+
+class RpcError(RayError):
+    """An error of the control-plane RPC layer."""
+
+    def __init__(self, message, rpc_code=None):
+        self.message = message
+        self.rpc_code = rpc_code
+
+    def __str__(self):
+        return self.message
+
+
+class ObjectFreedError(ObjectLostError):
+    """The object was freed explicitly (``ray.internal.free``) while a reference still existed."""
+
+
+class PlasmaObjectNotAvailable(RayError):
+    """An object was not available within the given timeout."""
+
+
+class ObjectRefStreamEndOfStreamError(RayError):
+    """A streaming generator has no more ObjectRefs to hand out."""

@@ -45,7 +45,11 @@ class RuntimeContext:
         return self._core.actor_id
 
     def get_actor_name(self):
-        return None
+        """The current actor's name (None outside an actor or for an anonymous one)."""
+        if self._core.actor_id is None:
+            return None
+        info = self._core.client.call("actor_info", self._core.actor_id)
+        return (info or {}).get("name") or None
 
     @property
     def namespace(self):
@@ -120,3 +124,10 @@ class RuntimeContext:
     @property
     def pid(self):
         return os.getpid()
+
+
+def get_runtime_context() -> RuntimeContext:
+    """The runtime context of the calling driver / task / actor (reference module-level API)."""
+    from ._private.worker import get_runtime_context as _g
+
+    return _g()

@@ -358,9 +358,21 @@ def status():
 
 
 class _ServeStatus(dict):
+    """``serve.status()``: the reference ``ServeStatus`` attributes (``applications`` ->
+    ``status`` / ``message`` / ``deployments`` -> ``status`` / ``replica_states`` / ``message``)
+    over the controller's plain dict, which stays readable by key."""
+
     @property
     def applications(self):
         return {k: _AppStatus(v) for k, v in self.items()}
+
+    @property
+    def proxies(self):
+        return {}
+
+    @property
+    def target_capacity(self):
+        return None
 
 
 class _AppStatus(dict):
@@ -369,8 +381,26 @@ class _AppStatus(dict):
         return self["status"]
 
     @property
+    def message(self):
+        return self.get("message") or ""
+
+    @property
     def deployments(self):
-        return self["deployments"]
+        return {k: _DeploymentStatus(v) for k, v in self["deployments"].items()}
+
+
+class _DeploymentStatus(dict):
+    @property
+    def status(self):
+        return self["status"]
+
+    @property
+    def message(self):
+        return self.get("message") or ""
+
+    @property
+    def replica_states(self):
+        return {"RUNNING": int(self.get("replicas", 0))}
 
 
 def shutdown():

@@ -118,3 +118,5 @@ class gRPCOptions:
                 f = getattr(importlib.import_module(mod), name)
             out.append(f)
         return out
+
+from .schema import ProxyLocation  # noqa: E402,F401  (reference exports it from serve.config too)

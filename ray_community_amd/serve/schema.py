@@ -204,3 +204,114 @@ def parse_config(obj: Union[str, Dict[str, Any]]) -> ServeDeploySchema:
     if "import_path" in obj and "applications" not in obj:
         obj = {"applications": [obj]}
     return ServeDeploySchema.model_validate(obj)
+
+
+# ============================================================================ status / details models
+# (reference schema.py: ServeStatus, ApplicationStatusOverview, DeploymentStatusOverview and the
+# ServeInstanceDetails tree the dashboard's GET /api/serve/applications/ returns)
+class EncodingType(str, Enum):
+    TEXT = "TEXT"
+    JSON = "JSON"
+
+
+class _Details(BaseModel):
+    model_config = ConfigDict(extra="allow", populate_by_name=True)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return self.model_dump(mode="json")
+
+
+class DeploymentStatusOverview(_Details):
+    status: Optional[str] = None
+    status_trigger: Optional[str] = None
+    replica_states: Dict[str, int] = Field(default_factory=dict)
+    message: str = ""
+
+
+class ApplicationStatusOverview(_Details):
+    status: Optional[str] = None
+    message: str = ""
+    last_deployed_time_s: Optional[float] = None
+    deployments: Dict[str, DeploymentStatusOverview] = Field(default_factory=dict)
+
+
+class ServeStatus(_Details):
+    proxies: Dict[str, str] = Field(default_factory=dict)
+    applications: Dict[str, ApplicationStatusOverview] = Field(default_factory=dict)
+    target_capacity: Optional[float] = None
+
+
+class ServeActorDetails(_Details):
+    node_id: Optional[str] = None
+    node_ip: Optional[str] = None
+    actor_id: Optional[str] = None
+    actor_name: Optional[str] = None
+    worker_id: Optional[str] = None
+    log_file_path: Optional[str] = None
+
+
+class ReplicaDetails(ServeActorDetails):
+    replica_id: str
+    state: str
+    pid: Optional[int] = None
+    start_time_s: Optional[float] = None
+
+
+class ProxyDetails(ServeActorDetails):
+    status: str
+
+
+class DeploymentDetails(_Details):
+    name: str
+    status: Optional[str] = None
+    status_trigger: Optional[str] = None
+    message: str = ""
+    deployment_config: Dict[str, Any] = Field(default_factory=dict)
+    target_num_replicas: Optional[int] = None
+    replicas: List[ReplicaDetails] = Field(default_factory=list)
+
+
+class ApplicationDetails(_Details):
+    name: str
+    route_prefix: Optional[str] = None
+    docs_path: Optional[str] = None
+    status: Optional[str] = None
+    message: str = ""
+    last_deployed_time_s: Optional[float] = None
+    deployed_app_config: Optional[Dict[str, Any]] = None
+    deployments: Dict[str, DeploymentDetails] = Field(default_factory=dict)
+
+
+class ServeInstanceDetails(_Details):
+    controller_info: Dict[str, Any] = Field(default_factory=dict)
+    proxy_location: Optional[str] = None
+    http_options: Optional[Dict[str, Any]] = None
+    grpc_options: Optional[Dict[str, Any]] = None
+    proxies: Dict[str, ProxyDetails] = Field(default_factory=dict)
+    deploy_mode: str = "MULTI_APP"
+    applications: Dict[str, ApplicationDetails] = Field(default_factory=dict)
+    target_capacity: Optional[float] = None
+
+    @staticmethod
+    def get_empty_schema_dict() -> Dict[str, Any]:
+        """The body of a Serve instance with nothing deployed."""
+        return {"controller_info": {}, "proxies": {}, "applications": {}, "deploy_mode": "MULTI_APP",
+                "target_capacity": None}
+
+    def _get_status(self) -> ServeStatus:
+        return ServeStatus(
+            target_capacity=self.target_capacity,
+            proxies={k: p.status for k, p in self.proxies.items()},
+            applications={name: ApplicationStatusOverview(
+                status=a.status, message=a.message, last_deployed_time_s=a.last_deployed_time_s,
+                deployments={dn: DeploymentStatusOverview(
+                    status=d.status, message=d.message,
+                    replica_states=_count_states(d.replicas)) for dn, d in a.deployments.items()})
+                for name, a in self.applications.items()})
+
+
+def _count_states(replicas) -> Dict[str, int]:
+    out: Dict[str, int] = {}
+    for r in replicas:
+        out[r.state] = out.get(r.state, 0) + 1
+    return out

@@ -260,23 +260,95 @@ class TBXLoggerCallback(LoggerCallback):
             w.close()
 
 
+class _LogTarget:
+    """What the logger callbacks read from a trial, for a ``Logger`` built as
+    ``Logger(config, logdir)`` without one."""
+
+    def __init__(self, config, logdir, trial):
+        self.trial_id = getattr(trial, "trial_id", None) or logdir
+        self.local_path = getattr(trial, "local_path", None) or logdir
+        self.config = config
+
+
 class CSVLogger(Logger):
     def _init(self):
         self._cb = CSVLoggerCallback()
+        self._t = _LogTarget(self.config, self.logdir, self.trial)
 
     def on_result(self, result):
-        self._cb.log_trial_result(0, self.trial, result)
+        self._cb.log_trial_result(0, self._t, result)
 
     def close(self):
-        self._cb.log_trial_end(self.trial)
+        self._cb.log_trial_end(self._t)
 
 
 class JsonLogger(Logger):
     def _init(self):
-        JsonLoggerCallback().log_trial_start(self.trial)
+        JsonLoggerCallback().log_trial_start(_LogTarget(self.config, self.logdir, self.trial))
 
     def on_result(self, result):
         pass
+
+    def update_config(self, config):
+        self.config = config
+        JsonLoggerCallback().log_trial_start(_LogTarget(config, self.logdir, self.trial))
+
+
+class TBXLogger(Logger):
+    """TensorBoard scalars for one trial (reference tune/logger/tensorboardx.py)."""
+
+    def _init(self):
+        self._cb = TBXLoggerCallback()
+        self._t = _LogTarget(self.config, self.logdir, self.trial)
+
+    def on_result(self, result):
+        self._cb.log_trial_result(0, self._t, result)
+
+    def close(self):
+        self._cb.log_trial_end(self._t)
+
+
+class NoopLogger(Logger):
+    def on_result(self, result):
+        pass
+
+
+class UnifiedLogger(Logger):
+    """Fans results out to ``loggers`` (default JSON, CSV and TensorBoard), reference
+    tune/logger/unified.py."""
+
+    def __init__(self, config: Dict, logdir: str, trial=None, loggers=None):
+        self._logger_cls_list = list(loggers) if loggers is not None else [JsonLogger, CSVLogger, TBXLogger]
+        super().__init__(config, logdir, trial)
+
+    def _init(self):
+        self._loggers = [cls(self.config, self.logdir, self.trial) for cls in self._logger_cls_list]
+
+    def on_result(self, result):
+        for lg in self._loggers:
+            lg.on_result(result)
+
+    def update_config(self, config):
+        for lg in self._loggers:
+            lg.update_config(config)
+
+    def close(self):
+        for lg in self._loggers:
+            lg.close()
+
+    def flush(self):
+        for lg in self._loggers:
+            lg.flush()
+
+
+def pretty_print(result: Dict, exclude=None) -> str:
+    """A result dict as YAML without ``config`` / ``hist_stats`` (and ``exclude`` keys), values
+    that JSON cannot hold shown as their repr (reference tune/logger/logger.py:pretty_print)."""
+    import yaml
+
+    out = {k: v for k, v in result.items()
+           if v is not None and k not in ("config", "hist_stats") and (exclude is None or k not in exclude)}
+    return yaml.safe_dump(json.loads(json.dumps(_jsonable(out))), default_flow_style=False)
 
 
 def default_logger_callbacks(existing) -> list:
@@ -294,4 +366,5 @@ def default_logger_callbacks(existing) -> list:
 
 
 __all__ = ["Logger", "LoggerCallback", "LegacyLoggerCallback", "CSVLoggerCallback", "JsonLoggerCallback",
-           "TBXLoggerCallback", "CSVLogger", "JsonLogger", "DEFAULT_LOGGERS", "default_logger_callbacks"]
+           "TBXLoggerCallback", "CSVLogger", "JsonLogger", "TBXLogger", "NoopLogger", "UnifiedLogger", "pretty_print",
+           "DEFAULT_LOGGERS", "default_logger_callbacks"]

@@ -70,11 +70,21 @@ def placement_group(bundles: List[Dict[str, float]], strategy: str = "PACK", nam
                     _soft_target_node_id: Optional[str] = None) -> PlacementGroup:
     from .._private.worker import _core
 
+    validate_placement_group(bundles, strategy, lifetime, _max_cpu_fraction_per_node, _soft_target_node_id)
+    norm = [{k: float(v) for k, v in b.items()} for b in bundles]
+    pid = PlacementGroupID(new_id())
+    _core().client.call("create_pg", pid.binary(), norm, strategy, name, lifetime)
+    return PlacementGroup(pid, norm, strategy)
+
+
+def validate_placement_group(bundles: List[Dict[str, float]], strategy: str = "PACK", lifetime: Optional[str] = None,
+                             _max_cpu_fraction_per_node: float = 1.0,
+                             _soft_target_node_id: Optional[str] = None) -> bool:
+    """Check ``placement_group`` arguments; raises ValueError on invalid ones, True otherwise."""
     if strategy not in VALID_STRATEGIES:
         raise ValueError(f"Invalid placement group strategy {strategy}. Supported strategies are: {VALID_STRATEGIES}.")
     if not bundles:
         raise ValueError("The placement group `bundles` argument cannot contain an empty list")
-    norm = []
     for b in bundles:
         if not isinstance(b, dict) or not b:
             raise ValueError(f"Bundles must be non-empty dicts, got {b!r}")
@@ -83,12 +93,13 @@ def placement_group(bundles: List[Dict[str, float]], strategy: str = "PACK", nam
         for k, v in b.items():
             if v < 0:
                 raise ValueError("resource quantities must be >= 0")
-        norm.append({k: float(v) for k, v in b.items()})
     if lifetime not in (None, "detached"):
         raise ValueError("placement group `lifetime` argument must be either `None` or 'detached'")
-    pid = PlacementGroupID(new_id())
-    _core().client.call("create_pg", pid.binary(), norm, strategy, name, lifetime)
-    return PlacementGroup(pid, norm, strategy)
+    if not 0 < _max_cpu_fraction_per_node <= 1:
+        raise ValueError("_max_cpu_fraction_per_node must be in (0, 1]")
+    if _soft_target_node_id is not None and strategy != "STRICT_PACK":
+        raise ValueError("_soft_target_node_id only works with STRICT_PACK placement groups")
+    return True
 
 
 def remove_placement_group(placement_group: PlacementGroup):
