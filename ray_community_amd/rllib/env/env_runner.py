@@ -32,7 +32,11 @@ class EnvRunner:
         self.seed = None if seed is None else int(seed) + 1000 * worker_index
         if self.seed is not None:
             torch.manual_seed(self.seed)
-        self.env = make_vector_env(config["env"], config.get("num_envs_per_env_runner", 1), config.get("env_config"),
+        from .env_context import EnvContext
+
+        self.env_context = EnvContext(config.get("env_config") or {}, worker_index=worker_index,
+                                      remote=worker_index > 0, num_workers=config.get("num_env_runners", 0))
+        self.env = make_vector_env(config["env"], config.get("num_envs_per_env_runner", 1), self.env_context,
                                    seed=self.seed)
         self.N = self.env.num_envs
         from ..connectors import VectorEnvContext, build_env_to_module, build_module_to_env
@@ -76,7 +80,7 @@ class EnvRunner:
         self._cb_step = overrides(self.callbacks, "on_episode_step")
         self.new_custom_metrics = []
         if self.callbacks is not None:
-            self.callbacks.on_environment_created(env_runner=self, env=self.env, env_context=config.get("env_config"))
+            self.callbacks.on_environment_created(env_runner=self, env=self.env, env_context=self.env_context)
             self._eps = [Episode(i) for i in range(self.N)]
             for i, ep in enumerate(self._eps):
                 self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i)

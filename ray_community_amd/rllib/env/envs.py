@@ -310,7 +310,9 @@ class SingleToVector(VectorEnv):
 
 
 def make_vector_env(env, num_envs: int, env_config: Optional[dict] = None, seed=None) -> VectorEnv:
-    cfg = dict(env_config or {})
+    from .env_context import EnvContext
+
+    cfg = env_config if isinstance(env_config, EnvContext) else dict(env_config or {})
     if isinstance(env, str):
         if env in _REGISTRY:
             return SingleToVector(lambda: _REGISTRY[env](cfg), num_envs, seed)

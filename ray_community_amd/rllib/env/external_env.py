@@ -69,6 +69,7 @@ class ExternalEnv(threading.Thread):
             if len(self._episodes) >= self.max_concurrent:
                 raise ValueError(f"too many concurrent episodes (max_concurrent={self.max_concurrent})")
             self._episodes[eid] = _Episode(eid, training_enabled)
+            self._episodes[eid].reward = self._zero_reward()
         return eid
 
     def get_action(self, episode_id: str, observation):
@@ -86,7 +87,15 @@ class ExternalEnv(threading.Thread):
 
     def log_returns(self, episode_id: str, reward: float, info: Optional[Dict] = None):
         with self._cv:
-            self._episodes[episode_id].reward += float(reward)
+            ep = self._episodes[episode_id]
+            ep.reward = self._add_reward(ep.reward, reward)
+
+    # reward accumulation between two polls: a float here, a per-agent dict in the multi-agent env
+    def _zero_reward(self):
+        return 0.0
+
+    def _add_reward(self, acc, reward):
+        return acc + float(reward)
 
     def end_episode(self, episode_id: str, observation):
         with self._cv:
@@ -120,13 +129,13 @@ class _ExternalBaseEnv(BaseEnv):
             for eid, ep in env._episodes.items():
                 if ep.pending_obs is not None:
                     obs[eid], rew[eid], term[eid], trunc[eid], infos[eid] = ep.pending_obs, ep.reward, False, False, {}
-                    ep.reward = 0.0
+                    ep.reward = env._zero_reward()
                     ep.pending_obs = None
                 elif ep.logged_action is not None:
                     o, a = ep.logged_action
                     obs[eid], rew[eid], term[eid], trunc[eid], infos[eid] = o, ep.reward, False, False, {}
                     off[eid] = a
-                    ep.reward = 0.0
+                    ep.reward = env._zero_reward()
                     ep.logged_action = None
         return obs, rew, term, trunc, infos, off
 
@@ -135,3 +144,18 @@ class _ExternalBaseEnv(BaseEnv):
             ep = self.env._episodes.get(eid)
             if ep is not None:
                 ep.action_q.put(a)
+
+
+class ExternalMultiAgentEnv(ExternalEnv):
+    """Multi-agent external env (reference rllib/env/external_multi_agent_env.py): observations and
+    actions are ``{agent_id: ...}`` dicts and ``log_returns`` takes ``{agent_id: reward}``, summed
+    per agent until the next action request."""
+
+    def _zero_reward(self):
+        return {}
+
+    def _add_reward(self, acc, reward):
+        out = dict(acc)
+        for aid, r in dict(reward).items():
+            out[aid] = out.get(aid, 0.0) + float(r)
+        return out

@@ -94,3 +94,5 @@ class JsonReader:
 
 
 from .dataset_reader import DatasetReader, get_dataset_and_shards, write_dataset_rows  # noqa: E402
+from .io import (D4RLReader, DatasetWriter, FeatureImportance, InputReader, IOContext, MixedInput,  # noqa: E402
+                 NoopOutput, OutputWriter, ShuffledInput, get_offline_io_resource_bundles)

@@ -80,3 +80,43 @@ class TorchPolicy(Policy):
 class TFPolicy(Policy):
     def __init__(self, *a, **k):
         raise ImportError("TensorFlow is not installed: use TorchPolicy / the torch RLModules")
+
+
+def build_policy_class(name: str, framework: str = "torch", *, loss_fn=None, get_default_config=None,
+                       optimizer_fn=None, stats_fn=None, make_model=None, mixins=None, **kw):
+    """A ``TorchPolicy`` subclass named ``name`` (reference rllib/policy/policy_template.py):
+    ``loss_fn(policy, model, dist_class, train_batch) -> loss`` drives ``learn_on_batch`` with the
+    optimizer from ``optimizer_fn(policy, config)`` (Adam at ``config["lr"]`` by default)."""
+    if framework != "torch":
+        raise ImportError(f"framework={framework!r} is not installed here; only torch policies can be built")
+
+    def _init(self, observation_space, action_space, config=None):
+        cfg = dict(get_default_config() if get_default_config else {})
+        cfg.update(config or {})
+        model = make_model(self, observation_space, action_space, cfg) if make_model else None
+        TorchPolicy.__init__(self, observation_space, action_space, cfg, model=model)
+        import torch
+
+        self._optimizer = optimizer_fn(self, self.config) if optimizer_fn else \
+            torch.optim.Adam(self.model.parameters(), lr=float(self.config.get("lr", 1e-3)))
+
+    def learn_on_batch(self, samples):
+        import torch
+
+        if loss_fn is None:
+            raise NotImplementedError(f"{name} was built without a loss_fn")
+        dev = next(self.model.parameters()).device
+        batch = {k: torch.as_tensor(v, device=dev) for k, v in samples.items()}
+        loss = loss_fn(self, self.model, None, batch)
+        self._optimizer.zero_grad()
+        loss.backward()
+        self._optimizer.step()
+        stats = stats_fn(self, batch) if stats_fn else {}
+        return {"learner_stats": dict(stats, total_loss=float(loss.detach()))}
+
+    bases = tuple(mixins or ()) + (TorchPolicy,)
+    return type(name, bases, {"__init__": _init, "learn_on_batch": learn_on_batch})
+
+
+def build_tf_policy(*a, **k):
+    raise ImportError("TensorFlow is not installed: use build_policy_class(..., framework='torch')")
