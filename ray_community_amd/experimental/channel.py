@@ -126,6 +126,123 @@ class Channel:
                 pass
 
 
+class ReaderInterface:
+    """Reads one value per execution from a list of input channels (reference
+    experimental/channel/common.py). ``read()`` returns the values in channel order."""
+
+    def __init__(self, input_channels, reader_index: int = 0):
+        self._channels = list(input_channels)
+        self._idx = reader_index
+        self._closed = False
+
+    def start(self):
+        pass
+
+    def read(self, timeout: Optional[float] = None) -> list:
+        if self._closed:
+            raise RayChannelErrorClosed("reader is closed")
+        return [c.read(self._idx, timeout) for c in self._channels]
+
+    def close(self):
+        self._closed = True
+
+
+class SynchronousReader(ReaderInterface):
+    pass
+
+
+class AwaitableBackgroundReader(ReaderInterface):
+    """Reads on a background thread; ``read()`` / ``await read_async()`` hand out the values."""
+
+    def __init__(self, input_channels, reader_index: int = 0):
+        super().__init__(input_channels, reader_index)
+        import queue
+        import threading
+
+        self._q: "queue.Queue" = queue.Queue(maxsize=1)
+        self._t = threading.Thread(target=self._loop, daemon=True)
+
+    def start(self):
+        self._t.start()
+
+    def _loop(self):
+        import queue
+
+        while not self._closed:
+            try:
+                v = ReaderInterface.read(self, timeout=0.5)
+            except ChannelTimeoutError:
+                continue
+            except Exception as e:  # noqa
+                v = e
+            while not self._closed:  # a bounded hand-off that still notices close()
+                try:
+                    self._q.put(v, timeout=0.5)
+                    break
+                except queue.Full:
+                    continue
+            if isinstance(v, Exception):
+                return
+
+    def read(self, timeout: Optional[float] = None) -> list:
+        import queue
+
+        try:
+            v = self._q.get(timeout=timeout)
+        except queue.Empty:
+            raise ChannelTimeoutError("channel read timed out")
+        if isinstance(v, Exception):
+            raise v
+        return v
+
+    async def read_async(self) -> list:
+        import asyncio
+
+        return await asyncio.get_running_loop().run_in_executor(None, self.read)
+
+    def close(self):
+        """Stop the background thread (it re-checks within its 0.5 s read timeout) before the
+        channels can be torn down."""
+        self._closed = True
+        if self._t.is_alive():
+            self._t.join(timeout=5.0)
+
+
+class WriterInterface:
+    def __init__(self, output_channels):
+        self._channels = list(output_channels)
+        self._closed = False
+
+    def start(self):
+        pass
+
+    def write(self, value, timeout: Optional[float] = None):
+        for c in self._channels:
+            c.write(value, timeout)
+
+    def close(self):
+        self._closed = True
+        for c in self._channels:
+            c.close()
+
+
+class SynchronousWriter(WriterInterface):
+    pass
+
+
+class AwaitableBackgroundWriter(WriterInterface):
+    """``await write_async(v)`` hands the value to a background thread that writes it."""
+
+    async def write_async(self, value):
+        import asyncio
+
+        await asyncio.get_running_loop().run_in_executor(None, self.write, value)
+
+
+class RayChannelErrorClosed(RuntimeError):
+    pass
+
+
 def _attach(name, capacity, num_readers):
     return Channel(capacity, num_readers, _name=name)
 

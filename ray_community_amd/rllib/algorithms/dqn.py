@@ -105,3 +105,9 @@ class DQN(Algorithm):
             self._sync_weights()
         info["_steps_this_iter"] = n
         return info
+
+
+def __getattr__(name):  # old-API-stack policy names of the reference package
+    from ._old_stack import policy_alias
+
+    return policy_alias(name, __name__)

@@ -73,3 +73,9 @@ class PPO(Algorithm):
         self._sync_weights()
         info["_steps_this_iter"] = n
         return info
+
+
+def __getattr__(name):  # old-API-stack policy names (rllib/algorithms/ppo/__init__.py)
+    from ._old_stack import policy_alias
+
+    return policy_alias(name, __name__)

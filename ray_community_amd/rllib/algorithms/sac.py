@@ -71,3 +71,9 @@ class SAC(Algorithm):
         info["_steps_this_iter"] = n
         info["num_updates"] = self._updates
         return info
+
+
+def __getattr__(name):  # old-API-stack policy names of the reference package
+    from ._old_stack import policy_alias
+
+    return policy_alias(name, __name__)

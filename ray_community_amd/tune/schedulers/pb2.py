@@ -76,3 +76,12 @@ class PB2(PopulationBasedTraining):
             lo, hi = self.bounds[k]
             new[k] = float(lo + u * (hi - lo))
         return self.custom_explore_fn(new) if self.custom_explore_fn else new
+
+
+def import_pb2_dependencies():
+    """(GPy, sklearn) in the reference; the GP here is sklearn's, so GPy is None."""
+    try:
+        import sklearn
+    except ImportError:
+        sklearn = None
+    return None, sklearn

@@ -75,3 +75,6 @@ class TuneBOHB(TPESearch):
         self._n_startup = 0
         cfg = super().suggest(trial_id)
         return cfg
+
+
+BOHB = TuneBOHB  # the short name of the reference package

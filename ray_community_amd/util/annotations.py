@@ -29,6 +29,13 @@ def DeveloperAPI(*args, **kwargs):
     return lambda obj: _annotate(obj, "DeveloperAPI")
 
 
+class RayDeprecationWarning(DeprecationWarning):
+    """Warning category of deprecated Ray APIs (shown by default, unlike DeprecationWarning)."""
+
+
+warnings.simplefilter("module", RayDeprecationWarning)
+
+
 def Deprecated(*args, **kwargs):
     message = kwargs.get("message")
 
@@ -38,7 +45,7 @@ def Deprecated(*args, **kwargs):
 
         @functools.wraps(obj)
         def inner(*a, **k):
-            warnings.warn(f"{obj.__name__} is deprecated. {message or ''}", DeprecationWarning, stacklevel=2)
+            warnings.warn(f"{obj.__name__} is deprecated. {message or ''}", RayDeprecationWarning, stacklevel=2)
             return obj(*a, **k)
 
         return _annotate(inner, "Deprecated", message)

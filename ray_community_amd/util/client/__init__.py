@@ -75,3 +75,32 @@ def is_connected() -> bool:
     from ..._private import worker
 
     return bool(worker._state.get("client_mode")) and worker._state.get("core") is not None
+
+
+def num_connected_contexts() -> int:
+    """Client contexts this process holds (0 or 1: one ``ray://`` session per process here)."""
+    from ..._private import worker as w
+
+    core = w._state.get("core")
+    return 1 if core is not None and isinstance(core, RemoteCoreWorker) else 0
+
+
+class RayAPIStub:
+    """The ``ray.util.client.ray`` object of the reference: ``connect(address)`` /
+    ``disconnect()`` / ``is_connected()`` around ``init("ray://...")``."""
+
+    def connect(self, conn_str: str, namespace: str = None, **kw):
+        from ..._private import worker as w
+
+        return w.init(conn_str if conn_str.startswith("ray://") else "ray://" + conn_str, namespace=namespace, **kw)
+
+    def disconnect(self):
+        from ..._private import worker as w
+
+        w.shutdown()
+
+    def is_connected(self) -> bool:
+        return num_connected_contexts() > 0
+
+
+ray = RayAPIStub()

@@ -1,0 +1,158 @@
+"""Round-5 API surface, part 3 (reference: rllib/models, rllib/execution, old-stack policy names,
+data/aggregate.py AggregateFn + Quantile, experimental/channel reader/writer interfaces,
+util/annotations.RayDeprecationWarning, util/client, air/integrations, autoscaler/sdk,
+tune.search.optuna / hyperopt, train.base_trainer)."""
+import importlib
+import queue
+import warnings
+
+import numpy as np
+import pytest
+
+import ray_community_amd as ray
+
+
+def test_custom_aggregate_fn_and_quantile(ray_start_regular):
+    from ray_community_amd.data.aggregate import AggregateFn, Quantile
+
+    ds = ray.data.from_items([{"g": i % 3, "v": i} for i in range(30)])
+    mean_fn = AggregateFn(init=lambda k: [0, 0], accumulate_row=lambda a, r: [a[0] + r["v"], a[1] + 1],
+                          merge=lambda a, b: [a[0] + b[0], a[1] + b[1]], finalize=lambda a: a[0] / a[1],
+                          name="avg")
+    rows = ds.groupby("g").aggregate(mean_fn, Quantile("v", q=0.5)).take_all()
+    assert [(r["g"], r["avg"], r["quantile(v)"]) for r in rows] == [(0, 13.5, 13.5), (1, 14.5, 14.5),
+                                                                     (2, 15.5, 15.5)]
+    total = AggregateFn(lambda k: 0, lambda a, b: a + b, "total",
+                        accumulate_block=lambda a, df: a + int(df["v"].sum()))
+    assert ds.aggregate(total) == {"total": 435}
+    with pytest.raises(ValueError):
+        AggregateFn(init=lambda k: 0, merge=lambda a, b: a, name="x")  # no accumulate_*
+
+
+def test_rllib_models_catalog():
+    import torch
+
+    from ray_community_amd.rllib.models import MODEL_DEFAULTS, ModelCatalog, TorchModelV2
+    from ray_community_amd.rllib.utils.spaces import Box, Dict, Discrete
+
+    obs, act = Box(-1, 1, (4,), np.float32), Discrete(3)
+    dist, n = ModelCatalog.get_action_dist(act, {})
+    model = ModelCatalog.get_model_v2(obs, act, n, {"fcnet_hiddens": [16]})
+    logits, _ = model({"obs": torch.zeros(5, 4)})
+    assert logits.shape == (5, 3) and model.value_function().shape == (5,)
+    d = dist(logits)
+    ent = d.entropy()
+    assert d.sample().shape == (5,) and bool(((ent > 0) & (ent <= np.log(3.0) + 1e-6)).all())
+
+    class Tiny(TorchModelV2, torch.nn.Module):
+        def __init__(self, obs_space, action_space, num_outputs, model_config, name, scale=1.0):
+            torch.nn.Module.__init__(self)
+            TorchModelV2.__init__(self, obs_space, action_space, num_outputs, model_config, name)
+            self.lin = torch.nn.Linear(4, num_outputs)
+            self.scale = scale
+
+        def forward(self, input_dict, state, seq_lens):
+            return self.scale * self.lin(input_dict["obs"]), state
+
+        def value_function(self):
+            return torch.zeros(1)
+
+    ModelCatalog.register_custom_model("tiny", Tiny)
+    m = ModelCatalog.get_model_v2(obs, act, 3, {"custom_model": "tiny", "custom_model_config": {"scale": 2.0}})
+    assert isinstance(m, Tiny) and m.scale == 2.0 and len(m.trainable_variables()) == 2
+    pre = ModelCatalog.get_preprocessor_for_space(Dict({"a": Discrete(2), "b": Box(-1, 1, (3,), np.float32)}))
+    assert pre.shape == (5,) and pre.transform({"a": 1, "b": np.zeros(3)}).tolist() == [0, 1, 0, 0, 0]
+    assert MODEL_DEFAULTS["fcnet_hiddens"] == [256, 256]
+
+
+def test_execution_helpers_drive_a_ppo_step(ray_start_regular):
+    from ray_community_amd.rllib.algorithms.ppo import PPOConfig
+    from ray_community_amd.rllib.execution import (MinibatchBuffer, SimpleReplayBuffer, standardize_fields,
+                                                   synchronous_parallel_sample, train_one_step)
+    from ray_community_amd.rllib.policy.sample_batch import SampleBatch
+
+    algo = (PPOConfig().environment("CartPole-v1").env_runners(num_env_runners=1, num_envs_per_env_runner=2)
+            .training(train_batch_size=128, minibatch_size=64, num_epochs=1)).build()
+    try:
+        frags = synchronous_parallel_sample(worker_set=algo.env_runner_group, max_env_steps=128, concat=False)
+        assert sum(len(f) for f in frags) >= 128
+        res = train_one_step(algo, frags)
+        assert "default_policy" in res and res["default_policy"]
+    finally:
+        algo.stop()
+    b = standardize_fields(SampleBatch({"advantages": np.arange(10, dtype=np.float32)}), ["advantages"])
+    assert abs(float(b["advantages"].mean())) < 1e-6 and abs(float(b["advantages"].std()) - 1) < 1e-5
+    rb = SimpleReplayBuffer(2)
+    for i in range(3):
+        rb.add_batch(i)
+    assert len(rb) == 2 and rb.replay() in (1, 2)
+    q = queue.Queue()
+    q.put("a")
+    mb = MinibatchBuffer(q, size=1, timeout=1, num_passes=2, init_num_passes=2)
+    assert mb.get() == ("a", False) and mb.get() == ("a", True)
+
+
+def test_old_stack_policy_names():
+    from ray_community_amd.rllib.algorithms import dqn, ppo, sac
+    from ray_community_amd.rllib.policy import TorchPolicy
+
+    assert issubclass(ppo.PPOTorchPolicy, TorchPolicy) and issubclass(dqn.DQNTorchPolicy, TorchPolicy)
+    assert issubclass(sac.SACTorchPolicy, TorchPolicy)
+    with pytest.raises(ImportError):
+        ppo.PPOTF2Policy(None, None, {})
+    with pytest.raises(ImportError):
+        sac.RNNSAC()
+    assert not hasattr(ppo, "NotAPolicyName")
+
+
+def test_channel_reader_writer_interfaces():
+    from ray_community_amd.experimental.channel import (AwaitableBackgroundReader, Channel, SynchronousReader,
+                                                        SynchronousWriter)
+
+    a, b = Channel(1 << 12), Channel(1 << 12)
+    try:
+        w = SynchronousWriter([a, b])
+        r = SynchronousReader([a, b])
+        w.write({"x": 1})
+        assert r.read(timeout=5) == [{"x": 1}, {"x": 1}]
+        bg = AwaitableBackgroundReader([a])
+        bg.start()
+        a.write(7, timeout=5)
+        assert bg.read(timeout=5) == [7]
+        bg.close()
+    finally:
+        a.destroy()
+        b.destroy()
+
+
+def test_misc_module_paths_and_stubs():
+    from ray_community_amd.util.annotations import Deprecated, RayDeprecationWarning
+
+    @Deprecated(message="use g")
+    def f():
+        return 1
+
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        assert f() == 1
+    assert any(issubclass(w.category, RayDeprecationWarning) for w in rec)
+    from ray_community_amd.util.client import RayAPIStub, num_connected_contexts
+
+    assert num_connected_contexts() == 0 and not RayAPIStub().is_connected()
+    for mod, cls in (("wandb", "WandbLoggerCallback"), ("mlflow", "MLflowLoggerCallback"),
+                     ("comet", "CometLoggerCallback")):
+        m = importlib.import_module(f"ray_community_amd.air.integrations.{mod}")
+        with pytest.raises(ImportError):
+            getattr(m, cls)()
+    from ray_community_amd.autoscaler import sdk
+
+    cfg = sdk.fillout_defaults({"cluster_name": "c"})
+    assert cfg["provider"] == {"type": "local"} and cfg["head_node_type"] == "head"
+    with pytest.raises(NotImplementedError):
+        sdk.create_or_update_cluster("cluster.yaml")
+    assert importlib.import_module("ray_community_amd.tune.search.optuna").OptunaSearch
+    assert importlib.import_module("ray_community_amd.tune.search.hyperopt").HyperOptSearch
+    assert importlib.import_module("ray_community_amd.train.base_trainer").BaseTrainer
+    from ray_community_amd.tune.search.bohb import BOHB, TuneBOHB
+
+    assert BOHB is TuneBOHB
