@@ -79,6 +79,12 @@ class Algorithm(Trainable):
         ld.update(cfg._connector_dict())
         ld.update(self._runner_extra())
         ld["_algo"] = rd["_algo"]
+        from ..execution import _update_kind
+
+        try:  # the fused Learner update this algorithm trains with (LearnerGroup.update_from_batch)
+            ld["_update_kind"] = _update_kind(self)
+        except ValueError:  # DreamerV3 trains its world model without a Learner update kind
+            pass
         self._learner_dict = ld
         if self.multi_agent:
             # one learner group (RLModule + optimizer, possibly several GPU learners) per policy

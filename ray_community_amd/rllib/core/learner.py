@@ -18,6 +18,7 @@ import torch
 
 from ... import ops
 from ..policy.sample_batch import SampleBatch
+from .learner_api import LearnerAPI, LearnerGroupAPI
 from .rl_module import RLModule, make_module
 
 
@@ -28,7 +29,7 @@ def _device(use_gpu: bool):
     return torch.device("cpu")
 
 
-class Learner:
+class Learner(LearnerAPI):
     def __init__(self, config: Dict, obs_space, act_space, use_gpu: bool = False):
         self.cfg = config
         self.device = _device(use_gpu)
@@ -579,7 +580,7 @@ def _learner_actor_cls():
     return _LearnerActor
 
 
-class LearnerGroup:
+class LearnerGroup(LearnerGroupAPI):
     """``num_learners == 0``: one local learner in the driver (on a GPU if the driver has one).
     ``num_learners >= 1``: GPU learner actors in a placement group, one RCCL process group."""
 

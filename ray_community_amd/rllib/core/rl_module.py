@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..utils.spaces import Box, Discrete
+from .learner_api import MultiRLModuleAPI, RLModuleAPI, StatefulFlag
 
 
 class Categorical:
@@ -100,7 +101,7 @@ def preprocess_obs(obs: torch.Tensor) -> torch.Tensor:
     return obs.float()
 
 
-class RLModule(nn.Module):
+class RLModule(RLModuleAPI, nn.Module):
     """Actor-critic module used by PPO/IMPALA/APPO (and DQN via ``q_head``)."""
 
     def __init__(self, observation_space, action_space, model_config: Optional[Dict] = None, q_head=False):
@@ -108,6 +109,7 @@ class RLModule(nn.Module):
         cfg = dict(model_config or {})
         self.obs_space = observation_space
         self.act_space = action_space
+        self.model_config = cfg
         hiddens = cfg.get("fcnet_hiddens", [256, 256])
         act = cfg.get("fcnet_activation", "tanh")
         self.vf_share = cfg.get("vf_share_layers", False)
@@ -171,7 +173,7 @@ class RLModule(nn.Module):
         self.load_state_dict(state)
 
 
-class RecurrentRLModule(nn.Module):
+class RecurrentRLModule(RLModuleAPI, nn.Module):
     """LSTM actor-critic (reference: the new-stack default ``use_lstm`` encoder,
     ``rllib/core/models/torch/encoder.py`` TorchLSTMEncoder): MLP encoder -> LSTM cell -> policy and
     value heads. Stateful: the env runner carries one ``(h, c)`` row per sub-env (zeroed at episode
@@ -179,7 +181,7 @@ class RecurrentRLModule(nn.Module):
     chunks from the recorded chunk-start states, zeroing the state inside a chunk where a new
     episode begins (``resets``), so training sees exactly the recurrence the rollout used."""
 
-    is_stateful = True
+    is_stateful = StatefulFlag(1)
 
     def __init__(self, observation_space, action_space, model_config: Optional[Dict] = None):
         super().__init__()
@@ -295,7 +297,7 @@ class RLModuleSpec:
 SingleAgentRLModuleSpec = RLModuleSpec
 
 
-class MultiRLModule(nn.Module):
+class MultiRLModule(MultiRLModuleAPI, nn.Module):
     """Container of per-module RLModules (reference ``rllib/core/rl_module/marl_module.py:45``
     ``MultiAgentRLModule``): one RLModule per module (policy) id, registered as torch submodules
     (``parameters()`` / ``to()`` / ``state_dict()`` cover all of them). Dict-like access
