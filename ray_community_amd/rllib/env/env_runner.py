@@ -429,6 +429,21 @@ class EnvRunner:
     def ping(self):
         return "ok"
 
+    def assert_healthy(self) -> None:
+        """Raises if this runner cannot sample (no env, or a module without weights)."""
+        assert self.env is not None and getattr(self.env, "num_envs", 0) > 0, "env runner has no env"
+        assert self.module is not None, "env runner has no RLModule"
+
+    def stop(self) -> None:
+        """Close the sub-environments (envs with a ``close()``)."""
+        for e in getattr(self.env, "envs", []) or []:
+            close = getattr(e, "close", None)
+            if callable(close):
+                try:
+                    close()
+                except Exception:
+                    pass
+
     def apply(self, func, *args, **kwargs):
         """``func(self, *args)`` (``EnvRunnerGroup.foreach_env_runner`` with a callable)."""
         return func(self, *args, **kwargs)

@@ -34,6 +34,7 @@ class MultiAgentEpisode:
         self._hanging_reward: Dict[Any, float] = {}
         self._hanging_extra: Dict[Any, Dict] = {}
         self._module_for: Dict[Any, Any] = {}
+        self._last_stepped = set()
 
     # ------------------------------------------------------------------ building
     def module_for(self, agent_id):
@@ -53,6 +54,7 @@ class MultiAgentEpisode:
         infos = infos or {}
         for aid, o in observations.items():
             self._agent_episode(aid).add_env_reset(o, infos.get(aid))
+        self._last_stepped = set(observations)
 
     def add_env_step(self, observations: Dict, actions: Dict, rewards: Dict, infos: Optional[Dict] = None, *,
                      terminateds: Optional[Dict] = None, truncateds: Optional[Dict] = None,
@@ -91,6 +93,7 @@ class MultiAgentEpisode:
                     last, self._hanging_action.pop(aid), self._hanging_reward.pop(aid), infos.get(aid),
                     terminated=term, truncated=trunc, extra_model_outputs=self._hanging_extra.pop(aid, None))
         self.env_t += 1
+        self._last_stepped = set(observations)
         self.is_terminated = all_term or (bool(self.agent_episodes) and all(
             e.is_terminated for e in self.agent_episodes.values()))
         self.is_truncated = (all_trunc and not self.is_terminated)
@@ -144,11 +147,54 @@ class MultiAgentEpisode:
         return {aid: self.agent_episodes[aid].get_rewards(indices, **kw) for aid in ids
                 if aid in self.agent_episodes and len(self.agent_episodes[aid].rewards)}
 
+    def get_infos(self, indices=-1, agent_ids=None, **kw) -> Dict:
+        ids = self.agent_episodes if agent_ids is None else agent_ids
+        return {aid: self.agent_episodes[aid].get_infos(indices, **kw) for aid in ids
+                if aid in self.agent_episodes and self.agent_episodes[aid].is_reset}
+
+    def get_extra_model_outputs(self, key: str, indices=-1, agent_ids=None, **kw) -> Dict:
+        ids = self.agent_episodes if agent_ids is None else agent_ids
+        return {aid: self.agent_episodes[aid].get_extra_model_outputs(key, indices, **kw) for aid in ids
+                if aid in self.agent_episodes and key in self.agent_episodes[aid].extra_model_outputs
+                and len(self.agent_episodes[aid].extra_model_outputs[key])}
+
+    def get_terminateds(self) -> Dict:
+        out = {aid: e.is_terminated for aid, e in self.agent_episodes.items()}
+        out["__all__"] = self.is_terminated
+        return out
+
+    def get_truncateds(self) -> Dict:
+        out = {aid: e.is_truncated for aid, e in self.agent_episodes.items()}
+        out["__all__"] = self.is_truncated
+        return out
+
+    @property
+    def agent_episode_ids(self) -> Dict:
+        return {aid: e.id_ for aid, e in self.agent_episodes.items()}
+
+    @property
+    def is_finalized(self) -> bool:
+        return bool(self.agent_episodes) and all(e.is_finalized for e in self.agent_episodes.values())
+
+    def get_agents_that_stepped(self):
+        """Agents that received an observation at the latest reset / env step."""
+        return set(self._last_stepped)
+
+    def validate(self) -> None:
+        for aid, e in self.agent_episodes.items():
+            e.validate()
+            if e.multi_agent_episode_id not in (None, self.id_):
+                raise AssertionError(f"agent {aid}'s episode belongs to {e.multi_agent_episode_id}")
+
+    def get_sample_batch(self):
+        return self.to_sample_batch()
+
     # ------------------------------------------------------------------ chunks / conversion
     def cut(self, len_lookback_buffer: int = 0) -> "MultiAgentEpisode":
         nxt = MultiAgentEpisode(self.id_, agent_to_module_mapping_fn=self.agent_to_module_mapping_fn,
                                 env_t_started=self.env_t)
         nxt._module_for = dict(self._module_for)
+        nxt._last_stepped = set(self._last_stepped)
         for aid, ep in self.agent_episodes.items():
             if not ep.is_done:
                 nxt.agent_episodes[aid] = ep.cut(len_lookback_buffer)

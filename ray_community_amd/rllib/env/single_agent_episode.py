@@ -125,7 +125,7 @@ class SingleAgentEpisode:
     def _resolve(self, n_items: int, lb: int, indices, neg_index_as_lookback: bool, fill):
         """Absolute positions (into the stored list of ``n_items`` with ``lb`` lookback items) of
         ``indices``; out-of-range -> None (filled) or IndexError."""
-        single = not isinstance(indices, (list, tuple, slice, range, np.ndarray))
+        single = indices is not None and not isinstance(indices, (list, tuple, slice, range, np.ndarray))
         if indices is None:
             idx = list(range(lb, n_items))
         elif isinstance(indices, slice):
@@ -271,7 +271,36 @@ class SingleAgentEpisode:
             ep.finalize()
         return ep
 
+    # ------------------------------------------------------------------ in-place edits
+    def _set(self, data, new_data, at_indices, neg_index_as_lookback):
+        pos, single = self._resolve(len(data), self._lb, at_indices, neg_index_as_lookback, None)
+        vals = [new_data] if single else list(new_data)
+        if len(vals) != len(pos):
+            raise IndexError(f"{len(vals)} new items for {len(pos)} positions")
+        for a, v in zip(pos, vals):
+            data[a] = v
+
+    def set_observations(self, *, new_data, at_indices=None, neg_index_as_lookback: bool = False):
+        """Overwrite stored observations (same index rules as ``get_observations``)."""
+        self._set(self.observations, new_data, at_indices, neg_index_as_lookback)
+
+    def set_actions(self, *, new_data, at_indices=None, neg_index_as_lookback: bool = False):
+        self._set(self.actions, new_data, at_indices, neg_index_as_lookback)
+
+    def set_rewards(self, *, new_data, at_indices=None, neg_index_as_lookback: bool = False):
+        self._set(self.rewards, new_data, at_indices, neg_index_as_lookback)
+
+    def set_extra_model_outputs(self, *, key, new_data, at_indices=None, neg_index_as_lookback: bool = False):
+        self._set(self.extra_model_outputs[key], new_data, at_indices, neg_index_as_lookback)
+
     # ------------------------------------------------------------------ conversion
+    def get_data_dict(self) -> Dict[str, Any]:
+        """The episode's columns (no lookback), one row per timestep (``SampleBatch`` keys)."""
+        return {k: v for k, v in self.to_sample_batch().items()}
+
+    def get_sample_batch(self):
+        return self.to_sample_batch()
+
     def to_sample_batch(self):
         from ..policy.sample_batch import SampleBatch
 

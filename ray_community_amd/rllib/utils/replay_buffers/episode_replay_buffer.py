@@ -73,7 +73,12 @@ class EpisodeReplayBuffer:
             self._cum = np.cumsum([len(e) for e in self.episodes])
         return self._cum
 
+    def get_sampled_timesteps(self) -> int:
+        """Timesteps handed out by ``sample`` so far."""
+        return getattr(self, "_num_timesteps_sampled", 0)
+
     def _draw(self, k: int):
+        self._num_timesteps_sampled = getattr(self, "_num_timesteps_sampled", 0) + int(k)
         cum = self._index()
         total = int(cum[-1])
         g = self.rng.integers(0, total, k)

@@ -228,6 +228,7 @@ class PrioritizedEpisodeReplayBuffer(EpisodeReplayBuffer):
         return out
 
     def _draw(self, k: int):
+        self._num_timesteps_sampled = getattr(self, "_num_timesteps_sampled", 0) + int(k)
         prios = self._prios()
         flat = np.concatenate(prios) ** self.alpha
         p = flat / flat.sum()

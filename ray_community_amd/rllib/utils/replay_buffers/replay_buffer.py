@@ -40,6 +40,13 @@ class ReplayBuffer:
         b["batch_indexes"] = idx
         return b
 
+    def stats(self, debug: bool = False) -> dict:
+        out = {"added_count": self.num_added, "num_entries": self.size, "capacity": self.capacity,
+               "est_size_bytes": int(sum(v.nbytes for v in self.storage.values()))}
+        if debug:
+            out["write_index"] = self.idx
+        return out
+
     def get_state(self):
         return {"storage": self.storage, "size": self.size, "idx": self.idx}
 

@@ -85,3 +85,36 @@ def test_rl_module_checkpoint_and_multi(tmp_path):
     back = MultiRLModule.from_checkpoint(str(tmp_path / "mm"))
     assert list(back.keys()) == ["default_policy"]
     assert "action_dist_inputs" in m.output_specs_train()
+
+
+def test_episode_setters_and_accessors():
+    from ray_community_amd.rllib.env.multi_agent_episode import MultiAgentEpisode
+    from ray_community_amd.rllib.env.single_agent_episode import SingleAgentEpisode
+    from ray_community_amd.rllib.utils.replay_buffers import EpisodeReplayBuffer, ReplayBuffer
+
+    ep = SingleAgentEpisode()
+    ep.add_env_reset(np.zeros(2))
+    for t in range(4):
+        ep.add_env_step(np.full(2, t + 1.0), t, 1.0)
+    ep.set_rewards(new_data=[5.0, 6.0], at_indices=[0, -1])
+    assert ep.get_rewards().tolist() == [5.0, 1.0, 1.0, 6.0]
+    ep.set_actions(new_data=9, at_indices=2)
+    assert ep.get_actions(2) == 9
+    d = ep.get_data_dict()
+    assert d["rewards"].tolist() == [5.0, 1.0, 1.0, 6.0] and len(ep.get_sample_batch()) == 4
+
+    ma = MultiAgentEpisode()
+    ma.add_env_reset({"a": 0, "b": 1})
+    ma.add_env_step({"a": 1}, {"a": 0, "b": 0}, {"a": 1.0, "b": 0.5}, terminateds={"b": True})
+    assert ma.get_agents_that_stepped() == {"a"}
+    assert ma.get_terminateds() == {"a": False, "b": True, "__all__": False}
+    assert set(ma.agent_episode_ids) == {"a", "b"} and not ma.is_finalized
+    ma.validate()
+
+    rb = ReplayBuffer(10)
+    rb.add(SampleBatch({"x": np.arange(4)}))
+    assert rb.stats()["num_entries"] == 4
+    erb = EpisodeReplayBuffer(100)
+    erb.add(ep)
+    erb.sample(3)
+    assert erb.get_sampled_timesteps() == 3
