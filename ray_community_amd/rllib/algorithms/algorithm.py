@@ -760,6 +760,11 @@ class Algorithm(Trainable):
             json.dump(info, f, default=str)
         with open(os.path.join(export_dir, "rllib_checkpoint.json"), "w") as f:
             json.dump({"type": "Policy", "format": "rca-1"}, f)
+        from ..policy.policy import TorchPolicy  # + policy_state.pkl: Policy.from_checkpoint(export_dir)
+
+        obs_space = getattr(m, "obs_space", None) or self.obs_space
+        act_space = getattr(m, "act_space", None) or self.act_space
+        TorchPolicy(obs_space, act_space, {"model": self.config.model}, model=m).export_checkpoint(export_dir)
         return export_dir
 
     def import_model(self, import_file: str):
