@@ -412,3 +412,19 @@ def get_runtime_context():
 
 def _head():
     return _state["head"]
+
+
+def get_dashboard_url() -> Optional[str]:
+    """``host:port`` of this session's dashboard (None when it runs without one);
+    ``RAY_OVERRIDE_DASHBOARD_URL`` wins, as in the reference."""
+    override = os.environ.get("RAY_OVERRIDE_DASHBOARD_URL")
+    if override:
+        return override.split("://", 1)[-1]
+    dash = _state.get("dashboard")
+    url = getattr(dash, "url", None)
+    return url.split("://", 1)[-1] if url else None
+
+
+def get_resource_ids():
+    """Deprecated alias of ``get_runtime_context().get_resource_ids()``."""
+    return get_runtime_context().get_resource_ids()

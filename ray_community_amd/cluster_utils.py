@@ -80,6 +80,17 @@ class Cluster:
     def wait_for_nodes(self, timeout: float = 30):
         return True
 
+    @property
+    def gcs_address(self) -> Optional[str]:
+        """The head's control-plane address (a Unix socket path here, as ``address``)."""
+        return self.address
+
+    def remaining_processes_alive(self) -> bool:
+        """True while the session's head is up (nodes are virtual: one head process)."""
+        from ._private import worker as w
+
+        return w.is_initialized()
+
     def list_all_nodes(self) -> List[NodeHandle]:
         return ([self.head_node] if self.head_node else []) + list(self.worker_nodes)
 

@@ -132,6 +132,21 @@ class DAGNode:
     def clear_cache(self):
         self.cache_from_last_execute = {}
 
+    def get_object_refs_from_last_execute(self) -> Dict[str, Any]:
+        """{node stable uuid: its ObjectRef} of the last ``execute(_ray_cache_refs=True)``."""
+        return dict(getattr(self, "cache_from_last_execute", {}) or {})
+
+    def apply_functional(self, source_input_list: Any, predictate_fn: Callable, apply_fn: Callable):
+        """``apply_fn(x)`` on every element of ``source_input_list`` (a node, or a nested
+        list / dict / tuple of them) that ``predictate_fn(x)`` accepts; the structure is kept."""
+        def go(x):
+            if isinstance(x, (list, tuple)):
+                return type(x)(go(v) for v in x)
+            if isinstance(x, dict):
+                return {k: go(v) for k, v in x.items()}
+            return apply_fn(x) if predictate_fn(x) else x
+        return go(source_input_list)
+
     def __reduce__(self):
         raise ValueError("DAGNode cannot be serialized; call .execute() to get ObjectRefs instead.")
 

@@ -6,11 +6,45 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 
 
+class PreprocessorNotFittedException(RuntimeError):
+    """``transform`` on a fittable preprocessor that was never fitted."""
+
+
 class Preprocessor:
     _is_fittable = True
 
+    class FitStatus(str):
+        NOT_FITTABLE = "NOT_FITTABLE"
+        NOT_FITTED = "NOT_FITTED"
+        PARTIALLY_FITTED = "PARTIALLY_FITTED"  # a Chain with some fitted stages
+        FITTED = "FITTED"
+
     def __init__(self):
         self.stats_: Optional[Dict] = None
+
+    def fit_status(self) -> str:
+        if not self._is_fittable:
+            return Preprocessor.FitStatus.NOT_FITTABLE
+        return Preprocessor.FitStatus.FITTED if self.stats_ is not None else Preprocessor.FitStatus.NOT_FITTED
+
+    @classmethod
+    def preferred_batch_format(cls) -> str:
+        return "pandas"
+
+    def serialize(self) -> str:
+        """A string form of this preprocessor (fitted state included); ``deserialize`` restores it."""
+        import base64
+
+        import cloudpickle
+
+        return base64.b64encode(cloudpickle.dumps(self)).decode("ascii")
+
+    @staticmethod
+    def deserialize(serialized: str) -> "Preprocessor":
+        import base64
+        import pickle
+
+        return pickle.loads(base64.b64decode(serialized))  # a string produced by serialize()
 
     def fit(self, ds) -> "Preprocessor":
         if self._is_fittable:
@@ -22,15 +56,21 @@ class Preprocessor:
 
     def transform(self, ds):
         if self._is_fittable and self.stats_ is None:
-            raise RuntimeError(f"`{type(self).__name__}` must be fitted before transform")
+            raise PreprocessorNotFittedException(f"`{type(self).__name__}` must be fitted before transform")
         return ds.map_batches(self._transform_pandas, batch_format="pandas")
 
     def transform_batch(self, batch):
         import pandas as pd
 
-        df = batch if isinstance(batch, pd.DataFrame) else pd.DataFrame({k: list(v) if np.ndim(v) > 1 else v
-                                                                        for k, v in batch.items()})
-        return self._transform_pandas(df)
+        if self._is_fittable and self.stats_ is None:
+            raise PreprocessorNotFittedException(f"`{type(self).__name__}` must be fitted before transform_batch")
+        is_df = isinstance(batch, pd.DataFrame)
+        df = batch if is_df else pd.DataFrame({k: list(v) if np.ndim(v) > 1 else v for k, v in batch.items()})
+        out = self._transform_pandas(df)
+        if is_df:
+            return out
+        return {c: np.stack(out[c].to_numpy()) if len(out) and isinstance(out[c].iloc[0], np.ndarray)
+                else out[c].to_numpy() for c in out.columns}  # the batch format it was given
 
     def _fit(self, ds) -> Dict:
         return {}

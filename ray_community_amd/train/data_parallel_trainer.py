@@ -75,6 +75,14 @@ class BaseTrainer:
 class DataParallelTrainer(BaseTrainer):
     _default_backend_config = BackendConfig()
 
+    def get_dataset_config(self):
+        """The ``DataConfig`` the datasets are split with (the default one if none was given)."""
+        if self.dataset_config is not None:
+            return self.dataset_config
+        from . import DataConfig
+
+        return DataConfig()
+
     def __init__(self, train_loop_per_worker: Callable, *, train_loop_config: Optional[Dict] = None,
                  backend_config: Optional[BackendConfig] = None, scaling_config: Optional[ScalingConfig] = None,
                  run_config: Optional[RunConfig] = None, datasets: Optional[Dict[str, Any]] = None,

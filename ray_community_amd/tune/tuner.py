@@ -365,6 +365,136 @@ class Trial:
     def __repr__(self):
         return f"Trial({self.trial_id}, {self.status})"
 
+    def __str__(self):
+        return getattr(self, "trial_name", None) or self.trial_id
+
+    # --------------------------------------------------------------- the reference Trial's read API
+    # (python/ray/tune/experiment/trial.py: what callbacks, schedulers and stoppers read)
+    @property
+    def path(self) -> str:
+        return self.local_path
+
+    logdir = path
+
+    @property
+    def local_dir(self) -> str:
+        return os.path.dirname(self.local_path)
+
+    @property
+    def experiment_dir_name(self) -> str:
+        return os.path.basename(os.path.dirname(self.local_path))
+
+    local_experiment_path = local_dir
+    remote_experiment_path = local_dir
+
+    @property
+    def experiment_tag(self) -> str:
+        return getattr(self, "_experiment_tag", "") or ",".join(f"{k}={v}" for k, v in _flat_cfg(self.config))
+
+    def set_experiment_tag(self, tag: str) -> None:
+        self._experiment_tag = tag
+
+    @property
+    def has_reported_at_least_once(self) -> bool:
+        return bool(self.last_result)
+
+    @property
+    def node_ip(self) -> str:
+        from ..util import get_node_ip_address
+
+        return get_node_ip_address()
+
+    def get_ray_actor_ip(self) -> Optional[str]:
+        return self.node_ip if self.runner is not None else None
+
+    @property
+    def placement_group_factory(self):
+        from .registry import PlacementGroupFactory
+
+        return PlacementGroupFactory([dict(self.resources)])
+
+    def create_placement_group_factory(self):
+        return self.placement_group_factory
+
+    def update_resources(self, resources: Dict) -> None:
+        self.resources = dict(getattr(resources, "required_resources", resources))
+
+    def set_status(self, status: str) -> None:
+        self.status = status
+
+    def set_config(self, config: Dict) -> None:
+        self.config = config
+
+    def update_last_result(self, result: Dict) -> None:
+        self.last_result = result
+        self.metrics_history.append(result)
+
+    @property
+    def metric_analysis(self) -> Dict[str, Dict[str, float]]:
+        """Per numeric metric: max / min / avg / last over the reported results."""
+        out: Dict[str, Dict[str, float]] = {}
+        for r in self.metrics_history:
+            for k, v in r.items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool):
+                    d = out.setdefault(k, {"max": v, "min": v, "sum": 0.0, "n": 0})
+                    d["max"], d["min"] = max(d["max"], v), min(d["min"], v)
+                    d["sum"] += v
+                    d["n"] += 1
+                    d["last"] = v
+        return {k: {"max": d["max"], "min": d["min"], "avg": d["sum"] / d["n"], "last": d["last"]}
+                for k, d in out.items()}
+
+    def is_finished(self) -> bool:
+        return self.status in (TERMINATED, ERROR)
+
+    def has_checkpoint(self) -> bool:
+        return self.checkpoint is not None
+
+    def clear_checkpoint(self) -> None:
+        self.checkpoint = None
+
+    @property
+    def latest_checkpoint_result(self) -> Optional[Dict]:
+        return self.last_result if self.checkpoint is not None else None
+
+    def get_error(self) -> Optional[BaseException]:
+        return self.error
+
+    @property
+    def error_file(self) -> Optional[str]:
+        return os.path.join(self.local_path, "error.txt") if self.error is not None else None
+
+    def should_stop(self, result: Dict) -> bool:
+        return bool(result.get("done"))
+
+    @staticmethod
+    def generate_id() -> str:
+        import uuid as _uuid
+
+        return _uuid.uuid4().hex[:8]
+
+    def get_json_state(self) -> str:
+        return json.dumps({"trial_id": self.trial_id, "config": _jsonable(self.config), "status": self.status,
+                           "local_path": self.local_path, "last_result": _jsonable(self.last_result),
+                           "checkpoint": self.checkpoint.path if self.checkpoint else None,
+                           "resources": self.resources})
+
+    @classmethod
+    def from_json_state(cls, json_state: str) -> "Trial":
+        d = json.loads(json_state)
+        t = cls(d["trial_id"], d["config"], d["local_path"], d.get("resources") or {"CPU": 1})
+        t.status, t.last_result = d["status"], d.get("last_result") or {}
+        t.checkpoint = _ckpt(d.get("checkpoint"))
+        return t
+
+
+def _flat_cfg(cfg, prefix=""):
+    for k, v in (cfg or {}).items():
+        if isinstance(v, dict):
+            yield from _flat_cfg(v, f"{prefix}{k}/")
+        else:
+            yield f"{prefix}{k}", v
+
 
 class ResultGrid:
     def __init__(self, results: List[Result], metric=None, mode=None, experiment_path=None):

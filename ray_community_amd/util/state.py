@@ -10,6 +10,31 @@ from typing import Any, Dict, Iterator, List, Optional, Tuple
 _LOCAL = threading.local()
 
 
+@contextlib.contextmanager
+def warnings_on_slow_request(*, address: str, endpoint: str, timeout: float, explain: bool):
+    """Log a warning at timeout/8, /4 and /2 while a state request is still waiting (only when
+    ``explain``); reference util/state/api.py."""
+    if not explain:
+        yield
+        return
+    import logging
+    import time
+
+    log = logging.getLogger("ray_community_amd.util.state")
+    t0 = time.monotonic()
+    timers = [threading.Timer(timeout * f, lambda f=f: log.warning(
+        f"({round(time.monotonic() - t0, 2)} / {timeout} seconds) waiting for the response from {address}{endpoint}"))
+              for f in (1 / 8, 1 / 4, 1 / 2)]
+    for t in timers:
+        t.daemon = True
+        t.start()
+    try:
+        yield
+    finally:
+        for t in timers:
+            t.cancel()
+
+
 def _call(method, *args):
     c = getattr(_LOCAL, "client", None)  # the dashboard answering /api/v0 with its own head link
     if c is not None:

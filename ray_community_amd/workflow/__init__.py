@@ -544,3 +544,10 @@ __all__ = ["init", "run", "run_async", "resume", "resume_async", "resume_all", "
            "get_output", "get_output_async", "get_status", "get_metadata", "continuation", "options",
            "WorkflowStatus", "WorkflowError", "WorkflowExecutionError", "WorkflowCancellationError",
            "WorkflowNotFoundError", "sleep", "wait_for_event", "EventListener", "TimerListener"]
+
+
+def client_mode_wrap(func):
+    """Identity here: a ``ray://`` client drives the same API as a local driver (the calls are
+    relayed), so there is nothing to wrap into a remote task (reference
+    _private/client_mode_hook.py)."""
+    return func

@@ -156,3 +156,55 @@ def test_misc_module_paths_and_stubs():
     from ray_community_amd.tune.search.bohb import BOHB, TuneBOHB
 
     assert BOHB is TuneBOHB
+
+
+def test_trial_preprocessor_dag_and_misc_methods(ray_start_regular, tmp_path):
+    from ray_community_amd import tune
+    from ray_community_amd._private.worker import get_dashboard_url
+    from ray_community_amd.data.preprocessors import Preprocessor, StandardScaler
+    from ray_community_amd.tune.tuner import Trial
+    from ray_community_amd.util.state import warnings_on_slow_request
+
+    seen = {}
+
+    class _CB(tune.Callback):
+        def on_trial_result(self, iteration, trials, trial, result, **info):
+            seen["tag"] = trial.experiment_tag
+            seen["analysis"] = trial.metric_analysis
+            seen["path"] = trial.path
+
+    def f(config):
+        for i in range(3):
+            tune.report({"v": i * config["a"]})
+
+    tune.Tuner(f, param_space={"a": 2}, run_config=ray.train.RunConfig(storage_path=str(tmp_path),
+                                                                       callbacks=[_CB()])).fit()
+    assert seen["tag"] == "a=2" and seen["analysis"]["v"]["max"] >= 2 and seen["path"].startswith(str(tmp_path))
+    t = Trial("abc", {"x": 1}, str(tmp_path / "t"), {"CPU": 1})
+    t2 = Trial.from_json_state(t.get_json_state())
+    assert t2.trial_id == "abc" and t2.config == {"x": 1} and not t2.is_finished()
+
+    ds = ray.data.from_items([{"x": float(i)} for i in range(10)])
+    sc = StandardScaler(["x"])
+    assert sc.fit_status() == Preprocessor.FitStatus.NOT_FITTED
+    with pytest.raises(RuntimeError):
+        sc.transform_batch({"x": np.zeros(2)})
+    sc.fit(ds)
+    back = Preprocessor.deserialize(sc.serialize())
+    out = back.transform_batch({"x": np.array([4.5])})
+    assert isinstance(out, dict) and abs(float(out["x"][0])) < 1e-9 and back.fit_status() == "FITTED"
+
+    @ray.remote
+    def inc(x):
+        return x + 1
+
+    from ray_community_amd.dag import InputNode
+
+    with InputNode() as inp:
+        dag = inc.bind(inc.bind(inp))
+    assert ray.get(dag.execute(1, _ray_cache_refs=True)) == 3
+    assert len(dag.get_object_refs_from_last_execute()) >= 2
+    assert dag.apply_functional([1, (2, {"k": 3})], lambda x: x > 1, lambda x: x * 10) == [1, (20, {"k": 30})]
+    with warnings_on_slow_request(address="http://x", endpoint="/api", timeout=0.01, explain=True):
+        pass
+    assert get_dashboard_url() is None or ":" in get_dashboard_url()
