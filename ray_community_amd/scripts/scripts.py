@@ -231,6 +231,85 @@ def cmd_healthcheck(args) -> int:
     return 0 if ok else 1
 
 
+def cmd_stack(args) -> int:
+    """Python stacks of every worker of the session on this machine: each worker process has a
+    faulthandler on SIGUSR1 (worker_main.py), which writes all thread stacks into its log; this
+    signals them and prints the dumps (the reference shells out to py-spy, not installed here)."""
+    import signal
+    import time
+
+    from ray_community_amd.util import state
+
+    ray = _connect(args)
+    try:
+        workers = [w for w in state.list_workers() if w.get("pid")]
+        sent = []
+        for w in workers:
+            try:
+                os.kill(int(w["pid"]), signal.SIGUSR1)
+                sent.append(w)
+            except (ProcessLookupError, PermissionError):
+                continue
+        time.sleep(args.wait)
+        for w in sent:
+            lines = list(state.get_log(pid=int(w["pid"]), tail=args.lines))
+            heads = [i for i, l in enumerate(lines) if l.startswith(("Thread 0x", "Current thread"))]
+            start = heads[0] if heads else 0  # the dump's first thread header within the tail
+            print(f"=== worker pid {w['pid']} ({str(w.get('worker_id', ''))[:12]}) ===")
+            print("\n".join(lines[start:]))
+        print(f"{len(sent)} worker(s) dumped")
+    finally:
+        ray.shutdown()
+    return 0
+
+
+def _usage_stats_path() -> str:
+    return os.path.join(os.path.expanduser("~"), ".ray", "config.json")
+
+
+def cmd_usage_stats(args) -> int:
+    """``disable-usage-stats`` / ``enable-usage-stats``: the reference's persistent opt-out
+    (``~/.ray/config.json``). Nothing is ever reported from this framework; the setting is kept
+    so tooling that reads it sees the user's choice."""
+    path = _usage_stats_path()
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    cfg = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            try:
+                cfg = json.load(f)
+            except ValueError:
+                cfg = {}
+    cfg["usage_stats"] = bool(args.enable)
+    with open(path, "w") as f:
+        json.dump(cfg, f)
+    print(f"usage stats {'enabled' if args.enable else 'disabled'} ({path})")
+    return 0
+
+
+def cmd_global_gc(args) -> int:
+    """Run ``gc.collect()`` in the driver and in one task per CPU slot of every node (the
+    workers the tasks land on free what only cyclic garbage kept alive)."""
+    import gc
+
+    ray = _connect(args)
+    try:
+        gc.collect()
+
+        @ray.remote(num_cpus=0)
+        def _collect():
+            import gc as _gc
+
+            return _gc.collect()
+
+        n = max(1, int(sum(nd.get("Resources", {}).get("CPU", 1) for nd in ray.nodes())))
+        freed = sum(ray.get([_collect.remote() for _ in range(n)]))
+        print(f"global gc: {freed} objects collected in workers")
+    finally:
+        ray.shutdown()
+    return 0
+
+
 _LISTS = {"actors": "list_actors", "tasks": "list_tasks", "objects": "list_objects", "nodes": "list_nodes",
           "workers": "list_workers", "placement-groups": "list_placement_groups"}
 
@@ -477,6 +556,20 @@ def build_parser() -> argparse.ArgumentParser:
     sp = sub.add_parser("healthcheck")
     conn_opts(sp)
     sp.set_defaults(fn=cmd_healthcheck)
+
+    sp = sub.add_parser("stack", help="dump the Python stacks of the session's workers")
+    sp.add_argument("--lines", type=int, default=200)
+    sp.add_argument("--wait", type=float, default=0.5)
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_stack)
+
+    for name, on in (("disable-usage-stats", False), ("enable-usage-stats", True)):
+        sp = sub.add_parser(name, help=f"{'enable' if on else 'disable'} usage stats collection (a persisted flag)")
+        sp.set_defaults(fn=cmd_usage_stats, enable=on)
+
+    sp = sub.add_parser("global-gc", help="garbage-collect in the driver and the workers")
+    conn_opts(sp)
+    sp.set_defaults(fn=cmd_global_gc)
 
     sp = sub.add_parser("list", help="state API listing")
     sp.add_argument("resource", choices=sorted(list(_LISTS) + ["jobs"]))

@@ -108,3 +108,26 @@ def test_job_config_namespace_runtime_env_and_lifetime(shutdown_only):
     assert ray.get(ray.get_actor("jc_actor", namespace="jcns").ping.remote()) == 1
     with pytest.raises(ValueError):
         jc.set_default_actor_lifetime("forever")
+
+
+def test_cli_stack_global_gc_and_usage_stats(tmp_path):
+    assert _cli(tmp_path, "start", "--head", "--num-cpus", "2").returncode == 0
+    try:
+        code = ("import ray_community_amd as ray, time; ray.init(address='auto');"
+                "A = ray.remote(type('A', (), {'ping': lambda self: 1}));"
+                "a = A.options(name='stackme', lifetime='detached').remote(); print(ray.get(a.ping.remote()))")
+        env = dict(os.environ, RCA_TEMP_DIR=str(tmp_path), PYTHONPATH=ROOT)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=90)
+        assert r.returncode == 0, r.stderr
+        r = _cli(tmp_path, "stack")
+        assert r.returncode == 0 and "worker(s) dumped" in r.stdout, r.stdout + r.stderr
+        assert "most recent call first" in r.stdout, r.stdout
+        r = _cli(tmp_path, "global-gc")
+        assert r.returncode == 0 and "global gc" in r.stdout, r.stdout + r.stderr
+    finally:
+        _cli(tmp_path, "stop", "--force")
+    home = tmp_path / "home"
+    env_home = dict(HOME=str(home))
+    r = subprocess.run([sys.executable, "-m", "ray_community_amd", "disable-usage-stats"], capture_output=True,
+                       text=True, timeout=60, cwd=ROOT, env=dict(os.environ, **env_home, PYTHONPATH=ROOT))
+    assert r.returncode == 0 and json.loads((home / ".ray" / "config.json").read_text()) == {"usage_stats": False}
