@@ -208,3 +208,19 @@ def test_trial_preprocessor_dag_and_misc_methods(ray_start_regular, tmp_path):
     with warnings_on_slow_request(address="http://x", endpoint="/api", timeout=0.01, explain=True):
         pass
     assert get_dashboard_url() is None or ":" in get_dashboard_url()
+
+
+def test_util_module_paths():
+    from ray_community_amd.util import iter_metrics, rpdb, serialization_addons
+    from ray_community_amd.util.debugpy import set_trace  # noqa: F401
+
+    sm = iter_metrics.SharedMetrics()
+    sm.get().counters["n"] += 2
+    child = iter_metrics.SharedMetrics(parents=[])
+    iter_metrics.SharedMetrics(sm.get(), parents=[child])
+    assert child.get().counters["n"] == 2
+    serialization_addons.apply(None)
+    assert callable(rpdb.set_trace)
+    for mod in ("dask", "spark", "horovod"):
+        with pytest.raises(ImportError):
+            importlib.import_module(f"ray_community_amd.util.{mod}")
