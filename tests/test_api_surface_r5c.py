@@ -224,3 +224,31 @@ def test_util_module_paths():
     for mod in ("dask", "spark", "horovod"):
         with pytest.raises(ImportError):
             importlib.import_module(f"ray_community_amd.util.{mod}")
+
+
+def test_train_module_paths_and_predictors():
+    import pandas as pd
+    import torch
+
+    from ray_community_amd.train import constants, context, error, session  # noqa: F401
+    from ray_community_amd.train.predictor import Predictor, PredictorNotSerializableException
+    from ray_community_amd.train.torch.torch_detection_predictor import TorchDetectionPredictor
+
+    p = Predictor.from_pandas_udf(lambda df: df.assign(y=df["x"] * 2))
+    assert p.predict({"x": [1, 2]})["y"].tolist() == [2, 4]
+    with pytest.raises(PredictorNotSerializableException):
+        import pickle
+
+        pickle.dumps(p)
+    assert constants.TRAIN_DATASET_KEY == "train" and issubclass(error.SessionMisuseError, Exception)
+
+    class Det(torch.nn.Module):
+        def forward(self, ims):
+            return [{"boxes": torch.zeros(1, 4), "labels": torch.ones(1), "scores": torch.ones(1)} for _ in ims]
+
+    out = TorchDetectionPredictor(Det()).predict(np.zeros((2, 3, 4, 4), np.float32))
+    assert out["pred_boxes"].shape == (2,) and out["pred_boxes"][1].shape == (1, 4)
+    for mod in ("lightning", "tensorflow", "horovod", "mosaic"):
+        with pytest.raises(ImportError):
+            importlib.import_module(f"ray_community_amd.train.{mod}")
+    assert isinstance(pd.DataFrame({"a": [1]}), pd.DataFrame)
