@@ -1,4 +1,8 @@
 """Ray Serve equivalent (reference: ``python/ray/serve``)."""
+# load the ``serve.deployment`` / ``serve.context`` MODULES first: binding the ``deployment``
+# decorator below then wins, and a later ``import ray_community_amd.serve.deployment`` (already in
+# sys.modules) does not replace the decorator with the module
+from . import context as _context_module, deployment as _deployment_module  # noqa: E402,F401
 from .api import (Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle,
                   get_replica_context, ingress, run, shutdown, start, status)
 from .batching import batch

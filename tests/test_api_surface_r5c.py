@@ -252,3 +252,39 @@ def test_train_module_paths_and_predictors():
         with pytest.raises(ImportError):
             importlib.import_module(f"ray_community_amd.train.{mod}")
     assert isinstance(pd.DataFrame({"a": [1]}), pd.DataFrame)
+
+
+def test_tune_serve_experimental_module_paths(ray_start_regular, tmp_path, capsys):
+    for mod in ("tune.callback", "tune.progress_reporter", "tune.result_grid", "tune.tune_config", "tune.error",
+                "tune.syncer", "tune.constants", "tune.result", "tune.trainable", "serve.deployment",
+                "serve.context", "experimental.locations", "experimental.dynamic_resources"):
+        importlib.import_module(f"ray_community_amd.{mod}")
+    from ray_community_amd import serve
+    from ray_community_amd.experimental.tqdm_ray import tqdm
+    from ray_community_amd.serve.autoscaling_policy import calculate_desired_num_replicas
+    from ray_community_amd.tune.syncer import Syncer
+
+    assert calculate_desired_num_replicas({"target_ongoing_requests": 2, "min_replicas": 1, "max_replicas": 3},
+                                          9, 1) == 3
+    (tmp_path / "a").mkdir()
+    (tmp_path / "a" / "f.txt").write_text("x")
+    assert Syncer().sync_up(str(tmp_path / "a"), str(tmp_path / "b")) and (tmp_path / "b" / "f.txt").exists()
+    assert list(tqdm(range(4), desc="bar", flush_interval_s=0)) == [0, 1, 2, 3]
+    assert "bar: 4/4" in capsys.readouterr().out
+
+    @serve.deployment
+    class M:
+        def __init__(self):
+            from ray_community_amd.serve.metrics import Counter
+
+            self.c = Counter("rca_test_requests_total", tag_keys=("route",))
+
+        def __call__(self, x):
+            self.c.inc(1, tags={"route": "/"})
+            return dict(self.c._default_tags)
+
+    try:
+        tags = serve.run(M.bind(), name="m", route_prefix=None).remote(1).result()
+        assert tags["deployment"] == "M" and tags["application"] == "m" and tags["replica"]
+    finally:
+        serve.shutdown()
