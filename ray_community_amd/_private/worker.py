@@ -36,6 +36,14 @@ def is_initialized() -> bool:
 def _core() -> CoreWorker:
     c = _state["core"]
     if c is None:
+        import threading
+
+        if _state.get("explicit_shutdown") and threading.current_thread() is not threading.main_thread():
+            # a background thread of the session that was shut down (a data pump, a router
+            # poller, ...): failing here beats auto-initialising a fresh session behind the user
+            from ..exceptions import RaySystemError
+
+            raise RaySystemError("the session was shut down; call init() to start a new one")
         init()
         c = _state["core"]
     return c
@@ -76,6 +84,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None, num_g
          logging_format=None, log_to_driver=True, namespace: Optional[str] = None, runtime_env=None,
          _system_config: Optional[dict] = None, _temp_dir: Optional[str] = None, **kwargs):
     """Start (or connect to) a session. Returns a context dict-like with ``address_info``."""
+    _state["explicit_shutdown"] = False
     with _state["init_lock"]:
         if _state["core"] is not None:
             if ignore_reinit_error:
@@ -221,6 +230,7 @@ class RayContext(dict):
 
 
 def shutdown(_exiting_interpreter: bool = False):
+    _state["explicit_shutdown"] = True
     with _state["init_lock"]:
         core = _state["core"]
         head = _state["head"]

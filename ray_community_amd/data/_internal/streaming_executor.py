@@ -388,6 +388,9 @@ class _SideInput:
         ex = getattr(self.ds, "_executor", None)
         if ex is not None and not self.exhausted:
             ex._stop.set()
+        t = self._t
+        if t is not None and t is not threading.current_thread():
+            t.join(timeout=10.0)  # the pump must not outlive the pipeline (nor the session)
 
 
 class UnionOp(PhysicalOp):
