@@ -169,6 +169,12 @@ class HyperBandScheduler(TrialScheduler):
         self._next_s = self.s_max
         self.decisions: List[tuple] = []  # (bracket index, milestone, kept ids, stopped ids)
 
+    def state(self) -> Dict:
+        """Bracket bookkeeping: per bracket its budget, size, trial ids and current milestone."""
+        return {"num_brackets": len(self.brackets), "s_max": self.s_max,
+                "brackets": [{k: (sorted(v) if isinstance(v, set) else v) for k, v in b.items()
+                              if isinstance(v, (int, float, str, list, set))} for b in self.brackets]}
+
     def _new_bracket(self):
         s = self._next_s
         self._next_s = self._next_s - 1 if self._next_s > 0 else self.s_max
@@ -309,6 +315,16 @@ class PopulationBasedTraining(TrialScheduler):
         self.scores: Dict[str, float] = {}
         self.num_perturbations = 0
         self._rng = random.Random(seed)
+
+    def reset_stats(self) -> None:
+        """Forget the recorded scores and perturbation times (e.g. between experiments)."""
+        self.scores = {}
+        self.last_perturb = {}
+        self.num_perturbations = 0
+
+    def last_scores(self, trials) -> List[float]:
+        """The latest recorded score of each trial that has one (higher is better)."""
+        return [self.scores[t.trial_id] for t in trials if t.trial_id in self.scores]
 
     def _explore(self, config):
         from .. import search as S

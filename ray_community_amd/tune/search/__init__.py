@@ -192,9 +192,34 @@ class BasicVariantGenerator(Searcher):
 
     def set_space(self, param_space: Dict, num_samples: int):
         self._queue = list(self._points) + generate_variants(param_space, num_samples, self._rng)
+        self._total = len(self._queue)
 
     def total(self):
         return len(self._queue)
+
+    @property
+    def total_samples(self) -> int:
+        """Configurations this generator was given (the initial queue length)."""
+        return getattr(self, "_total", len(self._queue))
+
+    def add_configurations(self, experiments) -> None:
+        """Queue the variants of more experiments: ``Experiment`` objects, ``{name: spec}`` dicts
+        or specs with ``config`` / ``num_samples``."""
+        if isinstance(experiments, dict) and "config" not in experiments:
+            experiments = list(experiments.values())
+        for e in (experiments if isinstance(experiments, (list, tuple)) else [experiments]):
+            cfg = getattr(e, "config", None) if not isinstance(e, dict) else e.get("config")
+            n = getattr(e, "num_samples", None) if not isinstance(e, dict) else e.get("num_samples", 1)
+            new = generate_variants(cfg or {}, int(n or 1), self._rng)
+            self._queue.extend(new)
+            self._total = self.total_samples + len(new)
+
+    def next_trial(self) -> Optional[Dict]:
+        """The next configuration, or None when the generator is exhausted."""
+        return self._queue.pop(0) if self._queue else None
+
+    def has_checkpoint(self, dirpath: str) -> bool:
+        return False
 
     def suggest(self, trial_id):
         if not self._queue:
@@ -203,21 +228,34 @@ class BasicVariantGenerator(Searcher):
 
 
 class ConcurrencyLimiter(Searcher):
+    """At most ``max_concurrent`` live trials. ``batch=True``: suggestions come in batches of
+    ``max_concurrent``; the next batch starts once every trial of the current one completed, and
+    the wrapped searcher sees the batch's results together (reference
+    tune/search/concurrency_limiter.py)."""
+
     def __init__(self, searcher: Searcher, max_concurrent: int, batch: bool = False):
         super().__init__(searcher.metric, searcher.mode)
+        if max_concurrent < 1:
+            raise ValueError("max_concurrent must be >= 1")
         self.searcher = searcher
         self.max_concurrent = max_concurrent
+        self.batch = batch
         self.live = set()
+        self._paused = set()
+        self._batch_full = False
+        self._cached: List[tuple] = []
 
     def set_search_properties(self, metric, mode, config, **spec):
         return self.searcher.set_search_properties(metric, mode, config, **spec)
 
     def suggest(self, trial_id):
-        if len(self.live) >= self.max_concurrent:
+        if len(self.live) >= self.max_concurrent or (self.batch and self._batch_full):
             return None
         s = self.searcher.suggest(trial_id)
         if s is not None and s != Searcher.FINISHED:
             self.live.add(trial_id)
+            if self.batch and len(self.live) >= self.max_concurrent:
+                self._batch_full = True
         return s
 
     def on_trial_result(self, trial_id, result):
@@ -225,7 +263,27 @@ class ConcurrencyLimiter(Searcher):
 
     def on_trial_complete(self, trial_id, result=None, error=False):
         self.live.discard(trial_id)
-        self.searcher.on_trial_complete(trial_id, result, error)
+        self._paused.discard(trial_id)
+        if not self.batch:
+            self.searcher.on_trial_complete(trial_id, result, error)
+            return
+        self._cached.append((trial_id, result, error))
+        if not self.live:  # the whole batch is done: report it and open the next one
+            for tid, res, err in self._cached:
+                self.searcher.on_trial_complete(tid, res, err)
+            self._cached = []
+            self._batch_full = False
+
+    def on_pause(self, trial_id) -> None:
+        """A paused trial frees its slot (schedulers pause trials at milestones)."""
+        if trial_id in self.live:
+            self.live.discard(trial_id)
+            self._paused.add(trial_id)
+
+    def on_unpause(self, trial_id) -> None:
+        if trial_id in self._paused:
+            self._paused.discard(trial_id)
+            self.live.add(trial_id)
 
 
 class RandomSearch(Searcher):

@@ -903,6 +903,8 @@ class TuneController:
         if trial.status != PAUSED:
             return
         trial.status = PENDING
+        if hasattr(self.searcher, "on_unpause"):
+            self.searcher.on_unpause(trial.trial_id)
         trial.restore_path = trial.checkpoint.path if trial.checkpoint else None
         trial.iteration_offset = trial.last_result.get("training_iteration", 0) if trial.checkpoint else 0
 
@@ -1048,6 +1050,8 @@ class TuneController:
                         if decision == TrialScheduler.PAUSE:
                             self._stop_runner(t, save=True, reuse=True)
                             t.status = PAUSED
+                            if hasattr(self.searcher, "on_pause"):  # frees a ConcurrencyLimiter slot
+                                self.searcher.on_pause(t.trial_id)
                             break
                         if decision == TrialScheduler.NOOP:
                             break  # exploit() already restarted the trial
@@ -1073,6 +1077,8 @@ class TuneController:
             for x in self.trials:
                 if x.status == PAUSED and len([y for y in self.trials if y.status == RUNNING]) < self.max_conc:
                     x.status = PENDING
+                    if hasattr(self.searcher, "on_unpause"):
+                        self.searcher.on_unpause(x.trial_id)
                     x.restore_path = x.checkpoint.path if x.checkpoint else None
                     x.iteration_offset = x.last_result.get("training_iteration", 0)
         return any(x.status in (PAUSED, PENDING) for x in self.trials)

@@ -147,3 +147,52 @@ def test_analysis_best_checkpoint_by_metric(ray_start_regular, tmp_path):
     last = ana.get_last_checkpoint(trial)
     with last.as_directory() as d:
         assert json.load(open(os.path.join(d, "n.json")))["n"] == 4
+
+
+def test_searcher_and_scheduler_helpers():
+    from ray_community_amd.tune.schedulers import HyperBandScheduler, PopulationBasedTraining
+    from ray_community_amd.tune.search import BasicVariantGenerator, ConcurrencyLimiter, Searcher
+
+    g = BasicVariantGenerator()
+    g.set_space({"a": tune.grid_search([1, 2])}, 1)
+    assert g.total_samples == 2
+    g.add_configurations({"exp": {"config": {"a": tune.grid_search([3, 4, 5])}, "num_samples": 1}})
+    assert g.total_samples == 5 and [g.next_trial()["a"] for _ in range(5)] == [1, 2, 3, 4, 5]
+    assert g.next_trial() is None and not g.has_checkpoint("/nonexistent")
+
+    class _Count(Searcher):
+        def __init__(self):
+            super().__init__()
+            self.n, self.completed = 0, []
+
+        def suggest(self, trial_id):
+            self.n += 1
+            return {"i": self.n}
+
+        def on_trial_complete(self, trial_id, result=None, error=False):
+            self.completed.append(trial_id)
+
+    inner = _Count()
+    lim = ConcurrencyLimiter(inner, max_concurrent=2, batch=True)
+    assert lim.suggest("t1") and lim.suggest("t2") and lim.suggest("t3") is None
+    lim.on_trial_complete("t1", {})
+    assert lim.suggest("t3") is None and inner.completed == []  # the batch is still running
+    lim.on_trial_complete("t2", {})
+    assert inner.completed == ["t1", "t2"] and lim.suggest("t3") is not None
+    plain = ConcurrencyLimiter(_Count(), max_concurrent=1)
+    assert plain.suggest("a") and plain.suggest("b") is None
+    plain.on_pause("a")
+    assert plain.suggest("b") is not None
+    plain.on_unpause("a")
+    assert plain.live == {"a", "b"}
+
+    pbt = PopulationBasedTraining(metric="m", mode="max", hyperparam_mutations={"lr": [0.1, 0.2]})
+    pbt.scores = {"x": 1.0}
+
+    class _T:
+        trial_id = "x"
+
+    assert pbt.last_scores([_T()]) == [1.0]
+    pbt.reset_stats()
+    assert pbt.last_scores([_T()]) == []
+    assert HyperBandScheduler(metric="m", mode="max", max_t=9).state()["s_max"] == 2
