@@ -214,3 +214,9 @@ class FrameStackingEnvToModule(ConnectorV2):
 
     def reset_state(self):
         self.hist = None
+
+# the reference package's default pieces (see connectors/common.py)
+from .common import (AddObservationsFromEpisodesToBatch, AddStatesFromEpisodesToBatch, AgentToModuleMapping, BatchIndividualItems, NumpyToTensor, WriteObservationsToEpisodes)  # noqa: E402,F401
+from .connector_v2 import EnvToModulePipeline  # noqa: E402,F401
+
+PrevActionsPrevRewardsConnector = PrevActionsPrevRewards

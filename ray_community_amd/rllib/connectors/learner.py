@@ -39,3 +39,7 @@ class ClipRewards(ConnectorV2):
         r = batch["rewards"]
         batch["rewards"] = torch.sign(r) if self.limit is True else r.clamp(-float(self.limit), float(self.limit))
         return batch
+
+# the reference package's default pieces (see connectors/common.py)
+from .common import (AddColumnsFromEpisodesToTrainBatch, AddObservationsFromEpisodesToBatch, AddStatesFromEpisodesToBatch, AgentToModuleMapping, BatchIndividualItems, NumpyToTensor)  # noqa: E402,F401
+from .connector_v2 import LearnerConnectorPipeline  # noqa: E402,F401

@@ -35,3 +35,7 @@ class NormalizeAndClipActions(ConnectorV2):
 class ClipActions(NormalizeAndClipActions):
     def __init__(self, input_observation_space=None, input_action_space=None, **kw):
         super().__init__(input_observation_space, input_action_space, normalize_actions=False, clip_actions=True)
+
+# the reference package's default pieces (see connectors/common.py)
+from .common import (GetActions, ListifyDataForVectorEnv, ModuleToAgentUnmapping, RemoveSingleTsTimeRankFromBatch, TensorToNumpy, UnBatchToIndividualItems)  # noqa: E402,F401
+from .connector_v2 import ModuleToEnvPipeline  # noqa: E402,F401

@@ -161,3 +161,27 @@ def test_policy_from_algorithm_export(ray_start_regular, tmp_path):
         assert a.shape == (2,) and int(a[0]) == int(ref)
     finally:
         algo.stop()
+
+
+def test_default_connector_pieces_in_a_pipeline():
+    from ray_community_amd.rllib.connectors.env_to_module import (AddObservationsFromEpisodesToBatch,
+                                                                  BatchIndividualItems, EnvToModulePipeline,
+                                                                  NumpyToTensor)
+    from ray_community_amd.rllib.connectors.module_to_env import GetActions, TensorToNumpy
+    from ray_community_amd.rllib.core import Columns
+    from ray_community_amd.rllib.env.single_agent_episode import SingleAgentEpisode
+
+    eps = []
+    for i in range(3):
+        e = SingleAgentEpisode()
+        e.add_env_reset(np.full(4, float(i), np.float32))
+        eps.append(e)
+    m = RLModule(OBS, ACT, {"fcnet_hiddens": [8]})
+    pipe = EnvToModulePipeline(connectors=[AddObservationsFromEpisodesToBatch(), BatchIndividualItems(),
+                                           NumpyToTensor()])
+    batch = pipe(rl_module=m, batch={}, episodes=eps)
+    assert torch.is_tensor(batch[Columns.OBS]) and batch[Columns.OBS].shape == (3, 4)
+    out = {Columns.ACTION_DIST_INPUTS: m.forward_train(batch)[Columns.ACTION_DIST_INPUTS]}
+    out = GetActions()(rl_module=m, batch=out, explore=False)
+    out = TensorToNumpy()(rl_module=m, batch=out)
+    assert out[Columns.ACTIONS].shape == (3,) and isinstance(out[Columns.ACTION_LOGP], np.ndarray)
