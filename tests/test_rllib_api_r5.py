@@ -270,3 +270,19 @@ def test_build_policy_class_and_feature_importance():
     fi = FeatureImportance(_FirstFeature(None, None), repeat=3, seed=0)
     imp = fi.estimate(SampleBatch({"obs": x}))
     assert imp["feature_0"] > 0.2 and imp["feature_1"] == 0.0 and imp["feature_2"] == 0.0
+
+
+def test_rllib_metrics_helpers():
+    from ray_community_amd.rllib.utils.metrics import NUM_ENV_STEPS_SAMPLED
+    from ray_community_amd.rllib.utils.metrics.learner_info import LearnerInfoBuilder
+    from ray_community_amd.rllib.utils.metrics.window_stat import WindowStat
+
+    b = LearnerInfoBuilder()
+    b.add_learn_on_batch_results({"learner_stats": {"loss": 1.0}, "tag": "a"})
+    b.add_learn_on_batch_results({"learner_stats": {"loss": 3.0}, "tag": "b"})
+    assert b.finalize() == {"default_policy": {"learner_stats": {"loss": 2.0}, "tag": "b"}}
+    w = WindowStat("x", 3)
+    for i in range(5):
+        w.push(i)
+    assert w.stats()["x_mean"] == 3.0 and w.stats()["x_count"] == 5
+    assert NUM_ENV_STEPS_SAMPLED == "num_env_steps_sampled"
