@@ -45,12 +45,14 @@ class FifoReplayBuffer(ReplayBuffer):
 
     def add(self, batch: SampleBatch):
         n = batch.count
+        if n > self.capacity:  # only the newest ``capacity`` rows can be queued
+            batch = SampleBatch({k: v[n - self.capacity:] for k, v in batch.items()})
+            n = self.capacity
         if self.size + n > self.capacity:  # overflow drops the oldest queued items
             drop = self.size + n - self.capacity
             self._head = (self._head + drop) % self.capacity
             self.size -= drop
-        pos = super().add(batch)
-        return pos
+        return super().add(batch)
 
     def sample(self, num_items: int = 1, **kw) -> SampleBatch:
         n = min(int(num_items), self.size)
