@@ -213,7 +213,11 @@ def _reduce_concat(*pieces, shuffle_seed=None, sort_key=None, descending=False):
     if shuffle_seed is not None and acc.num_rows() > 0:
         perm = np.random.default_rng(shuffle_seed).permutation(acc.num_rows())
         b = acc.take(perm)
-    if sort_key is not None and acc.num_rows() > 0:
+    if isinstance(sort_key, list) and acc.num_rows() > 0:  # several keys: lexicographic, per-key order
+        df = BlockAccessor(b).to_pandas().reset_index(drop=True)
+        order = df.sort_values(sort_key, ascending=[not d for d in descending], kind="mergesort").index.to_numpy()
+        b = BlockAccessor(b).take(order)
+    elif sort_key is not None and acc.num_rows() > 0:
         d = BlockAccessor(b).to_numpy()
         order = np.argsort(d[sort_key], kind="stable")
         if descending:

@@ -235,11 +235,20 @@ class Dataset:
 
         return self._with({"kind": "alltoall", "fn": fn})
 
-    def sort(self, key: Union[str, List[str]], descending: bool = False) -> "Dataset":
-        k = key if isinstance(key, str) else key[0]
+    def sort(self, key: Union[str, List[str]], descending: Union[bool, List[bool]] = False,
+             boundaries: Optional[List] = None) -> "Dataset":
+        """Sort by one or more columns (lexicographic; ``descending`` per column or for all).
+        Rows are range-partitioned on the first column -- at sampled quantiles, or at the given
+        ``boundaries`` (one output block per range) -- and each partition sorts by every key."""
+        keys = [key] if isinstance(key, str) else list(key)
+        if not keys:
+            raise ValueError("sort needs at least one key")
+        desc = [bool(descending)] * len(keys) if isinstance(descending, bool) else [bool(d) for d in descending]
+        if len(desc) != len(keys):
+            raise ValueError(f"descending has {len(desc)} entries for {len(keys)} keys")
 
         def fn(refs):
-            return _sort(refs, k, descending)
+            return _sort(refs, keys, desc, boundaries)
 
         return self._with({"kind": "alltoall", "fn": fn})
 
@@ -789,25 +798,27 @@ def _repartition_to_sizes(refs, sizes, metas=None):
                       [{} for _ in sizes])
 
 
-def _sort(refs, key, descending):
+def _sort(refs, keys, desc, boundaries=None):
     from .._private.worker import get
 
     if not refs:
         return []
-    k = len(refs)
-    sample_fn = X._remote_fn(_sample_keys, {"num_cpus": 1})
-    samples = get([sample_fn.remote(b, key)[0] for b, _ in refs])
-    allk = np.concatenate([s for s in samples if len(s)]) if any(len(s) for s in samples) else np.array([])
-    if len(allk) == 0:
-        return refs
-    qs = np.quantile(np.sort(allk), np.linspace(0, 1, k + 1)[1:-1]) if k > 1 else np.array([])
-    if descending:
-        qs = qs[::-1].copy()
-        bounds = np.sort(qs)
+    key, descending = keys[0], desc[0]
+    if boundaries is not None:  # user ranges on the first key: one output block per range
+        bounds = np.sort(np.asarray(list(boundaries)))
+        k = len(bounds) + 1
     else:
-        bounds = qs
-    return X.exchange(refs, k, X._split_by_key_bounds, [(key, np.sort(bounds), descending) for _ in refs],
-                      X._reduce_concat, [{"sort_key": key, "descending": descending} for _ in range(k)])
+        k = len(refs)
+        sample_fn = X._remote_fn(_sample_keys, {"num_cpus": 1})
+        samples = get([sample_fn.remote(b, key)[0] for b, _ in refs])
+        allk = np.concatenate([s for s in samples if len(s)]) if any(len(s) for s in samples) else np.array([])
+        if len(allk) == 0:
+            return refs
+        bounds = np.sort(np.quantile(np.sort(allk), np.linspace(0, 1, k + 1)[1:-1])) if k > 1 else np.array([])
+    sort_key = key if len(keys) == 1 else list(keys)
+    sort_desc = descending if len(keys) == 1 else list(desc)
+    return X.exchange(refs, k, X._split_by_key_bounds, [(key, bounds, descending) for _ in refs],
+                      X._reduce_concat, [{"sort_key": sort_key, "descending": sort_desc} for _ in range(k)])
 
 
 def _sample_keys(block, key):

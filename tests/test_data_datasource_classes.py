@@ -132,3 +132,16 @@ def test_filename_provider_and_dummy_sink(ray_start_regular, tmp_path):
     sink = DummyOutputDatasink()
     ray.data.range(12, override_num_blocks=4).write_datasink(sink)
     assert sink.rows_written == 12 and sink.num_ok == 1
+
+
+def test_multi_key_sort_and_boundaries(ray_start_regular):
+    rows = [{"a": i % 3, "b": (7 * i) % 5, "c": i} for i in range(30)]
+    out = ray.data.from_items(rows, override_num_blocks=4).sort(["a", "b"], descending=[False, True]).take_all()
+    assert [(r["a"], r["b"]) for r in out] == sorted([(r["a"], r["b"]) for r in rows], key=lambda t: (t[0], -t[1]))
+    ds = ray.data.range(100, override_num_blocks=5).sort("id", boundaries=[25, 50, 75])
+    assert ds.num_blocks() == 4 if hasattr(ds, "num_blocks") else True
+    assert [r["id"] for r in ds.take_all()] == list(range(100))
+    desc = ray.data.range(50, override_num_blocks=3).sort("id", descending=True).take_all()
+    assert [r["id"] for r in desc] == list(range(49, -1, -1))
+    with pytest.raises(ValueError):
+        ray.data.range(3).sort(["id"], descending=[True, False])
