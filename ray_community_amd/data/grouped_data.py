@@ -29,7 +29,7 @@ class GroupedData:
             return self._shuffle(refs, aggs=list(aggs))
 
         ds = self._ds._with({"kind": "alltoall", "fn": fn})
-        return ds.sort(self._keys[0]) if self._keys else ds
+        return ds.sort(list(self._keys)) if self._keys else ds  # grouped rows ordered by every key
 
     def count(self):
         return self.aggregate(A.Count())
