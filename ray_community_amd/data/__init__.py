@@ -7,6 +7,7 @@ from .grouped_data import GroupedData
 from .iterator import DataIterator
 from .context import ExecutionOptions
 from ._internal.resource_manager import ExecutionResources
+from .block import BlockMetadata
 from .datasource import (BlockBasedFileDatasink, Datasink, ReadTask, RowBasedFileDatasink, from_arrow_refs, from_dask,
                          from_mars, from_modin, from_pandas_refs, from_spark, from_tf, read_bigquery,
                          read_databricks_tables, read_mongo, read_parquet_bulk, read_sql, read_tfrecords,
@@ -34,7 +35,7 @@ __all__ = ["Dataset", "MaterializedDataset", "DataIterator", "GroupedData", "Act
            "read_parquet", "read_csv", "read_json", "read_text", "read_numpy", "read_binary_files", "read_images",
            "read_datasource", "Datasource", "AggregateFn", "Count", "Sum", "Min", "Max", "Mean", "Std", "AbsMax",
            "Unique", "Datasink", "read_sql", "read_webdataset", "read_tfrecords", "read_parquet_bulk",
-           "from_pandas_refs", "from_arrow_refs", "RandomAccessDataset", "ExecutionOptions", "ExecutionResources",
+           "from_pandas_refs", "from_arrow_refs", "RandomAccessDataset", "ExecutionOptions", "ExecutionResources", "BlockMetadata",
            "ReadTask", "RowBasedFileDatasink", "BlockBasedFileDatasink", "DatasetIterator", "NodeIdStr",
            "set_progress_bars", "Preprocessor", "from_dask", "from_mars", "from_modin", "from_spark", "from_tf",
            "read_mongo", "read_bigquery", "read_databricks_tables"]

@@ -42,6 +42,33 @@ class ExecutionResources:
         return ExecutionResources(f(self.cpu, o.cpu), f(self.gpu, o.gpu),
                                   f(self.object_store_memory, o.object_store_memory))
 
+    def _map2(self, o: "ExecutionResources", f) -> "ExecutionResources":
+        return ExecutionResources(f(self.cpu, o.cpu), f(self.gpu, o.gpu),
+                                  f(self.object_store_memory, o.object_store_memory))
+
+    def subtract(self, o: "ExecutionResources") -> "ExecutionResources":
+        return self._map2(o, lambda a, b: (a or 0.0) - (b or 0.0))
+
+    def min(self, o: "ExecutionResources") -> "ExecutionResources":
+        """Per resource the smaller value (None = unlimited on that side)."""
+        return self._map2(o, lambda a, b: b if a is None else a if b is None else min(a, b))
+
+    def max(self, o: "ExecutionResources") -> "ExecutionResources":
+        return self._map2(o, lambda a, b: None if a is None or b is None else max(a, b))
+
+    @classmethod
+    def zero(cls) -> "ExecutionResources":
+        return cls(0.0, 0.0, 0.0)
+
+    def is_zero(self) -> bool:
+        return not (self.cpu or self.gpu or self.object_store_memory)
+
+    def is_non_negative(self) -> bool:
+        return all((v or 0.0) >= 0 for v in (self.cpu, self.gpu, self.object_store_memory))
+
+    def copy(self) -> "ExecutionResources":
+        return ExecutionResources(self.cpu, self.gpu, self.object_store_memory)
+
     def satisfies_limit(self, limit: "ExecutionResources") -> bool:
         for mine, lim in ((self.cpu, limit.cpu), (self.gpu, limit.gpu),
                           (self.object_store_memory, limit.object_store_memory)):

@@ -145,3 +145,13 @@ def test_multi_key_sort_and_boundaries(ray_start_regular):
     assert [r["id"] for r in desc] == list(range(49, -1, -1))
     with pytest.raises(ValueError):
         ray.data.range(3).sort(["id"], descending=[True, False])
+
+
+def test_execution_resources_arithmetic():
+    from ray_community_amd.data import BlockMetadata, ExecutionResources as E
+
+    a, b = E(4, 1, 100), E(2, None, 50)
+    assert a.subtract(b) == E(2, 1.0, 50) and a.min(b) == E(2, 1, 50) and a.max(b) == E(4, None, 100)
+    assert E.zero().is_zero() and not a.is_zero() and a.copy() == a
+    assert not E(1, 0, 0).subtract(E(2, 0, 0)).is_non_negative()
+    assert BlockMetadata is not None
