@@ -167,7 +167,8 @@ class Dashboard:
         if method == "POST" and not rest:
             from ..runtime_env import validate
 
-            res = {k: body.get(k) for k in ("entrypoint_num_cpus", "entrypoint_num_gpus", "entrypoint_resources")}
+            res = {k: body.get(k) for k in ("entrypoint_num_cpus", "entrypoint_num_gpus", "entrypoint_resources",
+                                            "entrypoint_memory")}
             try:
                 sid = get(mgr.submit.remote(body["entrypoint"], body.get("submission_id") or body.get("job_id"),
                                             validate(body.get("runtime_env")), body.get("metadata"), res))

@@ -74,6 +74,17 @@ class DriverInfo:
     pid: str
 
 
+class _EntrypointReservation:
+    """Holds a job's ``entrypoint_num_cpus / _num_gpus / _memory / _resources`` for as long as its
+    driver runs (reference: the job supervisor actor is scheduled with them); the GPUs it was
+    given become the driver's visible devices."""
+
+    def gpu_ids(self):
+        from ._private.worker import get_gpu_ids
+
+        return [str(g) for g in get_gpu_ids()]
+
+
 class JobManager:
     """Detached actor owning the job processes."""
 
@@ -83,6 +94,7 @@ class JobManager:
         os.makedirs(logs_dir, exist_ok=True)
         self.jobs: Dict[str, Dict] = {}
         self.procs: Dict[str, subprocess.Popen] = {}
+        self.holders: Dict[str, Any] = {}  # sid -> the actor reserving the entrypoint's resources
         self.lock = threading.Lock()
         threading.Thread(target=self._monitor, daemon=True).start()
 
@@ -107,6 +119,33 @@ class JobManager:
                         j["error_type"] = "JOB_ENTRYPOINT_COMMAND_ERROR"
                         j["message"] = f"Job entrypoint command failed with exit code {rc}"
                     del self.procs[sid]
+                    self._release(sid)
+
+    def _release(self, sid: str) -> None:
+        holder = self.holders.pop(sid, None)
+        if holder is not None:
+            from ._private.worker import kill
+
+            try:
+                kill(holder)
+            except Exception:  # noqa: BLE001 -- already gone
+                pass
+
+    def _reserve(self, resources: Dict):
+        """An actor holding the requested entrypoint resources, and its GPU ids (blocks until the
+        cluster can place it: the job stays PENDING meanwhile)."""
+        from . import remote
+        from ._private.worker import get
+
+        ncpu = resources.get("entrypoint_num_cpus") or 0
+        ngpu = resources.get("entrypoint_num_gpus") or 0
+        custom = dict(resources.get("entrypoint_resources") or {})
+        mem = resources.get("entrypoint_memory")
+        opts = {"num_cpus": ncpu, "num_gpus": ngpu, "resources": custom}
+        if mem:
+            opts["memory"] = mem
+        holder = remote(_EntrypointReservation).options(**opts).remote()
+        return holder, get(holder.gpu_ids.remote())
 
     def submit(self, entrypoint: str, submission_id: Optional[str], runtime_env: Optional[Dict],
                metadata: Optional[Dict], resources: Dict) -> str:
@@ -135,13 +174,41 @@ class JobManager:
             self.jobs[sid] = {"status": JobStatus.PENDING, "entrypoint": entrypoint, "submission_id": sid,
                               "metadata": dict(metadata or {}), "runtime_env": renv,
                               "start_time": int(time.time() * 1000), "log": log, **resources}
-            with open(log, "ab") as f:
-                p = subprocess.Popen(entrypoint, shell=True, cwd=cwd, env=env, stdout=f, stderr=subprocess.STDOUT,
-                                     stdin=subprocess.DEVNULL, start_new_session=True)
-            self.procs[sid] = p
-            self.jobs[sid]["status"] = JobStatus.RUNNING
-            self.jobs[sid]["job_id"] = f"{p.pid:08x}"
+            if not any(resources.get(k) for k in ("entrypoint_num_cpus", "entrypoint_num_gpus",
+                                                  "entrypoint_resources", "entrypoint_memory")):
+                self._launch(sid, entrypoint, cwd, env, log)
+                return sid
+        # reserved entrypoint resources: PENDING until they are placed, then the driver starts
+        threading.Thread(target=self._launch_reserved, args=(sid, entrypoint, cwd, env, log, resources),
+                         daemon=True).start()
         return sid
+
+    def _launch(self, sid, entrypoint, cwd, env, log) -> None:
+        with open(log, "ab") as f:
+            p = subprocess.Popen(entrypoint, shell=True, cwd=cwd, env=env, stdout=f, stderr=subprocess.STDOUT,
+                                 stdin=subprocess.DEVNULL, start_new_session=True)
+        self.procs[sid] = p
+        self.jobs[sid]["status"] = JobStatus.RUNNING
+        self.jobs[sid]["job_id"] = f"{p.pid:08x}"
+
+    def _launch_reserved(self, sid, entrypoint, cwd, env, log, resources) -> None:
+        try:
+            holder, gpus = self._reserve(resources)
+        except Exception as e:  # noqa: BLE001 -- an unplaceable request fails the job
+            with self.lock:
+                j = self.jobs[sid]
+                j["status"], j["error_type"] = JobStatus.FAILED, "JOB_SUPERVISOR_ACTOR_START_FAILURE"
+                j["message"] = f"could not reserve the entrypoint resources: {e}"
+                j["end_time"] = int(time.time() * 1000)
+            return
+        if gpus:  # the driver sees exactly the GPUs reserved for it
+            env = dict(env, HIP_VISIBLE_DEVICES=",".join(gpus), CUDA_VISIBLE_DEVICES=",".join(gpus))
+        with self.lock:
+            self.holders[sid] = holder
+            if self.jobs[sid]["status"] == JobStatus.STOPPED:  # stopped while pending
+                self._release(sid)
+                return
+            self._launch(sid, entrypoint, cwd, env, log)
 
     def info(self, sid: str) -> Optional[Dict]:
         with self.lock:
@@ -167,6 +234,11 @@ class JobManager:
         with self.lock:
             p = self.procs.get(sid)
             if p is None:
+                j = self.jobs.get(sid)
+                if j is not None and j["status"] == JobStatus.PENDING:  # still waiting for its resources
+                    j["status"], j["end_time"] = JobStatus.STOPPED, int(time.time() * 1000)
+                    j["message"] = "Job was intentionally stopped."
+                    return True
                 return False
             self.jobs[sid]["status"] = JobStatus.STOPPED
         try:
@@ -278,7 +350,7 @@ class JobSubmissionClient:
         from .runtime_env import validate
 
         res = {"entrypoint_num_cpus": entrypoint_num_cpus, "entrypoint_num_gpus": entrypoint_num_gpus,
-               "entrypoint_resources": entrypoint_resources}
+               "entrypoint_resources": entrypoint_resources, "entrypoint_memory": kw.get("entrypoint_memory")}
         if self._http:
             body = {"entrypoint": entrypoint, "submission_id": submission_id or job_id,
                     "runtime_env": runtime_env, "metadata": metadata, **res}

@@ -73,3 +73,30 @@ def test_job_rest_api_over_http(shutdown_only, tmp_path):
     assert requests.get(f"{url}/api/jobs/rest-sleeper", timeout=10).status_code == 404
     r = requests.post(f"{url}/api/jobs/", json={"entrypoint": "true", "submission_id": sid}, timeout=10)
     assert r.status_code == 400  # duplicate submission id
+
+
+def test_entrypoint_resources_are_reserved_while_the_driver_runs(shutdown_only, tmp_path):
+    import time
+
+    ray.init(num_cpus=4, resources={"slot": 1})
+    client = JobSubmissionClient()
+    flag = tmp_path / "release"
+    code = (f"import os, time\n"
+            f"while not os.path.exists({str(flag)!r}): time.sleep(0.05)\n")
+    (tmp_path / "hold.py").write_text(code)
+    first = client.submit_job(entrypoint=f"{sys.executable} {tmp_path / 'hold.py'}", entrypoint_num_cpus=1,
+                              entrypoint_resources={"slot": 1})
+    deadline = time.time() + 60
+    while client.get_job_status(first) != JobStatus.RUNNING and time.time() < deadline:
+        time.sleep(0.1)
+    assert client.get_job_status(first) == JobStatus.RUNNING
+    assert ray.available_resources().get("slot", 0) == 0  # held by the running driver
+    second = client.submit_job(entrypoint=f"{sys.executable} -c 'print(1)'", entrypoint_resources={"slot": 1})
+    time.sleep(1.0)
+    assert client.get_job_status(second) == JobStatus.PENDING  # waits for the slot
+    flag.write_text("go")
+    assert client.wait_until_finish(first, 60) == JobStatus.SUCCEEDED
+    assert client.wait_until_finish(second, 60) == JobStatus.SUCCEEDED
+    third = client.submit_job(entrypoint=f"{sys.executable} -c 'print(1)'", entrypoint_resources={"slot": 5})
+    time.sleep(0.5)
+    assert client.stop_job(third) and client.get_job_status(third) == JobStatus.STOPPED
