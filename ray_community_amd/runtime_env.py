@@ -93,6 +93,76 @@ class RuntimeEnv(dict):
             return pip
         return {"packages": list(pip)}
 
+    # ---- the reference's accessors (runtime_env/runtime_env.py). Environments are local
+    # directories and env vars here: the uri getters return the local paths, and the fields
+    # that need conda / containers / MPI / Nsight report what the dict holds.
+    def set(self, name: str, value: Any) -> None:
+        if name not in _KNOWN and name not in ("env_vars", "working_dir", "py_modules", "pip", "conda", "config"):
+            raise ValueError(f"unknown runtime_env field {name!r}")
+        self[name] = value
+
+    def has_working_dir(self) -> bool:
+        return self.get("working_dir") is not None
+
+    def working_dir_uri(self) -> Optional[str]:
+        return self.get("working_dir")
+
+    def py_modules_uris(self) -> List[str]:
+        return self.py_modules()
+
+    def has_pip(self) -> bool:
+        return self.get("pip") is not None
+
+    def pip_uri(self) -> Optional[str]:
+        return None
+
+    def has_conda(self) -> bool:
+        return self.get("conda") is not None
+
+    def conda_uri(self) -> Optional[str]:
+        return None
+
+    def conda_env_name(self) -> Optional[str]:
+        c = self.get("conda")
+        return c if isinstance(c, str) else None
+
+    def conda_config(self) -> Optional[str]:
+        c = self.get("conda")
+        return json.dumps(c, sort_keys=True) if isinstance(c, dict) else None
+
+    def virtualenv_name(self) -> Optional[str]:
+        return None
+
+    def plugin_uris(self) -> List[str]:
+        return []
+
+    def plugins(self) -> List:
+        return []
+
+    def java_jars(self) -> List[str]:
+        return list(self.get("java_jars") or [])
+
+    def mpi(self) -> Optional[Dict]:
+        return self.get("mpi")
+
+    def nsight(self) -> Optional[Any]:
+        return self.get("nsight")
+
+    def has_py_container(self) -> bool:
+        return bool(self.get("container"))
+
+    def py_container_image(self) -> Optional[str]:
+        return (self.get("container") or {}).get("image")
+
+    def py_container_worker_path(self) -> Optional[str]:
+        return (self.get("container") or {}).get("worker_path")
+
+    def py_container_run_options(self) -> List:
+        return list((self.get("container") or {}).get("run_options") or [])
+
+    def get_extension(self, key, default=None):
+        return self.get(key, default)
+
     def to_dict(self) -> Dict[str, Any]:
         return dict(self)
 

@@ -288,3 +288,15 @@ def test_tune_serve_experimental_module_paths(ray_start_regular, tmp_path, capsy
         assert tags["deployment"] == "M" and tags["application"] == "m" and tags["replica"]
     finally:
         serve.shutdown()
+
+
+def test_runtime_env_accessors():
+    from ray_community_amd.runtime_env import RuntimeEnv
+
+    r = RuntimeEnv(env_vars={"A": "1"}, working_dir="/tmp/wd", conda="myenv")
+    assert r.has_working_dir() and r.working_dir_uri() == "/tmp/wd" and r.has_conda()
+    assert r.conda_env_name() == "myenv" and not r.has_pip() and r.plugin_uris() == []
+    r.set("env_vars", {"B": "2"})
+    assert r.env_vars() == {"B": "2"}
+    with pytest.raises(ValueError):
+        r.set("not_a_field", 1)
