@@ -218,6 +218,30 @@ class StandardAutoscaler:
                 "unmet": len(unmet) + len(unmet_req), "workers": dict(counts)}
 
     # ------------------------------------------------------------------ monitor loop
+    @property
+    def all_node_types(self):
+        return set(self.types)
+
+    def summary(self) -> Dict:
+        """Active nodes per type and the configured bounds (reference ``StandardAutoscaler.summary``)."""
+        nodes = self.provider.non_terminated_nodes()
+        counts = self._counts(nodes)
+        return {"active_nodes": counts, "num_nodes": len(nodes), "max_workers": self.max_workers,
+                "node_types": {n: {"min_workers": int(t.get("min_workers", 0)),
+                                   "max_workers": int(t.get("max_workers", 0))} for n, t in self.types.items()}}
+
+    def info_string(self) -> str:
+        s = self.summary()
+        lines = ["======== Autoscaler status ========", "Node types (active / min / max):"]
+        for n, b in sorted(s["node_types"].items()):
+            lines.append(f"  {n}: {s['active_nodes'].get(n, 0)} / {b['min_workers']} / {b['max_workers']}")
+        lines.append(f"Total nodes: {s['num_nodes']} (max workers {s['max_workers']})")
+        return "\n".join(lines)
+
+    def reset(self, errors_fatal: bool = False) -> None:
+        """Forget idle timers (a config reload in the reference)."""
+        self._idle_since = {}
+
     def start(self, interval_s: float = 1.0) -> "StandardAutoscaler":
         def loop():
             while not self._stop.wait(interval_s):

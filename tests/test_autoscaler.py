@@ -43,6 +43,8 @@ def test_scale_up_for_infeasible_tasks_then_idle_scale_down(one_cpu):
     rep = asc.update()
     # three queued {CPU:1, accel:1} shapes: one accel_worker each (accel: 1 per node), none on cpu_worker
     assert [n for n, _ in rep["launched"]] == ["accel_worker"] * 3
+    assert asc.summary()["active_nodes"]["accel_worker"] == 3 and "accel_worker: 3" in asc.info_string()
+    assert "accel_worker" in asc.all_node_types
     out = ray.get(refs, timeout=120)
     assert sorted(x for _, x in out) == [0, 1, 2]
     assert len({nid for nid, _ in out}) >= 1
