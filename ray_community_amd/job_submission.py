@@ -346,11 +346,12 @@ class JobSubmissionClient:
     def submit_job(self, *, entrypoint: str, job_id: Optional[str] = None, runtime_env: Optional[Dict] = None,
                    metadata: Optional[Dict[str, str]] = None, submission_id: Optional[str] = None,
                    entrypoint_num_cpus: Optional[float] = None, entrypoint_num_gpus: Optional[float] = None,
-                   entrypoint_resources: Optional[Dict[str, float]] = None, **kw) -> str:
+                   entrypoint_resources: Optional[Dict[str, float]] = None, entrypoint_memory: Optional[int] = None,
+                   **kw) -> str:
         from .runtime_env import validate
 
         res = {"entrypoint_num_cpus": entrypoint_num_cpus, "entrypoint_num_gpus": entrypoint_num_gpus,
-               "entrypoint_resources": entrypoint_resources, "entrypoint_memory": kw.get("entrypoint_memory")}
+               "entrypoint_resources": entrypoint_resources, "entrypoint_memory": entrypoint_memory}
         if self._http:
             body = {"entrypoint": entrypoint, "submission_id": submission_id or job_id,
                     "runtime_env": runtime_env, "metadata": metadata, **res}
