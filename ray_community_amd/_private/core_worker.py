@@ -425,6 +425,9 @@ class CoreWorker:
         self._put_lock = threading.Lock()
         # inline descriptors of this process's own live puts: ray.get on them is local
         self._put_cache: Dict[bytes, tuple] = {}
+        # puts the head REJECTED (the error arrives only on the ack future): the next get / wait of
+        # such a ref raises it instead of answering from _put_cache
+        self._put_errors: Dict[bytes, BaseException] = {}
         ser.set_escape_hook(self.sync_puts)
 
     # -------------------------------------------------------------- reference counting
@@ -449,6 +452,7 @@ class CoreWorker:
         if n == 0:
             self._ready_known.discard(oid)
             self._put_cache.pop(oid, None)
+            self._put_errors.pop(oid, None)
             if oid in self.owned.objs and not self.owned.drop(oid):
                 return  # a caller-owned result the head never heard of
             self.client.ref_delta((), (oid,))
@@ -508,16 +512,39 @@ class CoreWorker:
         if not fut.done():
             with self._put_lock:
                 self._unacked[oid] = fut
-            fut.add_done_callback(lambda _f, o=oid: self._acked(o))
-        elif fut.exception() is not None:
+            if desc[0] == "inline":
+                self._put_cache[oid] = (desc[0], desc[1], desc[2], s.flags)
+            fut.add_done_callback(lambda f, o=oid: self._acked(o, f))
+            return ref
+        if fut.exception() is not None:
             raise fut.exception()
         if desc[0] == "inline":
             self._put_cache[oid] = (desc[0], desc[1], desc[2], s.flags)
         return ref
 
-    def _acked(self, oid):
+    def _acked(self, oid, fut=None):
+        err = None
+        if fut is not None and not fut.cancelled():
+            err = fut.exception()
         with self._put_lock:
             self._unacked.pop(oid, None)
+            if err is not None:
+                # the head never registered it: the locally cached value must not be served
+                self._put_cache.pop(oid, None)
+                self._put_errors[oid] = err
+
+    def forget_puts(self, oids):
+        """``ray.internal.free``: freed objects are no longer answered from the local put cache."""
+        for o in oids:
+            self._put_cache.pop(o, None)
+
+    def _raise_put_errors(self, oids):
+        pe = self._put_errors
+        if pe:
+            for o in oids:
+                e = pe.get(o)
+                if e is not None:
+                    raise e
 
     def sync_puts(self, oids=None):
         """Wait until the head has registered this process's puts among ``oids`` (all if None)."""
@@ -601,6 +628,7 @@ class CoreWorker:
     def _get_descs(self, oids, timeout):
         """Descriptors for ``oids``: caller-owned results from the local table (no head round
         trip), the rest from the head."""
+        self._raise_put_errors(oids)
         pc = self._put_cache
         if pc:
             hit = [pc.get(o) for o in oids]
@@ -697,6 +725,7 @@ class CoreWorker:
         self._wait_rest = None
         refs = list(refs)
         ids = list(map(_REF_ID, refs))  # C-level pass (wait() is called once per completion when polling)
+        self._raise_put_errors(ids)
         sids = set(ids)
         if len(sids) != len(ids):
             raise ValueError("Wait requires a list of unique object refs.")

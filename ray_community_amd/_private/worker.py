@@ -346,6 +346,7 @@ def free(object_refs, local_only=False):
     for r in object_refs:
         if r._id in core.owned.objs:
             core.owned.publish(r._id)
+    core.forget_puts([r._id for r in object_refs])
     core.client.call("free", [r._id for r in object_refs])
 
 

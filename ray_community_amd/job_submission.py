@@ -84,6 +84,23 @@ class _EntrypointReservation:
 
         return [str(g) for g in get_gpu_ids()]
 
+    def device_env(self):
+        """The device-visibility variables the driver must run with to see exactly this holder's
+        GPUs: the holder's own ``HIP_VISIBLE_DEVICES`` -- already mapped through the head's parent
+        mask by the worker pool (``_private/head.py::worker_hip_visible_devices``), i.e. PHYSICAL
+        ids when the head was started with ``HIP_VISIBLE_DEVICES=4,5`` -- and the
+        ``ROCR_VISIBLE_DEVICES`` it indexes into. Empty when no GPU was reserved."""
+        if not self.gpu_ids():
+            return {}
+        out = {}
+        hip = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+        if hip:
+            out["HIP_VISIBLE_DEVICES"] = out["CUDA_VISIBLE_DEVICES"] = hip
+        rocr = os.environ.get("ROCR_VISIBLE_DEVICES")
+        if rocr is not None:
+            out["ROCR_VISIBLE_DEVICES"] = rocr
+        return out
+
 
 class JobManager:
     """Detached actor owning the job processes."""
@@ -145,7 +162,7 @@ class JobManager:
         if mem:
             opts["memory"] = mem
         holder = remote(_EntrypointReservation).options(**opts).remote()
-        return holder, get(holder.gpu_ids.remote())
+        return holder, get(holder.device_env.remote())
 
     def submit(self, entrypoint: str, submission_id: Optional[str], runtime_env: Optional[Dict],
                metadata: Optional[Dict], resources: Dict) -> str:
@@ -193,7 +210,7 @@ class JobManager:
 
     def _launch_reserved(self, sid, entrypoint, cwd, env, log, resources) -> None:
         try:
-            holder, gpus = self._reserve(resources)
+            holder, dev_env = self._reserve(resources)
         except Exception as e:  # noqa: BLE001 -- an unplaceable request fails the job
             with self.lock:
                 j = self.jobs[sid]
@@ -201,8 +218,8 @@ class JobManager:
                 j["message"] = f"could not reserve the entrypoint resources: {e}"
                 j["end_time"] = int(time.time() * 1000)
             return
-        if gpus:  # the driver sees exactly the GPUs reserved for it
-            env = dict(env, HIP_VISIBLE_DEVICES=",".join(gpus), CUDA_VISIBLE_DEVICES=",".join(gpus))
+        if dev_env:  # the driver sees exactly the GPUs reserved for it (physical ids, not logical)
+            env = dict(env, **dev_env)
         with self.lock:
             self.holders[sid] = holder
             if self.jobs[sid]["status"] == JobStatus.STOPPED:  # stopped while pending

@@ -12,6 +12,8 @@ per-step terminated/done flags.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -399,13 +401,18 @@ def ce_fused_supported(V: int) -> bool:
 _WS = {}
 
 
-def _workspace(device, key, numel, dtype=torch.float32):
+def _workspace(device, key, numel, dtype=torch.float32, zero=False):
     k = (str(device), key)
     t = _WS.get(k)
     if t is None or t.numel() < numel:
-        t = torch.empty(numel, device=device, dtype=dtype)
+        t = (torch.zeros if zero else torch.empty)(numel, device=device, dtype=dtype)
         _WS[k] = t
     return t
+
+
+# floats of the rca_sumsq workspace: 1024 block partials + the last-block ticket word (zeroed once;
+# every launch leaves it zero again)
+SUMSQ_WS = 1028
 
 
 def grad_sumsq(tensors, out=None):
@@ -421,7 +428,7 @@ def grad_sumsq(tensors, out=None):
         out.reshape(-1)[0] = s
         return out
     out = torch.zeros(1, device=dev, dtype=torch.float32) if out is None else out
-    part = _workspace(dev, "sumsq", 1024)
+    part = _workspace(dev, "sumsq", SUMSQ_WS, zero=True)
     L = lib()
     st = stream_ptr(dev)
     for i, t in enumerate(tensors):
@@ -884,13 +891,54 @@ def _attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, strides, 
     """Attention backward. With a dS workspace (D = 128, default mode) the dK/dV kernel stores the
     bf16 dS tiles and dQ = dS.K is read back from them (no S/P/dP recomputation for dQ); the
     workspace is a transient caching-allocator block (1.08 GB at the Llama-3-8B shape, reused by
-    every layer's backward)."""
+    every layer's backward).
+
+    The workspace grows as B*Hq*S^2 (34 GB at S = 32k, B*Hq = 32), so it is only taken when it fits
+    ``attn_ds_workspace_cap(device)`` -- an absolute cap (``RCA_ATTN_DS_WS_MAX_GB``, default 8) and
+    a fraction of the device's free memory -- and when the allocation itself succeeds; otherwise the
+    O(S)-memory recompute path (dQ kernel recomputing S, P, dP) runs, with the same gradients up to
+    rounding (``tests/test_attention_gpu.py::test_ds_workspace_cap_falls_back_to_recompute``)."""
     L = lib()
     nbytes = L.rca_attn_bwd_ws_bytes(B, S, Hq, Hk, D, int(causal))
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=device) if nbytes > 0 else None
+    ws = None
+    if nbytes > 0 and nbytes <= attn_ds_workspace_cap(device):
+        try:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        except torch.OutOfMemoryError:
+            ws = None
+    if ws is None:
+        nbytes = 0
     check(L.rca_attn_bwd2(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, Hq, Hk, D, *strides, scale, int(causal),
                           ws.data_ptr() if ws is not None else None, nbytes, stream_ptr()), "rca_attn_bwd2")
     del ws  # stream-ordered: the caching allocator reuses the block only for later work on this stream
+
+
+_DS_WS_CAP_OVERRIDE = None
+
+
+def attn_ds_workspace_cap(device=None) -> int:
+    """Largest dS workspace (bytes) the attention backward may allocate: min of the absolute cap
+    (``RCA_ATTN_DS_WS_MAX_GB``, default 8 GB: 7x the Llama-3-8B bench's 1.08 GB) and half of the
+    memory the caching allocator could still hand out (free device memory + its reserved-unused
+    blocks). ``set_attn_ds_workspace_cap(n)`` overrides it (tests, memory-tight jobs)."""
+    if _DS_WS_CAP_OVERRIDE is not None:
+        return int(_DS_WS_CAP_OVERRIDE)
+    cap = int(float(os.environ.get("RCA_ATTN_DS_WS_MAX_GB", "8")) * (1 << 30))
+    try:
+        free, _ = torch.cuda.mem_get_info(device)
+        idx = torch.device(device).index if device is not None else None
+        spare = torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
+        cap = min(cap, (free + max(spare, 0)) // 2)
+    except (RuntimeError, AssertionError, ValueError):
+        pass
+    return cap
+
+
+def set_attn_ds_workspace_cap(nbytes):
+    """Override the dS workspace cap (``None`` restores the default policy); returns the old override."""
+    global _DS_WS_CAP_OVERRIDE
+    old, _DS_WS_CAP_OVERRIDE = _DS_WS_CAP_OVERRIDE, nbytes
+    return old
 
 
 class _FlashAttnQKV(torch.autograd.Function):

@@ -219,10 +219,20 @@ RCA_API int rca_ce_fused(void* logits, const long long* labels, const float* gsc
 }
 
 // ----------------------------------------------------------------------------- grad norm
-// partial[b] = sum of squares of this block's grid-stride share; dtype 0 = bf16, 1 = f32
+// partial[b] = sum of squares of this block's grid-stride share; dtype 0 = bf16, 1 = f32.
+// The LAST block to finish folds the partials into out[0] itself (last-block-done ticket in
+// ticket[0], reset by that block), so there is no second single-workgroup launch: on the grad-norm
+// side stream such a launch queued behind the backward GEMMs' full-chip waves for ~200 us each
+// (68 per 8B step). Hand-off per cdna_hip_programming.md Guideline 16: every block stores its
+// partial, drains it (vmcnt(0)), barrier, one lane releases at agent scope and takes a ticket; the
+// block that draws nb-1 acquires at agent scope and sums the partials in index order, so the
+// result is bit-identical to the two-launch form and run-to-run deterministic.
 template <int DT>
-__global__ __launch_bounds__(256) void sumsq_partial_kernel(const void* __restrict__ g, long long n, float* __restrict__ partial) {
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const void* __restrict__ g, long long n, float* __restrict__ partial,
+                                                            unsigned* __restrict__ ticket, float* __restrict__ out,
+                                                            int accumulate) {
   __shared__ float red[16];
+  __shared__ int last;
   float acc = 0.f;
   if (DT == 0) {
     const bf16_t* x = (const bf16_t*)g;
@@ -273,28 +283,44 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const void* __restri
       acc += x[i] * x[i];
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+  const unsigned nb = gridDim.x;
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = acc;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == nb - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  float s = 0.f;
+  for (unsigned i = threadIdx.x; i < nb; i += blockDim.x) s += partial[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    out[0] = accumulate ? out[0] + s : s;
+    // re-arm for the next launch on this workspace (stream order: the next launch starts after
+    // this block has exited)
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partial, int nb, float* __restrict__ out,
-                                                           int accumulate) {
-  __shared__ float red[16];
-  float acc = 0.f;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += partial[i];
-  acc = block_sum(acc, red);
-  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + acc : acc;
-}
-
-// out[0] (+)= sum(g^2). partial must hold >= 1024 floats. Deterministic (no atomics).
+// out[0] (+)= sum(g^2). partial must hold >= RCA_SUMSQ_WS floats (1024 partials + the ticket word
+// at index 1024, zero before the first use; the kernel leaves it zero). Deterministic (no float
+// atomics: the partials are combined in index order by the last block).
 RCA_API int rca_sumsq(const void* g, long long n, int dtype, float* partial, float* out, int accumulate, hipStream_t stream) {
   long long nb = (n / (dtype == 0 ? 8 : 4) + 255) / 256;
   if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
+  unsigned* ticket = reinterpret_cast<unsigned*>(partial + 1024);
   if (dtype == 0)
-    hipLaunchKernelGGL(sumsq_partial_kernel<0>, dim3((int)nb), dim3(256), 0, stream, g, n, partial);
+    hipLaunchKernelGGL(sumsq_partial_kernel<0>, dim3((int)nb), dim3(256), 0, stream, g, n, partial, ticket, out, accumulate);
   else
-    hipLaunchKernelGGL(sumsq_partial_kernel<1>, dim3((int)nb), dim3(256), 0, stream, g, n, partial);
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, partial, (int)nb, out, accumulate);
+    hipLaunchKernelGGL(sumsq_partial_kernel<1>, dim3((int)nb), dim3(256), 0, stream, g, n, partial, ticket, out, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .. import ops
 from .flat import FlatParameters, register_grad_ready
 
 
@@ -92,7 +93,7 @@ class DistributedDataParallel(nn.Module):
         if precompute_grad_norm and self.flat.device.type == "cuda":
             dev = self.flat.device
             self._norm = {"stream": torch.cuda.Stream(device=dev), "sumsq": torch.zeros(1, device=dev),
-                          "partial": torch.empty(1024, device=dev), "n": 0, "done": torch.cuda.Event()}
+                          "partial": torch.zeros(ops.SUMSQ_WS, device=dev), "n": 0, "done": torch.cuda.Event()}
         if self.world > 1:
             src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
             dist.broadcast(self.flat.data, src=src, group=process_group)

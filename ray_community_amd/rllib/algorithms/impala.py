@@ -8,9 +8,20 @@ concatenated ``[N, T]`` fragments. Runners therefore act with weights that lag t
 few updates; V-trace (a HIP kernel over the env-major fragments, ``ops.vtrace``) corrects for the
 policy lag. Weights are broadcast without blocking every ``broadcast_interval`` updates (actor
 calls are ordered per caller, so a runner's next fragment uses them).
+
+Learner queue (reference ``rllib/execution/learner_thread.py``, ``impala.py``
+``place_processed_samples_on_learner_thread_queue``): with ``learner_queue_size > 0`` (default 16)
+a background learner thread owns the LearnerGroup updates. ``training_step`` only samples and
+enqueues train batches (blocking for at most ``learner_queue_timeout`` seconds when the queue is
+full) and collects whatever updates finished meanwhile, so sampling continues while the learner
+trains; the learner thread snapshots the weights after every ``broadcast_interval`` updates and
+the next ``training_step`` broadcasts them. ``learner_queue_size = 0`` trains inline.
 """
 from __future__ import annotations
 
+import queue
+import threading
+import time
 from typing import Dict, List
 
 from ..policy.sample_batch import concat_samples
@@ -35,6 +46,8 @@ class IMPALAConfig(AlgorithmConfig):
         self.max_requests_in_flight_per_env_runner = 2
         self.num_epochs = 1
         self.minibatch_size = None
+        self.learner_queue_size = 16
+        self.learner_queue_timeout = 300
 
 
 class IMPALA(Algorithm):
@@ -96,6 +109,8 @@ class IMPALA(Algorithm):
 
     def training_step(self) -> Dict:
         cfg = self.config
+        if int(getattr(cfg, "learner_queue_size", 0) or 0) > 0:
+            return self._training_step_queued()
         batch = self._sample_async(cfg.train_batch_size)
         n = batch.count
         self._timesteps_total += n
@@ -107,7 +122,137 @@ class IMPALA(Algorithm):
         info["num_weight_broadcasts"] = self._weights_version
         return info
 
+    # ------------------------------------------------------------------ learner thread
+    def _start_learner_thread(self):
+        cfg = self.config
+        self._lq = queue.Queue(maxsize=int(cfg.learner_queue_size))
+        self._lq_out = queue.Queue()
+        self._lq_stop = threading.Event()
+        self._lq_lock = threading.Lock()  # held around every update (checkpointing takes it too)
+        self._lq_weights = None  # (update count, weights) snapshot awaiting broadcast
+        self._lq_updates = 0
+        self._lq_error = None
+        # (start, end) wall times of the learner's updates and of the driver's sample collections:
+        # what ``learner_overlap_s`` (sampling while the learner trains) is computed from
+        self._lq_update_spans: List = []
+        self._sample_spans: List = []
+        every = max(1, int(cfg.broadcast_interval))
+
+        def run():
+            while not self._lq_stop.is_set():
+                try:
+                    batch = self._lq.get(timeout=0.05)
+                except queue.Empty:
+                    continue
+                try:
+                    t0 = time.perf_counter()
+                    with self._lq_lock:
+                        info = self.learner_group.update(self._update_kind, batch)
+                        self._lq_updates += 1
+                        if self._lq_updates % every == 0:
+                            self._lq_weights = (self._lq_updates, self.learner_group.get_weights())
+                    self._lq_update_spans.append((t0, time.perf_counter()))
+                    del self._lq_update_spans[:-256]
+                    self._lq_out.put(info)
+                except BaseException as e:  # noqa: BLE001 -- surfaced by the next training_step
+                    self._lq_error = e
+                    return
+
+        self._lq_thread = threading.Thread(target=run, name="rllib-learner-thread", daemon=True)
+        self._lq_thread.start()
+
+    def _training_step_queued(self) -> Dict:
+        cfg = self.config
+        if getattr(self, "_lq_thread", None) is None:
+            self._start_learner_thread()
+        if self._lq_error is not None:
+            raise self._lq_error
+        if not self._lq_thread.is_alive():
+            raise RuntimeError("The IMPALA learner thread has died")
+        t0 = time.perf_counter()
+        batch = self._sample_async(cfg.train_batch_size)
+        self._sample_spans.append((t0, time.perf_counter()))
+        del self._sample_spans[:-256]
+        n = batch.count
+        self._timesteps_total += n
+        try:
+            self._lq.put(batch, block=True, timeout=float(cfg.learner_queue_timeout))
+        except queue.Full:
+            raise RuntimeError(f"the learner queue stayed full for learner_queue_timeout="
+                               f"{cfg.learner_queue_timeout} s: the learner is not keeping up") from None
+        infos = []
+        # the first iteration waits for one result (there is nothing to report otherwise)
+        if getattr(self, "_lq_last_info", None) is None:
+            infos.append(self._wait_learner_result(float(cfg.learner_queue_timeout)))
+        while True:
+            try:
+                infos.append(self._lq_out.get_nowait())
+            except queue.Empty:
+                break
+        if infos:
+            self._lq_last_info = infos[-1]
+        snap, self._lq_weights = self._lq_weights, None
+        if snap is not None:
+            self._broadcast_weights(snap[1])
+        self._num_updates = self._lq_updates
+        info = dict(self._lq_last_info)
+        info["_steps_this_iter"] = n
+        info["num_weight_broadcasts"] = self._weights_version
+        info["learner_queue_size"] = self._lq.qsize()
+        info["num_learner_updates"] = self._lq_updates
+        info["num_updates_this_iter"] = len(infos)
+        info["learner_overlap_s"] = self._learner_overlap_s()
+        return info
+
+    def _wait_learner_result(self, timeout: float):
+        deadline = time.monotonic() + timeout
+        while True:
+            if self._lq_error is not None:
+                raise self._lq_error
+            try:
+                return self._lq_out.get(timeout=0.05)
+            except queue.Empty:
+                if time.monotonic() > deadline:
+                    raise RuntimeError("no learner result within learner_queue_timeout") from None
+
+    def _learner_overlap_s(self) -> float:
+        """Seconds in which the driver was collecting samples WHILE the learner thread was updating
+        (over the recorded spans): > 0 means sampling and learning overlap."""
+        tot = 0.0
+        ups = list(self._lq_update_spans)
+        for a, b in list(self._sample_spans):
+            for c, d in ups:
+                lo, hi = max(a, c), min(b, d)
+                if hi > lo:
+                    tot += hi - lo
+        return tot
+
+    def _broadcast_weights(self, st):
+        from ..._private.worker import put
+
+        self._weights_version += 1
+        self.local_runner.set_weights(st, self._weights_version)
+        if self.remote_runners:
+            ref = put(st)
+            for r in self.remote_runners:
+                r.set_weights.remote(ref, self._weights_version)
+
+    def _stop_learner_thread(self):
+        th = getattr(self, "_lq_thread", None)
+        if th is not None:
+            self._lq_stop.set()
+            th.join(timeout=30)
+            self._lq_thread = None
+
+    def save_checkpoint(self, checkpoint_dir: str):
+        lock = getattr(self, "_lq_lock", None)
+        if lock is None:
+            return super().save_checkpoint(checkpoint_dir)
+        with lock:  # no update half-applied in the saved learner state
+            return super().save_checkpoint(checkpoint_dir)
+
     def stop(self):
+        self._stop_learner_thread()
         self._inflight = {}
         super().stop()
 
@@ -123,6 +268,9 @@ class APPOConfig(IMPALAConfig):
         self.kl_target = 0.01
         self.num_epochs = 1
         self.lr = 0.0005
+        # target network (reference appo.py): Polyak coefficient and refresh period in learner updates
+        self.tau = 1.0
+        self.target_update_frequency = 1
 
 
 class APPO(IMPALA):

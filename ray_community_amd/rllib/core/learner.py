@@ -50,6 +50,8 @@ class Learner(LearnerAPI):
         self.kl_coeff = config.get("kl_coeff", 0.2)
         self.target = None
         self.num_updates = 0
+        self.last_target_update = 0  # APPO: learner update count at the last target refresh
+        self.num_target_updates = 0
         from ..connectors import build_learner_connector
 
         self.learner_connector = build_learner_connector(config, obs_space, act_space)
@@ -64,12 +66,28 @@ class Learner(LearnerAPI):
         self.module.set_state(state)
 
     def get_state(self):
-        return {"module": self.module.get_state(), "opt": self.opt.state_dict(), "kl_coeff": self.kl_coeff}
+        st = {"module": self.module.get_state(), "opt": self.opt.state_dict(), "kl_coeff": self.kl_coeff,
+              "num_updates": self.num_updates, "last_target_update": self.last_target_update,
+              "num_target_updates": self.num_target_updates}
+        if self.target is not None:
+            st["target"] = {k: v.detach().cpu().clone() for k, v in self.target.state_dict().items()}
+        return st
 
     def set_state(self, st):
         self.module.set_state(st["module"])
         self.opt.load_state_dict(st["opt"])
         self.kl_coeff = st.get("kl_coeff", self.kl_coeff)
+        self.num_updates = st.get("num_updates", self.num_updates)
+        self.last_target_update = st.get("last_target_update", self.last_target_update)
+        self.num_target_updates = st.get("num_target_updates", self.num_target_updates)
+        if "target" in st:
+            import copy
+
+            if self.target is None:
+                self.target = copy.deepcopy(self.module)
+                for p in self.target.parameters():
+                    p.requires_grad_(False)
+            self.target.load_state_dict({k: v.to(self.device) for k, v in st["target"].items()})
 
     def _lr(self):
         sched = self.cfg.get("lr_schedule")
@@ -302,47 +320,110 @@ class Learner(LearnerAPI):
         loss = pi_loss + cfg.get("vf_loss_coeff", 0.5) * vf_loss - cfg.get("entropy_coeff", 0.01) * ent
         gn = self._step(loss)
         self.num_updates += 1
-        return {"policy_loss": float(pi_loss), "vf_loss": float(vf_loss), "entropy": float(ent),
-                "total_loss": float(loss), "grad_gnorm": float(gn) if gn is not None else float("nan"),
+        gn_t = gn.detach().float().reshape(()) if gn is not None else torch.full((), float("nan"), device=self.device)
+        # ONE device->host transfer for every statistic (no per-stat sync)
+        pl, vl, en, tl, g = torch.stack([pi_loss.detach(), vf_loss.detach(), ent.detach(), loss.detach(),
+                                         gn_t.to(loss.device)]).tolist()
+        return {"policy_loss": pl, "vf_loss": vl, "entropy": en, "total_loss": tl, "grad_gnorm": g,
                 "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr()}
 
+    # ---------------------------------------------------------------- APPO target network
+    def _appo_target(self):
+        """The APPO target policy (reference ``appo_torch_learner._update_module_target_networks``):
+        a frozen copy of the module, created equal to it on the first update and then Polyak-updated
+        ``target <- tau * online + (1 - tau) * target`` every ``target_update_frequency`` learner
+        updates. It is the "old" policy of the surrogate's importance ratio and of the KL term."""
+        if self.target is None:
+            import copy
+
+            self.target = copy.deepcopy(self.module)
+            for p in self.target.parameters():
+                p.requires_grad_(False)
+            self.last_target_update = self.num_updates
+        return self.target
+
+    @torch.no_grad()
+    def update_target_network(self, tau: Optional[float] = None):
+        tgt = self._appo_target()
+        tau = float(self.cfg.get("tau", 1.0) if tau is None else tau)
+        for t, o in zip(tgt.state_dict().values(), self.module.state_dict().values()):
+            if t.is_floating_point():
+                if tau >= 1.0:
+                    t.copy_(o)
+                else:
+                    t.mul_(1.0 - tau).add_(o, alpha=tau)
+            else:
+                t.copy_(o)
+        self.num_target_updates += 1
+        self.last_target_update = self.num_updates
+
     def update_appo(self, batch: SampleBatch) -> Dict:
-        """APPO: PPO-clip surrogate on V-trace advantages (reference: rllib/algorithms/appo/)."""
+        """APPO (reference: ``rllib/algorithms/appo/torch/appo_torch_learner.py``): V-trace with the
+        TARGET policy as V-trace's target policy, the surrogate ratio
+        ``clip(pi_b / pi_target, 0, 2) * pi / pi_b`` clipped PPO-style, the KL term against the target
+        policy, and the target network refreshed every ``target_update_frequency`` updates (Polyak
+        ``tau``) with the KL coefficient adapted (x1.5 above 2 * kl_target, x0.5 below half of it).
+        Statistics are accumulated on the device and read back once per update."""
         cfg = self.cfg
         t0 = time.perf_counter()
         b = batch.to_device(self.device)
         N, T = batch.fragment_shape
         obs = b["obs"].reshape((N * T,) + tuple(b["obs"].shape[2:]))
+        act = b["actions"].reshape((N * T,) + tuple(b["actions"].shape[2:]))
+        target = self._appo_target()
+        behaviour_logp = b["action_logp"].reshape(-1).float()
         with torch.no_grad():
-            logits0, values0 = self.forward(obs)
-            _, _, act, vs, pg = self._vtrace_targets(b, N, T, logits0, values0)
-        old_logp = b["action_logp"].reshape(-1)
-        old_logits = b["action_dist_inputs"].reshape(N * T, -1) if "action_dist_inputs" in b else None
+            tgt_logits, _ = target(obs)
+            tgt_dist = self.module.dist(tgt_logits)
+            tgt_logp = tgt_dist.logp(act)
+            is_ratio = torch.clamp(torch.exp(behaviour_logp - tgt_logp), 0.0, 2.0)
         clip = cfg.get("clip_param", 0.4)
-        stats = {"policy_loss": 0.0, "vf_loss": 0.0, "entropy": 0.0, "mean_kl": 0.0, "total_loss": 0.0}
         epochs = int(cfg.get("num_epochs", 1))
+        use_kl = bool(cfg.get("use_kl_loss", False))
+        acc = torch.zeros(5, device=self.device)  # policy, vf, entropy, kl, total
         for _ in range(epochs):
             logits, values = self.forward(obs)
+            with torch.no_grad():
+                # V-trace corrections toward the target policy (its log-probs as the target policy's)
+                v = values.detach().reshape(N, T)
+                done = (b["terminateds"] | b["truncateds"]).bool()
+                nv = b["next_vf_preds"].float().clone()
+                nv[:, :-1] = torch.where(~done[:, :-1], v[:, 1:], nv[:, :-1])
+                log_rhos = (tgt_logp - behaviour_logp).reshape(N, T)
+                vs, pg = ops.vtrace(log_rhos, b["rewards"].float(), v, nv, b["terminateds"], done,
+                                    cfg.get("gamma", 0.99), cfg.get("vtrace_clip_rho_threshold", 1.0),
+                                    cfg.get("vtrace_clip_c_threshold", 1.0),
+                                    cfg.get("vtrace_clip_pg_rho_threshold", 1.0))
+                vs, pg = vs.reshape(-1), pg.reshape(-1)
             d = self.module.dist(logits)
-            ratio = torch.exp(d.logp(act) - old_logp)
-            surr = torch.min(ratio * pg, ratio.clamp(1 - clip, 1 + clip) * pg)
+            logp_ratio = is_ratio * torch.exp(d.logp(act) - behaviour_logp)
+            surr = torch.minimum(pg * logp_ratio, pg * torch.clamp(logp_ratio, 1 - clip, 1 + clip))
             vf_loss = 0.5 * ((values - vs) ** 2).mean()
             ent = d.entropy().mean()
-            loss = -surr.mean() + cfg.get("vf_loss_coeff", 0.5) * vf_loss - cfg.get("entropy_coeff", 0.01) * ent
-            kl = torch.zeros((), device=self.device)
-            if cfg.get("use_kl_loss", False) and old_logits is not None:
-                kl = self.module.dist(old_logits).kl(d).mean()
+            pi_loss = -surr.mean()
+            loss = pi_loss + cfg.get("vf_loss_coeff", 0.5) * vf_loss - cfg.get("entropy_coeff", 0.01) * ent
+            kl = tgt_dist.kl(d).mean() if use_kl else torch.zeros((), device=self.device)
+            if use_kl:
                 loss = loss + self.kl_coeff * kl
             self._step(loss)
-            stats["policy_loss"] += float(-surr.mean())
-            stats["vf_loss"] += float(vf_loss)
-            stats["entropy"] += float(ent)
-            stats["mean_kl"] += float(kl)
-            stats["total_loss"] += float(loss)
-        out = {k: v / max(epochs, 1) for k, v in stats.items()}
+            acc += torch.stack([pi_loss.detach(), vf_loss.detach(), ent.detach(), kl.detach(), loss.detach()])
+        pl, vl, en, klv, tl = (acc / max(epochs, 1)).tolist()  # the update's one host sync
         self.num_updates += 1
-        out.update({"learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr(), "kl_coeff": self.kl_coeff})
-        return out
+        freq = max(1, int(cfg.get("target_update_frequency", 1)))
+        updated = 0
+        if self.num_updates - self.last_target_update >= freq:
+            self.update_target_network()
+            updated = 1
+            if use_kl:
+                kt = cfg.get("kl_target", 0.01)
+                if klv > 2.0 * kt:
+                    self.kl_coeff *= 1.5
+                elif klv < 0.5 * kt:
+                    self.kl_coeff *= 0.5
+        return {"policy_loss": pl, "vf_loss": vl, "entropy": en, "mean_kl": klv, "total_loss": tl,
+                "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr(), "kl_coeff": self.kl_coeff,
+                "num_target_updates": self.num_target_updates, "target_updated": updated,
+                "last_target_update": self.last_target_update}
 
     # ------------------------------------------------------------------ DQN
     def update_dqn(self, batch: SampleBatch) -> Dict:

@@ -10,6 +10,7 @@
 #   smoke                      __graft_entry__.smoke()
 #   bench[:BENCH_ARGS]         bench.py (default --gpus 1 --steps 20 --warmup 3); prints the JSON line
 #   perstep                    1- vs 4-step rocprofv3 kernel traces of scripts/prof_llama.py, differenced
+#   cpath[:PROF_ARGS]          one kernel trace; per-stream busy time + main-stream critical path (scripts/critical_path.py)
 #   ab:STEP_AB_ARGS            scripts/step_ab.py: same-process interleaved A/B of the 8B step
 #   py:SCRIPT ARGS             any python script
 #   pmc:COUNTERS:SCRIPT ARGS   one rocprofv3 --pmc pass (kernel-trace only; counters comma-separated)
@@ -57,6 +58,19 @@ for step in "$@"; do
         tail -20 "$log"
       fi
       rm -rf gpurun_out/pd1 gpurun_out/pd4 ;;
+    cpath)
+      # one kernel trace of warmup + 4 steps; per-stream busy time and the main-stream critical path
+      rm -rf gpurun_out/cp
+      timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/cp -o run -- python scripts/prof_llama.py --steps 4 --warmup 2 ${arg} > "$log" 2>&1
+      rc=$?
+      if [ $rc -eq 0 ]; then
+        grep "ms/step" "$log"
+        python scripts/critical_path.py "$(find gpurun_out/cp -name '*.db' | head -1)" --steps 3 > "gpurun_out/${TAG}_cpath.md"
+        head -16 "gpurun_out/${TAG}_cpath.md"
+      else
+        tail -20 "$log"
+      fi
+      rm -rf gpurun_out/cp ;;
     ab)
       timeout -k 10 1000 python -u scripts/step_ab.py $arg > "$log" 2>&1
       rc=$?

@@ -230,6 +230,32 @@ def test_recompute_free_dq_matches_reference_and_recompute_path(B, S, Hq, Hk, ca
     assert torch.isfinite(dq1).all() and dq1.float().abs().amax(dim=(1, 3)).min() > 0
 
 
+def test_ds_workspace_cap_falls_back_to_recompute():
+    """A dS workspace over the cap is never allocated: the backward runs the O(S) recompute path
+    and its gradients match mode 0's exactly (same kernels) and the workspace path's to rounding."""
+    B, S, Hq, Hk, D = 1, 2048, 16, 4, 128
+    need = ops._lib.lib().rca_attn_bwd_ws_bytes(B, S, Hq, Hk, D, 1)
+    assert need > 0
+    q, k, v = _mk(B, S, Hq, D, 81), _mk(B, S, Hk, D, 82), _mk(B, S, Hk, D, 83)
+    do = _mk(B, S, Hq, D, 84)
+    ws_run = _bwd(q, k, v, do, True, 1)
+    old = ops.set_attn_ds_workspace_cap(need - 1)
+    try:
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        capped = _bwd(q, k, v, do, True, 1)
+        peak = torch.cuda.max_memory_allocated() - base
+    finally:
+        ops.set_attn_ds_workspace_cap(old)
+    recompute = _bwd(q, k, v, do, True, 0)
+    for a, b in zip(capped, recompute):
+        assert torch.equal(a, b)
+    assert peak < need  # the workspace was not taken
+    for a, b in zip(capped[1:], ws_run[1:]):
+        assert _err(a, b) < 1e-2
+    assert ops.attn_ds_workspace_cap() >= 1 << 30  # default policy: GBs on a 288 GB device
+
+
 def test_recompute_free_dq_large_logits_and_determinism():
     """Scores spanning hundreds of log2 units (P saturates to 0/1 across tiles) through the dS-tile
     path, and bitwise run-to-run reproducibility of dQ (each element summed by one wave, in key order)."""

@@ -23,6 +23,8 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
     assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["higher_is_better"] is True
     assert "ZeRO" in rec["config"]["data_parallel"] and rec["config"]["parallel_mode"] == "zero"
+    # a sharded optimizer is not the DDP headline: it reports under its own metric name
+    assert rec["metric"] == "ray_train_tokens_per_sec_llama3_8b_zero"
     assert rec["config"]["launch"] == "torchrun" and rec["config"]["grad_reduce_dtype"] == "fp32"
     # per-rank step times: the job's ms/step is the slowest rank's
     ranks = rec["extra"]["rank_ms_per_step"]
@@ -45,8 +47,9 @@ def test_bench_self_launch_two_workers_cpu(tmp_path):
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
-    # the default --parallel auto: ZeRO-sharded AdamW for N > 1
-    assert rec["config"]["parallel_mode"] == "zero" and rec["config"]["launch"] == "TorchTrainer worker actors"
+    # the default --parallel is ddp at every N, matching the headline metric's name
+    assert rec["config"]["parallel_mode"] == "ddp" and rec["config"]["launch"] == "TorchTrainer worker actors"
+    assert rec["metric"] == "ray_train_tokens_per_sec_llama3_8b_ddp"
     assert rec["extra"]["exposed_comm_ms"] == 0.0  # events are only recorded on GPUs
     assert rec["config"]["global_batch"] == 4
 

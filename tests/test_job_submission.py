@@ -100,3 +100,22 @@ def test_entrypoint_resources_are_reserved_while_the_driver_runs(shutdown_only, 
     third = client.submit_job(entrypoint=f"{sys.executable} -c 'print(1)'", entrypoint_resources={"slot": 5})
     time.sleep(0.5)
     assert client.stop_job(third) and client.get_job_status(third) == JobStatus.STOPPED
+
+
+def test_entrypoint_gpus_map_through_parent_mask(shutdown_only, tmp_path, monkeypatch):
+    """A head started with HIP_VISIBLE_DEVICES=4,5 owns logical GPUs 0,1 = physical 4,5: a job
+    reserving one GPU must see a PHYSICAL id (4 or 5), not the logical 0 (which would select
+    physical GPU 0). ROCR_VISIBLE_DEVICES, which the HIP ids index into, is passed on unchanged."""
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "4,5")
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    ray.init(num_cpus=2, num_gpus=2)
+    client = JobSubmissionClient()
+    sid = client.submit_job(
+        entrypoint=f"{sys.executable} -c \"import os; print('VIS', os.environ.get('HIP_VISIBLE_DEVICES'), "
+                   f"os.environ.get('ROCR_VISIBLE_DEVICES'))\"",
+        entrypoint_num_gpus=1)
+    assert client.wait_until_finish(sid, 120) == JobStatus.SUCCEEDED, client.get_job_logs(sid)
+    line = [ln for ln in client.get_job_logs(sid).splitlines() if ln.startswith("VIS")][0]
+    _, hip, rocr = line.split()
+    assert hip in ("4", "5"), line
+    assert rocr == "0,1,2,3,4,5,6,7"

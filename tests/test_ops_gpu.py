@@ -150,6 +150,25 @@ def test_grad_sumsq():
     assert abs(s.item() - r.item()) < 1e-3 * r.item()
 
 
+def test_grad_sumsq_last_block_finalize_many_launches():
+    """The last-block-done finalize (no separate reduce launch): sizes from one block to the
+    1024-block cap, bf16 and fp32, accumulate chains, and bitwise run-to-run determinism over
+    repeated launches on the same workspace (the ticket word must come back to zero)."""
+    torch.manual_seed(1)
+    sizes = [1, 7, 2048, 2049, 262_144 * 8 + 3, 64 << 20]
+    xs = [torch.randn(n, device=DEV, dtype=torch.bfloat16 if i % 2 == 0 else torch.float32)
+          for i, n in enumerate(sizes)]
+    ref_ = sum(x.double().pow(2).sum() for x in xs).item()
+    first = ops.grad_sumsq(xs).clone()
+    assert abs(first.item() - ref_) < 1e-4 * ref_
+    for _ in range(20):
+        again = ops.grad_sumsq(xs)
+        assert torch.equal(again, first)
+    ws = ops._workspace(xs[0].device, "sumsq", ops.SUMSQ_WS)
+    torch.cuda.synchronize()
+    assert int(ws[1024:1025].view(torch.int32).item()) == 0
+
+
 @pytest.mark.parametrize("B,T", [(1, 1000), (64, 128), (5, 63), (3, 1)])
 def test_gae(B, T):
     torch.manual_seed(0)
