@@ -44,12 +44,71 @@ def _jsonable(o):
 
 
 def _scope(req: Dict) -> Dict:
+    headers = [(k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str) else v)
+               for k, v in req.get("headers", [])]
+    if req.get("type") == "websocket":
+        return {"type": "websocket", "asgi": {"version": "3.0"}, "http_version": "1.1", "scheme": "ws",
+                "path": req["path"], "raw_path": req["path"].encode(), "query_string": req.get("query_string", b""),
+                "root_path": req.get("root_path", ""), "headers": headers,
+                "subprotocols": list(req.get("subprotocols") or []),
+                "client": ("127.0.0.1", 0), "server": ("127.0.0.1", 8000)}
     return {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1", "method": req["method"],
             "scheme": "http", "path": req["path"], "raw_path": req["path"].encode(),
             "query_string": req.get("query_string", b""), "root_path": req.get("root_path", ""),
-            "headers": [(k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str) else v)
-                        for k, v in req.get("headers", [])],
-            "client": ("127.0.0.1", 0), "server": ("127.0.0.1", 8000)}
+            "headers": headers, "client": ("127.0.0.1", 0), "server": ("127.0.0.1", 8000)}
+
+
+class _StreamReceive:
+    """The replica side of a streamed request (``req["stream"]``, serve/_private/proxy.py): ASGI
+    ``receive()`` that hands out the inline first chunk, then pulls the next client messages from
+    the proxy (``receive_asgi_messages``) only when the app asks for them. After the request body
+    ended it parks like a real server's receive (an app listening for a disconnect must not see
+    one); a WebSocket's ``websocket.disconnect`` is delivered and then repeated."""
+
+    def __init__(self, req: Dict):
+        from collections import deque
+
+        self.ws = req.get("type") == "websocket"
+        st = req.get("stream")
+        self.proxy = st["proxy"] if st else None
+        self.sid = st["id"] if st else None
+        self.buf = deque()
+        if not self.ws:
+            self.buf.append({"type": "http.request", "body": req.get("body", b""), "more_body": st is not None})
+        self.ended = st is None and not self.ws
+        self.last = None
+
+    async def __call__(self):
+        import asyncio
+
+        if self.buf:
+            msg = self.buf.popleft()
+            self._note(msg)
+            return msg
+        if self.ended:
+            if self.ws:
+                return self.last or {"type": "websocket.disconnect", "code": 1000}
+            await asyncio.sleep(3600)  # no more request body: park like a real server
+        msgs = await self.proxy.receive_asgi_messages.remote(self.sid)
+        if not msgs:
+            self.ended = True
+            if self.ws:
+                self.last = {"type": "websocket.disconnect", "code": 1006}
+                return self.last
+            return {"type": "http.disconnect"}
+        self.buf.extend(msgs)
+        msg = self.buf.popleft()
+        self._note(msg)
+        return msg
+
+    def _note(self, msg):
+        t = msg.get("type")
+        if t == "websocket.disconnect":
+            self.ended, self.last = True, msg
+        elif t == "http.request" and not msg.get("more_body"):
+            self.ended = True
+        elif t == "http.disconnect":
+            self.ended = True
 
 
 async def run_asgi_or_call(replica, req: Dict):
@@ -103,6 +162,11 @@ async def stream_asgi_or_call(replica, req: Dict):
 
     obj = replica.obj
     spec = getattr(type(obj), "_serve_ingress_spec", None) if not replica.is_function else None
+    ws = req.get("type") == "websocket"
+    if ws and spec is None:
+        # WebSockets need an ASGI ingress (reference: FastAPI @serve.ingress): refuse the handshake
+        yield ("ws", {"type": "websocket.close", "code": 1003})
+        return
     if spec is not None:
         app = getattr(replica, "_asgi_app", None)
         if app is None:
@@ -110,14 +174,7 @@ async def stream_asgi_or_call(replica, req: Dict):
 
             app = replica._asgi_app = _build_ingress_app(spec, obj)
         q: asyncio.Queue = asyncio.Queue()
-        body = req.get("body", b"")
-        got = {"v": False}
-
-        async def receive():
-            if got["v"]:
-                await asyncio.sleep(3600)  # no more request body: park like a real server
-            got["v"] = True
-            return {"type": "http.request", "body": body, "more_body": False}
+        receive = _StreamReceive(req)
 
         async def send(msg):
             await q.put(msg)
@@ -134,6 +191,9 @@ async def stream_asgi_or_call(replica, req: Dict):
                 msg = await q.get()
                 if msg is None:
                     break
+                if ws:
+                    yield ("ws", msg)
+                    continue
                 if msg["type"] == "http.response.start":
                     yield ("start", msg["status"], [(k.decode(), v.decode()) for k, v in msg.get("headers", [])])
                 elif msg["type"] == "http.response.body":
@@ -144,12 +204,7 @@ async def stream_asgi_or_call(replica, req: Dict):
         return
     from starlette.requests import Request
 
-    body = req.get("body", b"")
-
-    async def receive2():
-        return {"type": "http.request", "body": body, "more_body": False}
-
-    request = Request(_scope(req), receive2)
+    request = Request(_scope(req), _StreamReceive(req))
     res = await replica._invoke_user("__call__", (request,), {})
     try:
         from starlette.responses import StreamingResponse

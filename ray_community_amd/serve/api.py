@@ -477,12 +477,18 @@ def ingress(app):
 
 def _capture_routes(app, cls):
     try:
-        from fastapi.routing import APIRoute
+        from fastapi.routing import APIRoute, APIWebSocketRoute
     except ImportError:
         raise ImportError("@serve.ingress requires fastapi")
     meta = {k: getattr(app, k, None) for k in ("title", "version", "description")}
     routes = []
     for r in app.router.routes:
+        if isinstance(r, APIWebSocketRoute):
+            fn = r.endpoint
+            is_method = getattr(fn, "__qualname__", "").startswith(cls.__qualname__ + ".")
+            routes.append({"kind": "websocket", "path": r.path, "endpoint": fn.__name__ if is_method else fn,
+                           "is_method": is_method, "name": r.name})
+            continue
         if not isinstance(r, APIRoute):
             continue  # docs/openapi routes are recreated by the replica's FastAPI()
         fn = r.endpoint
@@ -499,6 +505,9 @@ def _build_ingress_app(spec, instance):
     app = FastAPI(**{k: v for k, v in spec["meta"].items() if v is not None})
     for r in spec["routes"]:
         ep = getattr(instance, r["endpoint"]) if r["is_method"] else r["endpoint"]
+        if r.get("kind") == "websocket":
+            app.add_api_websocket_route(r["path"], ep, name=r["name"])
+            continue
         app.add_api_route(r["path"], ep, methods=r["methods"], name=r["name"], status_code=r["status_code"],
                           response_model=r["response_model"], tags=r["tags"] or None)
     return app

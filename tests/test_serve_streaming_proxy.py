@@ -1,0 +1,141 @@
+"""Serve proxy: request bodies streamed to the replica as the app consumes them, and WebSocket
+sessions (reference python/ray/serve/_private/proxy.py:430,856-1103 receive_asgi_messages;
+tests/test_streaming_response.py, test_websockets.py). uvicorn's WebSocket backends
+(websockets / wsproto) are not installed here, so WebSocket sessions are driven through the
+proxy's ASGI app with a scripted client (``HTTPProxy.run_asgi_session``) -- the same ``_app``
+uvicorn calls; the end-to-end WebSocket socket path stays unpinned."""
+import hashlib
+
+import pytest
+import requests
+
+import ray_community_amd as ray
+from ray_community_amd import serve
+
+PORT = 18131
+
+
+@pytest.fixture
+def serve_instance():
+    ray.init(num_cpus=8, log_to_driver=False)
+    serve.start(http_options={"port": PORT})
+    yield
+    serve.shutdown()
+    ray.shutdown()
+
+
+def _proxy():
+    from ray_community_amd.serve.api import _STATE
+
+    return _STATE["proxy"]
+
+
+def test_large_upload_streams_with_bounded_proxy_memory(serve_instance):
+    from fastapi import FastAPI, Request
+
+    app = FastAPI()
+
+    @serve.deployment
+    @serve.ingress(app)
+    class Sink:
+        @app.post("/upload")
+        async def upload(self, request: Request):
+            h = hashlib.sha256()
+            n = chunks = 0
+            async for chunk in request.stream():  # consumed as it arrives
+                h.update(chunk)
+                n += len(chunk)
+                chunks += 1
+            return {"bytes": n, "sha": h.hexdigest(), "chunks": chunks}
+
+    serve.run(Sink.bind(), route_prefix="/s")
+    total, piece = 200 << 20, 1 << 20
+    block = bytes(range(256)) * (piece // 256)
+    ref = hashlib.sha256()
+    for _ in range(total // piece):
+        ref.update(block)
+
+    def gen():
+        for _ in range(total // piece):
+            yield block
+
+    r = requests.post(f"http://127.0.0.1:{PORT}/s/upload", data=gen(), timeout=300)
+    assert r.status_code == 200, r.text
+    out = r.json()
+    assert out["bytes"] == total and out["sha"] == ref.hexdigest()
+    st = ray.get(_proxy().stats.remote())
+    assert st["streamed_requests"] >= 1 and st["streamed_bytes"] >= total - piece
+    # the proxy never held more than one pull's budget (1 MiB) plus one client chunk at a time
+    assert st["max_pull_bytes"] <= (1 << 20) + (256 << 10), st
+    assert st["pulls"] >= total // ((1 << 20) + (256 << 10))
+    import time
+
+    deadline = time.time() + 10
+    while st["open_streams"] and time.time() < deadline:  # closed right after the last body message
+        time.sleep(0.05)
+        st = ray.get(_proxy().stats.remote())
+    assert st["open_streams"] == 0
+
+
+def test_small_body_stays_inline_and_function_deployment_reads_stream(serve_instance):
+    @serve.deployment
+    async def echo_len(request):
+        body = await request.body()
+        return {"n": len(body), "head": body[:4].decode()}
+
+    serve.run(echo_len.bind(), route_prefix="/e")
+    before = ray.get(_proxy().stats.remote())["streamed_requests"]
+    r = requests.post(f"http://127.0.0.1:{PORT}/e", data=b"abcd" * 10, timeout=60)
+    assert r.json() == {"n": 40, "head": "abcd"}
+    assert ray.get(_proxy().stats.remote())["streamed_requests"] == before  # one message: inline
+
+    def gen():
+        for i in range(40):
+            yield (b"wxyz" if i == 0 else b"-") * 4096
+
+    r = requests.post(f"http://127.0.0.1:{PORT}/e", data=gen(), timeout=60)
+    assert r.json() == {"n": 4 * 4096 + 39 * 4096, "head": "wxyz"}
+
+
+def test_websocket_echo_session_through_proxy_app(serve_instance):
+    from fastapi import FastAPI, WebSocket, WebSocketDisconnect
+
+    app = FastAPI()
+
+    @serve.deployment
+    @serve.ingress(app)
+    class Echo:
+        @app.websocket("/ws")
+        async def ws(self, websocket: WebSocket):
+            await websocket.accept()
+            try:
+                while True:
+                    text = await websocket.receive_text()
+                    await websocket.send_text(f"echo:{text}")
+                    if text == "bye":
+                        await websocket.close(code=1000)
+                        return
+            except WebSocketDisconnect:
+                return
+
+    serve.run(Echo.bind(), route_prefix="/chat")
+    scope = {"type": "websocket", "path": "/chat/ws", "query_string": b"", "headers": [], "subprotocols": []}
+    msgs = [{"type": "websocket.connect"}, {"type": "websocket.receive", "text": "hi"},
+            {"type": "websocket.receive", "text": "there"}, {"type": "websocket.receive", "text": "bye"}]
+    sent = ray.get(_proxy().run_asgi_session.remote(scope, msgs))
+    kinds = [m["type"] for m in sent]
+    assert kinds[0] == "websocket.accept"
+    texts = [m.get("text") for m in sent if m["type"] == "websocket.send"]
+    assert texts == ["echo:hi", "echo:there", "echo:bye"]
+    assert kinds[-1] == "websocket.close" and sent[-1].get("code", 1000) == 1000
+    assert ray.get(_proxy().stats.remote())["websocket_sessions"] >= 1
+
+    # client disconnects first: the app sees WebSocketDisconnect, the proxy closes normally
+    sent = ray.get(_proxy().run_asgi_session.remote(scope, [{"type": "websocket.connect"},
+                                                             {"type": "websocket.receive", "text": "x"},
+                                                             {"type": "websocket.disconnect", "code": 1001}]))
+    assert [m.get("text") for m in sent if m["type"] == "websocket.send"] == ["echo:x"]
+
+    # no route: the handshake is refused with a close
+    sent = ray.get(_proxy().run_asgi_session.remote(dict(scope, path="/nope/ws"), [{"type": "websocket.connect"}]))
+    assert sent == [{"type": "websocket.close", "code": 1000}] or sent[0]["type"] == "websocket.close"
