@@ -78,9 +78,13 @@ class Classifier:
     def __call__(self, x):
         import torch
 
+        t0 = time.perf_counter()
         with torch.inference_mode():
             x = x.to(self.dev, self.dtype, non_blocking=True)
-            return self.net(x).argmax(1).cpu().numpy()
+            pred = self.net(x).argmax(1).cpu().numpy()
+        # which replica served it and its own compute time: the caller derives the hand-off /
+        # routing time (round trip minus this) and per-replica load from them
+        return {"pred": pred, "replica": os.getpid(), "infer_ms": 1e3 * (time.perf_counter() - t0)}
 
 
 class PreprocessAndClassify:
@@ -98,11 +102,17 @@ class PreprocessAndClassify:
     def __call__(self, batch):
         import torch
 
+        import numpy as np
+
         x = self.norm(batch)["image"]
         if self.cuda:
             torch.cuda.current_stream().synchronize()  # the replica reads it from another process
-        pred = self.handle.remote(x).result()
-        return {"pred": pred, "id": batch["id"]}
+        t0 = time.perf_counter()
+        out = self.handle.remote(x).result()
+        rtt = 1e3 * (time.perf_counter() - t0)
+        n = len(batch["id"])
+        return {"pred": out["pred"], "id": batch["id"], "replica": np.full(n, out["replica"], np.int64),
+                "infer_ms": np.full(n, out["infer_ms"], np.float64), "rtt_ms": np.full(n, rtt, np.float64)}
 
 
 def main():
@@ -137,10 +147,19 @@ def main():
                            fn_constructor_kwargs={"app_name": "classifier", "device": a.device},
                            num_gpus=0.5 / a.preprocess_actors_per_gpu if cuda else None, num_cpus=1))
         stamps, seen, correct = [], 0, 0
+        per_rep = {}  # replica pid -> [blocks, infer ms, round-trip ms]
         for b in ds.iter_batches(batch_size=None, batch_format="numpy"):
             stamps.append((time.perf_counter(), len(b["pred"])))
             seen += len(b["pred"])
             correct += int(((b["pred"] >= 0) & (b["pred"] < 1000)).all())
+            if len(stamps) > a.warmup:
+                # one record per request (rows of one request repeat its values)
+                for rep, inf, rtt in {(int(r), float(i), float(t))
+                                      for r, i, t in zip(b["replica"], b["infer_ms"], b["rtt_ms"])}:
+                    e = per_rep.setdefault(rep, [0, 0.0, 0.0])
+                    e[0] += 1
+                    e[1] += inf
+                    e[2] += rtt
         if len(stamps) <= a.warmup:
             raise RuntimeError(f"pipeline produced {len(stamps)} blocks, need > {a.warmup}")
         t0 = stamps[a.warmup - 1][0] if a.warmup > 0 else stamps[0][0]
@@ -157,7 +176,16 @@ def main():
                        "preprocess_actors": nact,
                        "pipeline": "ray.data map_batches(HIP image_normalize) -> serve handle (HIP IPC) -> "
                                    "ResNet-50 bf16 (BN folded)"},
-            "extra": {"blocks": len(stamps), "images": seen}}), flush=True)
+            "extra": {"blocks": len(stamps), "images": seen, "replicas_used": len(per_rep),
+                      # per-replica requests and mean times over the timed window; handoff = the
+                      # request's round trip from the preprocess actor minus the replica's compute
+                      # (routing + device-tensor hand-off + queueing: the pipeline's exposed
+                      # communication)
+                      "per_replica": [{"requests": c, "infer_ms": round(i / c, 3), "rtt_ms": round(t / c, 3)}
+                                      for c, i, t in sorted(per_rep.values(), key=lambda e: -e[0])],
+                      "handoff_ms_mean": round(sum(t - i for _, i, t in per_rep.values())
+                                               / max(1, sum(c for c, _, _ in per_rep.values())), 3)}}),
+              flush=True)
     finally:
         serve.shutdown()
         ray.shutdown()

@@ -37,6 +37,9 @@ def main():
                          "the learner on that GPU gets the rest. Measured on 1x MI355X: 0.5 -> 35.1k env-steps/s "
                          "(12 runners x 22 envs: env stepping dominates, the learner slows on half a GPU) vs "
                          "40.9k with 16 CPU-inference runners, so off by default")
+    ap.add_argument("--profile-runner", action="store_true",
+                    help="per-phase breakdown of the env runners' sample loop (connectors, inference, env step, "
+                         "bookkeeping, fragment assembly) and of the driver's iteration, in the JSON's extra")
     args = ap.parse_args()
 
     import torch
@@ -65,6 +68,8 @@ def main():
            .training(lr=2.5e-4, train_batch_size=args.train_batch, minibatch_size=args.minibatch,
                      num_epochs=args.epochs, clip_param=0.1, vf_clip_param=10.0, entropy_coeff=0.01,
                      kl_coeff=0.5, lambda_=0.95, gamma=0.99, model={"vf_share_layers": True}))
+    if args.profile_runner:
+        cfg.profile_env_runner = True
     if args.learners > 0:
         cfg.learners(num_learners=args.learners, num_gpus_per_learner=(1.0 - share) if ngpu else 0)
     else:
@@ -84,14 +89,31 @@ def main():
     for i in range(args.warmup):
         algo.train()
         print(f"[bench_rllib] warmup {i} done at {time.perf_counter() - t_start:.1f} s", file=sys.stderr, flush=True)
+    if args.profile_runner:
+        algo.env_runner_group.foreach_env_runner("sample_profile")  # drop the warmup's numbers
     t0 = time.perf_counter()
     steps = 0
     last = None
+    phases = {"sample_time_s": 0.0, "learn_time_s": 0.0, "sync_weights_time_s": 0.0}
     for _ in range(args.iters):
         r = algo.train()
         steps += r["num_env_steps_sampled_this_iter"]
         last = r
+        li = r["info"]["learner"]["default_policy"]
+        for k in phases:
+            phases[k] += float(li.get(k, 0.0))
     dt = time.perf_counter() - t0
+    runner_profile = None
+    if args.profile_runner:
+        profs = [p for p in algo.env_runner_group.foreach_env_runner("sample_profile") if p]
+        if profs:
+            keys = sorted({k for p in profs for k in p if k.endswith("_s")})
+            frag = sum(p.get("fragments", 0) for p in profs)
+            # mean per fragment over all runners, ms
+            runner_profile = {k[:-2] + "_ms_per_fragment": round(1e3 * sum(p.get(k, 0.0) for p in profs)
+                                                                        / max(1, frag), 3) for k in keys}
+            runner_profile["fragments"] = frag
+            runner_profile["steps_per_fragment"] = round(sum(p.get("steps", 0) for p in profs) / max(1, frag), 1)
     out = {"metric": "rllib_ppo_env_steps_per_sec", "value": round(steps / dt, 1), "unit": "env-steps/s",
            "n_gpus": max(1, args.learners) if ngpu else 0, "iters": args.iters, "warmup": args.warmup,
            "higher_is_better": True, "vs_baseline": None, "data": "SyntheticAtari (84x84x4 uint8, Discrete(6))",
@@ -99,7 +121,9 @@ def main():
                       "train_batch_size": args.train_batch, "minibatch": args.minibatch, "epochs": args.epochs,
                       "learners": args.learners, "runner_gpu_share": share},
            "extra": {"learner_time_s": last["info"]["learner"]["default_policy"].get("learner_time_s"),
-                     "iter_time_s": dt / max(1, args.iters)}}
+                     "iter_time_s": dt / max(1, args.iters),
+                     "driver_phase_s_per_iter": {k: round(v / max(1, args.iters), 4) for k, v in phases.items()},
+                     "runner_profile": runner_profile}}
     stop.set()
     print(json.dumps(out), flush=True)
     algo.stop()

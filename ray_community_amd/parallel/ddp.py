@@ -24,6 +24,7 @@ model in ``torch.nn.parallel.DistributedDataParallel``. Here DDP is the framewor
 from __future__ import annotations
 
 import contextlib
+import time
 from typing import List, Optional
 
 import torch
@@ -44,11 +45,20 @@ class CommWaitTimer:
     def __init__(self):
         self.enabled = False
         self._pairs = []
+        self._host_ms = 0.0
 
     @contextlib.contextmanager
-    def region(self):
-        if not self.enabled or not torch.cuda.is_available():
+    def region(self, device=None):
+        if not self.enabled:
             yield
+            return
+        if not torch.cuda.is_available() or (device is not None and torch.device(device).type != "cuda"):
+            # host collectives (gloo on CPU): the wait itself is the stall -- wall-clock it
+            t0 = time.perf_counter()
+            try:
+                yield
+            finally:
+                self._host_ms += 1e3 * (time.perf_counter() - t0)
             return
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
@@ -59,12 +69,13 @@ class CommWaitTimer:
             self._pairs.append((a, b))
 
     def take_ms(self) -> float:
+        host, self._host_ms = self._host_ms, 0.0
         if not self._pairs:
-            return 0.0
+            return float(host)
         self._pairs[-1][1].synchronize()
         total = sum(a.elapsed_time(b) for a, b in self._pairs)
         self._pairs = []
-        return float(total)
+        return float(total) + host
 
 
 class DistributedDataParallel(nn.Module):
@@ -182,7 +193,7 @@ class DistributedDataParallel(nn.Module):
         for bi, w in enumerate(self._works):
             if w is None:
                 self._launch(bi)
-        with self.comm_timer.region():
+        with self.comm_timer.region(self.flat.device):
             for bi, w in enumerate(self._works):
                 if w is not None:
                     w.wait()

@@ -1,6 +1,8 @@
 """PPO (reference: ``rllib/algorithms/ppo/ppo.py``, ``ppo_torch_learner.py``)."""
 from __future__ import annotations
 
+import time
+
 from typing import Dict
 
 from .algorithm import Algorithm
@@ -59,18 +61,26 @@ class PPO(Algorithm):
 
     def training_step(self) -> Dict:
         cfg = self.config
+        t0 = time.perf_counter()
         if self.multi_agent:
             batch = self._sample(cfg.train_batch_size)
             n = batch.count
+            t1 = time.perf_counter()
             info = {p: self.learner_groups[p].update("ppo", batch.policy_batches[p])
                     for p in self.policies_to_train if p in batch.policy_batches}
         else:
             # runner fragments go to the learner(s) as they are: stacked on the GPU, not the host
             frags = self._sample_fragments(cfg.train_batch_size)
             n = sum(f.count for f in frags)
+            t1 = time.perf_counter()
             info = self.learner_group.update("ppo", frags)
+        t2 = time.perf_counter()
         self._timesteps_total += n
         self._sync_weights()
+        t3 = time.perf_counter()
+        # driver-side phase times of the iteration (sampling includes the fragments' transfer to
+        # the driver; the learner phase includes the host->device copy)
+        info["sample_time_s"], info["learn_time_s"], info["sync_weights_time_s"] = t1 - t0, t2 - t1, t3 - t2
         info["_steps_this_iter"] = n
         return info
 

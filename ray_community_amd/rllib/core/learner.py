@@ -45,6 +45,7 @@ class Learner(LearnerAPI):
 
             self.ddp = DistributedDataParallel(self.module, bucket_cap_mb=64, average_in_optimizer=False,
                                                auto_finalize=True)
+            self.ddp.comm_timer.enabled = True  # exposed gradient all-reduce time, per update
         self.opt = torch.optim.Adam(self.module.parameters(), lr=config.get("lr", 5e-5),
                                     eps=config.get("adam_epsilon", 1e-8))
         self.kl_coeff = config.get("kl_coeff", 0.2)
@@ -653,7 +654,13 @@ def _learner_actor_cls():
             return True
 
         def update(self, kind, batch):
-            return getattr(self.learner, f"update_{kind}")(batch)
+            t0 = time.perf_counter()
+            out = getattr(self.learner, f"update_{kind}")(batch)
+            out = dict(out)
+            out["rank_update_time_s"] = time.perf_counter() - t0
+            ddp = self.learner.ddp
+            out["exposed_comm_ms"] = ddp.comm_timer.take_ms() if ddp is not None else 0.0
+            return out
 
         def call(self, name, *args):
             return getattr(self.learner, name)(*args)
@@ -698,6 +705,11 @@ class LearnerGroup(LearnerGroupAPI):
             vals = [r[k] for r in res if isinstance(r.get(k), (int, float))]
             if vals:
                 out[k] = float(np.mean(vals))
+        # per-rank timings: the slowest learner sets the update's time; exposed_comm_ms is each
+        # rank's wait on the gradient all-reduce (what overlap with backward did not hide)
+        out["rank_update_time_s"] = [float(r.get("rank_update_time_s", 0.0)) for r in res]
+        out["rank_exposed_comm_ms"] = [float(r.get("exposed_comm_ms", 0.0)) for r in res]
+        out["exposed_comm_ms"] = max(out["rank_exposed_comm_ms"])
         return out
 
     def call(self, name, *args):

@@ -58,6 +58,10 @@ class EnvRunner:
         self.module = make_module(config, self._module_obs_space, self.env.action_space)
         self.module.eval()
         self.stateful = bool(getattr(self.module, "is_stateful", False))
+        # per-phase wall time of sample() (``profile_env_runner`` config / bench_rllib.py
+        # --profile-runner): env-to-module connectors, policy inference (+ device->host copy),
+        # module-to-env connectors, env.step, per-step bookkeeping, fragment assembly
+        self._prof = {} if config.get("profile_env_runner") else None
         # GPU inference (num_gpus_per_env_runner > 0): the module lives on the runner's GPU share,
         # observations go up once per step and ONE packed [N, 3 + A] tensor comes back
         self.device = torch.device("cpu")
@@ -194,11 +198,19 @@ class EnvRunner:
         trunc_fix = []  # (t, env indices, module-input final obs, state after the step)
         gpu = self.device.type == "cuda"
         ctx = self._ctx
+        prof = self._prof
+        clk = time.perf_counter
+        t_start = clk()
         for t in range(T):
+            if prof is not None:
+                t0 = clk()
             if self._pending_mobs is not None:
                 mobs, self._pending_mobs = self._pending_mobs, None
             else:
                 mobs = self._module_obs(self.obs, explore)
+            if prof is not None:
+                t1 = clk()
+                prof["env_to_module_s"] = prof.get("env_to_module_s", 0.0) + (t1 - t0)
             if obs_buf is None:
                 obs_buf = np.empty((N, T) + mobs.shape[1:], dtype=mobs.dtype)
             first_buf[:, t] = ctx.is_first
@@ -224,6 +236,9 @@ class EnvRunner:
                 logits = None
             if gpu:
                 a, lp, v, logits = self._to_host(a, lp, v, logits)
+            if prof is not None:
+                t2 = clk()
+                prof["inference_s"] = prof.get("inference_s", 0.0) + (t2 - t1)
             if logits is not None:
                 if logits_buf is None:
                     logits_buf = np.empty((N, T, logits.shape[-1]), dtype=np.float32)
@@ -233,7 +248,17 @@ class EnvRunner:
             acts[:, t] = an
             logp[:, t] = lp.numpy()
             vf[:, t] = v.numpy()
-            nobs, r, te, tr, info = self.env.step(self._env_actions(an, explore))
+            if prof is None:
+                nobs, r, te, tr, info = self.env.step(self._env_actions(an, explore))
+            else:
+                t3 = clk()
+                ea = self._env_actions(an, explore)
+                t4 = clk()
+                nobs, r, te, tr, info = self.env.step(ea)
+                t5 = clk()
+                prof["buffers_s"] = prof.get("buffers_s", 0.0) + (t3 - t2)
+                prof["module_to_env_s"] = prof.get("module_to_env_s", 0.0) + (t4 - t3)
+                prof["env_step_s"] = prof.get("env_step_s", 0.0) + (t5 - t4)
             rew[:, t] = r
             term[:, t] = te
             trunc[:, t] = tr
@@ -249,6 +274,9 @@ class EnvRunner:
             self.obs = nobs
             ctx.is_first = te | tr
             ctx.last_actions, ctx.last_rewards = an, r
+            if prof is not None:
+                prof["bookkeeping_s"] = prof.get("bookkeeping_s", 0.0) + (clk() - t5)
+        t_loop = clk()
         # bootstrap V(s_T): the next fragment starts from these module inputs (connector state
         # advances exactly once per env step)
         self._pending_mobs = self._module_obs(self.obs, explore)
@@ -282,7 +310,20 @@ class EnvRunner:
             self._writer.write(b)
         if self.callbacks is not None:
             self.callbacks.on_sample_end(env_runner=self, samples=b)
+        if prof is not None:
+            end = clk()
+            prof["bootstrap_and_assembly_s"] = prof.get("bootstrap_and_assembly_s", 0.0) + (end - t_loop)
+            prof["sample_total_s"] = prof.get("sample_total_s", 0.0) + (end - t_start)
+            prof["steps"] = prof.get("steps", 0) + N * T
+            prof["fragments"] = prof.get("fragments", 0) + 1
         return b
+
+    def sample_profile(self, reset: bool = True) -> Dict:
+        """The accumulated per-phase times of ``sample()`` (empty unless ``profile_env_runner``)."""
+        out = dict(self._prof or {})
+        if reset and self._prof is not None:
+            self._prof.clear()
+        return out
 
     @torch.no_grad()
     def sample_transitions(self, num_steps: int, epsilon: float = 0.0) -> SampleBatch:

@@ -34,10 +34,17 @@ def _set_lib(fn, value):
     return lambda: f(old)
 
 
+CTX = {}  # filled after the model is built: "ddp", "opt"
+
+
 def _toggles():
     from ray_community_amd.parallel import fused_linear as fl
     return {
         "base": lambda: (lambda: None),
+        # gradient-norm sum of squares: per bucket on the DDP side stream during backward (default)
+        # vs one pass on the compute stream before AdamW
+        "norm_side": lambda: (lambda: None),
+        "norm_main": lambda: _set_attr(CTX["ddp"], "_norm", None),
         # gate_up input gradient on hipBLASLt instead of the hand GEMM
         "noplan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", False),
         "plan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", True),
@@ -78,6 +85,7 @@ def main():
         if arm not in toggles:
             raise SystemExit(f"unknown arm {arm!r}; known: {sorted(toggles)}")
     net, ddp, opt, batch, step = build_llama_training(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch)
+    CTX.update(ddp=ddp, opt=opt)
     data = [batch() for _ in range(2)]
     times = {arm: [] for arm in arms}
     for arm in arms:  # warm every arm's code path once (kernel loads, W^T copies, allocator)

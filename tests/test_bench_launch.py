@@ -68,6 +68,26 @@ def test_bench_data_serve_pipeline_cpu(tmp_path):
     assert rec["value"] > 0 and rec["steps"] == 4 and rec["extra"]["images"] == 6 * 16
 
 
+def test_bench_data_serve_eight_replicas_cpu(tmp_path):
+    """The 8-GPU config-5 shape rehearsed on CPU: 8 Serve replicas behind the router, 16
+    preprocess actors; per-replica load/latency and the hand-off time are reported."""
+    env = dict(os.environ)
+    env.pop("RCA_ADDRESS", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench_data_serve.py"), "--gpus", "8", "--device", "cpu", "--model",
+           "tiny", "--image-size", "32", "--batch-size", "16", "--batches", "24", "--warmup", "4"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["config"]["replicas"] == 8 and rec["config"]["preprocess_actors"] == 16
+    ex = rec["extra"]
+    assert ex["images"] == 28 * 16 and rec["value"] > 0
+    assert ex["replicas_used"] >= 4, ex  # power-of-two-choices spreads the 16 callers
+    assert sum(r["requests"] for r in ex["per_replica"]) == 24
+    assert all(r["rtt_ms"] >= r["infer_ms"] for r in ex["per_replica"]) and ex["handoff_ms_mean"] >= 0
+
+
 def test_eight_virtual_gpu_workers_get_distinct_devices():
     """8 GPU worker actors on a node with 8 (virtual) GPUs: each sees its own GPU id, the plan
     gives every worker the union 0..7 in HIP_VISIBLE_DEVICES and a distinct device index that
