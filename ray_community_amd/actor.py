@@ -103,7 +103,7 @@ class ActorClass:
                 return parent._remote(args, kwargs, {**parent._options, **options})
 
             def bind(_self, *args, **kwargs):
-                from .dag.class_node import ClassNode
+                from .dag.dag_node import ClassNode
 
                 return ClassNode(parent, args, kwargs, {**parent._options, **options})
 
@@ -113,7 +113,7 @@ class ActorClass:
         return self._remote(args, kwargs, self._options)
 
     def bind(self, *args, **kwargs):
-        from .dag.class_node import ClassNode
+        from .dag.dag_node import ClassNode
 
         return ClassNode(self, args, kwargs, self._options)
 
@@ -207,7 +207,7 @@ class ActorMethod:
         return m
 
     def bind(self, *args, **kwargs):
-        from .dag.class_node import ClassMethodNode
+        from .dag.dag_node import ClassMethodNode
 
         return ClassMethodNode(self._handle, self._name, args, kwargs, self._opts)
 

@@ -142,7 +142,7 @@ class RemoteFunction:
                 return parent._remote(args, kwargs, {**parent._options, **options})
 
             def bind(_self, *args, **kwargs):
-                from .dag.function_node import FunctionNode
+                from .dag.dag_node import FunctionNode
 
                 return FunctionNode(parent, args, kwargs, {**parent._options, **options})
 
@@ -159,7 +159,7 @@ class RemoteFunction:
         return dict(self._res)  # the spec may be mutated downstream
 
     def bind(self, *args, **kwargs):
-        from .dag.function_node import FunctionNode
+        from .dag.dag_node import FunctionNode
 
         return FunctionNode(self, args, kwargs, self._options)
 
