@@ -428,6 +428,10 @@ class CoreWorker:
         # puts the head REJECTED (the error arrives only on the ack future): the next get / wait of
         # such a ref raises it instead of answering from _put_cache
         self._put_errors: Dict[bytes, BaseException] = {}
+        # shm-store descriptors this process already resolved through the head, for refs it holds:
+        # a repeated get maps the object straight from the shared-memory store (the native pin
+        # fails if it was spilled / evicted / freed since, and then the head is asked again)
+        self._shm_descs: Dict[bytes, tuple] = {}
         ser.set_escape_hook(self.sync_puts)
 
     # -------------------------------------------------------------- reference counting
@@ -453,6 +457,7 @@ class CoreWorker:
             self._ready_known.discard(oid)
             self._put_cache.pop(oid, None)
             self._put_errors.pop(oid, None)
+            self._shm_descs.pop(oid, None)
             if oid in self.owned.objs and not self.owned.drop(oid):
                 return  # a caller-owned result the head never heard of
             self.client.ref_delta((), (oid,))
@@ -534,9 +539,10 @@ class CoreWorker:
                 self._put_errors[oid] = err
 
     def forget_puts(self, oids):
-        """``ray.internal.free``: freed objects are no longer answered from the local put cache."""
+        """``ray.internal.free``: freed objects are no longer answered from the local caches."""
         for o in oids:
             self._put_cache.pop(o, None)
+            self._shm_descs.pop(o, None)
 
     def _raise_put_errors(self, oids):
         pe = self._put_errors
@@ -579,6 +585,12 @@ class CoreWorker:
                 self.client.call_async("gpu_restored", o, ("inline", b, len(b)) if b is not None else None,
                                        self.gpu_info(o))
 
+    def _note_shm(self, oids, descs):
+        refs = self._refs
+        for o, d in zip(oids, descs):
+            if d is not None and d[0] == "shm" and not (d[3] & ser.FLAG_GPU) and refs.get(o):
+                self._shm_descs[o] = d
+
     def _materialize(self, oid, desc):
         kind, data, size, flags = desc
         if kind == "inline":
@@ -586,7 +598,9 @@ class CoreWorker:
         elif kind == "shm":
             view = self.store.pin(oid)
             if view is None:
-                # raced with spilling: ask again (the head restores it)
+                # raced with spilling (or a cached descriptor went stale): ask again (the head
+                # restores it)
+                self._shm_descs.pop(oid, None)
                 d2 = self.client.call("get", [oid], None)[0]
                 if d2[0] == "shm":
                     view = self.store.pin(oid)
@@ -629,15 +643,17 @@ class CoreWorker:
         """Descriptors for ``oids``: caller-owned results from the local table (no head round
         trip), the rest from the head."""
         self._raise_put_errors(oids)
-        pc = self._put_cache
-        if pc:
-            hit = [pc.get(o) for o in oids]
+        pc, sc = self._put_cache, self._shm_descs
+        if pc or sc:
+            hit = [pc.get(o) or sc.get(o) for o in oids]
             if None not in hit:
                 return hit
         owned = self.owned.objs
         local = [o for o in oids if o in owned]
         if not local:
-            return self.client.call("get", oids, timeout)
+            descs = self.client.call("get", oids, timeout)
+            self._note_shm(oids, descs)
+            return descs
         deadline = None if timeout is None else time.monotonic() + timeout
         remote = [o for o in oids if o not in owned]
         got = {}

@@ -210,6 +210,28 @@ class Algorithm(Trainable):
             return self._foreach_runner("sample", max(1, steps_total // n))
         return [self.local_runner.sample(steps_total)]
 
+    def _sample_fragment_refs(self, steps_total: int):
+        """``(fragment refs, env steps)`` when the fragments can go to remote learners by reference
+        (remote runners, learner actors whose count divides the fragments, the default fail-fast
+        runner policy), else None. The driver only waits for the fragments to be ready."""
+        g = getattr(self, "env_runner_group", None)
+        lg = getattr(self, "learner_group", None)
+        n = len(self.remote_runners)
+        if (not n or g is None or lg is None or getattr(lg, "local", None) is not None or g.ignore
+                or n % max(1, getattr(lg, "n", 1)) or os.environ.get("RCA_RLLIB_FRAGMENT_REFS", "1") == "0"):
+            return None
+        from ..._private.worker import wait
+
+        per = max(1, steps_total // n)
+        res = g.manager.foreach_actor("sample", per, return_obj_refs=True)
+        refs = [r.get() for r in res.ignore_errors()]
+        if len(refs) != n:
+            return None
+        wait(refs, num_returns=len(refs))
+        envs = int(self.config.num_envs_per_env_runner or 1)
+        steps = n * envs * max(1, per // envs)
+        return refs, steps
+
     def _sample(self, steps_total: int) -> SampleBatch:
         return concat_samples(self._sample_fragments(steps_total))
 

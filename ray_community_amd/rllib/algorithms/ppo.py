@@ -69,9 +69,15 @@ class PPO(Algorithm):
             info = {p: self.learner_groups[p].update("ppo", batch.policy_batches[p])
                     for p in self.policies_to_train if p in batch.policy_batches}
         else:
-            # runner fragments go to the learner(s) as they are: stacked on the GPU, not the host
-            frags = self._sample_fragments(cfg.train_batch_size)
-            n = sum(f.count for f in frags)
+            # runner fragments go to the learner(s) as they are: stacked on the GPU, not the host.
+            # With learner actors the driver does not even materialise them: the learners read
+            # the runners' fragments straight from the shared-memory store (object refs)
+            refs = self._sample_fragment_refs(cfg.train_batch_size)
+            if refs is not None:
+                frags, n = refs
+            else:
+                frags = self._sample_fragments(cfg.train_batch_size)
+                n = sum(f.count for f in frags)
             t1 = time.perf_counter()
             info = self.learner_group.update("ppo", frags)
         t2 = time.perf_counter()

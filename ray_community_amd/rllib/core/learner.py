@@ -655,6 +655,10 @@ def _learner_actor_cls():
 
         def update(self, kind, batch):
             t0 = time.perf_counter()
+            if isinstance(batch, (list, tuple)) and batch and not isinstance(batch[0], SampleBatch):
+                from ..._private.worker import get
+
+                batch = get(list(batch))  # fragment refs: mapped from the shared-memory store
             out = getattr(self.learner, f"update_{kind}")(batch)
             out = dict(out)
             out["rank_update_time_s"] = time.perf_counter() - t0

@@ -104,12 +104,19 @@ class SampleBatch(dict):
         return out
 
     def to_device(self, device):
+        import warnings
+
         import torch
 
         out = SampleBatch()
         for k, v in self.items():
             if isinstance(v, np.ndarray) and v.dtype != object:
-                out[k] = torch.from_numpy(np.ascontiguousarray(v)).to(device, non_blocking=True)
+                with warnings.catch_warnings():
+                    # fragments mapped from the shared-memory store are read-only by contract; the
+                    # tensor made over them is only the source of this copy, never written
+                    warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+                    t = torch.from_numpy(np.ascontiguousarray(v))
+                out[k] = t.to(device, non_blocking=True)
             elif hasattr(v, "to"):
                 out[k] = v.to(device)
             else:
