@@ -23,7 +23,7 @@ def _dist_info():
 
 def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4, bucket_cap_mb=256.0,
                          device=None, seed=1234, max_grad_norm=1.0, parallel="ddp", grad_reduce_dtype="bf16",
-                         overlap_optimizer=False, **model_overrides):
+                         overlap_optimizer=False, grad_norm_side_stream=False, **model_overrides):
     """``parallel``: "ddp" (replicated AdamW after a bucketed all-reduce; the default, as the
     headline metric is DDP), "zero" (reduce-scatter, sharded AdamW, all-gather overlapped with the
     next forward — parallel/fsdp.py), "fsdp" (ZeRO-3: parameters sharded too, each block's weights
@@ -34,7 +34,12 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
     ``overlap_optimizer`` (DDP): the HBM-bound AdamW update runs bucket by bucket on a side stream
     overlapped with the next forward (``FlatAdamW.overlap_with_forward``). Off by default: on the
     8B step it measured 368 vs 366 ms serial -- the forward's 256-VGPR GEMM workgroups fill every
-    SIMD, so AdamW waves cannot be co-resident and only time-slice with them."""
+    SIMD, so AdamW waves cannot be co-resident and only time-slice with them.
+    ``grad_norm_side_stream`` (DDP): take the clip norm's sum of squares per finished bucket on a
+    side stream during backward instead of one pass before AdamW. Off by default: on the 8B step
+    the side-stream kernels (68 per step) compete with the memory-bound backward kernels for HBM
+    and the main stream lost more than the 16 GB pass costs (342.3 vs 344.0 ms median,
+    scripts/step_ab.py --arms norm_side,norm_main, profiles/llama8b_r6_cpath_baseline.md)."""
     from ..models import build_llama
     from ..parallel import (DistributedDataParallel, FlatAdamW, FullyShardedAdamW, FullyShardedDataParallel,
                             ShardedAdamW, ShardedDataParallel)
@@ -54,7 +59,8 @@ def build_llama_training(model="llama3-8b", seq_len=4096, micro_batch=2, lr=3e-4
         opt = FullyShardedAdamW(ddp, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
     elif parallel == "ddp":
         ddp = DistributedDataParallel(net, bucket_cap_mb=bucket_cap_mb, reduce_dtype=rdt,
-                                      precompute_grad_norm=max_grad_norm is not None and max_grad_norm > 0)
+                                      precompute_grad_norm=bool(grad_norm_side_stream) and max_grad_norm is not None
+                                      and max_grad_norm > 0)
         opt = FlatAdamW(ddp.flat, lr=lr, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=max_grad_norm)
         if overlap_optimizer:
             opt.overlap_with_forward(net)

@@ -43,7 +43,7 @@ def _toggles():
         "base": lambda: (lambda: None),
         # gradient-norm sum of squares: per bucket on the DDP side stream during backward (default)
         # vs one pass on the compute stream before AdamW
-        "norm_side": lambda: (lambda: None),
+        "norm_side": lambda: _set_attr(CTX["ddp"], "_norm", CTX["norm"]),
         "norm_main": lambda: _set_attr(CTX["ddp"], "_norm", None),
         # gate_up input gradient on hipBLASLt instead of the hand GEMM
         "noplan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", False),
@@ -84,8 +84,11 @@ def main():
     for arm in arms:
         if arm not in toggles:
             raise SystemExit(f"unknown arm {arm!r}; known: {sorted(toggles)}")
-    net, ddp, opt, batch, step = build_llama_training(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch)
-    CTX.update(ddp=ddp, opt=opt)
+    net, ddp, opt, batch, step = build_llama_training(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch,
+                                                      grad_norm_side_stream=True)
+    CTX.update(ddp=ddp, opt=opt, norm=ddp._norm)
+    if "norm_side" not in a.arms.split(","):
+        ddp._norm = None  # the shipped default: the norm pass runs on the compute stream
     data = [batch() for _ in range(2)]
     times = {arm: [] for arm in arms}
     for arm in arms:  # warm every arm's code path once (kernel loads, W^T copies, allocator)

@@ -42,3 +42,29 @@ def test_eight_learners_match_one_learner_over_three_updates(shutdown_only):
             assert all(torch.equal(r[k], reps[0][k]) for k in r)
     finally:
         eight.shutdown()
+
+
+def test_synthetic_atari_packed_frame_stack_is_bitwise_equal():
+    """The packed uint32 frame-stack render (one in-place shift per step) produces exactly the
+    observations, rewards, terminations and final observations of the per-channel HWC render."""
+    import numpy as np
+
+    from ray_community_amd.rllib.env.envs import SyntheticAtariVec
+
+    a = SyntheticAtariVec(num_envs=8, seed=11, max_episode_steps=120)
+    b = SyntheticAtariVec(num_envs=8, seed=11, max_episode_steps=120)
+    b._packed = None  # the generic path
+    assert a._packed is not None
+    oa, _ = a.reset()
+    ob, _ = b.reset()
+    assert np.array_equal(oa, ob)
+    rng = np.random.default_rng(5)
+    resets = 0
+    for _ in range(1500):
+        act = rng.integers(0, 6, 8)
+        ra, rb = a.step(act), b.step(act)
+        for x, y in zip(ra[:4], rb[:4]):
+            assert np.array_equal(x, y)
+        assert np.array_equal(ra[4]["final_obs"], rb[4]["final_obs"])
+        resets += int((ra[2] | ra[3]).sum())
+    assert resets > 0
