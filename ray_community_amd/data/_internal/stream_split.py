@@ -109,8 +109,12 @@ class SplitCoordinator:
                         break
                     self._cv.wait(_POLL_S)
             item = None
+            rows = None
             try:
                 item = next(self._it)
+                # the block's row count is fetched BEFORE taking the lock: routing under _cv never
+                # blocks on an object fetch, so other consumers' get / start_epoch calls proceed
+                rows = self._rows(item[1])
             except StopIteration:
                 pass
             except Exception:
@@ -125,7 +129,7 @@ class SplitCoordinator:
                     if item is None:
                         self._finish()
                     else:
-                        self._route(item, split_idx)
+                        self._route(item, split_idx, rows)
                 self._cv.notify_all()
 
     def _rows(self, meta_ref) -> int:
@@ -133,7 +137,7 @@ class SplitCoordinator:
 
         return int(get(meta_ref)["num_rows"])
 
-    def _route(self, item, requester: int):
+    def _route(self, item, requester: int, rows: int):
         b, m = item
         if not self._equal:
             dest = requester
@@ -145,9 +149,8 @@ class SplitCoordinator:
                             dest = j
                             break
             self._queues[dest].append((b, m))
-            self._stats["rows"][dest] += self._rows(m)
+            self._stats["rows"][dest] += rows
             return
-        rows = self._rows(m)
         if rows == 0:
             return
         self._buffer.append((b, m, rows))

@@ -462,12 +462,22 @@ class ZipOp(PhysicalOp):
         self.right: collections.deque = collections.deque()
         self._out = 0
         self._zip = None
+        self._zip_pending = None  # a side-input item polled but whose metadata is not ready yet
 
     @staticmethod
     def _rows(meta):
         from ..._private.worker import get
 
         return int(get(meta)["num_rows"])
+
+    @staticmethod
+    def _meta_ready(meta) -> bool:
+        """Non-blocking: is the block's metadata computed? (The executor loop never waits on an
+        object fetch here; a block whose metadata is pending is taken on a later pass.)"""
+        from ..._private.worker import wait
+
+        ready, _ = wait([meta], num_returns=1, timeout=0)
+        return bool(ready)
 
     def _refill(self):
         """Hold at most two blocks of each side here: the rest stays upstream (this op's input
@@ -476,13 +486,16 @@ class ZipOp(PhysicalOp):
         for q in (self.left, self.right):
             while q and q[0][1] - q[0][2] <= 0:
                 q.popleft()
-        while self.inq and len(self.left) < 2:
+        while self.inq and len(self.left) < 2 and self._meta_ready(self.inq[0].meta):
             b = self.inq.popleft()
             self.left.append([b.block, self._rows(b.meta), 0])
         while len(self.right) < 2:
-            it = self.side.poll()
-            if it is None:
+            if self._zip_pending is None:
+                self._zip_pending = self.side.poll()
+            it = self._zip_pending
+            if it is None or not self._meta_ready(it[1]):
                 break
+            self._zip_pending = None
             self.right.append([it[0], self._rows(it[1]), 0])
         for q in (self.left, self.right):
             while q and q[0][1] - q[0][2] <= 0:
@@ -511,7 +524,7 @@ class ZipOp(PhysicalOp):
 
     def done(self) -> bool:
         self._refill()
-        if not (self.upstream_done and self.side.drained() and not self.inq):
+        if not (self.upstream_done and self.side.drained() and not self.inq) or self._zip_pending is not None:
             return False
         self._refill()
         if self.left and self.right:

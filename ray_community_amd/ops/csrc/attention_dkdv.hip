@@ -669,8 +669,13 @@ static bool g_dkdv_hs = [] {
 }();
 static bool g_dkdv_hs_stage = false;
 // wait states ahead of each asm MFMA of the dS-storing kernel: the s_nop operand, 1 (2 wait
-// states, LLVM's VALU-write -> MFMA-read count; the default) or 3. Same-process A/B: bwd 1.025-1.050
-// vs 1.058-1.081 ms, 8B step 345.7 vs 349.0 ms median; gradients bitwise equal
+// states; the default) or 3. 2 is the documented requirement for the hazard these nops cover -- a
+// VALU write (or v_accvgpr_write) of a register that the next MFMA reads as its A/B operand:
+// cdna_hip_programming.md §3 'A/B operands may be AGPRs' and §5.7 item 2 ("a just-written "v"
+// operand or v_accvgpr_write -> MFMA operand (s_nop 1)", from cdna_asm_programming.md Table 38),
+// which is also the count LLVM's hazard recognizer inserts for this pair outside asm. Same-process
+// A/B: bwd 1.025-1.050 vs 1.058-1.081 ms, 8B step 345.7 vs 349.0 ms median; gradients bitwise
+// equal between the two counts on causal and full masks, MHA and GQA group sizes 1-8
 // (tests/test_attention_gpu.py::test_ds_kernel_wait_state_variants_agree_bitwise).
 static int g_hs_nops = [] {
   const char* e = getenv("RCA_ATTN_HS_NOPS");

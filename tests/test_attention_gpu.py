@@ -315,10 +315,12 @@ def test_dq_from_ds_two_blocks_per_wave_is_bitwise_equal(S, causal):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-def test_ds_kernel_wait_state_variants_agree_bitwise(causal):
+@pytest.mark.parametrize("B,S,Hq,Hk", [(2, 1024, 8, 2), (1, 512, 8, 8), (1, 768, 8, 1), (2, 2048, 32, 8)])
+def test_ds_kernel_wait_state_variants_agree_bitwise(causal, B, S, Hq, Hk):
     """The dS-storing dK/dV kernel with 2 (s_nop 1) and 4 (s_nop 3) wait states ahead of each asm MFMA
-    computes bit-identical gradients (a missing wait state shows up as stale MFMA operands)."""
-    B, S, Hq, Hk, D = 2, 1024, 8, 2, 128
+    computes bit-identical gradients (a missing wait state shows up as stale MFMA operands), on the
+    causal and full masks and MHA / GQA group sizes 1, 4 and 8 (the 8B bench's 32 q / 8 kv heads)."""
+    D = 128
     q, k, v = _mk(B, S, Hq, D, 81), _mk(B, S, Hk, D, 82), _mk(B, S, Hk, D, 83)
     do = _mk(B, S, Hq, D, 84)
     lib = ops._lib.lib()
