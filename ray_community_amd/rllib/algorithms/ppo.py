@@ -86,7 +86,12 @@ class PPO(Algorithm):
         t3 = time.perf_counter()
         # driver-side phase times of the iteration (sampling includes the fragments' transfer to
         # the driver; the learner phase includes the host->device copy)
-        info["sample_time_s"], info["learn_time_s"], info["sync_weights_time_s"] = t1 - t0, t2 - t1, t3 - t2
+        phases = {"sample_time_s": t1 - t0, "learn_time_s": t2 - t1, "sync_weights_time_s": t3 - t2}
+        if self.multi_agent:  # info is keyed by policy id: the iteration's phases go in each
+            for v in info.values():
+                v.update(phases)
+        else:
+            info.update(phases)
         info["_steps_this_iter"] = n
         return info
 

@@ -13,6 +13,7 @@ Reference: ``rllib/env/{vector_env,single_agent_env_runner}.py`` and gymnasium s
 from __future__ import annotations
 
 import math
+import os
 import sys
 from typing import Any, Callable, Dict, Optional, Tuple
 
@@ -250,7 +251,8 @@ class SyntheticAtariVec(VectorEnv):
         # pixels in the top byte, instead of a strided per-channel shift of the HWC uint8 stack
         # (the runner's env step was 30 % of its sample loop, profiles/rllib_runner_r6.md)
         self._packed = self.frames.view(np.uint32).reshape(n, self.H, self.W) \
-            if self.STACK == 4 and sys.byteorder == "little" else None
+            if (self.STACK == 4 and sys.byteorder == "little"
+                and os.environ.get("RCA_SYNTH_ATARI_PACKED", "1") != "0") else None
         self.bx = np.zeros(n)
         self.by = np.zeros(n)
         self.vx = np.zeros(n)
