@@ -210,10 +210,13 @@ class Algorithm(Trainable):
             return self._foreach_runner("sample", max(1, steps_total // n))
         return [self.local_runner.sample(steps_total)]
 
-    def _sample_fragment_refs(self, steps_total: int):
+    def _sample_fragment_refs(self, steps_total: int, wait_ready: bool = True):
         """``(fragment refs, env steps)`` when the fragments can go to remote learners by reference
         (remote runners, learner actors whose count divides the fragments, the default fail-fast
-        runner policy), else None. The driver only waits for the fragments to be ready."""
+        runner policy), else None. With ``wait_ready`` the driver waits for the fragments to be
+        ready (never fetching them); without, the refs go out at once and each learner copies the
+        fragments to its device as they arrive, overlapping the host->device transfer with the
+        runners still sampling."""
         g = getattr(self, "env_runner_group", None)
         lg = getattr(self, "learner_group", None)
         n = len(self.remote_runners)
@@ -227,7 +230,8 @@ class Algorithm(Trainable):
         refs = [r.get() for r in res.ignore_errors()]
         if len(refs) != n:
             return None
-        wait(refs, num_returns=len(refs))
+        if wait_ready:
+            wait(refs, num_returns=len(refs))
         envs = int(self.config.num_envs_per_env_runner or 1)
         steps = n * envs * max(1, per // envs)
         return refs, steps

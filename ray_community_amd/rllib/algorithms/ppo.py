@@ -72,7 +72,7 @@ class PPO(Algorithm):
             # runner fragments go to the learner(s) as they are: stacked on the GPU, not the host.
             # With learner actors the driver does not even materialise them: the learners read
             # the runners' fragments straight from the shared-memory store (object refs)
-            refs = self._sample_fragment_refs(cfg.train_batch_size)
+            refs = self._sample_fragment_refs(cfg.train_batch_size, wait_ready=False)
             if refs is not None:
                 frags, n = refs
             else:
@@ -86,6 +86,8 @@ class PPO(Algorithm):
         t3 = time.perf_counter()
         # driver-side phase times of the iteration (sampling includes the fragments' transfer to
         # the driver; the learner phase includes the host->device copy)
+        # (with fragment refs the sample phase only issues the requests: the learner phase then
+        # includes waiting for the runners, overlapped with the fragments' device copies)
         phases = {"sample_time_s": t1 - t0, "learn_time_s": t2 - t1, "sync_weights_time_s": t3 - t2}
         if self.multi_agent:  # info is keyed by policy id: the iteration's phases go in each
             for v in info.values():

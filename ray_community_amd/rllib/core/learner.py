@@ -656,9 +656,7 @@ def _learner_actor_cls():
         def update(self, kind, batch):
             t0 = time.perf_counter()
             if isinstance(batch, (list, tuple)) and batch and not isinstance(batch[0], SampleBatch):
-                from ..._private.worker import get
-
-                batch = get(list(batch))  # fragment refs: mapped from the shared-memory store
+                batch = self._fetch_fragments(list(batch))
             out = getattr(self.learner, f"update_{kind}")(batch)
             out = dict(out)
             out["rank_update_time_s"] = time.perf_counter() - t0
@@ -668,6 +666,23 @@ def _learner_actor_cls():
 
         def call(self, name, *args):
             return getattr(self.learner, name)(*args)
+
+        def _fetch_fragments(self, refs):
+            """Runner fragments by reference: each is mapped from the shared-memory store and copied
+            to this learner's device the moment its runner finishes, while the others still
+            sample (in fragment order in the result)."""
+            from ..._private.worker import get, wait
+
+            pos = {r: i for i, r in enumerate(refs)}
+            out = [None] * len(refs)
+            pending = list(refs)
+            dev = self.learner.device
+            while pending:
+                ready, pending = wait(pending, num_returns=1)
+                for r in ready:
+                    fr = get(r)
+                    out[pos[r]] = fr.to_device(dev) if dev.type == "cuda" else fr
+            return out
 
     return _LearnerActor
 

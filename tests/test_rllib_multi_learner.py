@@ -68,3 +68,32 @@ def test_synthetic_atari_packed_frame_stack_is_bitwise_equal():
         assert np.array_equal(ra[4]["final_obs"], rb[4]["final_obs"])
         resets += int((ra[2] | ra[3]).sum())
     assert resets > 0
+
+
+def test_ppo_fragment_refs_to_learner_actor_match_materialised_path(shutdown_only, monkeypatch):
+    """PPO with a learner actor takes the runners' fragments by reference (the learner maps them
+    from the shared-memory store and copies each to its device as it arrives); the weights after
+    three iterations are bitwise those of the path that materialises them in the driver."""
+    import torch
+
+    from ray_community_amd.rllib.algorithms import algorithm as A
+
+    ray.init(num_cpus=6)
+
+    def run():
+        cfg = (PPOConfig().environment("CartPole-v1").env_runners(num_env_runners=2, num_envs_per_env_runner=4)
+               .training(lr=1e-3, train_batch_size=256, minibatch_size=128, num_epochs=2,
+                         model={"fcnet_hiddens": [16]})
+               .learners(num_learners=1).debugging(seed=7))
+        algo = cfg.build()
+        try:
+            steps = [algo.train()["num_env_steps_sampled_this_iter"] for _ in range(3)]
+            return algo.learner_group.get_weights(), steps
+        finally:
+            algo.stop()
+
+    w_refs, s_refs = run()
+    monkeypatch.setenv("RCA_RLLIB_FRAGMENT_REFS", "0")
+    w_mat, s_mat = run()
+    assert s_refs == s_mat == [256, 256, 256]
+    assert all(torch.equal(w_refs[k], w_mat[k]) for k in w_refs)
