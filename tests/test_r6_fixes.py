@@ -50,3 +50,40 @@ def test_rejected_async_put_raises_on_get_and_wait(shutdown_only):
         ray.get(ref)
     with pytest.raises(ValueError, match="rejected"):
         ray.wait([ref], timeout=0.1)
+
+
+def test_repeated_shm_get_is_local_and_survives_spill(shutdown_only):
+    """A ref's shm descriptor is cached after the first get: repeated gets map the object with no
+    head round trip. When the object is spilled meanwhile, the native pin fails and the head is
+    asked again (it restores the object); freed objects are never answered from the cache."""
+    import numpy as np
+
+    ray.init(num_cpus=1, object_store_memory=40 << 20)
+    from ray_community_amd._private.worker import _core, free
+
+    core = _core()
+    big = np.arange(2_000_000, dtype=np.float64)  # 16 MB: the shm store
+    ref = ray.put(big)
+    assert np.array_equal(ray.get(ref), big)
+    calls = []
+    orig = core.client.call
+
+    def counting(method, *a, **k):
+        calls.append(method)
+        return orig(method, *a, **k)
+
+    core.client.call = counting
+    try:
+        for _ in range(5):
+            assert ray.get(ref)[123] == 123.0
+        assert "get" not in calls
+        # push it out of shared memory, then read it again
+        others = [ray.put(np.full(2_000_000, i, dtype=np.float64)) for i in range(6)]
+        assert orig("store_stats")["num_spilled"] > 0
+        assert np.array_equal(ray.get(ref), big)
+        del others
+    finally:
+        core.client.call = orig
+    free([ref])
+    with pytest.raises((rexc.RayError, TimeoutError)):
+        ray.get(ref, timeout=2)
