@@ -312,9 +312,22 @@ class _RoPE(torch.autograd.Function):
         pos = saved[1] if has_pos else None
         if not getattr(g, "_rca_owned_grad", False) or not g.is_contiguous():
             g = g.contiguous().clone()  # never rotate a gradient buffer someone else may still read
+        T, Wd = g.shape
+        if _ROPE_BWD_TR and D == 128 and T % 128 == 0 and Wd % 128 == 0:
+            # rotate back AND write g^T for the qkv weight gradient in one pass (the linear's
+            # backward picks the transposed copy up by the gradient's storage: no transpose pass)
+            g_t = torch.empty(Wd, T, device=g.device, dtype=g.dtype)
+            check(lib().rca_rope_bwd_tr(g.data_ptr(), cs.data_ptr(), _p(pos), g_t.data_ptr(), T, seq_len, Wd, n_rot,
+                                        stream_ptr(g.device)), "rope_bwd_tr")
+            put_grad_transposed(g, g_t)
+            return g, None, None, None, None, None
         check(lib().rca_rope(g.data_ptr(), cs.data_ptr(), _p(pos), g.shape[0], seq_len, n_rot, g.stride(0), D, 1,
                              stream_ptr(g.device)), "rope_bwd")
         return g, None, None, None, None, None
+
+
+# RCA_ROPE_BWD_TR=0: the separate in-place RoPE backward (+ the consumer's own transpose), for A/B
+_ROPE_BWD_TR = os.environ.get("RCA_ROPE_BWD_TR", "1") != "0"
 
 
 def apply_rope_(qkv, cs, seq_len: int, n_q_heads: int, n_kv_heads: int, head_dim: int, positions=None):

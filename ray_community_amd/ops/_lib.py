@@ -38,6 +38,7 @@ _SIGS = {
                                     c_void_p]),
     "rca_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_ll, c_void_p]),
     "rca_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "rca_rope_bwd_tr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "rca_ce_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_ll, c_void_p]),
     "rca_ce_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_ll, c_int, c_ll, c_void_p]),
     "rca_ce_fused": (c_int, [c_void_p] * 5 + [c_ll, c_int, c_ll, c_void_p]),

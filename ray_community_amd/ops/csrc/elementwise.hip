@@ -283,6 +283,84 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
   }
 }
 
+// RoPE backward fused with the transpose the qkv weight gradient reads: one 128-token x 128-column
+// tile (= one head of D = 128) per workgroup, the transpose128 tile scheme below. Each lane holds
+// 8 columns of 2 rows; the rotate-half partner (column c +- 64) is the lane 8 apart (same rows):
+// one __shfl_xor(.., 8) per register. Heads < nrot are rotated by -theta (the adjoint) and written
+// back in place; every head goes to g_t [W][T] transposed. Replaces the in-place rope_kernel pass
+// over dq / dk AND the transpose of dqkv: the v heads are only read, the q / k heads read once.
+__global__ __launch_bounds__(256) void rope_bwd_tr_kernel(bf16_t* __restrict__ g, const float2* __restrict__ cs,
+                                                          const int* __restrict__ pos, bf16_t* __restrict__ g_t,
+                                                          int T, int S, int W, int nrot) {
+  __shared__ u32x4 W4[128 * 64 / 4];
+  unsigned* Wd = reinterpret_cast<unsigned*>(W4);
+  const int tilesC = W >> 7;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = (bid / tilesC) << 7, c0 = (bid % tilesC) << 7;
+  const int t = threadIdx.x, ch = t & 15, rp = t >> 4;
+  const bool rot = (c0 >> 7) < nrot;
+  const bool hi = ch >= 8;                 // second half of the head: x[c] pairs with x[c - 64]
+  const int f0 = (ch & 7) * 8;             // frequency index of this lane's first column
+  u32x4 va[4], vb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    bf16_t* p = g + (long)(r0 + 2 * rp + 32 * k) * W + c0 + ch * 8;
+    va[k] = *reinterpret_cast<const u32x4*>(p);
+    vb[k] = *reinterpret_cast<const u32x4*>(p + W);
+  }
+  if (rot) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        u32x4& v = half ? vb[k] : va[k];
+        const int row = r0 + 2 * rp + 32 * k + half;
+        const int p_ = pos ? pos[row] : row % S;
+        u32x4 w;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) w[m] = (unsigned)__shfl_xor((int)v[m], 8, 64);
+        float a[8], b[8], o[8];
+        unpack8(v, a);  // own columns
+        unpack8(w, b);  // partner columns (c +- 64)
+        const float4* csr = reinterpret_cast<const float4*>(cs + (long)p_ * 64 + f0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 q = csr[j];  // (cos, sin) of frequencies f0 + 2j, f0 + 2j + 1
+          // backward = rotation by -theta: lo' = lo c + hi s, hi' = hi c - lo s
+          o[2 * j] = hi ? a[2 * j] * q.x - b[2 * j] * q.y : a[2 * j] * q.x + b[2 * j] * q.y;
+          o[2 * j + 1] = hi ? a[2 * j + 1] * q.z - b[2 * j + 1] * q.w : a[2 * j + 1] * q.z + b[2 * j + 1] * q.w;
+        }
+        v = pack8(o);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bf16_t* p = g + (long)(r0 + 2 * rp + 32 * k) * W + c0 + ch * 8;
+      *reinterpret_cast<u32x4*>(p) = va[k];
+      *reinterpret_cast<u32x4*>(p + W) = vb[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int q = (rp + 16 * k) ^ (2 * ch);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      Wd[(ch * 8 + 2 * m) * 64 + q] = __builtin_amdgcn_perm(vb[k][m], va[k][m], 0x05040100u);
+      Wd[(ch * 8 + 2 * m + 1) * 64 + q] = __builtin_amdgcn_perm(vb[k][m], va[k][m], 0x07060302u);
+    }
+  }
+  __syncthreads();
+  const int q4 = (t & 15) * 4;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int j = (t >> 4) + 16 * p;
+    const int sw = 2 * (j >> 3);
+    u32x4 o = W4[(j * 64 + (q4 ^ (sw & ~3))) >> 2];
+    if (sw & 2) o = u32x4{o[2], o[3], o[0], o[1]};
+    *reinterpret_cast<u32x4*>(g_t + (long)(c0 + j) * T + r0 + q4 * 2) = o;
+  }
+}
+
 // 128 x 128 tiles (R, C multiples of 128): 256-B row segments on both the read and the write side
 // (the 64 x 64 kernel's 128-B pieces, 8 KB apart, cost DRAM page locality) and no 16-bit LDS
 // traffic. Each lane loads two input rows (2q, 2q+1) x 8 columns and pairs them in registers
@@ -327,6 +405,19 @@ __global__ __launch_bounds__(256) void transpose128_bf16_kernel(const bf16_t* __
     if (sw & 2) o = u32x4{o[2], o[3], o[0], o[1]};
     *reinterpret_cast<u32x4*>(out + (long)(c0 + j) * R + r0 + q4 * 2) = o;
   }
+}
+
+// g [T][W] contiguous (W = heads x 128), D = 128: the first nrot heads rotated back in place, g_t
+// [W][T] = g^T of the result. Contract: T % 128 == 0, W % 128 == 0, 16-B aligned; else -1.
+RCA_API int rca_rope_bwd_tr(void* g, const void* cs, const int* pos, void* g_t, int T, int S, int W, int nrot,
+                            hipStream_t stream) {
+  if (T <= 0 || W <= 0 || (T & 127) || (W & 127) || nrot < 0 || nrot * 128 > W || S <= 0) return -1;
+  if (((uintptr_t)g | (uintptr_t)g_t | (uintptr_t)cs) & 15) return -1;
+  const long long tiles = (long long)(T >> 7) * (W >> 7);
+  if (tiles >= (1LL << 31)) return -2;
+  hipLaunchKernelGGL(rope_bwd_tr_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, (bf16_t*)g, (const float2*)cs,
+                     pos, (bf16_t*)g_t, T, S, W, nrot);
+  return (int)hipGetLastError();
 }
 
 RCA_API int rca_transpose_bf16(const void* in, void* out, int R, int C, long long ldi, hipStream_t stream) {

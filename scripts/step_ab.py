@@ -22,6 +22,11 @@ def _lib():
     return _lib.lib()
 
 
+def _ops():
+    from ray_community_amd import ops
+    return ops
+
+
 def _set_attr(mod, name, value):
     old = getattr(mod, name)
     setattr(mod, name, value)
@@ -45,6 +50,9 @@ def _toggles():
         # vs one pass on the compute stream before AdamW
         "norm_side": lambda: _set_attr(CTX["ddp"], "_norm", CTX["norm"]),
         "norm_main": lambda: _set_attr(CTX["ddp"], "_norm", None),
+        # RoPE backward fused with the dqkv transpose (default) vs the in-place kernel + transpose
+        "rope_tr": lambda: _set_attr(_ops(), "_ROPE_BWD_TR", True),
+        "rope_sep": lambda: _set_attr(_ops(), "_ROPE_BWD_TR", False),
         # gate_up input gradient on hipBLASLt instead of the hand GEMM
         "noplan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", False),
         "plan": lambda: _set_attr(fl, "_DGRAD_PLANS_ON", True),

@@ -96,6 +96,40 @@ def test_rope_inplace_fwd_bwd():
     _close(x.grad, xr.grad, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("T,S,Hq,Hk,with_pos", [(256, 128, 4, 2, False), (8192, 4096, 32, 8, False),
+                                                (384, 384, 8, 8, True), (128, 64, 2, 1, False)])
+def test_rope_backward_fused_with_transpose(T, S, Hq, Hk, with_pos):
+    """rca_rope_bwd_tr: the RoPE backward (rotation by -theta of the q / k heads) and the transpose
+    of the whole dqkv gradient in one pass, against the fp32 reference and the separate in-place
+    kernel (within one bf16 rounding: the two may contract the mul/adds differently)."""
+    from ray_community_amd.ops._lib import stream_ptr
+
+    torch.manual_seed(3)
+    D, n_rot = 128, Hq + Hk
+    W = (Hq + 2 * Hk) * D
+    cs = ops.rope_cos_sin(8192, D, 500000.0).to(DEV)
+    g = torch.randn(T, W, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 8192, (T,), device=DEV, dtype=torch.int32) if with_pos else None
+    L = ops.lib()
+    g1, g1t = g.clone(), torch.empty(W, T, device=DEV, dtype=torch.bfloat16)
+    assert L.rca_rope_bwd_tr(g1.data_ptr(), cs.data_ptr(), pos.data_ptr() if pos is not None else None,
+                             g1t.data_ptr(), T, S, W, n_rot, stream_ptr(g.device)) == 0
+    g2 = g.clone()
+    assert L.rca_rope(g2.data_ptr(), cs.data_ptr(), pos.data_ptr() if pos is not None else None, T, S, n_rot, W,
+                      D, 1, stream_ptr(g.device)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(g1t, g1.t())  # the transposed copy is exactly the rotated gradient
+    assert torch.equal(g1[:, n_rot * D:], g[:, n_rot * D:])  # v heads untouched
+    ulps = (g1.view(torch.int16).int() - g2.view(torch.int16).int()).abs()
+    assert int(ulps.max()) <= 1
+    # fp32 reference: rotation by -theta = rotation with sin negated
+    p = pos.long() if pos is not None else torch.arange(T, device=DEV) % S
+    csn = cs.clone()
+    csn[..., 1] = -csn[..., 1]
+    rot = ref.rope_ref(g[:, : n_rot * D].float().reshape(T, n_rot, D), csn, p).reshape(T, -1)
+    _close(g1[:, : n_rot * D], rot, atol=2e-2, rtol=1e-2)
+
+
 @pytest.mark.parametrize("V", [128256, 1000, 1003])
 def test_cross_entropy(V):
     torch.manual_seed(0)
