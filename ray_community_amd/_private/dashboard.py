@@ -2,11 +2,24 @@
 Prometheus exposition at ``/metrics``, JSON state at ``/api/*`` backed by the head's state RPCs, and
 the job REST API of ``dashboard/modules/job/job_head.py`` (``/api/jobs/``) on the session's
 JobManager actor, which ``JobSubmissionClient("http://host:port")`` speaks. Started by
-``init(include_dashboard=True, dashboard_port=...)``."""
+``init(include_dashboard=True, dashboard_port=...)``.
+
+Per-node agents (reference ``dashboard/agent.py`` + ``modules/reporter`` / ``modules/log``): the
+dashboard supervises one ``dashboard_agent`` process per alive node (``_AgentSupervisor``), which
+reports that node's and its workers' stats through the head KV and serves that node's logs.
+``/nodes?view=summary``, ``/nodes/<node_id>``, ``/api/v0/logs[/file]?node_id=`` and the
+``ray_component_*`` / ``ray_node_agent_*`` lines of ``/metrics`` come from them.
+``RCA_DASHBOARD_AGENTS=0`` turns the agents off."""
 from __future__ import annotations
 
 import json
+import os
+import subprocess
+import sys
 import threading
+import time
+import urllib.error
+import urllib.request
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from urllib.parse import parse_qs, urlparse
 
@@ -93,7 +106,16 @@ class Dashboard:
                                            int((query.get("lines") or ["-1"])[0]))
                         return self._send(200, "\n".join(lines), "text/plain; charset=utf-8")
                     if path == "/metrics":
-                        return self._send(200, dash._call("metrics_text"), "text/plain; version=0.0.4")
+                        text = dash._call("metrics_text")
+                        if dash.agents is not None:
+                            text = text.rstrip("\n") + "\n" + "\n".join(dash.agents.prometheus_lines()) + "\n"
+                        return self._send(200, text, "text/plain; version=0.0.4")
+                    if path == "/nodes" or path.startswith("/nodes/"):
+                        code, body = dash._nodes_route(path.split("/")[2:], query)
+                        return self._send(code, json.dumps(body, default=str), "application/json")
+                    if path in ("/api/v0/logs", "/api/v0/logs/file") and query.get("node_id"):
+                        code, body, ctype = dash._agent_log_route(path.endswith("/file"), query)
+                        return self._send(code, body, ctype)
                     if path.startswith("/api/v0/"):
                         code, body = dash._state_route(path[len("/api/v0/"):].split("/"), query)
                         return self._send(code, json.dumps(body, default=str), "application/json")
@@ -120,6 +142,10 @@ class Dashboard:
         self.host, self.port = host, self.server.server_address[1]
         self.thread = threading.Thread(target=self.server.serve_forever, daemon=True, name="rca-dashboard")
         self.thread.start()
+        self.agents = None
+        if os.environ.get("RCA_DASHBOARD_AGENTS", "1") != "0" and getattr(head, "sock_path", None):
+            self.agents = _AgentSupervisor(self, head.sock_path, getattr(head, "logs_dir", None),
+                                           float(os.environ.get("RCA_DASHBOARD_AGENT_PERIOD_S", "1.0")))
 
     def _call(self, method, *args):
         return self.client.call(method, *args)
@@ -249,8 +275,200 @@ class Dashboard:
         return f"http://{self.host}:{self.port}"
 
     def stop(self):
+        if self.agents is not None:
+            self.agents.stop()
         self.server.shutdown()
         self.server.server_close()
+
+    # ------------------------------------------------------------------ per-node agents
+    def _nodes_route(self, rest, query):
+        """``GET /nodes?view=summary`` and ``GET /nodes/<node_id>`` (reference
+        ``modules/node/node_head.py`` get_all_nodes / get_node), in the reference envelope."""
+        reports = self.agents.reports() if self.agents is not None else {}
+        nodes = {n["NodeID"]: n for n in self._call("nodes")}
+
+        def summary(nid, n):
+            rep = reports.get(nid) or {}
+            node = rep.get("node") or {}
+            return {"raylet": {"nodeId": nid, "state": "ALIVE" if n.get("Alive") else "DEAD",
+                               "isHeadNode": n.get("IsHead"), "resources": n.get("Resources"),
+                               "labels": n.get("Labels")},
+                    "hostname": rep.get("hostname"), "ip": n.get("NodeManagerAddress"),
+                    "cpu": node.get("cpu_percent"), "cpus": [node.get("cpu_count"), node.get("cpu_count")],
+                    "mem": [node.get("mem_total"), node.get("mem_available"),
+                            (100.0 * node["mem_used"] / node["mem_total"]) if node.get("mem_total") else None,
+                            node.get("mem_used")],
+                    "disk": {"/tmp": {"total": node.get("disk_total"), "used": node.get("disk_used")}},
+                    "gpus": rep.get("gpus", []), "numWorkers": rep.get("num_workers"),
+                    "agent": {"pid": rep.get("agent_pid"), "http": rep.get("agent_http"),
+                              "reportTime": rep.get("timestamp"), "reports": rep.get("reports")}}
+
+        if not rest:
+            view = (query.get("view") or ["summary"])[0]
+            if view not in ("summary", "hostnamelist"):
+                return 400, {"result": False, "msg": f"unknown view {view!r}", "data": {}}
+            if view == "hostnamelist":
+                hosts = sorted({(reports.get(nid) or {}).get("hostname") for nid in nodes} - {None})
+                return 200, {"result": True, "msg": "", "data": {"hostNameList": hosts}}
+            return 200, {"result": True, "msg": "Node summary fetched.",
+                         "data": {"summary": [summary(nid, n) for nid, n in nodes.items()]}}
+        nid = rest[0]
+        if nid not in nodes:
+            return 404, {"result": False, "msg": f"node {nid} not found", "data": {}}
+        detail = summary(nid, nodes[nid])
+        detail["workers"] = (reports.get(nid) or {}).get("workers", [])
+        return 200, {"result": True, "msg": "Node details fetched.", "data": {"detail": detail}}
+
+    def _agent_log_route(self, is_file, query):
+        """``/api/v0/logs?node_id=`` and ``/api/v0/logs/file?node_id=&filename=&lines=``: answered
+        by that node's agent (reference ``modules/log/log_manager.py`` -> the node's LogAgent)."""
+        nid = query["node_id"][0]
+        rep = (self.agents.reports() if self.agents is not None else {}).get(nid)
+        if not rep or not rep.get("agent_http"):
+            return 503, json.dumps({"result": False, "msg": f"no agent is reporting for node {nid}"}), \
+                "application/json"
+        base = rep["agent_http"]
+        try:
+            if is_file:
+                name = (query.get("filename") or [""])[0]
+                lines = int((query.get("lines") or ["-1"])[0])
+                url = f"{base}/logs/{urllib.request.quote(os.path.basename(name))}?lines={lines}"
+                with urllib.request.urlopen(url, timeout=10) as r:
+                    return 200, r.read(), "text/plain; charset=utf-8"
+            with urllib.request.urlopen(f"{base}/logs", timeout=10) as r:
+                names = json.loads(r.read())
+            return 200, json.dumps({"result": True, "msg": "", "data": {"result": {nid: names}}}), "application/json"
+        except urllib.error.HTTPError as e:
+            return e.code, e.read(), "application/json"
+
+
+class _AgentSupervisor:
+    """Keeps one ``dashboard_agent`` process per alive node: starts one for a node that has none
+    (or whose agent exited: restarted, counted in ``restarts``), stops the agent of a removed
+    node, stops them all with the dashboard. Reports are read back from the head KV."""
+
+    def __init__(self, dash, sock_path, logs_dir, period_s=1.0):
+        self.dash, self.sock_path, self.logs_dir, self.period_s = dash, sock_path, logs_dir, period_s
+        self.procs = {}
+        self.restarts = 0
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._loop, daemon=True, name="rca-agent-supervisor")
+        self._thread.start()
+
+    def _spawn(self, nid):
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ)
+        env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        cmd = [sys.executable, "-m", "ray_community_amd._private.dashboard_agent", "--sock", self.sock_path,
+               "--node-id", nid, "--period", str(self.period_s), "--parent-pid", str(os.getpid())]
+        out = subprocess.DEVNULL
+        if self.logs_dir and os.path.isdir(self.logs_dir):
+            out = open(os.path.join(self.logs_dir, f"dashboard_agent_{nid[:8]}.log"), "ab")
+        try:
+            return subprocess.Popen(cmd, env=env, stdout=out, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                    start_new_session=True)
+        finally:
+            if out is not subprocess.DEVNULL:
+                out.close()
+
+    def sync(self):
+        alive = {n["NodeID"] for n in self.dash._call("nodes") if n.get("Alive")}
+        with self._lock:
+            if self._stop.is_set():
+                return
+            for nid in list(self.procs):
+                if nid not in alive:
+                    self._terminate(self.procs.pop(nid))
+                    self._forget(nid)
+            for nid in alive:
+                p = self.procs.get(nid)
+                if p is not None and p.poll() is not None:
+                    self.restarts += 1
+                    p = None
+                if p is None:
+                    self.procs[nid] = self._spawn(nid)
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self.sync()
+            except Exception:  # noqa - head shutting down: the next period (or stop) decides
+                pass
+            self._stop.wait(max(self.period_s, 0.5))
+
+    def _forget(self, nid):
+        from .dashboard_agent import AGENT_NAMESPACE, agent_key
+
+        try:
+            self.dash._call("kv_del", agent_key(nid), AGENT_NAMESPACE)
+        except Exception:  # noqa
+            pass
+
+    @staticmethod
+    def _terminate(p):
+        if p.poll() is None:
+            p.terminate()
+            try:
+                p.wait(5)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait(5)
+
+    def stop(self):
+        self._stop.set()
+        with self._lock:
+            procs, self.procs = list(self.procs.values()), {}
+        for p in procs:
+            self._terminate(p)
+
+    def reports(self):
+        from .dashboard_agent import AGENT_NAMESPACE
+
+        out = {}
+        for key in self.dash._call("kv_keys", "node:", AGENT_NAMESPACE) or []:
+            k = key.decode() if isinstance(key, bytes) else key
+            raw = self.dash._call("kv_get", k, AGENT_NAMESPACE)
+            if raw:
+                try:
+                    out[k[len("node:"):]] = json.loads(raw)
+                except ValueError:
+                    pass
+        return out
+
+    def prometheus_lines(self):
+        """Per-node agent metrics (reference reporter_agent METRICS_GAUGES ``ray_component_*``):
+        labelled by NodeId, and by Component (worker id prefix) and pid for worker processes."""
+        reports = self.reports()
+        now = time.time()
+        gauges = {"ray_node_agent_up": ("1 while the node's dashboard agent reports (age < 5 periods)", []),
+                  "ray_node_agent_report_age_seconds": ("seconds since the node agent's last report", []),
+                  "ray_node_num_workers": ("alive worker processes on the node", []),
+                  "ray_component_cpu_percentage": ("CPU percent of a worker process", []),
+                  "ray_component_rss_mb": ("resident set size of a worker process, MB", []),
+                  "ray_component_uss_mb": ("unique set size of a worker process, MB", []),
+                  "ray_component_num_threads": ("threads of a worker process", [])}
+        for nid, rep in sorted(reports.items()):
+            lab = f'NodeId="{nid}"'
+            age = now - float(rep.get("timestamp") or 0)
+            gauges["ray_node_agent_up"][1].append((lab, 1 if age < 5 * max(self.period_s, 1.0) else 0))
+            gauges["ray_node_agent_report_age_seconds"][1].append((lab, round(age, 3)))
+            gauges["ray_node_num_workers"][1].append((lab, rep.get("num_workers", 0)))
+            for w in rep.get("workers", []):
+                wl = f'{lab},Component="worker-{(w.get("worker_id") or "")[:8]}",pid="{w.get("pid")}"'
+                gauges["ray_component_cpu_percentage"][1].append((wl, w.get("cpu_percent")))
+                gauges["ray_component_rss_mb"][1].append((wl, (w.get("rss") or 0) / 1e6))
+                if w.get("uss") is not None:
+                    gauges["ray_component_uss_mb"][1].append((wl, w["uss"] / 1e6))
+                gauges["ray_component_num_threads"][1].append((wl, w.get("num_threads")))
+        lines = []
+        for name, (help_, samples) in gauges.items():
+            samples = [(l, v) for l, v in samples if v is not None]
+            if not samples:
+                continue
+            lines += [f"# HELP {name} {help_}", f"# TYPE {name} gauge"]
+            lines += [f"{name}{{{l}}} {v}" for l, v in samples]
+        return lines
 
 
 def _version():
