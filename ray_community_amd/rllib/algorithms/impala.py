@@ -136,6 +136,8 @@ class IMPALA(Algorithm):
         # what ``learner_overlap_s`` (sampling while the learner trains) is computed from
         self._lq_update_spans: List = []
         self._sample_spans: List = []
+        self._lq_wait_s = 0.0  # driver time blocked on learner results
+        self._lq_busy_s = 0.0  # learner-thread update time
         every = max(1, int(cfg.broadcast_interval))
 
         def run():
@@ -151,7 +153,9 @@ class IMPALA(Algorithm):
                         self._lq_updates += 1
                         if self._lq_updates % every == 0:
                             self._lq_weights = (self._lq_updates, self.learner_group.get_weights())
-                    self._lq_update_spans.append((t0, time.perf_counter()))
+                    t1 = time.perf_counter()
+                    self._lq_busy_s += t1 - t0
+                    self._lq_update_spans.append((t0, t1))
                     del self._lq_update_spans[:-256]
                     self._lq_out.put(info)
                 except BaseException as e:  # noqa: BLE001 -- surfaced by the next training_step
@@ -205,27 +209,26 @@ class IMPALA(Algorithm):
         return info
 
     def _wait_learner_result(self, timeout: float):
+        t0 = time.perf_counter()
         deadline = time.monotonic() + timeout
-        while True:
-            if self._lq_error is not None:
-                raise self._lq_error
-            try:
-                return self._lq_out.get(timeout=0.05)
-            except queue.Empty:
-                if time.monotonic() > deadline:
-                    raise RuntimeError("no learner result within learner_queue_timeout") from None
+        try:
+            while True:
+                if self._lq_error is not None:
+                    raise self._lq_error
+                try:
+                    return self._lq_out.get(timeout=0.05)
+                except queue.Empty:
+                    if time.monotonic() > deadline:
+                        raise RuntimeError("no learner result within learner_queue_timeout") from None
+        finally:
+            self._lq_wait_s += time.perf_counter() - t0
 
     def _learner_overlap_s(self) -> float:
-        """Seconds in which the driver was collecting samples WHILE the learner thread was updating
-        (over the recorded spans): > 0 means sampling and learning overlap."""
-        tot = 0.0
-        ups = list(self._lq_update_spans)
-        for a, b in list(self._sample_spans):
-            for c, d in ups:
-                lo, hi = max(a, c), min(b, d)
-                if hi > lo:
-                    tot += hi - lo
-        return tot
+        """Learner-thread update seconds during which the driver was NOT blocked on the learner
+        (it was collecting fragments, broadcasting weights or between iterations, while the env
+        runners kept sampling): total update time minus the driver's waits for learner results.
+        0 means the learner ran inline in effect; > 0 means sampling and learning overlap."""
+        return max(0.0, self._lq_busy_s - self._lq_wait_s)
 
     def _broadcast_weights(self, st):
         from ..._private.worker import put
