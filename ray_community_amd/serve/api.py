@@ -406,7 +406,11 @@ class _DeploymentStatus(dict):
 def shutdown():
     from .._private import worker as w
 
+    # the next serve.start() begins from the default HTTP options again (a request_timeout_s or
+    # port given to this instance must not leak into a later one in the same process)
+    _STATE["http"] = {"host": "127.0.0.1", "port": 8000}
     if not w.is_initialized():
+        _STATE.update(controller=None, proxy=None, grpc_proxy=None, grpc=None)
         return
     try:
         c = _STATE["controller"] or w.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
