@@ -37,6 +37,11 @@ class Learner(LearnerAPI):
         if seed is not None:
             torch.manual_seed(int(seed))
         self.module = make_module(config, obs_space, act_space).to(self.device)
+        if self.device.type == "cuda" and config.get("learner_channels_last", True):
+            # NHWC conv weights (and NHWC frames from the normalize kernel, RLModule._x): MIOpen's
+            # NHWC implicit-GEMM convolutions run without the NCHW<->NHWC batched transposes that
+            # were ~10 % of the NatureCNN update's kernel time (scripts/learner_graph_bench.py)
+            self.module.to(memory_format=torch.channels_last)
         self.ddp = None
         import torch.distributed as dist
 
@@ -46,8 +51,11 @@ class Learner(LearnerAPI):
             self.ddp = DistributedDataParallel(self.module, bucket_cap_mb=64, average_in_optimizer=False,
                                                auto_finalize=True)
             self.ddp.comm_timer.enabled = True  # exposed gradient all-reduce time, per update
+        # capturable on the GPU: its step counters live on the device, so the PPO minibatch step
+        # (forward, loss, backward, clip, Adam) can be replayed as one HIP graph (_PPOStepGraph)
         self.opt = torch.optim.Adam(self.module.parameters(), lr=config.get("lr", 5e-5),
-                                    eps=config.get("adam_epsilon", 1e-8))
+                                    eps=config.get("adam_epsilon", 1e-8), capturable=self.device.type == "cuda")
+        self._ppo_graph = None
         self.kl_coeff = config.get("kl_coeff", 0.2)
         self.target = None
         self.num_updates = 0
@@ -65,6 +73,7 @@ class Learner(LearnerAPI):
 
     def set_weights(self, state):
         self.module.set_state(state)
+        self._ppo_graph = None  # a captured step holds the parameter tensors it was recorded with
 
     def get_state(self):
         st = {"module": self.module.get_state(), "opt": self.opt.state_dict(), "kl_coeff": self.kl_coeff,
@@ -76,7 +85,8 @@ class Learner(LearnerAPI):
 
     def set_state(self, st):
         self.module.set_state(st["module"])
-        self.opt.load_state_dict(st["opt"])
+        self.opt.load_state_dict(st["opt"])  # new optimizer-state tensors: recapture
+        self._ppo_graph = None
         self.kl_coeff = st.get("kl_coeff", self.kl_coeff)
         self.num_updates = st.get("num_updates", self.num_updates)
         self.last_target_update = st.get("last_target_update", self.last_target_update)
@@ -181,54 +191,50 @@ class Learner(LearnerAPI):
         clip, vclip = cfg.get("clip_param", 0.3), cfg.get("vf_clip_param", 10.0)
         vf_coeff, ent_coeff = cfg.get("vf_loss_coeff", 1.0), cfg.get("entropy_coeff", 0.0)
         use_kl = cfg.get("use_kl_loss", True) and old_logits is not None
-        stats = {"policy_loss": 0.0, "vf_loss": 0.0, "entropy": 0.0, "mean_kl": 0.0, "total_loss": 0.0}
+        keys = ["policy_loss", "vf_loss", "entropy", "mean_kl", "total_loss"]
+        hp = (clip, vclip, vf_coeff, ent_coeff, use_kl, use_kl and self.kl_coeff > 0)
         count = 0
         gen = torch.Generator(device=self.device)
         gen.manual_seed(1234 + self.num_updates)
-
-        def mean(x, w):
-            return x.mean() if w is None else (x * w).sum() / w.sum().clamp(min=1.0)
-
-        if getattr(self.module, "is_stateful", False):
-            minibatches = self._recurrent_minibatches(b, N, T, obs, act, old_logp, adv, vt, old_logits, mask, mb,
-                                                      epochs, gen)
+        stateful = getattr(self.module, "is_stateful", False)
+        graph = None
+        if not stateful and self._ppo_graph_ok():
+            full = {"obs": obs, "act": act, "olp": old_logp, "adv": adv, "vt": vt, "olg": old_logits, "w": mask}
+            key = (n, mb, hp, self.cfg.get("grad_clip"), self._lr(),
+                   tuple((k, tuple(v.shape), v.dtype) for k, v in full.items() if v is not None))
+            if self._ppo_graph is None or self._ppo_graph.key != key:
+                self._ppo_graph = _PPOStepGraph(key, full, mb, self.device)
+            graph = self._ppo_graph
+            graph.load(full, self.kl_coeff)
+            for _ in range(epochs):
+                perm = torch.randperm(n, device=self.device, generator=gen)
+                for i in range(0, n - mb + 1, mb):
+                    graph.step(self, perm[i: i + mb], hp)
+                    count += 1
+            acc = graph.acc
         else:
-            def minibatches():
-                for _ in range(epochs):
-                    perm = torch.randperm(n, device=self.device, generator=gen)
-                    for i in range(0, n - mb + 1, mb):
-                        idx = perm[i: i + mb]
-                        logits, v = self.forward(obs[idx])
-                        yield (logits, v, act[idx], old_logp[idx], adv[idx], vt[idx],
-                               old_logits[idx] if old_logits is not None else None,
-                               mask[idx] if mask is not None else None)
-
-        for logits, v, act_mb, olp_mb, a_mb, vt_mb, olg_mb, w in minibatches():
-            d = self.module.dist(logits)
-            lp = d.logp(act_mb)
-            ratio = torch.exp(lp - olp_mb)
-            surr = torch.min(ratio * a_mb, ratio.clamp(1 - clip, 1 + clip) * a_mb)
-            vf_err = (v - vt_mb) ** 2
-            vf_loss = vf_err.clamp(0, vclip) if vclip else vf_err
-            ent = d.entropy()
-            pi_term, vf_term, ent_term = mean(surr, w), mean(vf_loss, w), mean(ent, w)
-            loss = -pi_term + vf_coeff * vf_term - ent_coeff * ent_term
-            if use_kl:
-                kl = mean(self.module.dist(olg_mb).kl(d), w)
-                if self.kl_coeff > 0:
-                    loss = loss + self.kl_coeff * kl
+            acc = torch.zeros(len(keys), device=self.device)
+            kl_t = torch.full((), self.kl_coeff, device=self.device)
+            if stateful:
+                minibatches = self._recurrent_minibatches(b, N, T, obs, act, old_logp, adv, vt, old_logits, mask,
+                                                          mb, epochs, gen)
             else:
-                kl = torch.zeros((), device=self.device)
-            self._step(loss)
-            stats["policy_loss"] += -pi_term.detach()
-            stats["vf_loss"] += vf_term.detach()
-            stats["entropy"] += ent_term.detach()
-            stats["mean_kl"] += kl.detach()
-            stats["total_loss"] += loss.detach()
-            count += 1
-        keys = list(stats)
-        vec = torch.stack([torch.as_tensor(stats[k], device=self.device, dtype=torch.float64) for k in keys])
-        vec = vec / max(count, 1)
+                def minibatches():
+                    for _ in range(epochs):
+                        perm = torch.randperm(n, device=self.device, generator=gen)
+                        for i in range(0, n - mb + 1, mb):
+                            idx = perm[i: i + mb]
+                            logits, v = self.forward(obs[idx])
+                            yield (logits, v, act[idx], old_logp[idx], adv[idx], vt[idx],
+                                   old_logits[idx] if old_logits is not None else None,
+                                   mask[idx] if mask is not None else None)
+
+            for logits, v, act_mb, olp_mb, a_mb, vt_mb, olg_mb, w in minibatches():
+                loss, st = self._ppo_loss(logits, v, act_mb, olp_mb, a_mb, vt_mb, olg_mb, w, hp, kl_t)
+                self._step(loss)
+                acc.add_(st)
+                count += 1
+        vec = acc.double() / max(count, 1)
         if self._dist_group():  # every learner adapts kl_coeff from the same group-wide KL
             import torch.distributed as dist
 
@@ -244,8 +250,43 @@ class Learner(LearnerAPI):
         self.num_updates += 1
         ev = 1 - torch.var(vt - old_vf) / (torch.var(vt) + 1e-8)
         out.update({"kl_coeff": self.kl_coeff, "vf_explained_var": float(ev), "num_minibatches": count,
-                    "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr()})
+                    "learner_time_s": time.perf_counter() - t0, "cur_lr": self._lr(),
+                    "cuda_graph_replays": graph.replays if graph is not None else 0})
         return out
+
+    def _ppo_graph_ok(self) -> bool:
+        """The PPO minibatch step runs as a captured HIP graph on a single GPU learner (DDP's
+        bucket hooks issue collectives and host-side bookkeeping a graph cannot replay) without
+        an lr schedule (its per-step lr would be baked into the graph)."""
+        return (self.device.type == "cuda" and self.ddp is None and not self.cfg.get("lr_schedule")
+                and bool(self.cfg.get("learner_cuda_graph", True)) and os.environ.get("RCA_LEARNER_GRAPH", "1") != "0"
+                and self.opt.param_groups[0].get("capturable", False))
+
+    def _ppo_loss(self, logits, v, act_mb, olp_mb, a_mb, vt_mb, olg_mb, w, hp, kl_t):
+        """Clipped-surrogate loss of one minibatch and its 5 statistics (policy_loss, vf_loss,
+        entropy, mean_kl, total_loss) as one device vector. ``kl_t``: the KL coefficient as a
+        device scalar, so a captured graph reads the current value at replay."""
+        clip, vclip, vf_coeff, ent_coeff, use_kl, kl_on = hp
+
+        def mean(x, w):
+            return x.mean() if w is None else (x * w).sum() / w.sum().clamp(min=1.0)
+
+        d = self.module.dist(logits)
+        lp = d.logp(act_mb)
+        ratio = torch.exp(lp - olp_mb)
+        surr = torch.min(ratio * a_mb, ratio.clamp(1 - clip, 1 + clip) * a_mb)
+        vf_err = (v - vt_mb) ** 2
+        vf_loss = vf_err.clamp(0, vclip) if vclip else vf_err
+        ent = d.entropy()
+        pi_term, vf_term, ent_term = mean(surr, w), mean(vf_loss, w), mean(ent, w)
+        loss = -pi_term + vf_coeff * vf_term - ent_coeff * ent_term
+        if use_kl:
+            kl = mean(self.module.dist(olg_mb).kl(d), w)
+            if kl_on:
+                loss = loss + kl_t * kl
+        else:
+            kl = torch.zeros((), device=logits.device)
+        return loss, torch.stack([-pi_term, vf_term, ent_term, kl, loss]).detach()
 
     def _recurrent_minibatches(self, b, N, T, obs, act, old_logp, adv, vt, old_logits, mask, mb, epochs, gen):
         """Recurrent PPO: the ``[N, T]`` fragments are cut into ``max_seq_len`` chunks (the tail
@@ -637,6 +678,76 @@ class Learner(LearnerAPI):
     def sync_target(self):
         if self.target is not None:
             self.target.load_state_dict(self.module.state_dict())
+
+
+class _PPOStepGraph:
+    """One PPO minibatch step -- gather the minibatch rows by index, forward, loss, backward,
+    gradient clipping, capturable Adam, statistics accumulation -- captured once as a HIP graph
+    (``torch.cuda.CUDAGraph``) and replayed for every later minibatch with the same shapes.
+
+    The eager step is launch-bound at RLlib sizes (~150 small kernels, each a Python dispatch);
+    a replay is one graph launch. The whole train batch lives in static device buffers (one copy
+    per update), the minibatch is selected by a static index buffer (the device permutation's
+    slice, copied in before each replay), the KL coefficient is a device scalar, and the running
+    statistics are a device vector the graph adds into. The first ``WARM`` minibatches run eagerly
+    on a side stream (autograd / MIOpen / Adam-state initialisation must happen outside the
+    capture; they are real training steps), the next is captured and replayed. The replayed
+    kernels are the eager ones, so the path is bitwise equal to the eager loop
+    (tests/test_rllib_learner_graph_gpu.py)."""
+
+    WARM = 2
+
+    def __init__(self, key, full, mb, device):
+        self.key = key
+        self.device = device
+        self.full = {k: torch.empty_like(v) for k, v in full.items() if v is not None}
+        self.idx = torch.zeros(mb, dtype=torch.long, device=device)
+        self.kl_t = torch.zeros((), device=device)
+        self.acc = torch.zeros(5, device=device)
+        self.graph = None
+        self.warm = 0
+        self.replays = 0
+
+    def load(self, full, kl_coeff):
+        for k, v in full.items():
+            if v is not None:
+                self.full[k].copy_(v)
+        self.kl_t.fill_(kl_coeff)
+        self.acc.zero_()
+        self.replays = 0
+
+    def _body(self, lr):
+        f, idx = self.full, self.idx
+        g = lambda k: f[k][idx] if k in f else None  # noqa: E731
+        logits, v = lr.forward(g("obs"))
+        loss, st = lr._ppo_loss(logits, v, g("act"), g("olp"), g("adv"), g("vt"), g("olg"), g("w"), self._hp,
+                                self.kl_t)
+        lr._step(loss)
+        self.acc.add_(st)
+
+    def step(self, lr, idx, hp):
+        self._hp = hp
+        self.idx.copy_(idx)
+        if self.graph is not None:
+            self.graph.replay()
+            self.replays += 1
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if self.warm < self.WARM:
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._body(lr)
+            cur.wait_stream(side)
+            self.warm += 1
+            return
+        lr.opt.zero_grad(set_to_none=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self._body(lr)
+        self.graph = graph
+        graph.replay()  # the capture recorded this minibatch's step without running it
+        self.replays += 1
 
 
 def _learner_actor_cls():

@@ -89,14 +89,16 @@ class NatureCNN(nn.Module):
         return self.net(x)
 
 
-def preprocess_obs(obs: torch.Tensor) -> torch.Tensor:
-    """uint8 [B, H, W, C] frames -> float [B, C, H, W] / 255 (one HIP kernel on GPU)."""
+def preprocess_obs(obs: torch.Tensor, channels_last: bool = False) -> torch.Tensor:
+    """uint8 [B, H, W, C] frames -> float [B, C, H, W] / 255 (one HIP kernel on GPU;
+    ``channels_last``: written in NHWC memory, what a channels-last conv stack consumes)."""
     if obs.dtype == torch.uint8 and obs.dim() == 4:
         if obs.is_cuda:
             from ...ops import image_normalize
 
             C = obs.shape[-1]
-            return image_normalize(obs, mean=(0.0,) * C, std=(1.0,) * C, dtype=torch.float32)
+            return image_normalize(obs, mean=(0.0,) * C, std=(1.0,) * C, dtype=torch.float32,
+                                   channels_last=channels_last)
         return obs.permute(0, 3, 1, 2).float().div_(255.0)
     return obs.float()
 
@@ -136,8 +138,10 @@ class RLModule(RLModuleAPI, nn.Module):
         nn.init.zeros_(self.pi.bias)
 
     def _x(self, obs):
-        x = preprocess_obs(obs)
-        return x if self.is_image else x.reshape(x.shape[0], -1)
+        if self.is_image:
+            w = self.encoder.net[0].weight  # channels-last weights: feed NHWC frames (no MIOpen transposes)
+            return preprocess_obs(obs, channels_last=w.is_cuda and w.stride(1) == 1 and w.shape[1] > 1)
+        return preprocess_obs(obs).reshape(obs.shape[0], -1)
 
     def forward(self, obs):
         x = self._x(obs)
