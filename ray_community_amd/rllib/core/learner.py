@@ -37,7 +37,8 @@ class Learner(LearnerAPI):
         if seed is not None:
             torch.manual_seed(int(seed))
         self.module = make_module(config, obs_space, act_space).to(self.device)
-        if self.device.type == "cuda" and config.get("learner_channels_last", True):
+        if (self.device.type == "cuda" and config.get("learner_channels_last", True)
+                and os.environ.get("RCA_LEARNER_NHWC", "1") != "0"):
             # NHWC conv weights (and NHWC frames from the normalize kernel, RLModule._x): MIOpen's
             # NHWC implicit-GEMM convolutions run without the NCHW<->NHWC batched transposes that
             # were ~10 % of the NatureCNN update's kernel time (scripts/learner_graph_bench.py)
