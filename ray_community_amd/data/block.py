@@ -31,9 +31,23 @@ def _is_pandas(b):
         return False
 
 
+def _is_tensor_type(t) -> bool:
+    from .extensions.tensor_extension import is_tensor_type
+
+    return is_tensor_type(t)
+
+
+def _tensor_to_numpy(col) -> np.ndarray:
+    from .extensions.tensor_extension import tensor_column_to_numpy
+
+    return tensor_column_to_numpy(col)
+
+
 def _np_col(v):
     if isinstance(v, np.ndarray):
         return v
+    if type(v).__name__ == "TensorArray":
+        return v.to_numpy()
     if isinstance(v, list):
         try:
             arr = np.asarray(v)
@@ -103,6 +117,9 @@ class BlockAccessor:
             out = {}
             for name in b.column_names:
                 col = b.column(name)
+                if _is_tensor_type(col.type):  # fixed-shape tensor column: one reshape
+                    out[name] = _tensor_to_numpy(col)
+                    continue
                 try:
                     out[name] = col.to_numpy(zero_copy_only=False)
                 except Exception:
@@ -121,22 +138,21 @@ class BlockAccessor:
         b = self.b
         if _is_arrow(b):
             return b.to_pandas()
+        from .extensions import TensorArray
+
         cols = {}
         for k, v in b.items():
-            cols[k] = list(v) if v.ndim > 1 else v
+            cols[k] = TensorArray(v) if v.ndim > 1 else v
         return pd.DataFrame(cols)
 
     def to_arrow(self):
         b = self.b
         if _is_arrow(b):
             return b
-        cols = {}
-        for k, v in b.items():
-            if v.ndim > 1:
-                cols[k] = pa.array(list(v.reshape(len(v), -1)))
-            else:
-                cols[k] = pa.array(v) if v.dtype != object else pa.array(list(v))
-        return pa.table(cols)
+        from .extensions.tensor_extension import to_tensor_block_column
+
+        # ndim > 1 columns become ArrowTensorType columns: the row shape survives Arrow / Parquet
+        return pa.table({k: to_tensor_block_column(v) for k, v in b.items()})
 
     def to_batch(self, fmt: str):
         if fmt in ("numpy", "default", None):
@@ -278,7 +294,8 @@ def normalize_block(x) -> Block:
                 return pa.Table.from_pandas(x, preserve_index=False)
             except Exception:
                 pass
-        return {c: _np_col(list(x[c])) for c in x.columns}
+        return {c: _np_col(x[c].array if type(x[c].array).__name__ == "TensorArray" else list(x[c]))
+                for c in x.columns}
     if isinstance(x, dict):
         return {str(k): _np_col(v) for k, v in x.items()}
     if isinstance(x, list):
