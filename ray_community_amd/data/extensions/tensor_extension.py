@@ -85,9 +85,9 @@ class ArrowTensorArray(pa.ExtensionArray):
         """``arr``: ``[rows, *shape]`` ndarray (or a sequence of equally shaped ndarrays)."""
         if isinstance(arr, (list, tuple)):
             arr = np.stack([np.asarray(a) for a in arr]) if len(arr) else np.empty((0,))
-        arr = np.ascontiguousarray(arr)
-        if arr.ndim == 0:
+        if np.ndim(arr) == 0:
             raise ValueError("a tensor column needs a row axis")
+        arr = np.ascontiguousarray(arr)
         shape = arr.shape[1:]
         values = pa.array(arr.reshape(-1))
         storage = pa.FixedSizeListArray.from_arrays(values, max(1, _prod(shape)))
