@@ -144,11 +144,16 @@ class _Router:
             return grpc.unary_unary_rpc_method_handler(lambda req, ctx: b"success")
         method = path.rsplit("/", 1)[-1]
         kind, deser, ser = self.proxy.methods.get(path, ("unary_unary", None, None))
+        from ..grpc_util import RayServegRPCContext, _GrpcReply
+
         if kind == "unary_stream":
             def stream(req, ctx, method=method):
-                h = self.proxy.handle_for(ctx, method).options(stream=True)
+                h = self.proxy.handle_for(ctx, method).options(stream=True, _grpc_context=RayServegRPCContext(ctx))
                 try:
                     for item in h.remote(req):
+                        if isinstance(item, _GrpcReply):  # the stream's final context
+                            item.context._apply(ctx)
+                            continue
                         yield item
                 except BackPressureError as e:
                     ctx.abort(grpc.StatusCode.UNAVAILABLE, e.message)
@@ -158,9 +163,13 @@ class _Router:
             return grpc.unary_stream_rpc_method_handler(stream, request_deserializer=deser, response_serializer=ser)
 
         def unary(req, ctx, method=method):
-            h = self.proxy.handle_for(ctx, method)
+            h = self.proxy.handle_for(ctx, method).options(_grpc_context=RayServegRPCContext(ctx))
             try:
-                return h.remote(req).result()
+                out = h.remote(req).result()
+                if isinstance(out, _GrpcReply):
+                    out.context._apply(ctx)
+                    out = out.value
+                return out
             except BackPressureError as e:
                 ctx.abort(grpc.StatusCode.UNAVAILABLE, e.message)
             except Exception as e:  # noqa

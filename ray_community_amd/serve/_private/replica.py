@@ -195,6 +195,16 @@ class ServeReplica:
             self.logger.info(f"{route} {status} {ms:.1f}ms",
                              extra={"route": route, "status": status, "latency_ms": round(ms, 3)})
 
+    def _grpc_kwargs(self, method_name, kwargs, meta):
+        """A gRPC request's context goes to user methods that declare ``grpc_context``."""
+        ctx = meta.get("grpc_context")
+        if ctx is None:
+            return kwargs
+        from ..grpc_util import _wants_context
+
+        fn = self.obj if self.is_function else getattr(self.obj, method_name or "__call__")
+        return dict(kwargs, grpc_context=ctx) if _wants_context(fn) else kwargs
+
     async def handle_request(self, method_name, args, kwargs, meta=None):
         from ..handle import _resolve_handle_args
 
@@ -209,7 +219,13 @@ class ServeReplica:
             # chained DeploymentResponses arrive as ObjectRefs: resolve them here, not in the caller
             args = tuple([(await a) if isinstance(a, ObjectRef) else a for a in args])
             kwargs = {k: ((await v) if isinstance(v, ObjectRef) else v) for k, v in kwargs.items()}
-            return await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
+            kwargs = self._grpc_kwargs(method_name, kwargs, meta)
+            out = await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
+            if meta.get("grpc_context") is not None:  # the (possibly modified) context rides back
+                from ..grpc_util import _GrpcReply
+
+                return _GrpcReply(out, kwargs.get("grpc_context", meta["grpc_context"]))
+            return out
         except BaseException:
             status = "ERROR"
             raise
@@ -229,9 +245,14 @@ class ServeReplica:
         tok = multiplex._set_model_id(meta.get("multiplexed_model_id"))
         try:
             args, kwargs = _resolve_handle_args(args, kwargs)
+            kwargs = self._grpc_kwargs(method_name, kwargs, meta)
             res = await self._invoke_user(method_name, args, kwargs)
             async for x in _aiter(res, self._user_exec):
                 yield x
+            if meta.get("grpc_context") is not None:  # last item: the context the stream left
+                from ..grpc_util import _GrpcReply
+
+                yield _GrpcReply(None, kwargs.get("grpc_context", meta["grpc_context"]))
         finally:
             multiplex._reset_model_id(tok)
             self.ongoing -= 1

@@ -494,20 +494,23 @@ class DeploymentResponseGenerator:
 
 class DeploymentHandle:
     def __init__(self, deployment_name: str, app_name: str = "default", *, method_name: str = "__call__",
-                 multiplexed_model_id: str = "", stream: bool = False):
+                 multiplexed_model_id: str = "", stream: bool = False, _grpc_context=None):
         self.deployment_name = deployment_name
         self.app_name = app_name
         self._method = method_name
         self._model_id = multiplexed_model_id
         self._stream = stream
+        self._grpc_context = _grpc_context  # set by the gRPC proxy (serve.grpc_util)
 
     def options(self, *, method_name: Optional[str] = None, multiplexed_model_id: Optional[str] = None,
-                stream: Optional[bool] = None, use_new_handle_api=None, **kw) -> "DeploymentHandle":
+                stream: Optional[bool] = None, use_new_handle_api=None, _grpc_context=None,
+                **kw) -> "DeploymentHandle":
         return DeploymentHandle(self.deployment_name, self.app_name,
                                 method_name=method_name or self._method,
                                 multiplexed_model_id=self._model_id if multiplexed_model_id is None else
                                 multiplexed_model_id,
-                                stream=self._stream if stream is None else stream)
+                                stream=self._stream if stream is None else stream,
+                                _grpc_context=self._grpc_context if _grpc_context is None else _grpc_context)
 
     def __getattr__(self, name):
         if name.startswith("_"):
@@ -519,6 +522,8 @@ class DeploymentHandle:
         args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
         kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v) for k, v in kwargs.items()}
         meta = {"multiplexed_model_id": self._model_id} if self._model_id else {}
+        if self._grpc_context is not None:
+            meta["grpc_context"] = self._grpc_context
         if self._stream:
             return DeploymentResponseGenerator(router.submit(self._method, args, kwargs, meta,
                                                              actor_method="handle_request_stream"))

@@ -109,3 +109,50 @@ def test_grpc_user_errors_are_internal(grpc_serve):
         echo(_s(msg="x"), timeout=60)
     assert ei.value.code() == grpc.StatusCode.INTERNAL and "model exploded" in ei.value.details()
     ch.close()
+
+
+def test_grpc_context_reaches_the_deployment_and_its_settings_come_back(grpc_serve):
+    """reference serve/grpc_util.py RayServegRPCContext: a method declaring ``grpc_context`` gets
+    the request's metadata and can set the status code, details and trailing metadata."""
+
+    @serve.deployment
+    class Ctx:
+        def Echo(self, req, grpc_context):
+            md = dict(grpc_context.invocation_metadata())
+            if req["msg"] == "missing":
+                grpc_context.set_code(grpc.StatusCode.NOT_FOUND)
+                grpc_context.set_details("no such item")
+                return _s()
+            grpc_context.set_trailing_metadata([("x-served-by", "ctx"), ("x-user", md.get("user", ""))])
+            return _s(msg=req["msg"], peer=grpc_context.peer())
+
+        def Count(self, req, grpc_context):
+            for i in range(2):
+                yield _s(i=i)
+            grpc_context.set_trailing_metadata([("x-count", "2")])
+
+    serve.run(Ctx.bind(), name="c", route_prefix=None)
+    ch = grpc.insecure_channel(f"127.0.0.1:{grpc_serve}")
+    echo = ch.unary_unary("/test.Echo/Echo", request_serializer=Struct.SerializeToString,
+                          response_deserializer=Struct.FromString)
+    resp, call = echo.with_call(_s(msg="hi"), metadata=(("user", "ann"),), timeout=60)
+    assert resp["msg"] == "hi" and resp["peer"]
+    assert dict(call.trailing_metadata())["x-served-by"] == "ctx"
+    assert dict(call.trailing_metadata())["x-user"] == "ann"
+    with pytest.raises(grpc.RpcError) as e:
+        echo(_s(msg="missing"), timeout=60)
+    assert e.value.code() == grpc.StatusCode.NOT_FOUND and e.value.details() == "no such item"
+    count = ch.unary_stream("/test.Echo/Count", request_serializer=Struct.SerializeToString,
+                            response_deserializer=Struct.FromString)
+    it = count(_s(), timeout=60)
+    assert [int(m["i"]) for m in it] == [0, 1]
+    assert dict(it.trailing_metadata())["x-count"] == "2"
+
+    # a plain handle call (no gRPC request) never sees a context
+    @serve.deployment
+    class Plain:
+        def __call__(self, x):
+            return x + 1
+
+    h = serve.run(Plain.bind(), name="p", route_prefix=None)
+    assert h.remote(1).result() == 2
