@@ -75,6 +75,37 @@ def error_desc(err: BaseException):
 
 
 # ====================================================================== caller-owned objects
+class _Latch:
+    """One-shot event on a bare C lock (``threading.Event`` is a Python Condition: a lock
+    allocation and list juggling per wait) -- the wake-up a blocked ``get`` waits on."""
+
+    __slots__ = ("_l", "_set")
+
+    def __init__(self):
+        self._l = threading.Lock()
+        self._l.acquire()
+        self._set = False
+
+    def set(self):
+        if not self._set:
+            self._set = True
+            try:
+                self._l.release()
+            except RuntimeError:  # a concurrent set() released it first
+                pass
+
+    def is_set(self) -> bool:
+        return self._set
+
+    def wait(self, timeout=None) -> bool:
+        if self._set:
+            return True
+        if self._l.acquire(timeout=-1 if timeout is None else max(0.0, timeout)):
+            self._l.release()  # stays set for any later waiter
+            return True
+        return self._set
+
+
 class _Owned:
     __slots__ = ("desc", "callbacks", "published", "tid", "channel", "dropped")
 
@@ -183,7 +214,7 @@ class OwnedTable:
     def _arm(self, oids, need):
         """Event set once ``need`` of ``oids`` (the ones still pending) have results. Counted
         per-object callbacks, so a getter of N refs costs O(N), not O(N) per arriving result."""
-        ev = threading.Event()
+        ev = _Latch()
         lock = threading.Lock()
         left = [need]
 

@@ -86,7 +86,7 @@ class Worker:
         self.group_sems = {}
         env = os.environ
         self.wid = bytes.fromhex(env["RCA_WORKER_ID"])
-        self.inbox: "queue.Queue" = queue.Queue()
+        self.inbox: "queue.SimpleQueue" = queue.SimpleQueue()  # C-level put/get: the actor-call hand-off
         self.functions = {}
         self.actor = None
         self._value_keepalive = {}
