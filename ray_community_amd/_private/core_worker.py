@@ -732,7 +732,8 @@ class CoreWorker:
         # Only a weak reference to that list is cached: a caller that drops ``rest`` must release
         # its refs (free-on-last-ref), not have them pinned here until the next wait().
         last = self._wait_rest
-        if (num_returns == 1 and last is not None and refs is last[0]() and len(refs) == last[1] and refs):
+        same = (num_returns == 1 and last is not None and refs is last[0]() and len(refs) == last[1] and refs)
+        if same:
             e = self.owned.objs.get(refs[0]._id)
             if e is not None and e.desc is not None:
                 rest = _RefList(refs[1:])
@@ -742,15 +743,18 @@ class CoreWorker:
         refs = list(refs)
         ids = list(map(_REF_ID, refs))  # C-level pass (wait() is called once per completion when polling)
         self._raise_put_errors(ids)
-        sids = set(ids)
-        if len(sids) != len(ids):
-            raise ValueError("Wait requires a list of unique object refs.")
-        if num_returns <= 0:
-            raise ValueError("Invalid number of objects to return %d." % num_returns)
-        if num_returns > len(refs):
-            raise ValueError("num_returns cannot be greater than the number of objects provided.")
         owned = self.owned.objs
-        if sids <= owned.keys():
+        if same:  # the unchanged remainder of an earlier wait: unique and all owned here already
+            sids = None
+        else:
+            sids = set(ids)
+            if len(sids) != len(ids):
+                raise ValueError("Wait requires a list of unique object refs.")
+            if num_returns <= 0:
+                raise ValueError("Invalid number of objects to return %d." % num_returns)
+            if num_returns > len(refs):
+                raise ValueError("num_returns cannot be greater than the number of objects provided.")
+        if sids is None or sids <= owned.keys():
             deadline = None if timeout is None else time.monotonic() + timeout
             got = self.owned.wait_ready(ids, num_returns, deadline)
         else:
@@ -776,7 +780,7 @@ class CoreWorker:
                 not_ready.extend(refs[prev:i])
                 prev = i + 1
             not_ready.extend(refs[prev:])
-            if sids <= owned.keys():
+            if sids is None or sids <= owned.keys():
                 self._wait_rest = (weakref.ref(not_ready), len(not_ready))
             return ready, not_ready
         rs = set(got)

@@ -288,7 +288,16 @@ class OwnedTable:
                     self.waiters.remove(w)
                 except ValueError:
                     pass
-        return [o for o in oids if (o not in objs) or objs[o].desc is not None]
+        # in list order; once enough are ready the rest of the list is not looked at (the caller
+        # keeps the first ``num_returns``)
+        out = []
+        for o in oids:
+            e = objs.get(o)
+            if e is None or e.desc is not None:
+                out.append(o)
+                if len(out) >= num_returns:
+                    break
+        return out
 
 
 # ====================================================================== caller side
