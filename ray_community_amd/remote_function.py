@@ -5,9 +5,21 @@ import functools
 import inspect
 from typing import Any, Dict, Optional
 
+from ._private import core_worker as _cw
 from ._private import serialization as ser
 from ._private.core_worker import ObjectRef, ObjectRefGenerator
 from ._private.ids import new_id, return_ids
+
+_WORKER = None  # ._private.worker, bound on first use (it imports this module): no per-call import
+
+
+def _worker_mod():
+    global _WORKER
+    if _WORKER is None:
+        from ._private import worker
+
+        _WORKER = worker
+    return _WORKER
 
 _TASK_OPTIONS = {"num_cpus", "num_gpus", "memory", "resources", "accelerator_type", "num_returns", "max_retries",
                  "retry_exceptions", "scheduling_strategy", "runtime_env", "name", "max_calls", "placement_group",
@@ -35,9 +47,7 @@ def build_resources(opts: dict, default_cpus: float) -> Dict[str, float]:
 
 
 def _default_strategy():
-    from ._private import core_worker
-
-    core = core_worker._core
+    core = _cw._core
     return getattr(core.ctx, "capture_pg", None) if core is not None else None
 
 
@@ -82,9 +92,7 @@ def build_strategy(opts: dict):
 
 
 def _merge_runtime_env(opts):
-    from ._private.worker import _state
-
-    job_env = _state.get("runtime_env") or {}
+    job_env = _worker_mod()._state.get("runtime_env") or {}
     if not job_env and not opts.get("runtime_env"):
         return None
     from .runtime_env import validate
@@ -164,9 +172,7 @@ class RemoteFunction:
         return FunctionNode(self, args, kwargs, self._options)
 
     def _remote(self, args, kwargs, opts):
-        from ._private.worker import _core
-
-        core = _core()
+        core = _worker_mod()._core()
         fid = self._ensure_exported(core)
         num_returns = opts.get("num_returns", 1)
         generator = None
