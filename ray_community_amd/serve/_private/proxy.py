@@ -92,9 +92,13 @@ class HTTPProxy:
     def _run(self):
         import uvicorn
 
+        from .ws_protocol import RFC6455Protocol
+
+        # WebSocket upgrades go to the in-tree RFC 6455 protocol (uvicorn's own backends need the
+        # websockets / wsproto packages)
         config = uvicorn.Config(self._app, host=self.host, port=self.port, log_level="warning", lifespan="off",
                                 interface="asgi3", timeout_keep_alive=self.keep_alive_timeout_s,
-                                root_path=self.root_path)
+                                root_path=self.root_path, ws=RFC6455Protocol)
         self._server = uvicorn.Server(config)
         # our own loop (not uvicorn's asyncio.run) so replicas' receive_asgi_messages pulls and
         # run_asgi_session can schedule onto it from other threads

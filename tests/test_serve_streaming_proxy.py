@@ -139,3 +139,112 @@ def test_websocket_echo_session_through_proxy_app(serve_instance):
     # no route: the handshake is refused with a close
     sent = ray.get(_proxy().run_asgi_session.remote(dict(scope, path="/nope/ws"), [{"type": "websocket.connect"}]))
     assert sent == [{"type": "websocket.close", "code": 1000}] or sent[0]["type"] == "websocket.close"
+
+
+def _ws_connect(path, protocols=None):
+    """A minimal RFC 6455 client over a raw socket (no websocket client library is installed)."""
+    import base64
+    import os
+    import socket
+
+    from ray_community_amd.serve._private.ws_protocol import FrameParser, accept_key
+
+    s = socket.create_connection(("127.0.0.1", PORT), timeout=60)
+    key = base64.b64encode(os.urandom(16))
+    req = (f"GET {path} HTTP/1.1\r\nHost: 127.0.0.1:{PORT}\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+           f"Sec-WebSocket-Key: {key.decode()}\r\nSec-WebSocket-Version: 13\r\n")
+    if protocols:
+        req += f"Sec-WebSocket-Protocol: {', '.join(protocols)}\r\n"
+    s.sendall((req + "\r\n").encode())
+    head = b""
+    while b"\r\n\r\n" not in head:
+        chunk = s.recv(4096)
+        if not chunk:
+            break
+        head += chunk
+    status_line, _, rest = head.partition(b"\r\n")
+    hdrs, _, extra = rest.partition(b"\r\n\r\n")
+    return s, status_line, hdrs, extra, key, FrameParser(require_mask=False), accept_key
+
+
+def _ws_send(s, op, payload, fin=True):
+    import os
+
+    from ray_community_amd.serve._private.ws_protocol import encode_frame
+
+    s.sendall(encode_frame(op, payload, fin=fin, mask=os.urandom(4)))
+
+
+def _ws_recv(s, parser, pending):
+    while not pending:
+        data = s.recv(65536)
+        if not data:
+            return None
+        pending.extend(parser.feed(data))
+    return pending.pop(0)
+
+
+def test_websocket_over_a_real_socket(serve_instance):
+    """End to end: RFC 6455 handshake and framing in the proxy (serve/_private/ws_protocol.py),
+    the session routed to a FastAPI ``@app.websocket`` ingress."""
+    from fastapi import FastAPI, WebSocket, WebSocketDisconnect
+
+    app = FastAPI()
+
+    @serve.deployment
+    @serve.ingress(app)
+    class Echo:
+        @app.websocket("/ws")
+        async def ws(self, websocket: WebSocket):
+            await websocket.accept(subprotocol="chat" if "chat" in websocket.scope.get("subprotocols", []) else None)
+            try:
+                while True:
+                    msg = await websocket.receive()
+                    if msg["type"] == "websocket.disconnect":
+                        return
+                    if msg.get("bytes") is not None:
+                        await websocket.send_bytes(msg["bytes"][::-1])
+                    else:
+                        await websocket.send_text("echo:" + msg["text"])
+                        if msg["text"] == "bye":
+                            await websocket.close(code=4000)
+                            return
+            except WebSocketDisconnect:
+                return
+
+    serve.run(Echo.bind(), route_prefix="/chat")
+    s, status, hdrs, extra, key, parser, accept_key = _ws_connect("/chat/ws", protocols=["chat"])
+    assert status.startswith(b"HTTP/1.1 101"), status
+    h = dict(l.split(b": ", 1) for l in hdrs.split(b"\r\n") if b": " in l)
+    h = {k.lower(): v for k, v in h.items()}
+    assert h[b"sec-websocket-accept"] == accept_key(key) and h[b"sec-websocket-protocol"] == b"chat"
+    pending = parser.feed(extra) if extra else []
+    _ws_send(s, 0x1, b"hello")
+    assert _ws_recv(s, parser, pending) == (True, 0x1, b"echo:hello")
+    _ws_send(s, 0x2, bytes(range(200)) * 400)  # 80 KB binary: 64-bit length field both ways
+    fin, op, data = _ws_recv(s, parser, pending)
+    assert op == 0x2 and data == (bytes(range(200)) * 400)[::-1]
+    _ws_send(s, 0x1, b"frag", fin=False)  # a fragmented text message
+    _ws_send(s, 0x0, b"mented", fin=True)
+    assert _ws_recv(s, parser, pending)[2] == b"echo:fragmented"
+    _ws_send(s, 0x9, b"ping!")
+    assert _ws_recv(s, parser, pending) == (True, 0xA, b"ping!")
+    _ws_send(s, 0x1, b"bye")
+    assert _ws_recv(s, parser, pending)[2] == b"echo:bye"
+    fin, op, data = _ws_recv(s, parser, pending)
+    assert op == 0x8 and int.from_bytes(data[:2], "big") == 4000
+    s.close()
+
+    # client-initiated close: the app sees the disconnect, the proxy echoes the close frame
+    s, status, _h, extra, _k, parser, _a = _ws_connect("/chat/ws")
+    assert status.startswith(b"HTTP/1.1 101")
+    pending = parser.feed(extra) if extra else []
+    _ws_send(s, 0x8, (1000).to_bytes(2, "big"))
+    fin, op, data = _ws_recv(s, parser, pending)
+    assert op == 0x8 and int.from_bytes(data[:2], "big") == 1000
+    s.close()
+
+    # no such route: the handshake is refused
+    s, status, *_ = _ws_connect("/nowhere/ws")
+    assert status.startswith(b"HTTP/1.1 403"), status
+    s.close()
