@@ -1,9 +1,9 @@
 """Serve proxy: request bodies streamed to the replica as the app consumes them, and WebSocket
 sessions (reference python/ray/serve/_private/proxy.py:430,856-1103 receive_asgi_messages;
-tests/test_streaming_response.py, test_websockets.py). uvicorn's WebSocket backends
-(websockets / wsproto) are not installed here, so WebSocket sessions are driven through the
-proxy's ASGI app with a scripted client (``HTTPProxy.run_asgi_session``) -- the same ``_app``
-uvicorn calls; the end-to-end WebSocket socket path stays unpinned."""
+tests/test_streaming_response.py, test_websockets.py). WebSocket sessions are driven two ways: through the proxy's ASGI app with
+a scripted client (``HTTPProxy.run_asgi_session``), and end to end over a raw socket with a
+minimal RFC 6455 client against the proxy's own protocol (``serve/_private/ws_protocol.py``;
+uvicorn's websockets / wsproto backends are not installed here)."""
 import hashlib
 
 import pytest
