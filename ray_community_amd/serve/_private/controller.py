@@ -155,7 +155,8 @@ class ServeController:
             st.nodes[tag] = node
         cls = ActorClass(ServeReplica, opts)
         r = cls.remote(st.app, st.name, tag, spec["body"], spec["init_args"], spec["init_kwargs"],
-                       spec.get("user_config"), spec["is_function"], logging_config=spec.get("logging_config"))
+                       spec.get("user_config"), spec["is_function"], logging_config=spec.get("logging_config"),
+                       max_ongoing_requests=mc)
         st.replicas[tag] = r
         self._bump(st)
         asyncio.ensure_future(self._fetch_location(st, tag, r))

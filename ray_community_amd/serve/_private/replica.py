@@ -106,7 +106,8 @@ def configure_replica_logging(logging_config: Optional[Dict], app_name: str, dep
 
 class ServeReplica:
     def __init__(self, app_name: str, deployment_name: str, replica_tag: str, body_blob: bytes, init_args, init_kwargs,
-                 user_config=None, is_function: bool = False, logging_config: Optional[Dict] = None):
+                 user_config=None, is_function: bool = False, logging_config: Optional[Dict] = None,
+                 max_ongoing_requests: Optional[int] = None):
         from ..._private import serialization as ser
         from ..handle import _resolve_handle_args
 
@@ -138,8 +139,38 @@ class ServeReplica:
         self.ongoing = 0
         self.total = 0
         self.started = time.time()
+        # hard cap on user requests running at once (the actor's max_concurrency leaves headroom
+        # for control calls): routers in other processes can over-commit on stale queue lengths,
+        # so the excess waits here instead of running (reference: replica-side max_ongoing_requests)
+        self.max_ongoing = int(max_ongoing_requests) if max_ongoing_requests else None
+        self._slots = None
+        self.peak_running = 0
+        self._running = 0
         if user_config is not None:
             self._user_exec.submit(self._reconfigure_sync, user_config).result()
+
+    def _slot(self):
+        """Async context manager holding one of the replica's ``max_ongoing_requests`` slots."""
+        import contextlib
+
+        if self.max_ongoing is None:
+            return contextlib.nullcontext()
+        if self._slots is None:
+            self._slots = asyncio.Semaphore(self.max_ongoing)
+        replica = self
+
+        class _Held:
+            async def __aenter__(self):
+                await replica._slots.acquire()
+                replica._running += 1
+                replica.peak_running = max(replica.peak_running, replica._running)
+
+            async def __aexit__(self, *exc):
+                replica._running -= 1
+                replica._slots.release()
+                return False
+
+        return _Held()
 
     def _reconfigure_sync(self, user_config):
         fn = getattr(self.obj, "reconfigure", None)
@@ -220,7 +251,8 @@ class ServeReplica:
             args = tuple([(await a) if isinstance(a, ObjectRef) else a for a in args])
             kwargs = {k: ((await v) if isinstance(v, ObjectRef) else v) for k, v in kwargs.items()}
             kwargs = self._grpc_kwargs(method_name, kwargs, meta)
-            out = await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
+            async with self._slot():
+                out = await self._call_user(method_name, args, kwargs, meta.get("multiplexed_model_id"))
             if meta.get("grpc_context") is not None:  # the (possibly modified) context rides back
                 from ..grpc_util import _GrpcReply
 
@@ -246,9 +278,10 @@ class ServeReplica:
         try:
             args, kwargs = _resolve_handle_args(args, kwargs)
             kwargs = self._grpc_kwargs(method_name, kwargs, meta)
-            res = await self._invoke_user(method_name, args, kwargs)
-            async for x in _aiter(res, self._user_exec):
-                yield x
+            async with self._slot():
+                res = await self._invoke_user(method_name, args, kwargs)
+                async for x in _aiter(res, self._user_exec):
+                    yield x
             if meta.get("grpc_context") is not None:  # last item: the context the stream left
                 from ..grpc_util import _GrpcReply
 
@@ -265,8 +298,9 @@ class ServeReplica:
         try:
             from .http_util import stream_asgi_or_call
 
-            async for msg in stream_asgi_or_call(self, req):
-                yield msg
+            async with self._slot():
+                async for msg in stream_asgi_or_call(self, req):
+                    yield msg
         finally:
             self.ongoing -= 1
 
@@ -278,7 +312,8 @@ class ServeReplica:
         try:
             from .http_util import run_asgi_or_call
 
-            out = await run_asgi_or_call(self, req)
+            async with self._slot():
+                out = await run_asgi_or_call(self, req)
             status = out[0] if isinstance(out, tuple) and out else 200
             return out
         finally:

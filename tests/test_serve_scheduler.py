@@ -111,3 +111,44 @@ def test_gpu_tensor_request_prefers_replica_on_same_gpu(monkeypatch):
     assert set(picks) == {"a", "b"}  # this node's replicas first, until both are full (4 + 4)
     with r.cv:
         assert r._pick_locked(None)[0] == "c"  # then the other node
+
+
+def test_replica_enforces_max_ongoing_requests_against_overcommitting_routers(serve_instance):
+    """Routers in different processes decide on cached queue lengths and can send a replica more
+    than ``max_ongoing_requests`` at once; the replica runs at most that many and queues the rest."""
+
+    @serve.deployment(num_replicas=1, max_ongoing_requests=2)
+    class Slow:
+        def __init__(self):
+            self.active = 0
+            self.peak = 0
+
+        async def __call__(self, s):
+            import asyncio
+
+            self.active += 1
+            self.peak = max(self.peak, self.active)
+            await asyncio.sleep(s)
+            self.active -= 1
+            return True
+
+        async def peak_active(self):
+            return self.peak
+
+    serve.run(Slow.bind(), name="cap", route_prefix="/cap")
+
+    @ray.remote(num_cpus=0)
+    class Caller:
+        def __init__(self):
+            self.h = serve.get_deployment_handle("Slow", app_name="cap")
+
+        def burst(self, n, s):
+            return [r.result() for r in [self.h.remote(s) for _ in range(n)]]
+
+    callers = [Caller.remote() for _ in range(5)]
+    t0 = time.time()
+    out = ray.get([c.burst.remote(2, 0.5) for c in callers])
+    assert all(all(x) for x in out)
+    h = serve.get_deployment_handle("Slow", app_name="cap")
+    assert h.peak_active.remote().result() <= 2
+    assert time.time() - t0 >= 0.5 * 10 / 2 * 0.9  # 10 requests, 2 at a time
