@@ -143,6 +143,8 @@ class ServeReplica:
         # for control calls): routers in other processes can over-commit on stale queue lengths,
         # so the excess waits here instead of running (reference: replica-side max_ongoing_requests)
         self.max_ongoing = int(max_ongoing_requests) if max_ongoing_requests else None
+        if os.environ.get("RCA_SERVE_REPLICA_CAP", "1") == "0":  # A/B switch: router-side limits only
+            self.max_ongoing = None
         self._slots = None
         self.peak_running = 0
         self._running = 0
