@@ -21,4 +21,11 @@ def set_resource(resource_name: str, capacity: float, node_id=None):
                              "start time with the 'resources' field in the cluster autoscaler.")
 
 
-__all__ = ["get_object_locations", "set_resource"]
+def load_package(config_path: str):
+    """A code package with its own runtime environment (``experimental/packaging``)."""
+    from .packaging import load_package as _load
+
+    return _load(config_path)
+
+
+__all__ = ["get_object_locations", "set_resource", "load_package"]
