@@ -14,6 +14,24 @@ import numpy as np
 from .block import BlockAccessor, concat_blocks
 
 
+class _IterableFromIterator:
+    """What ``iter_batches`` / ``iter_torch_batches`` return: iterable any number of times (each
+    ``iter()`` runs a fresh pass -- an epoch, for a training loop or a framework's data loader
+    that re-iterates), and still an iterator itself (``next()`` draws from one lazily started pass)."""
+
+    def __init__(self, make):
+        self._make = make
+        self._it = None
+
+    def __iter__(self):
+        return self._make()
+
+    def __next__(self):
+        if self._it is None:
+            self._it = self._make()
+        return next(self._it)
+
+
 class DataIterator:
     def __init__(self, ds):
         self._ds = ds
@@ -34,10 +52,16 @@ class DataIterator:
                 return
             yield get(q.popleft())
 
-    def iter_batches(self, *, prefetch_batches: int = 1, batch_size: Optional[int] = 256,
-                     batch_format: Optional[str] = "default", drop_last: bool = False,
-                     local_shuffle_buffer_size: Optional[int] = None, local_shuffle_seed: Optional[int] = None,
-                     _collate_fn=None) -> Iterator:
+    def iter_batches(self, **kw) -> Iterator:
+        return _IterableFromIterator(lambda: self._iter_batches(**kw))
+
+    def iter_torch_batches(self, **kw) -> Iterator:
+        return _IterableFromIterator(lambda: self._iter_torch_batches(**kw))
+
+    def _iter_batches(self, *, prefetch_batches: int = 1, batch_size: Optional[int] = 256,
+                      batch_format: Optional[str] = "default", drop_last: bool = False,
+                      local_shuffle_buffer_size: Optional[int] = None, local_shuffle_seed: Optional[int] = None,
+                      _collate_fn=None) -> Iterator:
         rng = np.random.default_rng(local_shuffle_seed)
         buf = []
         buf_rows = 0
@@ -78,10 +102,10 @@ class DataIterator:
         for blk in self._blocks(prefetch_batches):
             yield from BlockAccessor(blk).iter_rows()
 
-    def iter_torch_batches(self, *, prefetch_batches: int = 1, batch_size: Optional[int] = 256,
-                           dtypes=None, device: str = "auto", collate_fn: Optional[Callable] = None,
-                           drop_last: bool = False, local_shuffle_buffer_size=None, local_shuffle_seed=None,
-                           pin_memory: bool = True) -> Iterator:
+    def _iter_torch_batches(self, *, prefetch_batches: int = 1, batch_size: Optional[int] = 256,
+                            dtypes=None, device: str = "auto", collate_fn: Optional[Callable] = None,
+                            drop_last: bool = False, local_shuffle_buffer_size=None, local_shuffle_seed=None,
+                            pin_memory: bool = True) -> Iterator:
         import torch
 
         if device == "auto":
@@ -90,7 +114,7 @@ class DataIterator:
             dev = get_device() if torch.cuda.is_available() else torch.device("cpu")
         else:
             dev = torch.device(device) if device is not None else torch.device("cpu")
-        for b in self.iter_batches(prefetch_batches=prefetch_batches, batch_size=batch_size, batch_format="numpy",
+        for b in self._iter_batches(prefetch_batches=prefetch_batches, batch_size=batch_size, batch_format="numpy",
                                    drop_last=drop_last, local_shuffle_buffer_size=local_shuffle_buffer_size,
                                    local_shuffle_seed=local_shuffle_seed):
             if collate_fn is not None:

@@ -1,90 +1,95 @@
-"""``transformers.Trainer`` inside a Train worker (reference:
+"""``transformers.Trainer`` inside Ray Train workers (reference:
 ``python/ray/train/huggingface/transformers/_transformers_utils.py``).
 
-Run a normal ``transformers.Trainer`` in the ``train_loop_per_worker`` of a ``TorchTrainer``: the
-worker group has already initialised ``torch.distributed`` (RCCL on GPUs, gloo on CPU) and set
-``RANK/LOCAL_RANK/WORLD_SIZE``, so the Trainer runs data-parallel across the workers.
-``RayTrainReportCallback`` forwards every save (metrics + checkpoint directory) to
-``train.report``; ``prepare_trainer`` makes Trainer consume Data iterators from
-``train.get_dataset_shard``.
+* ``RayTrainReportCallback``: after every checkpoint the HF Trainer saves, report the merged log
+  history as metrics together with a copy of that checkpoint (under ``checkpoint/`` in the Ray
+  Train checkpoint directory), so ``RunConfig`` / ``CheckpointConfig`` keep and rank them;
+* ``prepare_trainer``: let the Trainer consume Ray Data shards directly -- a dataset given as
+  ``get_dataset_shard(...).iter_torch_batches(...)`` (already batched, re-iterable per epoch) is
+  served by a pass-through DataLoader instead of HF's sampler / collator.
+
+The process group is the one ``TorchTrainer`` set up (RCCL on GPUs, gloo on CPU): the HF Trainer
+finds ``torch.distributed`` initialised and uses it.
 """
 from __future__ import annotations
 
 import os
 import shutil
 import tempfile
-from typing import Iterator
+from typing import Optional
 
-from transformers.trainer_callback import TrainerCallback
-
-CHECKPOINT_DIR_NAME = "checkpoint"
+try:
+    import transformers
+    from transformers.trainer_callback import TrainerCallback
+    _IMPORT_ERROR: Optional[ImportError] = None
+except ImportError as e:  # pragma: no cover - transformers is optional
+    transformers = None
+    TrainerCallback = object
+    _IMPORT_ERROR = e
 
 
 class RayTrainReportCallback(TrainerCallback):
-    CHECKPOINT_NAME = CHECKPOINT_DIR_NAME
-
-    def __init__(self, *args, **kwargs):
-        super().__init__()
-        self._last_logs = {}
-
-    def on_log(self, args, state, control, logs=None, **kwargs):
-        if logs:
-            self._last_logs.update({k: v for k, v in logs.items() if isinstance(v, (int, float))})
+    CHECKPOINT_NAME = "checkpoint"
 
     def on_save(self, args, state, control, **kwargs):
         from ... import Checkpoint, report
+        from transformers.trainer_utils import get_last_checkpoint
 
-        metrics = dict(self._last_logs)
-        for log in state.log_history:
-            metrics.update({k: v for k, v in log.items() if isinstance(v, (int, float))})
-        metrics["step"] = state.global_step
-        metrics["epoch"] = state.epoch
-        src = os.path.join(args.output_dir, f"checkpoint-{state.global_step}")
+        metrics = {}
+        for entry in state.log_history:  # later entries win (the latest loss / eval metrics)
+            metrics.update(entry)
+        metrics.setdefault("step", state.global_step)
+        metrics.setdefault("epoch", state.epoch)
+        src = get_last_checkpoint(args.output_dir) if os.path.isdir(args.output_dir) else None
+        if src is None:
+            report(metrics)
+            return
         with tempfile.TemporaryDirectory() as tmp:
-            ckpt = None
-            if os.path.isdir(src):
-                dst = os.path.join(tmp, self.CHECKPOINT_NAME)
-                shutil.copytree(src, dst)
-                ckpt = Checkpoint.from_directory(dst)
-            report(metrics, checkpoint=ckpt)
+            shutil.copytree(src, os.path.join(tmp, self.CHECKPOINT_NAME))
+            report(metrics, checkpoint=Checkpoint.from_directory(tmp))
 
 
-class RayTorchIterableDataset:
-    """Wraps a Data iterator (``iter_torch_batches`` / ``iter_rows``) as a torch IterableDataset."""
+def _is_ray_iterable(ds) -> bool:
+    from ....data.iterator import _IterableFromIterator
 
-    def __init__(self, data_iterable) -> None:
-        from torch.utils.data import IterableDataset
-
-        self._it = data_iterable
-        self.__class__ = type("RayTorchIterableDataset", (RayTorchIterableDataset, IterableDataset), {})
-
-    def __iter__(self) -> Iterator:
-        return iter(self._it)
+    return isinstance(ds, _IterableFromIterator)
 
 
 def prepare_trainer(trainer):
-    """Let ``trainer`` take framework Data iterators (from ``get_dataset_shard``) as datasets."""
-    from torch.utils.data import DataLoader
+    """Return ``trainer`` (same object) with data loaders that accept Ray Data iterables."""
+    if _IMPORT_ERROR is not None:
+        raise _IMPORT_ERROR
+    from torch.utils.data import DataLoader, IterableDataset
 
-    base = trainer.__class__
+    class _Batches(IterableDataset):
+        def __init__(self, it):
+            super().__init__()
+            self.it = it
 
-    class _RayTrainer(base):
+        def __iter__(self):
+            return iter(self.it)
+
+    def _loader(ds):
+        # batches arrive formed: a batch_size=1 loader that unwraps them
+        return DataLoader(_Batches(ds), batch_size=1, collate_fn=lambda items: items[0])
+
+    base = type(trainer)
+
+    class RayTransformersTrainer(base):
         def get_train_dataloader(self):
-            ds = self.train_dataset
-            if hasattr(ds, "iter_torch_batches"):
-                it = ds.iter_torch_batches(batch_size=self.args.per_device_train_batch_size)
-                return DataLoader(RayTorchIterableDataset(it), batch_size=None)
+            if _is_ray_iterable(self.train_dataset):
+                return _loader(self.train_dataset)
             return super().get_train_dataloader()
 
         def get_eval_dataloader(self, eval_dataset=None):
-            ds = eval_dataset if eval_dataset is not None else self.eval_dataset
-            if hasattr(ds, "iter_torch_batches"):
-                it = ds.iter_torch_batches(batch_size=self.args.per_device_eval_batch_size)
-                return DataLoader(RayTorchIterableDataset(it), batch_size=None)
+            ds = self.eval_dataset if eval_dataset is None else eval_dataset
+            if _is_ray_iterable(ds):
+                return _loader(ds)
             return super().get_eval_dataloader(eval_dataset)
 
-    trainer.__class__ = _RayTrainer
+    RayTransformersTrainer.__name__ = f"Ray{base.__name__}"
+    trainer.__class__ = RayTransformersTrainer
     return trainer
 
 
-__all__ = ["RayTrainReportCallback", "prepare_trainer", "RayTorchIterableDataset"]
+__all__ = ["RayTrainReportCallback", "prepare_trainer"]
