@@ -24,6 +24,7 @@ model in ``torch.nn.parallel.DistributedDataParallel``. Here DDP is the framewor
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 from typing import List, Optional
 
@@ -33,6 +34,11 @@ import torch.nn as nn
 
 from .. import ops
 from .flat import FlatParameters, register_grad_ready
+
+
+def _grad_ready_noop(p):
+    """World-1 ``_rca_grad_ready``: nothing to reduce; its presence lets fused kernels write the
+    gradient into the flat buffer."""
 
 
 class CommWaitTimer:
@@ -111,11 +117,18 @@ class DistributedDataParallel(nn.Module):
             if broadcast_buffers:
                 for b in module.buffers():
                     dist.broadcast(b, src=src, group=process_group)
-        # always: besides bucket bookkeeping, the hooks install ``p._rca_grad_ready``, which the fused
-        # backward kernels (RMSNorm weight column sums, the embedding's unique-row scatter) need to
-        # write straight into the flat buffer; without it they fall back to a dense dW + an
-        # AccumulateGrad add per parameter (67 extra add kernels, 0.9 ms per 8B step)
-        self._hooks += register_grad_ready(self.flat.params, self._on_grad)
+        # ``p._rca_grad_ready`` must exist at every world size: the fused backward kernels (RMSNorm
+        # weight column sums, the embedding's unique-row scatter, the fused-wgrad linears) write
+        # straight into the flat buffer only when it does; without it they fall back to a dense dW
+        # + an AccumulateGrad add per parameter (67 extra add kernels, 0.9 ms per 8B step). The
+        # per-parameter post-accumulate hooks (bucket counting -> collectives / side-stream norm)
+        # only have work with a peer to reduce with or the side-stream norm: at world 1 a no-op
+        # callback is installed instead (RCA_DDP_WORLD1_HOOKS=1 keeps the hooks, for A/Bs).
+        if self.world > 1 or self._norm is not None or os.environ.get("RCA_DDP_WORLD1_HOOKS") == "1":
+            self._hooks += register_grad_ready(self.flat.params, self._on_grad)
+        else:
+            for p in self.flat.params:
+                p._rca_grad_ready = _grad_ready_noop
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
