@@ -17,6 +17,7 @@ from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 import numpy as np
 
 from ..block import BlockAccessor, concat_blocks, normalize_block
+from ..exceptions import call_user_fn
 
 
 def _meta(block) -> Dict:
@@ -40,21 +41,21 @@ def _apply_map_op(block, op) -> List:
         step = n if bs in (None, "default") or bs <= 0 else bs
         for s in range(0, n, step):
             batch = BlockAccessor(acc.slice(s, min(n, s + step))).to_batch(fmt)
-            res = fn(batch, *op.get("fn_args", ()), **op.get("fn_kwargs", {}))
+            res = call_user_fn(fn, batch, *op.get("fn_args", ()), **op.get("fn_kwargs", {}))
             if hasattr(res, "__next__") and not isinstance(res, dict):
                 outs.extend(normalize_block(r) for r in res)
             else:
                 outs.append(normalize_block(res))
         return outs
     if kind == "map":
-        rows = [fn(r, *op.get("fn_args", ()), **op.get("fn_kwargs", {})) for r in acc.iter_rows()]
+        rows = [call_user_fn(fn, r, *op.get("fn_args", ()), **op.get("fn_kwargs", {})) for r in acc.iter_rows()]
         from ..block import rows_to_block
 
         return [rows_to_block(rows)]
     if kind == "flat_map":
         rows = []
         for r in acc.iter_rows():
-            rows.extend(fn(r, *op.get("fn_args", ()), **op.get("fn_kwargs", {})))
+            rows.extend(call_user_fn(fn, r, *op.get("fn_args", ()), **op.get("fn_kwargs", {})))
         from ..block import rows_to_block
 
         return [rows_to_block(rows)]
@@ -64,11 +65,11 @@ def _apply_map_op(block, op) -> List:
 
             df = acc.to_pandas()
             return [normalize_block(df.query(op["expr"]))]
-        mask = np.array([bool(fn(r)) for r in acc.iter_rows()], dtype=bool)
+        mask = np.array([bool(call_user_fn(fn, r)) for r in acc.iter_rows()], dtype=bool)
         return [acc.take(np.nonzero(mask)[0])]
     if kind == "add_column":
         b = acc.to_pandas() if op.get("batch_format", "pandas") == "pandas" else acc.to_numpy()
-        col = fn(b)
+        col = call_user_fn(fn, b)
         if hasattr(b, "assign"):
             b = b.assign(**{op["col"]: col})
         else:
