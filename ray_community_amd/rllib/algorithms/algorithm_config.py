@@ -620,12 +620,21 @@ class AlgorithmConfig:
         d["framework"] = self.framework_str
         return d
 
+    # old-stack config keys (tuned-example YAML files, ``rllib train --config``) -> current names
+    _LEGACY_KEYS = {"lambda": "lambda_", "num_workers": "num_env_runners", "num_rollout_workers": "num_env_runners",
+                    "num_envs_per_worker": "num_envs_per_env_runner", "num_sgd_iter": "num_epochs",
+                    "sgd_minibatch_size": "minibatch_size", "evaluation_num_workers": "evaluation_num_env_runners"}
+    _IGNORED_KEYS = ("framework", "eager_tracing", "log_level", "create_env_on_driver")
+
     def update_from_dict(self, d: Dict):
         for k, v in d.items():
-            if k == "framework":
+            if k in self._IGNORED_KEYS:
                 continue
-            if k == "lambda":
-                k = "lambda_"
+            k = self._LEGACY_KEYS.get(k, k)
+            if k == "model" and isinstance(v, dict):
+                m = dict(self.model or {})
+                m.update(v)
+                v = m
             setattr(self, k, v)
         return self
 

@@ -324,6 +324,24 @@ def _add_flat_keys(m: Dict, prefix: str = "", out: Optional[Dict] = None):
     return out
 
 
+def _result_value(result: Dict, key: str):
+    """``result[key]``; a ``"a/b"`` key walks nested dicts (the reference flattens results with
+    "/"), and RLlib's old ``sampler_results/<m>`` prefix falls back to the top-level ``<m>``."""
+    if key in result:
+        return result[key]
+    if "/" not in key:
+        return None
+    node = result
+    for part in key.split("/"):
+        if not isinstance(node, dict) or part not in node:
+            node = None
+            break
+        node = node[part]
+    if node is None and key.startswith("sampler_results/"):
+        node = result.get(key.split("/", 1)[1])
+    return None if isinstance(node, dict) else node
+
+
 def evaluate_stop(stop, trial_id, result):
     """``RunConfig.stop`` semantics (reference ``tune/stopper``): a dict stops once any listed
     metric reaches its value, a ``Stopper`` / callable decides per result (a Stopper's
@@ -333,7 +351,8 @@ def evaluate_stop(stop, trial_id, result):
         return bool(result.get("done")), False
     if isinstance(stop, dict):
         for k, v in stop.items():
-            if k in result and result[k] >= v:
+            got = _result_value(result, k)
+            if got is not None and got >= v:
                 return True, False
         return bool(result.get("done")), False
     if isinstance(stop, Stopper):
