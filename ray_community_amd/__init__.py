@@ -12,6 +12,10 @@ __version__ = "0.1.0"
 import functools
 import inspect
 
+from ._private import import_paths as _import_paths
+
+_import_paths.install()  # the reference's secondary module paths (``ray.tune.result_grid``, ...)
+
 from . import exceptions
 from ._private.core_worker import DynamicObjectRefGenerator, ObjectRef, ObjectRefGenerator
 from ._private.ids import (ActorClassID, ActorID, FunctionID, JobID, NodeID, ObjectID, PlacementGroupID, TaskID,

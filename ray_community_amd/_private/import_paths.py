@@ -1,0 +1,82 @@
+"""The reference's secondary module paths, served from one table instead of one tiny file each.
+
+Several public names live in one module here but are importable from a separate module in the
+reference (``ray.tune.result_grid.ResultGrid``, ``ray.serve.deployment.Deployment``,
+``ray.util.rpdb.set_trace``, ...), and a few integration packages exist only when an optional
+framework is installed (``ray.train.horovod``, ``ray.util.dask``, ...). A meta-path finder
+answers those imports: an alias module re-exports the listed names of the defining module, and an
+integration whose framework is not installed fails to import with an ``ImportError`` naming it.
+"""
+from __future__ import annotations
+
+import importlib
+import importlib.abc
+import importlib.machinery
+import sys
+from typing import Dict, Optional, Tuple
+
+_PKG = __name__.rsplit(".", 2)[0]  # "ray_community_amd"
+
+# alias module (relative to the package) -> (defining module, exported names; None = its public names)
+ALIASES: Dict[str, Tuple[str, Optional[Tuple[str, ...]]]] = {
+    "util.serialization": ("_private.serialization", ("register_serializer", "deregister_serializer")),
+    "util.debugpy": ("util.ray_debugpy", None),
+    "util.rpdb": ("util.pdb", None),
+    "tune.callback": ("tune", ("Callback",)),
+    "tune.progress_reporter": ("tune.registry", ("ProgressReporter", "CLIReporter", "JupyterNotebookReporter")),
+    "tune.result_grid": ("tune.tuner", ("ResultGrid",)),
+    "tune.tune_config": ("tune.tuner", ("TuneConfig",)),
+    "serve.deployment": ("serve.api", ("Deployment", "Application")),
+    "train.session": ("train", ("report", "get_checkpoint", "get_context", "get_dataset_shard")),
+    "train.torch.torch_predictor": ("train.torch.torch_checkpoint", ("TorchPredictor",)),
+    "data.preprocessor": ("data.preprocessors", ("Preprocessor",)),
+    "experimental.locations": ("experimental", ("get_object_locations",)),
+    "experimental.dynamic_resources": ("experimental", ("set_resource",)),
+}
+
+# integration package -> the framework it needs (not installed in this image)
+NEEDS: Dict[str, str] = {
+    "train.horovod": "horovod",
+    "train.lightning": "lightning",
+    "train.mosaic": "composer",
+    "train.tensorflow": "tensorflow",
+    "util.dask": "dask",
+    "util.spark": "pyspark",
+}
+
+
+class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+    def find_spec(self, fullname, path=None, target=None):
+        if not fullname.startswith(_PKG + "."):
+            return None
+        rel = fullname[len(_PKG) + 1:]
+        if rel in ALIASES:
+            return importlib.machinery.ModuleSpec(fullname, self)
+        if rel in NEEDS:
+            return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
+        return None
+
+    def create_module(self, spec):
+        return None  # default module object
+
+    def exec_module(self, module):
+        rel = module.__name__[len(_PKG) + 1:]
+        if rel in NEEDS:
+            raise ImportError(f"{module.__name__} needs `{NEEDS[rel]}`, which is not installed in this environment",
+                              name=module.__name__)
+        target, names = ALIASES[rel]
+        src = importlib.import_module(f"{_PKG}.{target}")
+        if names is None:
+            names = tuple(getattr(src, "__all__", None) or (n for n in vars(src) if not n.startswith("_")))
+        for n in names:
+            setattr(module, n, getattr(src, n))
+        module.__all__ = list(names)
+        module.__doc__ = f"``{rel}`` import path: re-exports {', '.join(names)} from ``{_PKG}.{target}``."
+
+
+_FINDER = _Finder()
+
+
+def install() -> None:
+    if _FINDER not in sys.meta_path:
+        sys.meta_path.append(_FINDER)
