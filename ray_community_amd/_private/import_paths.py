@@ -32,7 +32,16 @@ ALIASES: Dict[str, Tuple[str, Optional[Tuple[str, ...]]]] = {
     "data.preprocessor": ("data.preprocessors", ("Preprocessor",)),
     "experimental.locations": ("experimental", ("get_object_locations",)),
     "experimental.dynamic_resources": ("experimental", ("set_resource",)),
+    "serve.dag": ("dag", ("InputNode",)),
+    # the pre-2.x ``ray.air.callbacks.*`` names of the experiment-tracking integrations
+    "air.callbacks": ("air.integrations", ()),
+    "air.callbacks.mlflow": ("air.integrations.mlflow", None),
+    "air.callbacks.wandb": ("air.integrations.wandb", None),
+    "air.callbacks.comet": ("air.integrations.comet", None),
 }
+
+# aliases that are packages (their submodules resolve through ALIASES / NEEDS too)
+PACKAGES = {"air.callbacks"}
 
 # integration package -> the framework it needs (not installed in this image)
 NEEDS: Dict[str, str] = {
@@ -42,6 +51,9 @@ NEEDS: Dict[str, str] = {
     "train.tensorflow": "tensorflow",
     "util.dask": "dask",
     "util.spark": "pyspark",
+    "serve.gradio_integrations": "gradio",
+    "air.integrations.keras": "tensorflow",
+    "air.callbacks.keras": "tensorflow",
 }
 
 
@@ -51,7 +63,7 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
             return None
         rel = fullname[len(_PKG) + 1:]
         if rel in ALIASES:
-            return importlib.machinery.ModuleSpec(fullname, self)
+            return importlib.machinery.ModuleSpec(fullname, self, is_package=rel in PACKAGES)
         if rel in NEEDS:
             return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
         return None
