@@ -48,6 +48,8 @@ _REF_ID = operator.attrgetter("_id")
 # ====================================================================== ObjectRef
 class ObjectRef:
     __slots__ = ("_id", "_core", "__weakref__")
+    # ``ObjectRef[int]`` in annotations (the reference's typing stub ``ray.types.ObjectRef[T]``)
+    __class_getitem__ = classmethod(__import__("types").GenericAlias)
 
     def __init__(self, oid: bytes, _register=True):
         self._id = oid

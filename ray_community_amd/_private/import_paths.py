@@ -33,6 +33,7 @@ ALIASES: Dict[str, Tuple[str, Optional[Tuple[str, ...]]]] = {
     "experimental.locations": ("experimental", ("get_object_locations",)),
     "experimental.dynamic_resources": ("experimental", ("set_resource",)),
     "serve.dag": ("dag", ("InputNode",)),
+    "types": ("_private.core_worker", ("ObjectRef",)),
     # the pre-2.x ``ray.air.callbacks.*`` names of the experiment-tracking integrations
     "air.callbacks": ("air.integrations", ()),
     "air.callbacks.mlflow": ("air.integrations.mlflow", None),
