@@ -34,6 +34,8 @@ ALIASES: Dict[str, Tuple[str, Optional[Tuple[str, ...]]]] = {
     "experimental.dynamic_resources": ("experimental", ("set_resource",)),
     "serve.dag": ("dag", ("InputNode",)),
     "types": ("_private.core_worker", ("ObjectRef",)),
+    "experimental.queue": ("util.queue", ("Empty", "Full", "Queue")),
+    "experimental.multiprocessing": ("util.multiprocessing", ("Pool", "TimeoutError")),
     # the pre-2.x ``ray.air.callbacks.*`` names of the experiment-tracking integrations
     "air.callbacks": ("air.integrations", ()),
     "air.callbacks.mlflow": ("air.integrations.mlflow", None),
@@ -52,9 +54,18 @@ NEEDS: Dict[str, str] = {
     "train.tensorflow": "tensorflow",
     "util.dask": "dask",
     "util.spark": "pyspark",
+    "util.horovod": "horovod",
     "serve.gradio_integrations": "gradio",
     "air.integrations.keras": "tensorflow",
     "air.callbacks.keras": "tensorflow",
+}
+
+
+# APIs the reference removed: importing them raises DeprecationWarning, as the reference's do
+REMOVED: Dict[str, str] = {
+    "util.xgboost": "ray.util.xgboost has been removed as of Ray 2.0: use `XGBoostTrainer` in `ray.train.xgboost`.",
+    "util.lightgbm": "ray.util.lightgbm has been removed as of Ray 2.0: use `LightGBMTrainer` in "
+                     "`ray.train.lightgbm`.",
 }
 
 
@@ -65,7 +76,7 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
         rel = fullname[len(_PKG) + 1:]
         if rel in ALIASES:
             return importlib.machinery.ModuleSpec(fullname, self, is_package=rel in PACKAGES)
-        if rel in NEEDS:
+        if rel in NEEDS or rel in REMOVED:
             return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
         return None
 
@@ -74,6 +85,8 @@ class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
 
     def exec_module(self, module):
         rel = module.__name__[len(_PKG) + 1:]
+        if rel in REMOVED:
+            raise DeprecationWarning(REMOVED[rel])
         if rel in NEEDS:
             raise ImportError(f"{module.__name__} needs `{NEEDS[rel]}`, which is not installed in this environment",
                               name=module.__name__)

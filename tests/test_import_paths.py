@@ -32,3 +32,9 @@ def test_unknown_submodule_still_fails_normally():
     from ray_community_amd.util.pdb import set_trace as st2
 
     assert set_trace is st2
+
+
+@pytest.mark.parametrize("mod", sorted(ip.REMOVED))
+def test_removed_apis_raise_deprecation(mod):
+    with pytest.raises(DeprecationWarning, match="removed"):
+        importlib.import_module(f"ray_community_amd.{mod}")
