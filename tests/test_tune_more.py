@@ -57,7 +57,15 @@ def test_max_concurrent_trials_and_concurrency_limiter(ray6, tmp_path):
                 k = f[:-6]
                 iv.append((float(open(os.path.join(marks, f)).read()),
                            float(open(os.path.join(marks, k + ".end")).read())))
-        return max(sum(1 for s2, e2 in iv if s2 < e and s < e2) for s, e in iv)
+        # most trainables running at one instant (a sweep over the start / end events; counting
+        # the intervals that overlap one interval would also count two that ran one after another
+        # beside a longer third)
+        ev = sorted([(s, 1) for s, _ in iv] + [(e, -1) for _, e in iv], key=lambda x: (x[0], x[1]))
+        cur = peak = 0
+        for _, d in ev:
+            cur += d
+            peak = max(peak, cur)
+        return peak
 
     tune.Tuner(trainable, param_space={"i": tune.grid_search(list(range(6)))},
                tune_config=tune.TuneConfig(max_concurrent_trials=2), run_config=_run_cfg(tmp_path, "mct")).fit()
