@@ -57,6 +57,10 @@ NEEDS: Dict[str, str] = {
     "util.horovod": "horovod",
     "serve.gradio_integrations": "gradio",
     "air.integrations.keras": "tensorflow",
+    "tune.search.ax": "ax-platform",
+    "tune.search.nevergrad": "nevergrad",
+    "tune.search.zoopt": "zoopt",
+    "tune.search.hebo": "HEBO",
     "air.callbacks.keras": "tensorflow",
 }
 

@@ -129,6 +129,12 @@ def create_searcher(search_alg: str, **kwargs):
             table[k] = tpe.TPESearch
     except Exception:  # noqa
         pass
+    try:
+        from .search.bayesopt import BayesOptSearch
+
+        table["bayesopt"] = BayesOptSearch
+    except Exception:  # noqa
+        pass
     if search_alg not in table:
         raise ValueError(f"Search algorithm must be one of {sorted(table)}, got {search_alg!r}")
     return table[search_alg](**kwargs)

@@ -189,15 +189,16 @@ class BayesOptSearch(Searcher):
             raise RuntimeError("BayesOptSearch has no search space: pass `space` or a param_space to the Tuner")
         if not self._metric or not self._mode:
             raise RuntimeError("BayesOptSearch needs `metric` and `mode` (here or in the TuneConfig)")
-        random_phase = False
+        # warm-up: the first random_search_steps suggestions (points_to_evaluate included) are not
+        # modelled, and the GP waits until that many trials have finished
+        random_phase = len(self._y) < self.random_search_trials
+        if random_phase and self._random_issued >= self.random_search_trials:
+            return None
         if self._points:
             flat = dict(self._points.pop(0))
             flat.update({k: v for k, v in self._const.items() if k not in flat})
-        elif len(self._y) < self.random_search_trials:
-            if self._random_issued >= self.random_search_trials:
-                return None  # wait for the random trials to finish before modelling
+        elif random_phase:
             flat = self._from_unit(self._rng.uniform(size=len(self._names)))
-            random_phase = True
         else:
             flat = self._from_unit(self._maximize())
         key = self._key(flat)
