@@ -42,6 +42,62 @@ class Env:
     def close(self):
         pass
 
+    @property
+    def unwrapped(self):
+        return self
+
+
+class Wrapper(Env):
+    """gymnasium-style wrapper: delegates to ``self.env``; spaces default to the wrapped env's and
+    unknown attributes are looked up on it (``wrapper.unwrapped`` is the innermost env)."""
+
+    def __init__(self, env):
+        self.env = env
+        self.observation_space = getattr(env, "observation_space", None)
+        self.action_space = getattr(env, "action_space", None)
+
+    def __getattr__(self, name):
+        if name.startswith("_") or name == "env":
+            raise AttributeError(name)
+        return getattr(self.env, name)
+
+    @property
+    def unwrapped(self):
+        return getattr(self.env, "unwrapped", self.env)
+
+    def reset(self, **kwargs):
+        return self.env.reset(**kwargs)
+
+    def step(self, action):
+        return self.env.step(action)
+
+    def close(self):
+        close = getattr(self.env, "close", None)
+        if close is not None:
+            close()
+
+
+class ObservationWrapper(Wrapper):
+    def observation(self, observation):
+        raise NotImplementedError
+
+    def reset(self, **kwargs):
+        obs, info = self.env.reset(**kwargs)
+        return self.observation(obs), info
+
+    def step(self, action):
+        obs, r, te, tr, info = self.env.step(action)
+        return self.observation(obs), r, te, tr, info
+
+
+class RewardWrapper(Wrapper):
+    def reward(self, reward):
+        raise NotImplementedError
+
+    def step(self, action):
+        obs, r, te, tr, info = self.env.step(action)
+        return obs, self.reward(r), te, tr, info
+
 
 class VectorEnv:
     """N environments stepped as one batch. ``step`` auto-resets finished sub-envs and returns the

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 from typing import Any, Callable, Dict, List, Optional
 
-from .external_env import BaseEnv
+from ..external_env import BaseEnv
 
 
 class _NeedsPackage:
@@ -58,7 +58,7 @@ class RemoteBaseEnv(BaseEnv):
 
     def __init__(self, make_env: Callable[[int], Any], num_envs: int, remote_env_batch_wait_ms: int = 0,
                  restart_failed_sub_environments: bool = False):
-        from ... import remote
+        from .... import remote
 
         self.make_env, self.num_envs = make_env, int(num_envs)
         self.wait_ms = int(remote_env_batch_wait_ms)
@@ -68,7 +68,7 @@ class RemoteBaseEnv(BaseEnv):
         self._resetting = set(range(self.num_envs))
 
     def poll(self):
-        from ... import get, wait
+        from .... import get, wait
 
         refs = list(self._pending)
         if not refs:
@@ -109,7 +109,7 @@ class RemoteBaseEnv(BaseEnv):
         return list(self.actors)
 
     def stop(self):
-        from ... import kill
+        from .... import kill
 
         for a in self.actors:
             try:
