@@ -35,6 +35,12 @@ ALIASES: Dict[str, Tuple[str, Optional[Tuple[str, ...]]]] = {
     "serve.dag": ("dag", ("InputNode",)),
     "types": ("_private.core_worker", ("ObjectRef",)),
     "experimental.queue": ("util.queue", ("Empty", "Full", "Queue")),
+    # third-party simulator wrappers (constructing one names the missing package)
+    "rllib.env.wrappers.pettingzoo_env": ("rllib.env.wrappers", ("PettingZooEnv", "ParallelPettingZooEnv")),
+    "rllib.env.wrappers.dm_env_wrapper": ("rllib.env.wrappers", ("DMEnv",)),
+    "rllib.env.wrappers.dm_control_wrapper": ("rllib.env.wrappers", ("DMCEnv",)),
+    "rllib.env.wrappers.unity3d_env": ("rllib.env.wrappers", ("Unity3DEnv",)),
+    "rllib.env.remote_base_env": ("rllib.env.wrappers", ("RemoteBaseEnv",)),
     "experimental.multiprocessing": ("util.multiprocessing", ("Pool", "TimeoutError")),
     # the pre-2.x ``ray.air.callbacks.*`` names of the experiment-tracking integrations
     "air.callbacks": ("air.integrations", ()),
