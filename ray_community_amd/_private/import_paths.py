@@ -41,6 +41,29 @@ ALIASES: Dict[str, Tuple[str, Optional[Tuple[str, ...]]]] = {
     "rllib.env.wrappers.dm_control_wrapper": ("rllib.env.wrappers", ("DMCEnv",)),
     "rllib.env.wrappers.unity3d_env": ("rllib.env.wrappers", ("Unity3DEnv",)),
     "rllib.env.remote_base_env": ("rllib.env.wrappers", ("RemoteBaseEnv",)),
+    # RLlib helper modules user code imports from (custom models, policies, tests)
+    "rllib.utils.annotations": ("rllib.utils", ("override", "PublicAPI", "DeveloperAPI")),
+    "rllib.utils.framework": ("rllib.utils", ("try_import_torch", "try_import_tf", "try_import_tfp",
+                                              "try_import_jax")),
+    "rllib.utils.numpy": ("rllib.utils", ("one_hot", "softmax", "sigmoid", "relu", "fc", "lstm", "LARGE_INTEGER",
+                                          "SMALL_NUMBER", "MIN_LOG_NN_OUTPUT", "MAX_LOG_NN_OUTPUT")),
+    "rllib.utils.test_utils": ("rllib.utils", ("check", "check_compute_single_action", "check_train_results",
+                                               "framework_iterator")),
+    "rllib.utils.deprecation": ("rllib.utils", ("deprecation_warning",)),
+    "rllib.utils.filter_manager": ("rllib.utils", ("FilterManager",)),
+    "rllib.policy.torch_policy": ("rllib.policy", ("TorchPolicy",)),
+    "rllib.utils.replay_buffers.prioritized_replay_buffer": ("rllib.utils.replay_buffers",
+                                                             ("PrioritizedReplayBuffer",)),
+    "rllib.utils.replay_buffers.multi_agent_replay_buffer": ("rllib.utils.replay_buffers",
+                                                             ("MultiAgentReplayBuffer", "ReplayMode")),
+    "rllib.utils.replay_buffers.multi_agent_prioritized_replay_buffer": ("rllib.utils.replay_buffers",
+                                                                         ("MultiAgentPrioritizedReplayBuffer",)),
+    "rllib.utils.replay_buffers.multi_agent_mixin_replay_buffer": ("rllib.utils.replay_buffers",
+                                                                   ("MultiAgentMixInReplayBuffer",)),
+    "rllib.utils.replay_buffers.reservoir_replay_buffer": ("rllib.utils.replay_buffers", ("ReservoirReplayBuffer",)),
+    "rllib.utils.replay_buffers.fifo_replay_buffer": ("rllib.utils.replay_buffers", ("FifoReplayBuffer",)),
+    "rllib.utils.replay_buffers.prioritized_episode_replay_buffer": ("rllib.utils.replay_buffers",
+                                                                     ("PrioritizedEpisodeReplayBuffer",)),
     "experimental.multiprocessing": ("util.multiprocessing", ("Pool", "TimeoutError")),
     # the pre-2.x ``ray.air.callbacks.*`` names of the experiment-tracking integrations
     "air.callbacks": ("air.integrations", ()),
