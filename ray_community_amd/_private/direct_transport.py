@@ -123,11 +123,15 @@ class OwnedTable:
         self.core = core
         self.cond = threading.Condition(threading.Lock())
         self.objs: Dict[bytes, _Owned] = {}
+        # oids of entries still waiting for their result (desc None): wait_ready's set algebra
+        # runs on it in C instead of a Python loop over the caller's list
+        self.pending: set = set()
         self.waiters: List[list] = []  # wait_ready records: [pending oid set, still needed, Event]
 
     def create(self, oid, tid, channel):
         with self.cond:
             self.objs[oid] = _Owned(tid, channel)
+            self.pending.add(oid)
 
     def get_entry(self, oid) -> Optional[_Owned]:
         return self.objs.get(oid)
@@ -144,6 +148,7 @@ class OwnedTable:
             dropped = e is None or e.dropped
             if e is not None:
                 e.desc = desc
+                self.pending.discard(oid)
                 forward = e.published and not head_managed
                 if head_managed:
                     e.published = True
@@ -199,6 +204,7 @@ class OwnedTable:
                 e.dropped = True
                 return False
             del self.objs[oid]
+            self.pending.discard(oid)
         return e.published
 
     def revive(self, oid) -> bool:
@@ -242,6 +248,7 @@ class OwnedTable:
                     continue
                 if e.dropped and e.desc is None and not e.callbacks and not e.published:
                     del self.objs[o]
+                    self.pending.discard(o)
 
     def wait_descs(self, oids, deadline):
         """Block until every oid has a result (or the deadline passes). Returns the descs."""
@@ -265,16 +272,10 @@ class OwnedTable:
         themselves: one waiter record (the pending set + how many more it needs) is checked by
         ``set_ready`` -- polling a shrinking list (``ready, rest = wait(rest)``) over N refs costs
         O(N) per call, not O(N) stale callbacks per object."""
-        objs = self.objs
         with self.cond:
-            ready = []
-            for o in oids:  # in order, stopping once enough are ready (the usual polling case)
-                e = objs.get(o)
-                if e is None or e.desc is not None:
-                    ready.append(o)
-                    if len(ready) >= num_returns:
-                        return ready
-            pending = {o for o in oids if o in objs and objs[o].desc is None}
+            # not-ready = the caller's oids still pending (C-level set intersection; an oid this
+            # table does not hold counts as ready, as before)
+            pending = self.pending.intersection(oids)
             need = num_returns - (len(oids) - len(pending))
             w = None
             if need > 0:
@@ -288,12 +289,12 @@ class OwnedTable:
                     self.waiters.remove(w)
                 except ValueError:
                     pass
-        # in list order; once enough are ready the rest of the list is not looked at (the caller
-        # keeps the first ``num_returns``)
+            pending = self.pending.intersection(oids)
+        # the ready ones in list order; once enough are found the rest of the list is not looked
+        # at (the caller keeps the first ``num_returns``)
         out = []
         for o in oids:
-            e = objs.get(o)
-            if e is None or e.desc is not None:
+            if o not in pending:
                 out.append(o)
                 if len(out) >= num_returns:
                     break
